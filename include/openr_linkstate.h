@@ -1,0 +1,140 @@
+/*
+ * openr_linkstate.h -- C-ABI of the LinkState drop-in facade (libopenr_spf.so).
+ *
+ * Replaces the reference's C++ class openr::LinkState
+ * (openr/decision/LinkState.h:177-469) for its consumer SpfSolver
+ * (openr/decision/Decision.cpp:413, 926, 939, 1126, 1153, 1165).  Method for
+ * method:
+ *
+ *   LinkState::updateAdjacencyDatabase  (LinkState.h:330-333) -> ls_update_adjacency_databases
+ *   LinkState::deleteAdjacencyDatabase  (LinkState.h:337)     -> ls_delete_adjacency_database
+ *   LinkState::decrementHolds           (LinkState.h:327)     -> ls_decrement_holds
+ *   LinkState::hasHolds / numLinks / numNodes / hasNode / isNodeOverloaded
+ *                                        (LinkState.h:361-380) -> ls_has_holds, ls_num_links, ...
+ *   LinkState::linksFromNode            (LinkState.h:366)     -> ls_links_from_node
+ *   LinkState::getSpfResult             (LinkState.h:271-272) -> ls_get_spf_result
+ *   LinkState::getKthPaths              (LinkState.h:293-294) -> ls_get_kth_paths
+ *   LinkState::getMetricFromAToB / getHopsFromAToB / getMaxHopsToNode
+ *                                        (LinkState.h:343-354) -> ls_get_metric_a_to_b, ls_get_max_hops_to_node
+ *   fb303 counter decision.spf_runs     (LinkState.cpp:815)   -> ls_spf_runs
+ *
+ * The LSDB bookkeeping (bidirectional-link check, ordered-FIB holds, link and
+ * node overload) runs on the host exactly as the reference's; every shortest
+ * path computation is a batch on the MI355X engine (openr_spf.h).
+ *
+ * Ownership: views returned by ls_get_spf_result / ls_get_kth_paths point into
+ * memo storage owned by the ls_state and stay valid until the next call that
+ * reports topology_changed (the reference's memo invalidation,
+ * LinkState.cpp:509-512, 714-717, 730-731) or ls_destroy.
+ * Names are interned: ls_name_id()/ls_name() map between names and stable ids.
+ * Errors: spf_status codes + ls_last_error(); no exceptions cross the ABI.
+ */
+#ifndef OPENR_LINKSTATE_H_
+#define OPENR_LINKSTATE_H_
+
+#include <stdint.h>
+
+#include "openr_lsdb.h"
+#include "openr_spf.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ls_state ls_state;
+
+/* LinkState::LinkStateChange (LinkState.h:306-325) */
+typedef struct ls_change {
+  uint8_t topology_changed;
+  uint8_t link_attributes_changed;
+  uint8_t node_label_changed;
+  uint8_t pad;
+} ls_change;
+
+/* Snapshot of one Link (LinkState.h:82-175). */
+typedef struct ls_link_desc {
+  uint32_t node1, node2;      /* name ids, in construction order (n1_, n2_) */
+  const char* if1;            /* interface on node1 */
+  const char* if2;            /* interface on node2 */
+  uint32_t first_node;        /* orderedNames_.first.first  (name id) */
+  uint32_t second_node;       /* orderedNames_.second.first (name id) */
+  uint64_t metric1, metric2;  /* getMetricFromNode(node1/node2) (held value) */
+  int32_t adj_label1, adj_label2;
+  uint8_t overload1, overload2, is_up, pad;
+  uint64_t hash;              /* Link::hash */
+  const uint8_t* nh_v4_1;     /* 4 bytes each */
+  const uint8_t* nh_v4_2;
+  const uint8_t* nh_v6_1;     /* 16 bytes each */
+  const uint8_t* nh_v6_2;
+} ls_link_desc;
+
+/* LinkState::SpfResult: one entry per reached node (source included). */
+typedef struct ls_spf_view {
+  uint32_t n;
+  const uint32_t* node;      /* [n] name ids                              */
+  const uint64_t* metric;    /* [n] NodeSpfResult::metric()               */
+  const uint32_t* nh_ptr;    /* [n+1] into nh_node                        */
+  const uint32_t* nh_node;   /* next-hop name ids (ascending name)        */
+  const uint32_t* pl_ptr;    /* [n+1] into pl_link / pl_prev              */
+  const uint32_t* pl_link;   /* pathLinks().link  (link ids)              */
+  const uint32_t* pl_prev;   /* pathLinks().prevNode (name ids)           */
+} ls_spf_view;
+
+/* std::vector<LinkState::Path>: path p = link[path_ptr[p] .. path_ptr[p+1]) */
+typedef struct ls_paths_view {
+  uint32_t n_paths;
+  const uint32_t* path_ptr;
+  const uint32_t* link;
+} ls_paths_view;
+
+/* device < 0 creates a host-only state: LSDB bookkeeping and CSR flatten work,
+ * shortest-path queries fail with SPF_E_NO_DEVICE (used by CPU-only tests). */
+spf_status ls_create(const char* area, int device, ls_state** out);
+void ls_destroy(ls_state* ls);
+const char* ls_last_error(const ls_state* ls);
+
+spf_status ls_update_adjacency_databases(ls_state* ls, const openr_lsdb* lsdb,
+                                         uint64_t hold_up_ttl,
+                                         uint64_t hold_down_ttl,
+                                         ls_change* changes /* [n_dbs] */);
+spf_status ls_delete_adjacency_database(ls_state* ls, const char* node,
+                                        ls_change* change);
+spf_status ls_decrement_holds(ls_state* ls, ls_change* change);
+
+int ls_has_holds(const ls_state* ls);
+uint64_t ls_num_links(const ls_state* ls);
+uint64_t ls_num_nodes(const ls_state* ls);
+int ls_has_node(const ls_state* ls, const char* node);
+int ls_is_node_overloaded(const ls_state* ls, const char* node);
+
+uint32_t ls_name_id(ls_state* ls, const char* name);
+const char* ls_name(const ls_state* ls, uint32_t id);
+
+spf_status ls_links_from_node(const ls_state* ls, const char* node,
+                              uint32_t* link_ids, uint32_t cap, uint32_t* count);
+spf_status ls_link_info(const ls_state* ls, uint32_t link_id, ls_link_desc* out);
+
+spf_status ls_get_spf_result(ls_state* ls, const char* node, int use_link_metric,
+                             ls_spf_view* out);
+spf_status ls_get_kth_paths(ls_state* ls, const char* src, const char* dst,
+                            uint64_t k, ls_paths_view* out);
+spf_status ls_get_metric_a_to_b(ls_state* ls, const char* a, const char* b,
+                                int use_link_metric, uint64_t* metric,
+                                int* has_value);
+spf_status ls_get_max_hops_to_node(ls_state* ls, const char* node, uint64_t* out);
+
+uint64_t ls_spf_runs(const ls_state* ls);
+
+/* The flattened CSR handed to the engine (for inspection / batch callers):
+ * node ids are ascending-name ranks; returns the engine context. */
+spf_ctx* ls_engine(ls_state* ls);
+spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges);
+spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids /* [n_nodes] */);
+/* Copy of the flattened CSR (sizes from ls_flatten); any pointer may be NULL. */
+spf_status ls_graph_csr(ls_state* ls, uint32_t* row_ptr, uint32_t* col, int32_t* metric,
+                        uint32_t* link_id, uint8_t* overloaded);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPENR_LINKSTATE_H_ */

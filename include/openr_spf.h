@@ -1,0 +1,153 @@
+/*
+ * openr_spf.h -- C-ABI of the MI355X SPF engine (libopenr_spf.so).
+ *
+ * Graph-level interface: the caller (the LinkState facade of
+ * openr_linkstate.h, or a host program that already has a CSR) hands over a
+ * flattened link-state graph once, then asks for batches of single-source
+ * shortest-path-first solves.  Each solve reproduces, bit for bit, what the
+ * reference computes in LinkState::runSpf (openr/decision/LinkState.cpp:808-882):
+ *   - dist[v]  = NodeSpfResult::metric() of v, or SPF_UNREACHABLE
+ *   - nh bits  = NodeSpfResult::nextHops() of v as a bitset over the source's
+ *                distinct up neighbours (ascending node id = ascending name)
+ * The reference entry points this replaces are LinkState::getSpfResult
+ * (LinkState.h:271-272, LinkState.cpp:793-803) for a batch of sources at once.
+ *
+ * Conventions
+ *   - Node ids 0..n_nodes-1 MUST be assigned in ascending std::string order of
+ *     the node names: the reference's Dijkstra queue breaks metric ties by
+ *     node name (LinkState.h:488-498) and the engine breaks them by node id.
+ *   - A directed edge u->v exists for every *up* link (Link::isUp,
+ *     LinkState.cpp:233-236); its metric is the metric advertised by u
+ *     (Link::getMetricFromNode(u), LinkState.cpp:195-204).  Edges of one node
+ *     appear in linksFromNode(u) iteration order.
+ *   - overloaded[u] != 0: u is recorded but never expanded unless it is the
+ *     source (LinkState.cpp:831-838).
+ *   - Distances are u32.  spf_graph_load rejects graphs whose longest possible
+ *     path (max metric x (n_nodes-1)) does not fit; such graphs are out of
+ *     scope for this engine (SPF_E_UNSUPPORTED).
+ *   - Row pitch: dist and next-hop rows are stored with pitch
+ *     spf_row_pitch() = n_nodes rounded up to a multiple of 4.
+ *
+ * Errors: every call returns spf_status; spf_last_error() describes the last
+ * failure.  No exceptions cross the ABI.  All calls on one context must come
+ * from one host thread (the reference is single-threaded too,
+ * openr/decision/Decision.cpp:1484).
+ */
+#ifndef OPENR_SPF_H_
+#define OPENR_SPF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum spf_status {
+  SPF_OK = 0,
+  SPF_E_INVALID = 1,     /* bad argument / malformed graph            */
+  SPF_E_UNSUPPORTED = 2, /* input outside the exact-parity envelope   */
+  SPF_E_HIP = 3,         /* HIP runtime failure                       */
+  SPF_E_NO_DEVICE = 4,   /* no usable gfx950 device                   */
+  SPF_E_NOMEM = 5,
+  SPF_E_STATE = 6        /* call out of order (e.g. no graph loaded)  */
+} spf_status;
+
+#define SPF_UNREACHABLE 0xFFFFFFFFu
+
+/* solve flags */
+#define SPF_FLAG_HOP_COUNT 0x1u /* useLinkMetric == false: every edge costs 1 */
+
+typedef struct spf_ctx spf_ctx;
+typedef struct spf_plan spf_plan;
+
+typedef struct spf_graph {
+  uint32_t n_nodes;
+  uint32_t n_edges;             /* directed up edges                            */
+  const uint32_t* row_ptr;      /* [n_nodes+1]                                  */
+  const uint32_t* col;          /* [n_edges] head node of edge                  */
+  const int32_t* metric;        /* [n_edges] metric advertised by the tail      */
+  const uint32_t* link_id;      /* [n_edges] undirected link id (shared by both directions) */
+  const uint8_t* overloaded;    /* [n_nodes]                                    */
+} spf_graph;
+
+/* ---- context ------------------------------------------------------------ */
+spf_status spf_ctx_create(int device, spf_ctx** out);
+void spf_ctx_destroy(spf_ctx* ctx);
+const char* spf_last_error(const spf_ctx* ctx);
+/* Thread-local message for failures before a context exists. */
+const char* spf_global_error(void);
+
+/* Copies the graph to the device (replaces any previous graph). */
+spf_status spf_graph_load(spf_ctx* ctx, const spf_graph* g);
+uint32_t spf_row_pitch(const spf_ctx* ctx);
+/* 1 when the loaded graph has an up edge with metric <= 0 (weighted solves of
+ * such graphs return SPF_E_UNSUPPORTED: zero-cost plateaus make the reference's
+ * next-hop sets depend on heap pop order, not implemented yet). */
+int spf_graph_has_nonpositive_metric(const spf_ctx* ctx);
+
+/* Distinct up neighbours of `src` in ascending id: the bit order of its
+ * next-hop sets.  Writes min(count, cap) ids; *count = total. */
+spf_status spf_src_neighbors(const spf_ctx* ctx, uint32_t src, uint32_t* out,
+                             uint32_t cap, uint32_t* count);
+
+/* ---- plans: a fixed batch of sources, executable many times ------------- */
+/* Next-hop layout of source i of the plan: words_i = ceil(k_i/32) 32-bit words
+ * per node (k_i = #distinct up neighbours), stored word-planar:
+ *   bit j of node v  ->  nh[nh_off[i] + (j/32)*pitch + v]  bit (j%32). */
+spf_status spf_plan_create(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
+                           uint32_t flags, spf_plan** out);
+void spf_plan_destroy(spf_plan* plan);
+uint64_t spf_plan_nh_words(const spf_plan* plan);     /* total u32 words   */
+spf_status spf_plan_nh_layout(const spf_plan* plan, uint64_t* nh_off,
+                              uint32_t* words);       /* n_src entries each */
+uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved */
+
+/* Execute on device buffers: d_dist = [n_src][pitch] u32, d_nh = nh words.
+ * Enqueued on `stream` (a hipStream_t, NULL = the context's stream); no host
+ * synchronisation, no allocation: capturable into a hipGraph. */
+spf_status spf_plan_execute(spf_plan* plan, uint32_t* d_dist, uint32_t* d_nh,
+                            void* stream);
+
+/* Kernel timing with HIP events recorded on the execute stream: after
+ * spf_plan_enable_timing(plan, K), each of the next K executes records events
+ * around its SSSP and ECMP kernels; spf_plan_timing() waits for them and
+ * returns the summed milliseconds of each kernel and the number of executes
+ * (then resets the count). */
+spf_status spf_plan_enable_timing(spf_plan* plan, uint32_t max_executes);
+spf_status spf_plan_timing(spf_plan* plan, double* sssp_ms, double* ecmp_ms, uint32_t* n);
+
+/* Convenience: plan + execute + copy back to host buffers.
+ * dist_out = [n_src][n_nodes] (dense, no pitch); nh_out sized by
+ * spf_plan_nh_words with the planar layout above (pitch = spf_row_pitch). */
+spf_status spf_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
+                     uint32_t flags, uint32_t* dist_out, uint32_t* nh_out);
+
+/* ---- single-source primitives (LinkState facade, KSP) -------------------- */
+/* Distances of one source with an optional set of undirected link ids to
+ * ignore -- the reference's runSpf(src, true, linksToIgnore) used by
+ * getKthPaths (LinkState.cpp:776-779).  dist_out = [n_nodes]. */
+spf_status spf_sssp(spf_ctx* ctx, uint32_t src, uint32_t flags,
+                    const uint32_t* ignore_links, uint32_t n_ignore,
+                    uint32_t* dist_out);
+
+/* Predecessor ("pathLinks") lists of one source given its distance row `dist`
+ * (from spf_solve / spf_sssp with the same flags and ignore set), in the
+ * reference's order (LinkState.cpp:857-873: predecessors u in Dijkstra pop
+ * order, then u's links in linksFromNode(u) order).  Entries are directed
+ * edge ids u->v.  pred_ptr = [n_nodes+1]; call with pred_edge == NULL first
+ * to size (*n_preds). */
+spf_status spf_preds(spf_ctx* ctx, uint32_t src, uint32_t flags,
+                     const uint32_t* ignore_links, uint32_t n_ignore,
+                     const uint32_t* dist, uint32_t* pred_ptr,
+                     uint32_t* pred_edge, uint32_t cap, uint32_t* n_preds);
+
+/* ---- counters ----------------------------------------------------------- */
+/* Logical single-source solves executed (the reference's decision.spf_runs,
+ * LinkState.cpp:815) and kernel time of the last execute in ms. */
+uint64_t spf_solves(const spf_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPENR_SPF_H_ */

@@ -1,0 +1,224 @@
+"""ctypes binding of libopenr_spf.so (include/openr_spf.h, openr_linkstate.h).
+
+The library is built in-tree by ``python -m openr_amd.build`` (or
+``__graft_entry__.build()``) into ``openr_amd/lib/libopenr_spf.so``.  There is
+no fallback: if the library is missing, importing this module raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libopenr_spf.so"
+
+SPF_OK = 0
+SPF_E_INVALID = 1
+SPF_E_UNSUPPORTED = 2
+SPF_E_HIP = 3
+SPF_E_NO_DEVICE = 4
+SPF_E_NOMEM = 5
+SPF_E_STATE = 6
+SPF_UNREACHABLE = 0xFFFFFFFF
+SPF_FLAG_HOP_COUNT = 0x1
+
+_STATUS_NAMES = {
+    SPF_E_INVALID: "SPF_E_INVALID",
+    SPF_E_UNSUPPORTED: "SPF_E_UNSUPPORTED",
+    SPF_E_HIP: "SPF_E_HIP",
+    SPF_E_NO_DEVICE: "SPF_E_NO_DEVICE",
+    SPF_E_NOMEM: "SPF_E_NOMEM",
+    SPF_E_STATE: "SPF_E_STATE",
+}
+
+
+class SpfError(RuntimeError):
+    def __init__(self, status: int, msg: str) -> None:
+        super().__init__(f"{_STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class UnsupportedInput(SpfError):
+    """Input outside the engine's exact-parity envelope (SPF_E_UNSUPPORTED)."""
+
+
+class NoDevice(SpfError):
+    """No gfx950 device (SPF_E_NO_DEVICE)."""
+
+
+def raise_for(status: int, msg: str) -> None:
+    if status == SPF_OK:
+        return
+    if status == SPF_E_UNSUPPORTED:
+        raise UnsupportedInput(status, msg)
+    if status == SPF_E_NO_DEVICE:
+        raise NoDevice(status, msg)
+    raise SpfError(status, msg)
+
+
+# ---- structs -----------------------------------------------------------------
+class SpfGraph(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32),
+        ("n_edges", C.c_uint32),
+        ("row_ptr", C.POINTER(C.c_uint32)),
+        ("col", C.POINTER(C.c_uint32)),
+        ("metric", C.POINTER(C.c_int32)),
+        ("link_id", C.POINTER(C.c_uint32)),
+        ("overloaded", C.POINTER(C.c_uint8)),
+    ]
+
+
+class OpenrLsdb(C.Structure):
+    _fields_ = [
+        ("blob", C.c_char_p),
+        ("dbs", C.c_void_p),
+        ("n_dbs", C.c_uint32),
+        ("adjs", C.c_void_p),
+    ]
+
+
+class LsChange(C.Structure):
+    _fields_ = [
+        ("topology_changed", C.c_uint8),
+        ("link_attributes_changed", C.c_uint8),
+        ("node_label_changed", C.c_uint8),
+        ("pad", C.c_uint8),
+    ]
+
+
+class LsLinkDesc(C.Structure):
+    _fields_ = [
+        ("node1", C.c_uint32), ("node2", C.c_uint32),
+        ("if1", C.c_char_p), ("if2", C.c_char_p),
+        ("first_node", C.c_uint32), ("second_node", C.c_uint32),
+        ("metric1", C.c_uint64), ("metric2", C.c_uint64),
+        ("adj_label1", C.c_int32), ("adj_label2", C.c_int32),
+        ("overload1", C.c_uint8), ("overload2", C.c_uint8),
+        ("is_up", C.c_uint8), ("pad", C.c_uint8),
+        ("hash", C.c_uint64),
+        ("nh_v4_1", C.POINTER(C.c_uint8)), ("nh_v4_2", C.POINTER(C.c_uint8)),
+        ("nh_v6_1", C.POINTER(C.c_uint8)), ("nh_v6_2", C.POINTER(C.c_uint8)),
+    ]
+
+
+class LsSpfView(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32),
+        ("node", C.POINTER(C.c_uint32)),
+        ("metric", C.POINTER(C.c_uint64)),
+        ("nh_ptr", C.POINTER(C.c_uint32)),
+        ("nh_node", C.POINTER(C.c_uint32)),
+        ("pl_ptr", C.POINTER(C.c_uint32)),
+        ("pl_link", C.POINTER(C.c_uint32)),
+        ("pl_prev", C.POINTER(C.c_uint32)),
+    ]
+
+
+class LsPathsView(C.Structure):
+    _fields_ = [
+        ("n_paths", C.c_uint32),
+        ("path_ptr", C.POINTER(C.c_uint32)),
+        ("link", C.POINTER(C.c_uint32)),
+    ]
+
+
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+_vp = C.c_void_p
+
+# name -> (restype, argtypes); also the list of exported symbols checked by tests
+PROTOTYPES = {
+    # engine (openr_spf.h)
+    "spf_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "spf_ctx_destroy": (None, [_vp]),
+    "spf_last_error": (C.c_char_p, [_vp]),
+    "spf_global_error": (C.c_char_p, []),
+    "spf_graph_load": (C.c_int, [_vp, C.POINTER(SpfGraph)]),
+    "spf_row_pitch": (C.c_uint32, [_vp]),
+    "spf_graph_has_nonpositive_metric": (C.c_int, [_vp]),
+    "spf_src_neighbors": (C.c_int, [_vp, C.c_uint32, _u32p, C.c_uint32, _u32p]),
+    "spf_plan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.c_uint32, C.POINTER(_vp)]),
+    "spf_plan_destroy": (None, [_vp]),
+    "spf_plan_nh_words": (C.c_uint64, [_vp]),
+    "spf_plan_nh_layout": (C.c_int, [_vp, _u64p, _u32p]),
+    "spf_plan_closure_rows": (C.c_uint32, [_vp]),
+    "spf_plan_execute": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "spf_plan_enable_timing": (C.c_int, [_vp, C.c_uint32]),
+    "spf_plan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
+    "spf_solve": (C.c_int, [_vp, _u32p, C.c_uint32, C.c_uint32, _u32p, _u32p]),
+    "spf_sssp": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u32p]),
+    "spf_preds": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u32p,
+                            _u32p, _u32p, C.c_uint32, _u32p]),
+    "spf_solves": (C.c_uint64, [_vp]),
+    # LinkState facade (openr_linkstate.h)
+    "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
+    "ls_destroy": (None, [_vp]),
+    "ls_last_error": (C.c_char_p, [_vp]),
+    "ls_update_adjacency_databases": (C.c_int, [_vp, C.POINTER(OpenrLsdb), C.c_uint64,
+                                                C.c_uint64, C.POINTER(LsChange)]),
+    "ls_delete_adjacency_database": (C.c_int, [_vp, C.c_char_p, C.POINTER(LsChange)]),
+    "ls_decrement_holds": (C.c_int, [_vp, C.POINTER(LsChange)]),
+    "ls_has_holds": (C.c_int, [_vp]),
+    "ls_num_links": (C.c_uint64, [_vp]),
+    "ls_num_nodes": (C.c_uint64, [_vp]),
+    "ls_has_node": (C.c_int, [_vp, C.c_char_p]),
+    "ls_is_node_overloaded": (C.c_int, [_vp, C.c_char_p]),
+    "ls_name_id": (C.c_uint32, [_vp, C.c_char_p]),
+    "ls_name": (C.c_char_p, [_vp, C.c_uint32]),
+    "ls_links_from_node": (C.c_int, [_vp, C.c_char_p, _u32p, C.c_uint32, _u32p]),
+    "ls_link_info": (C.c_int, [_vp, C.c_uint32, C.POINTER(LsLinkDesc)]),
+    "ls_get_spf_result": (C.c_int, [_vp, C.c_char_p, C.c_int, C.POINTER(LsSpfView)]),
+    "ls_get_kth_paths": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_uint64,
+                                   C.POINTER(LsPathsView)]),
+    "ls_get_metric_a_to_b": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_int, _u64p,
+                                       C.POINTER(C.c_int)]),
+    "ls_get_max_hops_to_node": (C.c_int, [_vp, C.c_char_p, _u64p]),
+    "ls_spf_runs": (C.c_uint64, [_vp]),
+    "ls_engine": (_vp, [_vp]),
+    "ls_flatten": (C.c_int, [_vp, _u32p, _u32p]),
+    "ls_graph_node_names": (C.c_int, [_vp, _u32p]),
+    "ls_graph_csr": (C.c_int, [_vp, _u32p, _u32p, _i32p, _u32p, _u8p]),
+}
+
+
+def _load() -> C.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -m openr_amd.build` "
+            "(the SPF path has no CPU fallback)"
+        )
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def ptr(a: np.ndarray, ctype=C.c_uint32):
+    """ctypes pointer to a C-contiguous numpy array (caller keeps it alive)."""
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def global_error() -> str:
+    return (lib.spf_global_error() or b"").decode()
+
+
+def lsdb_struct(packed) -> OpenrLsdb:
+    """OpenrLsdb view of a PackedLsdb (keep `packed` alive while in use)."""
+    s = OpenrLsdb()
+    s.blob = packed.blob
+    s.dbs = packed.dbs.ctypes.data
+    s.n_dbs = len(packed.dbs)
+    s.adjs = packed.adjs.ctypes.data if len(packed.adjs) else None
+    return s

@@ -1,0 +1,885 @@
+// ============================================================================
+//  link_state.cpp -- host side of the LinkState drop-in (openr_linkstate.h).
+//
+//  Two halves:
+//   * LSDB bookkeeping with the reference's semantics -- bidirectional-link
+//     check (reference openr/decision/LinkState.cpp:531-547), ordered merge of
+//     old/new links (:564-719), ordered-FIB holds (HoldableValue, :54-125),
+//     link / node overload (:233-236, :480-498), deletion (:721-738).
+//     Links of a node are kept in a std::unordered_set hashed exactly like
+//     the reference's LinkSet (folly pair hash of the ordered (node, ifName)
+//     names, LinkState.cpp:138-142), so that its iteration order -- which the
+//     reference's Dijkstra uses to order parallel links in pathLinks -- is
+//     reproduced; the CSR lists each node's edges in that order.
+//   * Shortest paths: flatten the up links into a CSR once per topology
+//     version and run every SPF on the MI355X engine (spf_engine.hip).  Results
+//     are memoised per (node, useLinkMetric) and per (src, dst, k) and
+//     invalidated on topology changes, as LinkState.h:271-301 does.
+// ============================================================================
+#include <algorithm>
+#include <array>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <optional>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "openr_linkstate.h"
+
+namespace openr_amd {
+namespace {
+
+using Metric = uint64_t;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// folly::hash::hash_128_to_64, the combiner behind folly's
+// std::hash<std::pair<A, B>> (= mix(std::hash<A>(a), std::hash<B>(b))).
+inline uint64_t folly_mix(uint64_t upper, uint64_t lower) {
+  constexpr uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lower ^ upper) * kMul;
+  a ^= a >> 47;
+  uint64_t b = (upper ^ a) * kMul;
+  b ^= b >> 47;
+  return b * kMul;
+}
+
+// Ordered-FIB holdable value (rfc 6976), reference LinkState.h:36-58.
+template <class T>
+struct Holdable {
+  T val;
+  std::optional<T> held;
+  Metric ttl = 0;
+  explicit Holdable(T v) : val(v) {}
+  void set(T v) {  // plain assignment: clears any hold
+    val = v;
+    held.reset();
+    ttl = 0;
+  }
+  const T& get() const { return held ? *held : val; }
+  bool has_hold() const { return held.has_value(); }
+  bool tick() {
+    if (!held) return false;
+    if (--ttl != 0) return false;
+    held.reset();
+    return true;
+  }
+  bool bring_up(T v) const;
+  // returns true when the effective value changes now
+  bool update(T v, Metric up, Metric down) {
+    if (v == val) return false;
+    if (held) {
+      held.reset();
+      ttl = 0;
+    } else {
+      ttl = bring_up(v) ? up : down;
+      if (ttl) held = val;
+    }
+    val = v;
+    return !held;
+  }
+};
+template <>
+bool Holdable<bool>::bring_up(bool v) const { return val && !v; }
+template <>
+bool Holdable<Metric>::bring_up(Metric v) const { return v < val; }
+
+using OrderedNames =
+    std::pair<std::pair<std::string, std::string>, std::pair<std::string, std::string>>;
+
+struct Side {
+  uint32_t node;
+  std::string ifname;
+  Holdable<Metric> metric{1};
+  Holdable<bool> overload{false};
+  int32_t label = 0;
+  std::array<uint8_t, 4> v4{};
+  std::array<uint8_t, 16> v6{};
+};
+
+struct LinkObj {
+  uint32_t id = kNone;
+  Side s[2];
+  Metric hold_up = 0;
+  OrderedNames names;
+  uint64_t hash = 0;
+
+  int side_of(uint32_t n) const { return s[0].node == n ? 0 : (s[1].node == n ? 1 : -1); }
+  Side& from(uint32_t n) { return s[side_of(n)]; }
+  const Side& from(uint32_t n) const { return s[side_of(n)]; }
+  uint32_t other(uint32_t n) const { return s[0].node == n ? s[1].node : s[0].node; }
+  bool up() const { return hold_up == 0 && !s[0].overload.get() && !s[1].overload.get(); }
+  bool before(const LinkObj& o) const {  // Link::operator< (LinkState.cpp:347-353)
+    return hash != o.hash ? hash < o.hash : names < o.names;
+  }
+  bool same(const LinkObj& o) const { return hash == o.hash && names == o.names; }
+  bool tick() {
+    bool expired = false;
+    if (hold_up) expired |= (--hold_up == 0);
+    for (auto& x : s) {
+      expired |= x.metric.tick();
+      expired |= x.overload.tick();
+    }
+    return expired;
+  }
+  bool holds() const {
+    return hold_up || s[0].metric.has_hold() || s[1].metric.has_hold() ||
+           s[0].overload.has_hold() || s[1].overload.has_hold();
+  }
+};
+
+// NB: not noexcept, as the reference's LinkPtrHash -- keeps libstdc++'s node
+// layout (cached hash codes) identical; iteration order depends only on the
+// hash values and the insert/erase sequence.
+struct LinkHash {
+  size_t operator()(const LinkObj* l) const { return l->hash; }
+};
+struct LinkEq {
+  bool operator()(const LinkObj* a, const LinkObj* b) const { return a->same(*b); }
+};
+using LinkBag = std::unordered_set<LinkObj*, LinkHash, LinkEq>;
+
+struct AdjIn {
+  uint32_t other;
+  std::string ifname, other_if;
+  int32_t metric, label;
+  bool overload;
+  std::array<uint8_t, 4> v4;
+  std::array<uint8_t, 16> v6;
+};
+struct DbIn {
+  bool overload = false;
+  int32_t node_label = 0;
+  std::vector<AdjIn> adjs;
+};
+
+struct SpfMemo {
+  std::vector<uint32_t> node, nh_ptr{0}, nh_node, pl_ptr{0}, pl_link, pl_prev;
+  std::vector<uint64_t> metric;
+  // csr-indexed predecessor lists for path tracing
+  std::vector<uint32_t> pred_ptr, pred_edge;
+  std::vector<uint32_t> dist;  // csr-indexed (empty for an off-graph source)
+};
+struct PathMemo {
+  std::vector<uint32_t> path_ptr{0}, link;
+};
+
+}  // namespace
+}  // namespace openr_amd
+
+using namespace openr_amd;
+
+struct ls_state {
+  std::string area;
+  int device = 0;
+  std::string err;
+  spf_ctx* eng = nullptr;
+  uint64_t spf_runs = 0;
+
+  // names
+  std::vector<std::string> names;
+  std::unordered_map<std::string, uint32_t> name_ids;
+
+  // LSDB
+  std::unordered_map<uint32_t, DbIn> dbs;
+  std::unordered_map<uint32_t, LinkBag> link_map;
+  LinkBag all_links;
+  std::unordered_map<uint32_t, Holdable<bool>> node_ovl;
+  std::vector<std::unique_ptr<LinkObj>> slab;
+  std::vector<uint32_t> free_ids;
+
+  // flattened graph
+  bool dirty = true;
+  std::vector<uint32_t> csr_name;   // csr id -> name id
+  std::vector<uint32_t> csr_of;     // name id -> csr id (kNone)
+  std::vector<uint32_t> row_ptr, col, link_id, edge_tail;
+  std::vector<int32_t> metric;
+  std::vector<uint8_t> ovl;
+
+  // memo
+  std::map<std::pair<uint32_t, int>, SpfMemo> spf_memo;
+  std::map<std::tuple<uint32_t, uint32_t, uint64_t>, PathMemo> ksp_memo;
+
+  uint32_t intern(const std::string& s) {
+    auto it = name_ids.find(s);
+    if (it != name_ids.end()) return it->second;
+    const uint32_t id = (uint32_t)names.size();
+    names.push_back(s);
+    name_ids.emplace(s, id);
+    return id;
+  }
+  const uint32_t* find_name(const std::string& s) const {
+    auto it = name_ids.find(s);
+    return it == name_ids.end() ? nullptr : &it->second;
+  }
+};
+
+namespace {
+
+spf_status lfail(ls_state* ls, spf_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ls) ls->err = buf;
+  return st;
+}
+
+spf_status eng_fail(ls_state* ls, spf_status st) {
+  ls->err = std::string("engine: ") + spf_last_error(ls->eng);
+  return st;
+}
+
+void clear_memo(ls_state* ls) {
+  ls->spf_memo.clear();
+  ls->ksp_memo.clear();
+  ls->dirty = true;
+}
+
+void put_change(ls_change* out, bool topo, bool attrs, bool label) {
+  if (!out) return;
+  out->topology_changed = topo;
+  out->link_attributes_changed = attrs;
+  out->node_label_changed = label;
+  out->pad = 0;
+}
+
+std::unique_ptr<LinkObj> make_link(ls_state* ls, uint32_t n1, const AdjIn& a1, uint32_t n2,
+                                   const AdjIn& a2) {
+  auto l = std::make_unique<LinkObj>();
+  const AdjIn* in[2] = {&a1, &a2};
+  const uint32_t nodes[2] = {n1, n2};
+  for (int i = 0; i < 2; ++i) {
+    Side& s = l->s[i];
+    s.node = nodes[i];
+    s.ifname = in[i]->ifname;
+    s.metric.set((Metric)(int64_t)in[i]->metric);  // i32 -> u64 like the reference
+    s.overload.set(in[i]->overload);
+    s.label = in[i]->label;
+    s.v4 = in[i]->v4;
+    s.v6 = in[i]->v6;
+  }
+  l->names = std::minmax(std::make_pair(ls->names[n1], a1.ifname),
+                         std::make_pair(ls->names[n2], a2.ifname));
+  const auto& nm = l->names;
+  l->hash = folly_mix(folly_mix(std::hash<std::string>()(nm.first.first),
+                                std::hash<std::string>()(nm.first.second)),
+                      folly_mix(std::hash<std::string>()(nm.second.first),
+                                std::hash<std::string>()(nm.second.second)));
+  return l;
+}
+
+uint32_t first_node(const ls_state* ls, const LinkObj& l) {
+  return ls->name_ids.at(l.names.first.first);
+}
+uint32_t second_node(const ls_state* ls, const LinkObj& l) {
+  return ls->name_ids.at(l.names.second.first);
+}
+
+// maybeMakeLink (LinkState.cpp:531-547): only bidirectional adjacencies
+std::unique_ptr<LinkObj> bidir(ls_state* ls, uint32_t node, const AdjIn& a) {
+  auto it = ls->dbs.find(a.other);
+  if (it == ls->dbs.end()) return nullptr;
+  for (const AdjIn& b : it->second.adjs) {
+    if (b.other == node && a.other_if == b.ifname && a.ifname == b.other_if)
+      return make_link(ls, node, a, a.other, b);
+  }
+  return nullptr;
+}
+
+LinkObj* adopt(ls_state* ls, std::unique_ptr<LinkObj> l) {
+  uint32_t id;
+  if (!ls->free_ids.empty()) {
+    id = ls->free_ids.back();
+    ls->free_ids.pop_back();
+  } else {
+    id = (uint32_t)ls->slab.size();
+    ls->slab.emplace_back();
+  }
+  l->id = id;
+  ls->slab[id] = std::move(l);
+  return ls->slab[id].get();
+}
+
+void release(ls_state* ls, LinkObj* l) {
+  const uint32_t id = l->id;
+  ls->slab[id].reset();
+  ls->free_ids.push_back(id);
+}
+
+bool add_link(ls_state* ls, LinkObj* l) {
+  bool ok = ls->link_map[first_node(ls, *l)].insert(l).second;
+  ok &= ls->link_map[second_node(ls, *l)].insert(l).second;
+  ok &= ls->all_links.insert(l).second;
+  return ok;
+}
+
+bool set_node_overload(ls_state* ls, uint32_t node, bool o, Metric up, Metric down) {
+  auto it = ls->node_ovl.find(node);
+  if (it != ls->node_ovl.end()) return it->second.update(o, up, down);
+  ls->node_ovl.emplace(node, Holdable<bool>(o));
+  return false;  // a node seen for the first time never signals a change
+}
+
+bool node_overloaded(const ls_state* ls, uint32_t node) {
+  auto it = ls->node_ovl.find(node);
+  return it != ls->node_ovl.end() && it->second.get();
+}
+
+// updateAdjacencyDatabase (LinkState.cpp:564-719)
+spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric down,
+                    ls_change* out) {
+  bool topo = false, attrs = false, label;
+  DbIn& slot = ls->dbs[node];
+  const int32_t prior_label = slot.node_label;
+  slot = std::move(db);
+  const DbIn& cur = slot;
+
+  std::vector<LinkObj*> old_links;
+  if (auto it = ls->link_map.find(node); it != ls->link_map.end())
+    old_links.assign(it->second.begin(), it->second.end());
+  auto by_order = [](const LinkObj* a, const LinkObj* b) { return a->before(*b); };
+  std::sort(old_links.begin(), old_links.end(), by_order);
+
+  std::vector<std::unique_ptr<LinkObj>> fresh;
+  for (const AdjIn& a : cur.adjs)
+    if (auto l = bidir(ls, node, a)) fresh.push_back(std::move(l));
+  std::sort(fresh.begin(), fresh.end(),
+            [](const std::unique_ptr<LinkObj>& a, const std::unique_ptr<LinkObj>& b) {
+              return a->before(*b);
+            });
+
+  topo |= set_node_overload(ls, node, cur.overload, up, down);
+  label = prior_label != cur.node_label;
+
+  size_t i = 0, j = 0;
+  while (i < fresh.size() || j < old_links.size()) {
+    if (i < fresh.size() && (j == old_links.size() || fresh[i]->before(*old_links[j]))) {
+      fresh[i]->hold_up = up;
+      topo |= fresh[i]->up();
+      LinkObj* l = adopt(ls, std::move(fresh[i]));
+      if (!add_link(ls, l))
+        return lfail(ls, SPF_E_INVALID, "duplicate link while adding adjacency of %s",
+                     ls->names[node].c_str());
+      ++i;
+      continue;
+    }
+    if (j < old_links.size() && (i == fresh.size() || old_links[j]->before(*fresh[i]))) {
+      LinkObj* l = old_links[j];
+      topo |= l->up();
+      ls->link_map.at(first_node(ls, *l)).erase(l);
+      ls->link_map.at(second_node(ls, *l)).erase(l);
+      ls->all_links.erase(l);
+      release(ls, l);
+      ++j;
+      continue;
+    }
+    // same link: apply this node's side of the attributes
+    Side& o = old_links[j]->from(node);
+    const Side& n = fresh[i]->from(node);
+    if (n.metric.get() != o.metric.get()) {
+      topo |= o.metric.update(n.metric.get(), up, down);
+    }
+    if (n.overload.get() != o.overload.get()) {
+      const bool was_up = old_links[j]->up();
+      o.overload.update(n.overload.get(), up, down);
+      topo |= was_up != old_links[j]->up();
+    }
+    if (n.label != o.label) {
+      attrs = true;
+      o.label = n.label;
+    }
+    if (n.v4 != o.v4) {
+      attrs = true;
+      o.v4 = n.v4;
+    }
+    if (n.v6 != o.v6) {
+      attrs = true;
+      o.v6 = n.v6;
+    }
+    ++i;
+    ++j;
+  }
+  if (topo) clear_memo(ls);
+  put_change(out, topo, attrs, label);
+  return SPF_OK;
+}
+
+// CSR flatten: ids in ascending name order, edges in linksFromNode order.
+spf_status flatten(ls_state* ls) {
+  if (!ls->dirty) return SPF_OK;
+  std::vector<uint32_t> ids;
+  ids.reserve(ls->dbs.size());
+  for (const auto& kv : ls->dbs) ids.push_back(kv.first);
+  std::sort(ids.begin(), ids.end(),
+            [&](uint32_t a, uint32_t b) { return ls->names[a] < ls->names[b]; });
+  ls->csr_name = ids;
+  ls->csr_of.assign(ls->names.size(), kNone);
+  for (uint32_t i = 0; i < ids.size(); ++i) ls->csr_of[ids[i]] = i;
+  const uint32_t N = (uint32_t)ids.size();
+  ls->row_ptr.assign(N + 1, 0);
+  ls->col.clear();
+  ls->metric.clear();
+  ls->link_id.clear();
+  ls->edge_tail.clear();
+  ls->ovl.assign(N, 0);
+  for (uint32_t u = 0; u < N; ++u) {
+    const uint32_t nm = ids[u];
+    ls->ovl[u] = node_overloaded(ls, nm);
+    auto it = ls->link_map.find(nm);
+    if (it != ls->link_map.end()) {
+      for (const LinkObj* l : it->second) {
+        if (!l->up()) continue;
+        const uint32_t v = ls->csr_of[l->other(nm)];
+        if (v == kNone) return lfail(ls, SPF_E_INVALID, "link to node without a database");
+        ls->col.push_back(v);
+        ls->metric.push_back((int32_t)(uint32_t)l->from(nm).metric.get());
+        ls->link_id.push_back(l->id);
+        ls->edge_tail.push_back(u);
+      }
+    }
+    ls->row_ptr[u + 1] = (uint32_t)ls->col.size();
+  }
+  if (N > 0 && ls->eng) {
+    spf_graph g;
+    g.n_nodes = N;
+    g.n_edges = (uint32_t)ls->col.size();
+    g.row_ptr = ls->row_ptr.data();
+    g.col = ls->col.data();
+    g.metric = ls->metric.data();
+    g.link_id = ls->link_id.data();
+    g.overloaded = ls->ovl.data();
+    const spf_status st = spf_graph_load(ls->eng, &g);
+    if (st != SPF_OK) return eng_fail(ls, st);
+  }
+  ls->dirty = false;
+  return SPF_OK;
+}
+
+void fill_view(const SpfMemo& m, ls_spf_view* out) {
+  out->n = (uint32_t)m.node.size();
+  out->node = m.node.data();
+  out->metric = m.metric.data();
+  out->nh_ptr = m.nh_ptr.data();
+  out->nh_node = m.nh_node.data();
+  out->pl_ptr = m.pl_ptr.data();
+  out->pl_link = m.pl_link.data();
+  out->pl_prev = m.pl_prev.data();
+}
+
+// getSpfResult (LinkState.cpp:793-803) -> memo entry
+spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out) {
+  auto key = std::make_pair(node, (int)ulm);
+  auto it = ls->spf_memo.find(key);
+  if (it != ls->spf_memo.end()) {
+    *out = &it->second;
+    return SPF_OK;
+  }
+  spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  if (!ls->eng) return lfail(ls, SPF_E_NO_DEVICE, "LinkState created host-only (device < 0)");
+  SpfMemo m;
+  ls->spf_runs++;  // decision.spf_runs (LinkState.cpp:815)
+  const uint32_t s = node < ls->csr_of.size() ? ls->csr_of[node] : kNone;
+  if (s == kNone) {
+    // not in the graph: the reference's Dijkstra records only the source
+    m.node.push_back(node);
+    m.metric.push_back(0);
+    m.nh_ptr.push_back(0);
+    m.pl_ptr.push_back(0);
+  } else {
+    const uint32_t N = (uint32_t)ls->csr_name.size();
+    const uint32_t flags = ulm ? 0u : SPF_FLAG_HOP_COUNT;
+    uint32_t k = 0;
+    spf_src_neighbors(ls->eng, s, nullptr, 0, &k);
+    std::vector<uint32_t> nbr(k);
+    spf_src_neighbors(ls->eng, s, nbr.data(), k, &k);
+    const uint32_t pitch = spf_row_pitch(ls->eng);
+    const uint64_t words = (uint64_t)((k + 31) / 32) * pitch;
+    m.dist.resize(N);
+    std::vector<uint32_t> nh(std::max<uint64_t>(words, 1));
+    st = spf_solve(ls->eng, &s, 1, flags, m.dist.data(), nh.data());
+    if (st != SPF_OK) return eng_fail(ls, st);
+    uint32_t npred = 0;
+    m.pred_ptr.resize(N + 1);
+    st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(), nullptr, 0, &npred);
+    if (st != SPF_OK) return eng_fail(ls, st);
+    m.pred_edge.resize(npred);
+    st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(),
+                   m.pred_edge.data(), npred, &npred);
+    if (st != SPF_OK) return eng_fail(ls, st);
+    for (uint32_t v = 0; v < N; ++v) {
+      if (m.dist[v] == SPF_UNREACHABLE) continue;
+      m.node.push_back(ls->csr_name[v]);
+      m.metric.push_back(m.dist[v]);
+      for (uint32_t j = 0; j < k; ++j)
+        if ((nh[(size_t)(j >> 5) * pitch + v] >> (j & 31)) & 1u)
+          m.nh_node.push_back(ls->csr_name[nbr[j]]);
+      m.nh_ptr.push_back((uint32_t)m.nh_node.size());
+      for (uint32_t p = m.pred_ptr[v]; p < m.pred_ptr[v + 1]; ++p) {
+        const uint32_t e = m.pred_edge[p];
+        m.pl_link.push_back(ls->link_id[e]);
+        m.pl_prev.push_back(ls->csr_name[ls->edge_tail[e]]);
+      }
+      m.pl_ptr.push_back((uint32_t)m.pl_link.size());
+    }
+  }
+  *out = &ls->spf_memo.emplace(key, std::move(m)).first->second;
+  return SPF_OK;
+}
+
+// traceOnePath (LinkState.cpp:398-419) over csr predecessor lists
+bool trace(const ls_state* ls, uint32_t src, uint32_t dst, const std::vector<uint32_t>& pred_ptr,
+           const std::vector<uint32_t>& pred_edge, std::unordered_set<uint32_t>& used,
+           std::vector<uint32_t>& path) {
+  if (src == dst) return true;
+  for (uint32_t p = pred_ptr[dst]; p < pred_ptr[dst + 1]; ++p) {
+    const uint32_t e = pred_edge[p];
+    if (!used.insert(ls->link_id[e]).second) continue;
+    if (trace(ls, src, ls->edge_tail[e], pred_ptr, pred_edge, used, path)) {
+      path.push_back(ls->link_id[e]);
+      return true;
+    }
+  }
+  return false;
+}
+
+spf_status kth_paths(ls_state* ls, uint32_t src, uint32_t dst, uint64_t k, const PathMemo** out) {
+  auto key = std::make_tuple(src, dst, k);
+  auto it = ls->ksp_memo.find(key);
+  if (it != ls->ksp_memo.end()) {
+    *out = &it->second;
+    return SPF_OK;
+  }
+  std::vector<uint32_t> ignore;
+  {
+    std::unordered_set<uint32_t> seen;
+    for (uint64_t i = 1; i < k; ++i) {
+      const PathMemo* pm = nullptr;
+      const spf_status st = kth_paths(ls, src, dst, i, &pm);
+      if (st != SPF_OK) return st;
+      for (uint32_t l : pm->link)
+        if (seen.insert(l).second) ignore.push_back(l);
+    }
+  }
+  PathMemo res;
+  const std::vector<uint32_t>* pptr = nullptr;
+  const std::vector<uint32_t>* pedge = nullptr;
+  std::vector<uint32_t> dist, my_ptr, my_edge;
+  bool reachable = false;
+  uint32_t s = kNone, d = kNone;
+  if (ignore.empty()) {
+    const SpfMemo* m = nullptr;
+    const spf_status st = spf_result(ls, src, true, &m);
+    if (st != SPF_OK) return st;
+    s = src < ls->csr_of.size() ? ls->csr_of[src] : kNone;
+    d = dst < ls->csr_of.size() ? ls->csr_of[dst] : kNone;
+    if (s != kNone && d != kNone) {
+      reachable = m->dist[d] != SPF_UNREACHABLE;
+      pptr = &m->pred_ptr;
+      pedge = &m->pred_edge;
+    }
+  } else {
+    spf_status st = flatten(ls);
+    if (st != SPF_OK) return st;
+    if (!ls->eng) return lfail(ls, SPF_E_NO_DEVICE, "LinkState created host-only (device < 0)");
+    s = ls->csr_of[src];
+    d = ls->csr_of[dst];
+    ls->spf_runs++;  // the un-memoised runSpf of LinkState.cpp:778-779
+    const uint32_t N = (uint32_t)ls->csr_name.size();
+    dist.resize(N);
+    st = spf_sssp(ls->eng, s, 0, ignore.data(), (uint32_t)ignore.size(), dist.data());
+    if (st != SPF_OK) return eng_fail(ls, st);
+    reachable = dist[d] != SPF_UNREACHABLE;
+    if (reachable) {
+      uint32_t np = 0;
+      my_ptr.resize(N + 1);
+      st = spf_preds(ls->eng, s, 0, ignore.data(), (uint32_t)ignore.size(), dist.data(),
+                     my_ptr.data(), nullptr, 0, &np);
+      if (st != SPF_OK) return eng_fail(ls, st);
+      my_edge.resize(np);
+      st = spf_preds(ls->eng, s, 0, ignore.data(), (uint32_t)ignore.size(), dist.data(),
+                     my_ptr.data(), my_edge.data(), np, &np);
+      if (st != SPF_OK) return eng_fail(ls, st);
+      pptr = &my_ptr;
+      pedge = &my_edge;
+    }
+  }
+  if (reachable && s != d) {
+    std::unordered_set<uint32_t> used;
+    for (;;) {
+      std::vector<uint32_t> path;
+      if (!trace(ls, s, d, *pptr, *pedge, used, path) || path.empty()) break;
+      res.link.insert(res.link.end(), path.begin(), path.end());
+      res.path_ptr.push_back((uint32_t)res.link.size());
+    }
+  }
+  *out = &ls->ksp_memo.emplace(key, std::move(res)).first->second;
+  return SPF_OK;
+}
+
+spf_status read_lsdb(ls_state* ls, const openr_lsdb* in, uint32_t d, uint32_t* node, DbIn* db) {
+  const openr_db_rec& r = in->dbs[d];
+  *node = ls->intern(std::string(in->blob + r.name_off, r.name_len));
+  db->overload = r.is_overloaded != 0;
+  db->node_label = r.node_label;
+  db->adjs.clear();
+  db->adjs.reserve(r.adj_count);
+  for (uint32_t k = 0; k < r.adj_count; ++k) {
+    const openr_adj_rec& a = in->adjs[r.adj_begin + k];
+    AdjIn x;
+    x.other = ls->intern(std::string(in->blob + a.other_off, a.other_len));
+    x.ifname.assign(in->blob + a.if_off, a.if_len);
+    x.other_if.assign(in->blob + a.oif_off, a.oif_len);
+    x.metric = a.metric;
+    x.label = a.adj_label;
+    x.overload = a.is_overloaded != 0;
+    std::memcpy(x.v4.data(), a.nh_v4, 4);
+    std::memcpy(x.v6.data(), a.nh_v6, 16);
+    db->adjs.push_back(std::move(x));
+  }
+  return SPF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+spf_status ls_create(const char* area, int device, ls_state** out) {
+  if (!out) return SPF_E_INVALID;
+  *out = nullptr;
+  auto ls = std::make_unique<ls_state>();
+  ls->area = area ? area : "0";
+  ls->device = device;
+  if (device >= 0) {  // device < 0: host-only (LSDB + flatten, no solves)
+    const spf_status st = spf_ctx_create(device, &ls->eng);
+    if (st != SPF_OK) return st;  // spf_global_error() has the reason
+  }
+  *out = ls.release();
+  return SPF_OK;
+}
+
+void ls_destroy(ls_state* ls) {
+  if (!ls) return;
+  spf_ctx_destroy(ls->eng);
+  delete ls;
+}
+
+const char* ls_last_error(const ls_state* ls) {
+  return ls ? ls->err.c_str() : spf_global_error();
+}
+
+spf_status ls_update_adjacency_databases(ls_state* ls, const openr_lsdb* lsdb, uint64_t up,
+                                         uint64_t down, ls_change* changes) {
+  if (!ls || !lsdb) return SPF_E_INVALID;
+  for (uint32_t d = 0; d < lsdb->n_dbs; ++d) {
+    uint32_t node;
+    DbIn db;
+    spf_status st = read_lsdb(ls, lsdb, d, &node, &db);
+    if (st != SPF_OK) return st;
+    st = apply_db(ls, node, std::move(db), up, down, changes ? changes + d : nullptr);
+    if (st != SPF_OK) return st;
+  }
+  return SPF_OK;
+}
+
+// deleteAdjacencyDatabase (LinkState.cpp:721-738) + removeNode (:436-455)
+spf_status ls_delete_adjacency_database(ls_state* ls, const char* node, ls_change* change) {
+  if (!ls || !node) return SPF_E_INVALID;
+  const uint32_t* id = ls->find_name(node);
+  if (!id || !ls->dbs.count(*id)) {
+    put_change(change, false, false, false);
+    return SPF_OK;
+  }
+  const uint32_t n = *id;
+  auto it = ls->link_map.find(n);
+  if (it != ls->link_map.end()) {
+    std::vector<LinkObj*> doomed(it->second.begin(), it->second.end());
+    for (LinkObj* l : it->second) {
+      ls->link_map.at(l->other(n)).erase(l);
+      ls->all_links.erase(l);
+    }
+    ls->link_map.erase(it);
+    ls->node_ovl.erase(n);
+    for (LinkObj* l : doomed) release(ls, l);
+  }
+  ls->dbs.erase(n);
+  clear_memo(ls);
+  put_change(change, true, false, false);
+  return SPF_OK;
+}
+
+spf_status ls_decrement_holds(ls_state* ls, ls_change* change) {
+  if (!ls) return SPF_E_INVALID;
+  bool topo = false;
+  for (LinkObj* l : ls->all_links) topo |= l->tick();
+  for (auto& kv : ls->node_ovl) topo |= kv.second.tick();
+  if (topo) clear_memo(ls);
+  put_change(change, topo, false, false);
+  return SPF_OK;
+}
+
+int ls_has_holds(const ls_state* ls) {
+  for (const LinkObj* l : ls->all_links)
+    if (l->holds()) return 1;
+  for (const auto& kv : ls->node_ovl)
+    if (kv.second.has_hold()) return 1;
+  return 0;
+}
+uint64_t ls_num_links(const ls_state* ls) { return ls->all_links.size(); }
+uint64_t ls_num_nodes(const ls_state* ls) { return ls->link_map.size(); }
+int ls_has_node(const ls_state* ls, const char* node) {
+  const uint32_t* id = ls->find_name(node);
+  return id && ls->dbs.count(*id);
+}
+int ls_is_node_overloaded(const ls_state* ls, const char* node) {
+  const uint32_t* id = ls->find_name(node);
+  return id && node_overloaded(ls, *id);
+}
+uint32_t ls_name_id(ls_state* ls, const char* name) { return ls->intern(name); }
+const char* ls_name(const ls_state* ls, uint32_t id) {
+  return id < ls->names.size() ? ls->names[id].c_str() : nullptr;
+}
+
+spf_status ls_links_from_node(const ls_state* ls, const char* node, uint32_t* ids, uint32_t cap,
+                              uint32_t* count) {
+  if (!ls || !node || !count) return SPF_E_INVALID;
+  *count = 0;
+  const uint32_t* id = ls->find_name(node);
+  if (!id) return SPF_OK;
+  auto it = ls->link_map.find(*id);
+  if (it == ls->link_map.end()) return SPF_OK;
+  uint32_t n = 0;
+  for (const LinkObj* l : it->second) {
+    if (ids && n < cap) ids[n] = l->id;
+    ++n;
+  }
+  *count = n;
+  return SPF_OK;
+}
+
+spf_status ls_link_info(const ls_state* ls, uint32_t link_id, ls_link_desc* out) {
+  if (!ls || !out) return SPF_E_INVALID;
+  if (link_id >= ls->slab.size() || !ls->slab[link_id]) return SPF_E_INVALID;
+  const LinkObj& l = *ls->slab[link_id];
+  out->node1 = l.s[0].node;
+  out->node2 = l.s[1].node;
+  out->if1 = l.s[0].ifname.c_str();
+  out->if2 = l.s[1].ifname.c_str();
+  out->first_node = first_node(ls, l);
+  out->second_node = second_node(ls, l);
+  out->metric1 = l.s[0].metric.get();
+  out->metric2 = l.s[1].metric.get();
+  out->adj_label1 = l.s[0].label;
+  out->adj_label2 = l.s[1].label;
+  out->overload1 = l.s[0].overload.get();
+  out->overload2 = l.s[1].overload.get();
+  out->is_up = l.up();
+  out->pad = 0;
+  out->hash = l.hash;
+  out->nh_v4_1 = l.s[0].v4.data();
+  out->nh_v4_2 = l.s[1].v4.data();
+  out->nh_v6_1 = l.s[0].v6.data();
+  out->nh_v6_2 = l.s[1].v6.data();
+  return SPF_OK;
+}
+
+spf_status ls_get_spf_result(ls_state* ls, const char* node, int ulm, ls_spf_view* out) {
+  if (!ls || !node || !out) return SPF_E_INVALID;
+  const SpfMemo* m = nullptr;
+  const spf_status st = spf_result(ls, ls->intern(node), ulm != 0, &m);
+  if (st != SPF_OK) return st;
+  fill_view(*m, out);
+  return SPF_OK;
+}
+
+spf_status ls_get_kth_paths(ls_state* ls, const char* src, const char* dst, uint64_t k,
+                            ls_paths_view* out) {
+  if (!ls || !src || !dst || !out) return SPF_E_INVALID;
+  if (k < 1) return lfail(ls, SPF_E_INVALID, "getKthPaths: k must be >= 1 (CHECK_GE, LinkState.cpp:765)");
+  const PathMemo* pm = nullptr;
+  const spf_status st = kth_paths(ls, ls->intern(src), ls->intern(dst), k, &pm);
+  if (st != SPF_OK) return st;
+  out->n_paths = (uint32_t)pm->path_ptr.size() - 1;
+  out->path_ptr = pm->path_ptr.data();
+  out->link = pm->link.data();
+  return SPF_OK;
+}
+
+// getMetricFromAToB (LinkState.cpp:740-751)
+spf_status ls_get_metric_a_to_b(ls_state* ls, const char* a, const char* b, int ulm,
+                                uint64_t* metric, int* has) {
+  if (!ls || !a || !b || !metric || !has) return SPF_E_INVALID;
+  *has = 0;
+  if (std::strcmp(a, b) == 0) {
+    *metric = 0;
+    *has = 1;
+    return SPF_OK;
+  }
+  const SpfMemo* m = nullptr;
+  const spf_status st = spf_result(ls, ls->intern(a), ulm != 0, &m);
+  if (st != SPF_OK) return st;
+  const uint32_t bid = ls->intern(b);
+  for (size_t i = 0; i < m->node.size(); ++i)
+    if (m->node[i] == bid) {
+      *metric = m->metric[i];
+      *has = 1;
+      break;
+    }
+  return SPF_OK;
+}
+
+// getMaxHopsToNode (LinkState.cpp:753-760)
+spf_status ls_get_max_hops_to_node(ls_state* ls, const char* node, uint64_t* out) {
+  if (!ls || !node || !out) return SPF_E_INVALID;
+  const SpfMemo* m = nullptr;
+  const spf_status st = spf_result(ls, ls->intern(node), false, &m);
+  if (st != SPF_OK) return st;
+  uint64_t mx = 0;
+  for (uint64_t v : m->metric) mx = std::max(mx, v);
+  *out = mx;
+  return SPF_OK;
+}
+
+uint64_t ls_spf_runs(const ls_state* ls) { return ls ? ls->spf_runs : 0; }
+
+spf_ctx* ls_engine(ls_state* ls) { return ls ? ls->eng : nullptr; }
+
+spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges) {
+  if (!ls) return SPF_E_INVALID;
+  const spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  if (n_nodes) *n_nodes = (uint32_t)ls->csr_name.size();
+  if (n_edges) *n_edges = (uint32_t)ls->col.size();
+  return SPF_OK;
+}
+
+spf_status ls_graph_csr(ls_state* ls, uint32_t* row_ptr, uint32_t* col, int32_t* metric,
+                        uint32_t* link_id, uint8_t* overloaded) {
+  if (!ls) return SPF_E_INVALID;
+  const spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  if (row_ptr) std::copy(ls->row_ptr.begin(), ls->row_ptr.end(), row_ptr);
+  if (col) std::copy(ls->col.begin(), ls->col.end(), col);
+  if (metric) std::copy(ls->metric.begin(), ls->metric.end(), metric);
+  if (link_id) std::copy(ls->link_id.begin(), ls->link_id.end(), link_id);
+  if (overloaded) std::copy(ls->ovl.begin(), ls->ovl.end(), overloaded);
+  return SPF_OK;
+}
+
+spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids) {
+  if (!ls || !name_ids) return SPF_E_INVALID;
+  const spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  std::copy(ls->csr_name.begin(), ls->csr_name.end(), name_ids);
+  return SPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,909 @@
+// ============================================================================
+//  spf_engine.hip -- MI355X (gfx950) all-sources SPF + ECMP engine.
+//
+//  Implements include/openr_spf.h.  What the reference computes per source in
+//  LinkState::runSpf (openr/decision/LinkState.cpp:808-882) is produced here by
+//  two data-parallel passes over a CSR graph resident in HBM:
+//
+//   1. sssp_kernel  -- one workgroup per source row.  Frontier-based
+//      Bellman-Ford (== level-synchronous BFS for unit metrics) with the
+//      distance array and the frontier queue in LDS; the next frontier is a
+//      LDS bitmap compacted with wave ballots/scans.  Writes the distance row
+//      D[row][0..N) to HBM.
+//
+//   2. ecmp_kernel  -- the next-hop pass.  For positive metrics the
+//      reference's next-hop union over the shortest-path DAG equals
+//         x in nh_s(v)  <=>  (x == v  or  x not overloaded)
+//                            and  w(s,x) + d_x(v) == d_s(v)
+//      over the distinct up neighbours x of s (w = min metric over s->x
+//      links).  Proof sketch in DESIGN.md §3.  So the pass is a streaming
+//      compare of D rows: coalesced 16-byte loads, one bit per neighbour,
+//      planar u32 words written once.  Blocks are remapped so that the 32 CUs
+//      of one XCD walk a contiguous source range and share neighbour rows in
+//      their L2.
+//
+//   3. preds_kernel -- pathLinks of one source (tight in-edges of expanded
+//      predecessors, in (dist, node, edge) = Dijkstra pop order).
+//
+//  Everything is integer.  Distances are u32; spf_graph_load rejects graphs
+//  whose longest possible path does not fit (see openr_spf.h).
+// ============================================================================
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "openr_spf.h"
+
+namespace {
+
+constexpr uint32_t kInf = SPF_UNREACHABLE;
+constexpr int kSsspThreads = 256;
+constexpr int kEcmpThreads = 256;
+constexpr int kVecPerThread = 4;  // nodes per thread in the ECMP pass (16 B)
+constexpr uint32_t kBigDeg = 24;  // > kBigDeg: expanded by a whole wave
+constexpr size_t kMaxLds = 160 * 1024;
+
+thread_local std::string g_err;
+
+// ---------------------------------------------------------------------------
+//  device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
+  const uint32_t lane = lane_id();
+  uint32_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  *total = __shfl(inc, 63, 64);
+  return inc - x;
+}
+
+__device__ __forceinline__ bool link_ignored(const uint32_t* ign, uint32_t l) {
+  return (ign[l >> 5] >> (l & 31)) & 1u;
+}
+
+// LDS control words of the SSSP kernel
+enum { C_QLEN = 0, C_NBIG = 1, C_NWORDS = 4 };
+
+// ---------------------------------------------------------------------------
+//  1. single-source shortest paths, one workgroup per source row
+// ---------------------------------------------------------------------------
+template <typename QT, bool UNIT>
+__global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
+    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+    const uint32_t* __restrict__ wt, const uint8_t* __restrict__ ovl,
+    const uint32_t* __restrict__ link, const uint32_t* __restrict__ ign,
+    const uint32_t* __restrict__ rows_src, uint32_t N, uint32_t pitch,
+    uint32_t bm_words, uint32_t big_cap, uint32_t* __restrict__ D) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* dist = reinterpret_cast<uint32_t*>(smem);  // [pitch]
+  uint32_t* bm = dist + pitch;                         // [bm_words] next frontier
+  uint32_t* ctl = bm + bm_words;                       // [C_NWORDS]
+  uint32_t* big = ctl + C_NWORDS;                      // [big_cap]
+  QT* q = reinterpret_cast<QT*>(big + big_cap);        // [N] frontier list
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = tid >> 6;
+  constexpr uint32_t kWaves = kSsspThreads / 64;
+  const uint32_t row = blockIdx.x;
+  const uint32_t src = rows_src[row];
+
+  for (uint32_t v = tid; v < pitch; v += kSsspThreads) dist[v] = kInf;
+  for (uint32_t i = tid; i < bm_words; i += kSsspThreads) bm[i] = 0;
+  if (tid == 0) {
+    ctl[C_QLEN] = 0;
+    ctl[C_NBIG] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    dist[src] = 0;
+    q[0] = (QT)src;
+  }
+  __syncthreads();
+
+  uint32_t qlen = 1;
+  while (qlen != 0) {
+    // ---- expand: small-degree nodes one per thread, big ones per wave ----
+    for (uint32_t i = tid; i < qlen; i += kSsspThreads) {
+      const uint32_t u = q[i];
+      if (ovl[u] && u != src) continue;  // drained node: recorded, not expanded
+      const uint32_t b = row_ptr[u], e = row_ptr[u + 1];
+      if (e - b > kBigDeg) {
+        big[atomicAdd(&ctl[C_NBIG], 1u)] = u;
+        continue;
+      }
+      const uint32_t du = dist[u];
+      for (uint32_t k = b; k < e; ++k) {
+        if (ign && link_ignored(ign, link[k])) continue;  // KSP linksToIgnore
+        const uint32_t v = col[k];
+        const uint32_t nd = du + (UNIT ? 1u : wt[k]);
+        if (UNIT) {
+          // level-synchronous BFS: every writer of v writes the same value
+          if (dist[v] > nd) {
+            dist[v] = nd;
+            atomicOr(&bm[v >> 5], 1u << (v & 31));
+          }
+        } else {
+          if (nd < atomicMin(&dist[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t nbig = ctl[C_NBIG];
+    for (uint32_t i = wave; i < nbig; i += kWaves) {
+      const uint32_t u = big[i];
+      const uint32_t du = dist[u];
+      const uint32_t e = row_ptr[u + 1];
+      for (uint32_t k = row_ptr[u] + lane; k < e; k += 64) {
+        if (ign && link_ignored(ign, link[k])) continue;
+        const uint32_t v = col[k];
+        const uint32_t nd = du + (UNIT ? 1u : wt[k]);
+        if (UNIT) {
+          if (dist[v] > nd) {
+            dist[v] = nd;
+            atomicOr(&bm[v >> 5], 1u << (v & 31));
+          }
+        } else {
+          if (nd < atomicMin(&dist[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) ctl[C_NBIG] = 0;  // every thread has read nbig by now
+
+    // ---- compact the next-frontier bitmap into q (wave ballot/scan) ----
+    for (uint32_t base = 0; base < bm_words; base += kSsspThreads) {
+      const uint32_t i = base + tid;
+      uint32_t word = 0;
+      if (i < bm_words) {
+        word = bm[i];
+        bm[i] = 0;
+      }
+      uint32_t tot;
+      const uint32_t pre = wave_excl_scan(__popc(word), &tot);
+      uint32_t at = 0;
+      if (lane == 0 && tot) at = atomicAdd(&ctl[C_QLEN], tot);
+      at = __shfl(at, 0, 64) + pre;
+      while (word) {
+        const uint32_t b = __ffs(word) - 1;
+        word &= word - 1;
+        q[at++] = (QT)(i * 32 + b);
+      }
+    }
+    __syncthreads();
+    qlen = ctl[C_QLEN];
+    __syncthreads();
+    if (tid == 0) ctl[C_QLEN] = 0;
+  }
+  __syncthreads();
+
+  // ---- write the distance row (16-byte stores) ----
+  uint4* out = reinterpret_cast<uint4*>(D + (size_t)row * pitch);
+  const uint4* in = reinterpret_cast<const uint4*>(dist);
+  for (uint32_t i = tid; i < pitch / 4; i += kSsspThreads) out[i] = in[i];
+}
+
+// ---------------------------------------------------------------------------
+//  2. next-hop (ECMP) pass
+// ---------------------------------------------------------------------------
+// Bijective XCD-aware remap: dispatch deals blocks round-robin over 8 XCDs
+// (b and b+8 share one); give each XCD a contiguous run of virtual blocks so
+// consecutive sources -- which share neighbour rows -- meet in one L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+  const uint32_t xcd = b & 7, pos = b >> 3;
+  const uint32_t q = nb >> 3, r = nb & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+constexpr uint32_t kNbTile = 256;  // neighbours staged in LDS per tile
+
+__global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
+    const uint32_t* __restrict__ D, uint32_t pitch, uint32_t N,
+    const uint32_t* __restrict__ req_src, const uint32_t* __restrict__ row_of,
+    const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
+    const uint32_t* __restrict__ nb_w, const uint8_t* __restrict__ ovl,
+    uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
+    uint32_t chunks, uint32_t n_blocks) {
+  __shared__ uint32_t s_row[kNbTile];  // row index of neighbour, or kInf if overloaded
+  __shared__ uint32_t s_w[kNbTile];
+  __shared__ uint32_t s_id[kNbTile];
+
+  const uint32_t vb = xcd_remap(blockIdx.x, n_blocks);
+  const uint32_t i = vb / chunks;
+  const uint32_t c = vb - i * chunks;
+  const uint32_t s = req_src[i];
+  const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
+  if (k == 0) return;  // isolated source: no next-hop words at all
+  const uint32_t words = (k + 31) >> 5;
+  const uint32_t v0 = (c * kEcmpThreads + threadIdx.x) * kVecPerThread;
+  const bool active = v0 < N;
+
+  uint4 ds = make_uint4(kInf, kInf, kInf, kInf);
+  if (active) ds = *reinterpret_cast<const uint4*>(D + (size_t)row_of[s] * pitch + v0);
+  uint32_t* out = nh + nh_off[i] + v0;
+
+  for (uint32_t t0 = 0; t0 < k; t0 += kNbTile) {
+    const uint32_t tk = min(kNbTile, k - t0);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < tk; j += kEcmpThreads) {
+      const uint32_t x = nb_id[nb0 + t0 + j];
+      s_id[j] = x;
+      s_w[j] = hop ? 1u : nb_w[nb0 + t0 + j];
+      s_row[j] = ovl[x] ? kInf : row_of[x];
+    }
+    __syncthreads();
+    for (uint32_t w0 = 0; w0 < tk; w0 += 32) {
+      uint4 bits = make_uint4(0, 0, 0, 0);
+      const uint32_t wn = min(32u, tk - w0);
+      for (uint32_t jj = 0; jj < wn; ++jj) {
+        const uint32_t j = w0 + jj;
+        const uint32_t wj = s_w[j];
+        const uint32_t rj = s_row[j];
+        uint4 m;
+        if (rj == kInf) {
+          // drained neighbour: only the direct route to itself
+          const uint32_t x = s_id[j];
+          m.x = (v0 + 0 == x) & (ds.x == wj);
+          m.y = (v0 + 1 == x) & (ds.y == wj);
+          m.z = (v0 + 2 == x) & (ds.z == wj);
+          m.w = (v0 + 3 == x) & (ds.w == wj);
+        } else {
+          uint4 dx = make_uint4(kInf, kInf, kInf, kInf);
+          if (active) dx = *reinterpret_cast<const uint4*>(D + (size_t)rj * pitch + v0);
+          m.x = (dx.x != kInf) & (dx.x + wj == ds.x);
+          m.y = (dx.y != kInf) & (dx.y + wj == ds.y);
+          m.z = (dx.z != kInf) & (dx.z + wj == ds.z);
+          m.w = (dx.w != kInf) & (dx.w + wj == ds.w);
+        }
+        bits.x |= m.x << jj;
+        bits.y |= m.y << jj;
+        bits.z |= m.z << jj;
+        bits.w |= m.w << jj;
+      }
+      // unreachable nodes have an empty set (ds == INF never matches)
+      if (active) {
+        const uint32_t wd = (t0 + w0) >> 5;
+        *reinterpret_cast<uint4*>(out + (size_t)wd * pitch) = bits;
+      }
+    }
+  }
+  (void)words;
+}
+
+// ---------------------------------------------------------------------------
+//  copy selected D rows into the caller's dense output (non-direct plans)
+// ---------------------------------------------------------------------------
+__global__ void gather_rows_kernel(const uint32_t* __restrict__ D, uint32_t pitch,
+                                   const uint32_t* __restrict__ rows,
+                                   uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.y;
+  const uint4* in = reinterpret_cast<const uint4*>(D + (size_t)rows[i] * pitch);
+  uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * pitch);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < pitch / 4;
+       t += gridDim.x * blockDim.x)
+    o[t] = in[t];
+}
+
+// ---------------------------------------------------------------------------
+//  3. predecessor lists (pathLinks) of one source
+// ---------------------------------------------------------------------------
+// pass 0: count, pass 1: fill sorted by (dist[u], edge id) -- edge ids of one
+// tail are contiguous in CSR order and tails appear in id (= name) order, so
+// this is the reference's (pop order, linksFromNode order).
+template <int PASS>
+__global__ void preds_kernel(const uint32_t* __restrict__ dist,  // [N]
+                             const uint32_t* __restrict__ row_ptr,
+                             const uint32_t* __restrict__ col,
+                             const uint32_t* __restrict__ wt,
+                             const uint32_t* __restrict__ rev,
+                             const uint8_t* __restrict__ ovl,
+                             const uint32_t* __restrict__ link,
+                             const uint32_t* __restrict__ ign, uint32_t src,
+                             uint32_t N, uint32_t hop,
+                             uint32_t* __restrict__ cnt_or_ptr,
+                             uint32_t* __restrict__ pred_edge) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= N) return;
+  const uint32_t dv = dist[v];
+  uint32_t n = 0;
+  uint32_t base = PASS ? cnt_or_ptr[v] : 0;
+  if (dv != kInf && v != src) {
+    for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e) {
+      const uint32_t u = col[e];
+      const uint32_t r = rev[e];  // the directed edge u -> v
+      if (ovl[u] && u != src) continue;
+      if (ign && link_ignored(ign, link[e])) continue;
+      const uint32_t du = dist[u];
+      if (du == kInf) continue;
+      if (du + (hop ? 1u : wt[r]) != dv) continue;
+      if (PASS) {
+        // insertion into the sorted segment [base, base+n)
+        uint32_t p = base + n;
+        while (p > base) {
+          const uint32_t pe = pred_edge[p - 1];
+          const uint32_t pu = col[rev[pe]];  // tail of edge pe
+          const uint32_t pd = dist[pu];
+          if (pd < du || (pd == du && pe < r)) break;
+          pred_edge[p] = pe;
+          --p;
+        }
+        pred_edge[p] = r;
+      }
+      ++n;
+    }
+  }
+  if (!PASS) cnt_or_ptr[v] = n;
+}
+
+// ---------------------------------------------------------------------------
+//  host side
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    reset();
+    const hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  hipError_t upload(const T* h, size_t count, hipStream_t s) {
+    hipError_t e = alloc(count);
+    if (e != hipSuccess || count == 0) return e;
+    return hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s);
+  }
+};
+
+}  // namespace
+
+struct spf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  uint64_t solves = 0;
+  // graph
+  bool loaded = false;
+  uint32_t N = 0, E = 0, pitch = 0;
+  bool nonpos = false;
+  uint32_t max_metric = 0;
+  std::vector<uint32_t> row_ptr, col, wt, rev, link;
+  std::vector<uint8_t> ovl;
+  std::vector<uint32_t> nb_ptr, nb_id, nb_w;  // distinct up neighbours
+  uint32_t big_nodes = 0;                    // nodes with degree > kBigDeg
+  uint32_t max_link = 0;
+  DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
+  DevBuf<uint8_t> d_ovl;
+  // scratch for spf_preds
+  DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
+};
+
+struct spf_plan {
+  spf_ctx* ctx = nullptr;
+  uint32_t n_src = 0, flags = 0;
+  std::vector<uint32_t> srcs, closure;
+  std::vector<uint64_t> nh_off;
+  std::vector<uint32_t> words;
+  uint64_t nh_total = 0;
+  bool direct = false;  // closure == srcs: D is the caller's dist buffer
+  DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
+  DevBuf<uint64_t> d_nh_off;
+  size_t lds_bytes = 0;
+  bool q16 = true;
+  // optional per-kernel timing: 3 events per execute (before SSSP, between,
+  // after ECMP), ring of `timing_cap` executes
+  std::vector<hipEvent_t> ev;
+  uint32_t timing_cap = 0, timing_n = 0;
+  ~spf_plan() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+spf_status fail(spf_ctx* c, spf_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  g_err = buf;
+  return st;
+}
+
+#define HIP_TRY(ctx, expr)                                                   \
+  do {                                                                       \
+    const hipError_t e_ = (expr);                                            \
+    if (e_ != hipSuccess)                                                    \
+      return fail(ctx, SPF_E_HIP, "%s: %s (%s:%d)", #expr,                   \
+                  hipGetErrorString(e_), __FILE__, __LINE__);                \
+  } while (0)
+
+spf_status set_lds_limits(spf_ctx* c);
+
+size_t sssp_lds_bytes(uint32_t N, uint32_t pitch, uint32_t big, bool q16) {
+  const uint32_t bm_words = (N + 31) / 32;
+  size_t b = 4ull * pitch + 4ull * bm_words + 4ull * C_NWORDS + 4ull * big;
+  b += (q16 ? 2ull : 4ull) * N;
+  return (b + 15) & ~size_t(15);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* spf_global_error(void) { return g_err.c_str(); }
+const char* spf_last_error(const spf_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+uint64_t spf_solves(const spf_ctx* c) { return c ? c->solves : 0; }
+uint32_t spf_row_pitch(const spf_ctx* c) { return c ? c->pitch : 0; }
+int spf_graph_has_nonpositive_metric(const spf_ctx* c) { return c && c->nonpos; }
+
+spf_status spf_ctx_create(int device, spf_ctx** out) {
+  if (!out) return fail(nullptr, SPF_E_INVALID, "spf_ctx_create: out is NULL");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(nullptr, SPF_E_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n)
+    return fail(nullptr, SPF_E_NO_DEVICE, "device %d out of range (%d visible)", device, n);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return fail(nullptr, SPF_E_NO_DEVICE, "hipGetDeviceProperties failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(nullptr, SPF_E_NO_DEVICE, "device %d is %s, engine is built for gfx950",
+                device, prop.gcnArchName);
+  auto c = std::make_unique<spf_ctx>();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess)
+    return fail(nullptr, SPF_E_HIP, "hipSetDevice(%d) failed", device);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(nullptr, SPF_E_HIP, "hipStreamCreate failed");
+  *out = c.release();
+  return SPF_OK;
+}
+
+void spf_ctx_destroy(spf_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
+  if (!c || !g) return fail(c, SPF_E_INVALID, "spf_graph_load: NULL argument");
+  const uint32_t N = g->n_nodes, E = g->n_edges;
+  if (N == 0) return fail(c, SPF_E_INVALID, "graph has no nodes");
+  if (!g->row_ptr || (E && (!g->col || !g->metric || !g->link_id)) || !g->overloaded)
+    return fail(c, SPF_E_INVALID, "graph arrays missing");
+  if (g->row_ptr[0] != 0 || g->row_ptr[N] != E)
+    return fail(c, SPF_E_INVALID, "row_ptr must start at 0 and end at n_edges");
+  c->loaded = false;
+  c->N = N;
+  c->E = E;
+  c->pitch = (N + 3) & ~3u;
+  c->row_ptr.assign(g->row_ptr, g->row_ptr + N + 1);
+  c->col.assign(g->col, g->col + E);
+  c->link.assign(g->link_id, g->link_id + E);
+  c->ovl.assign(g->overloaded, g->overloaded + N);
+  c->wt.resize(E);
+  c->nonpos = false;
+  c->max_metric = 0;
+  for (uint32_t u = 0; u < N; ++u) {
+    if (c->row_ptr[u] > c->row_ptr[u + 1])
+      return fail(c, SPF_E_INVALID, "row_ptr not monotone at %u", u);
+  }
+  for (uint32_t e = 0; e < E; ++e) {
+    if (c->col[e] >= N) return fail(c, SPF_E_INVALID, "edge %u head %u out of range", e, c->col[e]);
+    const int32_t m = g->metric[e];
+    if (m <= 0) c->nonpos = true;
+    c->wt[e] = m > 0 ? (uint32_t)m : 0u;
+    c->max_metric = std::max(c->max_metric, c->wt[e]);
+  }
+  if ((uint64_t)c->max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf)
+    return fail(c, SPF_E_UNSUPPORTED,
+                "max metric %u x %u hops overflows 32-bit distances", c->max_metric, N - 1);
+  // reverse edge of every directed edge (same link id, swapped ends)
+  c->rev.assign(E, kInf);
+  {
+    std::vector<uint32_t> first(0);
+    uint32_t max_link = 0;
+    for (uint32_t e = 0; e < E; ++e) max_link = std::max(max_link, c->link[e]);
+    std::vector<uint32_t> seen((size_t)max_link + 1, kInf);
+    for (uint32_t u = 0; u < N; ++u)
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+        uint32_t& s = seen[c->link[e]];
+        if (s == kInf) {
+          s = e;
+        } else {
+          c->rev[e] = s;
+          c->rev[s] = e;
+        }
+      }
+    for (uint32_t e = 0; e < E; ++e)
+      if (c->rev[e] == kInf)
+        return fail(c, SPF_E_INVALID, "edge %u (link %u) has no reverse edge", e, c->link[e]);
+  }
+  // distinct up neighbours per node, ascending id, min metric
+  c->nb_ptr.assign(N + 1, 0);
+  c->nb_id.clear();
+  c->nb_w.clear();
+  c->big_nodes = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> tmp;
+  for (uint32_t u = 0; u < N; ++u) {
+    tmp.clear();
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) tmp.emplace_back(c->col[e], c->wt[e]);
+    if (c->row_ptr[u + 1] - c->row_ptr[u] > kBigDeg) ++c->big_nodes;
+    std::sort(tmp.begin(), tmp.end());
+    for (size_t i = 0; i < tmp.size(); ++i) {
+      if (i && tmp[i].first == tmp[i - 1].first) continue;  // first = min metric
+      c->nb_id.push_back(tmp[i].first);
+      c->nb_w.push_back(tmp[i].second);
+    }
+    c->nb_ptr[u + 1] = (uint32_t)c->nb_id.size();
+  }
+  if (sssp_lds_bytes(N, c->pitch, c->big_nodes, N <= 65535) > kMaxLds)
+    return fail(c, SPF_E_UNSUPPORTED,
+                "graph with %u nodes exceeds the LDS-resident SSSP kernel (max ~20k nodes)", N);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, c->d_row_ptr.upload(c->row_ptr.data(), N + 1, c->stream));
+  HIP_TRY(c, c->d_col.upload(c->col.data(), E, c->stream));
+  HIP_TRY(c, c->d_wt.upload(c->wt.data(), E, c->stream));
+  HIP_TRY(c, c->d_rev.upload(c->rev.data(), E, c->stream));
+  HIP_TRY(c, c->d_link.upload(c->link.data(), E, c->stream));
+  c->max_link = 0;
+  for (uint32_t e = 0; e < E; ++e) c->max_link = std::max(c->max_link, c->link[e]);
+  HIP_TRY(c, c->d_ovl.upload(c->ovl.data(), N, c->stream));
+  HIP_TRY(c, c->d_nb_ptr.upload(c->nb_ptr.data(), N + 1, c->stream));
+  HIP_TRY(c, c->d_nb_id.upload(c->nb_id.data(), c->nb_id.size(), c->stream));
+  HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->loaded = true;
+  return SPF_OK;
+}
+
+spf_status spf_src_neighbors(const spf_ctx* c, uint32_t src, uint32_t* out,
+                             uint32_t cap, uint32_t* count) {
+  if (!c || !c->loaded) return SPF_E_STATE;
+  if (src >= c->N) return SPF_E_INVALID;
+  const uint32_t b = c->nb_ptr[src], k = c->nb_ptr[src + 1] - b;
+  if (count) *count = k;
+  for (uint32_t i = 0; i < k && i < cap && out; ++i) out[i] = c->nb_id[b + i];
+  return SPF_OK;
+}
+
+spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
+                           uint32_t flags, spf_plan** out) {
+  if (!c || !out) return fail(c, SPF_E_INVALID, "spf_plan_create: NULL argument");
+  *out = nullptr;
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (n_src == 0 || !srcs) return fail(c, SPF_E_INVALID, "empty source list");
+  const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
+  if (!hop && c->nonpos)
+    return fail(c, SPF_E_UNSUPPORTED,
+                "graph has up links with metric <= 0; weighted SPF over zero/negative "
+                "metrics is outside the exact-parity envelope");
+  const uint32_t N = c->N;
+  auto p = std::make_unique<spf_plan>();
+  p->ctx = c;
+  p->n_src = n_src;
+  p->flags = flags;
+  p->srcs.assign(srcs, srcs + n_src);
+  std::vector<uint32_t> row_of(N, kInf);
+  bool distinct = true;
+  for (uint32_t i = 0; i < n_src; ++i) {
+    if (srcs[i] >= N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
+    if (row_of[srcs[i]] != kInf) distinct = false;
+    else row_of[srcs[i]] = i;
+  }
+  // closure: every non-overloaded neighbour's distance row is needed
+  bool closed = distinct;
+  if (closed) {
+    for (uint32_t i = 0; i < n_src && closed; ++i) {
+      const uint32_t s = srcs[i];
+      for (uint32_t j = c->nb_ptr[s]; j < c->nb_ptr[s + 1]; ++j) {
+        const uint32_t x = c->nb_id[j];
+        if (!c->ovl[x] && row_of[x] == kInf) {
+          closed = false;
+          break;
+        }
+      }
+    }
+  }
+  p->direct = closed;
+  if (closed) {
+    p->closure = p->srcs;
+  } else {
+    std::fill(row_of.begin(), row_of.end(), kInf);
+    auto add = [&](uint32_t x) {
+      if (row_of[x] == kInf) {
+        row_of[x] = (uint32_t)p->closure.size();
+        p->closure.push_back(x);
+      }
+    };
+    for (uint32_t i = 0; i < n_src; ++i) {
+      const uint32_t s = srcs[i];
+      add(s);
+      for (uint32_t j = c->nb_ptr[s]; j < c->nb_ptr[s + 1]; ++j)
+        if (!c->ovl[c->nb_id[j]]) add(c->nb_id[j]);
+    }
+  }
+  std::vector<uint32_t> req_rows(n_src);
+  for (uint32_t i = 0; i < n_src; ++i) req_rows[i] = row_of[srcs[i]];
+  // next-hop layout
+  p->nh_off.resize(n_src);
+  p->words.resize(n_src);
+  uint64_t off = 0;
+  for (uint32_t i = 0; i < n_src; ++i) {
+    const uint32_t k = c->nb_ptr[srcs[i] + 1] - c->nb_ptr[srcs[i]];
+    p->words[i] = (k + 31) / 32;
+    p->nh_off[i] = off;
+    off += (uint64_t)p->words[i] * c->pitch;
+  }
+  p->nh_total = off;
+  p->q16 = N <= 65535;
+  p->lds_bytes = sssp_lds_bytes(N, c->pitch, c->big_nodes, p->q16);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
+  HIP_TRY(c, p->d_closure.upload(p->closure.data(), p->closure.size(), c->stream));
+  HIP_TRY(c, p->d_row_of.upload(row_of.data(), N, c->stream));
+  HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
+  HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
+  if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
+  {
+    const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
+    if (st != SPF_OK) return st;
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  *out = p.release();
+  return SPF_OK;
+}
+
+void spf_plan_destroy(spf_plan* p) { delete p; }
+uint64_t spf_plan_nh_words(const spf_plan* p) { return p ? p->nh_total : 0; }
+uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->closure.size() : 0; }
+
+spf_status spf_plan_nh_layout(const spf_plan* p, uint64_t* nh_off, uint32_t* words) {
+  if (!p) return SPF_E_INVALID;
+  for (uint32_t i = 0; i < p->n_src; ++i) {
+    if (nh_off) nh_off[i] = p->nh_off[i];
+    if (words) words[i] = p->words[i];
+  }
+  return SPF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Launch the SSSP kernel over `rows` closure rows (device list rows_src).
+spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
+                       const uint32_t* ign, uint32_t* D, hipStream_t s) {
+  const uint32_t N = c->N, pitch = c->pitch, bm_words = (N + 31) / 32;
+  const bool q16 = N <= 65535;
+  const size_t lds = sssp_lds_bytes(N, pitch, c->big_nodes, q16);
+  const bool unit = hop || c->max_metric == 1;
+  const dim3 g(rows), b(kSsspThreads);
+#define SSSP_LAUNCH(QT, U)                                                                \
+  hipLaunchKernelGGL((sssp_kernel<QT, U>), g, b, lds, s, c->d_row_ptr.p, c->d_col.p,       \
+                     c->d_wt.p, c->d_ovl.p, c->d_link.p, ign, rows_src, N, pitch, bm_words, \
+                     c->big_nodes, D)
+  if (q16) {
+    if (unit) SSSP_LAUNCH(uint16_t, true);
+    else SSSP_LAUNCH(uint16_t, false);
+  } else {
+    if (unit) SSSP_LAUNCH(uint32_t, true);
+    else SSSP_LAUNCH(uint32_t, false);
+  }
+#undef SSSP_LAUNCH
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
+spf_status set_lds_limits(spf_ctx* c) {
+  static bool done = false;
+  if (done) return SPF_OK;
+  const void* fns[] = {(const void*)sssp_kernel<uint16_t, true>, (const void*)sssp_kernel<uint16_t, false>,
+                       (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>};
+  for (const void* f : fns)
+    HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+  done = true;
+  return SPF_OK;
+}
+
+// Upload an ignore set (undirected link ids) as a device bitmap; NULL if empty.
+spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
+                         const uint32_t** dev) {
+  *dev = nullptr;
+  if (!ignore || n_ignore == 0) return SPF_OK;
+  std::vector<uint32_t> bm(c->max_link / 32 + 1, 0);
+  for (uint32_t i = 0; i < n_ignore; ++i)
+    if (ignore[i] <= c->max_link) bm[ignore[i] >> 5] |= 1u << (ignore[i] & 31);
+  HIP_TRY(c, c->d_ign.upload(bm.data(), bm.size(), c->stream));
+  *dev = c->d_ign.p;
+  return SPF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void* stream) {
+  if (!p) return fail(nullptr, SPF_E_INVALID, "spf_plan_execute: NULL plan");
+  spf_ctx* c = p->ctx;
+  if (!c->loaded) return fail(c, SPF_E_STATE, "graph no longer loaded");
+  if (!d_dist || (p->nh_total && !d_nh))
+    return fail(c, SPF_E_INVALID, "spf_plan_execute: NULL output buffer");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const uint32_t N = c->N, pitch = c->pitch;
+  const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
+  uint32_t* D = p->direct ? d_dist : p->d_D.p;
+  const uint32_t rows = (uint32_t)p->closure.size();
+  hipEvent_t* ev = nullptr;
+  if (p->timing_cap) {
+    ev = &p->ev[3 * (p->timing_n % p->timing_cap)];
+    ++p->timing_n;
+    HIP_TRY(c, hipEventRecord(ev[0], s));
+  }
+  spf_status st = launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
+  if (st != SPF_OK) return st;
+  if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
+  if (p->nh_total) {
+    const uint32_t chunks = (N + kEcmpThreads * kVecPerThread - 1) / (kEcmpThreads * kVecPerThread);
+    const uint32_t nb = chunks * p->n_src;
+    hipLaunchKernelGGL(ecmp_kernel, dim3(nb), dim3(kEcmpThreads), 0, s, D, pitch, N, p->d_srcs.p,
+                       p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, c->d_ovl.p,
+                       hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, nb);
+    HIP_TRY(c, hipGetLastError());
+  }
+  if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+  if (!p->direct) {
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(std::min<uint32_t>((pitch / 4 + 255) / 256, 64), p->n_src),
+                       dim3(256), 0, s, D, pitch, p->d_req_rows.p, d_dist);
+    HIP_TRY(c, hipGetLastError());
+  }
+  c->solves += p->n_src;
+  return SPF_OK;
+}
+
+spf_status spf_plan_enable_timing(spf_plan* p, uint32_t max_executes) {
+  if (!p) return SPF_E_INVALID;
+  spf_ctx* c = p->ctx;
+  for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  p->ev.assign(3ull * max_executes, nullptr);
+  for (auto& e : p->ev) HIP_TRY(c, hipEventCreate(&e));
+  p->timing_cap = max_executes;
+  p->timing_n = 0;
+  return SPF_OK;
+}
+
+spf_status spf_plan_timing(spf_plan* p, double* sssp_ms, double* ecmp_ms, uint32_t* n) {
+  if (!p || !p->timing_cap) return SPF_E_STATE;
+  spf_ctx* c = p->ctx;
+  const uint32_t cnt = std::min(p->timing_n, p->timing_cap);
+  double a = 0, b = 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    float t0 = 0, t1 = 0;
+    HIP_TRY(c, hipEventSynchronize(p->ev[3 * i + 2]));
+    HIP_TRY(c, hipEventElapsedTime(&t0, p->ev[3 * i], p->ev[3 * i + 1]));
+    HIP_TRY(c, hipEventElapsedTime(&t1, p->ev[3 * i + 1], p->ev[3 * i + 2]));
+    a += t0;
+    b += t1;
+  }
+  if (sssp_ms) *sssp_ms = a;
+  if (ecmp_ms) *ecmp_ms = b;
+  if (n) *n = cnt;
+  p->timing_n = 0;
+  return SPF_OK;
+}
+
+spf_status spf_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
+                     uint32_t* dist_out, uint32_t* nh_out) {
+  spf_plan* raw = nullptr;
+  spf_status st = spf_plan_create(c, srcs, n_src, flags, &raw);
+  if (st != SPF_OK) return st;
+  std::unique_ptr<spf_plan> p(raw);
+  DevBuf<uint32_t> d_dist, d_nh;
+  HIP_TRY(c, d_dist.alloc((size_t)n_src * c->pitch));
+  HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(p->nh_total, 1)));
+  st = spf_plan_execute(p.get(), d_dist.p, d_nh.p, nullptr);
+  if (st != SPF_OK) return st;
+  if (dist_out) {
+    HIP_TRY(c, hipMemcpy2DAsync(dist_out, (size_t)c->N * 4, d_dist.p, (size_t)c->pitch * 4,
+                                (size_t)c->N * 4, n_src, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (nh_out && p->nh_total) {
+    HIP_TRY(c, hipMemcpyAsync(nh_out, d_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SPF_OK;
+}
+
+spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ignore_links,
+                    uint32_t n_ignore, uint32_t* dist_out) {
+  if (!c || !dist_out) return fail(c, SPF_E_INVALID, "spf_sssp: NULL argument");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
+  const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
+  if (!hop && c->nonpos)
+    return fail(c, SPF_E_UNSUPPORTED, "graph has up links with metric <= 0");
+  spf_status st = set_lds_limits(c);
+  if (st != SPF_OK) return st;
+  const uint32_t* ign = nullptr;
+  st = upload_ignore(c, ignore_links, n_ignore, &ign);
+  if (st != SPF_OK) return st;
+  HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
+  HIP_TRY(c, c->d_row.alloc(c->pitch));
+  st = launch_sssp(c, c->d_one_src.p, 1, hop, ign, c->d_row.p, c->stream);
+  if (st != SPF_OK) return st;
+  HIP_TRY(c, hipMemcpyAsync(dist_out, c->d_row.p, 4ull * c->N, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->solves += 1;
+  return SPF_OK;
+}
+
+spf_status spf_preds(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ignore_links,
+                     uint32_t n_ignore, const uint32_t* dist, uint32_t* pred_ptr,
+                     uint32_t* pred_edge, uint32_t cap, uint32_t* n_preds) {
+  if (!c || !dist || !pred_ptr || !n_preds) return fail(c, SPF_E_INVALID, "spf_preds: NULL argument");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
+  const uint32_t N = c->N;
+  const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
+  const uint32_t* ign = nullptr;
+  spf_status st = upload_ignore(c, ignore_links, n_ignore, &ign);
+  if (st != SPF_OK) return st;
+  HIP_TRY(c, c->d_row.upload(dist, N, c->stream));
+  HIP_TRY(c, c->d_pred_cnt.alloc(N + 1));
+  const dim3 g((N + 255) / 256), b(256);
+  hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, c->d_row.p, c->d_row_ptr.p, c->d_col.p,
+                     c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign, src, N, hop ? 1u : 0u,
+                     c->d_pred_cnt.p, (uint32_t*)nullptr);
+  HIP_TRY(c, hipGetLastError());
+  std::vector<uint32_t> cnt(N);
+  HIP_TRY(c, hipMemcpyAsync(cnt.data(), c->d_pred_cnt.p, 4ull * N, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  pred_ptr[0] = 0;
+  for (uint32_t v = 0; v < N; ++v) pred_ptr[v + 1] = pred_ptr[v] + cnt[v];
+  *n_preds = pred_ptr[N];
+  if (!pred_edge) return SPF_OK;
+  if (cap < pred_ptr[N]) return fail(c, SPF_E_INVALID, "pred_edge capacity %u < %u", cap, pred_ptr[N]);
+  HIP_TRY(c, hipMemcpyAsync(c->d_pred_cnt.p, pred_ptr, 4ull * N, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, c->d_pred_edge.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
+  hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, c->d_row.p, c->d_row_ptr.p, c->d_col.p,
+                     c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign, src, N, hop ? 1u : 0u,
+                     c->d_pred_cnt.p, c->d_pred_edge.p);
+  HIP_TRY(c, hipGetLastError());
+  if (pred_ptr[N])
+    HIP_TRY(c, hipMemcpyAsync(pred_edge, c->d_pred_edge.p, 4ull * pred_ptr[N], hipMemcpyDeviceToHost,
+                              c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+"""Batched all-sources SPF on device buffers (include/openr_spf.h).
+
+This is the path ``SpfSolver`` takes when it needs many sources at once
+(all-sources route builds, ``breeze decision routes --nodes all`` =
+``Decision::getDecisionRouteDb`` per node, Decision.cpp:1480-1500; LFA's
+SPF-from-every-neighbour, Decision.cpp:1158-1192).  One ``SpfPlan`` fixes the
+source batch; ``execute`` enqueues the kernels on a HIP stream without host
+synchronisation, so it can be timed with HIP events or captured in a graph.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+HOP_COUNT = N.SPF_FLAG_HOP_COUNT
+UNREACHABLE = N.SPF_UNREACHABLE
+
+
+@dataclass
+class SolveResult:
+    dist: np.ndarray  # [n_src, n_nodes] uint32 (UNREACHABLE)
+    nh: np.ndarray  # planar next-hop words (see nh_bits)
+    nh_off: np.ndarray  # [n_src] uint64 word offset of each source
+    words: np.ndarray  # [n_src] words per node (= ceil(#neighbours / 32))
+    pitch: int
+
+    def nh_bits(self, i: int) -> np.ndarray:
+        """[n_nodes, words_i] next-hop words of source i."""
+        w = int(self.words[i])
+        n = self.dist.shape[1]
+        o = int(self.nh_off[i])
+        return self.nh[o: o + w * self.pitch].reshape(w, self.pitch)[:, :n].T.copy()
+
+
+class SpfPlan:
+    def __init__(self, eng: "SpfEngine", srcs: Sequence[int], flags: int) -> None:
+        self._eng = eng
+        self.srcs = np.ascontiguousarray(srcs, np.uint32)
+        self.flags = flags
+        h = C.c_void_p()
+        eng._err(N.lib.spf_plan_create(eng._h, N.ptr(self.srcs), len(self.srcs), flags,
+                                       C.byref(h)))
+        self._h = h
+        self.nh_words = int(N.lib.spf_plan_nh_words(h))
+        self.closure_rows = int(N.lib.spf_plan_closure_rows(h))
+        self.nh_off = np.zeros(len(self.srcs), np.uint64)
+        self.words = np.zeros(len(self.srcs), np.uint32)
+        N.lib.spf_plan_nh_layout(h, N.ptr(self.nh_off, C.c_uint64), N.ptr(self.words))
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            N.lib.spf_plan_destroy(h)
+            self._h = C.c_void_p()
+
+    @property
+    def n_src(self) -> int:
+        return len(self.srcs)
+
+    def execute(self, d_dist: int, d_nh: int, stream: int = 0) -> None:
+        """Enqueue on `stream` (raw hipStream_t as int; 0 = engine stream)."""
+        self._eng._err(N.lib.spf_plan_execute(self._h, C.c_void_p(d_dist), C.c_void_p(d_nh),
+                                              C.c_void_p(stream) if stream else None))
+
+    def enable_timing(self, max_executes: int) -> None:
+        self._eng._err(N.lib.spf_plan_enable_timing(self._h, max_executes))
+
+    def timing(self) -> Tuple[float, float, int]:
+        """(summed SSSP ms, summed ECMP ms, executes) since enable/last call."""
+        a, b, n = C.c_double(), C.c_double(), C.c_uint32()
+        self._eng._err(N.lib.spf_plan_timing(self._h, C.byref(a), C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
+
+    def execute_torch(self, dist, nh, stream=None) -> None:
+        """dist: int32/uint32 tensor [n_src, pitch] on the engine's device;
+        nh: tensor with >= nh_words 32-bit words; stream: torch.cuda.Stream."""
+        import torch
+
+        assert dist.is_cuda and dist.numel() >= self.n_src * self._eng.pitch
+        assert nh.is_cuda and nh.numel() >= max(1, self.nh_words)
+        s = (stream or torch.cuda.current_stream(dist.device)).cuda_stream
+        self.execute(dist.data_ptr(), nh.data_ptr(), s)
+
+
+class SpfEngine:
+    """An engine context with one graph loaded (``spf_ctx``)."""
+
+    def __init__(self, device: int = 0, handle: Optional[C.c_void_p] = None) -> None:
+        self._owned = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            st = N.lib.spf_ctx_create(device, C.byref(h))
+            N.raise_for(st, N.global_error())
+            self._h = h
+        else:
+            self._h = handle
+        self._graph = None
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if getattr(self, "_owned", False) and h is not None and h.value:
+            N.lib.spf_ctx_destroy(h)
+            self._h = C.c_void_p()
+
+    def _err(self, st: int) -> None:
+        N.raise_for(st, (N.lib.spf_last_error(self._h) or b"").decode())
+
+    # ---- graph -----------------------------------------------------------------
+    def load(self, row_ptr, col, metric, link_id, overloaded) -> None:
+        arrs = (np.ascontiguousarray(row_ptr, np.uint32), np.ascontiguousarray(col, np.uint32),
+                np.ascontiguousarray(metric, np.int32), np.ascontiguousarray(link_id, np.uint32),
+                np.ascontiguousarray(overloaded, np.uint8))
+        g = N.SpfGraph()
+        g.n_nodes = len(arrs[0]) - 1
+        g.n_edges = len(arrs[1])
+        g.row_ptr = N.ptr(arrs[0])
+        g.col = N.ptr(arrs[1])
+        g.metric = N.ptr(arrs[2], C.c_int32)
+        g.link_id = N.ptr(arrs[3])
+        g.overloaded = N.ptr(arrs[4], C.c_uint8)
+        self._err(N.lib.spf_graph_load(self._h, C.byref(g)))
+        self._graph = arrs
+
+    @property
+    def pitch(self) -> int:
+        return int(N.lib.spf_row_pitch(self._h))
+
+    @property
+    def n_nodes(self) -> int:
+        return len(self._graph[0]) - 1 if self._graph is not None else 0
+
+    def neighbors(self, src: int) -> np.ndarray:
+        cnt = C.c_uint32()
+        self._err(N.lib.spf_src_neighbors(self._h, src, None, 0, C.byref(cnt)))
+        out = np.zeros(max(1, cnt.value), np.uint32)
+        self._err(N.lib.spf_src_neighbors(self._h, src, N.ptr(out), cnt.value, C.byref(cnt)))
+        return out[: cnt.value]
+
+    def solves(self) -> int:
+        return int(N.lib.spf_solves(self._h))
+
+    # ---- solves -----------------------------------------------------------------
+    def plan(self, srcs: Sequence[int], hop: bool = False) -> SpfPlan:
+        return SpfPlan(self, srcs, HOP_COUNT if hop else 0)
+
+    def solve(self, srcs: Sequence[int], hop: bool = False) -> SolveResult:
+        p = self.plan(srcs, hop)
+        n = self.n_nodes
+        dist = np.zeros((p.n_src, n), np.uint32)
+        nh = np.zeros(max(1, p.nh_words), np.uint32)
+        self._err(N.lib.spf_solve(self._h, N.ptr(p.srcs), p.n_src, p.flags, N.ptr(dist),
+                                  N.ptr(nh)))
+        return SolveResult(dist, nh, p.nh_off, p.words, self.pitch)
+
+    def sssp(self, src: int, hop: bool = False,
+             ignore_links: Optional[Sequence[int]] = None) -> np.ndarray:
+        ign = np.ascontiguousarray(ignore_links if ignore_links is not None else [], np.uint32)
+        out = np.zeros(self.n_nodes, np.uint32)
+        self._err(N.lib.spf_sssp(self._h, src, HOP_COUNT if hop else 0,
+                                 N.ptr(ign) if len(ign) else None, len(ign), N.ptr(out)))
+        return out
+
+    def preds(self, src: int, dist: np.ndarray, hop: bool = False,
+              ignore_links: Optional[Sequence[int]] = None) -> Tuple[np.ndarray, np.ndarray]:
+        ign = np.ascontiguousarray(ignore_links if ignore_links is not None else [], np.uint32)
+        dist = np.ascontiguousarray(dist, np.uint32)
+        ptr_ = np.zeros(self.n_nodes + 1, np.uint32)
+        cnt = C.c_uint32()
+        args = (self._h, src, HOP_COUNT if hop else 0, N.ptr(ign) if len(ign) else None, len(ign),
+                N.ptr(dist), N.ptr(ptr_))
+        self._err(N.lib.spf_preds(*args, None, 0, C.byref(cnt)))
+        edges = np.zeros(max(1, cnt.value), np.uint32)
+        self._err(N.lib.spf_preds(*args, N.ptr(edges), cnt.value, C.byref(cnt)))
+        return ptr_, edges[: cnt.value]
+
+
+def graph_from_lsdb(lsdb, area: str = "0"):
+    """Flatten a packed LSDB with the LinkState facade (host side only).
+    Returns (node_names, row_ptr, col, metric, link_id, overloaded)."""
+    from .link_state import LinkState
+
+    ls = LinkState(area, device=-1)
+    ls.updateAdjacencyDatabases(lsdb)
+    return ls.flatten()

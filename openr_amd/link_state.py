@@ -1,0 +1,357 @@
+"""LinkState drop-in: the reference's ``openr::LinkState`` API over the MI355X engine.
+
+Python mirror of ``openr/decision/LinkState.h:82-469`` (same method names,
+argument meaning and error behaviour) backed by the C-ABI facade
+``include/openr_linkstate.h``: LSDB bookkeeping on the host, every shortest
+path batch on the GPU.  Parity tests drive this class exactly like the
+reference's ``LinkStateTest.cpp`` / ``DecisionTest.cpp`` drive the C++ one.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple, Union
+
+from . import _native as N
+from .lsdb import K_DEFAULT_AREA, AdjacencyDatabase, PackedLsdb, pack
+
+LinkStateMetric = int
+
+
+@dataclass(frozen=True)
+class LinkStateChange:
+    """``LinkState::LinkStateChange`` (LinkState.h:306-325)."""
+
+    topologyChanged: bool = False
+    linkAttributesChanged: bool = False
+    nodeLabelChanged: bool = False
+
+
+class Link:
+    """Snapshot of ``openr::Link`` (LinkState.h:82-175) taken at query time."""
+
+    __slots__ = ("_n1", "_n2", "_if1", "_if2", "_m1", "_m2", "_l1", "_l2",
+                 "_o1", "_o2", "_up", "hash", "_key", "_area", "_v4", "_v6")
+
+    def __init__(self, ls: "LinkState", d: N.LsLinkDesc) -> None:
+        name = ls._name
+        self._n1, self._n2 = name(d.node1), name(d.node2)
+        self._if1, self._if2 = d.if1.decode(), d.if2.decode()
+        self._m1, self._m2 = int(d.metric1), int(d.metric2)
+        self._l1, self._l2 = int(d.adj_label1), int(d.adj_label2)
+        self._o1, self._o2 = bool(d.overload1), bool(d.overload2)
+        self._up = bool(d.is_up)
+        self.hash = int(d.hash)
+        self._key = tuple(sorted([(self._n1, self._if1), (self._n2, self._if2)]))
+        self._area = ls.getArea()
+        self._v4 = (bytes(d.nh_v4_1[:4]), bytes(d.nh_v4_2[:4]))
+        self._v6 = (bytes(d.nh_v6_1[:16]), bytes(d.nh_v6_2[:16]))
+
+    def _side(self, node: str) -> int:
+        if node == self._n1:
+            return 0
+        if node == self._n2:
+            return 1
+        raise ValueError(node)  # std::invalid_argument in the reference
+
+    def getArea(self) -> str:
+        return self._area
+
+    def getOtherNodeName(self, node: str) -> str:
+        return self._n2 if self._side(node) == 0 else self._n1
+
+    def firstNodeName(self) -> str:
+        return self._key[0][0]
+
+    def secondNodeName(self) -> str:
+        return self._key[1][0]
+
+    def getIfaceFromNode(self, node: str) -> str:
+        return (self._if1, self._if2)[self._side(node)]
+
+    def getMetricFromNode(self, node: str) -> int:
+        return (self._m1, self._m2)[self._side(node)]
+
+    def getAdjLabelFromNode(self, node: str) -> int:
+        return (self._l1, self._l2)[self._side(node)]
+
+    def getOverloadFromNode(self, node: str) -> bool:
+        return (self._o1, self._o2)[self._side(node)]
+
+    def getNhV4FromNode(self, node: str) -> bytes:
+        return self._v4[self._side(node)]
+
+    def getNhV6FromNode(self, node: str) -> bytes:
+        return self._v6[self._side(node)]
+
+    def isUp(self) -> bool:
+        return self._up
+
+    @property
+    def orderedNames(self) -> Tuple[Tuple[str, str], Tuple[str, str]]:
+        return self._key  # type: ignore[return-value]
+
+    def __eq__(self, other: object) -> bool:
+        return isinstance(other, Link) and self.hash == other.hash and self._key == other._key
+
+    def __lt__(self, other: "Link") -> bool:  # Link::operator< (LinkState.cpp:347-353)
+        if self.hash != other.hash:
+            return self.hash < other.hash
+        return self._key < other._key
+
+    def __hash__(self) -> int:
+        return self.hash
+
+    def toString(self) -> str:
+        return f"{self._area} - {self._n1}%{self._if1} <---> {self._n2}%{self._if2}"
+
+    def directionalToString(self, fromNode: str) -> str:
+        other = self.getOtherNodeName(fromNode)
+        return (f"{self._area} - {fromNode}%{self.getIfaceFromNode(fromNode)} ---> "
+                f"{other}%{self.getIfaceFromNode(other)}")
+
+    def __repr__(self) -> str:
+        return f"Link({self.toString()})"
+
+
+@dataclass(frozen=True)
+class PathLink:
+    """``NodeSpfResult::PathLink`` (LinkState.h:207-213)."""
+
+    link: Link
+    prevNode: str
+
+
+class NodeSpfResult:
+    """``LinkState::NodeSpfResult`` (LinkState.h:203-257)."""
+
+    __slots__ = ("_metric", "_nh", "_pl")
+
+    def __init__(self, metric: int, nh: Set[str], pl: List[PathLink]) -> None:
+        self._metric, self._nh, self._pl = metric, nh, pl
+
+    def metric(self) -> int:
+        return self._metric
+
+    def nextHops(self) -> Set[str]:
+        return self._nh
+
+    def pathLinks(self) -> List[PathLink]:
+        return self._pl
+
+    def __repr__(self) -> str:
+        return f"NodeSpfResult(metric={self._metric}, nextHops={sorted(self._nh)})"
+
+
+SpfResult = Dict[str, NodeSpfResult]
+Path = List[Link]
+
+
+def _change(c: N.LsChange) -> LinkStateChange:
+    return LinkStateChange(bool(c.topology_changed), bool(c.link_attributes_changed),
+                           bool(c.node_label_changed))
+
+
+class LinkState:
+    """``openr::LinkState`` (LinkState.h:177-469) on the MI355X engine.
+
+    ``device`` selects the GPU; ``device=-1`` builds a host-only state (LSDB
+    bookkeeping and graph flatten, no shortest-path queries).
+    """
+
+    def __init__(self, area: str = K_DEFAULT_AREA, device: int = 0) -> None:
+        h = C.c_void_p()
+        st = N.lib.ls_create(area.encode(), device, C.byref(h))
+        N.raise_for(st, N.global_error())
+        self._h = h
+        self._area = area
+        self._names: List[Optional[str]] = []
+        self._gen = 0
+        self._spf_cache: Dict[Tuple[str, bool], SpfResult] = {}
+        self._ksp_cache: Dict[Tuple[str, str, int], List[Path]] = {}
+        self._link_cache: Dict[int, Link] = {}
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            N.lib.ls_destroy(h)
+            self._h = C.c_void_p()
+
+    # -- helpers ---------------------------------------------------------------
+    def _err(self, st: int) -> None:
+        N.raise_for(st, (N.lib.ls_last_error(self._h) or b"").decode())
+
+    def _name(self, i: int) -> str:
+        while i >= len(self._names):
+            self._names.append(None)
+        s = self._names[i]
+        if s is None:
+            s = N.lib.ls_name(self._h, i).decode()
+            self._names[i] = s
+        return s
+
+    def _topology(self, changes: Iterable[LinkStateChange]) -> None:
+        if any(c.topologyChanged for c in changes):
+            self._gen += 1
+            self._spf_cache.clear()
+            self._ksp_cache.clear()
+            self._link_cache.clear()
+
+    def _link(self, link_id: int) -> Link:
+        lk = self._link_cache.get(link_id)
+        if lk is None:
+            d = N.LsLinkDesc()
+            self._err(N.lib.ls_link_info(self._h, link_id, C.byref(d)))
+            lk = Link(self, d)
+            self._link_cache[link_id] = lk
+        return lk
+
+    # -- mutators (LinkState.h:327-337) -----------------------------------------
+    def updateAdjacencyDatabase(self, adjacencyDb: AdjacencyDatabase, holdUpTtl: int = 0,
+                                holdDownTtl: int = 0) -> LinkStateChange:
+        return self.updateAdjacencyDatabases([adjacencyDb], holdUpTtl, holdDownTtl)[0]
+
+    def updateAdjacencyDatabases(self, dbs: Union[PackedLsdb, Sequence[AdjacencyDatabase]],
+                                 holdUpTtl: int = 0, holdDownTtl: int = 0
+                                 ) -> List[LinkStateChange]:
+        """Apply databases in order (one updateAdjacencyDatabase each)."""
+        packed = dbs if isinstance(dbs, PackedLsdb) else pack(dbs)
+        s = N.lsdb_struct(packed)
+        out = (N.LsChange * max(1, len(packed)))()
+        self._err(N.lib.ls_update_adjacency_databases(self._h, C.byref(s), holdUpTtl,
+                                                      holdDownTtl, out))
+        res = [_change(out[i]) for i in range(len(packed))]
+        self._link_cache.clear()  # attributes may have changed
+        self._topology(res)
+        return res
+
+    def deleteAdjacencyDatabase(self, nodeName: str) -> LinkStateChange:
+        c = N.LsChange()
+        self._err(N.lib.ls_delete_adjacency_database(self._h, nodeName.encode(), C.byref(c)))
+        res = _change(c)
+        self._link_cache.clear()
+        self._topology([res])
+        return res
+
+    def decrementHolds(self) -> LinkStateChange:
+        c = N.LsChange()
+        self._err(N.lib.ls_decrement_holds(self._h, C.byref(c)))
+        res = _change(c)
+        self._link_cache.clear()
+        self._topology([res])
+        return res
+
+    # -- const queries -----------------------------------------------------------
+    def getArea(self) -> str:
+        return self._area
+
+    def hasHolds(self) -> bool:
+        return bool(N.lib.ls_has_holds(self._h))
+
+    def numLinks(self) -> int:
+        return int(N.lib.ls_num_links(self._h))
+
+    def numNodes(self) -> int:
+        return int(N.lib.ls_num_nodes(self._h))
+
+    def hasNode(self, nodeName: str) -> bool:
+        return bool(N.lib.ls_has_node(self._h, nodeName.encode()))
+
+    def isNodeOverloaded(self, nodeName: str) -> bool:
+        return bool(N.lib.ls_is_node_overloaded(self._h, nodeName.encode()))
+
+    def linksFromNode(self, nodeName: str) -> List[Link]:
+        """Links of ``nodeName`` in the reference's LinkSet iteration order."""
+        cnt = C.c_uint32()
+        self._err(N.lib.ls_links_from_node(self._h, nodeName.encode(), None, 0, C.byref(cnt)))
+        ids = (C.c_uint32 * max(1, cnt.value))()
+        self._err(N.lib.ls_links_from_node(self._h, nodeName.encode(), ids, cnt.value,
+                                           C.byref(cnt)))
+        return [self._link(ids[i]) for i in range(cnt.value)]
+
+    def spfRuns(self) -> int:
+        """The reference's ``decision.spf_runs`` counter (LinkState.cpp:815)."""
+        return int(N.lib.ls_spf_runs(self._h))
+
+    # -- shortest paths ----------------------------------------------------------
+    def getSpfResult(self, nodeName: str, useLinkMetric: bool = True) -> SpfResult:
+        key = (nodeName, bool(useLinkMetric))
+        hit = self._spf_cache.get(key)
+        if hit is not None:
+            return hit
+        v = N.LsSpfView()
+        self._err(N.lib.ls_get_spf_result(self._h, nodeName.encode(), int(bool(useLinkMetric)),
+                                          C.byref(v)))
+        res: SpfResult = {}
+        for i in range(v.n):
+            nh = {self._name(v.nh_node[j]) for j in range(v.nh_ptr[i], v.nh_ptr[i + 1])}
+            pl = [PathLink(self._link(v.pl_link[j]), self._name(v.pl_prev[j]))
+                  for j in range(v.pl_ptr[i], v.pl_ptr[i + 1])]
+            res[self._name(v.node[i])] = NodeSpfResult(int(v.metric[i]), nh, pl)
+        self._spf_cache[key] = res
+        return res
+
+    def getKthPaths(self, src: str, dest: str, k: int) -> List[Path]:
+        key = (src, dest, int(k))
+        hit = self._ksp_cache.get(key)
+        if hit is not None:
+            return hit
+        if k < 1:
+            raise ValueError("getKthPaths: k must be >= 1")
+        v = N.LsPathsView()
+        self._err(N.lib.ls_get_kth_paths(self._h, src.encode(), dest.encode(), k, C.byref(v)))
+        paths = [[self._link(v.link[j]) for j in range(v.path_ptr[p], v.path_ptr[p + 1])]
+                 for p in range(v.n_paths)]
+        self._ksp_cache[key] = paths
+        return paths
+
+    def getMetricFromAToB(self, a: str, b: str, useLinkMetric: bool = True) -> Optional[int]:
+        m = C.c_uint64()
+        has = C.c_int()
+        self._err(N.lib.ls_get_metric_a_to_b(self._h, a.encode(), b.encode(),
+                                             int(bool(useLinkMetric)), C.byref(m), C.byref(has)))
+        return int(m.value) if has.value else None
+
+    def getHopsFromAToB(self, a: str, b: str) -> Optional[int]:
+        return self.getMetricFromAToB(a, b, False)
+
+    def getMaxHopsToNode(self, nodeName: str) -> int:
+        m = C.c_uint64()
+        self._err(N.lib.ls_get_max_hops_to_node(self._h, nodeName.encode(), C.byref(m)))
+        return int(m.value)
+
+    @staticmethod
+    def pathAInPathB(a: Sequence[Link], b: Sequence[Link]) -> bool:
+        """``LinkState::pathAInPathB`` (LinkState.h:395-410): a is a contiguous
+        sub-path of b."""
+        if len(a) > len(b):
+            return False
+        for i in range(len(b) - len(a) + 1):
+            if all(a[j] == b[i + j] for j in range(len(a))):
+                return True
+        return False
+
+    # -- batch access to the flattened graph ---------------------------------------
+    def flatten(self):
+        """(node names in id order, row_ptr, col, metric, link_id, overloaded)."""
+        import numpy as np
+
+        n = C.c_uint32()
+        e = C.c_uint32()
+        self._err(N.lib.ls_flatten(self._h, C.byref(n), C.byref(e)))
+        ids = np.zeros(n.value, np.uint32)
+        rp = np.zeros(n.value + 1, np.uint32)
+        col = np.zeros(max(1, e.value), np.uint32)
+        met = np.zeros(max(1, e.value), np.int32)
+        lid = np.zeros(max(1, e.value), np.uint32)
+        ovl = np.zeros(max(1, n.value), np.uint8)
+        if n.value:
+            self._err(N.lib.ls_graph_node_names(self._h, N.ptr(ids)))
+        self._err(N.lib.ls_graph_csr(self._h, N.ptr(rp), N.ptr(col), N.ptr(met, C.c_int32),
+                                     N.ptr(lid), N.ptr(ovl, C.c_uint8)))
+        names = [self._name(int(i)) for i in ids]
+        return names, rp, col[: e.value], met[: e.value], lid[: e.value], ovl[: n.value]
+
+    def engine_handle(self) -> C.c_void_p:
+        return C.c_void_p(N.lib.ls_engine(self._h))

@@ -1,0 +1,867 @@
+// ============================================================================
+//  oracle/spf_oracle.cpp -- TEST INFRASTRUCTURE ONLY (the parity checker).
+//
+//  A from-scratch CPU restatement of Open/R's link-state SPF path:
+//    * HoldableValue          -> reference openr/decision/LinkState.h:36-58,
+//                                LinkState.cpp:54-125
+//    * Link                   -> LinkState.h:82-175, LinkState.cpp:127-377
+//    * LinkState (LSDB side)  -> LinkState.cpp:421-738
+//    * runSpf / getSpfResult  -> LinkState.cpp:793-882 (Dijkstra with the
+//                                (metric, nodeName) heap of LinkState.h:475-535)
+//    * getKthPaths/traceOnePath -> LinkState.cpp:398-419, 762-791
+//
+//  It keeps the reference's data structures on purpose (string keys,
+//  shared_ptr links, unordered containers hashed like folly, a binary heap
+//  rebuilt with make_heap after every strict decrease) so that
+//    (1) its results -- including the order of pathLinks among parallel links,
+//        which follows libstdc++ unordered_set iteration -- match the
+//        reference bit for bit, and
+//    (2) its run time is representative of the reference (bench.py times it
+//        as the "port" CPU baseline).
+//
+//  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+//  load this library.  The product (openr_amd/, libopenr_spf.so) never links
+//  or calls it.  The reference itself cannot be built here (it needs folly,
+//  fbthrift, fb303, glog); parity of this restatement is pinned against the
+//  reference's own test expectations (tests/golden/, tests/test_oracle_*.py).
+// ============================================================================
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <map>
+#include <memory>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace orc {
+
+using Metric = uint64_t;
+
+// folly::hash::hash_128_to_64 (restated; folly rev pinned by the reference in
+// build/deps/github_hashes/facebook/folly-rev.txt).  folly's
+// std::hash<std::pair<A,B>> is hash_128_to_64(std::hash<A>(a), std::hash<B>(b)).
+static inline uint64_t mix128(uint64_t upper, uint64_t lower) {
+  const uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lower ^ upper) * kMul;
+  a ^= (a >> 47);
+  uint64_t b = (upper ^ a) * kMul;
+  b ^= (b >> 47);
+  b *= kMul;
+  return b;
+}
+static inline uint64_t hashStrPair(const std::string& x, const std::string& y) {
+  return mix128(std::hash<std::string>()(x), std::hash<std::string>()(y));
+}
+
+struct Adj {
+  std::string other, ifName, otherIf;
+  int32_t metric{0};
+  int32_t adjLabel{0};
+  bool overloaded{false};
+  int32_t rtt{0};
+  int64_t timestamp{0};
+  int64_t weight{1};
+  std::string nhV6, nhV4;  // raw address bytes
+};
+
+struct AdjDb {
+  std::string node;
+  bool overloaded{false};
+  std::vector<Adj> adjs;
+  int32_t nodeLabel{0};
+  std::string area;
+};
+
+// ---- HoldableValue (LinkState.cpp:54-125) ----------------------------------
+template <class T>
+class Held {
+ public:
+  explicit Held(T v) : cur_(v) {}
+  void assign(T v) {
+    cur_ = v;
+    old_.reset();
+    ttl_ = 0;
+  }
+  const T& value() const { return old_ ? *old_ : cur_; }
+  bool hasHold() const { return old_.has_value(); }
+  bool decrementTtl() {
+    if (old_ && --ttl_ == 0) {
+      old_.reset();
+      return true;
+    }
+    return false;
+  }
+  bool updateValue(T v, Metric upTtl, Metric downTtl) {
+    if (v == cur_) return false;
+    if (hasHold()) {
+      old_.reset();
+      ttl_ = 0;
+    } else {
+      ttl_ = bringsUp(v) ? upTtl : downTtl;
+      if (ttl_ != 0) old_ = cur_;
+    }
+    cur_ = v;
+    return !hasHold();
+  }
+
+ private:
+  bool bringsUp(T v) const;
+  T cur_;
+  std::optional<T> old_;
+  Metric ttl_{0};
+};
+template <>
+bool Held<bool>::bringsUp(bool v) const { return cur_ && !v; }
+template <>
+bool Held<Metric>::bringsUp(Metric v) const { return v < cur_; }
+
+// ---- Link (LinkState.cpp:127-377) ---------------------------------------------
+class Link {
+ public:
+  Link(const std::string& n1, const std::string& i1, const std::string& n2,
+       const std::string& i2)
+      : n1_(n1), n2_(n2), if1_(i1), if2_(i2),
+        key_(std::minmax(std::make_pair(n1, i1), std::make_pair(n2, i2))),
+        hash(mix128(hashStrPair(key_.first.first, key_.first.second),
+                    hashStrPair(key_.second.first, key_.second.second))) {}
+  Link(const std::string& n1, const Adj& a1, const std::string& n2,
+       const Adj& a2)
+      : Link(n1, a1.ifName, n2, a2.ifName) {
+    m1_.assign((Metric)(int64_t)a1.metric);  // i32 -> u64 as the reference
+    m2_.assign((Metric)(int64_t)a2.metric);
+    o1_.assign(a1.overloaded);
+    o2_.assign(a2.overloaded);
+    l1_ = a1.adjLabel;
+    l2_ = a2.adjLabel;
+    v4a_ = a1.nhV4; v4b_ = a2.nhV4;
+    v6a_ = a1.nhV6; v6b_ = a2.nhV6;
+  }
+
+  int side(const std::string& n) const {
+    if (n == n1_) return 1;
+    if (n == n2_) return 2;
+    throw std::invalid_argument(n);
+  }
+  const std::string& other(const std::string& n) const {
+    return side(n) == 1 ? n2_ : n1_;
+  }
+  const std::string& firstNode() const { return key_.first.first; }
+  const std::string& secondNode() const { return key_.second.first; }
+  const std::string& ifaceFrom(const std::string& n) const {
+    return side(n) == 1 ? if1_ : if2_;
+  }
+  Metric metricFrom(const std::string& n) const {
+    return side(n) == 1 ? m1_.value() : m2_.value();
+  }
+  bool overloadFrom(const std::string& n) const {
+    return side(n) == 1 ? o1_.value() : o2_.value();
+  }
+  int32_t labelFrom(const std::string& n) const {
+    return side(n) == 1 ? l1_ : l2_;
+  }
+  const std::string& v4From(const std::string& n) const {
+    return side(n) == 1 ? v4a_ : v4b_;
+  }
+  const std::string& v6From(const std::string& n) const {
+    return side(n) == 1 ? v6a_ : v6b_;
+  }
+  void setV4From(const std::string& n, const std::string& v) {
+    (side(n) == 1 ? v4a_ : v4b_) = v;
+  }
+  void setV6From(const std::string& n, const std::string& v) {
+    (side(n) == 1 ? v6a_ : v6b_) = v;
+  }
+  void setLabelFrom(const std::string& n, int32_t l) {
+    (side(n) == 1 ? l1_ : l2_) = l;
+  }
+  bool setMetricFrom(const std::string& n, Metric m, Metric up, Metric down) {
+    return (side(n) == 1 ? m1_ : m2_).updateValue(m, up, down);
+  }
+  bool setOverloadFrom(const std::string& n, bool o, Metric up, Metric down) {
+    bool wasUp = isUp();
+    (side(n) == 1 ? o1_ : o2_).updateValue(o, up, down);
+    return wasUp != isUp();
+  }
+  void setHoldUpTtl(Metric t) { holdUp_ = t; }
+  bool isUp() const { return holdUp_ == 0 && !o1_.value() && !o2_.value(); }
+  bool decrementHolds() {
+    bool expired = false;
+    if (holdUp_ != 0) expired |= (--holdUp_ == 0);
+    expired |= m1_.decrementTtl();
+    expired |= m2_.decrementTtl();
+    expired |= o1_.decrementTtl();
+    expired |= o2_.decrementTtl();
+    return expired;
+  }
+  bool hasHolds() const {
+    return holdUp_ != 0 || m1_.hasHold() || m2_.hasHold() || o1_.hasHold() ||
+           o2_.hasHold();
+  }
+  bool lessThan(const Link& o) const {
+    if (hash != o.hash) return hash < o.hash;
+    return key_ < o.key_;
+  }
+  bool sameAs(const Link& o) const { return hash == o.hash && key_ == o.key_; }
+  const std::pair<std::pair<std::string, std::string>,
+                  std::pair<std::string, std::string>>&
+  key() const {
+    return key_;
+  }
+
+ private:
+  std::string n1_, n2_, if1_, if2_;
+  Held<Metric> m1_{1}, m2_{1};
+  Held<bool> o1_{false}, o2_{false};
+  int32_t l1_{0}, l2_{0};
+  std::string v4a_, v4b_, v6a_, v6b_;
+  Metric holdUp_{0};
+  std::pair<std::pair<std::string, std::string>,
+            std::pair<std::string, std::string>>
+      key_;
+
+ public:
+  const size_t hash;
+};
+
+using LinkPtr = std::shared_ptr<Link>;
+struct LinkHash {
+  size_t operator()(const LinkPtr& l) const { return l->hash; }
+};
+struct LinkEq {
+  bool operator()(const LinkPtr& a, const LinkPtr& b) const {
+    return a->sameAs(*b);
+  }
+};
+struct LinkLess {
+  bool operator()(const LinkPtr& a, const LinkPtr& b) const {
+    return a->lessThan(*b);
+  }
+};
+using LinkSet = std::unordered_set<LinkPtr, LinkHash, LinkEq>;
+
+struct NodeResult {
+  explicit NodeResult(Metric m) : metric(m) {}
+  Metric metric;
+  std::vector<std::pair<LinkPtr, std::string>> pathLinks;  // (link, prevNode)
+  std::unordered_set<std::string> nextHops;
+  void reset(Metric m) {
+    metric = m;
+    pathLinks.clear();
+    nextHops.clear();
+  }
+};
+using SpfResult = std::unordered_map<std::string, NodeResult>;
+using Path = std::vector<LinkPtr>;
+
+static uint64_t g_spf_runs = 0;
+
+// ---- Dijkstra priority queue (LinkState.h:475-535) -------------------------
+struct QNode {
+  QNode(const std::string& n, Metric m) : name(n), res(m) {}
+  const std::string name;
+  NodeResult res;
+};
+class DQueue {
+ public:
+  void insert(const std::string& n, Metric d) {
+    heap_.push_back(std::make_shared<QNode>(n, d));
+    byName_[n] = heap_.back();
+    std::push_heap(heap_.begin(), heap_.end(), greater);
+  }
+  std::shared_ptr<QNode> get(const std::string& n) {
+    auto it = byName_.find(n);
+    return it == byName_.end() ? nullptr : it->second;
+  }
+  std::shared_ptr<QNode> popMin() {
+    if (heap_.empty()) return nullptr;
+    auto m = heap_.front();
+    byName_.erase(m->name);
+    std::pop_heap(heap_.begin(), heap_.end(), greater);
+    heap_.pop_back();
+    return m;
+  }
+  void rebuild() { std::make_heap(heap_.begin(), heap_.end(), greater); }
+
+ private:
+  static bool greater(const std::shared_ptr<QNode>& a,
+                      const std::shared_ptr<QNode>& b) {
+    if (a->res.metric != b->res.metric) return a->res.metric > b->res.metric;
+    return a->name > b->name;
+  }
+  std::vector<std::shared_ptr<QNode>> heap_;
+  std::unordered_map<std::string, std::shared_ptr<QNode>> byName_;
+};
+
+struct Change {
+  bool topo{false}, attrs{false}, label{false};
+};
+
+// ---- LinkState (LinkState.cpp:379-882) -------------------------------------
+class LinkState {
+ public:
+  explicit LinkState(std::string area) : area_(std::move(area)) {}
+
+  const LinkSet& linksFrom(const std::string& n) const {
+    static const LinkSet kEmpty;
+    auto it = linkMap_.find(n);
+    return it == linkMap_.end() ? kEmpty : it->second;
+  }
+  bool nodeOverloaded(const std::string& n) const {
+    auto it = nodeOvl_.find(n);
+    return it != nodeOvl_.end() && it->second.value();
+  }
+  bool hasNode(const std::string& n) const { return dbs_.count(n) != 0; }
+  size_t numLinks() const { return allLinks_.size(); }
+  size_t numNodes() const { return linkMap_.size(); }
+  const std::unordered_map<std::string, AdjDb>& dbs() const { return dbs_; }
+
+  Change decrementHolds() {
+    Change c;
+    for (auto& l : allLinks_) c.topo |= l->decrementHolds();
+    for (auto& kv : nodeOvl_) c.topo |= kv.second.decrementTtl();
+    if (c.topo) clearMemo();
+    return c;
+  }
+  bool hasHolds() const {
+    for (auto& l : allLinks_)
+      if (l->hasHolds()) return true;
+    for (auto& kv : nodeOvl_)
+      if (kv.second.hasHold()) return true;
+    return false;
+  }
+
+  Change update(const AdjDb& db, Metric holdUp, Metric holdDown) {
+    Change c;
+    const std::string node = db.node;
+    AdjDb prior = std::move(dbs_[node]);
+    dbs_[node] = db;
+
+    // both sides ordered by Link::operator< (hash first), merged below
+    std::vector<LinkPtr> oldL, newL;
+    auto lm = linkMap_.find(node);
+    if (lm != linkMap_.end()) {
+      oldL.assign(lm->second.begin(), lm->second.end());
+      std::sort(oldL.begin(), oldL.end(), LinkLess{});
+    }
+    for (const auto& a : db.adjs) {
+      if (auto l = bidirectional(node, a)) newL.push_back(l);
+    }
+    std::sort(newL.begin(), newL.end(), LinkLess{});
+
+    c.topo |= setNodeOverload(node, db.overloaded, holdUp, holdDown);
+    c.label = prior.nodeLabel != db.nodeLabel;
+
+    size_t i = 0, j = 0;
+    while (i < newL.size() || j < oldL.size()) {
+      if (i < newL.size() && (j == oldL.size() || newL[i]->lessThan(*oldL[j]))) {
+        newL[i]->setHoldUpTtl(holdUp);
+        c.topo |= newL[i]->isUp();
+        addLink(newL[i]);
+        ++i;
+        continue;
+      }
+      if (j < oldL.size() && (i == newL.size() || oldL[j]->lessThan(*newL[i]))) {
+        c.topo |= oldL[j]->isUp();
+        removeLink(oldL[j]);
+        ++j;
+        continue;
+      }
+      Link& nl = *newL[i];
+      Link& ol = *oldL[j];
+      if (nl.metricFrom(node) != ol.metricFrom(node)) {
+        c.topo |= ol.setMetricFrom(node, nl.metricFrom(node), holdUp, holdDown);
+      }
+      if (nl.overloadFrom(node) != ol.overloadFrom(node)) {
+        c.topo |=
+            ol.setOverloadFrom(node, nl.overloadFrom(node), holdUp, holdDown);
+      }
+      if (nl.labelFrom(node) != ol.labelFrom(node)) {
+        c.attrs = true;
+        ol.setLabelFrom(node, nl.labelFrom(node));
+      }
+      if (nl.v4From(node) != ol.v4From(node)) {
+        c.attrs = true;
+        ol.setV4From(node, nl.v4From(node));
+      }
+      if (nl.v6From(node) != ol.v6From(node)) {
+        c.attrs = true;
+        ol.setV6From(node, nl.v6From(node));
+      }
+      ++i;
+      ++j;
+    }
+    if (c.topo) clearMemo();
+    return c;
+  }
+
+  Change remove(const std::string& node) {
+    Change c;
+    auto it = dbs_.find(node);
+    if (it != dbs_.end()) {
+      auto lm = linkMap_.find(node);
+      if (lm != linkMap_.end()) {
+        for (const auto& l : lm->second) {
+          if (!linkMap_.at(l->other(node)).erase(l)) abort();
+          if (!allLinks_.erase(l)) abort();
+        }
+        linkMap_.erase(lm);
+        nodeOvl_.erase(node);
+      }
+      dbs_.erase(it);
+      clearMemo();
+      c.topo = true;
+    }
+    return c;
+  }
+
+  // --- SPF (LinkState.cpp:808-882) ---
+  SpfResult runSpf(const std::string& src, bool useLinkMetric,
+                   const LinkSet& ignore = {}) const {
+    SpfResult result;
+    ++g_spf_runs;
+    DQueue q;
+    q.insert(src, 0);
+    while (auto cur = q.popMin()) {
+      auto ins = result.emplace(cur->name, std::move(cur->res));
+      if (!ins.second) abort();
+      const std::string& u = ins.first->first;
+      const Metric du = ins.first->second.metric;
+      const auto& nhU = ins.first->second.nextHops;
+      if (nodeOverloaded(u) && u != src) continue;  // drained: no transit
+      for (const auto& l : linksFrom(u)) {
+        const std::string& v = l->other(u);
+        if (!l->isUp() || result.count(v) || ignore.count(l)) continue;
+        const Metric w = useLinkMetric ? l->metricFrom(u) : 1;
+        auto qv = q.get(v);
+        if (!qv) {
+          q.insert(v, du + w);
+          qv = q.get(v);
+        }
+        if (qv->res.metric >= du + w) {
+          if (qv->res.metric > du + w) {
+            qv->res.reset(du + w);
+            q.rebuild();
+          }
+          qv->res.pathLinks.emplace_back(l, u);
+          qv->res.nextHops.insert(nhU.begin(), nhU.end());
+          if (qv->res.nextHops.empty()) qv->res.nextHops.insert(v);
+        }
+      }
+    }
+    return result;
+  }
+
+  const SpfResult& getSpfResult(const std::string& n, bool useLinkMetric) const {
+    auto key = std::make_pair(n, useLinkMetric);
+    auto it = spfMemo_.find(key);
+    if (it == spfMemo_.end()) {
+      it = spfMemo_.emplace(key, runSpf(n, useLinkMetric)).first;
+    }
+    return it->second;
+  }
+
+  std::optional<Metric> metricAToB(const std::string& a, const std::string& b,
+                                   bool useLinkMetric) const {
+    if (a == b) return 0;
+    const auto& r = getSpfResult(a, useLinkMetric);
+    auto it = r.find(b);
+    if (it == r.end()) return std::nullopt;
+    return it->second.metric;
+  }
+  Metric maxHops(const std::string& n) const {
+    Metric m = 0;
+    for (const auto& kv : getSpfResult(n, false)) m = std::max(m, kv.second.metric);
+    return m;
+  }
+
+  // --- KSP (LinkState.cpp:398-419, 762-791) ---
+  std::optional<Path> trace(const std::string& src, const std::string& dst,
+                            const SpfResult& r, LinkSet& used) const {
+    if (src == dst) return Path{};
+    for (const auto& pl : r.at(dst).pathLinks) {
+      if (used.insert(pl.first).second) {
+        auto p = trace(src, pl.second, r, used);
+        if (p) {
+          p->push_back(pl.first);
+          return p;
+        }
+      }
+    }
+    return std::nullopt;
+  }
+  const std::vector<Path>& kthPaths(const std::string& src,
+                                    const std::string& dst, size_t k) const {
+    if (k < 1) abort();
+    auto key = std::make_tuple(src, dst, k);
+    auto it = kspMemo_.find(key);
+    if (it != kspMemo_.end()) return it->second;
+    LinkSet ignore;
+    for (size_t i = 1; i < k; ++i)
+      for (const auto& p : kthPaths(src, dst, i))
+        for (const auto& l : p) ignore.insert(l);
+    std::vector<Path> paths;
+    SpfResult fresh;
+    const SpfResult* res;
+    if (ignore.empty()) {
+      res = &getSpfResult(src, true);
+    } else {
+      fresh = runSpf(src, true, ignore);
+      res = &fresh;
+    }
+    if (res->count(dst)) {
+      LinkSet visited;
+      auto p = trace(src, dst, *res, visited);
+      while (p && !p->empty()) {
+        paths.push_back(std::move(*p));
+        p = trace(src, dst, *res, visited);
+      }
+    }
+    return kspMemo_.emplace(key, std::move(paths)).first->second;
+  }
+
+ private:
+  void clearMemo() {
+    spfMemo_.clear();
+    kspMemo_.clear();
+  }
+  bool setNodeOverload(const std::string& n, bool o, Metric up, Metric down) {
+    auto it = nodeOvl_.find(n);
+    if (it != nodeOvl_.end()) return it->second.updateValue(o, up, down);
+    nodeOvl_.emplace(n, Held<bool>{o});
+    return false;  // a new node never signals a change
+  }
+  LinkPtr bidirectional(const std::string& node, const Adj& a) const {
+    auto it = dbs_.find(a.other);
+    if (it == dbs_.end()) return nullptr;
+    for (const auto& b : it->second.adjs) {
+      if (b.other == node && a.otherIf == b.ifName && a.ifName == b.otherIf) {
+        return std::make_shared<Link>(node, a, a.other, b);
+      }
+    }
+    return nullptr;
+  }
+  void addLink(const LinkPtr& l) {
+    if (!linkMap_[l->firstNode()].insert(l).second) abort();
+    if (!linkMap_[l->secondNode()].insert(l).second) abort();
+    if (!allLinks_.insert(l).second) abort();
+  }
+  void removeLink(const LinkPtr& l) {
+    if (!linkMap_.at(l->firstNode()).erase(l)) abort();
+    if (!linkMap_.at(l->secondNode()).erase(l)) abort();
+    if (!allLinks_.erase(l)) abort();
+  }
+
+  struct PairHash {
+    size_t operator()(const std::pair<std::string, bool>& p) const {
+      return mix128(std::hash<std::string>()(p.first), std::hash<bool>()(p.second));
+    }
+  };
+  struct TupHash {
+    size_t operator()(const std::tuple<std::string, std::string, size_t>& t) const {
+      return mix128(std::hash<std::string>()(std::get<0>(t)),
+                    mix128(std::hash<std::string>()(std::get<1>(t)),
+                           std::hash<size_t>()(std::get<2>(t))));
+    }
+  };
+
+  std::string area_;
+  std::unordered_map<std::string, LinkSet> linkMap_;
+  LinkSet allLinks_;
+  std::unordered_map<std::string, Held<bool>> nodeOvl_;
+  std::unordered_map<std::string, AdjDb> dbs_;
+  mutable std::unordered_map<std::pair<std::string, bool>, SpfResult, PairHash>
+      spfMemo_;
+  mutable std::unordered_map<std::tuple<std::string, std::string, size_t>,
+                             std::vector<Path>, TupHash>
+      kspMemo_;
+};
+
+}  // namespace orc
+
+// ============================================================================
+//  C API used by tests/ and bench.py (ctypes).  Input: the packed LSDB layout
+//  documented in include/openr_lsdb.h (string blob + fixed-size records).
+// ============================================================================
+extern "C" {
+
+struct orc_db_rec {
+  uint32_t name_off, name_len, area_off, area_len;
+  int32_t is_overloaded, node_label;
+  uint32_t adj_begin, adj_count;
+};
+struct orc_adj_rec {
+  uint32_t other_off, other_len, if_off, if_len, oif_off, oif_len;
+  int32_t metric, adj_label, is_overloaded, rtt;
+  int64_t timestamp, weight;
+  uint8_t nh_v6[16];
+  uint8_t nh_v4[4];
+  uint8_t pad[4];
+};
+static_assert(sizeof(orc_db_rec) == 32, "db record layout");
+static_assert(sizeof(orc_adj_rec) == 80, "adj record layout");
+
+struct orc_ls {
+  orc::LinkState ls;
+  std::string scratch;
+  explicit orc_ls(const char* a) : ls(a ? a : "") {}
+};
+
+static std::string str_at(const char* blob, uint32_t off, uint32_t len) {
+  return std::string(blob + off, len);
+}
+
+orc_ls* orc_ls_new(const char* area) { return new orc_ls(area); }
+void orc_ls_free(orc_ls* p) { delete p; }
+uint64_t orc_spf_runs(void) { return orc::g_spf_runs; }
+
+static void put_change(const orc::Change& c, uint8_t* out) {
+  if (!out) return;
+  out[0] = c.topo;
+  out[1] = c.attrs;
+  out[2] = c.label;
+}
+
+// Apply n_db adjacency databases in order (each one a separate
+// updateAdjacencyDatabase call).  changes_out: 3 bytes per db.
+int orc_ls_update_packed(orc_ls* p, const char* blob, const orc_db_rec* dbs,
+                         uint32_t n_db, const orc_adj_rec* adjs,
+                         uint64_t hold_up, uint64_t hold_down,
+                         uint8_t* changes_out) {
+  for (uint32_t d = 0; d < n_db; ++d) {
+    orc::AdjDb db;
+    db.node = str_at(blob, dbs[d].name_off, dbs[d].name_len);
+    db.area = str_at(blob, dbs[d].area_off, dbs[d].area_len);
+    db.overloaded = dbs[d].is_overloaded != 0;
+    db.nodeLabel = dbs[d].node_label;
+    db.adjs.reserve(dbs[d].adj_count);
+    for (uint32_t k = 0; k < dbs[d].adj_count; ++k) {
+      const orc_adj_rec& r = adjs[dbs[d].adj_begin + k];
+      orc::Adj a;
+      a.other = str_at(blob, r.other_off, r.other_len);
+      a.ifName = str_at(blob, r.if_off, r.if_len);
+      a.otherIf = str_at(blob, r.oif_off, r.oif_len);
+      a.metric = r.metric;
+      a.adjLabel = r.adj_label;
+      a.overloaded = r.is_overloaded != 0;
+      a.rtt = r.rtt;
+      a.timestamp = r.timestamp;
+      a.weight = r.weight;
+      a.nhV6.assign((const char*)r.nh_v6, 16);
+      a.nhV4.assign((const char*)r.nh_v4, 4);
+      db.adjs.push_back(std::move(a));
+    }
+    put_change(p->ls.update(db, hold_up, hold_down),
+               changes_out ? changes_out + 3 * d : nullptr);
+  }
+  return 0;
+}
+
+int orc_ls_delete(orc_ls* p, const char* node, uint8_t* change_out) {
+  put_change(p->ls.remove(node), change_out);
+  return 0;
+}
+int orc_ls_decrement_holds(orc_ls* p, uint8_t* change_out) {
+  put_change(p->ls.decrementHolds(), change_out);
+  return 0;
+}
+int orc_ls_has_holds(orc_ls* p) { return p->ls.hasHolds(); }
+uint64_t orc_ls_num_links(orc_ls* p) { return p->ls.numLinks(); }
+uint64_t orc_ls_num_nodes(orc_ls* p) { return p->ls.numNodes(); }
+int orc_ls_is_overloaded(orc_ls* p, const char* n) {
+  return p->ls.nodeOverloaded(n);
+}
+int orc_ls_metric_a_to_b(orc_ls* p, const char* a, const char* b, int ulm,
+                         uint64_t* out) {
+  auto m = p->ls.metricAToB(a, b, ulm != 0);
+  if (!m) return 0;
+  *out = *m;
+  return 1;
+}
+uint64_t orc_ls_max_hops(orc_ls* p, const char* n) { return p->ls.maxHops(n); }
+
+// ---- JSON rendering for small graphs ----
+static void json_str(std::string& o, const std::string& s) {
+  o += '"';
+  for (char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += c;
+    } else if ((unsigned char)c < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", (unsigned char)c);
+      o += b;
+    } else {
+      o += c;
+    }
+  }
+  o += '"';
+}
+static void json_link(std::string& o, const orc::Link& l) {
+  const auto& k = l.key();
+  o += '[';
+  json_str(o, k.first.first);
+  o += ',';
+  json_str(o, k.first.second);
+  o += ',';
+  json_str(o, k.second.first);
+  o += ',';
+  json_str(o, k.second.second);
+  o += ']';
+}
+
+// {"node": {"metric": m, "nextHops": [sorted], "pathLinks": [[link, prev],..]}}
+const char* orc_ls_spf_json(orc_ls* p, const char* src, int ulm) {
+  const auto& r = p->ls.getSpfResult(src, ulm != 0);
+  std::map<std::string, const orc::NodeResult*> sorted;
+  for (const auto& kv : r) sorted[kv.first] = &kv.second;
+  std::string& o = p->scratch;
+  o = "{";
+  bool first = true;
+  for (const auto& kv : sorted) {
+    if (!first) o += ',';
+    first = false;
+    json_str(o, kv.first);
+    o += ":{\"metric\":" + std::to_string(kv.second->metric) + ",\"nextHops\":[";
+    std::set<std::string> nh(kv.second->nextHops.begin(), kv.second->nextHops.end());
+    bool f2 = true;
+    for (const auto& h : nh) {
+      if (!f2) o += ',';
+      f2 = false;
+      json_str(o, h);
+    }
+    o += "],\"pathLinks\":[";
+    f2 = true;
+    for (const auto& pl : kv.second->pathLinks) {
+      if (!f2) o += ',';
+      f2 = false;
+      o += '[';
+      json_link(o, *pl.first);
+      o += ',';
+      json_str(o, pl.second);
+      o += ']';
+    }
+    o += "]}";
+  }
+  o += '}';
+  return o.c_str();
+}
+
+// [[link, link, ...], ...]  (paths in discovery order, links src -> dst)
+const char* orc_ls_kth_paths_json(orc_ls* p, const char* src, const char* dst,
+                                  uint64_t k) {
+  const auto& paths = p->ls.kthPaths(src, dst, k);
+  std::string& o = p->scratch;
+  o = "[";
+  for (size_t i = 0; i < paths.size(); ++i) {
+    if (i) o += ',';
+    o += '[';
+    for (size_t j = 0; j < paths[i].size(); ++j) {
+      if (j) o += ',';
+      json_link(o, *paths[i][j]);
+    }
+    o += ']';
+  }
+  o += ']';
+  return o.c_str();
+}
+
+// linksFromNode(node) in container iteration order:
+// [[link, metricFromNode, isUp], ...]
+const char* orc_ls_links_json(orc_ls* p, const char* node) {
+  std::string& o = p->scratch;
+  o = "[";
+  bool first = true;
+  for (const auto& l : p->ls.linksFrom(node)) {
+    if (!first) o += ',';
+    first = false;
+    o += '[';
+    json_link(o, *l);
+    o += ',' + std::to_string(l->metricFrom(node)) + ',' +
+         (l->isUp() ? "true" : "false") + ']';
+  }
+  o += ']';
+  return o.c_str();
+}
+
+// ---- dense all-sources rendering ------------------------------------------
+// Node ids: the caller supplies the node names in ascending std::string order
+// (node_blob/node_off/node_len, n_nodes).  For each source id in srcs:
+//   dist_out[i*n_nodes + v]  = metric (UINT64_MAX if unreachable)
+//   nh bitset: bit j of source i = j-th node (ascending name) among the
+//   distinct other ends of src's up links; u32 words, ceil(k/32) per node,
+//   stored at nh_out[nh_off[i] + v*words_i + w].  nh_words_out[i] = words_i.
+// Set nh_out == NULL to only compute nh_words_out (sizing pass).
+// Memoization is bypassed (each source is one runSpf, result discarded):
+// this is the timed CPU-baseline path.
+int orc_ls_dense(orc_ls* p, const char* node_blob, const uint32_t* node_off,
+                 const uint32_t* node_len, uint32_t n_nodes,
+                 const uint32_t* srcs, uint32_t n_src, int ulm,
+                 uint64_t* dist_out, uint32_t* nh_out, const uint64_t* nh_off,
+                 uint32_t* nh_words_out) {
+  std::unordered_map<std::string, uint32_t> idOf;
+  idOf.reserve(n_nodes * 2);
+  std::vector<std::string> names(n_nodes);
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    names[i] = std::string(node_blob + node_off[i], node_len[i]);
+    idOf.emplace(names[i], i);
+  }
+  for (uint32_t i = 0; i < n_src; ++i) {
+    const std::string& s = names[srcs[i]];
+    std::set<std::string> nbrSet;
+    for (const auto& l : p->ls.linksFrom(s))
+      if (l->isUp()) nbrSet.insert(l->other(s));
+    std::unordered_map<std::string, uint32_t> bitOf;
+    uint32_t b = 0;
+    for (const auto& n : nbrSet) bitOf[n] = b++;
+    const uint32_t words = (b + 31) / 32;
+    if (nh_words_out) nh_words_out[i] = words;
+    if (!dist_out && !nh_out) continue;
+    orc::SpfResult r = p->ls.runSpf(s, ulm != 0);
+    if (dist_out) {
+      uint64_t* d = dist_out + (uint64_t)i * n_nodes;
+      for (uint32_t v = 0; v < n_nodes; ++v) d[v] = UINT64_MAX;
+    }
+    if (nh_out && words) {
+      uint32_t* h = nh_out + nh_off[i];
+      std::memset(h, 0, sizeof(uint32_t) * (size_t)words * n_nodes);
+    }
+    for (const auto& kv : r) {
+      auto it = idOf.find(kv.first);
+      if (it == idOf.end()) continue;  // node outside the supplied table
+      const uint32_t v = it->second;
+      if (dist_out) dist_out[(uint64_t)i * n_nodes + v] = kv.second.metric;
+      if (nh_out && words) {
+        uint32_t* h = nh_out + nh_off[i] + (uint64_t)v * words;
+        for (const auto& nh : kv.second.nextHops) {
+          const uint32_t j = bitOf.at(nh);
+          h[j >> 5] |= 1u << (j & 31);
+        }
+      }
+    }
+  }
+  return 0;
+}
+
+// Time-only baseline: run runSpf for each source, fold (metric, |nh|) of every
+// reached node into a checksum so the work cannot be elided.  Returns the
+// checksum.
+uint64_t orc_ls_time_sources(orc_ls* p, const char* const* srcs, uint32_t n,
+                             int ulm) {
+  uint64_t acc = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    orc::SpfResult r = p->ls.runSpf(srcs[i], ulm != 0);
+    for (const auto& kv : r) acc += kv.second.metric * 31 + kv.second.nextHops.size();
+  }
+  return acc;
+}
+
+}  // extern "C"

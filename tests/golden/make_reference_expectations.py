@@ -1,0 +1,309 @@
+"""Writes tests/golden/reference_expectations.json.
+
+Every case below is transcribed from the reference's own test suite
+(/root/reference/openr/decision/tests/{LinkStateTest,DecisionTest}.cpp) -- the
+topology the test builds and the values it asserts, reduced to what the SPF
+path produces (metric + next-hop node set; a route's next hops in
+DecisionTest are the neighbours behind ``createNextHopFromAdj(adjXY, ...)``).
+Run from the repo root:  python tests/golden/make_reference_expectations.py
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent))
+sys.path.insert(0, str(HERE.parents[1]))
+
+from helpers import get_link_state_dbs  # noqa: E402
+from openr_amd.lsdb import create_adj_db, create_adjacency  # noqa: E402
+
+
+def db_json(db):
+    return {
+        "node": db.thisNodeName,
+        "overloaded": db.isOverloaded,
+        "nodeLabel": db.nodeLabel,
+        "adjs": [
+            {"other": a.otherNodeName, "if": a.ifName, "oif": a.otherIfName,
+             "metric": a.metric, "label": a.adjLabel, "overloaded": a.isOverloaded,
+             "v6": a.nextHopV6.hex(), "v4": a.nextHopV4.hex()}
+            for a in db.adjacencies
+        ],
+    }
+
+
+def spf(src, expect, cite, exact=True, ulm=True):
+    return {"type": "spf", "src": src, "use_link_metric": ulm, "exact_keys": exact,
+            "expect": {k: {"metric": m, "nextHops": sorted(nh)} for k, (m, nh) in expect.items()},
+            "cite": cite}
+
+
+cases = []
+
+# ---------------- LinkStateTest.cpp ----------------
+cases.append({
+    "name": "linkstate_kth_weighted_box",
+    "cite": "LinkStateTest.cpp:244-281",
+    "steps": [{"update": [db_json(d) for d in get_link_state_dbs({
+        1: [(2, 10), (3, 5)], 2: [(1, 10), (4, 15), (4, 35)],
+        3: [(1, 5), (4, 20)], 4: [(2, 15), (3, 20), (2, 35)]})]}],
+    "checks": [
+        {"type": "kth", "src": "2", "dst": "4", "k": 1, "n_paths": 1, "sizes": [1],
+         "first_link_metric_from_src": 15, "cite": "LinkStateTest.cpp:261-264"},
+        {"type": "kth", "src": "2", "dst": "4", "k": 2, "n_paths": 2, "sizes": [1, 3],
+         "path_metric": 35, "cite": "LinkStateTest.cpp:266-280"},
+    ],
+})
+cases.append({
+    "name": "linkstate_kth_mesh_parallel",
+    "cite": "LinkStateTest.cpp:283-316",
+    "steps": [{"update": [db_json(d) for d in get_link_state_dbs({
+        1: [2, 2, 3, 3, 4, 4], 2: [1, 1, 3, 3, 4, 4],
+        3: [1, 1, 2, 2, 4, 4], 4: [1, 1, 2, 2, 3, 3]})]}],
+    "checks": [
+        {"type": "kth", "src": "2", "dst": "4", "k": 1, "n_paths": 2, "sizes": [1, 1],
+         "cite": "LinkStateTest.cpp:299-301"},
+        {"type": "kth", "src": "2", "dst": "4", "k": 2, "n_paths": 4, "sizes": [2, 2, 2, 2],
+         "disjoint_with_k": [1], "cite": "LinkStateTest.cpp:303-315"},
+    ],
+})
+for name, adj, checks, cite in [
+    ("box", {1: [2, 3], 2: [1, 4], 3: [1, 4], 4: [2, 3]},
+     [("1", "2", 1), ("1", "4", 2), ("max", "1", 2)], "LinkStateTest.cpp:319-337"),
+    ("line", {1: [2], 2: [1, 3], 3: [2, 4], 4: [3, 5], 5: [4]},
+     [("1", "2", 1), ("1", "4", 3), ("2", "3", 1), ("max", "1", 4), ("max", "2", 3),
+      ("max", "3", 2)], "LinkStateTest.cpp:339-358"),
+    ("disconnected_line", {1: [2], 2: [1, 3], 3: [2, 4], 4: [3], 5: []},
+     [("1", "5", None), ("2", "3", 1), ("max", "1", 3), ("max", "5", 0)],
+     "LinkStateTest.cpp:360-376"),
+]:
+    chk = []
+    for a, b, v in checks:
+        if a == "max":
+            chk.append({"type": "max_hops", "node": b, "expect": v, "cite": cite})
+        else:
+            chk.append({"type": "hops", "a": a, "b": b, "expect": v, "cite": cite})
+    cases.append({"name": f"linkstate_hops_{name}", "cite": cite,
+                  "steps": [{"update": [db_json(d) for d in get_link_state_dbs(adj)]}],
+                  "checks": chk})
+
+# LinkStateTest.cpp:139-200 BasicOperation: change flags and link sets
+n1, n2, n3 = "node1", "node2", "node3"
+adj12 = create_adjacency(n2, "if2", "if1", "fe80::2", "10.0.0.2", 1, 1, 1)
+adj13 = create_adjacency(n3, "if3", "if1", "fe80::3", "10.0.0.3", 1, 1, 1)
+adj21 = create_adjacency(n1, "if1", "if2", "fe80::1", "10.0.0.1", 1, 1, 1)
+adj23 = create_adjacency(n3, "if3", "if2", "fe80::3", "10.0.0.3", 1, 1, 1)
+adj31 = create_adjacency(n1, "if1", "if3", "fe80::1", "10.0.0.1", 1, 1, 1)
+adj32 = create_adjacency(n2, "if2", "if3", "fe80::2", "10.0.0.2", 1, 1, 1)
+db1 = create_adj_db(n1, [adj12, adj13], 1)
+db2 = create_adj_db(n2, [adj21, adj23], 2)
+db3 = create_adj_db(n3, [adj31, adj32], 3)
+db1o = create_adj_db(n1, [adj12, adj13], 1, True)
+db1b = create_adj_db(n1, [adj13], 1)
+L1 = [n1, "if2", n2, "if1"]  # Link(n1, adj12, n2, adj21): (node1,if2)-(node2,if1)
+L2 = [n2, "if3", n3, "if2"]
+L3 = [n1, "if3", n3, "if1"]
+cases.append({
+    "name": "linkstate_basic_operation",
+    "cite": "LinkStateTest.cpp:139-200",
+    "steps": [
+        {"update": [db_json(db1)], "expect_change": [[False, False, True]]},
+        {"update": [db_json(db2)], "expect_change": [[True, False, True]]},
+        {"update": [db_json(db3)], "expect_change": [[True, False, True]]},
+        {"check_links": {n1: [L1, L3], n2: [L1, L2], n3: [L2, L3], "node4": []},
+         "check_overloaded": {n1: False}},
+        {"update": [db_json(db1o)], "expect_change": [[True, False, False]],
+         "check_overloaded": {n1: True}},
+        {"update": [db_json(db1o)], "expect_change": [[False, False, False]]},
+        {"update": [db_json(db1)], "expect_change": [[True, False, False]],
+         "check_overloaded": {n1: False}},
+        {"update": [db_json(db1b)], "expect_change": [[True, False, False]],
+         "check_links": {n1: [L3], n2: [L2], n3: [L2, L3]}},
+        {"delete": n1, "expect_change": [True, False, False],
+         "check_links": {n1: [], n2: [L2], n3: [L2]}},
+    ],
+    "checks": [],
+})
+
+# ---------------- DecisionTest.cpp ----------------
+R = {}
+R["adj12"] = create_adjacency("2", "1/2", "2/1", "fe80::2", "192.168.0.2", 10, 100002)
+R["adj13"] = create_adjacency("3", "1/3", "3/1", "fe80::3", "192.168.0.3", 10, 100003)
+R["adj21"] = create_adjacency("1", "2/1", "1/2", "fe80::1", "192.168.0.1", 10, 100001)
+R["adj23"] = create_adjacency("3", "2/3", "3/2", "fe80::3", "192.168.0.3", 10, 100003)
+R["adj24"] = create_adjacency("4", "2/4", "4/2", "fe80::4", "192.168.0.4", 10, 100004)
+R["adj31"] = create_adjacency("1", "3/1", "1/3", "fe80::1", "192.168.0.1", 10, 100001)
+R["adj32"] = create_adjacency("2", "3/2", "2/3", "fe80::2", "192.168.0.2", 10, 100002)
+R["adj34"] = create_adjacency("4", "3/4", "4/3", "fe80::4", "192.168.0.4", 10, 100004)
+R["adj42"] = create_adjacency("2", "4/2", "2/4", "fe80::2", "192.168.0.2", 10, 100002)
+R["adj43"] = create_adjacency("3", "4/3", "3/4", "fe80::3", "192.168.0.3", 10, 100003)
+ring = [create_adj_db("1", [R["adj12"], R["adj13"]], 1),
+        create_adj_db("2", [R["adj21"], R["adj24"]], 2),
+        create_adj_db("3", [R["adj31"], R["adj34"]], 3),
+        create_adj_db("4", [R["adj42"], R["adj43"]], 4)]
+ring_steps = [{"update": [db_json(d) for d in ring],
+               "expect_change": [[False, False, True], [True, False, True],
+                                 [True, False, True], [True, False, True]]}]
+cases.append({
+    "name": "decision_simple_ring",
+    "cite": "DecisionTest.cpp:1687-1944 (SimpleRingTopologyFixture, ShortestPathTest)",
+    "steps": ring_steps,
+    "checks": [
+        spf("1", {"1": (0, []), "2": (10, ["2"]), "3": (10, ["3"]), "4": (20, ["2", "3"])},
+            "DecisionTest.cpp:1828-1847"),
+        spf("2", {"2": (0, []), "4": (10, ["4"]), "3": (20, ["1", "4"]), "1": (10, ["1"])},
+            "DecisionTest.cpp:1852-1870"),
+        spf("3", {"3": (0, []), "4": (10, ["4"]), "2": (20, ["1", "4"]), "1": (10, ["1"])},
+            "DecisionTest.cpp:1875-1893"),
+        spf("4", {"4": (0, []), "3": (10, ["3"]), "2": (10, ["2"]), "1": (20, ["2", "3"])},
+            "DecisionTest.cpp:1898-1916"),
+        {"type": "spf_runs_all_nodes", "expect": 4, "cite": "DecisionTest.cpp:1825-1827"},
+        {"type": "ksp2_runs_all_pairs", "expect": 16, "cite": "DecisionTest.cpp:2305-2309"},
+    ],
+})
+db3a = create_adj_db("3", [create_adjacency("1", "3/1", "1/3", "fe80::1", "192.168.0.1", 10, 100001),
+                           R["adj34"]], 3)
+db3a.adjacencies[0].isOverloaded = True
+db3b = create_adj_db("3", [create_adjacency("1", "3/1", "1/3", "fe80::1", "192.168.0.1", 10, 100001),
+                           create_adjacency("4", "3/4", "4/3", "fe80::4", "192.168.0.4", 10, 100004)], 3)
+db3b.adjacencies[0].isOverloaded = True
+db3b.adjacencies[1].isOverloaded = True
+cases.append({
+    "name": "decision_ring_overload_link",
+    "cite": "DecisionTest.cpp:2936-3117 (SimpleRingTopologyFixture, OverloadLinkTest)",
+    "steps": ring_steps + [
+        {"update": [db_json(db3a)], "expect_change": [[True, False, False]]},
+        {"checks": [
+            spf("1", {"4": (20, ["2"]), "3": (30, ["2"]), "2": (10, ["2"])},
+                "DecisionTest.cpp:2951-2968", exact=False),
+            spf("2", {"4": (10, ["4"]), "3": (20, ["4"]), "1": (10, ["1"])},
+                "DecisionTest.cpp:2973-2991", exact=False),
+            spf("3", {"4": (10, ["4"]), "2": (20, ["4"]), "1": (30, ["4"])},
+                "DecisionTest.cpp:2996-3014", exact=False),
+            spf("4", {"3": (10, ["3"]), "2": (10, ["2"]), "1": (20, ["2"])},
+                "DecisionTest.cpp:3019-3037", exact=False),
+        ]},
+        {"update": [db_json(db3b)], "expect_change": [[True, False, False]]},
+        {"checks": [
+            spf("1", {"1": (0, []), "4": (20, ["2"]), "2": (10, ["2"])},
+                "DecisionTest.cpp:3055-3066 (node 3 disconnected)"),
+            spf("2", {"2": (0, []), "4": (10, ["4"]), "1": (10, ["1"])},
+                "DecisionTest.cpp:3071-3082"),
+            spf("3", {"3": (0, [])}, "DecisionTest.cpp:3084-3085 (no routes for node 3)"),
+            spf("4", {"4": (0, []), "2": (10, ["2"]), "1": (20, ["2"])},
+                "DecisionTest.cpp:3095-3106"),
+        ]},
+    ],
+    "checks": [],
+})
+line = [create_adj_db("1", [R["adj12"]], 1),
+        create_adj_db("2", [R["adj21"], R["adj23"]], 2, True),
+        create_adj_db("3", [R["adj32"]], 3)]
+cases.append({
+    "name": "decision_connectivity_overload_node",
+    "cite": "DecisionTest.cpp:1279-1375 (ConnectivityTest, OverloadNodeTest)",
+    "steps": [{"update": [db_json(d) for d in line],
+               "expect_change": [[False, False, True], [True, False, True], [True, False, True]]}],
+    "checks": [
+        spf("1", {"1": (0, []), "2": (10, ["2"])}, "DecisionTest.cpp:1325-1334"),
+        spf("2", {"2": (0, []), "1": (10, ["1"]), "3": (10, ["3"])}, "DecisionTest.cpp:1339-1356"),
+        spf("3", {"3": (0, []), "2": (10, ["2"])}, "DecisionTest.cpp:1361-1370"),
+    ],
+})
+cases.append({
+    "name": "decision_partitioned",
+    "cite": "DecisionTest.cpp:1214-1277 (ConnectivityTest, partitioned=true)",
+    "steps": [{"update": [db_json(create_adj_db("1", [], 1)),
+                          db_json(create_adj_db("2", [R["adj21"], R["adj23"]], 2)),
+                          db_json(create_adj_db("3", [], 3))],
+               "expect_change": [[False, False, True], [False, False, True],
+                                 [False, False, True]]}],
+    "checks": [spf("1", {"1": (0, [])}, "DecisionTest.cpp:1275-1276 (no route 1 -> 3)")],
+})
+cases.append({
+    "name": "decision_connected",
+    "cite": "DecisionTest.cpp:1214-1277 (ConnectivityTest, partitioned=false)",
+    "steps": [{"update": [db_json(create_adj_db("1", [R["adj12"]], 1)),
+                          db_json(create_adj_db("2", [R["adj21"], R["adj23"]], 2)),
+                          db_json(create_adj_db("3", [R["adj32"]], 3))],
+               "expect_change": [[False, False, True], [True, False, True],
+                                 [True, False, True]]}],
+    "checks": [spf("1", {"1": (0, []), "2": (10, ["2"]), "3": (20, ["2"])},
+                   "DecisionTest.cpp:1275-1276 (route 1 -> 3 exists)")],
+})
+cases.append({
+    "name": "decision_missing_neighbor_db",
+    "cite": "DecisionTest.cpp:444-474, 476-510 (Missing/EmptyNeighborAdjacencyDb)",
+    "steps": [{"update": [db_json(create_adj_db("1", [R["adj12"]], 0)),
+                          db_json(create_adj_db("2", [], 0))],
+               "expect_change": [[False, False, False], [False, False, False]]}],
+    "checks": [spf("1", {"1": (0, [])}, "DecisionTest.cpp:467-473"),
+               spf("2", {"2": (0, [])}, "DecisionTest.cpp:505-509")],
+})
+cases.append({
+    "name": "decision_unknown_node",
+    "cite": "DecisionTest.cpp:512-529 (UnknownNode: empty LinkState)",
+    "steps": [],
+    "checks": [spf("1", {"1": (0, [])}, "LinkState.cpp:818-825 (source always recorded)")],
+})
+
+P = {}
+P["adj12_1"] = create_adjacency("2", "2/1", "1/1", "fe80::2:1", "192.168.2.1", 11, 201)
+P["adj12_2"] = create_adjacency("2", "2/2", "1/2", "fe80::2:2", "192.168.2.2", 11, 202)
+P["adj12_3"] = create_adjacency("2", "2/3", "1/3", "fe80::2:3", "192.168.2.3", 20, 203)
+P["adj13_1"] = create_adjacency("3", "3/1", "1/1", "fe80::3:1", "192.168.3.1", 11, 301)
+P["adj21_1"] = create_adjacency("1", "1/1", "2/1", "fe80::1:1", "192.168.1.1", 11, 101)
+P["adj21_2"] = create_adjacency("1", "1/2", "2/2", "fe80::1:2", "192.168.1.2", 11, 102)
+P["adj21_3"] = create_adjacency("1", "1/3", "2/3", "fe80::1:3", "192.168.1.3", 20, 103)
+P["adj24_1"] = create_adjacency("4", "4/1", "2/1", "fe80::4:1", "192.168.4.1", 11, 401)
+P["adj31_1"] = create_adjacency("1", "1/1", "3/1", "fe80::1:1", "192.168.1.1", 11, 101)
+P["adj34_1"] = create_adjacency("4", "4/1", "3/1", "fe80::4:1", "192.168.4.1", 11, 401)
+P["adj34_2"] = create_adjacency("4", "4/2", "3/2", "fe80::4:2", "192.168.4.2", 20, 402)
+P["adj34_3"] = create_adjacency("4", "4/3", "3/3", "fe80::4:3", "192.168.4.3", 20, 403)
+P["adj42_1"] = create_adjacency("2", "2/1", "4/1", "fe80::2:1", "192.168.2.1", 11, 201)
+P["adj43_1"] = create_adjacency("3", "3/1", "4/1", "fe80::3:1", "192.168.3.1", 11, 301)
+P["adj43_2"] = create_adjacency("3", "3/2", "4/2", "fe80::3:2", "192.168.3.2", 20, 302)
+P["adj43_3"] = create_adjacency("3", "3/3", "4/3", "fe80::3:3", "192.168.3.3", 20, 303)
+par = [create_adj_db("1", [P["adj12_1"], P["adj12_2"], P["adj12_3"], P["adj13_1"]], 1),
+       create_adj_db("2", [P["adj21_1"], P["adj21_2"], P["adj21_3"], P["adj24_1"]], 2),
+       create_adj_db("3", [P["adj31_1"], P["adj34_1"], P["adj34_2"], P["adj34_3"]], 3),
+       create_adj_db("4", [P["adj42_1"], P["adj43_1"], P["adj43_2"], P["adj43_3"]], 4)]
+cases.append({
+    "name": "decision_parallel_adj_ring",
+    "cite": "DecisionTest.cpp:3120-3250 (ParallelAdjRingTopologyFixture)",
+    "steps": [{"update": [db_json(d) for d in par],
+               "expect_change": [[False, False, True], [True, False, True],
+                                 [True, False, True], [True, False, True]]}],
+    "checks": [
+        spf("1", {"1": (0, []), "4": (22, ["2", "3"]), "3": (11, ["3"]), "2": (11, ["2"])},
+            "DecisionTest.cpp:3262-3282"),
+        spf("2", {"2": (0, []), "4": (11, ["4"]), "3": (22, ["1", "4"]), "1": (11, ["1"])},
+            "DecisionTest.cpp:3288-3308"),
+        spf("3", {"3": (0, []), "4": (11, ["4"]), "2": (22, ["1", "4"]), "1": (11, ["1"])},
+            "DecisionTest.cpp:3313-3333"),
+        spf("4", {"4": (0, []), "3": (11, ["3"]), "2": (11, ["2"]), "1": (22, ["2", "3"])},
+            "DecisionTest.cpp:3338-3358"),
+        # KSP2 tie-break among parallel links: node 1's first hops on the k=1
+        # edge-disjoint paths to 4 are adj12_2 (ifName "2/2") and adj13_1 ("3/1")
+        {"type": "kth_first_hop_ifaces", "src": "1", "dst": "4", "k": 1,
+         "expect": ["2/2", "3/1"], "cite": "DecisionTest.cpp:3583-3599"},
+    ],
+})
+for n in range(2, 17, 2):
+    cases.append({
+        "name": f"decision_grid_{n}",
+        "cite": "DecisionTest.cpp:4301-4355 (GridTopologyFixture, n in Range(2,17,2))",
+        "grid": n,
+        "steps": [],
+        "checks": [{"type": "grid_manhattan", "n": n,
+                    "cite": "DecisionTest.cpp:4283-4290 gridDistance; :4318-4354"}],
+    })
+
+out = HERE / "reference_expectations.json"
+out.write_text(json.dumps({"source": "fredxia/openr openr/decision/tests", "cases": cases},
+                          indent=1, sort_keys=False))
+print(f"wrote {out} ({len(cases)} cases)")

@@ -1,0 +1,71 @@
+"""Shared test helpers: fixture builders that mirror the reference's test utils."""
+
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple, Union
+
+from openr_amd.lsdb import AdjacencyDatabase, create_adj_db, create_adjacency
+
+# libstdc++ _Prime_rehash_policy::_M_next_bkt fast path (hashtable_c++0x.cc)
+_FAST_BKT = [2, 2, 2, 3, 5, 5, 7, 7, 11, 11, 11, 11, 13, 13]
+
+
+def libstdcxx_int_map_order(keys: Sequence[int]) -> List[int]:
+    """Iteration order of ``std::unordered_map<int, T>`` built from an
+    initializer list holding ``keys`` in this order (libstdc++, identity
+    std::hash<int>, max_load_factor 1).  Exact for fewer than 14 keys, where
+    the constructor's bucket count (_M_next_bkt fast path) never rehashes."""
+    n = len(keys)
+    if n >= len(_FAST_BKT):
+        raise ValueError("emulation covers maps with < 14 keys")
+    nb = _FAST_BKT[n]
+    order: List[int] = []
+    for k in keys:
+        b = k % nb
+        idx = next((i for i, x in enumerate(order) if x % nb == b), None)
+        # a node goes first in its bucket's run; a new bucket's run goes first
+        order.insert(0 if idx is None else idx, k)
+    return order
+
+
+def get_link_state_dbs(
+    adj_map: Dict[int, Sequence[Union[int, Tuple[int, int]]]]
+) -> List[AdjacencyDatabase]:
+    """Adjacency databases in the order ``getLinkState`` applies them
+    (reference openr/decision/tests/DecisionTestUtils.cpp:16-44): integer node
+    names, ifName ``node/adj/k`` (k-th parallel adjacency), label
+    ``(node << 16) + adj``, fe80::/192.168 addresses from the neighbour id."""
+    dbs = []
+    for node in libstdcxx_int_map_order(list(adj_map.keys())):
+        assert node < (1 << 16)
+        adjs = []
+        num_parallel: Dict[int, int] = {}
+        for entry in adj_map[node]:
+            adj, weight = (entry, 1) if isinstance(entry, int) else entry
+            k = num_parallel.get(adj, 0)
+            num_parallel[adj] = k + 1
+            bottom, top = adj & 0xFF, (adj & 0xFF00) >> 8
+            adjs.append(create_adjacency(
+                str(adj), f"{node}/{adj}/{k}", f"{adj}/{node}/{k}",
+                f"fe80::{top:02x}{bottom:02x}", f"192.168.{top}.{bottom}", weight,
+                (node << 16) + adj))
+        dbs.append(create_adj_db(str(node), adjs, node))
+    return dbs
+
+
+def link_key(link) -> list:
+    """Canonical [n1, if1, n2, if2] (ordered names) of a product Link."""
+    (a, b), (c, d) = link.orderedNames
+    return [a, b, c, d]
+
+
+def spf_canonical(res) -> dict:
+    """Product SpfResult -> the oracle's JSON shape."""
+    return {
+        node: {
+            "metric": r.metric(),
+            "nextHops": sorted(r.nextHops()),
+            "pathLinks": [[link_key(pl.link), pl.prevNode] for pl in r.pathLinks()],
+        }
+        for node, r in sorted(res.items())
+    }

@@ -1,0 +1,127 @@
+"""Engine parity on the MI355X: batched all-sources SPF + ECMP (libopenr_spf.so)
+against the CPU oracle, bit-exact.
+
+Small graphs: every source, full dist + next-hop bitsets.  Full BASELINE sizes
+(fabric 10k, grid 100x100): sampled sources compared exactly, plus
+size-independent properties over ALL sources of one batched plan.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import OracleLinkState
+from openr_amd import topology as T
+from openr_amd.engine import SpfEngine, graph_from_lsdb
+
+pytestmark = pytest.mark.gpu
+
+U32_INF = np.uint32(0xFFFFFFFF)
+
+
+def load(topo):
+    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+    eng = SpfEngine(0)
+    eng.load(rp, col, met, lid, ovl)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    return names, eng, orc
+
+
+def compare(names, eng, orc, srcs, hop=False):
+    res = eng.solve(srcs, hop=hop)
+    dist, nh, off, words = orc.dense(names, srcs, ulm=not hop, pitch=eng.pitch)
+    exp = np.where(dist == np.iinfo(np.uint64).max, U32_INF, dist).astype(np.uint32)
+    assert np.array_equal(res.dist, exp), "distance mismatch"
+    assert np.array_equal(res.words, words)
+    assert np.array_equal(res.nh_off, off)
+    for i in range(len(srcs)):
+        w = int(words[i])
+        o = int(off[i])
+        for j in range(w):
+            a = res.nh[o + j * eng.pitch: o + j * eng.pitch + len(names)]
+            b = nh[o + j * eng.pitch: o + j * eng.pitch + len(names)]
+            if not np.array_equal(a, b):
+                bad = int(np.nonzero(a != b)[0][0])
+                raise AssertionError(f"next-hop mismatch src {names[srcs[i]]} dst {names[bad]} "
+                                     f"word {j}: {a[bad]:#x} vs {b[bad]:#x}")
+    return res
+
+
+SMALL = [
+    ("grid10", lambda: T.grid(10)),
+    ("dtgrid8", lambda: T.decision_test_grid(8)),
+    ("fabric_ref1000", lambda: T.fabric(1000, full=False)),
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("wan300", lambda: T.wan(300, 150, seed=3)),
+] + [
+    (f"rand{seed}", (lambda s: lambda: T.random_graph(
+        60, 150, s, max_metric=8, parallel_frac=0.2, overload_frac=0.1,
+        link_overload_frac=0.05))(seed))
+    for seed in range(6)
+]
+
+
+@pytest.mark.parametrize("name,make", SMALL, ids=[s[0] for s in SMALL])
+@pytest.mark.parametrize("hop", [False, True], ids=["metric", "hops"])
+def test_all_sources_exact(name, make, hop):
+    names, eng, orc = load(make())
+    compare(names, eng, orc, list(range(len(names))), hop=hop)
+
+
+def test_subset_and_duplicates_exact():
+    """Non-closed source sets (engine adds neighbour rows internally),
+    duplicates and a single source."""
+    names, eng, orc = load(T.random_graph(50, 120, 11, overload_frac=0.15))
+    rng = np.random.default_rng(0)
+    for srcs in ([7], [3, 3, 9], list(rng.choice(len(names), 13, replace=False))):
+        compare(names, eng, orc, [int(s) for s in srcs])
+
+
+def test_all_overloaded_and_isolated():
+    topo = T.random_graph(30, 40, 5, overload_frac=0.9)
+    names, eng, orc = load(topo)
+    compare(names, eng, orc, list(range(len(names))))
+
+
+@pytest.mark.parametrize("which", ["fabric_full", "grid100"])
+def test_baseline_size_sampled_exact_and_all_sources_properties(which):
+    topo = T.fabric(10000, full=True) if which == "fabric_full" else T.grid(100)
+    names, eng, orc = load(topo)
+    n = len(names)
+    rng = np.random.default_rng(1)
+    sample = sorted(int(x) for x in rng.choice(n, 6, replace=False))
+    compare(names, eng, orc, sample)
+    # all sources in one batched plan: properties that hold for any source
+    res = eng.solve(list(range(n)))
+    d = res.dist
+    assert (d.diagonal() == 0).all()
+    assert (d != U32_INF).all()  # connected
+    assert np.array_equal(d, d.T)  # unit symmetric metrics, nothing drained
+    # rows of the batch equal the same sources solved alone
+    for s in sample:
+        one = eng.solve([s])
+        assert np.array_equal(one.dist[0], d[s])
+        assert np.array_equal(one.nh_bits(0), res.nh_bits(s))
+    # next hops: empty only at the source, and x in nh_s(v) => d(s,x)=1 & d(x,v)=d(s,v)-1
+    for s in sample:
+        bits = res.nh_bits(s)
+        nbrs = eng.neighbors(s)
+        has = bits.any(axis=1)
+        assert not has[s] and has[np.arange(n) != s].all()
+        for j, x in enumerate(nbrs):
+            sel = (bits[:, j // 32] >> (j % 32)) & 1
+            v = np.nonzero(sel)[0]
+            assert (d[x, v] + 1 == d[s, v]).all()
+
+
+def test_zero_metric_is_rejected_loudly():
+    from openr_amd._native import UnsupportedInput
+
+    topo = T.random_graph(20, 30, 2)
+    topo.lsdb.adjs["metric"][0] = 0
+    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+    eng = SpfEngine(0)
+    eng.load(rp, col, met, lid, ovl)
+    with pytest.raises(UnsupportedInput):
+        eng.solve([0])
+    eng.solve([0], hop=True)  # hop counts ignore metrics: fine
