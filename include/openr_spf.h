@@ -26,7 +26,7 @@
  *     path (max metric x (n_nodes-1)) does not fit; such graphs are out of
  *     scope for this engine (SPF_E_UNSUPPORTED).
  *   - Row pitch: dist and next-hop rows are stored with pitch
- *     spf_row_pitch() = n_nodes rounded up to a multiple of 4.
+ *     spf_row_pitch() = n_nodes rounded up to a multiple of 16.
  *
  * Errors: every call returns spf_status; spf_last_error() describes the last
  * failure.  No exceptions cross the ABI.  All calls on one context must come

@@ -46,7 +46,6 @@ namespace {
 constexpr uint32_t kInf = SPF_UNREACHABLE;
 constexpr int kSsspThreads = 256;
 constexpr int kEcmpThreads = 256;
-constexpr int kVecPerThread = 4;  // nodes per thread in the ECMP pass (16 B)
 constexpr uint32_t kBigDeg = 24;  // > kBigDeg: expanded by a whole wave
 constexpr size_t kMaxLds = 160 * 1024;
 
@@ -196,6 +195,141 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
 }
 
 // ---------------------------------------------------------------------------
+//  1b. multi-source BFS for unit metrics: 64 sources per workgroup
+// ---------------------------------------------------------------------------
+// Every node carries a 64-bit mask, bit s = "source s of this batch".  A level
+// is one pull sweep: new(v) = OR_{u in N(v)} F(u) & ~visited(v), where F holds
+// the previous level's new masks, restricted for drained nodes to their own
+// source bit (a drained node is recorded but expands only as the source,
+// LinkState.cpp:831-838).  One edge sweep serves 64 sources, against 64 sweeps
+// for the per-source kernel.  F lives in LDS (8 B/node); visited and new masks
+// of the nodes a thread owns (v = tid + i*1024) live in registers.
+// Distances are written per level as predicated stores: for a wave-uniform
+// source s, the 64 lanes own 64 consecutive nodes, so the store to D[s][v..v+63]
+// is one coalesced 256 B segment.
+constexpr int kMsThreads = 1024;
+constexpr uint32_t kMsBatch = 64;
+constexpr int kMsMaxOwn = 16;
+constexpr uint32_t kMsMaxNodes = kMsThreads * kMsMaxOwn;  // 16384 (F: 128 KiB of LDS)
+
+template <int OWN, typename NT>
+__global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
+    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+    const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
+    uint32_t n_rows, uint32_t N, uint32_t pitch, uint32_t* __restrict__ D,
+    NT* __restrict__ Dn /* narrow copy, same pitch, may be null */) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* F = reinterpret_cast<uint64_t*>(smem);           // [N]
+  uint32_t* obm = reinterpret_cast<uint32_t*>(F + N);        // [ceil(N/32)] drained bitmap
+  uint32_t* o_node = obm + ((N + 31) >> 5);                  // [64] drained batch sources
+  uint32_t* o_cnt = o_node + kMsBatch;                       // [1]
+  uint32_t* flag = o_cnt + 1;                                // [2] per-parity "progress"
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t row0 = blockIdx.x * kMsBatch;
+  const uint32_t nb = min(kMsBatch, n_rows - row0);
+  const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+  constexpr NT kNInf = (NT)~(NT)0;
+
+  for (uint32_t v = tid; v < N; v += kMsThreads) F[v] = 0;
+  for (uint32_t i = tid; i < ((N + 31) >> 5); i += kMsThreads) obm[i] = 0;
+  if (tid == 0) {
+    *o_cnt = 0;
+    flag[0] = flag[1] = 0;
+  }
+  __syncthreads();
+  for (uint32_t v = tid; v < N; v += kMsThreads)
+    if (ovl[v]) atomicOr(&obm[v >> 5], 1u << (v & 31));
+  if (tid < nb) {
+    const uint32_t src = rows_src[row0 + tid];
+    atomicOr(reinterpret_cast<unsigned long long*>(&F[src]), 1ull << tid);
+    if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
+  }
+  __syncthreads();
+  const uint32_t n_ovl_src = *o_cnt;
+
+  uint64_t vis[OWN], nv[OWN];
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const uint32_t v = tid + i * kMsThreads;
+    nv[i] = v < N ? F[v] : 0ull;
+    vis[i] = nv[i];
+  }
+
+  for (uint32_t L = 0;; ++L) {
+    // ---- record level L: D[s][v] = L for every new (s, v) ----
+    for (uint32_t s = 0; s < nb; ++s) {
+      uint32_t* drow = D + (size_t)(row0 + s) * pitch;
+      NT* nrow = Dn ? Dn + (size_t)(row0 + s) * pitch : nullptr;
+#pragma unroll
+      for (int i = 0; i < OWN; ++i) {
+        const uint32_t v = tid + i * kMsThreads;
+        if ((nv[i] >> s) & 1ull) {
+          drow[v] = L;
+          if (nrow) nrow[v] = (NT)min<uint32_t>(L, (uint32_t)(NT)(kNInf - 1));
+        }
+      }
+    }
+    // ---- pull sweep for level L+1 ----
+    uint64_t any = 0;
+    uint64_t nx[OWN];
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const uint32_t v = tid + i * kMsThreads;
+      nx[i] = 0;
+      if (v < N && vis[i] != all) {
+        uint64_t acc = 0;
+        const uint32_t e1 = row_ptr[v + 1];
+        for (uint32_t e = row_ptr[v]; e < e1; ++e) {
+          const uint32_t u = col[e];
+          uint64_t f = F[u];
+          if (f && ((obm[u >> 5] >> (u & 31)) & 1u)) {
+            // drained u expands only for its own source bit (if in batch)
+            uint64_t own = 0;
+            for (uint32_t k = 0; k < n_ovl_src; ++k)
+              if ((o_node[k] & 0xFFFFFFu) == u) own = 1ull << (o_node[k] >> 24);
+            f &= own;
+          }
+          acc |= f;
+        }
+        nx[i] = acc & ~vis[i];
+        vis[i] |= nx[i];
+        any |= nx[i];
+      }
+    }
+    __syncthreads();  // every read of F for this level is done
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const uint32_t v = tid + i * kMsThreads;
+      if (v < N) F[v] = nx[i];
+      nv[i] = nx[i];
+    }
+    if (any) flag[L & 1] = 1;
+    if (tid == 0) flag[(L + 1) & 1] = 0;
+    __syncthreads();
+    if (!flag[L & 1]) break;
+  }
+  // ---- unreachable (s, v) pairs ----
+  for (uint32_t s = 0; s < nb; ++s) {
+    uint32_t* drow = D + (size_t)(row0 + s) * pitch;
+    NT* nrow = Dn ? Dn + (size_t)(row0 + s) * pitch : nullptr;
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const uint32_t v = tid + i * kMsThreads;
+      if (v < N && !((vis[i] >> s) & 1ull)) {
+        drow[v] = kInf;
+        if (nrow) nrow[v] = kNInf;
+      }
+    }
+    // row padding
+    for (uint32_t v = N + tid; v < pitch; v += kMsThreads) {
+      drow[v] = kInf;
+      if (nrow) nrow[v] = kNInf;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 //  2. next-hop (ECMP) pass
 // ---------------------------------------------------------------------------
 // Bijective XCD-aware remap: dispatch deals blocks round-robin over 8 XCDs
@@ -208,15 +342,66 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
 }
 
 constexpr uint32_t kNbTile = 256;  // neighbours staged in LDS per tile
+constexpr int kEcmpUnroll = 8;      // independent row loads in flight per thread
 
+// 16 bytes of a distance row: 16 / sizeof(DT) packed elements, kept packed in
+// 4 VGPRs and extracted on use.
+template <typename DT>
+struct Vec16 {
+  static constexpr int N = 16 / sizeof(DT);
+  uint4 raw;
+  __device__ __forceinline__ uint32_t get(int q) const {
+    const uint32_t w = (&raw.x)[(q * (int)sizeof(DT)) >> 2];
+    if constexpr (sizeof(DT) == 4) {
+      return w;
+    } else {
+      constexpr uint32_t mask = (1u << (8 * sizeof(DT))) - 1u;
+      return (w >> ((q * 8 * (int)sizeof(DT)) & 31)) & mask;
+    }
+  }
+  // does any element equal `val`? (SWAR zero-element test)
+  __device__ __forceinline__ bool any_eq(uint32_t val) const {
+    if constexpr (sizeof(DT) == 4) {
+      return raw.x == val || raw.y == val || raw.z == val || raw.w == val;
+    } else {
+      constexpr uint32_t ones = sizeof(DT) == 1 ? 0x01010101u : 0x00010001u;
+      constexpr uint32_t high = sizeof(DT) == 1 ? 0x80808080u : 0x80008000u;
+      const uint32_t pat = val * ones;
+      uint32_t hit = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = (&raw.x)[k] ^ pat;
+        hit |= (x - ones) & ~x & high;
+      }
+      return hit != 0;
+    }
+  }
+};
+
+template <typename DT>
+__device__ __forceinline__ Vec16<DT> load16(const DT* p) {
+  Vec16<DT> r;
+  r.raw = *reinterpret_cast<const uint4*>(p);
+  return r;
+}
+
+// DT = element type of the distance matrix the pass reads: u32 (the output
+// itself) or the u8 narrow copy written by the multi-source BFS (saturated at
+// 254; such entries are decided on the exact u32 row Dw).
+template <typename DT>
 __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
-    const uint32_t* __restrict__ D, uint32_t pitch, uint32_t N,
+    const DT* __restrict__ D, uint32_t dpitch, uint32_t N, uint32_t pitch,
+    const uint32_t* __restrict__ Dw,
     const uint32_t* __restrict__ req_src, const uint32_t* __restrict__ row_of,
     const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
     const uint32_t* __restrict__ nb_w, const uint8_t* __restrict__ ovl,
     uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
     uint32_t chunks, uint32_t n_blocks) {
-  __shared__ uint32_t s_row[kNbTile];  // row index of neighbour, or kInf if overloaded
+  constexpr int VEC = Vec16<DT>::N;
+  constexpr uint32_t kDInf = (uint32_t)(DT)~(DT)0;
+  constexpr uint32_t kSat = kDInf - 1u;
+  constexpr bool kNarrow = sizeof(DT) < 4;
+  __shared__ uint32_t s_row[kNbTile];  // row of neighbour, or kInf if drained
   __shared__ uint32_t s_w[kNbTile];
   __shared__ uint32_t s_id[kNbTile];
 
@@ -226,12 +411,14 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
   const uint32_t s = req_src[i];
   const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
   if (k == 0) return;  // isolated source: no next-hop words at all
-  const uint32_t words = (k + 31) >> 5;
-  const uint32_t v0 = (c * kEcmpThreads + threadIdx.x) * kVecPerThread;
+  const uint32_t v0 = (c * kEcmpThreads + threadIdx.x) * VEC;
   const bool active = v0 < N;
+  const uint32_t srow = row_of[s];
 
-  uint4 ds = make_uint4(kInf, kInf, kInf, kInf);
-  if (active) ds = *reinterpret_cast<const uint4*>(D + (size_t)row_of[s] * pitch + v0);
+  Vec16<DT> ds;
+  ds.raw = make_uint4(~0u, ~0u, ~0u, ~0u);
+  if (active) ds = load16(D + (size_t)srow * dpitch + v0);
+  const bool ds_sat = kNarrow && ds.any_eq(kSat);
   uint32_t* out = nh + nh_off[i] + v0;
 
   for (uint32_t t0 = 0; t0 < k; t0 += kNbTile) {
@@ -245,41 +432,62 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     }
     __syncthreads();
     for (uint32_t w0 = 0; w0 < tk; w0 += 32) {
-      uint4 bits = make_uint4(0, 0, 0, 0);
+      uint32_t bits[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) bits[q] = 0;
       const uint32_t wn = min(32u, tk - w0);
-      for (uint32_t jj = 0; jj < wn; ++jj) {
-        const uint32_t j = w0 + jj;
-        const uint32_t wj = s_w[j];
-        const uint32_t rj = s_row[j];
-        uint4 m;
-        if (rj == kInf) {
-          // drained neighbour: only the direct route to itself
-          const uint32_t x = s_id[j];
-          m.x = (v0 + 0 == x) & (ds.x == wj);
-          m.y = (v0 + 1 == x) & (ds.y == wj);
-          m.z = (v0 + 2 == x) & (ds.z == wj);
-          m.w = (v0 + 3 == x) & (ds.w == wj);
-        } else {
-          uint4 dx = make_uint4(kInf, kInf, kInf, kInf);
-          if (active) dx = *reinterpret_cast<const uint4*>(D + (size_t)rj * pitch + v0);
-          m.x = (dx.x != kInf) & (dx.x + wj == ds.x);
-          m.y = (dx.y != kInf) & (dx.y + wj == ds.y);
-          m.z = (dx.z != kInf) & (dx.z + wj == ds.z);
-          m.w = (dx.w != kInf) & (dx.w + wj == ds.w);
+      // kEcmpUnroll neighbour rows per batch: issue all loads, then consume
+      for (uint32_t jb = 0; jb < wn; jb += kEcmpUnroll) {
+        Vec16<DT> dx[kEcmpUnroll];
+#pragma unroll
+        for (int u = 0; u < kEcmpUnroll; ++u) {
+          const uint32_t rj = (jb + u < wn) ? s_row[w0 + jb + u] : kInf;
+          dx[u].raw = make_uint4(~0u, ~0u, ~0u, ~0u);
+          if (active && rj != kInf) dx[u] = load16(D + (size_t)rj * dpitch + v0);
         }
-        bits.x |= m.x << jj;
-        bits.y |= m.y << jj;
-        bits.z |= m.z << jj;
-        bits.w |= m.w << jj;
+#pragma unroll
+        for (int u = 0; u < kEcmpUnroll; ++u) {
+          const uint32_t jj = jb + u;
+          if (jj >= wn) break;
+          const uint32_t j = w0 + jj;
+          const uint32_t wj = s_w[j];
+          const uint32_t rj = s_row[j];
+          if (rj == kInf) {
+            // drained neighbour: only the direct route to itself
+            const uint32_t x = s_id[j];
+            if (x >= v0 && x < v0 + VEC) {
+#pragma unroll
+              for (int q = 0; q < VEC; ++q)
+                if (v0 + q == x && ds.get(q) != kDInf && ds.get(q) == wj) bits[q] |= 1u << jj;
+            }
+            continue;
+          }
+          if (kNarrow && (ds_sat || dx[u].any_eq(kSat))) {
+            // saturated narrow entries: decide on the exact u32 distances
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+              const uint32_t da = Dw[(size_t)rj * pitch + v0 + q];
+              const uint32_t db = Dw[(size_t)srow * pitch + v0 + q];
+              bits[q] |= (uint32_t)(da != kInf && db != kInf && da + wj == db) << jj;
+            }
+            continue;
+          }
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            const uint32_t a = dx[u].get(q), b = ds.get(q);
+            bits[q] |= (uint32_t)(a != kDInf && b != kDInf && a + wj == b) << jj;
+          }
+        }
       }
-      // unreachable nodes have an empty set (ds == INF never matches)
       if (active) {
         const uint32_t wd = (t0 + w0) >> 5;
-        *reinterpret_cast<uint4*>(out + (size_t)wd * pitch) = bits;
+        uint4* o = reinterpret_cast<uint4*>(out + (size_t)wd * pitch);
+#pragma unroll
+        for (int q = 0; q < VEC / 4; ++q)
+          o[q] = make_uint4(bits[4 * q], bits[4 * q + 1], bits[4 * q + 2], bits[4 * q + 3]);
       }
     }
   }
-  (void)words;
 }
 
 // ---------------------------------------------------------------------------
@@ -394,6 +602,7 @@ struct spf_ctx {
   std::vector<uint32_t> nb_ptr, nb_id, nb_w;  // distinct up neighbours
   uint32_t big_nodes = 0;                    // nodes with degree > kBigDeg
   uint32_t max_link = 0;
+  bool unit = false;                         // every up edge has metric 1
   DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
   DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
@@ -408,7 +617,9 @@ struct spf_plan {
   std::vector<uint32_t> words;
   uint64_t nh_total = 0;
   bool direct = false;  // closure == srcs: D is the caller's dist buffer
+  bool ms = false;      // unit metrics: multi-source BFS + u8 narrow copy
   DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
+  DevBuf<uint8_t> d_Dn;
   DevBuf<uint64_t> d_nh_off;
   size_t lds_bytes = 0;
   bool q16 = true;
@@ -506,7 +717,7 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   c->loaded = false;
   c->N = N;
   c->E = E;
-  c->pitch = (N + 3) & ~3u;
+  c->pitch = (N + 15) & ~15u;  // 16-byte rows for u8 vector access
   c->row_ptr.assign(g->row_ptr, g->row_ptr + N + 1);
   c->col.assign(g->col, g->col + E);
   c->link.assign(g->link_id, g->link_id + E);
@@ -525,6 +736,7 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     c->wt[e] = m > 0 ? (uint32_t)m : 0u;
     c->max_metric = std::max(c->max_metric, c->wt[e]);
   }
+  c->unit = !c->nonpos && c->max_metric <= 1;
   if ((uint64_t)c->max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf)
     return fail(c, SPF_E_UNSUPPORTED,
                 "max metric %u x %u hops overflows 32-bit distances", c->max_metric, N - 1);
@@ -675,6 +887,8 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
+  p->ms = (hop || c->unit) && N <= kMsMaxNodes;
+  if (p->ms) HIP_TRY(c, p->d_Dn.alloc((size_t)p->closure.size() * c->pitch));
   {
     const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
     if (st != SPF_OK) return st;
@@ -725,11 +939,54 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
   return SPF_OK;
 }
 
+size_t msbfs_lds_bytes(uint32_t N) {
+  return 8ull * N + 4ull * ((N + 31) / 32) + 4ull * (kMsBatch + 4);
+}
+
+template <int OWN>
+void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
+                  hipStream_t s) {
+  hipLaunchKernelGGL((msbfs_kernel<OWN, uint8_t>), dim3((rows + kMsBatch - 1) / kMsBatch),
+                     dim3(kMsThreads), msbfs_lds_bytes(c->N), s, c->d_row_ptr.p, c->d_col.p,
+                     c->d_ovl.p, rows_src, rows, c->N, c->pitch, D, Dn);
+}
+
+spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
+                        uint8_t* Dn, hipStream_t s) {
+  const uint32_t own = (c->N + kMsThreads - 1) / kMsThreads;
+  if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, s);
+  else msbfs_launch<16>(c, rows_src, rows, D, Dn, s);
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
+template <typename DT>
+spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const DT* Dsrc, const uint32_t* Dw, bool hop,
+                       uint32_t* d_nh, hipStream_t s) {
+  constexpr uint32_t vec = 16 / sizeof(DT);
+  const uint32_t chunks = (c->N + kEcmpThreads * vec - 1) / (kEcmpThreads * vec);
+  const uint32_t nb = chunks * p->n_src;
+  hipLaunchKernelGGL((ecmp_kernel<DT>), dim3(nb), dim3(kEcmpThreads), 0, s, Dsrc, c->pitch, c->N,
+                     c->pitch, Dw, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
+                     c->d_nb_w.p, c->d_ovl.p, hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, nb);
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
 spf_status set_lds_limits(spf_ctx* c) {
   static bool done = false;
   if (done) return SPF_OK;
   const void* fns[] = {(const void*)sssp_kernel<uint16_t, true>, (const void*)sssp_kernel<uint16_t, false>,
-                       (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>};
+                       (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>,
+                       (const void*)msbfs_kernel<1, uint8_t>, (const void*)msbfs_kernel<2, uint8_t>,
+                       (const void*)msbfs_kernel<4, uint8_t>, (const void*)msbfs_kernel<8, uint8_t>,
+                       (const void*)msbfs_kernel<10, uint8_t>, (const void*)msbfs_kernel<12, uint8_t>,
+                       (const void*)msbfs_kernel<16, uint8_t>};
   for (const void* f : fns)
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
   done = true;
@@ -760,7 +1017,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   if (!d_dist || (p->nh_total && !d_nh))
     return fail(c, SPF_E_INVALID, "spf_plan_execute: NULL output buffer");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  const uint32_t N = c->N, pitch = c->pitch;
+  const uint32_t pitch = c->pitch;
   const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
   uint32_t* D = p->direct ? d_dist : p->d_D.p;
   const uint32_t rows = (uint32_t)p->closure.size();
@@ -770,16 +1027,14 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     ++p->timing_n;
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
-  spf_status st = launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
+  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->d_Dn.p, s)
+                        : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   if (p->nh_total) {
-    const uint32_t chunks = (N + kEcmpThreads * kVecPerThread - 1) / (kEcmpThreads * kVecPerThread);
-    const uint32_t nb = chunks * p->n_src;
-    hipLaunchKernelGGL(ecmp_kernel, dim3(nb), dim3(kEcmpThreads), 0, s, D, pitch, N, p->d_srcs.p,
-                       p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, c->d_ovl.p,
-                       hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, nb);
-    HIP_TRY(c, hipGetLastError());
+    st = p->ms ? launch_ecmp<uint8_t>(c, p, p->d_Dn.p, D, hop, d_nh, s)
+               : launch_ecmp<uint32_t>(c, p, D, D, hop, d_nh, s);
+    if (st != SPF_OK) return st;
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
   if (!p->direct) {
