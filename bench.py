@@ -47,10 +47,10 @@ def build_workload(name: str, rank: int):
         desc = "grid 100x100 (RoutingBenchmarkUtils.cpp:161-240)"
     else:
         raise SystemExit(f"unknown workload {name}")
-    if rank > 0:
-        # rank r's snapshot: one node drained, as BM_Decision* toggles per iteration
-        victim = (rank * 7919) % topo.n_nodes
-        topo.lsdb.dbs["is_overloaded"][victim] = 1
+    from openr_amd.sharding import snapshot_for_rank
+
+    # rank r's snapshot: one node drained, as BM_Decision* toggles per iteration
+    topo.lsdb = snapshot_for_rank(topo.lsdb, rank)
     return topo, desc
 
 
