@@ -26,7 +26,7 @@
  *     path (max metric x (n_nodes-1)) does not fit; such graphs are out of
  *     scope for this engine (SPF_E_UNSUPPORTED).
  *   - Row pitch: dist and next-hop rows are stored with pitch
- *     spf_row_pitch() = n_nodes rounded up to a multiple of 16.
+ *     spf_row_pitch() = n_nodes rounded up to a multiple of 64.
  *
  * Errors: every call returns spf_status; spf_last_error() describes the last
  * failure.  No exceptions cross the ABI.  All calls on one context must come
@@ -92,9 +92,11 @@ spf_status spf_src_neighbors(const spf_ctx* ctx, uint32_t src, uint32_t* out,
                              uint32_t cap, uint32_t* count);
 
 /* ---- plans: a fixed batch of sources, executable many times ------------- */
-/* Next-hop layout of source i of the plan: words_i = ceil(k_i/32) 32-bit words
- * per node (k_i = #distinct up neighbours), stored word-planar:
- *   bit j of node v  ->  nh[nh_off[i] + (j/32)*pitch + v]  bit (j%32). */
+/* Next-hop layout of source i of the plan: one destination bitmap per
+ * distinct up neighbour (k_i bitmaps, neighbours in ascending id), each of
+ * pitch/32 32-bit words:
+ *   neighbour j in nextHops(v)  <=>  nh[nh_off[i] + j*(pitch/32) + v/32] bit (v%32).
+ * spf_plan_nh_layout reports nh_off[i] and k_i ("words" = bitmaps). */
 spf_status spf_plan_create(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
                            uint32_t flags, spf_plan** out);
 void spf_plan_destroy(spf_plan* plan);

@@ -502,7 +502,8 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
     std::vector<uint32_t> nbr(k);
     spf_src_neighbors(ls->eng, s, nbr.data(), k, &k);
     const uint32_t pitch = spf_row_pitch(ls->eng);
-    const uint64_t words = (uint64_t)((k + 31) / 32) * pitch;
+    const uint32_t wpm = pitch / 32;  // u32 words per destination bitmap
+    const uint64_t words = (uint64_t)k * wpm;
     m.dist.resize(N);
     std::vector<uint32_t> nh(std::max<uint64_t>(words, 1));
     st = spf_solve(ls->eng, &s, 1, flags, m.dist.data(), nh.data());
@@ -519,8 +520,8 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
       if (m.dist[v] == SPF_UNREACHABLE) continue;
       m.node.push_back(ls->csr_name[v]);
       m.metric.push_back(m.dist[v]);
-      for (uint32_t j = 0; j < k; ++j)
-        if ((nh[(size_t)(j >> 5) * pitch + v] >> (j & 31)) & 1u)
+      for (uint32_t j = 0; j < k; ++j)  // bitmap j: destinations routed via neighbour j
+        if ((nh[(size_t)j * wpm + (v >> 5)] >> (v & 31)) & 1u)
           m.nh_node.push_back(ls->csr_name[nbr[j]]);
       m.nh_ptr.push_back((uint32_t)m.nh_node.size());
       for (uint32_t p = m.pred_ptr[v]; p < m.pred_ptr[v + 1]; ++p) {

@@ -199,74 +199,101 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
 // ---------------------------------------------------------------------------
 // Every node carries a 64-bit mask, bit s = "source s of this batch".  A level
 // is one pull sweep: new(v) = OR_{u in N(v)} F(u) & ~visited(v), where F holds
-// the previous level's new masks, restricted for drained nodes to their own
-// source bit (a drained node is recorded but expands only as the source,
-// LinkState.cpp:831-838).  One edge sweep serves 64 sources, against 64 sweeps
-// for the per-source kernel.  F lives in LDS (8 B/node); visited and new masks
-// of the nodes a thread owns (v = tid + i*1024) live in registers.
-// Distances are written per level as predicated stores: for a wave-uniform
-// source s, the 64 lanes own 64 consecutive nodes, so the store to D[s][v..v+63]
-// is one coalesced 256 B segment.
+// the previous level's new masks.  A drained node is recorded but expands only
+// as the source (LinkState.cpp:831-838): its producer writes F(v) masked to its
+// own source bit, so the consumer loop is branch-free.  One edge sweep serves
+// 64 sources, against 64 sweeps for the per-source kernel.
+//   * F lives in LDS (8 B/node, F[N] = 0 is the padding target).
+//   * visited / new masks of the nodes a thread owns (v = tid + i*1024) live in
+//     registers; the 64 lanes of a wave own 64 consecutive nodes = one slice
+//     of the sliced-ELL column array, so neighbour j of all 64 nodes is one
+//     coalesced 256-byte load (kMsUnroll of them in flight).
+//   * distances are written per level as predicated stores over the sources
+//     that have new nodes in the wave; one store covers 64 consecutive nodes
+//     of one source row.  The u8 narrow copy for the next-hop pass saturates at
+//     254 and is stored lane-interleaved (narrow_pos).
 constexpr int kMsThreads = 1024;
 constexpr uint32_t kMsBatch = 64;
 constexpr int kMsMaxOwn = 16;
 constexpr uint32_t kMsMaxNodes = kMsThreads * kMsMaxOwn;  // 16384 (F: 128 KiB of LDS)
+constexpr int kMsUnroll = 8;
+constexpr uint32_t kSliceW = 64;  // nodes per sliced-ELL slice (= wave width)
 
-template <int OWN, typename NT>
+// Narrow (u8) distance rows: npitch bytes (a multiple of 1024).  Within a
+// 1024-node chunk, node q*64 + l (q = 0..15, l = 0..63) is byte l*16 + q, so a
+// 16-byte load by lane l returns nodes {q*64 + l} of the chunk: byte q of every
+// lane forms one 64-node ballot, i.e. one u64 word of a destination bitmap.
+__host__ __device__ __forceinline__ uint32_t narrow_pos(uint32_t v) {
+  return (v & ~1023u) | ((v & 63u) << 4) | ((v >> 6) & 15u);
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    lo |= __shfl_xor(lo, d, 64);
+    hi |= __shfl_xor(hi, d, 64);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int OWN>
 __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
-    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+    const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
-    uint32_t n_rows, uint32_t N, uint32_t pitch, uint32_t* __restrict__ D,
-    NT* __restrict__ Dn /* narrow copy, same pitch, may be null */) {
+    uint32_t n_rows, uint32_t N, uint32_t pitch, uint32_t npitch,
+    uint32_t* __restrict__ D, uint8_t* __restrict__ Dn) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint64_t* F = reinterpret_cast<uint64_t*>(smem);           // [N]
-  uint32_t* obm = reinterpret_cast<uint32_t*>(F + N);        // [ceil(N/32)] drained bitmap
-  uint32_t* o_node = obm + ((N + 31) >> 5);                  // [64] drained batch sources
-  uint32_t* o_cnt = o_node + kMsBatch;                       // [1]
-  uint32_t* flag = o_cnt + 1;                                // [2] per-parity "progress"
+  uint64_t* F = reinterpret_cast<uint64_t*>(smem);             // [N + 1]
+  uint32_t* o_node = reinterpret_cast<uint32_t*>(F + N + 1);   // [64] drained batch sources
+  uint32_t* o_cnt = o_node + kMsBatch;                         // [1]
+  uint32_t* flag = o_cnt + 1;                                  // [2] per-parity progress
 
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t row0 = blockIdx.x * kMsBatch;
   const uint32_t nb = min(kMsBatch, n_rows - row0);
   const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-  constexpr NT kNInf = (NT)~(NT)0;
 
-  for (uint32_t v = tid; v < N; v += kMsThreads) F[v] = 0;
-  for (uint32_t i = tid; i < ((N + 31) >> 5); i += kMsThreads) obm[i] = 0;
+  for (uint32_t v = tid; v <= N; v += kMsThreads) F[v] = 0;
   if (tid == 0) {
     *o_cnt = 0;
     flag[0] = flag[1] = 0;
   }
   __syncthreads();
-  for (uint32_t v = tid; v < N; v += kMsThreads)
-    if (ovl[v]) atomicOr(&obm[v >> 5], 1u << (v & 31));
   if (tid < nb) {
     const uint32_t src = rows_src[row0 + tid];
-    atomicOr(reinterpret_cast<unsigned long long*>(&F[src]), 1ull << tid);
+    F[src] = 1ull << tid;  // sources of a batch are distinct
     if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
   }
   __syncthreads();
-  const uint32_t n_ovl_src = *o_cnt;
+  const uint32_t n_osrc = *o_cnt;
 
   uint64_t vis[OWN], nv[OWN];
+  uint32_t drained = 0;  // bit i: owned node i is drained
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     const uint32_t v = tid + i * kMsThreads;
     nv[i] = v < N ? F[v] : 0ull;
     vis[i] = nv[i];
+    if (v < N && ovl[v]) drained |= 1u << i;
   }
 
   for (uint32_t L = 0;; ++L) {
     // ---- record level L: D[s][v] = L for every new (s, v) ----
-    for (uint32_t s = 0; s < nb; ++s) {
+    uint64_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) mine |= nv[i];
+    const uint32_t nl = min(L, 254u);
+    for (uint64_t m = wave_or64(mine); m; m &= m - 1) {
+      const uint32_t s = __ffsll((unsigned long long)m) - 1;
       uint32_t* drow = D + (size_t)(row0 + s) * pitch;
-      NT* nrow = Dn ? Dn + (size_t)(row0 + s) * pitch : nullptr;
+      uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
 #pragma unroll
       for (int i = 0; i < OWN; ++i) {
         const uint32_t v = tid + i * kMsThreads;
         if ((nv[i] >> s) & 1ull) {
           drow[v] = L;
-          if (nrow) nrow[v] = (NT)min<uint32_t>(L, (uint32_t)(NT)(kNInf - 1));
+          nrow[narrow_pos(v)] = (uint8_t)nl;
         }
       }
     }
@@ -275,33 +302,45 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     uint64_t nx[OWN];
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
-      const uint32_t v = tid + i * kMsThreads;
       nx[i] = 0;
-      if (v < N && vis[i] != all) {
+      const uint32_t v = tid + i * kMsThreads;
+      const bool need = v < N && vis[i] != all;
+      if (__ballot(need)) {  // wave-uniform: the slice has unfinished nodes
+        const uint32_t slice = v / kSliceW;
+        const uint32_t b = sell_ptr[slice];
+        const uint32_t w = (sell_ptr[slice + 1] - b) / kSliceW;
+        const uint32_t* cp = sell_col + b + lane;
         uint64_t acc = 0;
-        const uint32_t e1 = row_ptr[v + 1];
-        for (uint32_t e = row_ptr[v]; e < e1; ++e) {
-          const uint32_t u = col[e];
-          uint64_t f = F[u];
-          if (f && ((obm[u >> 5] >> (u & 31)) & 1u)) {
-            // drained u expands only for its own source bit (if in batch)
-            uint64_t own = 0;
-            for (uint32_t k = 0; k < n_ovl_src; ++k)
-              if ((o_node[k] & 0xFFFFFFu) == u) own = 1ull << (o_node[k] >> 24);
-            f &= own;
-          }
-          acc |= f;
+        uint32_t j = 0;
+        for (; j + kMsUnroll <= w; j += kMsUnroll) {
+          uint32_t c[kMsUnroll];
+#pragma unroll
+          for (int u = 0; u < kMsUnroll; ++u) c[u] = cp[(j + u) * kSliceW];
+#pragma unroll
+          for (int u = 0; u < kMsUnroll; ++u) acc |= F[c[u]];
         }
-        nx[i] = acc & ~vis[i];
-        vis[i] |= nx[i];
-        any |= nx[i];
+        for (; j < w; ++j) acc |= F[cp[j * kSliceW]];
+        if (need) {
+          nx[i] = acc & ~vis[i];
+          vis[i] |= nx[i];
+          any |= nx[i];
+        }
       }
     }
     __syncthreads();  // every read of F for this level is done
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = tid + i * kMsThreads;
-      if (v < N) F[v] = nx[i];
+      if (v < N) {
+        uint64_t f = nx[i];
+        if ((drained >> i) & 1u) {  // drained: expands only as its own source
+          uint64_t own = 0;
+          for (uint32_t k = 0; k < n_osrc; ++k)
+            if ((o_node[k] & 0xFFFFFFu) == v) own = 1ull << (o_node[k] >> 24);
+          f &= own;
+        }
+        F[v] = f;
+      }
       nv[i] = nx[i];
     }
     if (any) flag[L & 1] = 1;
@@ -309,22 +348,30 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     __syncthreads();
     if (!flag[L & 1]) break;
   }
-  // ---- unreachable (s, v) pairs ----
-  for (uint32_t s = 0; s < nb; ++s) {
+  // ---- unreachable (s, v) pairs and row padding ----
+  uint64_t miss = 0;
+#pragma unroll
+  for (int i = 0; i < OWN; ++i)
+    if (tid + i * kMsThreads < N) miss |= ~vis[i] & all;
+  for (uint64_t m = wave_or64(miss); m; m &= m - 1) {
+    const uint32_t s = __ffsll((unsigned long long)m) - 1;
     uint32_t* drow = D + (size_t)(row0 + s) * pitch;
-    NT* nrow = Dn ? Dn + (size_t)(row0 + s) * pitch : nullptr;
+    uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = tid + i * kMsThreads;
       if (v < N && !((vis[i] >> s) & 1ull)) {
         drow[v] = kInf;
-        if (nrow) nrow[v] = kNInf;
+        nrow[narrow_pos(v)] = 0xFF;
       }
     }
-    // row padding
-    for (uint32_t v = N + tid; v < pitch; v += kMsThreads) {
-      drow[v] = kInf;
-      if (nrow) nrow[v] = kNInf;
+  }
+  for (uint32_t s = 0; s < nb; ++s) {
+    uint32_t* drow = D + (size_t)(row0 + s) * pitch;
+    uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
+    for (uint32_t v = N + tid; v < npitch; v += kMsThreads) {
+      if (v < pitch) drow[v] = kInf;
+      nrow[narrow_pos(v)] = 0xFF;
     }
   }
 }
@@ -332,75 +379,42 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 // ---------------------------------------------------------------------------
 //  2. next-hop (ECMP) pass
 // ---------------------------------------------------------------------------
-// Bijective XCD-aware remap: dispatch deals blocks round-robin over 8 XCDs
-// (b and b+8 share one); give each XCD a contiguous run of virtual blocks so
-// consecutive sources -- which share neighbour rows -- meet in one L2.
+// Output: per source, one destination bitmap per distinct up neighbour x
+// (ascending id): bit v of bitmap j <=> neighbour j is in nh_s(v).  Each wave
+// owns a 1024-destination chunk; for neighbour x it forms 16 ballots -- one
+// per 64 destinations -- and stores them as 32 consecutive u32 words.
+//   NARROW: distances from the lane-interleaved u8 copy (one 16-byte load per
+//           lane per neighbour, target = d_s(v) - 1 precomputed); a wave whose
+//           source row holds a saturated entry (>= 254) decides on the exact
+//           u32 rows instead.
+//   exact:  u32 rows, one coalesced dword load per 64 destinations.
+// Blocks are remapped so each XCD walks a contiguous source range (sources
+// that share neighbours -- e.g. the racks of one pod -- meet in one L2).
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
   const uint32_t xcd = b & 7, pos = b >> 3;
   const uint32_t q = nb >> 3, r = nb & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
 }
 
-constexpr uint32_t kNbTile = 256;  // neighbours staged in LDS per tile
-constexpr int kEcmpUnroll = 8;      // independent row loads in flight per thread
+constexpr uint32_t kNbTile = 256;      // neighbours staged in LDS per tile
+constexpr int kEcmpUnroll = 4;         // neighbour rows in flight per wave
+constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
+constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
 
-// 16 bytes of a distance row: 16 / sizeof(DT) packed elements, kept packed in
-// 4 VGPRs and extracted on use.
-template <typename DT>
-struct Vec16 {
-  static constexpr int N = 16 / sizeof(DT);
-  uint4 raw;
-  __device__ __forceinline__ uint32_t get(int q) const {
-    const uint32_t w = (&raw.x)[(q * (int)sizeof(DT)) >> 2];
-    if constexpr (sizeof(DT) == 4) {
-      return w;
-    } else {
-      constexpr uint32_t mask = (1u << (8 * sizeof(DT))) - 1u;
-      return (w >> ((q * 8 * (int)sizeof(DT)) & 31)) & mask;
-    }
-  }
-  // does any element equal `val`? (SWAR zero-element test)
-  __device__ __forceinline__ bool any_eq(uint32_t val) const {
-    if constexpr (sizeof(DT) == 4) {
-      return raw.x == val || raw.y == val || raw.z == val || raw.w == val;
-    } else {
-      constexpr uint32_t ones = sizeof(DT) == 1 ? 0x01010101u : 0x00010001u;
-      constexpr uint32_t high = sizeof(DT) == 1 ? 0x80808080u : 0x80008000u;
-      const uint32_t pat = val * ones;
-      uint32_t hit = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t x = (&raw.x)[k] ^ pat;
-        hit |= (x - ones) & ~x & high;
-      }
-      return hit != 0;
-    }
-  }
-};
-
-template <typename DT>
-__device__ __forceinline__ Vec16<DT> load16(const DT* p) {
-  Vec16<DT> r;
-  r.raw = *reinterpret_cast<const uint4*>(p);
-  return r;
+// Lane t (< 32) of the wave keeps dword t of the 16 ballots (q = t / 2).
+__device__ __forceinline__ uint32_t put_mask(uint32_t out, uint64_t m, int q, uint32_t lane) {
+  const uint32_t pick = (lane & 1u) ? (uint32_t)(m >> 32) : (uint32_t)m;
+  return (lane >> 1) == (uint32_t)q ? pick : out;
 }
 
-// DT = element type of the distance matrix the pass reads: u32 (the output
-// itself) or the u8 narrow copy written by the multi-source BFS (saturated at
-// 254; such entries are decided on the exact u32 row Dw).
-template <typename DT>
+template <bool NARROW>
 __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
-    const DT* __restrict__ D, uint32_t dpitch, uint32_t N, uint32_t pitch,
-    const uint32_t* __restrict__ Dw,
-    const uint32_t* __restrict__ req_src, const uint32_t* __restrict__ row_of,
-    const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
-    const uint32_t* __restrict__ nb_w, const uint8_t* __restrict__ ovl,
-    uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
-    uint32_t chunks, uint32_t n_blocks) {
-  constexpr int VEC = Vec16<DT>::N;
-  constexpr uint32_t kDInf = (uint32_t)(DT)~(DT)0;
-  constexpr uint32_t kSat = kDInf - 1u;
-  constexpr bool kNarrow = sizeof(DT) < 4;
+    const uint8_t* __restrict__ Dn, uint32_t npitch, const uint32_t* __restrict__ D,
+    uint32_t pitch, uint32_t N, const uint32_t* __restrict__ req_src,
+    const uint32_t* __restrict__ row_of, const uint32_t* __restrict__ nb_ptr,
+    const uint32_t* __restrict__ nb_id, const uint32_t* __restrict__ nb_w,
+    const uint8_t* __restrict__ ovl, uint32_t hop, const uint64_t* __restrict__ nh_off,
+    uint32_t* __restrict__ nh, uint32_t chunks, uint32_t n_blocks) {
   __shared__ uint32_t s_row[kNbTile];  // row of neighbour, or kInf if drained
   __shared__ uint32_t s_w[kNbTile];
   __shared__ uint32_t s_id[kNbTile];
@@ -410,16 +424,39 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
   const uint32_t c = vb - i * chunks;
   const uint32_t s = req_src[i];
   const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
-  if (k == 0) return;  // isolated source: no next-hop words at all
-  const uint32_t v0 = (c * kEcmpThreads + threadIdx.x) * VEC;
-  const bool active = v0 < N;
+  if (k == 0) return;  // isolated source: no bitmaps at all
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t cbase = (c * kEcmpWaves + (threadIdx.x >> 6)) * kEcmpChunk;
+  const bool live = cbase < N;  // wave-uniform
   const uint32_t srow = row_of[s];
+  const uint32_t wpm = pitch / 32;  // u32 words per bitmap
+  uint32_t* out_base = nh + nh_off[i] + cbase / 32 + lane;
+  const bool store_lane = lane < 32 && cbase / 32 + lane < wpm;
 
-  Vec16<DT> ds;
-  ds.raw = make_uint4(~0u, ~0u, ~0u, ~0u);
-  if (active) ds = load16(D + (size_t)srow * dpitch + v0);
-  const bool ds_sat = kNarrow && ds.any_eq(kSat);
-  uint32_t* out = nh + nh_off[i] + v0;
+  // source distances of this lane's 16 destinations (cbase + q*64 + lane)
+  uint32_t b[16];
+  uint32_t tgt[16];  // NARROW: the u8 value a neighbour must hold, 0x100 = none
+  bool exact = !NARROW;
+  if (live) {
+    if (NARROW) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(Dn + (size_t)srow * npitch + cbase + lane * 16);
+      bool sat = false;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t x = ((&raw.x)[q >> 2] >> ((q & 3) * 8)) & 0xFFu;
+        sat |= x == 0xFEu;
+        tgt[q] = (x == 0u || x >= 0xFEu) ? 0x100u : x - 1u;  // unit metric: d_x = d_s - 1
+      }
+      exact = __ballot(sat) != 0;
+    }
+    if (exact) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t v = cbase + q * 64 + lane;
+        b[q] = v < N ? D[(size_t)srow * pitch + v] : kInf;
+      }
+    }
+  }
 
   for (uint32_t t0 = 0; t0 < k; t0 += kNbTile) {
     const uint32_t tk = min(kNbTile, k - t0);
@@ -431,61 +468,60 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
       s_row[j] = ovl[x] ? kInf : row_of[x];
     }
     __syncthreads();
-    for (uint32_t w0 = 0; w0 < tk; w0 += 32) {
-      uint32_t bits[VEC];
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) bits[q] = 0;
-      const uint32_t wn = min(32u, tk - w0);
-      // kEcmpUnroll neighbour rows per batch: issue all loads, then consume
-      for (uint32_t jb = 0; jb < wn; jb += kEcmpUnroll) {
-        Vec16<DT> dx[kEcmpUnroll];
+    if (!live) continue;
+    uint32_t* out = out_base + (size_t)t0 * wpm;
+    if (!exact) {
+      // fast path: kEcmpUnroll neighbour rows in flight; a drained neighbour's
+      // row reads as "unreachable" (0xFF never equals a target) and its single
+      // possible bit is patched below
+      for (uint32_t j0 = 0; j0 < tk; j0 += kEcmpUnroll) {
+        uint4 raw[kEcmpUnroll];
 #pragma unroll
         for (int u = 0; u < kEcmpUnroll; ++u) {
-          const uint32_t rj = (jb + u < wn) ? s_row[w0 + jb + u] : kInf;
-          dx[u].raw = make_uint4(~0u, ~0u, ~0u, ~0u);
-          if (active && rj != kInf) dx[u] = load16(D + (size_t)rj * dpitch + v0);
+          const uint32_t rj = j0 + u < tk ? s_row[j0 + u] : kInf;
+          raw[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+          if (rj != kInf)
+            raw[u] = *reinterpret_cast<const uint4*>(Dn + (size_t)rj * npitch + cbase + lane * 16);
         }
 #pragma unroll
         for (int u = 0; u < kEcmpUnroll; ++u) {
-          const uint32_t jj = jb + u;
-          if (jj >= wn) break;
-          const uint32_t j = w0 + jj;
-          const uint32_t wj = s_w[j];
-          const uint32_t rj = s_row[j];
-          if (rj == kInf) {
-            // drained neighbour: only the direct route to itself
-            const uint32_t x = s_id[j];
-            if (x >= v0 && x < v0 + VEC) {
+          if (j0 + u >= tk) break;
+          uint32_t word = 0;
 #pragma unroll
-              for (int q = 0; q < VEC; ++q)
-                if (v0 + q == x && ds.get(q) != kDInf && ds.get(q) == wj) bits[q] |= 1u << jj;
-            }
-            continue;
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t a = ((&raw[u].x)[q >> 2] >> ((q & 3) * 8)) & 0xFFu;
+            word = put_mask(word, __ballot(a == tgt[q]), q, lane);
           }
-          if (kNarrow && (ds_sat || dx[u].any_eq(kSat))) {
-            // saturated narrow entries: decide on the exact u32 distances
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) {
-              const uint32_t da = Dw[(size_t)rj * pitch + v0 + q];
-              const uint32_t db = Dw[(size_t)srow * pitch + v0 + q];
-              bits[q] |= (uint32_t)(da != kInf && db != kInf && da + wj == db) << jj;
-            }
-            continue;
-          }
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) {
-            const uint32_t a = dx[u].get(q), b = ds.get(q);
-            bits[q] |= (uint32_t)(a != kDInf && b != kDInf && a + wj == b) << jj;
-          }
+          if (store_lane) out[(size_t)(j0 + u) * wpm] = word;
         }
       }
-      if (active) {
-        const uint32_t wd = (t0 + w0) >> 5;
-        uint4* o = reinterpret_cast<uint4*>(out + (size_t)wd * pitch);
+    } else {
+      for (uint32_t j = 0; j < tk; ++j) {
+        const uint32_t rj = s_row[j], wj = s_w[j];
+        uint32_t word = 0;
+        if (rj != kInf) {
+          uint32_t a[16];
 #pragma unroll
-        for (int q = 0; q < VEC / 4; ++q)
-          o[q] = make_uint4(bits[4 * q], bits[4 * q + 1], bits[4 * q + 2], bits[4 * q + 3]);
+          for (int q = 0; q < 16; ++q) {
+            const uint32_t v = cbase + q * 64 + lane;
+            a[q] = v < N ? D[(size_t)rj * pitch + v] : kInf;
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            word = put_mask(word, __ballot(a[q] != kInf && b[q] != kInf && a[q] + wj == b[q]), q,
+                            lane);
+        }
+        if (store_lane) out[(size_t)j * wpm] = word;
       }
+    }
+    // drained neighbour x: its bitmap is empty except, possibly, x itself --
+    // reached directly over the link when d_s(x) == w(s, x)
+    for (uint32_t j = 0; j < tk; ++j) {
+      if (s_row[j] != kInf) continue;
+      const uint32_t x = s_id[j];
+      if (x < cbase || x >= cbase + kEcmpChunk) continue;
+      if (lane == (x - cbase) / 32 && D[(size_t)srow * pitch + x] == s_w[j])
+        out[(size_t)j * wpm] = 1u << (x & 31);
     }
   }
 }
@@ -603,6 +639,9 @@ struct spf_ctx {
   uint32_t big_nodes = 0;                    // nodes with degree > kBigDeg
   uint32_t max_link = 0;
   bool unit = false;                         // every up edge has metric 1
+  uint32_t npitch = 0;                       // narrow (u8) row pitch
+  std::vector<uint32_t> sell_ptr, sell_col;  // sliced-ELL columns (64-node slices)
+  DevBuf<uint32_t> d_sell_ptr, d_sell_col;
   DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
   DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
@@ -717,7 +756,8 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   c->loaded = false;
   c->N = N;
   c->E = E;
-  c->pitch = (N + 15) & ~15u;  // 16-byte rows for u8 vector access
+  c->pitch = (N + 63) & ~63u;      // dist rows / bitmap rows: whole u64 words
+  c->npitch = (N + 1023) & ~1023u;  // narrow rows: whole 1024-node chunks
   c->row_ptr.assign(g->row_ptr, g->row_ptr + N + 1);
   c->col.assign(g->col, g->col + E);
   c->link.assign(g->link_id, g->link_id + E);
@@ -794,6 +834,27 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   HIP_TRY(c, c->d_nb_ptr.upload(c->nb_ptr.data(), N + 1, c->stream));
   HIP_TRY(c, c->d_nb_id.upload(c->nb_id.data(), c->nb_id.size(), c->stream));
   HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  // sliced ELL (SELL-64): slice = 64 consecutive nodes, width = max degree in
+  // the slice, entry (slice, j, lane) = j-th neighbour of node slice*64+lane,
+  // padded with N (F[N] == 0 in the BFS kernel)
+  {
+    const uint32_t n_slices = (N + kSliceW - 1) / kSliceW;
+    c->sell_ptr.assign(n_slices + 1, 0);
+    for (uint32_t sl = 0; sl < n_slices; ++sl) {
+      uint32_t w = 0;
+      for (uint32_t v = sl * kSliceW; v < std::min(N, (sl + 1) * kSliceW); ++v)
+        w = std::max(w, c->row_ptr[v + 1] - c->row_ptr[v]);
+      c->sell_ptr[sl + 1] = c->sell_ptr[sl] + w * kSliceW;
+    }
+    c->sell_col.assign(c->sell_ptr[n_slices], N);
+    for (uint32_t v = 0; v < N; ++v) {
+      const uint32_t sl = v / kSliceW, ln = v % kSliceW;
+      for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j)
+        c->sell_col[c->sell_ptr[sl] + j * kSliceW + ln] = c->col[c->row_ptr[v] + j];
+    }
+    HIP_TRY(c, c->d_sell_ptr.upload(c->sell_ptr.data(), c->sell_ptr.size(), c->stream));
+    HIP_TRY(c, c->d_sell_col.upload(c->sell_col.data(), c->sell_col.size(), c->stream));
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->loaded = true;
   return SPF_OK;
@@ -873,9 +934,9 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   uint64_t off = 0;
   for (uint32_t i = 0; i < n_src; ++i) {
     const uint32_t k = c->nb_ptr[srcs[i] + 1] - c->nb_ptr[srcs[i]];
-    p->words[i] = (k + 31) / 32;
+    p->words[i] = k;  // one destination bitmap per distinct up neighbour
     p->nh_off[i] = off;
-    off += (uint64_t)p->words[i] * c->pitch;
+    off += (uint64_t)k * (c->pitch / 32);
   }
   p->nh_total = off;
   p->q16 = N <= 65535;
@@ -888,7 +949,7 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
-  if (p->ms) HIP_TRY(c, p->d_Dn.alloc((size_t)p->closure.size() * c->pitch));
+  if (p->ms) HIP_TRY(c, p->d_Dn.alloc((size_t)p->closure.size() * c->npitch));
   {
     const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
     if (st != SPF_OK) return st;
@@ -939,16 +1000,14 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
   return SPF_OK;
 }
 
-size_t msbfs_lds_bytes(uint32_t N) {
-  return 8ull * N + 4ull * ((N + 31) / 32) + 4ull * (kMsBatch + 4);
-}
+size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 4); }
 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
                   hipStream_t s) {
-  hipLaunchKernelGGL((msbfs_kernel<OWN, uint8_t>), dim3((rows + kMsBatch - 1) / kMsBatch),
-                     dim3(kMsThreads), msbfs_lds_bytes(c->N), s, c->d_row_ptr.p, c->d_col.p,
-                     c->d_ovl.p, rows_src, rows, c->N, c->pitch, D, Dn);
+  hipLaunchKernelGGL((msbfs_kernel<OWN>), dim3((rows + kMsBatch - 1) / kMsBatch), dim3(kMsThreads),
+                     msbfs_lds_bytes(c->N), s, c->d_sell_ptr.p, c->d_sell_col.p, c->d_ovl.p,
+                     rows_src, rows, c->N, c->pitch, c->npitch, D, Dn);
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
@@ -965,14 +1024,14 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
   return SPF_OK;
 }
 
-template <typename DT>
-spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const DT* Dsrc, const uint32_t* Dw, bool hop,
+template <bool NARROW>
+spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_t* D, bool hop,
                        uint32_t* d_nh, hipStream_t s) {
-  constexpr uint32_t vec = 16 / sizeof(DT);
-  const uint32_t chunks = (c->N + kEcmpThreads * vec - 1) / (kEcmpThreads * vec);
+  const uint32_t per_block = kEcmpChunk * kEcmpWaves;
+  const uint32_t chunks = (c->N + per_block - 1) / per_block;
   const uint32_t nb = chunks * p->n_src;
-  hipLaunchKernelGGL((ecmp_kernel<DT>), dim3(nb), dim3(kEcmpThreads), 0, s, Dsrc, c->pitch, c->N,
-                     c->pitch, Dw, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
+  hipLaunchKernelGGL((ecmp_kernel<NARROW>), dim3(nb), dim3(kEcmpThreads), 0, s, Dn, c->npitch, D,
+                     c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
                      c->d_nb_w.p, c->d_ovl.p, hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, nb);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
@@ -983,10 +1042,10 @@ spf_status set_lds_limits(spf_ctx* c) {
   if (done) return SPF_OK;
   const void* fns[] = {(const void*)sssp_kernel<uint16_t, true>, (const void*)sssp_kernel<uint16_t, false>,
                        (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>,
-                       (const void*)msbfs_kernel<1, uint8_t>, (const void*)msbfs_kernel<2, uint8_t>,
-                       (const void*)msbfs_kernel<4, uint8_t>, (const void*)msbfs_kernel<8, uint8_t>,
-                       (const void*)msbfs_kernel<10, uint8_t>, (const void*)msbfs_kernel<12, uint8_t>,
-                       (const void*)msbfs_kernel<16, uint8_t>};
+                       (const void*)msbfs_kernel<1>, (const void*)msbfs_kernel<2>,
+                       (const void*)msbfs_kernel<4>, (const void*)msbfs_kernel<8>,
+                       (const void*)msbfs_kernel<10>, (const void*)msbfs_kernel<12>,
+                       (const void*)msbfs_kernel<16>};
   for (const void* f : fns)
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
   done = true;
@@ -1032,8 +1091,8 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   if (p->nh_total) {
-    st = p->ms ? launch_ecmp<uint8_t>(c, p, p->d_Dn.p, D, hop, d_nh, s)
-               : launch_ecmp<uint32_t>(c, p, D, D, hop, d_nh, s);
+    st = p->ms ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
+               : launch_ecmp<false>(c, p, nullptr, D, hop, d_nh, s);
     if (st != SPF_OK) return st;
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));

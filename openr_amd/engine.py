@@ -25,17 +25,23 @@ UNREACHABLE = N.SPF_UNREACHABLE
 @dataclass
 class SolveResult:
     dist: np.ndarray  # [n_src, n_nodes] uint32 (UNREACHABLE)
-    nh: np.ndarray  # planar next-hop words (see nh_bits)
-    nh_off: np.ndarray  # [n_src] uint64 word offset of each source
-    words: np.ndarray  # [n_src] words per node (= ceil(#neighbours / 32))
+    nh: np.ndarray  # destination bitmaps, one per (source, neighbour)
+    nh_off: np.ndarray  # [n_src] uint64 word offset of each source's bitmaps
+    words: np.ndarray  # [n_src] number of bitmaps (= distinct up neighbours)
     pitch: int
 
-    def nh_bits(self, i: int) -> np.ndarray:
-        """[n_nodes, words_i] next-hop words of source i."""
-        w = int(self.words[i])
-        n = self.dist.shape[1]
-        o = int(self.nh_off[i])
-        return self.nh[o: o + w * self.pitch].reshape(w, self.pitch)[:, :n].T.copy()
+    def nh_matrix(self, i: int) -> np.ndarray:
+        """bool [k_i, n_nodes]: row j = destinations whose next-hop set holds
+        the source's j-th neighbour (ascending id)."""
+        return nh_matrix(self.nh, int(self.nh_off[i]), int(self.words[i]), self.pitch,
+                         self.dist.shape[1])
+
+
+def nh_matrix(nh: np.ndarray, off: int, k: int, pitch: int, n: int) -> np.ndarray:
+    wpm = pitch // 32
+    words = nh[off: off + k * wpm].reshape(k, wpm).astype(np.uint32)
+    bits = np.unpackbits(words.view(np.uint8).reshape(k, wpm * 4), axis=1, bitorder="little")
+    return bits[:, :n].astype(bool)
 
 
 class SpfPlan:

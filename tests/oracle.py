@@ -126,35 +126,32 @@ class OracleLinkState:
     def max_hops(self, n: str) -> int:
         return int(lib.orc_ls_max_hops(self._h, n.encode()))
 
-    def dense(self, names: Sequence[str], src_ids: Sequence[int], ulm: bool = True,
-              pitch: Optional[int] = None):
-        """All-sources rendering: dist [n_src, N] u64 (UINT64_MAX = unreachable),
-        nh planar words (pitch = N rounded to 4, like the engine), words per src."""
+    def dense(self, names: Sequence[str], src_ids: Sequence[int], ulm: bool = True):
+        """All-sources rendering in node-id order (names ascending):
+        dist [n_src, N] u64 (UINT64_MAX = unreachable) and, per source, a bool
+        matrix [k, N] whose row j marks the destinations whose nextHops()
+        contain the source's j-th distinct up neighbour (ascending name)."""
         blob = "".join(names).encode()
         lens = np.array([len(s.encode()) for s in names], np.uint32)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint32)
         srcs = np.asarray(src_ids, np.uint32)
         n, ns = len(names), len(srcs)
-        pitch = pitch or ((n + 3) & ~3)
         words = np.zeros(ns, np.uint32)
         lib.orc_ls_dense(self._h, blob, _p(offs), _p(lens), n, _p(srcs), ns, int(ulm), None,
                          None, None, _p(words))
-        # the oracle writes [v*W + w] rows of length N; convert to planar pitch layout
-        off_dense = np.concatenate([[0], np.cumsum(words.astype(np.uint64) * n)[:-1]]).astype(np.uint64)
+        off = np.concatenate([[0], np.cumsum(words.astype(np.uint64) * n)[:-1]]).astype(np.uint64)
         dist = np.zeros((ns, n), np.uint64)
-        nh_dense = np.zeros(max(1, int((words.astype(np.uint64) * n).sum())), np.uint32)
+        raw = np.zeros(max(1, int((words.astype(np.uint64) * n).sum())), np.uint32)
         lib.orc_ls_dense(self._h, blob, _p(offs), _p(lens), n, _p(srcs), ns, int(ulm),
-                         _p(dist, C.c_uint64), _p(nh_dense), _p(off_dense, C.c_uint64), _p(words))
-        planar_off = np.concatenate([[0], np.cumsum(words.astype(np.uint64) * pitch)[:-1]]).astype(np.uint64)
-        nh = np.zeros(max(1, int((words.astype(np.uint64) * pitch).sum())), np.uint32)
+                         _p(dist, C.c_uint64), _p(raw), _p(off, C.c_uint64), _p(words))
+        mats = []
         for i in range(ns):
             w = int(words[i])
-            if w == 0:
-                continue
-            blk = nh_dense[int(off_dense[i]): int(off_dense[i]) + w * n].reshape(n, w)
-            for j in range(w):
-                nh[int(planar_off[i]) + j * pitch: int(planar_off[i]) + j * pitch + n] = blk[:, j]
-        return dist, nh, planar_off, words
+            blk = raw[int(off[i]): int(off[i]) + w * n].reshape(n, w)
+            bits = np.unpackbits(blk.astype("<u4").view(np.uint8).reshape(n, 4 * w), axis=1,
+                                 bitorder="little").astype(bool)  # [N, 32w]
+            mats.append(bits.T.copy())  # [32w, N]; rows >= k are all False
+        return dist, mats
 
     def time_sources(self, srcs: Sequence[str], ulm: bool = True) -> int:
         arr = (C.c_char_p * len(srcs))(*[s.encode() for s in srcs])

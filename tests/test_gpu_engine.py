@@ -29,21 +29,20 @@ def load(topo):
 
 def compare(names, eng, orc, srcs, hop=False):
     res = eng.solve(srcs, hop=hop)
-    dist, nh, off, words = orc.dense(names, srcs, ulm=not hop, pitch=eng.pitch)
+    dist, mats = orc.dense(names, srcs, ulm=not hop)
     exp = np.where(dist == np.iinfo(np.uint64).max, U32_INF, dist).astype(np.uint32)
     assert np.array_equal(res.dist, exp), "distance mismatch"
-    assert np.array_equal(res.words, words)
-    assert np.array_equal(res.nh_off, off)
-    for i in range(len(srcs)):
-        w = int(words[i])
-        o = int(off[i])
-        for j in range(w):
-            a = res.nh[o + j * eng.pitch: o + j * eng.pitch + len(names)]
-            b = nh[o + j * eng.pitch: o + j * eng.pitch + len(names)]
-            if not np.array_equal(a, b):
-                bad = int(np.nonzero(a != b)[0][0])
-                raise AssertionError(f"next-hop mismatch src {names[srcs[i]]} dst {names[bad]} "
-                                     f"word {j}: {a[bad]:#x} vs {b[bad]:#x}")
+    for i, s in enumerate(srcs):
+        k = len(eng.neighbors(s))
+        assert int(res.words[i]) == k
+        got = res.nh_matrix(i)
+        want = mats[i][:k]
+        assert not mats[i][k:].any()
+        if not np.array_equal(got, want):
+            j, v = (int(x[0]) for x in np.nonzero(got != want))
+            raise AssertionError(f"next-hop mismatch src {names[s]} dst {names[v]} "
+                                 f"neighbour {names[eng.neighbors(s)[j]]}: "
+                                 f"gpu {bool(got[j, v])} oracle {bool(want[j, v])}")
     return res
 
 
@@ -101,17 +100,15 @@ def test_baseline_size_sampled_exact_and_all_sources_properties(which):
     for s in sample:
         one = eng.solve([s])
         assert np.array_equal(one.dist[0], d[s])
-        assert np.array_equal(one.nh_bits(0), res.nh_bits(s))
-    # next hops: empty only at the source, and x in nh_s(v) => d(s,x)=1 & d(x,v)=d(s,v)-1
+        assert np.array_equal(one.nh_matrix(0), res.nh_matrix(s))
+    # next hops: empty only at the source, and x in nh_s(v) <=> d(x,v) = d(s,v) - 1
     for s in sample:
-        bits = res.nh_bits(s)
+        mat = res.nh_matrix(s)
         nbrs = eng.neighbors(s)
-        has = bits.any(axis=1)
+        has = mat.any(axis=0)
         assert not has[s] and has[np.arange(n) != s].all()
         for j, x in enumerate(nbrs):
-            sel = (bits[:, j // 32] >> (j % 32)) & 1
-            v = np.nonzero(sel)[0]
-            assert (d[x, v] + 1 == d[s, v]).all()
+            assert np.array_equal(mat[j], d[x].astype(np.int64) + 1 == d[s])
 
 
 def test_zero_metric_is_rejected_loudly():

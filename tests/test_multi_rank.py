@@ -31,9 +31,8 @@ def _solve(lsdb, srcs):
     names = graph_from_lsdb(lsdb)[0]
     orc = OracleLinkState()
     orc.update_packed(lsdb)
-    dist, nh, off, words = orc.dense(names, list(srcs))
-    pitch = (len(names) + 15) & ~15
-    return [row_digest(dist[i], nh[int(off[i]): int(off[i]) + int(words[i]) * pitch])
+    dist, mats = orc.dense(names, list(srcs))
+    return [row_digest(dist[i], np.packbits(mats[i], axis=1, bitorder="little"))
             for i in range(len(srcs))]
 
 
