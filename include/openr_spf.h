@@ -144,6 +144,12 @@ spf_status spf_preds(spf_ctx* ctx, uint32_t src, uint32_t flags,
                      const uint32_t* dist, uint32_t* pred_ptr,
                      uint32_t* pred_edge, uint32_t cap, uint32_t* n_preds);
 
+/* ---- diagnostics ---------------------------------------------------------- */
+/* With SPF_STAMPS set in the environment, the multi-source BFS kernel records
+ * s_memtime stamps of workgroup 0 at its phase boundaries (init, then per level:
+ * distance stores, pull sweep, barrier; end).  Copies up to cap stamps. */
+spf_status spf_debug_stamps(spf_ctx* ctx, uint64_t* out, uint32_t cap, uint32_t* n);
+
 /* ---- counters ----------------------------------------------------------- */
 /* Logical single-source solves executed (the reference's decision.spf_runs,
  * LinkState.cpp:815) and kernel time of the last execute in ms. */

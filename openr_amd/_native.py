@@ -156,6 +156,7 @@ PROTOTYPES = {
     "spf_preds": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u32p,
                             _u32p, _u32p, C.c_uint32, _u32p]),
     "spf_solves": (C.c_uint64, [_vp]),
+    "spf_debug_stamps": (C.c_int, [_vp, _u64p, C.c_uint32, _u32p]),
     # LinkState facade (openr_linkstate.h)
     "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "ls_destroy": (None, [_vp]),

@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -242,7 +243,8 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
     uint32_t n_rows, uint32_t N, uint32_t pitch, uint32_t npitch,
-    uint32_t* __restrict__ D, uint8_t* __restrict__ Dn) {
+    uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
+    unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* F = reinterpret_cast<uint64_t*>(smem);             // [N + 1]
   uint32_t* o_node = reinterpret_cast<uint32_t*>(F + N + 1);   // [64] drained batch sources
@@ -253,6 +255,13 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   const uint32_t row0 = blockIdx.x * kMsBatch;
   const uint32_t nb = min(kMsBatch, n_rows - row0);
   const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+  const bool stamp = stamps && blockIdx.x == 0 && tid == 0;
+  uint32_t n_stamp = 0;
+#define MS_STAMP()                                                   \
+  do {                                                               \
+    if (stamp && n_stamp < 63) stamps[++n_stamp] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  MS_STAMP();
 
   for (uint32_t v = tid; v <= N; v += kMsThreads) F[v] = 0;
   if (tid == 0) {
@@ -278,25 +287,25 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     if (v < N && ovl[v]) drained |= 1u << i;
   }
 
+  MS_STAMP();
   for (uint32_t L = 0;; ++L) {
     // ---- record level L: D[s][v] = L for every new (s, v) ----
-    uint64_t mine = 0;
-#pragma unroll
-    for (int i = 0; i < OWN; ++i) mine |= nv[i];
+    // per owned slice, only the sources with a new node in it (wave OR);
+    // one store covers 64 consecutive nodes of one source row
     const uint32_t nl = min(L, 254u);
-    for (uint64_t m = wave_or64(mine); m; m &= m - 1) {
-      const uint32_t s = __ffsll((unsigned long long)m) - 1;
-      uint32_t* drow = D + (size_t)(row0 + s) * pitch;
-      uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
 #pragma unroll
-      for (int i = 0; i < OWN; ++i) {
-        const uint32_t v = tid + i * kMsThreads;
+    for (int i = 0; i < OWN; ++i) {
+      const uint32_t v = tid + i * kMsThreads;
+      const uint32_t npos = narrow_pos(v);
+      for (uint64_t m = wave_or64(nv[i]); m; m &= m - 1) {
+        const uint32_t s = __ffsll((unsigned long long)m) - 1;
         if ((nv[i] >> s) & 1ull) {
-          drow[v] = L;
-          nrow[narrow_pos(v)] = (uint8_t)nl;
+          D[(size_t)(row0 + s) * pitch + v] = L;
+          Dn[(size_t)(row0 + s) * npitch + npos] = (uint8_t)nl;
         }
       }
     }
+    MS_STAMP();
     // ---- pull sweep for level L+1 ----
     uint64_t any = 0;
     uint64_t nx[OWN];
@@ -327,7 +336,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
         }
       }
     }
+    MS_STAMP();
     __syncthreads();  // every read of F for this level is done
+    MS_STAMP();
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = tid + i * kMsThreads;
@@ -348,6 +359,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     __syncthreads();
     if (!flag[L & 1]) break;
   }
+  MS_STAMP();
   // ---- unreachable (s, v) pairs and row padding ----
   uint64_t miss = 0;
 #pragma unroll
@@ -374,6 +386,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       nrow[narrow_pos(v)] = 0xFF;
     }
   }
+  MS_STAMP();
+  if (stamp) stamps[0] = n_stamp;
+#undef MS_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -388,13 +403,6 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 //           source row holds a saturated entry (>= 254) decides on the exact
 //           u32 rows instead.
 //   exact:  u32 rows, one coalesced dword load per 64 destinations.
-// Blocks are remapped so each XCD walks a contiguous source range (sources
-// that share neighbours -- e.g. the racks of one pod -- meet in one L2).
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
-  const uint32_t xcd = b & 7, pos = b >> 3;
-  const uint32_t q = nb >> 3, r = nb & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
-}
 
 constexpr uint32_t kNbTile = 256;      // neighbours staged in LDS per tile
 constexpr int kEcmpUnroll = 4;         // neighbour rows in flight per wave
@@ -414,14 +422,19 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     const uint32_t* __restrict__ row_of, const uint32_t* __restrict__ nb_ptr,
     const uint32_t* __restrict__ nb_id, const uint32_t* __restrict__ nb_w,
     const uint8_t* __restrict__ ovl, uint32_t hop, const uint64_t* __restrict__ nh_off,
-    uint32_t* __restrict__ nh, uint32_t chunks, uint32_t n_blocks) {
+    uint32_t* __restrict__ nh, uint32_t chunks, uint32_t n_src) {
   __shared__ uint32_t s_row[kNbTile];  // row of neighbour, or kInf if drained
   __shared__ uint32_t s_w[kNbTile];
   __shared__ uint32_t s_id[kNbTile];
 
-  const uint32_t vb = xcd_remap(blockIdx.x, n_blocks);
-  const uint32_t i = vb / chunks;
-  const uint32_t c = vb - i * chunks;
+  // Sources are dealt round-robin over the 8 XCD groups (block b runs on the
+  // XCD group b % 8): every XCD gets the same mix of switch roles (work per
+  // source ~ its neighbour count), and inside a group the sources come in id
+  // order, so e.g. the racks of one pod -- same neighbour rows -- share an L2.
+  const uint32_t grp = blockIdx.x & 7, pos = blockIdx.x >> 3;
+  const uint32_t i = (pos / chunks) * 8 + grp;
+  const uint32_t c = pos % chunks;
+  if (i >= n_src) return;
   const uint32_t s = req_src[i];
   const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
   if (k == 0) return;  // isolated source: no bitmaps at all
@@ -646,6 +659,7 @@ struct spf_ctx {
   DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
   DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
+  DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
 };
 
 struct spf_plan {
@@ -1007,11 +1021,15 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
                   hipStream_t s) {
   hipLaunchKernelGGL((msbfs_kernel<OWN>), dim3((rows + kMsBatch - 1) / kMsBatch), dim3(kMsThreads),
                      msbfs_lds_bytes(c->N), s, c->d_sell_ptr.p, c->d_sell_col.p, c->d_ovl.p,
-                     rows_src, rows, c->N, c->pitch, c->npitch, D, Dn);
+                     rows_src, rows, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
                         uint8_t* Dn, hipStream_t s) {
+  if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
+    HIP_TRY(c, c->d_stamps.alloc(64));
+    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 8, s));
+  }
   const uint32_t own = (c->N + kMsThreads - 1) / kMsThreads;
   if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, s);
   else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, s);
@@ -1029,10 +1047,10 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
                        uint32_t* d_nh, hipStream_t s) {
   const uint32_t per_block = kEcmpChunk * kEcmpWaves;
   const uint32_t chunks = (c->N + per_block - 1) / per_block;
-  const uint32_t nb = chunks * p->n_src;
+  const uint32_t nb = chunks * ((p->n_src + 7) / 8) * 8;
   hipLaunchKernelGGL((ecmp_kernel<NARROW>), dim3(nb), dim3(kEcmpThreads), 0, s, Dn, c->npitch, D,
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
-                     c->d_nb_w.p, c->d_ovl.p, hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, nb);
+                     c->d_nb_w.p, c->d_ovl.p, hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, p->n_src);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -1155,6 +1173,17 @@ spf_status spf_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src, uint32_t 
     HIP_TRY(c, hipMemcpyAsync(nh_out, d_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SPF_OK;
+}
+
+spf_status spf_debug_stamps(spf_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n) {
+  if (!c || !n) return SPF_E_INVALID;
+  *n = 0;
+  if (!c->d_stamps.p) return SPF_OK;
+  uint64_t buf[64];
+  HIP_TRY(c, hipMemcpy(buf, c->d_stamps.p, sizeof buf, hipMemcpyDeviceToHost));
+  *n = (uint32_t)std::min<uint64_t>(buf[0], 63);
+  for (uint32_t i = 0; i < *n && i < cap; ++i) out[i] = buf[i + 1];
   return SPF_OK;
 }
 

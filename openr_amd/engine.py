@@ -61,8 +61,9 @@ class SpfPlan:
 
     def __del__(self) -> None:
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            N.lib.spf_plan_destroy(h)
+        lib = getattr(N, "lib", None)  # None during interpreter shutdown
+        if h is not None and h.value and lib is not None:
+            lib.spf_plan_destroy(h)
             self._h = C.c_void_p()
 
     @property
@@ -110,8 +111,9 @@ class SpfEngine:
 
     def __del__(self) -> None:
         h = getattr(self, "_h", None)
-        if getattr(self, "_owned", False) and h is not None and h.value:
-            N.lib.spf_ctx_destroy(h)
+        lib = getattr(N, "lib", None)
+        if getattr(self, "_owned", False) and h is not None and h.value and lib is not None:
+            lib.spf_ctx_destroy(h)
             self._h = C.c_void_p()
 
     def _err(self, st: int) -> None:
@@ -147,6 +149,13 @@ class SpfEngine:
         out = np.zeros(max(1, cnt.value), np.uint32)
         self._err(N.lib.spf_src_neighbors(self._h, src, N.ptr(out), cnt.value, C.byref(cnt)))
         return out[: cnt.value]
+
+    def debug_stamps(self) -> np.ndarray:
+        """BFS phase stamps of workgroup 0 (needs SPF_STAMPS=1 at first execute)."""
+        out = np.zeros(64, np.uint64)
+        n = C.c_uint32()
+        self._err(N.lib.spf_debug_stamps(self._h, N.ptr(out, C.c_uint64), 64, C.byref(n)))
+        return out[: n.value]
 
     def solves(self) -> int:
         return int(N.lib.spf_solves(self._h))

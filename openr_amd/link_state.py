@@ -174,8 +174,9 @@ class LinkState:
 
     def __del__(self) -> None:
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            N.lib.ls_destroy(h)
+        lib = getattr(N, "lib", None)  # None during interpreter shutdown
+        if h is not None and h.value and lib is not None:
+            lib.ls_destroy(h)
             self._h = C.c_void_p()
 
     # -- helpers ---------------------------------------------------------------
