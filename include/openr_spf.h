@@ -146,8 +146,9 @@ spf_status spf_preds(spf_ctx* ctx, uint32_t src, uint32_t flags,
 
 /* ---- diagnostics ---------------------------------------------------------- */
 /* With SPF_STAMPS set in the environment, the multi-source BFS kernel records
- * s_memtime stamps of workgroup 0 at its phase boundaries (init, then per level:
- * distance stores, pull sweep, barrier; end).  Copies up to cap stamps. */
+ * s_memtime clocks of workgroup 0 at its phase boundaries (init, then per level:
+ * distance stores, pull sweep, barrier; end), per wave: out[w*64] = count,
+ * out[w*64 + 1 ..] = clocks of wave w (16 waves).  Copies up to cap words. */
 spf_status spf_debug_stamps(spf_ctx* ctx, uint64_t* out, uint32_t cap, uint32_t* n);
 
 /* ---- counters ----------------------------------------------------------- */

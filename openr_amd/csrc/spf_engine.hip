@@ -242,7 +242,7 @@ template <int OWN>
 __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
-    uint32_t n_rows, uint32_t N, uint32_t pitch, uint32_t npitch,
+    uint32_t n_rows, uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch,
     uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
     unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -252,14 +252,17 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   uint32_t* flag = o_cnt + 1;                                  // [2] per-parity progress
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t row0 = blockIdx.x * kMsBatch;
-  const uint32_t nb = min(kMsBatch, n_rows - row0);
+  const uint32_t row0 = blockIdx.x * bs;  // bs <= 64 sources per workgroup
+  const uint32_t nb = min(bs, n_rows - row0);
   const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-  const bool stamp = stamps && blockIdx.x == 0 && tid == 0;
+  // diagnostics: lane 0 of every wave of workgroup 0 logs phase clocks into
+  // stamps[wave * 64 + 1 ..], the count into stamps[wave * 64]
+  const bool stamp = stamps && blockIdx.x == 0 && lane == 0;
+  unsigned long long* my_stamps = stamps + (tid >> 6) * 64;
   uint32_t n_stamp = 0;
 #define MS_STAMP()                                                   \
   do {                                                               \
-    if (stamp && n_stamp < 63) stamps[++n_stamp] = __builtin_amdgcn_s_memtime(); \
+    if (stamp && n_stamp < 63) my_stamps[++n_stamp] = __builtin_amdgcn_s_memtime(); \
   } while (0)
   MS_STAMP();
 
@@ -279,12 +282,19 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 
   uint64_t vis[OWN], nv[OWN];
   uint32_t drained = 0;  // bit i: owned node i is drained
+  uint32_t sb[OWN], sw[OWN];  // owned slice i: column base, width (wave-uniform)
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     const uint32_t v = tid + i * kMsThreads;
     nv[i] = v < N ? F[v] : 0ull;
     vis[i] = nv[i];
     if (v < N && ovl[v]) drained |= 1u << i;
+    const uint32_t slice = (tid - lane + i * kMsThreads) / kSliceW;
+    const bool live = slice * kSliceW < N;
+    const uint32_t b = live ? sell_ptr[slice] : 0u;
+    const uint32_t e = live ? sell_ptr[slice + 1] : 0u;
+    sb[i] = __builtin_amdgcn_readfirstlane(b);
+    sw[i] = __builtin_amdgcn_readfirstlane((e - b) / kSliceW);
   }
 
   MS_STAMP();
@@ -295,13 +305,16 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t nl = min(L, 254u);
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
-      const uint32_t v = tid + i * kMsThreads;
-      const uint32_t npos = narrow_pos(v);
-      for (uint64_t m = wave_or64(nv[i]); m; m &= m - 1) {
+      // the wave-uniform mask lives in SGPRs: row addressing is scalar work
+      const uint64_t wm = wave_or64(nv[i]);
+      uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
+      uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
+      for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
         const uint32_t s = __ffsll((unsigned long long)m) - 1;
         if ((nv[i] >> s) & 1ull) {
+          const uint32_t v = tid + i * kMsThreads;
           D[(size_t)(row0 + s) * pitch + v] = L;
-          Dn[(size_t)(row0 + s) * npitch + npos] = (uint8_t)nl;
+          Dn[(size_t)(row0 + s) * npitch + narrow_pos(v)] = (uint8_t)nl;
         }
       }
     }
@@ -315,20 +328,18 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const uint32_t v = tid + i * kMsThreads;
       const bool need = v < N && vis[i] != all;
       if (__ballot(need)) {  // wave-uniform: the slice has unfinished nodes
-        const uint32_t slice = v / kSliceW;
-        const uint32_t b = sell_ptr[slice];
-        const uint32_t w = (sell_ptr[slice + 1] - b) / kSliceW;
-        const uint32_t* cp = sell_col + b + lane;
+        const uint32_t* cp = sell_col + sb[i] + lane;
+        const uint32_t w = sw[i];
         uint64_t acc = 0;
-        uint32_t j = 0;
-        for (; j + kMsUnroll <= w; j += kMsUnroll) {
+        for (uint32_t j = 0; j < w; j += kMsUnroll) {
+          // kMsUnroll column loads in flight; past the slice width the
+          // padding index N reads F[N] = 0
           uint32_t c[kMsUnroll];
 #pragma unroll
-          for (int u = 0; u < kMsUnroll; ++u) c[u] = cp[(j + u) * kSliceW];
+          for (int u = 0; u < kMsUnroll; ++u) c[u] = j + u < w ? cp[(j + u) * kSliceW] : N;
 #pragma unroll
           for (int u = 0; u < kMsUnroll; ++u) acc |= F[c[u]];
         }
-        for (; j < w; ++j) acc |= F[cp[j * kSliceW]];
         if (need) {
           nx[i] = acc & ~vis[i];
           vis[i] |= nx[i];
@@ -387,7 +398,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     }
   }
   MS_STAMP();
-  if (stamp) stamps[0] = n_stamp;
+  if (stamp) my_stamps[0] = n_stamp;
 #undef MS_STAMP
 }
 
@@ -638,6 +649,7 @@ struct DevBuf {
 
 struct spf_ctx {
   int device = 0;
+  uint32_t n_cu = 256;  // compute units (BFS batch sizing)
   hipStream_t stream = nullptr;
   std::string err;
   uint64_t solves = 0;
@@ -741,6 +753,7 @@ spf_status spf_ctx_create(int device, spf_ctx** out) {
                 device, prop.gcnArchName);
   auto c = std::make_unique<spf_ctx>();
   c->device = device;
+  c->n_cu = (uint32_t)std::max(1, prop.multiProcessorCount);
   if (hipSetDevice(device) != hipSuccess)
     return fail(nullptr, SPF_E_HIP, "hipSetDevice(%d) failed", device);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
@@ -1019,16 +1032,21 @@ size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
                   hipStream_t s) {
-  hipLaunchKernelGGL((msbfs_kernel<OWN>), dim3((rows + kMsBatch - 1) / kMsBatch), dim3(kMsThreads),
+  // one workgroup per CU per round: a batch costs one edge sweep per level
+  // whatever its size, but its stores scale with it, so spread the sources
+  // over every CU rather than fill 64-source batches on fewer CUs
+  const uint32_t rounds = (rows + kMsBatch * c->n_cu - 1) / (kMsBatch * c->n_cu);
+  const uint32_t bs = std::min<uint32_t>(kMsBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
+  hipLaunchKernelGGL((msbfs_kernel<OWN>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                      msbfs_lds_bytes(c->N), s, c->d_sell_ptr.p, c->d_sell_col.p, c->d_ovl.p,
-                     rows_src, rows, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
+                     rows_src, rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
                         uint8_t* Dn, hipStream_t s) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
-    HIP_TRY(c, c->d_stamps.alloc(64));
-    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 8, s));
+    HIP_TRY(c, c->d_stamps.alloc(64 * 16));
+    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
   }
   const uint32_t own = (c->N + kMsThreads - 1) / kMsThreads;
   if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, s);
@@ -1180,10 +1198,10 @@ spf_status spf_debug_stamps(spf_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n
   if (!c || !n) return SPF_E_INVALID;
   *n = 0;
   if (!c->d_stamps.p) return SPF_OK;
-  uint64_t buf[64];
-  HIP_TRY(c, hipMemcpy(buf, c->d_stamps.p, sizeof buf, hipMemcpyDeviceToHost));
-  *n = (uint32_t)std::min<uint64_t>(buf[0], 63);
-  for (uint32_t i = 0; i < *n && i < cap; ++i) out[i] = buf[i + 1];
+  std::vector<uint64_t> buf(64 * 16);
+  HIP_TRY(c, hipMemcpy(buf.data(), c->d_stamps.p, buf.size() * 8, hipMemcpyDeviceToHost));
+  *n = (uint32_t)std::min<size_t>(cap, buf.size());
+  std::copy(buf.begin(), buf.begin() + *n, out);
   return SPF_OK;
 }
 

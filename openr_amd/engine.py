@@ -151,11 +151,12 @@ class SpfEngine:
         return out[: cnt.value]
 
     def debug_stamps(self) -> np.ndarray:
-        """BFS phase stamps of workgroup 0 (needs SPF_STAMPS=1 at first execute)."""
-        out = np.zeros(64, np.uint64)
+        """BFS phase clocks of workgroup 0 (needs SPF_STAMPS=1 at first execute):
+        [16 waves, 64] -- column 0 is the count, columns 1.. the clocks."""
+        out = np.zeros(64 * 16, np.uint64)
         n = C.c_uint32()
-        self._err(N.lib.spf_debug_stamps(self._h, N.ptr(out, C.c_uint64), 64, C.byref(n)))
-        return out[: n.value]
+        self._err(N.lib.spf_debug_stamps(self._h, N.ptr(out, C.c_uint64), out.size, C.byref(n)))
+        return out.reshape(16, 64)
 
     def solves(self) -> int:
         return int(N.lib.spf_solves(self._h))

@@ -1,4 +1,9 @@
-"""Print the BFS kernel's per-phase cycle breakdown (workgroup 0) on fabric_full."""
+"""Per-phase cycle breakdown of the BFS kernel (workgroup 0, every wave).
+
+Diagnostic only: SPF_STAMPS=1 makes msbfs_kernel log s_memtime at each phase
+boundary.  Prints, per level, the min/max over the 16 waves of the store phase,
+pull phase and barrier wait, and which wave is the slowest.
+"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["SPF_STAMPS"] = "1"
@@ -6,7 +11,9 @@ import numpy as np
 import torch
 from openr_amd import topology as T
 from openr_amd.engine import SpfEngine, graph_from_lsdb
-topo = T.fabric(10000, full=True) if (len(sys.argv) < 2 or sys.argv[1] == "fabric") else T.grid(100)
+
+which = sys.argv[1] if len(sys.argv) > 1 else "fabric"
+topo = T.fabric(10000, full=True) if which == "fabric" else T.grid(100)
 names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
 eng = SpfEngine(0); eng.load(rp, col, met, lid, ovl)
 plan = eng.plan(list(range(len(names))))
@@ -15,14 +22,19 @@ h = torch.empty(max(1, plan.nh_words), dtype=torch.int32, device="cuda")
 for _ in range(3):
     plan.execute_torch(d, h)
 torch.cuda.synchronize()
-st = eng.debug_stamps().astype(np.int64)
-dt = np.diff(st)
-print("stamps:", len(st), "total cycles", int(st[-1] - st[0]))
-print("init", int(st[1] - st[0]))
-lv = st[2:-2]
-prev = st[1]
-for L in range(len(lv) // 3):
-    A, B, Cc = lv[3 * L: 3 * L + 3]
-    print(f"level {L}: F-write(prev)+stores {A - prev:8d}  pull {B - A:8d}  barrier-wait {Cc - B:8d}")
+raw = eng.debug_stamps().astype(np.int64)
+waves = [raw[w, 1:1 + raw[w, 0]] for w in range(16) if raw[w, 0] > 0]
+n = min(len(x) for x in waves)
+st = np.stack([x[:n] for x in waves])  # [W, n]
+t0 = st[:, 0].min()
+print(f"{which}: {st.shape[0]} waves, {n} stamps, total cycles {int(st[:, -1].max() - t0)}")
+n_lv = (n - 3) // 3
+prev = st[:, 1]
+print("init max", int((st[:, 1] - st[:, 0]).max()))
+for L in range(n_lv):
+    A, B, Cc = st[:, 2 + 3 * L], st[:, 3 + 3 * L], st[:, 4 + 3 * L]
+    sto, pul, bar = A - prev, B - A, Cc - B
+    print(f"level {L:3d}: stores {sto.min():7d}..{sto.max():7d} (w{sto.argmax():2d})  "
+          f"pull {pul.min():7d}..{pul.max():7d} (w{pul.argmax():2d})  barrier {bar.min():7d}..{bar.max():7d}")
     prev = Cc
-print("last F-write/flag", int(st[-2] - prev), " tail (unreachable+padding)", int(st[-1] - st[-2]))
+print("tail max", int((st[:, -1] - prev).max()))
