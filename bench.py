@@ -194,6 +194,10 @@ def main() -> None:
             "dominant": dominant,
             "kernel_ms": {"sssp_kernel": sssp_avg, "ecmp_kernel": ecmp_avg},
             "algorithmic_bytes_per_launch": bytes_launch,
+            # measured HBM bytes (PMC, profiles/pmc_<workload>.json) over the
+            # same launch time: the real DRAM-side utilisation
+            "traffic_gbs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
+            "traffic_frac": traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
         },
         "cpu_baseline": None,
     }

@@ -1,12 +1,53 @@
-"""Summarise rocprofv3 --pmc counter_collection.csv files per kernel (avg per dispatch)."""
-import csv, glob, sys, collections
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+"""Summarise rocprofv3 --pmc counter_collection.csv files per kernel (avg per dispatch).
+
+    python tools/pmc_summary.py [pmc_dir] [--json profiles/pmc_<workload>.json --kernels a,b]
+
+With --json, writes the HBM traffic of one plan execute (the sum over the
+listed kernels of one dispatch each) in bytes, with the gfx950 corrections of
+MI355X_MICROARCH.md's HBM section applied:
+  * FETCH_SIZE (KB) counts half the bytes of wide coalesced reads -> x2;
+  * WRITE_SIZE (KB) is exact for 16-B/lane stores; narrower stores are
+    reported as counted (uncalibrated, stated in the JSON).
+bench.py reads `hbm_bytes_per_launch` from that file into roofline.traffic.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+
+ap = argparse.ArgumentParser()
+ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
+ap.add_argument("--json")
+ap.add_argument("--kernels", default="")
+args = ap.parse_args()
+
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
+for f in sorted(glob.glob(f"{args.root}/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, cs in acc.items():
+avg = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+for k, cs in avg.items():
     print(k)
     for c, v in sorted(cs.items()):
-        print(f"   {c:28s} avg/dispatch = {sum(v)/len(v):.4g}  (n={len(v)})")
+        print(f"   {c:28s} avg/dispatch = {v:.4g}  (n={len(acc[k][c])})")
+
+if args.json:
+    want = [w for w in args.kernels.split(",") if w]
+    per = {}
+    total = 0.0
+    for k, cs in avg.items():
+        if want and not any(k.startswith(w) for w in want):
+            continue
+        fetch = 2.0 * cs.get("FETCH_SIZE", 0.0) * 1024
+        write = cs.get("WRITE_SIZE", 0.0) * 1024
+        hit, miss = cs.get("TCC_HIT_sum", 0.0), cs.get("TCC_MISS_sum", 0.0)
+        per[k] = {"fetch_bytes_x2": fetch, "write_bytes": write,
+                  "l2_hit_rate": hit / (hit + miss) if hit + miss else None}
+        total += fetch + write
+    out = {"hbm_bytes_per_launch": total, "per_kernel": per,
+           "note": "FETCH_SIZE doubled (gfx950 wide-read correction); WRITE_SIZE as counted"}
+    with open(args.json, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
