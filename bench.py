@@ -3,13 +3,20 @@
 fabric (BASELINE.json configs[2]; metric "all-sources SPF solves/sec + GTEPS,
 10k-node fabric, 1/2/4/8 MI355X").
 
-A step = one all-sources pass: every node of the rank's LSDB snapshot solved
-as a source (distances + ECMP next-hop bitsets, bit-exact with the reference's
-LinkState::runSpf, openr/decision/LinkState.cpp:808-882), results resident in
-HBM.  Scaling is weak: rank r solves its own LSDB snapshot -- the fabric with
-rack switch r's overload bit toggled, the perturbation the reference's
-BM_DecisionFabric applies per iteration (RoutingBenchmarkUtils.cpp:406-447) --
-so per-GPU work is fixed and no collective touches the data path.
+Default workload (fabric_full): a step = one all-sources pass, every node of
+the rank's LSDB snapshot solved as a source (distances + ECMP next-hop
+bitsets, bit-exact with the reference's LinkState::runSpf,
+openr/decision/LinkState.cpp:808-882), results resident in HBM.  Scaling is
+weak: rank r solves its own LSDB snapshot -- the fabric with rack switch r's
+overload bit toggled, the perturbation the reference's BM_DecisionFabric
+applies per iteration (RoutingBenchmarkUtils.cpp:406-447) -- so per-GPU work
+is fixed and no collective touches the data path.
+
+Other BASELINE configs (--workload):
+  grid100    configs[1]: all-sources SPF + ECMP on grid 100x100 (weak, as above)
+  wan_ksp2   configs[3]: getKthPaths(s, d, 1) and (s, d, 2) for ALL pairs of the
+             2000-node WAN graph; sources sharded over ranks (strong scaling),
+             every rank's paths gathered to rank 0 with RCCL inside the step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fabric_full]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -33,56 +40,196 @@ METRIC = "all-sources SPF solves/sec + GTEPS, 10k-node fabric, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
 
-def build_workload(name: str, rank: int):
-    from openr_amd import topology as T
-
-    if name == "fabric_full":
-        topo = T.fabric(10000, full=True)
-        desc = "fabric_full numOfSws=10000 (RoutingBenchmarkUtils.cpp:247-400, every pod wired)"
-    elif name == "fabric_ref":
-        topo = T.fabric(10000, full=False)
-        desc = "fabric_ref numOfSws=10000 (reference generator incl. per-pod emplace quirk)"
-    elif name == "grid100":
-        topo = T.grid(100)
-        desc = "grid 100x100 (RoutingBenchmarkUtils.cpp:161-240)"
-    else:
-        raise SystemExit(f"unknown workload {name}")
-    from openr_amd.sharding import snapshot_for_rank
-
-    # rank r's snapshot: one node drained, as BM_Decision* toggles per iteration
-    topo.lsdb = snapshot_for_rank(topo.lsdb, rank)
-    return topo, desc
+def cpu_model() -> str:
+    try:
+        return next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                    if l.startswith("model name"))
+    except Exception:  # noqa: BLE001
+        return "unknown"
 
 
-def cpu_baseline(topo, budget_s: float):
-    """The CPU oracle (faithful restatement of LinkState::runSpf, kind 'port')
-    timed on this host, 1 core, on a seeded sample of sources of the same
-    workload, until `budget_s` seconds of work have accumulated."""
+def oracle():
     sys.path.insert(0, str(ROOT / "tests"))
     from oracle import OracleLinkState  # CPU baseline leg only
 
-    orc = OracleLinkState()
-    orc.update_packed(topo.lsdb)
-    order = np.random.default_rng(0).permutation(topo.n_nodes)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and done < len(order):
-        batch = [topo.nodes[int(i)] for i in order[done: done + 4]]
-        orc.time_sources(batch)
-        done += len(batch)
-    dt = time.perf_counter() - t0
-    try:
-        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
-                         if l.startswith("model name"))
-    except Exception:  # noqa: BLE001
-        cpu_model = "unknown"
-    return {
-        "value": done / dt,
-        "unit": "solves/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{done} seeded-random sources of the same topology, full runSpf each "
-                  f"({dt:.1f} s on 1 core of {cpu_model}; oracle/spf_oracle.cpp)",
-    }
+    return OracleLinkState
+
+
+class AllSources:
+    """configs[1]/[2]: one all-sources SPF + ECMP pass per step (weak scaling)."""
+
+    scaling = "weak"
+    unit = "solves/s"
+    kernels = ("sssp_kernel", "ecmp_kernel")
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        import torch
+
+        from openr_amd import topology as T
+        from openr_amd.sharding import snapshot_for_rank
+
+        if name == "fabric_full":
+            topo = T.fabric(10000, full=True)
+            self.desc = "fabric_full numOfSws=10000 (RoutingBenchmarkUtils.cpp:247-400, every pod wired)"
+        elif name == "fabric_ref":
+            topo = T.fabric(10000, full=False)
+            self.desc = "fabric_ref numOfSws=10000 (reference generator incl. per-pod emplace quirk)"
+        else:
+            topo = T.grid(100)
+            self.desc = "grid 100x100 (RoutingBenchmarkUtils.cpp:161-240)"
+        # rank r's snapshot: one node drained, as BM_Decision* toggles per iteration
+        topo.lsdb = snapshot_for_rank(topo.lsdb, rank)
+        self.topo = topo
+        names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+        self.n, self.e = len(names), len(col)
+        eng = eng_cls(dev.index)
+        eng.load(rp, col, met, lid, ovl)
+        self.eng = eng
+        self.plan = eng.plan(list(range(self.n)))
+        self.d_dist = torch.empty(self.n * eng.pitch, dtype=torch.int32, device=dev)
+        self.d_nh = torch.empty(max(1, self.plan.nh_words), dtype=torch.int32, device=dev)
+        self.units = self.n
+        self.world = world
+        # SURVEY.md §8(d): B_solve = 4(N+1) + 8E + N + 4N + N*ceil(deg(src)/8)
+        nbr = np.array([len(eng.neighbors(s)) for s in range(self.n)], np.int64)
+        n, e = self.n, self.e
+        self.bytes_launch = int(n * (4 * (n + 1) + 8 * e + n + 4 * n)
+                                + n * int(np.sum((nbr + 7) // 8)))
+        self.parallelism = (f"source-sharded over {world} rank(s): one LSDB snapshot per rank, "
+                            "no data-path collective")
+
+    def step(self, stream) -> None:
+        self.plan.execute_torch(self.d_dist, self.d_nh, stream)
+
+    def enable_timing(self, k: int) -> None:
+        self.plan.enable_timing(k)
+
+    def kernel_ms(self):
+        a, b, cnt = self.plan.timing()
+        return {"sssp_kernel": a / max(cnt, 1), "ecmp_kernel": b / max(cnt, 1)}
+
+    def edges_per_unit(self) -> int:
+        return self.e
+
+    def cpu_baseline(self, budget_s: float):
+        """The CPU oracle (faithful restatement of LinkState::runSpf, kind
+        'port') timed on this host, 1 core, on a seeded sample of sources of
+        the same workload, until `budget_s` seconds of work have accumulated."""
+        orc = oracle()()
+        orc.update_packed(self.topo.lsdb)
+        order = np.random.default_rng(0).permutation(self.topo.n_nodes)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s and done < len(order):
+            batch = [self.topo.nodes[int(i)] for i in order[done: done + 4]]
+            orc.time_sources(batch)
+            done += len(batch)
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+                "sample": f"{done} seeded-random sources of the same topology, full runSpf "
+                          f"each ({dt:.1f} s on 1 core of {cpu_model()}; oracle/spf_oracle.cpp)"}
+
+
+class Ksp2AllPairs:
+    """configs[3]: KSP2 (k = 1 and k = 2 paths) for every pair of the WAN
+    graph; sources dealt round-robin over ranks (strong scaling), the ranks'
+    pair headers and path pools gathered to rank 0 with RCCL in the step."""
+
+    scaling = "strong"
+    unit = "pairs/s"
+    kernels = ("sssp_kernel", "ksp2_kernel")
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        import torch
+
+        from openr_amd import topology as T
+        from openr_amd.engine import PAIR_DTYPE
+
+        self.topo = T.wan(2000, 1000, seed=1)
+        self.desc = "wan N=2000, ring + 1000 seeded chords, metrics U[1,1000] (SURVEY.md §8(d) config 4)"
+        names, rp, col, met, lid, ovl = graph_from_lsdb(self.topo.lsdb)
+        self.n, self.e = len(names), len(col)
+        eng = eng_cls(dev.index)
+        eng.load(rp, col, met, lid, ovl)
+        self.eng, self.dev, self.rank, self.world = eng, dev, rank, world
+        self.srcs = list(range(rank, self.n, world))
+        self.plan = eng.ksp2_plan(self.srcs)
+        n_pairs = len(self.srcs) * self.n
+        self.units = n_pairs
+        self.pair_words = PAIR_DTYPE.itemsize // 4
+        self.d_pairs = torch.empty(n_pairs * self.pair_words, dtype=torch.int32, device=dev)
+        self.d_cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+        # size the path pool with one untimed sizing run (the counter keeps
+        # counting past an overflow)
+        self.pool_words = 1 << 20
+        self.d_pool = torch.empty(self.pool_words, dtype=torch.int32, device=dev)
+        self.plan.execute(self.d_pairs.data_ptr(), self.d_pool.data_ptr(), self.pool_words,
+                          self.d_cnt.data_ptr(), 0)
+        torch.cuda.synchronize(dev)
+        self.pool_words = int(int(self.d_cnt[0].item()) * 1.05) + (1 << 22)
+        self.d_pool = torch.empty(self.pool_words, dtype=torch.int32, device=dev)
+        self.gathered = 0
+        # SURVEY.md §8(d): one k = 2 solve per pair (B_solve without next hops)
+        # + 4 B per output link; the k = 1 SPF rows are charged per source.
+        n, e = self.n, self.e
+        self.b_solve = 4 * (n + 1) + 8 * e + n + 4 * n
+        self.bytes_launch = None  # known after the first execute (output links)
+        self.parallelism = (f"sources dealt round-robin over {world} rank(s), graph replicated; "
+                            "pair headers + path pools gathered to rank 0 (RCCL gather) in the step")
+
+    def step(self, stream) -> None:
+        import torch
+        import torch.distributed as dist
+
+        self.plan.execute(self.d_pairs.data_ptr(), self.d_pool.data_ptr(), self.pool_words,
+                          self.d_cnt.data_ptr(), stream.cuda_stream)
+        if self.world > 1:
+            # variable-length pools: agree on the largest, then one gather each
+            used = self.d_cnt[0:1].clone()
+            dist.all_reduce(used, op=dist.ReduceOp.MAX)
+            m = int(used.item())
+            dst_p = [torch.empty_like(self.d_pairs) for _ in range(self.world)] if self.rank == 0 else None
+            dst_q = ([torch.empty(m, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
+                     if self.rank == 0 else None)
+            dist.gather(self.d_pairs, dst_p, dst=0)
+            dist.gather(self.d_pool[:m].contiguous(), dst_q, dst=0)
+            self.gathered = m
+
+    def enable_timing(self, k: int) -> None:
+        self.plan.enable_timing(k)
+
+    def kernel_ms(self):
+        a, b, cnt = self.plan.timing()
+        cnt_h = self.d_cnt.cpu().numpy()
+        if cnt_h[2] & 1:
+            raise SystemExit("KSP2 path pool overflowed: raise pool_words")
+        # path pool words = records [len, next, links]; output links ~ words
+        self.bytes_launch = int(self.units * self.b_solve + len(self.srcs) * self.b_solve
+                                + 4 * int(cnt_h[0]))
+        self.k2_runs = int(cnt_h[1])
+        return {"sssp_kernel": a / max(cnt, 1), "ksp2_kernel": b / max(cnt, 1)}
+
+    def edges_per_unit(self) -> int:
+        return self.e
+
+    def cpu_baseline(self, budget_s: float):
+        orc = oracle()()
+        orc.update_packed(self.topo.lsdb)
+        rng = np.random.default_rng(0)
+        src = self.topo.nodes[int(rng.integers(self.n))]
+        dsts = [self.topo.nodes[int(i)] for i in rng.permutation(self.n)]
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s and done < len(dsts):
+            orc.time_ksp2(src, dsts[done: done + 16])
+            done += 16
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+                "sample": f"{done} seeded-random destinations of one source, getKthPaths k=1 "
+                          f"and k=2 each ({dt:.1f} s on 1 core of {cpu_model()}; "
+                          "oracle/spf_oracle.cpp)"}
+
+
+WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
+             "wan_ksp2": Ksp2AllPairs}
 
 
 def main() -> None:
@@ -90,8 +237,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="fabric_full",
-                    choices=["fabric_full", "fabric_ref", "grid100"])
+    ap.add_argument("--workload", default="fabric_full", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of CPU-baseline sampling (0 disables)")
     args = ap.parse_args()
@@ -109,28 +255,20 @@ def main() -> None:
 
     from openr_amd.engine import SpfEngine, graph_from_lsdb
 
-    topo, desc = build_workload(args.workload, rank)
-    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
-    n, e = len(names), len(col)
-    eng = SpfEngine(local)
-    eng.load(rp, col, met, lid, ovl)
-    plan = eng.plan(list(range(n)))
-    pitch = eng.pitch
-    d_dist = torch.empty(n * pitch, dtype=torch.int32, device=dev)
-    d_nh = torch.empty(max(1, plan.nh_words), dtype=torch.int32, device=dev)
+    wl = WORKLOADS[args.workload](args.workload, rank, world, dev, SpfEngine, graph_from_lsdb)
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
-        plan.execute_torch(d_dist, d_nh, stream)
+        wl.step(stream)
     torch.cuda.synchronize(dev)
-    plan.enable_timing(max(1, args.steps))
+    wl.enable_timing(max(1, args.steps))
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.execute_torch(d_dist, d_nh, stream)
+        wl.step(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -139,20 +277,20 @@ def main() -> None:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    sssp_ms, ecmp_ms, cnt = plan.timing()
-    sssp_avg, ecmp_avg = sssp_ms / max(cnt, 1), ecmp_ms / max(cnt, 1)
+    kms = wl.kernel_ms()
+    launch_ms = sum(kms.values())
 
-    solves = world * n * args.steps
-    value = solves / elapsed
-    gteps = world * n * e * args.steps / elapsed / 1e9
+    # whole-job units: weak = every rank did `units`; strong = ranks split them
+    units = wl.units
+    if world > 1:
+        u = torch.tensor([units], dtype=torch.float64, device=dev)
+        dist.all_reduce(u)
+        units = float(u.item())
+    value = units * args.steps / elapsed
+    gteps = units * wl.edges_per_unit() * args.steps / elapsed / 1e9
 
-    # B_solve = 4(N+1) + 8E + N + 4N + N*ceil(deg(src)/8)
-    deg = np.diff(rp).astype(np.int64)
-    nbr = np.array([len(eng.neighbors(s)) for s in range(n)], np.int64)
-    bytes_launch = int(n * (4 * (n + 1) + 8 * e + n + 4 * n) + n * int(np.sum((nbr + 7) // 8)))
-    launch_ms = sssp_avg + ecmp_avg
-    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
-    dominant = "sssp_kernel" if sssp_avg >= ecmp_avg else "ecmp_kernel"
+    achieved = wl.bytes_launch / (launch_ms * 1e-3) / 1e9
+    dominant = max(kms, key=kms.get)
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
     if pmc.exists():
@@ -162,26 +300,26 @@ def main() -> None:
             traffic = None
 
     out = {
-        "metric": METRIC,
+        "metric": METRIC if isinstance(wl, AllSources) else
+        "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN",
         "value": value,
-        "unit": "solves/s",
+        "unit": wl.unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl.scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
         "gteps": gteps,
         "config": {
-            "workload": desc,
-            "nodes": n,
-            "directed_up_edges": e,
-            "solves_per_step_per_rank": n,
-            "parallelism": f"source-sharded over {world} rank(s): one LSDB snapshot per rank, "
-                           "no data-path collective",
+            "workload": wl.desc,
+            "nodes": wl.n,
+            "directed_up_edges": wl.e,
+            "units_per_step_per_rank": wl.units,
+            "parallelism": wl.parallelism,
         },
         "roofline": {
             "bound": "hbm",
@@ -190,10 +328,10 @@ def main() -> None:
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "sssp_kernel+ecmp_kernel (one spf_plan_execute)",
+            "kernel": "+".join(wl.kernels) + " (one execute)",
             "dominant": dominant,
-            "kernel_ms": {"sssp_kernel": sssp_avg, "ecmp_kernel": ecmp_avg},
-            "algorithmic_bytes_per_launch": bytes_launch,
+            "kernel_ms": kms,
+            "algorithmic_bytes_per_launch": wl.bytes_launch,
             # measured HBM bytes (PMC, profiles/pmc_<workload>.json) over the
             # same launch time: the real DRAM-side utilisation
             "traffic_gbs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
@@ -202,7 +340,7 @@ def main() -> None:
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_budget > 0:
-        out["cpu_baseline"] = cpu_baseline(topo, args.cpu_budget)
+        out["cpu_baseline"] = wl.cpu_baseline(args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

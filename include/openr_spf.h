@@ -144,6 +144,47 @@ spf_status spf_preds(spf_ctx* ctx, uint32_t src, uint32_t flags,
                      const uint32_t* dist, uint32_t* pred_ptr,
                      uint32_t* pred_edge, uint32_t cap, uint32_t* n_preds);
 
+/* ---- batched KSP2: getKthPaths(src, dst, 1) and (src, dst, 2) ------------ */
+/* For every pair (srcs[i], d), d = 0..n_nodes-1, the k = 1 and k = 2 paths the
+ * reference returns from LinkState::getKthPaths (LinkState.cpp:762-791): k = 1
+ * traces edge-disjoint paths in the SPF of src (traceOnePath, :398-419, with
+ * the shared visited-link set); k = 2 re-runs SPF from src ignoring every link
+ * of the k = 1 paths and traces again.  Paths are lists of undirected link
+ * ids (spf_graph.link_id) in src -> dst order, in the reference's discovery
+ * order.  src == dst and unreachable pairs have no paths.
+ *
+ * Output: pairs[i * n_nodes + d] (below) and a pool of u32 words holding path
+ * records [n_links, next record offset (SPF_KSP2_NONE = last), link ids...];
+ * the k = 1 and k = 2 lists of a pair start at first[0] / first[1]. */
+#define SPF_KSP2_NONE 0xFFFFFFFFu
+typedef struct spf_ksp2_pair {
+  uint32_t first[2];   /* pool offset of the first k = 1 / k = 2 record */
+  uint32_t n_paths[2]; /* number of k = 1 / k = 2 paths                  */
+} spf_ksp2_pair;
+
+typedef struct spf_ksp2_plan spf_ksp2_plan;
+spf_status spf_ksp2_plan_create(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
+                                spf_ksp2_plan** out);
+void spf_ksp2_plan_destroy(spf_ksp2_plan* plan);
+/* Enqueue on `stream` (NULL = context stream).  d_pairs = [n_src * n_nodes],
+ * d_pool = pool_words u32, d_counters = 4 u64 zeroed by the call:
+ *   [0] pool words claimed (> pool_words means the pool overflowed),
+ *   [1] k = 2 SPF runs (the reference's un-memoised runSpf calls, :778-779),
+ *   [2] bit 0 = overflow.  No host synchronisation, no allocation. */
+spf_status spf_ksp2_execute(spf_ksp2_plan* plan, spf_ksp2_pair* d_pairs, uint32_t* d_pool,
+                            uint64_t pool_words, uint64_t* d_counters, void* stream);
+/* HIP-event kernel timing of the next `max_executes` executes: summed ms of
+ * the k = 1 SPF kernel and of the KSP2 kernel. */
+spf_status spf_ksp2_enable_timing(spf_ksp2_plan* plan, uint32_t max_executes);
+spf_status spf_ksp2_timing(spf_ksp2_plan* plan, double* spf_ms, double* ksp_ms, uint32_t* n);
+/* Convenience: plan + execute (growing the device pool on overflow) + copy
+ * back.  pairs_out = [n_src * n_nodes]; *pool_used = words written.  With
+ * pool_out == NULL or pool_cap < *pool_used only the pairs are copied (the
+ * latter returns SPF_E_NOMEM): call again with a pool of *pool_used words. */
+spf_status spf_ksp2_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
+                          spf_ksp2_pair* pairs_out, uint32_t* pool_out, uint64_t pool_cap,
+                          uint64_t* pool_used);
+
 /* ---- diagnostics ---------------------------------------------------------- */
 /* With SPF_STAMPS set in the environment, the multi-source BFS kernel records
  * s_memtime clocks of workgroup 0 at its phase boundaries (init, then per level:

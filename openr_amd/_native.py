@@ -24,6 +24,7 @@ SPF_E_NOMEM = 5
 SPF_E_STATE = 6
 SPF_UNREACHABLE = 0xFFFFFFFF
 SPF_FLAG_HOP_COUNT = 0x1
+SPF_KSP2_NONE = 0xFFFFFFFF
 
 _STATUS_NAMES = {
     SPF_E_INVALID: "SPF_E_INVALID",
@@ -157,6 +158,12 @@ PROTOTYPES = {
                             _u32p, _u32p, C.c_uint32, _u32p]),
     "spf_solves": (C.c_uint64, [_vp]),
     "spf_debug_stamps": (C.c_int, [_vp, _u64p, C.c_uint32, _u32p]),
+    "spf_ksp2_plan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.POINTER(_vp)]),
+    "spf_ksp2_plan_destroy": (None, [_vp]),
+    "spf_ksp2_execute": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "spf_ksp2_enable_timing": (C.c_int, [_vp, C.c_uint32]),
+    "spf_ksp2_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
+    "spf_ksp2_solve": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _u32p, C.c_uint64, _u64p]),
     # LinkState facade (openr_linkstate.h)
     "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "ls_destroy": (None, [_vp]),

@@ -18,7 +18,8 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 OUT = PKG / "lib" / "libopenr_spf.so"
-SOURCES = [CSRC / "spf_engine.hip", CSRC / "link_state.cpp"]
+SOURCES = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
+INTERNAL = sorted(CSRC.glob("*.h"))
 HEADERS = sorted((ROOT / "include").glob("*.h"))
 
 
@@ -33,7 +34,7 @@ def needs_build() -> bool:
     if not OUT.exists():
         return True
     t = OUT.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS)
+    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS + INTERNAL)
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:

@@ -1,0 +1,132 @@
+// ============================================================================
+//  engine_internal.h -- state shared by the engine's translation units
+//  (spf_engine.hip: SPF/ECMP plans; ksp2.hip: batched KSP2).  Not part of the
+//  C-ABI: include/openr_spf.h is the boundary.
+// ============================================================================
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "openr_spf.h"
+
+namespace spfi {
+
+constexpr uint32_t kInf = SPF_UNREACHABLE;
+
+extern thread_local std::string g_err;
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    reset();
+    const hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  hipError_t upload(const T* h, size_t count, hipStream_t s) {
+    hipError_t e = alloc(count);
+    if (e != hipSuccess || count == 0) return e;
+    return hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s);
+  }
+};
+
+// Launch the per-source SSSP kernel (distances only) over `rows` sources
+// (device list rows_src), writing rows [rows][pitch] of D.
+spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
+                       const uint32_t* ign, uint32_t* D, hipStream_t s);
+// Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
+spf_status set_lds_limits(spf_ctx* c);
+
+}  // namespace spfi
+
+struct spf_ctx {
+  int device = 0;
+  uint32_t n_cu = 256;  // compute units (BFS batch sizing)
+  hipStream_t stream = nullptr;
+  std::string err;
+  uint64_t solves = 0;
+  // graph
+  bool loaded = false;
+  uint32_t N = 0, E = 0, pitch = 0;
+  bool nonpos = false;
+  uint32_t max_metric = 0;
+  std::vector<uint32_t> row_ptr, col, wt, rev, link;
+  std::vector<uint8_t> ovl;
+  std::vector<uint32_t> nb_ptr, nb_id, nb_w;  // distinct up neighbours
+  uint32_t big_nodes = 0;                    // nodes with degree > kBigDeg
+  uint32_t max_link = 0;
+  bool unit = false;                         // every up edge has metric 1
+  uint32_t npitch = 0;                       // narrow (u8) row pitch
+  std::vector<uint32_t> sell_ptr, sell_col;  // sliced-ELL columns (64-node slices)
+  spfi::DevBuf<uint32_t> d_sell_ptr, d_sell_col;
+  spfi::DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
+  spfi::DevBuf<uint8_t> d_ovl;
+  // scratch for spf_preds
+  spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
+  spfi::DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
+};
+
+struct spf_plan {
+  spf_ctx* ctx = nullptr;
+  uint32_t n_src = 0, flags = 0;
+  std::vector<uint32_t> srcs, closure;
+  std::vector<uint64_t> nh_off;
+  std::vector<uint32_t> words;
+  uint64_t nh_total = 0;
+  bool direct = false;  // closure == srcs: D is the caller's dist buffer
+  bool ms = false;      // unit metrics: multi-source BFS + u8 narrow copy
+  spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
+  spfi::DevBuf<uint8_t> d_Dn;
+  spfi::DevBuf<uint64_t> d_nh_off;
+  size_t lds_bytes = 0;
+  bool q16 = true;
+  // optional per-kernel timing: 3 events per execute (before SSSP, between,
+  // after ECMP), ring of `timing_cap` executes
+  std::vector<hipEvent_t> ev;
+  uint32_t timing_cap = 0, timing_n = 0;
+  ~spf_plan() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+};
+
+namespace spfi {
+
+spf_status fail(spf_ctx* c, spf_status st, const char* fmt, ...);
+
+#define HIP_TRY(ctx, expr)                                                   \
+  do {                                                                       \
+    const hipError_t e_ = (expr);                                            \
+    if (e_ != hipSuccess)                                                    \
+      return fail(ctx, SPF_E_HIP, "%s: %s (%s:%d)", #expr,                   \
+                  hipGetErrorString(e_), __FILE__, __LINE__);                \
+  } while (0)
+
+// Upload an ignore set (undirected link ids) as a device bitmap; NULL if empty.
+spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
+                         const uint32_t** dev);
+
+// Launch the per-source SSSP kernel (distances only) over `rows` sources
+// (device list rows_src), writing rows [rows][pitch] of D.
+spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
+                       const uint32_t* ign, uint32_t* D, hipStream_t s);
+// Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
+spf_status set_lds_limits(spf_ctx* c);
+
+}  // namespace spfi

@@ -1,0 +1,477 @@
+// ============================================================================
+//  ksp2.hip -- batched KSP2 (k = 1 and k = 2 edge-disjoint shortest paths)
+//  for every (source, destination) pair of a source batch.
+//
+//  Reference: LinkState::getKthPaths (openr/decision/LinkState.cpp:762-791)
+//  with traceOnePath (:398-419) over the pathLinks of runSpf (:808-882):
+//    k = 1: trace paths in getSpfResult(src) until the shared visited-link set
+//           makes the trace fail;
+//    k = 2: linksToIgnore = every link of the k = 1 paths, a fresh
+//           runSpf(src, true, linksToIgnore), trace again.
+//
+//  GPU mapping (one wavefront per pair, 4 pairs in flight per workgroup):
+//    * the k = 1 distance row of the workgroup's source (computed by the
+//      per-source SSSP kernel beforehand) is staged once in LDS;
+//    * traceOnePath is a DFS with an explicit stack; a DFS step evaluates the
+//      in-edges of the current node across the lanes and picks the first
+//      untried tight one in pathLinks order with a wave min-reduction of the
+//      key (dist[tail], edge id) -- the reference iterates pathLinks in
+//      Dijkstra pop order (dist, name = id) and then linksFromNode order
+//      (= edge id order inside a tail's CSR row).  A link tried once stays in
+//      the visited bitmap, exactly like LinkState.cpp:410-416, so "first
+//      untried candidate" reproduces the recursion's iteration order;
+//    * the k = 2 SPF is a wave-local label-correcting frontier sweep in LDS
+//      over the links not ignored, pruned at the destination's tentative
+//      distance: a node whose distance is >= d'(dst) can never be a tail of a
+//      tight edge on a path to dst (metrics are positive), and tentative
+//      values are upper bounds, so every node the trace inspects is exact.
+//    * paths go to a pool through a per-wave bump allocator (records
+//      [n_links, next, links src->dst]), pairs get a fixed header.
+// ============================================================================
+#include "engine_internal.h"
+
+#include <memory>
+
+using namespace spfi;
+
+namespace {
+
+constexpr int kKspThreads = 256;             // 4 waves, one pair each
+constexpr int kKspWaves = kKspThreads / 64;
+constexpr uint32_t kKspChunk = 64;          // destinations per workgroup
+constexpr uint32_t kPoolGrab = 2048;        // words a wave reserves at a time
+constexpr size_t kMaxLdsKsp = 160 * 1024;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)x, d, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), d, 64);
+    const uint64_t y = ((uint64_t)hi << 32) | lo;
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x, uint32_t* total) {
+  const uint32_t lane = __lane_id();
+  uint32_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  *total = __shfl(inc, 63, 64);
+  return inc - x;
+}
+
+__device__ __forceinline__ bool bit(const uint32_t* bm, uint32_t i) {
+  return (bm[i >> 5] >> (i & 31)) & 1u;
+}
+
+struct KspGraph {
+  const uint32_t* row_ptr;
+  const uint32_t* col;
+  const uint32_t* wt;
+  const uint32_t* rev;
+  const uint32_t* link;
+  const uint8_t* ovl;
+  uint32_t N;
+};
+
+// Per-wave bump allocation in the path pool.  Returns the word offset, or
+// kInf when the pool is exhausted (the counter keeps counting, so the host
+// learns the size it needs).
+struct PoolCursor {
+  uint64_t cur = 0, end = 0;
+};
+
+__device__ uint32_t pool_alloc(PoolCursor& pc, uint32_t words, unsigned long long* used,
+                               uint64_t cap, uint32_t* overflow) {
+  if (pc.cur + words > pc.end) {
+    const uint32_t grab = words > kPoolGrab ? words : kPoolGrab;
+    uint64_t base = 0;
+    if (__lane_id() == 0) base = atomicAdd(used, (unsigned long long)grab);
+    base = __shfl(base, 0, 64);
+    pc.cur = base;
+    pc.end = base + grab;
+  }
+  const uint64_t at = pc.cur;
+  pc.cur += words;
+  if (at + words > cap || at + words > 0xFFFFFFF0ull) {
+    if (__lane_id() == 0) atomicOr(overflow, 1u);
+    return kInf;
+  }
+  return (uint32_t)at;
+}
+
+// traceOnePath (LinkState.cpp:398-419) from dst back to src over the tight
+// in-edges of D (tails expanded, links not in `ign` when given, links not in
+// `vis`).  On success the stack holds the edges dst-first and *depth their
+// count; every link tried is left in `vis`.
+__device__ bool trace_one(const KspGraph& g, const uint32_t* D, const uint32_t* ign,
+                          uint32_t* vis, uint32_t* stack, uint32_t src, uint32_t dst,
+                          uint32_t* depth) {
+  const uint32_t lane = __lane_id();
+  uint32_t k = 0, v = dst;
+  for (;;) {
+    if (v == src) {
+      *depth = k;
+      return true;
+    }
+    const uint32_t dv = D[v];
+    uint64_t best = ~0ull;
+    const uint32_t e_end = g.row_ptr[v + 1];
+    for (uint32_t e = g.row_ptr[v] + lane; e < e_end; e += 64) {
+      // in-edge u -> v is the reverse of the out-edge v -> u
+      const uint32_t u = g.col[e];
+      const uint32_t r = g.rev[e];
+      const uint32_t l = g.link[e];
+      bool ok = !(g.ovl[u] && u != src) && !bit(vis, l) && !(ign && bit(ign, l));
+      if (ok) {
+        const uint32_t du = D[u];
+        ok = du != kInf && du + g.wt[r] == dv;
+        if (ok) best = min(best, ((uint64_t)du << 32) | r);
+      }
+    }
+    best = wave_min64(best);
+    if (best == ~0ull) {  // every pathLink of v tried: back up one level
+      if (k == 0) return false;
+      --k;
+      v = k == 0 ? dst : g.col[g.rev[stack[k - 1]]];
+      continue;
+    }
+    const uint32_t r = (uint32_t)best;
+    const uint32_t l = g.link[r];
+    if (lane == 0) {
+      vis[l >> 5] |= 1u << (l & 31);
+      stack[k] = r;
+    }
+    wave_sync();
+    ++k;
+    v = g.col[g.rev[r]];  // tail of r
+  }
+}
+
+// Writes the traced path as a pool record [n_links, next, links src->dst],
+// chains it after the record at `prev_at` (kInf: first of its list) and
+// returns its offset (kInf if the pool overflowed).  Marks the path's links
+// in `mark` when given.
+__device__ uint32_t emit_path(const KspGraph& g, const uint32_t* stack, uint32_t depth,
+                              uint32_t* pool, PoolCursor& pc, unsigned long long* used,
+                              uint64_t cap, uint32_t* overflow, uint32_t prev_at,
+                              uint32_t* mark) {
+  const uint32_t lane = __lane_id();
+  const uint32_t at = pool_alloc(pc, depth + 2, used, cap, overflow);
+  for (uint32_t j = lane; j < depth; j += 64) {
+    const uint32_t l = g.link[stack[depth - 1 - j]];  // src -> dst order
+    if (mark) atomicOr(&mark[l >> 5], 1u << (l & 31));
+    if (at != kInf) pool[(size_t)at + 2 + j] = l;
+  }
+  if (at != kInf && lane == 0) {
+    pool[at] = depth;
+    pool[(size_t)at + 1] = kInf;
+    if (prev_at != kInf) pool[(size_t)prev_at + 1] = at;
+  }
+  wave_sync();
+  return at;
+}
+
+// Wave-local SPF from src over links not in `ign`, pruned at D[dst].
+__device__ void wave_sssp(const KspGraph& g, uint32_t* D, uint16_t* q, uint32_t* bm,
+                          uint32_t bm_words, const uint32_t* ign, uint32_t src, uint32_t dst,
+                          uint32_t pitch) {
+  const uint32_t lane = __lane_id();
+  for (uint32_t v = lane; v < pitch; v += 64) D[v] = kInf;
+  for (uint32_t i = lane; i < bm_words; i += 64) bm[i] = 0;
+  wave_sync();
+  if (lane == 0) {
+    D[src] = 0;
+    q[0] = (uint16_t)src;
+  }
+  wave_sync();
+  uint32_t qlen = 1;
+  while (qlen) {
+    for (uint32_t i = lane; i < qlen; i += 64) {
+      const uint32_t u = q[i];
+      if (g.ovl[u] && u != src) continue;  // drained: recorded, not expanded
+      const uint32_t du = D[u];
+      const uint32_t bound = D[dst];
+      if (du >= bound) continue;
+      const uint32_t e_end = g.row_ptr[u + 1];
+      for (uint32_t e = g.row_ptr[u]; e < e_end; ++e) {
+        if (bit(ign, g.link[e])) continue;
+        const uint32_t nd = du + g.wt[e];
+        if (nd >= bound) continue;
+        const uint32_t v = g.col[e];
+        if (nd < atomicMin(&D[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+      }
+    }
+    wave_sync();
+    uint32_t n = 0;
+    for (uint32_t base = 0; base < bm_words; base += 64) {
+      const uint32_t i = base + lane;
+      uint32_t word = 0;
+      if (i < bm_words) {
+        word = bm[i];
+        bm[i] = 0;
+      }
+      uint32_t tot;
+      uint32_t at = n + wave_excl_scan32(__popc(word), &tot);
+      while (word) {
+        const uint32_t b = __ffs(word) - 1;
+        word &= word - 1;
+        q[at++] = (uint16_t)(i * 32 + b);
+      }
+      n += tot;
+    }
+    wave_sync();
+    qlen = n;
+  }
+}
+
+__global__ __launch_bounds__(kKspThreads) void ksp2_kernel(
+    KspGraph g, const uint32_t* __restrict__ Dsrc, const uint32_t* __restrict__ srcs,
+    uint32_t n_src, uint32_t pitch, uint32_t lw, uint32_t chunks,
+    spf_ksp2_pair* __restrict__ pairs, uint32_t* __restrict__ pool, uint64_t cap,
+    unsigned long long* __restrict__ counters) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t N = g.N, bm_words = (N + 31) / 32;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t* Ds = reinterpret_cast<uint32_t*>(smem);  // [pitch] k = 1 distances
+  uint32_t* ctl = Ds + pitch;                        // [4] next destination
+  const size_t per_wave = 2ull * pitch + bm_words + 2ull * lw;
+  uint32_t* mine = ctl + 4 + w * per_wave;
+  uint32_t* Dw = mine;                                      // [pitch] k = 2 distances
+  uint32_t* stack = Dw + pitch;                             // [pitch] DFS stack ...
+  uint16_t* q = reinterpret_cast<uint16_t*>(stack);         // ... or SPF queue
+  uint32_t* bm = stack + pitch;                             // [bm_words]
+  uint32_t* ign = bm + bm_words;                            // [lw] k = 1 links
+  uint32_t* vis = ign + lw;                                 // [lw] visited links
+
+  const uint32_t i = blockIdx.x / chunks;
+  const uint32_t c = blockIdx.x % chunks;
+  if (i >= n_src) return;
+  const uint32_t s = srcs[i];
+  {
+    const uint4* in = reinterpret_cast<const uint4*>(Dsrc + (size_t)i * pitch);
+    uint4* o = reinterpret_cast<uint4*>(Ds);
+    for (uint32_t t = tid; t < pitch / 4; t += kKspThreads) o[t] = in[t];
+    if (tid == 0) ctl[0] = c * kKspChunk;
+  }
+  __syncthreads();
+  const uint32_t d_end = min(N, (c + 1) * kKspChunk);
+  unsigned long long* used = counters;
+  uint32_t* overflow = reinterpret_cast<uint32_t*>(counters + 2);
+  PoolCursor pc;
+  uint32_t k2_runs = 0;
+
+  for (;;) {
+    uint32_t d = 0;
+    if (lane == 0) d = atomicAdd(&ctl[0], 1u);
+    d = __shfl(d, 0, 64);
+    if (d >= d_end) break;
+    spf_ksp2_pair hdr;
+    hdr.first[0] = hdr.first[1] = kInf;
+    hdr.n_paths[0] = hdr.n_paths[1] = 0;
+    if (d != s && Ds[d] != kInf) {
+      // ---- k = 1: trace in getSpfResult(src) ----
+      for (uint32_t j = lane; j < lw; j += 64) {
+        vis[j] = 0;
+        ign[j] = 0;
+      }
+      wave_sync();
+      uint32_t prev = kInf;
+      uint32_t depth = 0;
+      uint32_t n1 = 0;
+      while (trace_one(g, Ds, nullptr, vis, stack, s, d, &depth) && depth) {
+        prev = emit_path(g, stack, depth, pool, pc, used, cap, overflow, prev, ign);
+        if (n1++ == 0) hdr.first[0] = prev;
+      }
+      hdr.n_paths[0] = n1;
+      // ---- k = 2: runSpf(src, true, links of the k = 1 paths), trace ----
+      if (n1) {
+        ++k2_runs;
+        wave_sync();
+        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch);
+        if (Dw[d] != kInf) {
+          for (uint32_t j = lane; j < lw; j += 64) vis[j] = 0;
+          wave_sync();
+          prev = kInf;
+          uint32_t n2 = 0;
+          while (trace_one(g, Dw, ign, vis, stack, s, d, &depth) && depth) {
+            prev = emit_path(g, stack, depth, pool, pc, used, cap, overflow, prev, nullptr);
+            if (n2++ == 0) hdr.first[1] = prev;
+          }
+          hdr.n_paths[1] = n2;
+        }
+      }
+    }
+    if (lane == 0) pairs[(size_t)i * N + d] = hdr;
+  }
+  if (lane == 0 && k2_runs) atomicAdd(&counters[1], (unsigned long long)k2_runs);
+}
+
+size_t ksp2_lds_bytes(uint32_t N, uint32_t pitch, uint32_t lw) {
+  const size_t bm_words = (N + 31) / 32;
+  return 4ull * (pitch + 4 + kKspWaves * (2ull * pitch + bm_words + 2ull * lw));
+}
+
+}  // namespace
+
+struct spf_ksp2_plan {
+  spf_ctx* ctx = nullptr;
+  uint32_t n_src = 0, lw = 0;
+  std::vector<uint32_t> srcs;
+  DevBuf<uint32_t> d_srcs, d_D;
+  size_t lds = 0;
+  std::vector<hipEvent_t> ev;
+  uint32_t timing_cap = 0, timing_n = 0;
+  ~spf_ksp2_plan() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+};
+
+extern "C" {
+
+spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
+                                spf_ksp2_plan** out) {
+  if (!c || !out) return fail(c, SPF_E_INVALID, "spf_ksp2_plan_create: NULL argument");
+  *out = nullptr;
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (n_src == 0 || !srcs) return fail(c, SPF_E_INVALID, "empty source list");
+  if (c->nonpos)
+    return fail(c, SPF_E_UNSUPPORTED,
+                "graph has up links with metric <= 0 (KSP2 runs weighted SPF)");
+  if (c->N > 65535) return fail(c, SPF_E_UNSUPPORTED, "KSP2 kernel supports <= 65535 nodes");
+  auto p = std::make_unique<spf_ksp2_plan>();
+  p->ctx = c;
+  p->n_src = n_src;
+  p->srcs.assign(srcs, srcs + n_src);
+  for (uint32_t i = 0; i < n_src; ++i)
+    if (srcs[i] >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
+  p->lw = c->max_link / 32 + 1;
+  p->lds = ksp2_lds_bytes(c->N, c->pitch, p->lw);
+  if (p->lds > kMaxLdsKsp)
+    return fail(c, SPF_E_UNSUPPORTED, "KSP2 working set of %zu B exceeds the LDS (%u nodes)",
+                p->lds, c->N);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
+  {
+    const spf_status st = set_lds_limits(c);
+    if (st != SPF_OK) return st;
+  }
+  HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
+  HIP_TRY(c, p->d_D.alloc((size_t)n_src * c->pitch));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  *out = p.release();
+  return SPF_OK;
+}
+
+void spf_ksp2_plan_destroy(spf_ksp2_plan* p) { delete p; }
+
+spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* d_pool,
+                            uint64_t pool_words, uint64_t* d_counters, void* stream) {
+  if (!p) return fail(nullptr, SPF_E_INVALID, "spf_ksp2_execute: NULL plan");
+  spf_ctx* c = p->ctx;
+  if (!c->loaded) return fail(c, SPF_E_STATE, "graph no longer loaded");
+  if (!d_pairs || !d_counters || (pool_words && !d_pool))
+    return fail(c, SPF_E_INVALID, "spf_ksp2_execute: NULL output buffer");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipEvent_t* ev = nullptr;
+  if (p->timing_cap) {
+    ev = &p->ev[3 * (p->timing_n % p->timing_cap)];
+    ++p->timing_n;
+    HIP_TRY(c, hipEventRecord(ev[0], s));
+  }
+  HIP_TRY(c, hipMemsetAsync(d_counters, 0, 4 * sizeof(uint64_t), s));
+  spf_status st = launch_sssp(c, p->d_srcs.p, p->n_src, false, nullptr, p->d_D.p, s);
+  if (st != SPF_OK) return st;
+  if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
+  KspGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p, c->N};
+  const uint32_t chunks = (c->N + kKspChunk - 1) / kKspChunk;
+  hipLaunchKernelGGL(ksp2_kernel, dim3(p->n_src * chunks), dim3(kKspThreads), p->lds, s, g,
+                     p->d_D.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, d_pairs, d_pool,
+                     pool_words, reinterpret_cast<unsigned long long*>(d_counters));
+  HIP_TRY(c, hipGetLastError());
+  if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+  c->solves += p->n_src;  // k = 2 runs are added by spf_ksp2_solve / the caller
+  return SPF_OK;
+}
+
+spf_status spf_ksp2_enable_timing(spf_ksp2_plan* p, uint32_t max_executes) {
+  if (!p) return SPF_E_INVALID;
+  spf_ctx* c = p->ctx;
+  for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  p->ev.assign(3ull * max_executes, nullptr);
+  for (auto& e : p->ev) HIP_TRY(c, hipEventCreate(&e));
+  p->timing_cap = max_executes;
+  p->timing_n = 0;
+  return SPF_OK;
+}
+
+spf_status spf_ksp2_timing(spf_ksp2_plan* p, double* spf_ms, double* ksp_ms, uint32_t* n) {
+  if (!p || !p->timing_cap) return SPF_E_STATE;
+  spf_ctx* c = p->ctx;
+  const uint32_t cnt = std::min(p->timing_n, p->timing_cap);
+  double a = 0, b = 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    float t0 = 0, t1 = 0;
+    HIP_TRY(c, hipEventSynchronize(p->ev[3 * i + 2]));
+    HIP_TRY(c, hipEventElapsedTime(&t0, p->ev[3 * i], p->ev[3 * i + 1]));
+    HIP_TRY(c, hipEventElapsedTime(&t1, p->ev[3 * i + 1], p->ev[3 * i + 2]));
+    a += t0;
+    b += t1;
+  }
+  if (spf_ms) *spf_ms = a;
+  if (ksp_ms) *ksp_ms = b;
+  if (n) *n = cnt;
+  p->timing_n = 0;
+  return SPF_OK;
+}
+
+spf_status spf_ksp2_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
+                          spf_ksp2_pair* pairs_out, uint32_t* pool_out, uint64_t pool_cap,
+                          uint64_t* pool_used) {
+  if (!c || !pairs_out || !pool_used) return fail(c, SPF_E_INVALID, "spf_ksp2_solve: NULL argument");
+  spf_ksp2_plan* raw = nullptr;
+  spf_status st = spf_ksp2_plan_create(c, srcs, n_src, &raw);
+  if (st != SPF_OK) return st;
+  std::unique_ptr<spf_ksp2_plan> p(raw);
+  const size_t n_pairs = (size_t)n_src * c->N;
+  DevBuf<spf_ksp2_pair> d_pairs;
+  DevBuf<uint32_t> d_pool;
+  DevBuf<uint64_t> d_cnt;
+  HIP_TRY(c, d_pairs.alloc(n_pairs));
+  HIP_TRY(c, d_cnt.alloc(4));
+  uint64_t cap = std::max<uint64_t>(pool_cap, (uint64_t)n_pairs * 16 + kPoolGrab * 4096ull);
+  uint64_t cnt[4] = {0, 0, 0, 0};
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(c, d_pool.alloc(cap));
+    st = spf_ksp2_execute(p.get(), d_pairs.p, d_pool.p, cap, d_cnt.p, c->stream);
+    if (st != SPF_OK) return st;
+    HIP_TRY(c, hipMemcpyAsync(cnt, d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (!(cnt[2] & 1)) break;
+    cap = cnt[0] + cnt[0] / 4;  // overflowed: the counter says how much it wanted
+  }
+  if (cnt[2] & 1) return fail(c, SPF_E_NOMEM, "KSP2 path pool overflow");
+  c->solves += cnt[1];
+  *pool_used = cnt[0];
+  HIP_TRY(c, hipMemcpy(pairs_out, d_pairs.p, n_pairs * sizeof(spf_ksp2_pair),
+                       hipMemcpyDeviceToHost));
+  if (!pool_out) return SPF_OK;
+  if (pool_cap < cnt[0])
+    return fail(c, SPF_E_NOMEM, "pool_out holds %llu words, %llu needed",
+                (unsigned long long)pool_cap, (unsigned long long)cnt[0]);
+  if (cnt[0]) HIP_TRY(c, hipMemcpy(pool_out, d_pool.p, cnt[0] * 4, hipMemcpyDeviceToHost));
+  return SPF_OK;
+}
+
+}  // extern "C"

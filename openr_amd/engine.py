@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -95,6 +95,63 @@ class SpfPlan:
         self.execute(dist.data_ptr(), nh.data_ptr(), s)
 
 
+KSP2_NONE = N.SPF_KSP2_NONE
+PAIR_DTYPE = np.dtype([("first", "<u4", (2,)), ("n_paths", "<u4", (2,))])  # spf_ksp2_pair
+
+
+@dataclass
+class Ksp2Result:
+    """All-destinations KSP2 of a source batch (include/openr_spf.h)."""
+
+    srcs: np.ndarray  # [n_src]
+    n_nodes: int
+    pairs: np.ndarray  # [n_src * n_nodes] PAIR_DTYPE
+    pool: np.ndarray  # u32 path records [n_links, next, links...]
+
+    def paths(self, i: int, d: int, k: int) -> List[List[int]]:
+        """getKthPaths(srcs[i], d, k) for k in (1, 2): lists of link ids."""
+        rec = self.pairs[i * self.n_nodes + d]
+        out: List[List[int]] = []
+        at = int(rec["first"][k - 1])
+        for _ in range(int(rec["n_paths"][k - 1])):
+            n = int(self.pool[at])
+            out.append([int(x) for x in self.pool[at + 2: at + 2 + n]])
+            at = int(self.pool[at + 1])
+        return out
+
+
+class Ksp2Plan:
+    """A fixed source batch for batched KSP2 (``spf_ksp2_plan``)."""
+
+    def __init__(self, eng: "SpfEngine", srcs: Sequence[int]) -> None:
+        self._eng = eng
+        self.srcs = np.ascontiguousarray(srcs, np.uint32)
+        h = C.c_void_p()
+        eng._err(N.lib.spf_ksp2_plan_create(eng._h, N.ptr(self.srcs), len(self.srcs), C.byref(h)))
+        self._h = h
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        lib = getattr(N, "lib", None)
+        if h is not None and h.value and lib is not None:
+            lib.spf_ksp2_plan_destroy(h)
+            self._h = C.c_void_p()
+
+    def execute(self, d_pairs: int, d_pool: int, pool_words: int, d_counters: int,
+                stream: int = 0) -> None:
+        self._eng._err(N.lib.spf_ksp2_execute(self._h, C.c_void_p(d_pairs), C.c_void_p(d_pool),
+                                              pool_words, C.c_void_p(d_counters),
+                                              C.c_void_p(stream) if stream else None))
+
+    def enable_timing(self, max_executes: int) -> None:
+        self._eng._err(N.lib.spf_ksp2_enable_timing(self._h, max_executes))
+
+    def timing(self) -> Tuple[float, float, int]:
+        a, b, n = C.c_double(), C.c_double(), C.c_uint32()
+        self._eng._err(N.lib.spf_ksp2_timing(self._h, C.byref(a), C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
+
+
 class SpfEngine:
     """An engine context with one graph loaded (``spf_ctx``)."""
 
@@ -173,6 +230,27 @@ class SpfEngine:
         self._err(N.lib.spf_solve(self._h, N.ptr(p.srcs), p.n_src, p.flags, N.ptr(dist),
                                   N.ptr(nh)))
         return SolveResult(dist, nh, p.nh_off, p.words, self.pitch)
+
+    def ksp2_plan(self, srcs: Sequence[int]) -> Ksp2Plan:
+        return Ksp2Plan(self, srcs)
+
+    def ksp2(self, srcs: Sequence[int]) -> Ksp2Result:
+        """getKthPaths(s, d, 1) and (s, d, 2) for every s in srcs, every d."""
+        srcs = np.ascontiguousarray(srcs, np.uint32)
+        n = self.n_nodes
+        pairs = np.zeros(len(srcs) * n, PAIR_DTYPE)
+        used = C.c_uint64()
+        pool = np.empty(len(pairs) * 12 + (1 << 20), np.uint32)  # lazily backed
+        for _ in range(2):
+            st = N.lib.spf_ksp2_solve(self._h, N.ptr(srcs), len(srcs),
+                                      N.ptr(pairs.view(np.uint32)), N.ptr(pool), pool.size,
+                                      C.byref(used))
+            if st != N.SPF_E_NOMEM or used.value <= pool.size:
+                break
+            pool = np.empty(used.value, np.uint32)  # too small: size it exactly, rerun
+        self._err(st)
+        pool = pool[: used.value]
+        return Ksp2Result(srcs, n, pairs, pool)
 
     def sssp(self, src: int, hop: bool = False,
              ignore_links: Optional[Sequence[int]] = None) -> np.ndarray:

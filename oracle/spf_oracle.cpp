@@ -528,6 +528,8 @@ class LinkState {
     return kspMemo_.emplace(key, std::move(paths)).first->second;
   }
 
+  void dropKspMemo() const { kspMemo_.clear(); }
+
  private:
   void clearMemo() {
     spfMemo_.clear();
@@ -860,6 +862,20 @@ uint64_t orc_ls_time_sources(orc_ls* p, const char* const* srcs, uint32_t n,
   for (uint32_t i = 0; i < n; ++i) {
     orc::SpfResult r = p->ls.runSpf(srcs[i], ulm != 0);
     for (const auto& kv : r) acc += kv.second.metric * 31 + kv.second.nextHops.size();
+  }
+  return acc;
+}
+
+// Time-only KSP2 baseline: getKthPaths(src, d, 1) then (src, d, 2) for every
+// d (k = 1 reuses the memoised SPF of src, exactly as the reference's
+// kthPathResults_/spfResults_ memos do); the k-paths memo is dropped after
+// each pair so memory stays flat.  Returns a checksum of the path lengths.
+uint64_t orc_ls_time_ksp2(orc_ls* p, const char* src, const char* const* dsts, uint32_t n) {
+  uint64_t acc = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    for (size_t k = 1; k <= 2; ++k)
+      for (const auto& path : p->ls.kthPaths(src, dsts[i], k)) acc = acc * 31 + path.size() + k;
+    p->ls.dropKspMemo();
   }
   return acc;
 }

@@ -48,6 +48,7 @@ def _load() -> C.CDLL:
         "orc_ls_dense": (C.c_int, [vp, C.c_char_p, u32p, u32p, C.c_uint32, u32p, C.c_uint32,
                                    C.c_int, u64p, u32p, u64p, u32p]),
         "orc_ls_time_sources": (C.c_uint64, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.c_int]),
+        "orc_ls_time_ksp2": (C.c_uint64, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -156,6 +157,11 @@ class OracleLinkState:
     def time_sources(self, srcs: Sequence[str], ulm: bool = True) -> int:
         arr = (C.c_char_p * len(srcs))(*[s.encode() for s in srcs])
         return int(lib.orc_ls_time_sources(self._h, arr, len(srcs), int(ulm)))
+
+
+    def time_ksp2(self, src: str, dsts: Sequence[str]) -> int:
+        arr = (C.c_char_p * len(dsts))(*[s.encode() for s in dsts])
+        return int(lib.orc_ls_time_ksp2(self._h, src.encode(), arr, len(dsts)))
 
 
 def spf_runs() -> int:
