@@ -17,6 +17,9 @@ Other BASELINE configs (--workload):
   wan_ksp2   configs[3]: getKthPaths(s, d, 1) and (s, d, 2) for ALL pairs of the
              2000-node WAN graph; sources sharded over ranks (strong scaling),
              every rank's paths gathered to rank 0 with RCCL inside the step.
+  ba_whatif  configs[4]: SPF of one source re-run for every single-link failure
+             of a 250k-node / 1M-link scale-free graph, per-failure digests;
+             failures sharded over ranks, digests gathered with RCCL.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fabric_full]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -228,8 +231,95 @@ class Ksp2AllPairs:
                           "oracle/spf_oracle.cpp)"}
 
 
+class WhatIfAllLinks:
+    """configs[4]: SPF of node "0" re-run for every single-link failure of the
+    Barabasi-Albert graph (250k nodes, ~1M links), one digest per failure
+    (include/openr_spf.h spf_whatif_*).  Failures dealt round-robin over ranks
+    (strong scaling); every rank recomputes the unfailed SPF and its digests
+    are gathered to rank 0 with RCCL inside the step."""
+
+    scaling = "strong"
+    unit = "failures/s"
+    kernels = ("base", "failures")
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        import torch
+
+        from openr_amd import topology as T
+        from openr_amd.engine import DIGEST_DTYPE
+        from openr_amd.link_state import LinkState
+
+        self.topo = T.barabasi_albert(250_000, 4, seed=1)
+        self.desc = ("Barabasi-Albert N=250000 m=4 seed=1, metrics U[1,16]; source \"0\"; "
+                     "every single-link failure (SURVEY.md §8(d) config 5)")
+        ls = LinkState(device=-1)
+        ls.updateAdjacencyDatabases(self.topo.lsdb)
+        names, rp, col, met, lid, ovl = ls.flatten()
+        self.ls, self.names = ls, names
+        self.n, self.e = len(names), len(col)
+        eng = eng_cls(dev.index)
+        eng.load(rp, col, met, lid, ovl)
+        self.eng, self.dev, self.rank, self.world = eng, dev, rank, world
+        self.src = names.index("0")
+        all_links = np.unique(lid).astype(np.uint32)  # every up link
+        self.links = all_links[rank::world]
+        self.plan = eng.whatif_plan(self.src, self.links)
+        self.units = len(self.links)
+        self.d_out = torch.empty(max(1, self.units) * DIGEST_DTYPE.itemsize // 8,
+                                 dtype=torch.int64, device=dev)
+        self.d_base = torch.empty(2, dtype=torch.int64, device=dev)
+        # SURVEY.md §8(d): a what-if solve is B_solve with a 24 B digest in
+        # place of the dense result: 4(N+1) + 8E + N + 24
+        n, e = self.n, self.e
+        self.bytes_launch = int((self.units + 1) * (4 * (n + 1) + 8 * e + n + 24))
+        self.parallelism = (f"failures dealt round-robin over {world} rank(s), graph replicated, "
+                            "unfailed SPF recomputed per rank; digests gathered to rank 0 "
+                            "(RCCL gather) in the step")
+
+    def step(self, stream) -> None:
+        import torch
+        import torch.distributed as dist
+
+        self.plan.execute(self.d_out.data_ptr(), self.d_base.data_ptr(), stream.cuda_stream)
+        if self.world > 1:
+            dst = ([torch.empty_like(self.d_out) for _ in range(self.world)]
+                   if self.rank == 0 else None)
+            dist.gather(self.d_out, dst, dst=0)
+
+    def enable_timing(self, k: int) -> None:
+        self.plan.enable_timing(k)
+
+    def kernel_ms(self):
+        a, b, cnt = self.plan.timing()
+        self.n_hot, self.n_big = self.plan.stats()
+        return {"base": a / max(cnt, 1), "failures": b / max(cnt, 1)}
+
+    def edges_per_unit(self) -> int:
+        return self.e - 2
+
+    def cpu_baseline(self, budget_s: float):
+        orc = oracle()()
+        from oracle import time_whatif  # tests/ is on sys.path now
+
+        orc.update_packed(self.topo.lsdb)
+        rng = np.random.default_rng(0)
+        order = rng.permutation(len(self.links))
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s and done < len(order):
+            lk = self.ls._link(int(self.links[order[done]]))
+            time_whatif(orc, "0", [(lk._n1, lk._if1)], fast=True)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "failures/s", "cores": 1, "kind": "port",
+                "sample": f"{done} seeded-random single-link failures, one full runSpf each "
+                          f"({dt:.1f} s on 1 core of {cpu_model()}; oracle/spf_oracle.cpp "
+                          "runSpfFast: same result as the reference's runSpf with a lazy heap "
+                          "instead of make_heap per decrease, which needs ~18 min per run on "
+                          "this graph)"}
+
+
 WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
-             "wan_ksp2": Ksp2AllPairs}
+             "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks}
 
 
 def main() -> None:
@@ -300,8 +390,10 @@ def main() -> None:
             traffic = None
 
     out = {
-        "metric": METRIC if isinstance(wl, AllSources) else
-        "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN",
+        "metric": METRIC if isinstance(wl, AllSources) else (
+            "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN"
+            if isinstance(wl, Ksp2AllPairs) else
+            "what-if single-link-failure SPF reruns/sec, 1M-link scale-free graph"),
         "value": value,
         "unit": wl.unit,
         "n_gpus": world,

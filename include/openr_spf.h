@@ -185,6 +185,50 @@ spf_status spf_ksp2_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
                           spf_ksp2_pair* pairs_out, uint32_t* pool_out, uint64_t pool_cap,
                           uint64_t* pool_used);
 
+/* ---- what-if batches: one source, every single-link failure -------------- */
+/* For each failed link l of the list: the reference's
+ * runSpf(src, true, {l}) (LinkState.cpp:808-882 with linksToIgnore = {l}),
+ * reduced to a digest against the unfailed runSpf(src):
+ *   n_dist_changed  nodes whose metric changed (incl. becoming unreachable)
+ *   n_nh_changed    nodes whose nextHops() changed (incl. becoming unreachable)
+ *   hash            sum over reachable v of
+ *                     mix(mix(v + 1) + metric(v)) ^ fnv1a64(nh(v) as u32 words)
+ *                   mod 2^64, mix = splitmix64's finaliser, nh(v) = bitset over
+ *                   the distinct up neighbours of src in the unfailed graph
+ *                   (ascending id), ceil(k/32) words.
+ * The unfailed result's digest is {0, 0, hash}.  Works on graphs of any size
+ * (global-memory kernels); weighted metrics must be positive. */
+typedef struct spf_whatif_digest {
+  uint32_t n_dist_changed;
+  uint32_t n_nh_changed;
+  uint64_t hash;
+} spf_whatif_digest;
+
+typedef struct spf_whatif_plan spf_whatif_plan;
+/* fail_links: undirected link ids (spf_graph.link_id) of up links; NULL =
+ * every up link of the graph in ascending id order. */
+spf_status spf_whatif_plan_create(spf_ctx* ctx, uint32_t src, const uint32_t* fail_links,
+                                  uint32_t n_fail, spf_whatif_plan** out);
+void spf_whatif_plan_destroy(spf_whatif_plan* plan);
+uint32_t spf_whatif_plan_failures(const spf_whatif_plan* plan);
+spf_status spf_whatif_plan_links(const spf_whatif_plan* plan, uint32_t* links /* [n_fail] */);
+/* d_out = [n_fail] digests, d_base = 1 digest (may be NULL).  Enqueued on
+ * `stream`; the unfailed next-hop propagation synchronises the stream once
+ * per DAG level (host-side convergence test). */
+spf_status spf_whatif_execute(spf_whatif_plan* plan, spf_whatif_digest* d_out,
+                              spf_whatif_digest* d_base, void* stream);
+/* After an execute: failures that needed a re-solve (tight links) and those
+ * re-solved by whole workgroups (large affected region). */
+spf_status spf_whatif_stats(spf_whatif_plan* plan, uint32_t* n_hot, uint32_t* n_big);
+spf_status spf_whatif_enable_timing(spf_whatif_plan* plan, uint32_t max_executes);
+/* summed ms of the unfailed solve (SPF + next hops + hash) and of the failures */
+spf_status spf_whatif_timing(spf_whatif_plan* plan, double* base_ms, double* fail_ms,
+                             uint32_t* n);
+/* Convenience: plan + execute + copy back. out = [n_fail] (n_fail = number of
+ * up links when fail_links is NULL), base may be NULL. */
+spf_status spf_whatif_solve(spf_ctx* ctx, uint32_t src, const uint32_t* fail_links,
+                            uint32_t n_fail, spf_whatif_digest* out, spf_whatif_digest* base);
+
 /* ---- diagnostics ---------------------------------------------------------- */
 /* With SPF_STAMPS set in the environment, the multi-source BFS kernel records
  * s_memtime clocks of workgroup 0 at its phase boundaries (init, then per level:

@@ -164,6 +164,15 @@ PROTOTYPES = {
     "spf_ksp2_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_ksp2_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
     "spf_ksp2_solve": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _u32p, C.c_uint64, _u64p]),
+    "spf_whatif_plan_create": (C.c_int, [_vp, C.c_uint32, _u32p, C.c_uint32, C.POINTER(_vp)]),
+    "spf_whatif_plan_destroy": (None, [_vp]),
+    "spf_whatif_plan_failures": (C.c_uint32, [_vp]),
+    "spf_whatif_plan_links": (C.c_int, [_vp, _u32p]),
+    "spf_whatif_execute": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "spf_whatif_stats": (C.c_int, [_vp, _u32p, _u32p]),
+    "spf_whatif_enable_timing": (C.c_int, [_vp, C.c_uint32]),
+    "spf_whatif_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
+    "spf_whatif_solve": (C.c_int, [_vp, C.c_uint32, _u32p, C.c_uint32, _vp, _vp]),
     # LinkState facade (openr_linkstate.h)
     "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "ls_destroy": (None, [_vp]),

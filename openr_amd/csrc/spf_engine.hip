@@ -765,9 +765,6 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     }
     c->nb_ptr[u + 1] = (uint32_t)c->nb_id.size();
   }
-  if (sssp_lds_bytes(N, c->pitch, c->big_nodes, N <= 65535) > kMaxLds)
-    return fail(c, SPF_E_UNSUPPORTED,
-                "graph with %u nodes exceeds the LDS-resident SSSP kernel (max ~20k nodes)", N);
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, c->d_row_ptr.upload(c->row_ptr.data(), N + 1, c->stream));
   HIP_TRY(c, c->d_col.upload(c->col.data(), E, c->stream));
@@ -895,6 +892,10 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
+  if (!p->ms && p->lds_bytes > kMaxLds)
+    return fail(c, SPF_E_UNSUPPORTED,
+                "batched plans keep a distance row per source in LDS: %u nodes do not fit "
+                "(single-source spf_sssp and what-if batches handle large graphs)", N);
   if (p->ms) HIP_TRY(c, p->d_Dn.alloc((size_t)p->closure.size() * c->npitch));
   {
     const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
@@ -1159,7 +1160,13 @@ spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ig
   if (st != SPF_OK) return st;
   HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
   HIP_TRY(c, c->d_row.alloc(c->pitch));
-  st = launch_sssp(c, c->d_one_src.p, 1, hop, ign, c->d_row.p, c->stream);
+  if (sssp_lds_bytes(c->N, c->pitch, c->big_nodes, c->N <= 65535) > kMaxLds) {
+    HIP_TRY(c, c->d_gq.alloc(c->N));
+    HIP_TRY(c, c->d_gbm.alloc((c->N + 31) / 32));
+    st = launch_gsssp(c, src, hop, ign, c->d_row.p, c->d_gq.p, c->d_gbm.p, c->stream);
+  } else {
+    st = launch_sssp(c, c->d_one_src.p, 1, hop, ign, c->d_row.p, c->stream);
+  }
   if (st != SPF_OK) return st;
   HIP_TRY(c, hipMemcpyAsync(dist_out, c->d_row.p, 4ull * c->N, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -152,6 +152,51 @@ class Ksp2Plan:
         return a.value, b.value, n.value
 
 
+DIGEST_DTYPE = np.dtype([("n_dist_changed", "<u4"), ("n_nh_changed", "<u4"),
+                         ("hash", "<u8")])  # spf_whatif_digest
+
+
+class WhatIfPlan:
+    """One source, a list of single-link failures (``spf_whatif_plan``)."""
+
+    def __init__(self, eng: "SpfEngine", src: int, links: Optional[Sequence[int]]) -> None:
+        self._eng = eng
+        h = C.c_void_p()
+        arr = None if links is None else np.ascontiguousarray(links, np.uint32)
+        eng._err(N.lib.spf_whatif_plan_create(eng._h, src, None if arr is None else N.ptr(arr),
+                                              0 if arr is None else len(arr), C.byref(h)))
+        self._h = h
+        self.n_fail = int(N.lib.spf_whatif_plan_failures(h))
+        self.links = np.zeros(max(1, self.n_fail), np.uint32)
+        eng._err(N.lib.spf_whatif_plan_links(h, N.ptr(self.links)))
+        self.links = self.links[: self.n_fail]
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        lib = getattr(N, "lib", None)
+        if h is not None and h.value and lib is not None:
+            lib.spf_whatif_plan_destroy(h)
+            self._h = C.c_void_p()
+
+    def execute(self, d_out: int, d_base: int = 0, stream: int = 0) -> None:
+        self._eng._err(N.lib.spf_whatif_execute(self._h, C.c_void_p(d_out),
+                                                C.c_void_p(d_base) if d_base else None,
+                                                C.c_void_p(stream) if stream else None))
+
+    def stats(self) -> Tuple[int, int]:
+        a, b = C.c_uint32(), C.c_uint32()
+        self._eng._err(N.lib.spf_whatif_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def enable_timing(self, max_executes: int) -> None:
+        self._eng._err(N.lib.spf_whatif_enable_timing(self._h, max_executes))
+
+    def timing(self) -> Tuple[float, float, int]:
+        a, b, n = C.c_double(), C.c_double(), C.c_uint32()
+        self._eng._err(N.lib.spf_whatif_timing(self._h, C.byref(a), C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
+
+
 class SpfEngine:
     """An engine context with one graph loaded (``spf_ctx``)."""
 
@@ -251,6 +296,21 @@ class SpfEngine:
         self._err(st)
         pool = pool[: used.value]
         return Ksp2Result(srcs, n, pairs, pool)
+
+    def whatif_plan(self, src: int, links: Optional[Sequence[int]] = None) -> WhatIfPlan:
+        return WhatIfPlan(self, src, links)
+
+    def whatif(self, src: int, links: Optional[Sequence[int]] = None):
+        """Digests of runSpf(src, true, {l}) for each failed link l (every up
+        link when `links` is None): (links, digests[n], base digest)."""
+        if links is None:
+            links = self.whatif_plan(src).links
+        arr = np.ascontiguousarray(links, np.uint32)
+        out = np.zeros(max(1, len(arr)), DIGEST_DTYPE)
+        base = np.zeros(1, DIGEST_DTYPE)
+        self._err(N.lib.spf_whatif_solve(self._h, src, N.ptr(arr), len(arr),
+                                         out.ctypes.data, base.ctypes.data))
+        return arr, out[: len(arr)], base[0]
 
     def sssp(self, src: int, hop: bool = False,
              ignore_links: Optional[Sequence[int]] = None) -> np.ndarray:

@@ -460,6 +460,61 @@ class LinkState {
     return result;
   }
 
+  // runSpf with a lazy-deletion heap instead of DijkstraQ's make_heap after
+  // every strict decrease.  Pops follow the same (metric, name) order over
+  // the current labels and the relax step is the same code, so the result is
+  // identical; only the heap maintenance is O(log n).  Used where the
+  // reference's O(n) reMake makes a faithful run impractically slow (the
+  // 250k-node what-if graph: ~18 min per run) and pinned to runSpf by
+  // tests/test_oracle_whatif.py.
+  SpfResult runSpfFast(const std::string& src, bool useLinkMetric,
+                       const LinkSet& ignore = {}) const {
+    SpfResult result;
+    ++g_spf_runs;
+    using Item = std::pair<Metric, const std::string*>;
+    auto cmp = [](const Item& a, const Item& b) {
+      if (a.first != b.first) return a.first > b.first;
+      return *a.second > *b.second;
+    };
+    std::vector<Item> heap;
+    std::unordered_map<std::string, NodeResult> open;
+    open.emplace(src, NodeResult(0));
+    // heap items point at names owned by the Links (or at src): stable for
+    // the whole run, unlike the keys of `open`, which are erased on settle
+    heap.emplace_back(0, &src);
+    while (!heap.empty()) {
+      std::pop_heap(heap.begin(), heap.end(), cmp);
+      const Item top = heap.back();
+      heap.pop_back();
+      auto oit = open.find(*top.second);
+      if (oit == open.end() || oit->second.metric != top.first) continue;  // stale
+      auto ins = result.emplace(oit->first, std::move(oit->second));
+      open.erase(oit);
+      if (!ins.second) abort();
+      const std::string& u = ins.first->first;
+      const Metric du = ins.first->second.metric;
+      const auto& nhU = ins.first->second.nextHops;
+      if (nodeOverloaded(u) && u != src) continue;  // drained: no transit
+      for (const auto& l : linksFrom(u)) {
+        const std::string& v = l->other(u);
+        if (!l->isUp() || result.count(v) || ignore.count(l)) continue;
+        const Metric w = useLinkMetric ? l->metricFrom(u) : 1;
+        auto it = open.find(v);
+        if (it == open.end()) it = open.emplace(v, NodeResult(du + w)).first;
+        NodeResult& r = it->second;
+        if (r.metric >= du + w) {
+          if (r.metric > du + w) r.reset(du + w);
+          r.pathLinks.emplace_back(l, u);
+          r.nextHops.insert(nhU.begin(), nhU.end());
+          if (r.nextHops.empty()) r.nextHops.insert(v);
+          heap.emplace_back(r.metric, &v);
+          std::push_heap(heap.begin(), heap.end(), cmp);
+        }
+      }
+    }
+    return result;
+  }
+
   const SpfResult& getSpfResult(const std::string& n, bool useLinkMetric) const {
     auto key = std::make_pair(n, useLinkMetric);
     auto it = spfMemo_.find(key);
@@ -876,6 +931,113 @@ uint64_t orc_ls_time_ksp2(orc_ls* p, const char* src, const char* const* dsts, u
     for (size_t k = 1; k <= 2; ++k)
       for (const auto& path : p->ls.kthPaths(src, dsts[i], k)) acc = acc * 31 + path.size() + k;
     p->ls.dropKspMemo();
+  }
+  return acc;
+}
+
+// ---- what-if digests ------------------------------
+// Result digest of runSpf(src, true, {link}) -- or of the unfailed SPF when
+// fail_node is NULL -- over node ids = the caller's names table (ascending):
+//   n_dist_changed / n_nh_changed against the unfailed result (a node that
+//   becomes unreachable counts in both), and
+//   hash = sum over reachable v of mix(mix(v + 1) + metric(v)) ^ fnv(nh bitset)
+// (mod 2^64), the nh bitset having bit j = j-th distinct up neighbour (by
+// name) of src in the UNFAILED graph, as u32 words, ceil(k/32) of them.
+// The link is the one of fail_node's links whose interface on fail_node is
+// fail_if.  fast != 0 uses runSpfFast.
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+struct orc_digest {
+  uint32_t n_dist_changed, n_nh_changed;
+  uint64_t hash;
+};
+int orc_ls_whatif_digests(orc_ls* p, const char* node_blob, const uint32_t* node_off,
+                          const uint32_t* node_len, uint32_t n_nodes, const char* src,
+                          const char* const* fail_nodes, const char* const* fail_ifs,
+                          uint32_t n_fail, int fast, orc_digest* base_out, orc_digest* out) {
+  std::unordered_map<std::string, uint32_t> idOf;
+  idOf.reserve(n_nodes * 2);
+  for (uint32_t i = 0; i < n_nodes; ++i)
+    idOf.emplace(std::string(node_blob + node_off[i], node_len[i]), i);
+  const std::string s(src);
+  std::set<std::string> nbrSet;
+  for (const auto& l : p->ls.linksFrom(s))
+    if (l->isUp()) nbrSet.insert(l->other(s));
+  std::unordered_map<std::string, uint32_t> bitOf;
+  uint32_t b = 0;
+  for (const auto& n : nbrSet) bitOf[n] = b++;
+  const uint32_t words = (b + 31) / 32;
+  auto render = [&](const orc::SpfResult& r, std::vector<uint64_t>& dist,
+                    std::vector<uint32_t>& nh) {
+    dist.assign(n_nodes, UINT64_MAX);
+    nh.assign((size_t)n_nodes * words, 0);
+    for (const auto& kv : r) {
+      auto it = idOf.find(kv.first);
+      if (it == idOf.end()) continue;
+      dist[it->second] = kv.second.metric;
+      for (const auto& h : kv.second.nextHops) {
+        const uint32_t j = bitOf.at(h);
+        nh[(size_t)it->second * words + (j >> 5)] |= 1u << (j & 31);
+      }
+    }
+  };
+  auto run = [&](const orc::LinkSet& ign) {
+    return fast ? p->ls.runSpfFast(s, true, ign) : p->ls.runSpf(s, true, ign);
+  };
+  auto digest = [&](const std::vector<uint64_t>& d0, const std::vector<uint32_t>& h0,
+                    const std::vector<uint64_t>& d1, const std::vector<uint32_t>& h1) {
+    orc_digest dg{0, 0, 0};
+    for (uint32_t v = 0; v < n_nodes; ++v) {
+      const uint32_t* a = &h0[(size_t)v * words];
+      const uint32_t* c = &h1[(size_t)v * words];
+      if (d0[v] != d1[v]) ++dg.n_dist_changed;
+      if ((d0[v] == UINT64_MAX) != (d1[v] == UINT64_MAX) || !std::equal(a, a + words, c))
+        ++dg.n_nh_changed;
+      if (d1[v] == UINT64_MAX) continue;
+      uint64_t f = 0xcbf29ce484222325ULL;
+      for (uint32_t w = 0; w < words; ++w) {
+        f ^= c[w];
+        f *= 0x100000001b3ULL;
+      }
+      dg.hash += mix64(mix64((uint64_t)v + 1) + d1[v]) ^ f;
+    }
+    return dg;
+  };
+  std::vector<uint64_t> d0, d1;
+  std::vector<uint32_t> h0, h1;
+  render(run({}), d0, h0);
+  if (base_out) *base_out = digest(d0, h0, d0, h0);
+  for (uint32_t i = 0; i < n_fail; ++i) {
+    orc::LinkSet ignore;
+    for (const auto& l : p->ls.linksFrom(fail_nodes[i]))
+      if (l->ifaceFrom(fail_nodes[i]) == fail_ifs[i]) {
+        ignore.insert(l);
+        break;
+      }
+    if (ignore.empty()) return -1 - (int)i;
+    render(run(ignore), d1, h1);
+    out[i] = digest(d0, h0, d1, h1);
+  }
+  return 0;
+}
+
+// Time-only what-if baseline: runSpf(src, true, {link}) per failed link
+// (fast != 0: runSpfFast); returns a checksum.
+uint64_t orc_ls_time_whatif(orc_ls* p, const char* src, const char* const* fail_nodes,
+                            const char* const* fail_ifs, uint32_t n, int fast) {
+  uint64_t acc = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    orc::LinkSet ignore;
+    for (const auto& l : p->ls.linksFrom(fail_nodes[i]))
+      if (l->ifaceFrom(fail_nodes[i]) == fail_ifs[i]) {
+        ignore.insert(l);
+        break;
+      }
+    auto r = fast ? p->ls.runSpfFast(src, true, ignore) : p->ls.runSpf(src, true, ignore);
+    for (const auto& kv : r) acc += kv.second.metric * 31 + kv.second.nextHops.size();
   }
   return acc;
 }

@@ -166,3 +166,53 @@ class OracleLinkState:
 
 def spf_runs() -> int:
     return int(lib.orc_spf_runs())
+
+
+# ---- what-if digests ----------------------------------------------------------
+class OrcDigest(C.Structure):
+    _fields_ = [("n_dist_changed", C.c_uint32), ("n_nh_changed", C.c_uint32),
+                ("hash", C.c_uint64)]
+
+
+lib.orc_ls_whatif_digests.restype = C.c_int
+lib.orc_ls_whatif_digests.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint32),
+                                      C.POINTER(C.c_uint32), C.c_uint32, C.c_char_p,
+                                      C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_uint32,
+                                      C.c_int, C.POINTER(OrcDigest), C.POINTER(OrcDigest)]
+lib.orc_ls_time_whatif.restype = C.c_uint64
+lib.orc_ls_time_whatif.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p),
+                                   C.POINTER(C.c_char_p), C.c_uint32, C.c_int]
+
+
+class NameTable:
+    """Node names in id order (ascending), packed for the oracle's C API."""
+
+    def __init__(self, names: Sequence[str]) -> None:
+        self.blob = "".join(names).encode()
+        self.lens = np.array([len(s.encode()) for s in names], np.uint32)
+        self.offs = np.concatenate([[0], np.cumsum(self.lens)[:-1]]).astype(np.uint32)
+        self.n = len(names)
+
+
+def whatif_digests(orc: "OracleLinkState", table: NameTable, src: str,
+                   fails: Sequence[tuple], fast: bool = True):
+    """Digests (n_dist_changed, n_nh_changed, hash) of the unfailed SPF of
+    src and of runSpf(src, true, {link}) for each failure (node, ifName): the
+    link of `node` whose interface on `node` is `ifName`.  Returns
+    (base, [per failure])."""
+    n = len(fails)
+    fn = (C.c_char_p * max(1, n))(*[f[0].encode() for f in fails])
+    fi = (C.c_char_p * max(1, n))(*[f[1].encode() for f in fails])
+    base = OrcDigest()
+    out = (OrcDigest * max(1, n))()
+    rc = lib.orc_ls_whatif_digests(orc._h, table.blob, _p(table.offs), _p(table.lens), table.n,
+                                   src.encode(), fn, fi, n, int(fast), C.byref(base), out)
+    assert rc == 0, f"failed link {-rc - 1} not found"
+    t = lambda d: (int(d.n_dist_changed), int(d.n_nh_changed), int(d.hash))  # noqa: E731
+    return t(base), [t(out[i]) for i in range(n)]
+
+
+def time_whatif(orc: "OracleLinkState", src: str, fails: Sequence[tuple], fast: bool = True) -> int:
+    fn = (C.c_char_p * len(fails))(*[f[0].encode() for f in fails])
+    fi = (C.c_char_p * len(fails))(*[f[1].encode() for f in fails])
+    return int(lib.orc_ls_time_whatif(orc._h, src.encode(), fn, fi, len(fails), int(fast)))
