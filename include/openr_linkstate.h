@@ -110,6 +110,11 @@ int ls_is_node_overloaded(const ls_state* ls, const char* node);
 uint32_t ls_name_id(ls_state* ls, const char* name);
 const char* ls_name(const ls_state* ls, uint32_t id);
 
+/* getAdjacencyDatabases() (LinkState.h:357-359) reduced to what SpfSolver
+ * reads from it: the nodes that advertised a database (name ids, ascending
+ * name) and their node labels.  Call with cap 0 to size (*count). */
+spf_status ls_adjacency_databases(const ls_state* ls, uint32_t* name_ids, int32_t* node_labels,
+                                  uint32_t cap, uint32_t* count);
 spf_status ls_links_from_node(const ls_state* ls, const char* node,
                               uint32_t* link_ids, uint32_t cap, uint32_t* count);
 spf_status ls_link_info(const ls_state* ls, uint32_t link_id, ls_link_desc* out);

@@ -229,6 +229,26 @@ spf_status spf_whatif_timing(spf_whatif_plan* plan, double* base_ms, double* fai
 spf_status spf_whatif_solve(spf_ctx* ctx, uint32_t src, const uint32_t* fail_links,
                             uint32_t n_fail, spf_whatif_digest* out, spf_whatif_digest* base);
 
+/* ---- SpfSolver next-hop selection (Decision.cpp:1082-1305) -------------- */
+/* For node `me` and n_sets destination sets (set i = set_nodes[set_ptr[i] ..
+ * set_ptr[i+1]), the advertisers of one prefix or the owner of one node
+ * label, already filtered for reachability / drain as buildRouteDb does):
+ *   getMinCostNodes      -> min_metric[i] (UINT64_MAX: no member reachable)
+ *   getNextHopsWithMetric + getNextHopsThrift (single area, perDestination
+ *   false) -> nh_count[i] next hops, each an up link of me (nh_edge = the
+ *   directed CSR edge me -> neighbour, so link_id[] and the metric advertised
+ *   by me come with it) and its metric w(link) + dist(neighbour, dst)
+ *   (nh_metric).  Without SPF_ROUTE_LFA only links on shortest paths are
+ *   kept; with it every neighbour passing the RFC 5286 condition of
+ *   Decision.cpp:1180 is added.
+ * nh_edge / nh_metric hold deg(me) entries per set: [n_sets * deg(me)], where
+ * deg(me) = row_ptr[me+1] - row_ptr[me]. */
+#define SPF_ROUTE_LFA 0x1u
+spf_status spf_routes(spf_ctx* ctx, uint32_t me, const uint32_t* set_ptr,
+                      const uint32_t* set_nodes, uint32_t n_sets, uint32_t flags,
+                      uint64_t* min_metric, uint32_t* nh_count, uint32_t* nh_edge,
+                      uint64_t* nh_metric);
+
 /* ---- diagnostics ---------------------------------------------------------- */
 /* With SPF_STAMPS set in the environment, the multi-source BFS kernel records
  * s_memtime clocks of workgroup 0 at its phase boundaries (init, then per level:

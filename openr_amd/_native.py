@@ -25,6 +25,7 @@ SPF_E_STATE = 6
 SPF_UNREACHABLE = 0xFFFFFFFF
 SPF_FLAG_HOP_COUNT = 0x1
 SPF_KSP2_NONE = 0xFFFFFFFF
+SPF_ROUTE_LFA = 0x1
 
 _STATUS_NAMES = {
     SPF_E_INVALID: "SPF_E_INVALID",
@@ -173,6 +174,8 @@ PROTOTYPES = {
     "spf_whatif_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_whatif_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
     "spf_whatif_solve": (C.c_int, [_vp, C.c_uint32, _u32p, C.c_uint32, _vp, _vp]),
+    "spf_routes": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p, C.c_uint32, C.c_uint32, _u64p,
+                             _u32p, _u32p, _u64p]),
     # LinkState facade (openr_linkstate.h)
     "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "ls_destroy": (None, [_vp]),
@@ -188,6 +191,7 @@ PROTOTYPES = {
     "ls_is_node_overloaded": (C.c_int, [_vp, C.c_char_p]),
     "ls_name_id": (C.c_uint32, [_vp, C.c_char_p]),
     "ls_name": (C.c_char_p, [_vp, C.c_uint32]),
+    "ls_adjacency_databases": (C.c_int, [_vp, _u32p, _i32p, C.c_uint32, _u32p]),
     "ls_links_from_node": (C.c_int, [_vp, C.c_char_p, _u32p, C.c_uint32, _u32p]),
     "ls_link_info": (C.c_int, [_vp, C.c_uint32, C.POINTER(LsLinkDesc)]),
     "ls_get_spf_result": (C.c_int, [_vp, C.c_char_p, C.c_int, C.POINTER(LsSpfView)]),

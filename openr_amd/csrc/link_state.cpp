@@ -740,6 +740,22 @@ int ls_has_node(const ls_state* ls, const char* node) {
   const uint32_t* id = ls->find_name(node);
   return id && ls->dbs.count(*id);
 }
+spf_status ls_adjacency_databases(const ls_state* ls, uint32_t* name_ids, int32_t* node_labels,
+                                  uint32_t cap, uint32_t* count) {
+  if (!ls || !count) return SPF_E_INVALID;
+  std::vector<uint32_t> ids;
+  ids.reserve(ls->dbs.size());
+  for (const auto& kv : ls->dbs) ids.push_back(kv.first);
+  std::sort(ids.begin(), ids.end(),
+            [&](uint32_t a, uint32_t b) { return ls->names[a] < ls->names[b]; });
+  *count = (uint32_t)ids.size();
+  for (uint32_t i = 0; i < ids.size() && i < cap; ++i) {
+    if (name_ids) name_ids[i] = ids[i];
+    if (node_labels) node_labels[i] = ls->dbs.at(ids[i]).node_label;
+  }
+  return SPF_OK;
+}
+
 int ls_is_node_overloaded(const ls_state* ls, const char* node) {
   const uint32_t* id = ls->find_name(node);
   return id && node_overloaded(ls, *id);

@@ -1,0 +1,167 @@
+// ============================================================================
+//  routes.hip -- SpfSolver's next-hop selection for one node and a batch of
+//  destination sets (one set per prefix / node label).
+//
+//  Reference: SpfSolver::SpfSolverImpl in openr/decision/Decision.cpp
+//    getMinCostNodes        :1082-1105  closest reachable nodes of the set
+//    getNextHopsWithMetric  :1107-1196  shortest-path next hops (+ LFA,
+//                                       RFC 5286 condition at :1180)
+//    getNextHopsThrift      :1198-1305  one next hop per up link of me towards
+//                                       a selected neighbour, metric
+//                                       w(link) + dist(neighbour, dst)
+//  for a single area and perDestination = false (IP routes and node-label
+//  MPLS routes).  The SPF inputs -- dist rows of me and, with LFA, of every
+//  neighbour, and me's next-hop bitmaps -- come from one batched plan; the
+//  selection runs one wavefront per destination set, lanes over me's links.
+// ============================================================================
+#include "engine_internal.h"
+
+#include <memory>
+
+using namespace spfi;
+
+namespace {
+
+constexpr uint64_t kInf64 = ~0ull;
+
+// D rows: row_of[v] = row of v's distances (me and, with LFA, neighbours).
+// nh: me's destination bitmaps, bitmap j = neighbour j (ascending id).
+__global__ __launch_bounds__(64) void routes_kernel(
+    const uint32_t* __restrict__ D, uint32_t pitch, const uint32_t* __restrict__ row_of,
+    const uint32_t* __restrict__ nh, uint32_t me, const uint32_t* __restrict__ me_edges_col,
+    const uint32_t* __restrict__ me_edges_w, const uint32_t* __restrict__ me_edges_j,
+    uint32_t me_deg, const uint32_t* __restrict__ set_ptr, const uint32_t* __restrict__ set_nodes,
+    uint32_t lfa, uint64_t* __restrict__ out_min, uint32_t* __restrict__ out_cnt,
+    uint32_t* __restrict__ out_edge, uint64_t* __restrict__ out_metric) {
+  const uint32_t p = blockIdx.x, lane = threadIdx.x;
+  const uint32_t b = set_ptr[p], e = set_ptr[p + 1];
+  const uint32_t* Dme = D + (size_t)row_of[me] * pitch;
+  const uint32_t wpm = pitch / 32;
+  // getMinCostNodes: shortest metric over the reachable members
+  uint64_t shortest = kInf64;
+  for (uint32_t i = b; i < e; ++i) {
+    const uint32_t d = Dme[set_nodes[i]];
+    if (d != kInf && d < shortest) shortest = d;
+  }
+  uint32_t cnt = 0;
+  if (shortest != kInf64) {
+    for (uint32_t base = 0; base < me_deg; base += 64) {
+      const uint32_t k = base + lane;
+      bool keep = false;
+      uint64_t metric = 0;
+      if (k < me_deg) {
+        const uint32_t x = me_edges_col[k], j = me_edges_j[k];
+        // shortest-path next hop: x in nextHops() of a min-cost member
+        uint64_t val = kInf64;
+        for (uint32_t i = b; i < e; ++i) {
+          const uint32_t d = set_nodes[i];
+          if (Dme[d] != shortest) continue;
+          if ((nh[(size_t)j * wpm + (d >> 5)] >> (d & 31)) & 1u) {
+            val = shortest - Dme[x];
+            break;
+          }
+        }
+        if (lfa) {  // loop-free alternate: d(x, dst) < shortest + d(x, me)
+          const uint32_t* Dx = D + (size_t)row_of[x] * pitch;
+          const uint64_t back = Dx[me];
+          for (uint32_t i = b; i < e; ++i) {
+            const uint32_t dxd = Dx[set_nodes[i]];
+            if (dxd == kInf || back == kInf) continue;
+            if ((uint64_t)dxd < shortest + back && (val == kInf64 || val > dxd)) val = dxd;
+          }
+        }
+        if (val != kInf64) {
+          metric = (uint64_t)me_edges_w[k] + val;
+          keep = lfa || metric == shortest;
+        }
+      }
+      const uint64_t m = __ballot(keep);
+      if (keep) {
+        const uint32_t at = cnt + __popcll(m & ((1ull << lane) - 1));
+        out_edge[(size_t)p * me_deg + at] = k;
+        out_metric[(size_t)p * me_deg + at] = metric;
+      }
+      cnt += __popcll(m);
+    }
+  }
+  if (lane == 0) {
+    out_min[p] = shortest;
+    out_cnt[p] = cnt;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
+                      const uint32_t* set_nodes, uint32_t n_sets, uint32_t flags,
+                      uint64_t* min_metric, uint32_t* nh_count, uint32_t* nh_edge,
+                      uint64_t* nh_metric) {
+  if (!c || !set_ptr || !min_metric || !nh_count || !nh_edge || !nh_metric)
+    return fail(c, SPF_E_INVALID, "spf_routes: NULL argument");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (me >= c->N) return fail(c, SPF_E_INVALID, "node %u out of range", me);
+  const uint32_t N = c->N;
+  const uint32_t n_members = set_ptr[n_sets];
+  for (uint32_t i = 0; i < n_members; ++i)
+    if (set_nodes[i] >= N) return fail(c, SPF_E_INVALID, "set member %u out of range", set_nodes[i]);
+  const bool lfa = (flags & SPF_ROUTE_LFA) != 0;
+  // sources: me, and with LFA every distinct up neighbour (getSpfResult(nbr),
+  // Decision.cpp:1165)
+  std::vector<uint32_t> srcs{me};
+  const uint32_t nb0 = c->nb_ptr[me], k = c->nb_ptr[me + 1] - nb0;
+  if (lfa)
+    for (uint32_t j = 0; j < k; ++j) srcs.push_back(c->nb_id[nb0 + j]);
+  spf_plan* raw = nullptr;
+  spf_status st = spf_plan_create(c, srcs.data(), (uint32_t)srcs.size(), 0, &raw);
+  if (st != SPF_OK) return st;
+  std::unique_ptr<spf_plan, void (*)(spf_plan*)> p(raw, spf_plan_destroy);
+  // me's up links in linksFromNode order, with the bitmap index of their far end
+  const uint32_t e0 = c->row_ptr[me], deg = c->row_ptr[me + 1] - e0;
+  std::vector<uint32_t> ecol(deg), ew(deg), ej(deg);
+  for (uint32_t i = 0; i < deg; ++i) {
+    ecol[i] = c->col[e0 + i];
+    ew[i] = c->wt[e0 + i];
+    const uint32_t* f = std::lower_bound(c->nb_id.data() + nb0, c->nb_id.data() + nb0 + k, ecol[i]);
+    ej[i] = (uint32_t)(f - (c->nb_id.data() + nb0));
+  }
+  DevBuf<uint32_t> d_dist, d_nh, d_ecol, d_ew, d_ej, d_sp, d_sn, d_cnt, d_edge;
+  DevBuf<uint64_t> d_min, d_metric;
+  HIP_TRY(c, d_dist.alloc((size_t)srcs.size() * c->pitch));
+  HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(1, spf_plan_nh_words(p.get()))));
+  HIP_TRY(c, d_ecol.upload(ecol.data(), deg, c->stream));
+  HIP_TRY(c, d_ew.upload(ew.data(), deg, c->stream));
+  HIP_TRY(c, d_ej.upload(ej.data(), deg, c->stream));
+  HIP_TRY(c, d_sp.upload(set_ptr, n_sets + 1, c->stream));
+  HIP_TRY(c, d_sn.upload(set_nodes, std::max<uint32_t>(1, n_members), c->stream));
+  const size_t cap = (size_t)n_sets * std::max<uint32_t>(1, deg);
+  HIP_TRY(c, d_min.alloc(std::max<uint32_t>(1, n_sets)));
+  HIP_TRY(c, d_cnt.alloc(std::max<uint32_t>(1, n_sets)));
+  HIP_TRY(c, d_edge.alloc(cap));
+  HIP_TRY(c, d_metric.alloc(cap));
+  st = spf_plan_execute(p.get(), d_dist.p, d_nh.p, c->stream);
+  if (st != SPF_OK) return st;
+  // the plan's D rows: the caller buffer when the source set is closed,
+  // otherwise the plan's own closure rows
+  const uint32_t* D = p->direct ? d_dist.p : p->d_D.p;
+  if (n_sets) {
+    hipLaunchKernelGGL(routes_kernel, dim3(n_sets), dim3(64), 0, c->stream, D, c->pitch,
+                       p->d_row_of.p, d_nh.p, me, d_ecol.p, d_ew.p, d_ej.p, deg, d_sp.p, d_sn.p,
+                       lfa ? 1u : 0u, d_min.p, d_cnt.p, d_edge.p, d_metric.p);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(min_metric, d_min.p, 8ull * n_sets, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(nh_count, d_cnt.p, 4ull * n_sets, hipMemcpyDeviceToHost, c->stream));
+    if (deg) {
+      HIP_TRY(c, hipMemcpyAsync(nh_edge, d_edge.p, 4ull * cap, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(nh_metric, d_metric.p, 8ull * cap, hipMemcpyDeviceToHost, c->stream));
+    }
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // out edges are positions in me's CSR row: make them global edge ids
+  for (size_t i = 0; i < (size_t)n_sets; ++i)
+    for (uint32_t t = 0; t < nh_count[i]; ++t) nh_edge[i * deg + t] += e0;
+  return SPF_OK;
+}
+
+}  // extern "C"

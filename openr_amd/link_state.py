@@ -262,6 +262,16 @@ class LinkState:
     def isNodeOverloaded(self, nodeName: str) -> bool:
         return bool(N.lib.ls_is_node_overloaded(self._h, nodeName.encode()))
 
+    def getAdjacencyDatabaseLabels(self) -> Dict[str, int]:
+        """{node: nodeLabel} of every node with an adjacency database -- the
+        part of getAdjacencyDatabases() (LinkState.h:357-359) SpfSolver reads."""
+        cnt = C.c_uint32()
+        self._err(N.lib.ls_adjacency_databases(self._h, None, None, 0, C.byref(cnt)))
+        ids = (C.c_uint32 * max(1, cnt.value))()
+        labels = (C.c_int32 * max(1, cnt.value))()
+        self._err(N.lib.ls_adjacency_databases(self._h, ids, labels, cnt.value, C.byref(cnt)))
+        return {self._name(ids[i]): int(labels[i]) for i in range(cnt.value)}
+
     def linksFromNode(self, nodeName: str) -> List[Link]:
         """Links of ``nodeName`` in the reference's LinkSet iteration order."""
         cnt = C.c_uint32()

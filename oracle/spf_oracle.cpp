@@ -1042,4 +1042,103 @@ uint64_t orc_ls_time_whatif(orc_ls* p, const char* src, const char* const* fail_
   return acc;
 }
 
+// ---- SpfSolver next hops (Decision.cpp:1082-1305, one area) ----------------
+// getMinCostNodes + getNextHopsWithMetric(perDestination = false) +
+// getNextHopsThrift for `me` towards the destination node set `dsts`
+// (n_dsts names).  swap_label >= 0: node-label route semantics (SWAP, or PHP
+// when the neighbour is a destination).  Output JSON:
+//   {"min": metric|null, "nh": [[ifName, metric(i32), neighbour, addrHex,
+//                                 action|null, swap|null], ...]} (sorted)
+static std::string hexOf(const std::string& raw) {
+  static const char* d = "0123456789abcdef";
+  std::string o;
+  for (unsigned char c : raw) {
+    o += d[c >> 4];
+    o += d[c & 15];
+  }
+  return o;
+}
+const char* orc_ls_nexthops_json(orc_ls* p, const char* me_c, const char* const* dsts,
+                                 uint32_t n_dsts, int lfa, int v4, int64_t swap_label) {
+  const orc::LinkState& ls = p->ls;
+  const std::string me(me_c);
+  std::set<std::string> dstSet;
+  for (uint32_t i = 0; i < n_dsts; ++i) dstSet.insert(dsts[i]);
+  // getMinCostNodes (Decision.cpp:1082-1105)
+  const auto& mine = ls.getSpfResult(me, true);
+  orc::Metric shortest = std::numeric_limits<orc::Metric>::max();
+  std::set<std::string> minCost;
+  for (const auto& d : dstSet) {
+    auto it = mine.find(d);
+    if (it == mine.end()) continue;
+    if (shortest >= it->second.metric) {
+      if (shortest > it->second.metric) {
+        shortest = it->second.metric;
+        minCost.clear();
+      }
+      minCost.insert(d);
+    }
+  }
+  // getNextHopsWithMetric (:1107-1196)
+  std::map<std::string, orc::Metric> nextHopNodes;
+  if (!minCost.empty()) {
+    for (const auto& d : minCost)
+      for (const auto& nh : mine.at(d).nextHops)
+        nextHopNodes[nh] = shortest - mine.at(nh).metric;
+    if (lfa) {
+      for (const auto& l : ls.linksFrom(me)) {
+        if (!l->isUp()) continue;
+        const std::string& nb = l->other(me);
+        const auto& fromNb = ls.getSpfResult(nb, true);
+        const orc::Metric nbToHere = fromNb.at(me).metric;
+        for (const auto& d : dstSet) {
+          auto it = fromNb.find(d);
+          if (it == fromNb.end()) continue;
+          const orc::Metric dn = it->second.metric;
+          if (dn < shortest + nbToHere) {
+            auto f = nextHopNodes.find(nb);
+            if (f == nextHopNodes.end()) nextHopNodes.emplace(nb, dn);
+            else if (f->second > dn) f->second = dn;
+          }
+        }
+      }
+    }
+  }
+  // getNextHopsThrift (:1198-1305)
+  std::set<std::string> rows;
+  for (const auto& l : ls.linksFrom(me)) {
+    const std::string& nb = l->other(me);
+    auto f = nextHopNodes.find(nb);
+    if (f == nextHopNodes.end() || !l->isUp()) continue;
+    const orc::Metric over = l->metricFrom(me) + f->second;
+    if (!lfa && over != shortest) continue;
+    std::string act = "null", swp = "null";
+    if (swap_label >= 0) {
+      const bool nhIsDst = dstSet.count(nb) != 0;
+      act = nhIsDst ? "\"PHP\"" : "\"SWAP\"";
+      if (!nhIsDst) swp = std::to_string(swap_label);
+    }
+    std::string r = "[";
+    json_str(r, l->ifaceFrom(me));
+    r += "," + std::to_string((int32_t)over) + ",";
+    json_str(r, nb);
+    r += ",";
+    json_str(r, hexOf(v4 ? l->v4From(me) : l->v6From(me)));
+    r += "," + act + "," + swp + "]";
+    rows.insert(r);
+  }
+  std::string& o = p->scratch;
+  o = "{\"min\":";
+  o += minCost.empty() ? std::string("null") : std::to_string(shortest);
+  o += ",\"nh\":[";
+  bool first = true;
+  for (const auto& r : rows) {
+    if (!first) o += ',';
+    first = false;
+    o += r;
+  }
+  o += "]}";
+  return o.c_str();
+}
+
 }  // extern "C"

@@ -59,6 +59,23 @@ class OracleAdapter(_Replay):
     def spf_runs(self) -> int:
         return self._runs()
 
+    def routes(self, me, lfa, v4, labels: Dict[str, int]) -> Dict[str, list]:
+        """{"ip:X": rows, "label:X": rows} for every other node X: the
+        restated getNextHopsWithMetric + getNextHopsThrift (Decision.cpp)."""
+        from oracle import nexthops
+
+        out = {}
+        for x, label in labels.items():
+            if x == me:
+                continue
+            r = nexthops(self.ls, me, [x], lfa, v4)
+            if r["nh"]:
+                out[f"ip:{x}"] = sorted(r["nh"], key=str)
+            r = nexthops(self.ls, me, [x], lfa, False, label)
+            if r["nh"]:
+                out[f"label:{x}"] = sorted(r["nh"], key=str)
+        return out
+
 
 class ProductAdapter(_Replay):
     device = 0
@@ -105,6 +122,36 @@ class ProductAdapter(_Replay):
 
     def spf_runs(self):
         return self.ls.spfRuns()
+
+    def routes(self, me, lfa, v4, labels: Dict[str, int]) -> Dict[str, list]:
+        """The same rows from the product's SpfSolver.buildRouteDb, every node
+        advertising one loopback prefix."""
+        from openr_amd.spf_solver import PrefixEntry, PrefixState, SpfSolver
+
+        ps = PrefixState()
+        pfx = {}
+        for i, x in enumerate(sorted(labels)):
+            pfx[x] = f"10.0.{i // 250}.{i % 250 + 1}/32" if v4 else f"fc00::{i + 1:x}/128"
+            ps.updatePrefix(x, self.ls.getArea(), PrefixEntry(pfx[x]))
+        db = SpfSolver(me, True, lfa).buildRouteDb(me, {self.ls.getArea(): self.ls}, ps)
+
+        def rows(nhs):
+            return sorted(([n.ifName, n.metric, n.neighborNodeName, n.address.hex(),
+                            n.mplsAction.action if n.mplsAction else None,
+                            n.mplsAction.swapLabel if n.mplsAction else None] for n in nhs),
+                          key=str)
+
+        out = {}
+        for x in labels:
+            if x == me:
+                continue
+            r = db.unicastRoutes.get(pfx[x])
+            if r is not None:
+                out[f"ip:{x}"] = rows(r.nexthops)
+            r = db.mplsRoutes.get(labels[x])
+            if r is not None:
+                out[f"label:{x}"] = rows(r.nexthops)
+        return out
 
 
 class HostOnlyProductAdapter(ProductAdapter):

@@ -303,6 +303,96 @@ for n in range(2, 17, 2):
                     "cite": "DecisionTest.cpp:4283-4290 gridDistance; :4318-4354"}],
     })
 
+# ---------------- SpfSolver routes (DecisionTest.cpp) ----------------
+# Route next hops as rows [ifName, metric, neighbour, addrHex, action, swap]:
+# createNextHopFromAdj(adj, isV4, metric, mplsAction) (DecisionTest.cpp:201-215)
+# = createNextHop(adj.nextHopV4/V6, adj.ifName, metric, action, area,
+# adj.otherNodeName).  "ip:X" = the unicast route to node X's loopback,
+# "label:X" = the MPLS route for X's node label (labelSwapActionX = SWAP(X),
+# labelPhpAction = PHP).
+
+
+def hop(adj, metric, action=None, swap=None, v4=False):
+    return [adj.ifName, metric, adj.otherNodeName,
+            (adj.nextHopV4 if v4 else adj.nextHopV6).hex(), action, swap]
+
+
+def ring_routes(D, spec, v4=False):
+    """spec: {me: {dst: ([(adj_key, metric)], label_action)}} with
+    label_action "PHP" or "SWAP"."""
+    exp = {}
+    for me, dsts in spec.items():
+        e = {}
+        for dst, (hops, act) in dsts.items():
+            e[f"ip:{dst}"] = sorted(hop(D[k], m, v4=v4) for k, m in hops)
+            e[f"label:{dst}"] = sorted(
+                hop(D[k], m, act, int(dst) if act == "SWAP" else None) for k, m in hops)
+        exp[me] = e
+    return exp
+
+
+RING_SP = {
+    "1": {"4": ([("adj12", 20), ("adj13", 20)], "SWAP"), "3": ([("adj13", 10)], "PHP"),
+          "2": ([("adj12", 10)], "PHP")},
+    "2": {"4": ([("adj24", 10)], "PHP"), "3": ([("adj21", 20), ("adj24", 20)], "SWAP"),
+          "1": ([("adj21", 10)], "PHP")},
+    "3": {"4": ([("adj34", 10)], "PHP"), "2": ([("adj31", 20), ("adj34", 20)], "SWAP"),
+          "1": ([("adj31", 10)], "PHP")},
+    "4": {"3": ([("adj43", 10)], "PHP"), "2": ([("adj42", 10)], "PHP"),
+          "1": ([("adj42", 20), ("adj43", 20)], "SWAP")},
+}
+for lfa, cite in ((False, "DecisionTest.cpp:1814-1944 (SimpleRing ShortestPathTest)"),
+                  (True, "DecisionTest.cpp:1999-2127 (SimpleRing MultiPathTest, LFA)")):
+    for v4 in (False, True):
+        cases.append({
+            "name": f"decision_ring_routes_{'lfa' if lfa else 'sp'}_{'v4' if v4 else 'v6'}",
+            "cite": cite,
+            "steps": ring_steps,
+            "checks": [{"type": "routes", "lfa": lfa, "v4": v4,
+                        "expect": ring_routes(R, RING_SP, v4), "cite": cite}],
+        })
+
+PAR_SP = {
+    "1": {"4": ([("adj12_2", 22), ("adj13_1", 22), ("adj12_1", 22)], "SWAP"),
+          "3": ([("adj13_1", 11)], "PHP"), "2": ([("adj12_2", 11), ("adj12_1", 11)], "PHP")},
+    "2": {"4": ([("adj24_1", 11)], "PHP"),
+          "3": ([("adj21_2", 22), ("adj21_1", 22), ("adj24_1", 22)], "SWAP"),
+          "1": ([("adj21_2", 11), ("adj21_1", 11)], "PHP")},
+    "3": {"4": ([("adj34_1", 11)], "PHP"), "2": ([("adj31_1", 22), ("adj34_1", 22)], "SWAP"),
+          "1": ([("adj31_1", 11)], "PHP")},
+    "4": {"3": ([("adj43_1", 11)], "PHP"), "2": ([("adj42_1", 11)], "PHP"),
+          "1": ([("adj42_1", 22), ("adj43_1", 22)], "SWAP")},
+}
+PAR_LFA = {
+    "1": {"4": ([("adj12_1", 22), ("adj12_2", 22), ("adj12_3", 31), ("adj13_1", 22)], "SWAP"),
+          "3": ([("adj13_1", 11)], "PHP"),
+          "2": ([("adj12_1", 11), ("adj12_2", 11), ("adj12_3", 20)], "PHP")},
+    "2": {"4": ([("adj24_1", 11)], "PHP"),
+          "3": ([("adj21_1", 22), ("adj21_2", 22), ("adj21_3", 31), ("adj24_1", 22)], "SWAP"),
+          "1": ([("adj21_1", 11), ("adj21_2", 11), ("adj21_3", 20)], "PHP")},
+    "3": {"4": ([("adj34_1", 11), ("adj34_2", 20), ("adj34_3", 20)], "PHP"),
+          "2": ([("adj31_1", 22), ("adj34_1", 22), ("adj34_2", 31), ("adj34_3", 31)], "SWAP"),
+          "1": ([("adj31_1", 11)], "PHP")},
+    "4": {"3": ([("adj43_1", 11), ("adj43_2", 20), ("adj43_3", 20)], "PHP"),
+          "2": ([("adj42_1", 11)], "PHP"),
+          "1": ([("adj42_1", 22), ("adj43_1", 22), ("adj43_2", 31), ("adj43_3", 31)], "SWAP")},
+}
+par_steps = [{"update": [db_json(d) for d in par]}]
+cases.append({
+    "name": "decision_parallel_routes_sp",
+    "cite": "DecisionTest.cpp:3252-3370 (ParallelAdjRing ShortestPathTest)",
+    "steps": par_steps,
+    "checks": [{"type": "routes", "lfa": False, "v4": False, "expect": ring_routes(P, PAR_SP),
+                "cite": "DecisionTest.cpp:3262-3367"}],
+})
+cases.append({
+    "name": "decision_parallel_routes_lfa",
+    "cite": "DecisionTest.cpp:3374-3530 (ParallelAdjRing MultiPathTest, LFA)",
+    "steps": par_steps,
+    "checks": [{"type": "routes", "lfa": True, "v4": False, "expect": ring_routes(P, PAR_LFA),
+                "cite": "DecisionTest.cpp:3386-3528"}],
+})
+
 out = HERE / "reference_expectations.json"
 out.write_text(json.dumps({"source": "fredxia/openr openr/decision/tests", "cases": cases},
                           indent=1, sort_keys=False))

@@ -216,3 +216,20 @@ def time_whatif(orc: "OracleLinkState", src: str, fails: Sequence[tuple], fast: 
     fn = (C.c_char_p * len(fails))(*[f[0].encode() for f in fails])
     fi = (C.c_char_p * len(fails))(*[f[1].encode() for f in fails])
     return int(lib.orc_ls_time_whatif(orc._h, src.encode(), fn, fi, len(fails), int(fast)))
+
+
+# ---- SpfSolver next hops --------------------------------------------------------
+lib.orc_ls_nexthops_json.restype = C.c_char_p
+lib.orc_ls_nexthops_json.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
+                                     C.c_int, C.c_int, C.c_int64]
+
+
+def nexthops(orc: "OracleLinkState", me: str, dsts: Sequence[str], lfa: bool = False,
+             v4: bool = False, swap_label: Optional[int] = None) -> Dict:
+    """getNextHopsWithMetric + getNextHopsThrift (Decision.cpp:1107-1305) of
+    `me` towards `dsts`: {"min": metric|None, "nh": sorted rows [ifName, metric,
+    neighbour, addrHex, action|None, swapLabel|None]}."""
+    arr = (C.c_char_p * max(1, len(dsts)))(*[d.encode() for d in dsts])
+    raw = lib.orc_ls_nexthops_json(orc._h, me.encode(), arr, len(dsts), int(lfa), int(v4),
+                                   -1 if swap_label is None else swap_label)
+    return json.loads(raw)

@@ -167,5 +167,11 @@ def _check(chk: dict, ad, dbs, case) -> None:
             for d in range(n * n):
                 md = abs(s % n - d % n) + abs(s // n - d // n)
                 assert res[str(d)]["metric"] == md, (where, s, d)
+    elif t == "routes":
+        labels = {n: db.nodeLabel for n, db in dbs.items()}
+        for me, exp in chk["expect"].items():
+            got = ad.routes(me, chk["lfa"], chk["v4"], labels)
+            for key, rows in exp.items():
+                assert got.get(key) == sorted(rows, key=str), (where, me, key, got.get(key), rows)
     else:
         raise AssertionError(f"unknown check {t}")

@@ -1,0 +1,90 @@
+"""SpfSolver route computation on the MI355X (spf_routes + openr_amd.spf_solver)
+against the oracle's restatement of getMinCostNodes / getNextHopsWithMetric /
+getNextHopsThrift (Decision.cpp:1082-1305), which tests/test_oracle_reference.py
+pins to DecisionTest's route expectations.
+
+Random multigraphs (parallel links, drained nodes and links) and a fabric:
+every node's unicast + node-label routes from several vantage points, with and
+without LFA, v4 and v6; anycast destination sets; adjacency-label and POP
+routes of buildRouteDb.
+"""
+
+import numpy as np
+import pytest
+
+from adapters import OracleAdapter, ProductAdapter
+from oracle import nexthops
+from openr_amd import topology as T
+from openr_amd.link_state import LinkState
+from openr_amd.spf_solver import SpfSolver
+
+pytestmark = pytest.mark.gpu
+
+GRAPHS = [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("wan120", lambda: T.wan(120, 60, seed=8)),
+] + [
+    (f"rand{seed}", (lambda s: lambda: T.random_graph(
+        40, 110, 400 + s, max_metric=6, parallel_frac=0.25, overload_frac=0.1,
+        link_overload_frac=0.05))(seed))
+    for seed in range(4)
+]
+
+
+def load(topo):
+    o, p = OracleAdapter(), ProductAdapter()
+    o.update_packed(topo.lsdb)
+    p.update_packed(topo.lsdb)
+    return o, p
+
+
+@pytest.mark.parametrize("name,make", GRAPHS, ids=[g[0] for g in GRAPHS])
+@pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
+def test_route_db_matches_oracle(name, make, lfa):
+    topo = make()
+    o, p = load(topo)
+    labels = p.ls.getAdjacencyDatabaseLabels()
+    rng = np.random.default_rng(3)
+    mes = [topo.nodes[int(i)] for i in rng.choice(len(topo.nodes), 3, replace=False)]
+    for me in mes:
+        for v4 in (False, True):
+            assert p.routes(me, lfa, v4, labels) == o.routes(me, lfa, v4, labels), (me, v4)
+
+
+@pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
+def test_anycast_sets_match_oracle(lfa):
+    topo = T.random_graph(50, 140, 77, max_metric=4, parallel_frac=0.2, overload_frac=0.05)
+    o, p = load(topo)
+    rng = np.random.default_rng(9)
+    solver = SpfSolver("x", True, lfa)
+    names = topo.nodes
+    for _ in range(6):
+        me = names[int(rng.integers(len(names)))]
+        sets = [[names[int(i)] for i in rng.choice(len(names), int(rng.integers(1, 5)),
+                                                   replace=False)] for _ in range(12)]
+        got = solver.getNextHopsBatch(p.ls, me, sets)
+        for s, (mn, nhs) in zip(sets, got):
+            want = nexthops(o.ls, me, s, lfa)
+            assert mn == want["min"] or (not nhs and not want["nh"])
+            rows = sorted(([n.ifName, n.metric, n.neighborNodeName, n.address.hex(), None, None]
+                           for n in nhs), key=str)
+            assert rows == sorted(want["nh"], key=str), (me, s)
+
+
+def test_pop_and_adjacency_label_routes():
+    topo = T.random_graph(20, 40, 5, parallel_frac=0.3)
+    ls = LinkState()
+    ls.updateAdjacencyDatabases(topo.lsdb)
+    from openr_amd.spf_solver import PrefixState
+
+    me = topo.nodes[3]
+    db = SpfSolver(me, True, False).buildRouteDb(me, {ls.getArea(): ls}, PrefixState())
+    labels = ls.getAdjacencyDatabaseLabels()
+    pop = db.mplsRoutes[labels[me]]
+    assert [n.mplsAction.action for n in pop.nexthops] == ["POP_AND_LOOKUP"]
+    for link in ls.linksFromNode(me):
+        lab = link.getAdjLabelFromNode(me)
+        if lab:
+            (nh,) = db.mplsRoutes[lab].nexthops
+            assert nh.mplsAction.action == "PHP" and nh.ifName == link.getIfaceFromNode(me)
+            assert nh.metric == link.getMetricFromNode(me)
