@@ -213,8 +213,8 @@ void spf_whatif_plan_destroy(spf_whatif_plan* plan);
 uint32_t spf_whatif_plan_failures(const spf_whatif_plan* plan);
 spf_status spf_whatif_plan_links(const spf_whatif_plan* plan, uint32_t* links /* [n_fail] */);
 /* d_out = [n_fail] digests, d_base = 1 digest (may be NULL).  Enqueued on
- * `stream`; the unfailed next-hop propagation synchronises the stream once
- * per DAG level (host-side convergence test). */
+ * `stream` (cooperative launch for the unfailed solve); no host
+ * synchronisation. */
 spf_status spf_whatif_execute(spf_whatif_plan* plan, spf_whatif_digest* d_out,
                               spf_whatif_digest* d_base, void* stream);
 /* After an execute: failures that needed a re-solve (tight links) and those

@@ -51,10 +51,10 @@ struct DevBuf {
 // (device list rows_src), writing rows [rows][pitch] of D.
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
                        const uint32_t* ign, uint32_t* D, hipStream_t s);
-// Single-source SSSP in global memory (one workgroup; any graph size):
-// dist = [N], q = [N] and bm = [ceil(N/32)] scratch.
+// Single-source SSSP in global memory, one cooperative grid (any graph
+// size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
-                        uint32_t* q, uint32_t* bm, hipStream_t s);
+                        hipStream_t s);
 // Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
 spf_status set_lds_limits(spf_ctx* c);
 
@@ -84,7 +84,7 @@ struct spf_ctx {
   spfi::DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
   spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
-  spfi::DevBuf<uint32_t> d_gq, d_gbm;     // global-memory SSSP scratch
+  spfi::DevBuf<uint32_t> d_gq, d_gq2, d_gbm, d_gctr;  // global-memory SSSP scratch
   spfi::DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
 };
 
@@ -131,10 +131,10 @@ spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
 // (device list rows_src), writing rows [rows][pitch] of D.
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
                        const uint32_t* ign, uint32_t* D, hipStream_t s);
-// Single-source SSSP in global memory (one workgroup; any graph size):
-// dist = [N], q = [N] and bm = [ceil(N/32)] scratch.
+// Single-source SSSP in global memory, one cooperative grid (any graph
+// size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
-                        uint32_t* q, uint32_t* bm, hipStream_t s);
+                        hipStream_t s);
 // Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
 spf_status set_lds_limits(spf_ctx* c);
 

@@ -1161,9 +1161,7 @@ spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ig
   HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
   HIP_TRY(c, c->d_row.alloc(c->pitch));
   if (sssp_lds_bytes(c->N, c->pitch, c->big_nodes, c->N <= 65535) > kMaxLds) {
-    HIP_TRY(c, c->d_gq.alloc(c->N));
-    HIP_TRY(c, c->d_gbm.alloc((c->N + 31) / 32));
-    st = launch_gsssp(c, src, hop, ign, c->d_row.p, c->d_gq.p, c->d_gbm.p, c->stream);
+    st = launch_gsssp(c, src, hop, ign, c->d_row.p, c->stream);
   } else {
     st = launch_sssp(c, c->d_one_src.p, 1, hop, ign, c->d_row.p, c->stream);
   }

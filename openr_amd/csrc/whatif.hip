@@ -34,6 +34,8 @@
 // ============================================================================
 #include "engine_internal.h"
 
+#include <hip/hip_cooperative_groups.h>
+
 #include <memory>
 
 using namespace spfi;
@@ -41,9 +43,8 @@ using namespace spfi;
 namespace {
 
 constexpr uint32_t kBusy = 0xFFFFFFFEu;
-constexpr int kGThreads = 1024;     // global-memory SSSP (one workgroup)
-constexpr uint32_t kWaveCap = 4096; // |D| a wave team can hold
-constexpr int kBigTeams = 32;       // workgroup teams for large D
+constexpr uint32_t kWaveCap = 1024;            // |D| a wave team can hold
+constexpr size_t kBigScratch = 8ull << 30;     // HBM budget of the workgroup teams
 
 __device__ __forceinline__ uint32_t ld(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -86,79 +87,105 @@ struct WiBase {
 };
 
 // ---------------------------------------------------------------------------
-//  global-memory SSSP from one source (graphs beyond the LDS kernels)
+//  cooperative (grid-synchronised) single-source SSSP and unfailed result
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kGThreads) void gsssp_kernel(
-    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-    const uint32_t* __restrict__ wt, const uint8_t* __restrict__ ovl,
-    const uint32_t* __restrict__ link, const uint32_t* __restrict__ ign, uint32_t src,
-    uint32_t N, uint32_t hop, uint32_t* dist, uint32_t* q, uint32_t* bm) {
-  __shared__ uint32_t s_len;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t bm_words = (N + 31) / 32;
-  for (uint32_t v = tid; v < N; v += kGThreads) st(&dist[v], v == src ? 0u : kInf);
-  for (uint32_t i = tid; i < bm_words; i += kGThreads) st(&bm[i], 0u);
-  if (tid == 0) {
-    q[0] = src;
-    s_len = 0;
+namespace cg = cooperative_groups;
+constexpr int kCoopThreads = 512;  // one block per CU: always co-resident
+
+struct CoopSssp {
+  const uint32_t* row_ptr;
+  const uint32_t* col;
+  const uint32_t* wt;
+  const uint8_t* ovl;
+  const uint32_t* link;
+  const uint32_t* ign;  // optional link bitmap
+  uint32_t N, src, hop;
+  uint32_t* dist;
+  uint32_t* qa;
+  uint32_t* qb;
+  uint32_t* bm;   // [ceil(N/32)] next-frontier bitmap
+  uint32_t* ctr;  // [4] rotating queue lengths + spare
+};
+
+// Frontier Bellman-Ford over the whole grid: expansion, grid barrier,
+// bitmap compaction into the other queue, grid barrier.  Data written by
+// other workgroups is read with agent-scope atomics (ld) or atomicExch.
+__device__ void coop_sssp(cg::grid_group& grid, const CoopSssp& a) {
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gsz = gridDim.x * blockDim.x;
+  const uint32_t bm_words = (a.N + 31) / 32;
+  for (uint32_t v = gtid; v < a.N; v += gsz) st(&a.dist[v], v == a.src ? 0u : kInf);
+  for (uint32_t i = gtid; i < bm_words; i += gsz) st(&a.bm[i], 0u);
+  if (gtid == 0) {
+    st(&a.qa[0], a.src);
+    st(&a.ctr[0], 1u);
+    st(&a.ctr[1], 0u);
+    st(&a.ctr[2], 0u);
   }
-  __syncthreads();
-  uint32_t qlen = 1;
-  while (qlen) {
-    for (uint32_t i = tid; i < qlen; i += kGThreads) {
-      const uint32_t u = q[i];
-      if (ovl[u] && u != src) continue;  // drained: recorded, not expanded
-      const uint32_t du = ld(&dist[u]);
-      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
-        if (ign && ((ign[link[e] >> 5] >> (link[e] & 31)) & 1u)) continue;
-        const uint32_t v = col[e];
-        const uint32_t nd = du + (hop ? 1u : wt[e]);
-        if (nd < atomicMin(&dist[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+  grid.sync();
+  for (uint32_t it = 0;; ++it) {
+    const uint32_t len = ld(&a.ctr[it % 3]);
+    if (len == 0) break;
+    const uint32_t* cur = (it & 1) ? a.qb : a.qa;
+    uint32_t* nxt = (it & 1) ? a.qa : a.qb;
+    uint32_t* nctr = &a.ctr[(it + 1) % 3];
+    if (gtid == 0) st(&a.ctr[(it + 2) % 3], 0u);  // read last at iteration it - 1
+    for (uint32_t i = gtid; i < len; i += gsz) {
+      const uint32_t u = ld(&cur[i]);
+      if (a.ovl[u] && u != a.src) continue;  // drained: recorded, not expanded
+      const uint32_t du = ld(&a.dist[u]);
+      for (uint32_t e = a.row_ptr[u]; e < a.row_ptr[u + 1]; ++e) {
+        if (a.ign && ((a.ign[a.link[e] >> 5] >> (a.link[e] & 31)) & 1u)) continue;
+        const uint32_t v = a.col[e];
+        const uint32_t nd = du + (a.hop ? 1u : a.wt[e]);
+        if (nd < atomicMin(&a.dist[v], nd)) atomicOr(&a.bm[v >> 5], 1u << (v & 31));
       }
     }
-    __syncthreads();
-    for (uint32_t base = 0; base < bm_words; base += kGThreads) {
-      const uint32_t i = base + tid;
-      uint32_t word = i < bm_words ? atomicExch(&bm[i], 0u) : 0u;
-      // wave scan of the popcounts, one LDS atomic per wave
-      uint32_t x = __popc(word), inc = x;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += y;
-      }
-      const uint32_t tot = __shfl(inc, 63, 64);
-      uint32_t at = 0;
-      if (lane == 63 && tot) at = atomicAdd(&s_len, tot);
-      at = __shfl(at, 63, 64) + inc - x;
+    grid.sync();
+    for (uint32_t w = gtid; w < bm_words; w += gsz) {
+      uint32_t word = atomicExch(&a.bm[w], 0u);
+      if (!word) continue;
+      uint32_t at = atomicAdd(nctr, (uint32_t)__popc(word));
       while (word) {
         const uint32_t b = __ffs(word) - 1;
         word &= word - 1;
-        q[at++] = i * 32 + b;
+        st(&nxt[at++], w * 32 + b);
       }
     }
-    __syncthreads();
-    qlen = s_len;
-    __syncthreads();
-    if (tid == 0) s_len = 0;
+    grid.sync();
   }
 }
 
-// ---------------------------------------------------------------------------
-//  unfailed next hops: nh(v) = union over tight expanded preds, to fixed point
-// ---------------------------------------------------------------------------
-__global__ void nh_base_kernel(WiGraph g, const uint32_t* __restrict__ dist, uint32_t* nhb,
-                               uint32_t* changed) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (uint64_t)g.N * g.W) return;
-  const uint32_t v = (uint32_t)(t / g.W), j = (uint32_t)(t % g.W);
+__global__ __launch_bounds__(kCoopThreads) void gsssp_coop_kernel(CoopSssp a) {
+  cg::grid_group grid = cg::this_grid();
+  coop_sssp(grid, a);
+}
+
+// The unfailed result of a what-if batch in one cooperative launch:
+// SPF, next-hop bitsets in distance order (bucketed by distance value when
+// at most kMaxLevels distinct values occur, fixed-point sweeps otherwise),
+// result hash.
+constexpr uint32_t kLevelCap = 1u << 16;  // distance values bucketed directly
+constexpr uint32_t kMaxLevels = 1024;     // non-empty levels worth a barrier each
+
+struct BaseArgs {
+  CoopSssp sp;
+  WiGraph g;
+  uint32_t* nhb;        // [N][W]
+  uint32_t* lvl;        // [kLevelCap + 1] bucket counts / offsets
+  uint32_t* order;      // [N] nodes by distance
+  uint32_t* misc;       // [8]: 0 max dist, 1 nonempty levels, 2..4 flags
+  unsigned long long* H;
+};
+
+__device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* dist,
+                                            const uint32_t* nhb, uint32_t v, uint32_t j) {
   const uint32_t dv = dist[v];
-  if (dv == kInf || v == g.src) return;
   uint32_t acc = 0;
   for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
     const uint32_t u = g.col[e];
     if (g.ovl[u] && u != g.src) continue;
-    const uint32_t du = dist[u];
+    const uint32_t du = ld(&dist[u]);
     if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
     if (u == g.src) {
       const uint32_t jb = g.nbr_bit[v];
@@ -167,26 +194,127 @@ __global__ void nh_base_kernel(WiGraph g, const uint32_t* __restrict__ dist, uin
       acc |= ld(&nhb[(size_t)u * g.W + j]);
     }
   }
-  if (acc != ld(&nhb[(size_t)v * g.W + j])) {
-    st(&nhb[(size_t)v * g.W + j], acc);
-    *changed = 1;
-  }
+  return acc;
 }
 
-__global__ void hash_base_kernel(WiGraph g, const uint32_t* __restrict__ dist,
-                                 const uint32_t* __restrict__ nhb, unsigned long long* H) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t h = 0;
-  if (v < g.N && dist[v] != kInf) h = node_hash(v, dist[v], nhb + (size_t)v * g.W, g.W);
-  // wave sum, one atomic per wave
-  uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t l2 = __shfl_down(lo, d, 64), h2 = __shfl_down(hi, d, 64);
-    const uint64_t s = ((uint64_t)hi << 32 | lo) + ((uint64_t)h2 << 32 | l2);
-    lo = (uint32_t)s;
-    hi = (uint32_t)(s >> 32);
+__global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
+  cg::grid_group grid = cg::this_grid();
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gsz = gridDim.x * blockDim.x;
+  const WiGraph& g = a.g;
+  const uint32_t N = g.N, W = g.W;
+  const uint64_t NW = (uint64_t)N * W;
+  for (uint64_t x = gtid; x < NW; x += gsz) st(&a.nhb[x], 0u);
+  for (uint32_t i = gtid; i <= kLevelCap; i += gsz) st(&a.lvl[i], 0u);
+  if (gtid == 0) {
+    for (int i = 0; i < 8; ++i) st(&a.misc[i], 0u);
+    *a.H = 0;
   }
-  if ((threadIdx.x & 63) == 0) atomicAdd(H, ((unsigned long long)hi << 32) | lo);
+  coop_sssp(grid, a.sp);  // starts and ends with a grid barrier
+  const uint32_t* dist = a.sp.dist;
+  // ---- distance range and per-value counts ----
+  for (uint32_t v = gtid; v < N; v += gsz) {
+    const uint32_t d = ld(&dist[v]);
+    if (d != kInf) atomicMax(&a.misc[0], d);
+  }
+  grid.sync();
+  const uint32_t maxd = ld(&a.misc[0]);
+  bool levels = maxd < kLevelCap;
+  if (levels) {
+    for (uint32_t v = gtid; v < N; v += gsz) {
+      const uint32_t d = ld(&dist[v]);
+      if (d != kInf && atomicAdd(&a.lvl[d], 1u) == 0) atomicAdd(&a.misc[1], 1u);
+    }
+    grid.sync();
+    levels = ld(&a.misc[1]) <= kMaxLevels;
+  }
+  if (levels) {
+    // exclusive scan of the counts by block 0 (maxd + 1 <= kLevelCap entries)
+    if (blockIdx.x == 0) {
+      __shared__ uint32_t carry;
+      if (threadIdx.x == 0) carry = 0;
+      __syncthreads();
+      for (uint32_t base = 0; base <= maxd; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t x = i <= maxd ? ld(&a.lvl[i]) : 0u;
+        // block scan through LDS
+        __shared__ uint32_t buf[kCoopThreads];
+        buf[threadIdx.x] = x;
+        __syncthreads();
+        for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
+          const uint32_t y = threadIdx.x >= d ? buf[threadIdx.x - d] : 0u;
+          __syncthreads();
+          buf[threadIdx.x] += y;
+          __syncthreads();
+        }
+        const uint32_t incl = buf[threadIdx.x] + carry;
+        if (i <= maxd) st(&a.lvl[i], incl - x);
+        __syncthreads();
+        if (threadIdx.x == blockDim.x - 1) carry = incl;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) st(&a.lvl[maxd + 1], carry);
+    }
+    grid.sync();
+    // scatter nodes into distance order (lvl[d] advances to the bucket end)
+    for (uint32_t v = gtid; v < N; v += gsz) {
+      const uint32_t d = ld(&dist[v]);
+      if (d != kInf) st(&a.order[atomicAdd(&a.lvl[d], 1u)], v);
+    }
+    grid.sync();
+    // level by level: every predecessor of a level-d node sits at a lower level
+    uint32_t begin = ld(&a.lvl[0]);  // bucket 0 (the source) ends here
+    for (uint32_t d = 1; d <= maxd; ++d) {
+      const uint32_t end = ld(&a.lvl[d]);
+      if (end == begin) continue;  // empty level: uniform skip
+      const uint64_t items = (uint64_t)(end - begin) * W;
+      for (uint64_t x = gtid; x < items; x += gsz) {
+        const uint32_t v = ld(&a.order[begin + (uint32_t)(x / W)]);
+        const uint32_t j = (uint32_t)(x % W);
+        st(&a.nhb[(size_t)v * W + j], nh_word(g, dist, a.nhb, v, j));
+      }
+      begin = end;
+      grid.sync();
+    }
+  } else {
+    // fixed-point sweeps (monotone union over the DAG), flags rotate by 3
+    for (uint32_t it = 0;; ++it) {
+      bool any = false;
+      for (uint64_t x = gtid; x < NW; x += gsz) {
+        const uint32_t v = (uint32_t)(x / W), j = (uint32_t)(x % W);
+        if (v == g.src || ld(&dist[v]) == kInf) continue;
+        const uint32_t acc = nh_word(g, dist, a.nhb, v, j);
+        if (acc != ld(&a.nhb[x])) {
+          st(&a.nhb[x], acc);
+          any = true;
+        }
+      }
+      if (any) st(&a.misc[2 + it % 3], 1u);
+      if (gtid == 0) st(&a.misc[2 + (it + 1) % 3], 0u);
+      grid.sync();
+      if (!ld(&a.misc[2 + it % 3])) break;
+    }
+  }
+  // ---- result hash ----
+  uint64_t h = 0;
+  for (uint32_t v = gtid; v < N; v += gsz) {
+    const uint32_t d = ld(&dist[v]);
+    if (d == kInf) continue;
+    uint64_t f = 0xcbf29ce484222325ull;
+    for (uint32_t w = 0; w < W; ++w) {
+      f ^= ld(&a.nhb[(size_t)v * W + w]);
+      f *= 0x100000001b3ull;
+    }
+    h += mix64(mix64((uint64_t)v + 1) + d) ^ f;
+  }
+  uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+  for (int d = 32; d >= 1; d >>= 1) {  // wave sum, one atomic per wave
+    const uint32_t l2 = __shfl_down(lo, d, 64), h2 = __shfl_down(hi, d, 64);
+    const uint64_t t = ((uint64_t)hi << 32 | lo) + ((uint64_t)h2 << 32 | l2);
+    lo = (uint32_t)t;
+    hi = (uint32_t)(t >> 32);
+  }
+  if ((threadIdx.x & 63) == 0 && (lo | hi)) atomicAdd(a.H, ((unsigned long long)hi << 32) | lo);
 }
 
 // ---------------------------------------------------------------------------
@@ -220,7 +348,7 @@ __global__ void classify_kernel(WiGraph g, const uint32_t* __restrict__ dist,
 //  repair of one hot failure by a team (a wave, or a whole workgroup)
 // ---------------------------------------------------------------------------
 struct TeamCtl {
-  uint32_t n, ovf, flag[3];
+  uint32_t n, ovf, flag[3], dmin, dmax;
   unsigned long long ndist, nnh, dh;
 };
 
@@ -238,8 +366,8 @@ __device__ __forceinline__ void team_sync() {
 // Returns false (nothing written, scratch clean) when |D| exceeds cap.
 template <int TEAM>
 __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
-                       uint32_t* dnew, uint32_t* nhn, uint32_t cap, TeamCtl* ctl, uint32_t tt,
-                       uint32_t e_fail, spf_whatif_digest* out) {
+                       uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, uint32_t cap,
+                       TeamCtl* ctl, uint32_t tt, uint32_t e_fail, spf_whatif_digest* out) {
   const uint32_t W = g.W;
   const uint32_t l = g.link[e_fail];
   const uint32_t b = g.col[e_fail];
@@ -323,43 +451,106 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     team_sync<TEAM>();
     if (!ctl->flag[it % 3]) break;
   }
-  // ---- next hops inside D, to the fixed point ----
-  const uint32_t nw = n * W;
-  for (uint32_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
-  team_sync<TEAM>();
-  if (tt == 0) ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
-  team_sync<TEAM>();
-  for (uint32_t it = 0;; ++it) {
-    bool any = false;
-    for (uint32_t x = tt; x < nw; x += TEAM) {
-      const uint32_t i = x / W, j = x % W;
-      const uint32_t v = dlist[i];
-      const uint32_t dv = ld(&dnew[i]);
-      if (dv == kInf) continue;
-      uint32_t acc = 0;
-      for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-        if (g.link[e] == l) continue;
-        const uint32_t u = g.col[e];
-        if (g.ovl[u] && u != g.src) continue;
-        const uint32_t mu = ld(&mark[u]);
-        const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
-        if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
-        if (u == g.src) {
-          const uint32_t jb = g.nbr_bit[v];
-          if ((jb >> 5) == j) acc |= 1u << (jb & 31);
-        } else {
-          acc |= mu != kInf ? nhn[(size_t)mu * W + j] : B.nhb[(size_t)u * W + j];
-        }
-      }
-      if (acc != nhn[x]) {
-        nhn[x] = acc;
-        any = true;
+  // ---- next hops inside D ----
+  // nh(v) of a D node from its tight expanded predecessors (D or not)
+  auto nh_of = [&](uint32_t i, uint32_t j) -> uint32_t {
+    const uint32_t v = dlist[i];
+    const uint32_t dv = ld(&dnew[i]);
+    uint32_t acc = 0;
+    for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
+      if (g.link[e] == l) continue;
+      const uint32_t u = g.col[e];
+      if (g.ovl[u] && u != g.src) continue;
+      const uint32_t mu = ld(&mark[u]);
+      const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
+      if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
+      if (u == g.src) {
+        const uint32_t jb = g.nbr_bit[v];
+        if ((jb >> 5) == j) acc |= 1u << (jb & 31);
+      } else {
+        acc |= mu != kInf ? nhn[(size_t)mu * W + j] : B.nhb[(size_t)u * W + j];
       }
     }
-    if (any) ctl->flag[it % 3] = 1;
-    if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
+    return acc;
+  };
+  const uint32_t nw = n * W;
+  for (uint32_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
+  if (tt == 0) {
+    ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
+    ctl->dmin = kInf;
+    ctl->dmax = 0;
+  }
+  team_sync<TEAM>();
+  for (uint32_t i = tt; i < n; i += TEAM) {
+    const uint32_t d = ld(&dnew[i]);
+    if (d != kInf) {
+      atomicMin(&ctl->dmin, d);
+      atomicMax(&ctl->dmax, d);
+    }
+  }
+  team_sync<TEAM>();
+  const uint32_t dmin = ctl->dmin;
+  const uint32_t nlev = dmin == kInf ? 0u : ctl->dmax - dmin + 1;
+  if (nlev <= cap) {
+    // counting sort of D by new distance; a predecessor always sits in a
+    // lower level (positive metrics), so one pass per level is exact
+    for (uint32_t b = tt; b < nlev; b += TEAM) st(&lvl[b], 0u);
     team_sync<TEAM>();
-    if (!ctl->flag[it % 3]) break;
+    for (uint32_t i = tt; i < n; i += TEAM) {
+      const uint32_t d = ld(&dnew[i]);
+      if (d != kInf) atomicAdd(&lvl[d - dmin], 1u);
+    }
+    team_sync<TEAM>();
+    if (tt < 64) {  // exclusive scan by the team's first wave
+      uint32_t carry = 0;
+      for (uint32_t base = 0; base < nlev; base += 64) {
+        const uint32_t b = base + tt;
+        const uint32_t x = b < nlev ? ld(&lvl[b]) : 0u;
+        uint32_t inc = x;
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(inc, d, 64);
+          if (tt >= (uint32_t)d) inc += y;
+        }
+        if (b < nlev) st(&lvl[b], carry + inc - x);
+        carry += __shfl(inc, 63, 64);
+      }
+    }
+    team_sync<TEAM>();
+    for (uint32_t i = tt; i < n; i += TEAM) {
+      const uint32_t d = ld(&dnew[i]);
+      if (d != kInf) st(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
+    }
+    team_sync<TEAM>();
+    uint32_t begin = 0;
+    for (uint32_t b = 0; b < nlev; ++b) {
+      const uint32_t end = ld(&lvl[b]);
+      if (end == begin) continue;
+      const uint32_t items = (end - begin) * W;
+      for (uint32_t x = tt; x < items; x += TEAM) {
+        const uint32_t i = ld(&ord[begin + x / W]), j = x % W;
+        nhn[(size_t)i * W + j] = nh_of(i, j);
+      }
+      begin = end;
+      team_sync<TEAM>();
+    }
+  } else {
+    // fixed-point sweeps (monotone union over the DAG)
+    for (uint32_t it = 0;; ++it) {
+      bool any = false;
+      for (uint32_t x = tt; x < nw; x += TEAM) {
+        const uint32_t i = x / W, j = x % W;
+        if (ld(&dnew[i]) == kInf) continue;
+        const uint32_t acc = nh_of(i, j);
+        if (acc != nhn[x]) {
+          nhn[x] = acc;
+          any = true;
+        }
+      }
+      if (any) ctl->flag[it % 3] = 1;
+      if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
+      team_sync<TEAM>();
+      if (!ctl->flag[it % 3]) break;
+    }
   }
   // ---- digest delta over D, scratch reset ----
   uint32_t nd_ = 0, nn_ = 0;
@@ -392,7 +583,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
 __global__ __launch_bounds__(256) void repair_wave_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ hot, const uint32_t* __restrict__ n_hot,
     uint32_t* cursor, uint2* big, uint32_t* n_big, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
-    uint32_t* nhn, spf_whatif_digest* out) {
+    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out) {
   __shared__ TeamCtl ctl[4];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t team = (size_t)blockIdx.x * 4 + w;
@@ -400,6 +591,8 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
   dlist += team * kWaveCap;
   dnew += team * kWaveCap;
   nhn += team * kWaveCap * g.W;
+  lvl += team * (kWaveCap + 1);
+  ord += team * kWaveCap;
   const uint32_t total = *n_hot;
   for (;;) {
     uint32_t k = 0;
@@ -407,7 +600,8 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
     k = __shfl(k, 0, 64);
     if (k >= total) break;
     const uint2 h = hot[k];
-    if (!repair<64>(g, B, mark, dlist, dnew, nhn, kWaveCap, &ctl[w], lane, h.y, out + h.x)) {
+    if (!repair<64>(g, B, mark, dlist, dnew, nhn, lvl, ord, kWaveCap, &ctl[w], lane, h.y,
+                    out + h.x)) {
       if (lane == 0) big[atomicAdd(n_big, 1u)] = h;
     }
   }
@@ -415,17 +609,20 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
 
 __global__ __launch_bounds__(1024) void repair_block_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
-    uint32_t* mark, uint32_t* dlist, uint32_t* dnew, uint32_t* nhn, spf_whatif_digest* out) {
+    uint32_t* mark, uint32_t* dlist, uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord,
+    spf_whatif_digest* out) {
   __shared__ TeamCtl ctl;
   const size_t team = blockIdx.x;
   mark += team * g.N;
   dlist += team * g.N;
   dnew += team * g.N;
   nhn += team * (size_t)g.N * g.W;
+  lvl += team * ((size_t)g.N + 1);
+  ord += team * (size_t)g.N;
   const uint32_t total = *n_big;
   for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
     const uint2 h = big[k];
-    repair<1024>(g, B, mark, dlist, dnew, nhn, g.N, &ctl, threadIdx.x, h.y, out + h.x);
+    repair<1024>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, &ctl, threadIdx.x, h.y, out + h.x);
   }
 }
 
@@ -438,12 +635,14 @@ __global__ void base_digest_kernel(spf_whatif_digest* o, const unsigned long lon
 struct spf_whatif_plan {
   spf_ctx* ctx = nullptr;
   uint32_t src = 0, n_fail = 0, W = 0, wave_teams = 0;
-  DevBuf<uint32_t> d_fails, d_link_edge, d_nbr_bit, d_dist, d_q, d_bm, d_nhb, d_flag;
+  DevBuf<uint32_t> d_fails, d_link_edge, d_nbr_bit, d_dist, d_q, d_q2, d_bm, d_nhb, d_ctr;
+  DevBuf<uint32_t> d_lvl, d_order, d_misc;
   DevBuf<unsigned long long> d_H;
   DevBuf<uint2> d_hot, d_big;
   DevBuf<uint32_t> d_cnt;  // [0] n_hot, [1] cursor, [2] n_big
-  DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn;  // wave-team scratch
-  DevBuf<uint32_t> b_mark, b_dlist, b_dnew, b_nhn;  // workgroup-team scratch
+  uint32_t big_teams = 0;
+  DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
+  DevBuf<uint32_t> b_mark, b_dlist, b_dnew, b_nhn, b_lvl, b_ord;  // workgroup-team scratch
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
   ~spf_whatif_plan() {
@@ -453,12 +652,20 @@ struct spf_whatif_plan {
 
 namespace spfi {
 
+uint32_t coop_blocks(spf_ctx* c) { return c->n_cu; }  // one 512-thread block per CU
+
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
-                        uint32_t* q, uint32_t* bm, hipStream_t s) {
-  hipLaunchKernelGGL(gsssp_kernel, dim3(1), dim3(kGThreads), 0, s, c->d_row_ptr.p, c->d_col.p,
-                     c->d_wt.p, c->d_ovl.p, c->d_link.p, ign, src, c->N, hop ? 1u : 0u, dist, q,
-                     bm);
-  HIP_TRY(c, hipGetLastError());
+                        hipStream_t s) {
+  const uint32_t N = c->N;
+  HIP_TRY(c, c->d_gq.alloc(N));
+  HIP_TRY(c, c->d_gq2.alloc(N));
+  HIP_TRY(c, c->d_gbm.alloc((N + 31) / 32));
+  HIP_TRY(c, c->d_gctr.alloc(4));
+  CoopSssp a{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, ign, N, src,
+             hop ? 1u : 0u, dist, c->d_gq.p, c->d_gq2.p, c->d_gbm.p, c->d_gctr.p};
+  void* args[] = {&a};
+  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)gsssp_coop_kernel, dim3(coop_blocks(c)),
+                                        dim3(kCoopThreads), args, 0, s));
   return SPF_OK;
 }
 
@@ -505,9 +712,13 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->d_nbr_bit.upload(nbr_bit.data(), N, c->stream));
   HIP_TRY(c, p->d_dist.alloc(N));
   HIP_TRY(c, p->d_q.alloc(N));
+  HIP_TRY(c, p->d_q2.alloc(N));
   HIP_TRY(c, p->d_bm.alloc((N + 31) / 32));
   HIP_TRY(c, p->d_nhb.alloc((size_t)N * p->W));
-  HIP_TRY(c, p->d_flag.alloc(1));
+  HIP_TRY(c, p->d_ctr.alloc(4));
+  HIP_TRY(c, p->d_lvl.alloc(kLevelCap + 1));
+  HIP_TRY(c, p->d_order.alloc(N));
+  HIP_TRY(c, p->d_misc.alloc(8));
   HIP_TRY(c, p->d_H.alloc(1));
   HIP_TRY(c, p->d_hot.alloc(std::max<uint32_t>(1, p->n_fail)));
   HIP_TRY(c, p->d_big.alloc(std::max<uint32_t>(1, p->n_fail)));
@@ -517,13 +728,22 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->w_dlist.alloc(wt * kWaveCap));
   HIP_TRY(c, p->w_dnew.alloc(wt * kWaveCap));
   HIP_TRY(c, p->w_nhn.alloc(wt * kWaveCap * p->W));
-  HIP_TRY(c, p->b_mark.alloc((size_t)kBigTeams * N));
-  HIP_TRY(c, p->b_dlist.alloc((size_t)kBigTeams * N));
-  HIP_TRY(c, p->b_dnew.alloc((size_t)kBigTeams * N));
-  HIP_TRY(c, p->b_nhn.alloc((size_t)kBigTeams * N * p->W));
+  HIP_TRY(c, p->w_lvl.alloc(wt * (kWaveCap + 1)));
+  HIP_TRY(c, p->w_ord.alloc(wt * kWaveCap));
+  {  // workgroup teams: one per CU within the scratch budget
+    const size_t per_team = 4ull * ((size_t)N * (5 + p->W) + 1);
+    p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / per_team));
+  }
+  const size_t bt = p->big_teams;
+  HIP_TRY(c, p->b_mark.alloc(bt * N));
+  HIP_TRY(c, p->b_dlist.alloc(bt * N));
+  HIP_TRY(c, p->b_dnew.alloc(bt * N));
+  HIP_TRY(c, p->b_nhn.alloc(bt * N * p->W));
+  HIP_TRY(c, p->b_lvl.alloc(bt * (N + 1)));
+  HIP_TRY(c, p->b_ord.alloc(bt * N));
   // marks start (and are always left) at kInf
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
-  HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, (size_t)kBigTeams * N * 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   *out = p.release();
   return SPF_OK;
@@ -554,26 +774,15 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   }
   WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
             p->d_nbr_bit.p, N, p->src, p->W};
-  // 1. unfailed SPF, next hops, hash
-  spf_status st = launch_gsssp(c, p->src, false, nullptr, p->d_dist.p, p->d_q.p, p->d_bm.p, s);
-  if (st != SPF_OK) return st;
-  HIP_TRY(c, hipMemsetAsync(p->d_nhb.p, 0, 4ull * N * p->W, s));
-  const uint64_t items = (uint64_t)N * p->W;
-  for (int pass = 0;; ++pass) {
-    uint32_t changed = 0;
-    HIP_TRY(c, hipMemsetAsync(p->d_flag.p, 0, 4, s));
-    hipLaunchKernelGGL(nh_base_kernel, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, s, g,
-                       p->d_dist.p, p->d_nhb.p, p->d_flag.p);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipMemcpyAsync(&changed, p->d_flag.p, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    if (!changed) break;
-    if (pass > (int)N) return fail(c, SPF_E_HIP, "next-hop propagation did not converge");
+  // 1. unfailed SPF, next hops, hash: one cooperative launch
+  {
+    BaseArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr,
+                        N, p->src, 0u, p->d_dist.p, p->d_q.p, p->d_q2.p, p->d_bm.p, p->d_ctr.p},
+               g, p->d_nhb.p, p->d_lvl.p, p->d_order.p, p->d_misc.p, p->d_H.p};
+    void* args[] = {&a};
+    HIP_TRY(c, hipLaunchCooperativeKernel((const void*)whatif_base_kernel, dim3(coop_blocks(c)),
+                                          dim3(kCoopThreads), args, 0, s));
   }
-  HIP_TRY(c, hipMemsetAsync(p->d_H.p, 0, 8, s));
-  hipLaunchKernelGGL(hash_base_kernel, dim3((N + 255) / 256), dim3(256), 0, s, g, p->d_dist.p,
-                     p->d_nhb.p, p->d_H.p);
-  HIP_TRY(c, hipGetLastError());
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   // 2. failures
   HIP_TRY(c, hipMemsetAsync(p->d_cnt.p, 0, 16, s));
@@ -585,10 +794,12 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     WiBase B{p->d_dist.p, p->d_nhb.p, p->d_H.p};
     hipLaunchKernelGGL(repair_wave_kernel, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                        p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                       p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, d_out);
+                       p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p, p->w_ord.p,
+                       d_out);
     HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(repair_block_kernel, dim3(kBigTeams), dim3(1024), 0, s, g, B, p->d_big.p,
-                       p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p, d_out);
+    hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
+                       p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
+                       p->b_lvl.p, p->b_ord.p, d_out);
     HIP_TRY(c, hipGetLastError());
   }
   if (d_base) {
