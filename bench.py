@@ -431,6 +431,9 @@ def main() -> None:
         },
         "cpu_baseline": None,
     }
+    if isinstance(wl, WhatIfAllLinks):
+        out["config"]["hot_failures_per_rank"] = wl.n_hot
+        out["config"]["workgroup_team_failures_per_rank"] = wl.n_big
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         out["cpu_baseline"] = wl.cpu_baseline(args.cpu_budget)
     if rank == 0:

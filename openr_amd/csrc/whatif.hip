@@ -36,6 +36,8 @@
 
 #include <hip/hip_cooperative_groups.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 
 using namespace spfi;
@@ -45,12 +47,20 @@ namespace {
 constexpr uint32_t kBusy = 0xFFFFFFFEu;
 constexpr uint32_t kWaveCap = 1024;            // |D| a wave team can hold
 constexpr size_t kBigScratch = 8ull << 30;     // HBM budget of the workgroup teams
+constexpr uint32_t kDialLevels = 1024;         // distinct distances settled bucket by bucket
+constexpr uint32_t kHubDeg = 32;               // nodes above this degree get a whole wave
 
 __device__ __forceinline__ uint32_t ld(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) x = min(x, (uint32_t)__shfl_xor(x, d, 64));
+  return x;
 }
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -348,7 +358,7 @@ __global__ void classify_kernel(WiGraph g, const uint32_t* __restrict__ dist,
 //  repair of one hot failure by a team (a wave, or a whole workgroup)
 // ---------------------------------------------------------------------------
 struct TeamCtl {
-  uint32_t n, ovf, flag[3], dmin, dmax;
+  uint32_t n, ovf, flag[3], dmin, dmax, nxt[3], lc[3], hub;
   unsigned long long ndist, nnh, dh;
 };
 
@@ -367,13 +377,23 @@ __device__ __forceinline__ void team_sync() {
 template <int TEAM>
 __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
                        uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, uint32_t cap,
-                       TeamCtl* ctl, uint32_t tt, uint32_t e_fail, spf_whatif_digest* out) {
+                       TeamCtl* ctl, uint32_t tt, uint32_t e_fail, spf_whatif_digest* out,
+                       unsigned long long* prof = nullptr) {
+  // diagnostics (SPF_WHATIF_PROF): phase clocks of this team's last failure
+#define WI_STAMP(k)                                                      \
+  do {                                                                   \
+    if (prof && tt == 0) prof[k] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+  WI_STAMP(0);
   const uint32_t W = g.W;
+  constexpr uint32_t kWaves = TEAM / 64;
+  const uint32_t lane = tt & 63, wv = tt >> 6;
   const uint32_t l = g.link[e_fail];
   const uint32_t b = g.col[e_fail];
   if (tt == 0) {
     ctl->n = 1;
     ctl->ovf = 0;
+    ctl->hub = 0;
     ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
     ctl->ndist = ctl->nnh = ctl->dh = 0;
     dlist[0] = b;
@@ -386,29 +406,50 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     const uint32_t n = ctl->n;
     team_sync<TEAM>();
     if (lo >= n || ctl->ovf) break;
+    // a thread per frontier node; hubs (thousands of edges) are queued in
+    // ord and expanded by a whole wave each
+    auto child = [&](uint32_t dv, uint32_t e) {
+      const uint32_t c = g.col[e];
+      if (dv + g.wt[e] != B.dist[c]) return;
+      if (atomicCAS(&mark[c], kInf, kBusy) != kInf) return;
+      const uint32_t idx = atomicAdd(&ctl->n, 1u);
+      if (idx < cap) {
+        dlist[idx] = c;
+        st(&mark[c], idx);
+      } else {
+        st(&mark[c], kInf);
+        ctl->ovf = 1;
+      }
+    };
     for (uint32_t i = lo + tt; i < n; i += TEAM) {
       const uint32_t v = dlist[i];
       if (g.ovl[v]) continue;  // drained (v != src): no DAG children
+      const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
+      if (b1 - b0 > kHubDeg) {
+        st(&ord[atomicAdd(&ctl->hub, 1u)], i);
+        continue;
+      }
       const uint32_t dv = B.dist[v];
-      for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-        const uint32_t c = g.col[e];
-        if (dv + g.wt[e] != B.dist[c]) continue;
-        if (atomicCAS(&mark[c], kInf, kBusy) != kInf) continue;
-        const uint32_t idx = atomicAdd(&ctl->n, 1u);
-        if (idx < cap) {
-          dlist[idx] = c;
-          st(&mark[c], idx);
-        } else {
-          st(&mark[c], kInf);
-          ctl->ovf = 1;
-        }
+      for (uint32_t e = b0; e < b1; ++e) child(dv, e);
+    }
+    team_sync<TEAM>();
+    {
+      const uint32_t nh_ = ctl->hub;
+      for (uint32_t k = wv; k < nh_; k += kWaves) {
+        const uint32_t v = dlist[ld(&ord[k])];
+        const uint32_t dv = B.dist[v];
+        for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) child(dv, e);
       }
     }
+    team_sync<TEAM>();
+    if (tt == 0) ctl->hub = 0;
     lo = n;
     team_sync<TEAM>();
   }
   const uint32_t n = min(ctl->n, cap);
   const bool ovf = ctl->ovf != 0;
+  WI_STAMP(1);
+  if (prof && tt == 0) prof[8] = n;
   team_sync<TEAM>();
   if (ovf) {
     for (uint32_t i = tt; i < n; i += TEAM) st(&mark[dlist[i]], kInf);
@@ -416,43 +457,42 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     return false;
   }
   // ---- seeds: best in-edge from outside D (unchanged distances) ----
+  auto seed_edge = [&](uint32_t e) -> uint32_t {
+    if (g.link[e] == l) return kInf;
+    const uint32_t u = g.col[e];
+    if (ld(&mark[u]) != kInf) return kInf;
+    if (g.ovl[u] && u != g.src) return kInf;
+    const uint32_t du = B.dist[u];
+    return du == kInf ? kInf : du + g.wt[g.rev[e]];
+  };
   for (uint32_t i = tt; i < n; i += TEAM) {
     const uint32_t v = dlist[i];
-    uint32_t best = kInf;
-    for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-      if (g.link[e] == l) continue;
-      const uint32_t u = g.col[e];
-      if (ld(&mark[u]) != kInf) continue;
-      if (g.ovl[u] && u != g.src) continue;
-      const uint32_t du = B.dist[u];
-      if (du == kInf) continue;
-      best = min(best, du + g.wt[g.rev[e]]);
+    const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
+    if (b1 - b0 > kHubDeg) {
+      st(&ord[atomicAdd(&ctl->hub, 1u)], i);
+      continue;
     }
+    uint32_t best = kInf;
+    for (uint32_t e = b0; e < b1; ++e) best = min(best, seed_edge(e));
     st(&dnew[i], best);
   }
   team_sync<TEAM>();
-  // ---- label-correcting sweeps inside D ----
-  for (uint32_t it = 0;; ++it) {
-    bool any = false;
-    for (uint32_t i = tt; i < n; i += TEAM) {
+  {
+    const uint32_t nh_ = ctl->hub;
+    for (uint32_t k = wv; k < nh_; k += kWaves) {
+      const uint32_t i = ld(&ord[k]);
       const uint32_t v = dlist[i];
-      const uint32_t dv = ld(&dnew[i]);
-      if (dv == kInf || g.ovl[v]) continue;
-      for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-        if (g.link[e] == l) continue;
-        const uint32_t ic = ld(&mark[g.col[e]]);
-        if (ic == kInf) continue;
-        const uint32_t nd = dv + g.wt[e];
-        if (nd < atomicMin(&dnew[ic], nd)) any = true;
-      }
+      uint32_t best = kInf;
+      for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64)
+        best = min(best, seed_edge(e));
+      best = wave_min32(best);
+      if (lane == 0) st(&dnew[i], best);
     }
-    if (any) ctl->flag[it % 3] = 1;
-    if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
-    team_sync<TEAM>();
-    if (!ctl->flag[it % 3]) break;
   }
-  // ---- next hops inside D ----
-  // nh(v) of a D node from its tight expanded predecessors (D or not)
+  team_sync<TEAM>();
+  if (tt == 0) ctl->hub = 0;
+  // nh word j of a D node from its tight expanded predecessors (D or not);
+  // used by the fixed-point fallback
   auto nh_of = [&](uint32_t i, uint32_t j) -> uint32_t {
     const uint32_t v = dlist[i];
     const uint32_t dv = ld(&dnew[i]);
@@ -473,77 +513,145 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }
     return acc;
   };
+  // nh row of a D node whose distance is final, every tight predecessor's
+  // row final too: one thread per node, the W words in a loop
+  auto nh_row = [&](uint32_t i, uint32_t v, uint32_t dv) {
+    uint32_t* row = nhn + (size_t)i * W;
+    for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
+      if (g.link[e] == l) continue;
+      const uint32_t u = g.col[e];
+      if (g.ovl[u] && u != g.src) continue;
+      const uint32_t mu = ld(&mark[u]);
+      const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
+      if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
+      if (u == g.src) {
+        const uint32_t jb = g.nbr_bit[v];
+        row[jb >> 5] |= 1u << (jb & 31);
+      } else {
+        const uint32_t* from = mu != kInf ? nhn + (size_t)mu * W : B.nhb + (size_t)u * W;
+        for (uint32_t j = 0; j < W; ++j) row[j] |= from[j];
+      }
+    }
+  };
   const uint32_t nw = n * W;
   for (uint32_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
   if (tt == 0) {
-    ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
     ctl->dmin = kInf;
-    ctl->dmax = 0;
+    ctl->nxt[0] = kInf;
+    ctl->lc[0] = 0;
   }
   team_sync<TEAM>();
-  for (uint32_t i = tt; i < n; i += TEAM) {
-    const uint32_t d = ld(&dnew[i]);
-    if (d != kInf) {
-      atomicMin(&ctl->dmin, d);
-      atomicMax(&ctl->dmax, d);
+  {
+    uint32_t m = kInf;
+    for (uint32_t i = tt; i < n; i += TEAM) m = min(m, ld(&dnew[i]));
+    if (m != kInf) atomicMin(&ctl->dmin, m);
+  }
+  team_sync<TEAM>();
+  WI_STAMP(2);
+  // ---- Dial: settle D one distance value at a time (metrics are positive:
+  // a node holding the smallest pending value is final), next hops inline ----
+  bool settled = true;
+  uint32_t t = ctl->dmin;
+  for (uint32_t it = 0; t != kInf; ++it) {
+    if (it >= kDialLevels) {  // too many distinct values: sweep instead
+      settled = false;
+      break;
     }
-  }
-  team_sync<TEAM>();
-  const uint32_t dmin = ctl->dmin;
-  const uint32_t nlev = dmin == kInf ? 0u : ctl->dmax - dmin + 1;
-  if (nlev <= cap) {
-    // counting sort of D by new distance; a predecessor always sits in a
-    // lower level (positive metrics), so one pass per level is exact
-    for (uint32_t b = tt; b < nlev; b += TEAM) st(&lvl[b], 0u);
-    team_sync<TEAM>();
+    uint32_t* next = &ctl->nxt[it % 3];
+    uint32_t* cnt = &ctl->lc[it % 3];
+    if (tt == 0) {  // the next level's slots, last read two levels ago
+      ctl->nxt[(it + 1) % 3] = kInf;
+      ctl->lc[(it + 1) % 3] = 0;
+      ctl->lc[(it + 2) % 3] = 0;  // this level's hub counter
+    }
+    // (a) the level's nodes (their distance is final) into ord
+    uint32_t m = kInf;
     for (uint32_t i = tt; i < n; i += TEAM) {
       const uint32_t d = ld(&dnew[i]);
-      if (d != kInf) atomicAdd(&lvl[d - dmin], 1u);
+      if (d == t) st(&ord[atomicAdd(cnt, 1u)], i);
+      else if (d != kInf && d > t) m = min(m, d);
     }
     team_sync<TEAM>();
-    if (tt < 64) {  // exclusive scan by the team's first wave
-      uint32_t carry = 0;
-      for (uint32_t base = 0; base < nlev; base += 64) {
-        const uint32_t b = base + tt;
-        const uint32_t x = b < nlev ? ld(&lvl[b]) : 0u;
-        uint32_t inc = x;
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t y = __shfl_up(inc, d, 64);
-          if (tt >= (uint32_t)d) inc += y;
+    // (b) level nodes: next hops from their tight predecessors, then relax
+    // their edges.  A thread per node; hubs (queued after the level list)
+    // by a whole wave: ballot over the in-edges, coalesced row ORs.
+    const uint32_t K = *cnt;
+    uint32_t* hubs = ord + K;
+    uint32_t* hub_cnt = &ctl->lc[(it + 2) % 3];  // free this level
+    auto relax = [&](uint32_t v, uint32_t e) {
+      if (g.link[e] == l) return;
+      const uint32_t ic = ld(&mark[g.col[e]]);
+      if (ic == kInf) return;
+      const uint32_t nd = t + g.wt[e];
+      if (nd < atomicMin(&dnew[ic], nd)) m = min(m, nd);
+    };
+    for (uint32_t k = tt; k < K; k += TEAM) {
+      const uint32_t i = ld(&ord[k]);
+      const uint32_t v = dlist[i];
+      const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
+      if (b1 - b0 > kHubDeg) {
+        st(&hubs[atomicAdd(hub_cnt, 1u)], i);
+        continue;
+      }
+      nh_row(i, v, t);
+      if (!g.ovl[v])
+        for (uint32_t e = b0; e < b1; ++e) relax(v, e);
+    }
+    team_sync<TEAM>();
+    const uint32_t H_ = *hub_cnt;
+    for (uint32_t k = wv; k < H_; k += kWaves) {
+      const uint32_t i = ld(&hubs[k]);
+      const uint32_t v = dlist[i];
+      uint32_t* row = nhn + (size_t)i * W;
+      const uint32_t jb = g.nbr_bit[v];
+      bool from_src = false;
+      for (uint32_t base = g.row_ptr[v]; base < g.row_ptr[v + 1]; base += 64) {
+        const uint32_t e = base + lane;
+        uint32_t u = 0, mu = kInf;
+        bool tight = false;
+        if (e < g.row_ptr[v + 1] && g.link[e] != l) {
+          u = g.col[e];
+          if (!(g.ovl[u] && u != g.src)) {
+            mu = ld(&mark[u]);
+            const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
+            tight = du != kInf && du + g.wt[g.rev[e]] == t;
+          }
         }
-        if (b < nlev) st(&lvl[b], carry + inc - x);
-        carry += __shfl(inc, 63, 64);
+        if (tight && u == g.src) {
+          from_src = true;
+          tight = false;
+        }
+        for (uint64_t mask = __ballot(tight); mask; mask &= mask - 1) {
+          const uint32_t b = __ffsll((unsigned long long)mask) - 1;
+          const uint32_t pu = __shfl(u, b, 64), pm = __shfl(mu, b, 64);
+          const uint32_t* from = pm != kInf ? nhn + (size_t)pm * W : B.nhb + (size_t)pu * W;
+          for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
+        }
       }
+      if (__ballot(from_src) && lane == ((jb >> 5) & 63)) row[jb >> 5] |= 1u << (jb & 31);
+      if (g.ovl[v]) continue;  // drained: no transit
+      for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) relax(v, e);
     }
+    if (m != kInf) atomicMin(next, m);
     team_sync<TEAM>();
-    for (uint32_t i = tt; i < n; i += TEAM) {
-      const uint32_t d = ld(&dnew[i]);
-      if (d != kInf) st(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
-    }
-    team_sync<TEAM>();
-    uint32_t begin = 0;
-    for (uint32_t b = 0; b < nlev; ++b) {
-      const uint32_t end = ld(&lvl[b]);
-      if (end == begin) continue;
-      const uint32_t items = (end - begin) * W;
-      for (uint32_t x = tt; x < items; x += TEAM) {
-        const uint32_t i = ld(&ord[begin + x / W]), j = x % W;
-        nhn[(size_t)i * W + j] = nh_of(i, j);
-      }
-      begin = end;
-      team_sync<TEAM>();
-    }
-  } else {
-    // fixed-point sweeps (monotone union over the DAG)
+    t = *next;
+    if (prof && tt == 0) prof[9] = it + 1;
+  }
+  WI_STAMP(3);
+  if (!settled) {
+    // ---- label-correcting sweeps inside D ----
     for (uint32_t it = 0;; ++it) {
       bool any = false;
-      for (uint32_t x = tt; x < nw; x += TEAM) {
-        const uint32_t i = x / W, j = x % W;
-        if (ld(&dnew[i]) == kInf) continue;
-        const uint32_t acc = nh_of(i, j);
-        if (acc != nhn[x]) {
-          nhn[x] = acc;
-          any = true;
+      for (uint32_t i = tt; i < n; i += TEAM) {
+        const uint32_t v = dlist[i];
+        const uint32_t dv = ld(&dnew[i]);
+        if (dv == kInf || g.ovl[v]) continue;
+        for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
+          if (g.link[e] == l) continue;
+          const uint32_t ic = ld(&mark[g.col[e]]);
+          if (ic == kInf) continue;
+          const uint32_t nd = dv + g.wt[e];
+          if (nd < atomicMin(&dnew[ic], nd)) any = true;
         }
       }
       if (any) ctl->flag[it % 3] = 1;
@@ -551,7 +659,88 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       team_sync<TEAM>();
       if (!ctl->flag[it % 3]) break;
     }
+
+    const uint32_t nw = n * W;
+    for (uint32_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
+    if (tt == 0) {
+      ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
+      ctl->dmin = kInf;
+      ctl->dmax = 0;
+    }
+    team_sync<TEAM>();
+    for (uint32_t i = tt; i < n; i += TEAM) {
+      const uint32_t d = ld(&dnew[i]);
+      if (d != kInf) {
+        atomicMin(&ctl->dmin, d);
+        atomicMax(&ctl->dmax, d);
+      }
+    }
+    team_sync<TEAM>();
+    const uint32_t dmin = ctl->dmin;
+    const uint32_t nlev = dmin == kInf ? 0u : ctl->dmax - dmin + 1;
+    if (nlev <= cap) {
+      // counting sort of D by new distance; a predecessor always sits in a
+      // lower level (positive metrics), so one pass per level is exact
+      for (uint32_t b = tt; b < nlev; b += TEAM) st(&lvl[b], 0u);
+      team_sync<TEAM>();
+      for (uint32_t i = tt; i < n; i += TEAM) {
+        const uint32_t d = ld(&dnew[i]);
+        if (d != kInf) atomicAdd(&lvl[d - dmin], 1u);
+      }
+      team_sync<TEAM>();
+      if (tt < 64) {  // exclusive scan by the team's first wave
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < nlev; base += 64) {
+          const uint32_t b = base + tt;
+          const uint32_t x = b < nlev ? ld(&lvl[b]) : 0u;
+          uint32_t inc = x;
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if (tt >= (uint32_t)d) inc += y;
+          }
+          if (b < nlev) st(&lvl[b], carry + inc - x);
+          carry += __shfl(inc, 63, 64);
+        }
+      }
+      team_sync<TEAM>();
+      for (uint32_t i = tt; i < n; i += TEAM) {
+        const uint32_t d = ld(&dnew[i]);
+        if (d != kInf) st(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
+      }
+      team_sync<TEAM>();
+      uint32_t begin = 0;
+      for (uint32_t b = 0; b < nlev; ++b) {
+        const uint32_t end = ld(&lvl[b]);
+        if (end == begin) continue;
+        const uint32_t items = (end - begin) * W;
+        for (uint32_t x = tt; x < items; x += TEAM) {
+          const uint32_t i = ld(&ord[begin + x / W]), j = x % W;
+          nhn[(size_t)i * W + j] = nh_of(i, j);
+        }
+        begin = end;
+        team_sync<TEAM>();
+      }
+    } else {
+      // fixed-point sweeps (monotone union over the DAG)
+      for (uint32_t it = 0;; ++it) {
+        bool any = false;
+        for (uint32_t x = tt; x < nw; x += TEAM) {
+          const uint32_t i = x / W, j = x % W;
+          if (ld(&dnew[i]) == kInf) continue;
+          const uint32_t acc = nh_of(i, j);
+          if (acc != nhn[x]) {
+            nhn[x] = acc;
+            any = true;
+          }
+        }
+        if (any) ctl->flag[it % 3] = 1;
+        if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
+        team_sync<TEAM>();
+        if (!ctl->flag[it % 3]) break;
+      }
+    }
   }
+  WI_STAMP(4);
   // ---- digest delta over D, scratch reset ----
   uint32_t nd_ = 0, nn_ = 0;
   uint64_t dh = 0;
@@ -575,6 +764,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     *out = spf_whatif_digest{(uint32_t)ctl->ndist, (uint32_t)ctl->nnh,
                              (uint64_t)(*B.H + ctl->dh)};
   team_sync<TEAM>();
+  WI_STAMP(5);
+#undef WI_STAMP
   return true;
 }
 
@@ -592,7 +783,7 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
   dnew += team * kWaveCap;
   nhn += team * kWaveCap * g.W;
   lvl += team * (kWaveCap + 1);
-  ord += team * kWaveCap;
+  ord += team * 2 * kWaveCap;  // level list + its hubs
   const uint32_t total = *n_hot;
   for (;;) {
     uint32_t k = 0;
@@ -610,7 +801,7 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
 __global__ __launch_bounds__(1024) void repair_block_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
     uint32_t* mark, uint32_t* dlist, uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord,
-    spf_whatif_digest* out) {
+    spf_whatif_digest* out, unsigned long long* prof) {
   __shared__ TeamCtl ctl;
   const size_t team = blockIdx.x;
   mark += team * g.N;
@@ -618,11 +809,12 @@ __global__ __launch_bounds__(1024) void repair_block_kernel(
   dnew += team * g.N;
   nhn += team * (size_t)g.N * g.W;
   lvl += team * ((size_t)g.N + 1);
-  ord += team * (size_t)g.N;
+  ord += team * 2 * (size_t)g.N;  // level list + its hubs
   const uint32_t total = *n_big;
   for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
     const uint2 h = big[k];
-    repair<1024>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, &ctl, threadIdx.x, h.y, out + h.x);
+    repair<1024>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, &ctl, threadIdx.x, h.y, out + h.x,
+                 prof ? prof + team * 16 : nullptr);
   }
 }
 
@@ -641,6 +833,7 @@ struct spf_whatif_plan {
   DevBuf<uint2> d_hot, d_big;
   DevBuf<uint32_t> d_cnt;  // [0] n_hot, [1] cursor, [2] n_big
   uint32_t big_teams = 0;
+  DevBuf<unsigned long long> d_prof;  // SPF_WHATIF_PROF diagnostics
   DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
   DevBuf<uint32_t> b_mark, b_dlist, b_dnew, b_nhn, b_lvl, b_ord;  // workgroup-team scratch
   std::vector<hipEvent_t> ev;
@@ -729,9 +922,9 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->w_dnew.alloc(wt * kWaveCap));
   HIP_TRY(c, p->w_nhn.alloc(wt * kWaveCap * p->W));
   HIP_TRY(c, p->w_lvl.alloc(wt * (kWaveCap + 1)));
-  HIP_TRY(c, p->w_ord.alloc(wt * kWaveCap));
+  HIP_TRY(c, p->w_ord.alloc(wt * 2 * kWaveCap));
   {  // workgroup teams: one per CU within the scratch budget
-    const size_t per_team = 4ull * ((size_t)N * (5 + p->W) + 1);
+    const size_t per_team = 4ull * ((size_t)N * (6 + p->W) + 1);
     p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / per_team));
   }
   const size_t bt = p->big_teams;
@@ -740,10 +933,14 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->b_dnew.alloc(bt * N));
   HIP_TRY(c, p->b_nhn.alloc(bt * N * p->W));
   HIP_TRY(c, p->b_lvl.alloc(bt * (N + 1)));
-  HIP_TRY(c, p->b_ord.alloc(bt * N));
+  HIP_TRY(c, p->b_ord.alloc(bt * 2 * N));
   // marks start (and are always left) at kInf
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
+  if (std::getenv("SPF_WHATIF_PROF")) {
+    HIP_TRY(c, p->d_prof.alloc(16 * bt));
+    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 16 * bt * 8, c->stream));
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   *out = p.release();
   return SPF_OK;
@@ -799,8 +996,20 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     HIP_TRY(c, hipGetLastError());
     hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
-                       p->b_lvl.p, p->b_ord.p, d_out);
+                       p->b_lvl.p, p->b_ord.p, d_out, p->d_prof.p);
     HIP_TRY(c, hipGetLastError());
+  }
+  if (p->d_prof.p) {  // diagnostics: phase times of the workgroup teams
+    std::vector<unsigned long long> h(16ull * p->big_teams);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), p->d_prof.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    for (uint32_t t = 0; t < p->big_teams; ++t) {
+      const unsigned long long* r = &h[16ull * t];
+      if (!r[8]) continue;
+      std::fprintf(stderr, "whatif team %u |D|=%llu levels=%llu bfs=%llu seeds=%llu dial=%llu "
+                   "fallback=%llu digest=%llu (x10ns)\n", t, r[8], r[9], (r[1] - r[0]) / 1,
+                   r[2] - r[1], r[3] - r[2], r[4] - r[3], r[5] - r[4]);
+    }
   }
   if (d_base) {
     // the unfailed digest: nothing changed, hash = H
