@@ -186,16 +186,12 @@ class Ksp2AllPairs:
         self.plan.execute(self.d_pairs.data_ptr(), self.d_pool.data_ptr(), self.pool_words,
                           self.d_cnt.data_ptr(), stream.cuda_stream)
         if self.world > 1:
-            # variable-length pools: agree on the largest, then one gather each
-            used = self.d_cnt[0:1].clone()
-            dist.all_reduce(used, op=dist.ReduceOp.MAX)
-            m = int(used.item())
-            dst_p = [torch.empty_like(self.d_pairs) for _ in range(self.world)] if self.rank == 0 else None
-            dst_q = ([torch.empty(m, dtype=torch.int32, device=self.dev) for _ in range(self.world)]
-                     if self.rank == 0 else None)
-            dist.gather(self.d_pairs, dst_p, dst=0)
-            dist.gather(self.d_pool[:m].contiguous(), dst_q, dst=0)
-            self.gathered = m
+            # one exchange: every rank's pair headers and path pool to rank 0
+            from openr_amd.sharding import gather_padded
+
+            used = int(self.d_cnt[0].item())
+            gather_padded(self.d_pairs, self.d_pairs.numel())
+            gather_padded(self.d_pool, used)
 
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
@@ -281,10 +277,10 @@ class WhatIfAllLinks:
         import torch.distributed as dist
 
         self.plan.execute(self.d_out.data_ptr(), self.d_base.data_ptr(), stream.cuda_stream)
-        if self.world > 1:
-            dst = ([torch.empty_like(self.d_out) for _ in range(self.world)]
-                   if self.rank == 0 else None)
-            dist.gather(self.d_out, dst, dst=0)
+        if self.world > 1:  # one exchange: every rank's digests to rank 0
+            from openr_amd.sharding import gather_padded
+
+            gather_padded(self.d_out, self.d_out.numel())
 
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)

@@ -30,6 +30,8 @@
 // ============================================================================
 #include "engine_internal.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 
 using namespace spfi;
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(kKspThreads) void ksp2_kernel(
     KspGraph g, const uint32_t* __restrict__ Dsrc, const uint32_t* __restrict__ srcs,
     uint32_t n_src, uint32_t pitch, uint32_t lw, uint32_t chunks,
     spf_ksp2_pair* __restrict__ pairs, uint32_t* __restrict__ pool, uint64_t cap,
-    unsigned long long* __restrict__ counters) {
+    unsigned long long* __restrict__ counters, unsigned long long* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t N = g.N, bm_words = (N + 31) / 32;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -289,16 +291,20 @@ __global__ __launch_bounds__(kKspThreads) void ksp2_kernel(
       uint32_t prev = kInf;
       uint32_t depth = 0;
       uint32_t n1 = 0;
+      unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
       while (trace_one(g, Ds, nullptr, vis, stack, s, d, &depth) && depth) {
         prev = emit_path(g, stack, depth, pool, pc, used, cap, overflow, prev, ign);
         if (n1++ == 0) hdr.first[0] = prev;
       }
       hdr.n_paths[0] = n1;
+      unsigned long long t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+      unsigned long long t2 = t1;
       // ---- k = 2: runSpf(src, true, links of the k = 1 paths), trace ----
       if (n1) {
         ++k2_runs;
         wave_sync();
         wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch);
+        if (prof) t2 = __builtin_amdgcn_s_memtime();
         if (Dw[d] != kInf) {
           for (uint32_t j = lane; j < lw; j += 64) vis[j] = 0;
           wave_sync();
@@ -310,6 +316,13 @@ __global__ __launch_bounds__(kKspThreads) void ksp2_kernel(
           }
           hdr.n_paths[1] = n2;
         }
+      }
+      if (prof && lane == 0) {
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&prof[0], t1 - t0);
+        atomicAdd(&prof[1], t2 - t1);
+        atomicAdd(&prof[2], t3 - t2);
+        atomicAdd(&prof[3], 1ull);
       }
     }
     if (lane == 0) pairs[(size_t)i * N + d] = hdr;
@@ -329,6 +342,7 @@ struct spf_ksp2_plan {
   uint32_t n_src = 0, lw = 0;
   std::vector<uint32_t> srcs;
   DevBuf<uint32_t> d_srcs, d_D;
+  DevBuf<unsigned long long> d_prof;  // SPF_KSP2_PROF diagnostics
   size_t lds = 0;
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
@@ -369,6 +383,10 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   }
   HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
   HIP_TRY(c, p->d_D.alloc((size_t)n_src * c->pitch));
+  if (std::getenv("SPF_KSP2_PROF")) {
+    HIP_TRY(c, p->d_prof.alloc(4));
+    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 32, c->stream));
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   *out = p.release();
   return SPF_OK;
@@ -398,10 +416,19 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
   const uint32_t chunks = (c->N + kKspChunk - 1) / kKspChunk;
   hipLaunchKernelGGL(ksp2_kernel, dim3(p->n_src * chunks), dim3(kKspThreads), p->lds, s, g,
                      p->d_D.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, d_pairs, d_pool,
-                     pool_words, reinterpret_cast<unsigned long long*>(d_counters));
+                     pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p);
   HIP_TRY(c, hipGetLastError());
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
   c->solves += p->n_src;  // k = 2 runs are added by spf_ksp2_solve / the caller
+  return SPF_OK;
+}
+
+static spf_status ksp2_debug_phases(spf_ksp2_plan* p) {
+  if (!p || !p->d_prof.p) return SPF_OK;
+  unsigned long long h[4];
+  HIP_TRY(p->ctx, hipMemcpy(h, p->d_prof.p, sizeof h, hipMemcpyDeviceToHost));
+  std::fprintf(stderr, "ksp2 phases (clock sums over waves): k1 trace %llu, k2 spf %llu, "
+               "k2 trace %llu, pairs %llu\n", h[0], h[1], h[2], h[3]);
   return SPF_OK;
 }
 
@@ -431,6 +458,7 @@ spf_status spf_ksp2_timing(spf_ksp2_plan* p, double* spf_ms, double* ksp_ms, uin
   }
   if (spf_ms) *spf_ms = a;
   if (ksp_ms) *ksp_ms = b;
+  (void)ksp2_debug_phases(p);
   if (n) *n = cnt;
   p->timing_n = 0;
   return SPF_OK;

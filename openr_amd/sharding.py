@@ -9,9 +9,12 @@ Two ways a node's worth of SPF work spreads over ranks:
 * ``strong``: one LSDB, its sources interleaved over ranks (source i -> rank
   i mod world) so per-rank cost is balanced across switch roles.
 
-Neither puts a collective on the data path: results stay in each GPU's HBM.
-Only timings (MAX) and, for verification, 64-bit digests of per-source
-results (all_gather) cross ranks.
+For all-sources SPF neither puts a collective on the data path: results stay
+in each GPU's HBM; only timings (MAX) and, for verification, 64-bit digests of
+per-source results (all_gather) cross ranks.  KSP2 (sources dealt over ranks)
+and what-if batches (failed links dealt over ranks) end with one exchange:
+``gather_padded`` moves every rank's variable-length result buffer to rank 0
+(RCCL on GPU tensors, gloo on CPU tensors in the tests).
 """
 
 from __future__ import annotations
@@ -74,6 +77,34 @@ def gather_digests(local: Sequence[int], group=None) -> List[List[int]]:
     dist.all_gather(out, buf, group=group)
     return [[int(v) & ((1 << 64) - 1) for v in o[: int(s.item())].tolist()]
             for o, s in zip(out, sizes)]
+
+
+def gather_padded(t, length: int, dst: int = 0, group=None):
+    """Gather the first `length` elements of the 1-D tensor `t` from every
+    rank to rank `dst`: lengths are all_gathered, buffers padded to the
+    longest, one ``dist.gather``.  Returns the per-rank tensors (trimmed) on
+    `dst`, None elsewhere.  `t` must hold at least the longest length."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = torch.tensor([length], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=t.device) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    lens = [int(x.item()) for x in sizes]
+    cap = max(lens)
+    if t.numel() < cap:  # pad a short local buffer
+        pad = torch.zeros(cap, dtype=t.dtype, device=t.device)
+        pad[: t.numel()] = t
+        t = pad
+    send = t[:cap].contiguous()
+    out = [torch.empty(cap, dtype=t.dtype, device=t.device) for _ in range(world)] \
+        if rank == dst else None
+    dist.gather(send, out, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return [o[:m] for o, m in zip(out, lens)]
 
 
 def max_over_ranks(x: float, device=None) -> float:
