@@ -47,17 +47,6 @@ struct DevBuf {
   }
 };
 
-// Launch the per-source SSSP kernel (distances only) over `rows` sources
-// (device list rows_src), writing rows [rows][pitch] of D.
-spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
-                       const uint32_t* ign, uint32_t* D, hipStream_t s);
-// Single-source SSSP in global memory, one cooperative grid (any graph
-// size); scratch lives in the context.  dist = [N].
-spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
-                        hipStream_t s);
-// Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
-spf_status set_lds_limits(spf_ctx* c);
-
 }  // namespace spfi
 
 struct spf_ctx {
@@ -129,8 +118,11 @@ spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
 
 // Launch the per-source SSSP kernel (distances only) over `rows` sources
 // (device list rows_src), writing rows [rows][pitch] of D.
+// wt / ovl override the graph's metrics / drain bits (e.g. transposed
+// metrics and no drains for distances TO the rows' nodes).
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
-                       const uint32_t* ign, uint32_t* D, hipStream_t s);
+                       const uint32_t* ign, uint32_t* D, hipStream_t s,
+                       const uint32_t* wt = nullptr, const uint8_t* ovl = nullptr);
 // Single-source SSSP in global memory, one cooperative grid (any graph
 // size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,

@@ -40,6 +40,7 @@ namespace {
 
 constexpr int kKspThreads = 256;             // 4 waves, one pair each
 constexpr int kKspWaves = kKspThreads / 64;
+constexpr int kKspLdsMaxThreads = 1024;      // staged-graph kernel: up to 16 waves
 constexpr uint32_t kKspChunk = 64;          // destinations per workgroup
 constexpr uint32_t kPoolGrab = 2048;        // words a wave reserves at a time
 constexpr size_t kMaxLdsKsp = 160 * 1024;
@@ -76,14 +77,39 @@ __device__ __forceinline__ bool bit(const uint32_t* bm, uint32_t i) {
   return (bm[i >> 5] >> (i & 31)) & 1u;
 }
 
-struct KspGraph {
+// Graph accessors: the CSR in HBM (any size), or a 16-bit copy staged in
+// LDS by each workgroup (small graphs: every DFS step and relaxation then
+// costs LDS latency instead of L2 latency).
+struct GGraph {
   const uint32_t* row_ptr;
-  const uint32_t* col;
+  const uint32_t* col_;
   const uint32_t* wt;
-  const uint32_t* rev;
-  const uint32_t* link;
-  const uint8_t* ovl;
+  const uint32_t* rev_;
+  const uint32_t* link_;
+  const uint8_t* ovl_;
   uint32_t N;
+  __device__ uint32_t rp(uint32_t v) const { return row_ptr[v]; }
+  __device__ uint32_t col(uint32_t e) const { return col_[e]; }
+  __device__ uint32_t w(uint32_t e) const { return wt[e]; }
+  __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
+  __device__ uint32_t link(uint32_t e) const { return link_[e]; }
+  __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
+};
+
+struct LGraph {
+  const uint16_t* row_ptr;  // [N+1] (E < 65536)
+  const uint16_t* col_;
+  const uint16_t* wt;       // metrics < 65536
+  const uint16_t* rev_;
+  const uint16_t* link_;    // link ids < 65536
+  const uint8_t* ovl_;
+  uint32_t N;
+  __device__ uint32_t rp(uint32_t v) const { return row_ptr[v]; }
+  __device__ uint32_t col(uint32_t e) const { return col_[e]; }
+  __device__ uint32_t w(uint32_t e) const { return wt[e]; }
+  __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
+  __device__ uint32_t link(uint32_t e) const { return link_[e]; }
+  __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
 };
 
 // Per-wave bump allocation in the path pool.  Returns the word offset, or
@@ -116,9 +142,9 @@ __device__ uint32_t pool_alloc(PoolCursor& pc, uint32_t words, unsigned long lon
 // in-edges of D (tails expanded, links not in `ign` when given, links not in
 // `vis`).  On success the stack holds the edges dst-first and *depth their
 // count; every link tried is left in `vis`.
-__device__ bool trace_one(const KspGraph& g, const uint32_t* D, const uint32_t* ign,
-                          uint32_t* vis, uint32_t* stack, uint32_t src, uint32_t dst,
-                          uint32_t* depth) {
+template <class G, class ST>
+__device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, uint32_t* vis,
+                          ST* stack, uint32_t src, uint32_t dst, uint32_t* depth) {
   const uint32_t lane = __lane_id();
   uint32_t k = 0, v = dst;
   for (;;) {
@@ -128,16 +154,16 @@ __device__ bool trace_one(const KspGraph& g, const uint32_t* D, const uint32_t* 
     }
     const uint32_t dv = D[v];
     uint64_t best = ~0ull;
-    const uint32_t e_end = g.row_ptr[v + 1];
-    for (uint32_t e = g.row_ptr[v] + lane; e < e_end; e += 64) {
+    const uint32_t e_end = g.rp(v + 1);
+    for (uint32_t e = g.rp(v) + lane; e < e_end; e += 64) {
       // in-edge u -> v is the reverse of the out-edge v -> u
-      const uint32_t u = g.col[e];
-      const uint32_t r = g.rev[e];
-      const uint32_t l = g.link[e];
-      bool ok = !(g.ovl[u] && u != src) && !bit(vis, l) && !(ign && bit(ign, l));
+      const uint32_t u = g.col(e);
+      const uint32_t r = g.rev(e);
+      const uint32_t l = g.link(e);
+      bool ok = !(g.ovl(u) && u != src) && !bit(vis, l) && !(ign && bit(ign, l));
       if (ok) {
         const uint32_t du = D[u];
-        ok = du != kInf && du + g.wt[r] == dv;
+        ok = du != kInf && du + g.w(r) == dv;
         if (ok) best = min(best, ((uint64_t)du << 32) | r);
       }
     }
@@ -145,18 +171,18 @@ __device__ bool trace_one(const KspGraph& g, const uint32_t* D, const uint32_t* 
     if (best == ~0ull) {  // every pathLink of v tried: back up one level
       if (k == 0) return false;
       --k;
-      v = k == 0 ? dst : g.col[g.rev[stack[k - 1]]];
+      v = k == 0 ? dst : g.col(g.rev(stack[k - 1]));
       continue;
     }
     const uint32_t r = (uint32_t)best;
-    const uint32_t l = g.link[r];
+    const uint32_t l = g.link(r);
     if (lane == 0) {
       vis[l >> 5] |= 1u << (l & 31);
-      stack[k] = r;
+      stack[k] = (ST)r;
     }
     wave_sync();
     ++k;
-    v = g.col[g.rev[r]];  // tail of r
+    v = g.col(g.rev(r));  // tail of r
   }
 }
 
@@ -164,14 +190,14 @@ __device__ bool trace_one(const KspGraph& g, const uint32_t* D, const uint32_t* 
 // chains it after the record at `prev_at` (kInf: first of its list) and
 // returns its offset (kInf if the pool overflowed).  Marks the path's links
 // in `mark` when given.
-__device__ uint32_t emit_path(const KspGraph& g, const uint32_t* stack, uint32_t depth,
-                              uint32_t* pool, PoolCursor& pc, unsigned long long* used,
-                              uint64_t cap, uint32_t* overflow, uint32_t prev_at,
-                              uint32_t* mark) {
+template <class G, class ST>
+__device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint32_t* pool,
+                              PoolCursor& pc, unsigned long long* used, uint64_t cap,
+                              uint32_t* overflow, uint32_t prev_at, uint32_t* mark) {
   const uint32_t lane = __lane_id();
   const uint32_t at = pool_alloc(pc, depth + 2, used, cap, overflow);
   for (uint32_t j = lane; j < depth; j += 64) {
-    const uint32_t l = g.link[stack[depth - 1 - j]];  // src -> dst order
+    const uint32_t l = g.link(stack[depth - 1 - j]);  // src -> dst order
     if (mark) atomicOr(&mark[l >> 5], 1u << (l & 31));
     if (at != kInf) pool[(size_t)at + 2 + j] = l;
   }
@@ -184,10 +210,17 @@ __device__ uint32_t emit_path(const KspGraph& g, const uint32_t* stack, uint32_t
   return at;
 }
 
-// Wave-local SPF from src over links not in `ign`, pruned at D[dst].
-__device__ void wave_sssp(const KspGraph& g, uint32_t* D, uint16_t* q, uint32_t* bm,
-                          uint32_t bm_words, const uint32_t* ign, uint32_t src, uint32_t dst,
-                          uint32_t pitch) {
+// Wave-local SPF from src over links not in `ign`, A*-pruned towards dst:
+// H[v] = distance from v to dst in the graph with nothing ignored (a
+// consistent lower bound of the distance left once links are ignored), so a
+// node with D + H > D[dst] lies on no shortest path to dst and is not
+// expanded.  Every node with exact D + H <= the final D[dst] -- all the
+// nodes a trace to dst can inspect as tight tails -- ends exact (induction
+// along its shortest path, whose nodes all satisfy the same bound).
+template <class G>
+__device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, uint32_t bm_words,
+                          const uint32_t* ign, uint32_t src, uint32_t dst, uint32_t pitch,
+                          const uint32_t* H) {
   const uint32_t lane = __lane_id();
   for (uint32_t v = lane; v < pitch; v += 64) D[v] = kInf;
   for (uint32_t i = lane; i < bm_words; i += 64) bm[i] = 0;
@@ -201,16 +234,17 @@ __device__ void wave_sssp(const KspGraph& g, uint32_t* D, uint16_t* q, uint32_t*
   while (qlen) {
     for (uint32_t i = lane; i < qlen; i += 64) {
       const uint32_t u = q[i];
-      if (g.ovl[u] && u != src) continue;  // drained: recorded, not expanded
+      if (g.ovl(u) && u != src) continue;  // drained: recorded, not expanded
       const uint32_t du = D[u];
       const uint32_t bound = D[dst];
-      if (du >= bound) continue;
-      const uint32_t e_end = g.row_ptr[u + 1];
-      for (uint32_t e = g.row_ptr[u]; e < e_end; ++e) {
-        if (bit(ign, g.link[e])) continue;
-        const uint32_t nd = du + g.wt[e];
-        if (nd >= bound) continue;
-        const uint32_t v = g.col[e];
+      if ((uint64_t)du + H[u] > bound || u == dst) continue;
+      const uint32_t e_end = g.rp(u + 1);
+      for (uint32_t e = g.rp(u); e < e_end; ++e) {
+        if (bit(ign, g.link(e))) continue;
+        const uint32_t nd = du + g.w(e);
+        const uint32_t v = g.col(e);
+        const uint32_t hv = H[v];
+        if (hv == kInf || (uint64_t)nd + hv > bound) continue;
         if (nd < atomicMin(&D[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
       }
     }
@@ -237,52 +271,67 @@ __device__ void wave_sssp(const KspGraph& g, uint32_t* D, uint16_t* q, uint32_t*
   }
 }
 
-__global__ __launch_bounds__(kKspThreads) void ksp2_kernel(
-    KspGraph g, const uint32_t* __restrict__ Dsrc, const uint32_t* __restrict__ srcs,
-    uint32_t n_src, uint32_t pitch, uint32_t lw, uint32_t chunks,
-    spf_ksp2_pair* __restrict__ pairs, uint32_t* __restrict__ pool, uint64_t cap,
-    unsigned long long* __restrict__ counters, unsigned long long* __restrict__ prof) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t N = g.N, bm_words = (N + 31) / 32;
+struct KspArgs {
+  const uint32_t* Dsrc;   // [n_src][pitch] SPF rows of the sources
+  const uint32_t* Hrows;  // [N][pitch] distances TO each node (transposed SPF)
+  const uint32_t* srcs;
+  uint32_t n_src, pitch, lw, chunks;
+  spf_ksp2_pair* pairs;
+  uint32_t* pool;
+  uint64_t cap;
+  unsigned long long* counters;
+  unsigned long long* prof;
+};
+
+// Per-wave LDS: Dw [pitch] u32, stack/queue [pitch] ST, bitmap, ign, vis.
+template <class ST>
+__host__ __device__ constexpr size_t wave_lds_words(uint32_t pitch, uint32_t bm_words,
+                                                    uint32_t lw) {
+  return pitch + (pitch * sizeof(ST) + 3) / 4 + bm_words + 2ull * lw;
+}
+
+// The pair loop of one workgroup: the block owns one destination d (its
+// distances-to-d row H, the A* heuristic, staged in LDS) and a chunk of the
+// sources; waves pull sources from a shared counter and run, per pair,
+// k = 1 (trace on the source's SPF row copied into the wave's D), the k = 2
+// SPF (into the same D) and k = 2.
+template <class G, class ST>
+__device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint32_t* ctl,
+                           uint32_t* wave_base) {
+  const uint32_t N = g.N, bm_words = (N + 31) / 32, pitch = a.pitch, lw = a.lw;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t* Ds = reinterpret_cast<uint32_t*>(smem);  // [pitch] k = 1 distances
-  uint32_t* ctl = Ds + pitch;                        // [4] next destination
-  const size_t per_wave = 2ull * pitch + bm_words + 2ull * lw;
-  uint32_t* mine = ctl + 4 + w * per_wave;
-  uint32_t* Dw = mine;                                      // [pitch] k = 2 distances
-  uint32_t* stack = Dw + pitch;                             // [pitch] DFS stack ...
+  uint32_t* Dw = wave_base + (size_t)w * wave_lds_words<ST>(pitch, bm_words, lw);
+  ST* stack = reinterpret_cast<ST*>(Dw + pitch);           // DFS stack ...
   uint16_t* q = reinterpret_cast<uint16_t*>(stack);         // ... or SPF queue
-  uint32_t* bm = stack + pitch;                             // [bm_words]
+  uint32_t* bm = Dw + pitch + (pitch * sizeof(ST) + 3) / 4;
   uint32_t* ign = bm + bm_words;                            // [lw] k = 1 links
   uint32_t* vis = ign + lw;                                 // [lw] visited links
 
-  const uint32_t i = blockIdx.x / chunks;
-  const uint32_t c = blockIdx.x % chunks;
-  if (i >= n_src) return;
-  const uint32_t s = srcs[i];
-  {
-    const uint4* in = reinterpret_cast<const uint4*>(Dsrc + (size_t)i * pitch);
-    uint4* o = reinterpret_cast<uint4*>(Ds);
-    for (uint32_t t = tid; t < pitch / 4; t += kKspThreads) o[t] = in[t];
-    if (tid == 0) ctl[0] = c * kKspChunk;
-  }
-  __syncthreads();
-  const uint32_t d_end = min(N, (c + 1) * kKspChunk);
-  unsigned long long* used = counters;
-  uint32_t* overflow = reinterpret_cast<uint32_t*>(counters + 2);
+  const uint32_t d = blockIdx.x / a.chunks;
+  const uint32_t c = blockIdx.x % a.chunks;
+  const uint32_t i_end = min(a.n_src, (c + 1) * kKspChunk);
+  unsigned long long* used = a.counters;
+  uint32_t* overflow = reinterpret_cast<uint32_t*>(a.counters + 2);
   PoolCursor pc;
   uint32_t k2_runs = 0;
 
   for (;;) {
-    uint32_t d = 0;
-    if (lane == 0) d = atomicAdd(&ctl[0], 1u);
-    d = __shfl(d, 0, 64);
-    if (d >= d_end) break;
+    uint32_t i = 0;
+    if (lane == 0) i = atomicAdd(&ctl[0], 1u);
+    i = __shfl(i, 0, 64);
+    if (i >= i_end) break;
+    const uint32_t s = a.srcs[i];
+    const uint32_t* Drow = a.Dsrc + (size_t)i * pitch;
     spf_ksp2_pair hdr;
     hdr.first[0] = hdr.first[1] = kInf;
     hdr.n_paths[0] = hdr.n_paths[1] = 0;
-    if (d != s && Ds[d] != kInf) {
-      // ---- k = 1: trace in getSpfResult(src) ----
+    if (d != s && Drow[d] != kInf) {
+      // ---- k = 1: trace in getSpfResult(src) (its row copied to LDS) ----
+      {
+        const uint4* in = reinterpret_cast<const uint4*>(Drow);
+        uint4* o = reinterpret_cast<uint4*>(Dw);
+        for (uint32_t t = lane; t < pitch / 4; t += 64) o[t] = in[t];
+      }
       for (uint32_t j = lane; j < lw; j += 64) {
         vis[j] = 0;
         ign[j] = 0;
@@ -291,48 +340,103 @@ __global__ __launch_bounds__(kKspThreads) void ksp2_kernel(
       uint32_t prev = kInf;
       uint32_t depth = 0;
       uint32_t n1 = 0;
-      unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-      while (trace_one(g, Ds, nullptr, vis, stack, s, d, &depth) && depth) {
-        prev = emit_path(g, stack, depth, pool, pc, used, cap, overflow, prev, ign);
+      unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+      while (trace_one(g, Dw, nullptr, vis, stack, s, d, &depth) && depth) {
+        prev = emit_path(g, stack, depth, a.pool, pc, used, a.cap, overflow, prev, ign);
         if (n1++ == 0) hdr.first[0] = prev;
       }
       hdr.n_paths[0] = n1;
-      unsigned long long t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+      unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
       unsigned long long t2 = t1;
       // ---- k = 2: runSpf(src, true, links of the k = 1 paths), trace ----
       if (n1) {
         ++k2_runs;
         wave_sync();
-        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch);
-        if (prof) t2 = __builtin_amdgcn_s_memtime();
+        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch, H);
+        if (a.prof) t2 = __builtin_amdgcn_s_memtime();
         if (Dw[d] != kInf) {
           for (uint32_t j = lane; j < lw; j += 64) vis[j] = 0;
           wave_sync();
           prev = kInf;
           uint32_t n2 = 0;
           while (trace_one(g, Dw, ign, vis, stack, s, d, &depth) && depth) {
-            prev = emit_path(g, stack, depth, pool, pc, used, cap, overflow, prev, nullptr);
+            prev = emit_path(g, stack, depth, a.pool, pc, used, a.cap, overflow, prev, nullptr);
             if (n2++ == 0) hdr.first[1] = prev;
           }
           hdr.n_paths[1] = n2;
         }
       }
-      if (prof && lane == 0) {
+      if (a.prof && lane == 0) {
         const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-        atomicAdd(&prof[0], t1 - t0);
-        atomicAdd(&prof[1], t2 - t1);
-        atomicAdd(&prof[2], t3 - t2);
-        atomicAdd(&prof[3], 1ull);
+        atomicAdd(&a.prof[0], t1 - t0);
+        atomicAdd(&a.prof[1], t2 - t1);
+        atomicAdd(&a.prof[2], t3 - t2);
+        atomicAdd(&a.prof[3], 1ull);
       }
     }
-    if (lane == 0) pairs[(size_t)i * N + d] = hdr;
+    if (lane == 0) a.pairs[(size_t)i * N + d] = hdr;
   }
-  if (lane == 0 && k2_runs) atomicAdd(&counters[1], (unsigned long long)k2_runs);
+  if (lane == 0 && k2_runs) atomicAdd(&a.counters[1], (unsigned long long)k2_runs);
+}
+
+__device__ void stage_heuristic_row(const KspArgs& a, uint32_t* H, uint32_t* ctl) {
+  const uint32_t d = blockIdx.x / a.chunks, c = blockIdx.x % a.chunks;
+  const uint4* in = reinterpret_cast<const uint4*>(a.Hrows + (size_t)d * a.pitch);
+  uint4* o = reinterpret_cast<uint4*>(H);
+  for (uint32_t t = threadIdx.x; t < a.pitch / 4; t += blockDim.x) o[t] = in[t];
+  if (threadIdx.x == 0) ctl[0] = c * kKspChunk;
+}
+
+// Graph in HBM: 4 waves per workgroup, 32-bit DFS stack.
+__global__ __launch_bounds__(kKspThreads) void ksp2_kernel(GGraph g, KspArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* H = reinterpret_cast<uint32_t*>(smem);  // [pitch] distances to d
+  uint32_t* ctl = H + a.pitch;                      // [4] next source
+  stage_heuristic_row(a, H, ctl);
+  __syncthreads();
+  ksp2_block<GGraph, uint32_t>(g, a, H, ctl, ctl + 4);
+}
+
+// Graph staged in LDS as 16-bit arrays; waves per workgroup = blockDim / 64.
+__global__ __launch_bounds__(kKspLdsMaxThreads) void ksp2_lds_kernel(GGraph gg, KspArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t N = gg.N;
+  uint32_t* H = reinterpret_cast<uint32_t*>(smem);  // [pitch] distances to d
+  uint32_t* ctl = H + a.pitch;                      // [4] next source
+  const uint32_t E = gg.row_ptr[N];
+  const uint32_t rp_words = (N + 2) / 2, e_words = (E + 1) / 2;
+  uint16_t* rp = reinterpret_cast<uint16_t*>(ctl + 4);
+  uint16_t* col = rp + 2 * rp_words;
+  uint16_t* wt = col + 2 * e_words;
+  uint16_t* rev = wt + 2 * e_words;
+  uint16_t* link = rev + 2 * e_words;
+  uint8_t* ovl = reinterpret_cast<uint8_t*>(link + 2 * e_words);
+  uint32_t* wave_base = reinterpret_cast<uint32_t*>(ovl + ((N + 3) & ~3u));
+  for (uint32_t v = threadIdx.x; v <= N; v += blockDim.x) rp[v] = (uint16_t)gg.row_ptr[v];
+  for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
+    col[e] = (uint16_t)gg.col_[e];
+    wt[e] = (uint16_t)gg.wt[e];
+    rev[e] = (uint16_t)gg.rev_[e];
+    link[e] = (uint16_t)gg.link_[e];
+  }
+  for (uint32_t v = threadIdx.x; v < N; v += blockDim.x) ovl[v] = gg.ovl_[v];
+  stage_heuristic_row(a, H, ctl);
+  __syncthreads();
+  const LGraph g{rp, col, wt, rev, link, ovl, N};
+  ksp2_block<LGraph, uint16_t>(g, a, H, ctl, wave_base);
 }
 
 size_t ksp2_lds_bytes(uint32_t N, uint32_t pitch, uint32_t lw) {
   const size_t bm_words = (N + 31) / 32;
-  return 4ull * (pitch + 4 + kKspWaves * (2ull * pitch + bm_words + 2ull * lw));
+  return 4ull * (pitch + 4 + kKspWaves * wave_lds_words<uint32_t>(pitch, bm_words, lw));
+}
+
+// LDS bytes of the staged-graph kernel with `waves` waves per workgroup
+size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw,
+                            uint32_t waves) {
+  const size_t bm_words = (N + 31) / 32;
+  const size_t graph = 4ull * ((N + 2) / 2 + 4ull * ((E + 1) / 2)) + ((N + 3) & ~3u);
+  return 4ull * (pitch + 4) + graph + 4ull * waves * wave_lds_words<uint16_t>(pitch, bm_words, lw);
 }
 
 }  // namespace
@@ -341,9 +445,11 @@ struct spf_ksp2_plan {
   spf_ctx* ctx = nullptr;
   uint32_t n_src = 0, lw = 0;
   std::vector<uint32_t> srcs;
-  DevBuf<uint32_t> d_srcs, d_D;
+  DevBuf<uint32_t> d_srcs, d_D, d_H, d_all, d_wt_rev;
+  DevBuf<uint8_t> d_no_drain;
   DevBuf<unsigned long long> d_prof;  // SPF_KSP2_PROF diagnostics
   size_t lds = 0;
+  uint32_t lds_waves = 0;  // > 0: the staged-graph kernel with this many waves
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
   ~spf_ksp2_plan() {
@@ -370,12 +476,23 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   for (uint32_t i = 0; i < n_src; ++i)
     if (srcs[i] >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
   p->lw = c->max_link / 32 + 1;
-  p->lds = ksp2_lds_bytes(c->N, c->pitch, p->lw);
+  // graph staged in LDS when its 16-bit copy fits beside >= 2 waves
+  if (c->E < 65536 && c->max_metric < 65536 && c->max_link < 65536 && !std::getenv("SPF_KSP2_HBM")) {
+    for (uint32_t w = kKspLdsMaxThreads / 64; w >= 2; --w)
+      if (ksp2_lds_graph_bytes(c->N, c->E, c->pitch, p->lw, w) <= kMaxLdsKsp) {
+        p->lds_waves = w;
+        p->lds = ksp2_lds_graph_bytes(c->N, c->E, c->pitch, p->lw, w);
+        break;
+      }
+  }
+  if (!p->lds_waves) p->lds = ksp2_lds_bytes(c->N, c->pitch, p->lw);
   if (p->lds > kMaxLdsKsp)
     return fail(c, SPF_E_UNSUPPORTED, "KSP2 working set of %zu B exceeds the LDS (%u nodes)",
                 p->lds, c->N);
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
+  HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_lds_kernel,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
   {
     const spf_status st = set_lds_limits(c);
@@ -383,6 +500,17 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   }
   HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
   HIP_TRY(c, p->d_D.alloc((size_t)n_src * c->pitch));
+  {  // distances TO every node: SPF over transposed metrics, no drains (a
+     // lower bound of every drained / link-ignored distance)
+    std::vector<uint32_t> all(c->N), wr(c->E);
+    for (uint32_t v = 0; v < c->N; ++v) all[v] = v;
+    for (uint32_t e = 0; e < c->E; ++e) wr[e] = c->wt[c->rev[e]];
+    std::vector<uint8_t> z(c->N, 0);
+    HIP_TRY(c, p->d_all.upload(all.data(), c->N, c->stream));
+    HIP_TRY(c, p->d_wt_rev.upload(wr.data(), c->E, c->stream));
+    HIP_TRY(c, p->d_no_drain.upload(z.data(), c->N, c->stream));
+    HIP_TRY(c, p->d_H.alloc((size_t)c->N * c->pitch));
+  }
   if (std::getenv("SPF_KSP2_PROF")) {
     HIP_TRY(c, p->d_prof.alloc(4));
     HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 32, c->stream));
@@ -411,12 +539,20 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
   HIP_TRY(c, hipMemsetAsync(d_counters, 0, 4 * sizeof(uint64_t), s));
   spf_status st = launch_sssp(c, p->d_srcs.p, p->n_src, false, nullptr, p->d_D.p, s);
   if (st != SPF_OK) return st;
+  st = launch_sssp(c, p->d_all.p, c->N, false, nullptr, p->d_H.p, s, p->d_wt_rev.p,
+                   p->d_no_drain.p);
+  if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
-  KspGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p, c->N};
-  const uint32_t chunks = (c->N + kKspChunk - 1) / kKspChunk;
-  hipLaunchKernelGGL(ksp2_kernel, dim3(p->n_src * chunks), dim3(kKspThreads), p->lds, s, g,
-                     p->d_D.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, d_pairs, d_pool,
-                     pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p);
+  GGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p, c->N};
+  // blocks: (destination, chunk of kKspChunk sources)
+  const uint32_t chunks = (p->n_src + kKspChunk - 1) / kKspChunk;
+  KspArgs a{p->d_D.p, p->d_H.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, d_pairs,
+            d_pool, pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p};
+  if (p->lds_waves)
+    hipLaunchKernelGGL(ksp2_lds_kernel, dim3(c->N * chunks), dim3(64 * p->lds_waves), p->lds, s,
+                       g, a);
+  else
+    hipLaunchKernelGGL(ksp2_kernel, dim3(c->N * chunks), dim3(kKspThreads), p->lds, s, g, a);
   HIP_TRY(c, hipGetLastError());
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
   c->solves += p->n_src;  // k = 2 runs are added by spf_ksp2_solve / the caller

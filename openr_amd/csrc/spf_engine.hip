@@ -929,7 +929,10 @@ namespace spfi {
 
 // Launch the SSSP kernel over `rows` closure rows (device list rows_src).
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
-                       const uint32_t* ign, uint32_t* D, hipStream_t s) {
+                       const uint32_t* ign, uint32_t* D, hipStream_t s, const uint32_t* wt,
+                       const uint8_t* ovl) {
+  if (!wt) wt = c->d_wt.p;
+  if (!ovl) ovl = c->d_ovl.p;
   const uint32_t N = c->N, pitch = c->pitch, bm_words = (N + 31) / 32;
   const bool q16 = N <= 65535;
   const size_t lds = sssp_lds_bytes(N, pitch, c->big_nodes, q16);
@@ -937,7 +940,7 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
   const dim3 g(rows), b(kSsspThreads);
 #define SSSP_LAUNCH(QT, U)                                                                \
   hipLaunchKernelGGL((sssp_kernel<QT, U>), g, b, lds, s, c->d_row_ptr.p, c->d_col.p,       \
-                     c->d_wt.p, c->d_ovl.p, c->d_link.p, ign, rows_src, N, pitch, bm_words, \
+                     wt, ovl, c->d_link.p, ign, rows_src, N, pitch, bm_words,             \
                      c->big_nodes, D)
   if (q16) {
     if (unit) SSSP_LAUNCH(uint16_t, true);
