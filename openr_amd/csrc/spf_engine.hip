@@ -322,6 +322,8 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t nl = min(L, 254u);
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
+      // most slices have no new node at a given level: one ballot skips them
+      if (__ballot(nv[i] != 0ull) == 0ull) continue;
       // the wave-uniform mask lives in SGPRs: row addressing is scalar work
       const uint64_t wm = wave_or64(nv[i]);
       uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
