@@ -38,6 +38,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "engine_internal.h"
@@ -439,6 +440,46 @@ constexpr int kEcmpUnroll = 4;         // neighbour rows in flight per wave
 constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
 constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
 
+// 16 byte-compare ballots of a 16-byte lane-interleaved row slice against
+// the packed targets: ballot q covers destinations q*64 .. q*64+63; lanes
+// 2q / 2q+1 of the result hold its low / high half (one coalesced store
+// later).  The halves go into lanes with v_writelane, eight ballots per asm
+// block behind one s_nop that covers the VALU-writes-SGPR -> v_writelane
+// hazard.
+template <int Q0>
+__device__ __forceinline__ uint32_t ballots8(uint32_t word, const uint4& a, const uint4& t) {
+  uint32_t m[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int q = Q0 + k, sh = (q & 3) * 8;
+    const uint64_t b = __ballot(((((&a.x)[q >> 2]) >> sh) & 0xFFu) == ((((&t.x)[q >> 2]) >> sh) & 0xFFu));
+    m[2 * k] = (uint32_t)b;
+    m[2 * k + 1] = (uint32_t)(b >> 32);
+  }
+  asm volatile(
+      "s_nop 4\n\t"
+      "v_writelane_b32 %0, %1, %17\n\tv_writelane_b32 %0, %2, %18\n\t"
+      "v_writelane_b32 %0, %3, %19\n\tv_writelane_b32 %0, %4, %20\n\t"
+      "v_writelane_b32 %0, %5, %21\n\tv_writelane_b32 %0, %6, %22\n\t"
+      "v_writelane_b32 %0, %7, %23\n\tv_writelane_b32 %0, %8, %24\n\t"
+      "v_writelane_b32 %0, %9, %25\n\tv_writelane_b32 %0, %10, %26\n\t"
+      "v_writelane_b32 %0, %11, %27\n\tv_writelane_b32 %0, %12, %28\n\t"
+      "v_writelane_b32 %0, %13, %29\n\tv_writelane_b32 %0, %14, %30\n\t"
+      "v_writelane_b32 %0, %15, %31\n\tv_writelane_b32 %0, %16, %32"
+      : "+v"(word)
+      : "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), "s"(m[7]),
+        "s"(m[8]), "s"(m[9]), "s"(m[10]), "s"(m[11]), "s"(m[12]), "s"(m[13]), "s"(m[14]),
+        "s"(m[15]), "i"(2 * Q0), "i"(2 * Q0 + 1), "i"(2 * Q0 + 2), "i"(2 * Q0 + 3),
+        "i"(2 * Q0 + 4), "i"(2 * Q0 + 5), "i"(2 * Q0 + 6), "i"(2 * Q0 + 7), "i"(2 * Q0 + 8),
+        "i"(2 * Q0 + 9), "i"(2 * Q0 + 10), "i"(2 * Q0 + 11), "i"(2 * Q0 + 12), "i"(2 * Q0 + 13),
+        "i"(2 * Q0 + 14), "i"(2 * Q0 + 15));
+  return word;
+}
+
+__device__ __forceinline__ uint32_t ballots16(const uint4& a, const uint4& t) {
+  return ballots8<8>(ballots8<0>(0u, a, t), a, t);
+}
+
 // Lane t (< 32) of the wave keeps dword t of the 16 ballots (q = t / 2).
 __device__ __forceinline__ uint32_t put_mask(uint32_t out, uint64_t m, int q, uint32_t lane) {
   const uint32_t pick = (lane & 1u) ? (uint32_t)(m >> 32) : (uint32_t)m;
@@ -476,29 +517,28 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
   uint32_t* out_base = nh + nh_off[i] + cbase / 32 + lane;
   const bool store_lane = lane < 32 && cbase / 32 + lane < wpm;
 
-  // source distances of this lane's 16 destinations (cbase + q*64 + lane)
-  uint32_t b[16];
-  uint32_t tgt[16];  // NARROW: the u8 value a neighbour must hold, 0x100 = none
+  // NARROW: the u8 value a neighbour must hold at this lane's 16
+  // destinations (cbase + q*64 + lane), packed four per dword; 0xFE = none
+  // (never held by a non-drained neighbour where the source row is not
+  // saturated: d_x(s) = w(x, s) < 0xFE, and a node s cannot reach no
+  // neighbour reaches either)
+  uint4 tg = make_uint4(0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu);
   bool exact = !NARROW;
-  if (live) {
-    if (NARROW) {
-      const uint4 raw = *reinterpret_cast<const uint4*>(Dn + (size_t)srow * npitch + cbase + lane * 16);
-      bool sat = false;
+  if (live && NARROW) {
+    const uint4 raw = *reinterpret_cast<const uint4*>(Dn + (size_t)srow * npitch + cbase + lane * 16);
+    bool sat = false;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t x = ((&raw.x)[q >> 2] >> ((q & 3) * 8)) & 0xFFu;
+    for (int w = 0; w < 4; ++w) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int bq = 0; bq < 4; ++bq) {
+        const uint32_t x = ((&raw.x)[w] >> (8 * bq)) & 0xFFu;
         sat |= x == 0xFEu;
-        tgt[q] = (x == 0u || x >= 0xFEu) ? 0x100u : x - 1u;  // unit metric: d_x = d_s - 1
+        o |= ((x == 0u || x >= 0xFEu) ? 0xFEu : x - 1u) << (8 * bq);  // d_x = d_s - 1
       }
-      exact = __ballot(sat) != 0;
+      (&tg.x)[w] = o;
     }
-    if (exact) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t v = cbase + q * 64 + lane;
-        b[q] = v < N ? D[(size_t)srow * pitch + v] : kInf;
-      }
-    }
+    exact = __ballot(sat) != 0;
   }
 
   for (uint32_t t0 = 0; t0 < k; t0 += kNbTile) {
@@ -529,12 +569,7 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
 #pragma unroll
         for (int u = 0; u < kEcmpUnroll; ++u) {
           if (j0 + u >= tk) break;
-          uint32_t word = 0;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const uint32_t a = ((&raw[u].x)[q >> 2] >> ((q & 3) * 8)) & 0xFFu;
-            word = put_mask(word, __ballot(a == tgt[q]), q, lane);
-          }
+          const uint32_t word = ballots16(raw[u], tg);
           if (store_lane) out[(size_t)(j0 + u) * wpm] = word;
         }
       }
@@ -543,11 +578,12 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
         const uint32_t rj = s_row[j], wj = s_w[j];
         uint32_t word = 0;
         if (rj != kInf) {
-          uint32_t a[16];
+          uint32_t a[16], b[16];
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const uint32_t v = cbase + q * 64 + lane;
             a[q] = v < N ? D[(size_t)rj * pitch + v] : kInf;
+            b[q] = v < N ? D[(size_t)srow * pitch + v] : kInf;
           }
 #pragma unroll
           for (int q = 0; q < 16; ++q)
