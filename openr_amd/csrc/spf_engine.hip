@@ -38,7 +38,6 @@
 #include <memory>
 #include <numeric>
 #include <string>
-#include <utility>
 #include <vector>
 
 #include "engine_internal.h"
@@ -230,7 +229,7 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
 //   * distances are written per level as predicated stores over the sources
 //     that have new nodes in the wave; one store covers 64 consecutive nodes
 //     of one source row.  The u8 narrow copy for the next-hop pass saturates at
-//     254 and is stored lane-interleaved (narrow_pos).
+//     254.
 constexpr int kMsThreads = 1024;
 constexpr uint32_t kMsBatch = 64;
 constexpr int kMsMaxOwn = 16;
@@ -238,14 +237,8 @@ constexpr uint32_t kMsMaxNodes = kMsThreads * kMsMaxOwn;  // 16384 (F: 128 KiB o
 constexpr int kMsUnroll = 8;
 constexpr uint32_t kSliceW = 64;  // nodes per sliced-ELL slice (= wave width)
 
-// Narrow (u8) distance rows: npitch bytes (a multiple of 1024).  Within a
-// 1024-node chunk, node q*64 + l (q = 0..15, l = 0..63) is byte l*16 + q, so a
-// 16-byte load by lane l returns nodes {q*64 + l} of the chunk: byte q of every
-// lane forms one 64-node ballot, i.e. one u64 word of a destination bitmap.
-__host__ __device__ __forceinline__ uint32_t narrow_pos(uint32_t v) {
-  return (v & ~1023u) | ((v & 63u) << 4) | ((v >> 6) & 15u);
-}
-
+// Narrow (u8) distance rows: npitch bytes (a multiple of 1024), node v at
+// byte v -- a level's stores are 64 consecutive bytes per (source, slice).
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
   uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
 #pragma unroll
@@ -334,7 +327,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
         if ((nv[i] >> s) & 1ull) {
           const uint32_t v = tid + i * kMsThreads;
           D[(size_t)(row0 + s) * pitch + v] = L;
-          Dn[(size_t)(row0 + s) * npitch + narrow_pos(v)] = (uint8_t)nl;
+          Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
         }
       }
     }
@@ -405,7 +398,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const uint32_t v = tid + i * kMsThreads;
       if (v < N && !((vis[i] >> s) & 1ull)) {
         drow[v] = kInf;
-        nrow[narrow_pos(v)] = 0xFF;
+        nrow[v] = 0xFF;
       }
     }
   }
@@ -414,7 +407,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
     for (uint32_t v = N + tid; v < npitch; v += kMsThreads) {
       if (v < pitch) drow[v] = kInf;
-      nrow[narrow_pos(v)] = 0xFF;
+      nrow[v] = 0xFF;
     }
   }
   MS_STAMP();
@@ -427,12 +420,14 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 // ---------------------------------------------------------------------------
 // Output: per source, one destination bitmap per distinct up neighbour x
 // (ascending id): bit v of bitmap j <=> neighbour j is in nh_s(v).  Each wave
-// owns a 1024-destination chunk; for neighbour x it forms 16 ballots -- one
-// per 64 destinations -- and stores them as 32 consecutive u32 words.
-//   NARROW: distances from the lane-interleaved u8 copy (one 16-byte load per
-//           lane per neighbour, target = d_s(v) - 1 precomputed); a wave whose
-//           source row holds a saturated entry (>= 254) decides on the exact
-//           u32 rows instead.
+// owns a 1024-destination chunk and stores, per neighbour, 32 consecutive u32
+// words.
+//   NARROW: distances from the u8 copy: lane l loads destinations
+//           cbase + 16l .. +15 of the neighbour's row (16 bytes), compares
+//           them with the precomputed targets d_s(v) - 1 into a 16-bit mask,
+//           and even lanes merge their odd neighbour's half into one word; a
+//           wave whose source row holds a saturated entry (>= 254) decides on
+//           the exact u32 rows instead.
 //   exact:  u32 rows, one coalesced dword load per 64 destinations.
 
 constexpr uint32_t kNbTile = 256;      // neighbours staged in LDS per tile
@@ -440,44 +435,19 @@ constexpr int kEcmpUnroll = 4;         // neighbour rows in flight per wave
 constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
 constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
 
-// 16 byte-compare ballots of a 16-byte lane-interleaved row slice against
-// the packed targets: ballot q covers destinations q*64 .. q*64+63; lanes
-// 2q / 2q+1 of the result hold its low / high half (one coalesced store
-// later).  The halves go into lanes with v_writelane, eight ballots per asm
-// block behind one s_nop that covers the VALU-writes-SGPR -> v_writelane
-// hazard.
-template <int Q0>
-__device__ __forceinline__ uint32_t ballots8(uint32_t word, const uint4& a, const uint4& t) {
-  uint32_t m[16];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int q = Q0 + k, sh = (q & 3) * 8;
-    const uint64_t b = __ballot(((((&a.x)[q >> 2]) >> sh) & 0xFFu) == ((((&t.x)[q >> 2]) >> sh) & 0xFFu));
-    m[2 * k] = (uint32_t)b;
-    m[2 * k + 1] = (uint32_t)(b >> 32);
-  }
-  asm volatile(
-      "s_nop 4\n\t"
-      "v_writelane_b32 %0, %1, %17\n\tv_writelane_b32 %0, %2, %18\n\t"
-      "v_writelane_b32 %0, %3, %19\n\tv_writelane_b32 %0, %4, %20\n\t"
-      "v_writelane_b32 %0, %5, %21\n\tv_writelane_b32 %0, %6, %22\n\t"
-      "v_writelane_b32 %0, %7, %23\n\tv_writelane_b32 %0, %8, %24\n\t"
-      "v_writelane_b32 %0, %9, %25\n\tv_writelane_b32 %0, %10, %26\n\t"
-      "v_writelane_b32 %0, %11, %27\n\tv_writelane_b32 %0, %12, %28\n\t"
-      "v_writelane_b32 %0, %13, %29\n\tv_writelane_b32 %0, %14, %30\n\t"
-      "v_writelane_b32 %0, %15, %31\n\tv_writelane_b32 %0, %16, %32"
-      : "+v"(word)
-      : "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), "s"(m[7]),
-        "s"(m[8]), "s"(m[9]), "s"(m[10]), "s"(m[11]), "s"(m[12]), "s"(m[13]), "s"(m[14]),
-        "s"(m[15]), "i"(2 * Q0), "i"(2 * Q0 + 1), "i"(2 * Q0 + 2), "i"(2 * Q0 + 3),
-        "i"(2 * Q0 + 4), "i"(2 * Q0 + 5), "i"(2 * Q0 + 6), "i"(2 * Q0 + 7), "i"(2 * Q0 + 8),
-        "i"(2 * Q0 + 9), "i"(2 * Q0 + 10), "i"(2 * Q0 + 11), "i"(2 * Q0 + 12), "i"(2 * Q0 + 13),
-        "i"(2 * Q0 + 14), "i"(2 * Q0 + 15));
-  return word;
+// Byte-equality mask of a 16-byte row slice against the packed targets: bit k
+// = (byte k of a == byte k of t), i.e. destination cbase + 16*lane + k.  Exact
+// zero-byte test per dword, then the four byte flags gathered into a nibble
+// with one multiply (partial products land on distinct bits: no carries).
+__device__ __forceinline__ uint32_t eq_nibble(uint32_t a, uint32_t t) {
+  const uint32_t x = a ^ t;
+  const uint32_t y = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+  return ((y >> 7) * 0x00204081u) >> 21 & 0xFu;
 }
 
-__device__ __forceinline__ uint32_t ballots16(const uint4& a, const uint4& t) {
-  return ballots8<8>(ballots8<0>(0u, a, t), a, t);
+__device__ __forceinline__ uint32_t eq_mask16(const uint4& a, const uint4& t) {
+  return eq_nibble(a.x, t.x) | eq_nibble(a.y, t.y) << 4 | eq_nibble(a.z, t.z) << 8 |
+         eq_nibble(a.w, t.w) << 12;
 }
 
 // Lane t (< 32) of the wave keeps dword t of the 16 ballots (q = t / 2).
@@ -516,9 +486,12 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
   const uint32_t wpm = pitch / 32;  // u32 words per bitmap
   uint32_t* out_base = nh + nh_off[i] + cbase / 32 + lane;
   const bool store_lane = lane < 32 && cbase / 32 + lane < wpm;
+  // fast path: even lane 2t stores word t
+  uint32_t* out_base2 = nh + nh_off[i] + cbase / 32 + lane / 2;
+  const bool store_lane2 = (lane & 1u) == 0 && cbase / 32 + lane / 2 < wpm;
 
   // NARROW: the u8 value a neighbour must hold at this lane's 16
-  // destinations (cbase + q*64 + lane), packed four per dword; 0xFE = none
+  // destinations (cbase + 16*lane + k), packed four per dword; 0xFE = none
   // (never held by a non-drained neighbour where the source row is not
   // saturated: d_x(s) = w(x, s) < 0xFE, and a node s cannot reach no
   // neighbour reaches either)
@@ -553,6 +526,7 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     __syncthreads();
     if (!live) continue;
     uint32_t* out = out_base + (size_t)t0 * wpm;
+    uint32_t* out2 = out_base2 + (size_t)t0 * wpm;
     if (!exact) {
       // fast path: kEcmpUnroll neighbour rows in flight; a drained neighbour's
       // row reads as "unreachable" (0xFF never equals a target) and its single
@@ -569,8 +543,9 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
 #pragma unroll
         for (int u = 0; u < kEcmpUnroll; ++u) {
           if (j0 + u >= tk) break;
-          const uint32_t word = ballots16(raw[u], tg);
-          if (store_lane) out[(size_t)(j0 + u) * wpm] = word;
+          const uint32_t m = eq_mask16(raw[u], tg);
+          const uint32_t word = m | (uint32_t)__shfl_xor((int)m, 1, 64) << 16;
+          if (store_lane2) out2[(size_t)(j0 + u) * wpm] = word;
         }
       }
     } else {
