@@ -89,6 +89,8 @@ struct spf_plan {
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
   spfi::DevBuf<uint8_t> d_Dn;
   spfi::DevBuf<uint64_t> d_nh_off;
+  spfi::DevBuf<uint32_t> d_nb_row, d_nb_row_off, d_nb_drained;  // next-hop pass inputs
+  uint32_t dead = 0;  // nb_row value of a drained neighbour
   size_t lds_bytes = 0;
   bool q16 = true;
   // optional per-kernel timing: 3 events per execute (before SSSP, between,

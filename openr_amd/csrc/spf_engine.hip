@@ -238,7 +238,10 @@ constexpr int kMsUnroll = 8;
 constexpr uint32_t kSliceW = 64;  // nodes per sliced-ELL slice (= wave width)
 
 // Narrow (u8) distance rows: npitch bytes (a multiple of 1024), node v at
-// byte v -- a level's stores are 64 consecutive bytes per (source, slice).
+// byte v -- a level's stores are 64 consecutive bytes per (source, slice),
+// lane-ordered like the u32 ones (any permutation of the lanes' addresses
+// costs the store path measurably).
+
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
   uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
 #pragma unroll
@@ -322,10 +325,10 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const uint64_t wm = wave_or64(nv[i]);
       uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
       uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
+      const uint32_t v = tid + i * kMsThreads;
       for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
         const uint32_t s = __ffsll((unsigned long long)m) - 1;
         if ((nv[i] >> s) & 1ull) {
-          const uint32_t v = tid + i * kMsThreads;
           D[(size_t)(row0 + s) * pitch + v] = L;
           Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
         }
@@ -430,24 +433,29 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 //           the exact u32 rows instead.
 //   exact:  u32 rows, one coalesced dword load per 64 destinations.
 
-constexpr uint32_t kNbTile = 256;      // neighbours staged in LDS per tile
-constexpr int kEcmpUnroll = 4;         // neighbour rows in flight per wave
+constexpr int kEcmpUnroll = 4;         // neighbour rows per group (two groups in flight)
 constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
 constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
 
-// Byte-equality mask of a 16-byte row slice against the packed targets: bit k
-// = (byte k of a == byte k of t), i.e. destination cbase + 16*lane + k.  Exact
-// zero-byte test per dword, then the four byte flags gathered into a nibble
-// with one multiply (partial products land on distinct bits: no carries).
-__device__ __forceinline__ uint32_t eq_nibble(uint32_t a, uint32_t t) {
-  const uint32_t x = a ^ t;
-  const uint32_t y = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-  return ((y >> 7) * 0x00204081u) >> 21 & 0xFu;
+// Zero-byte flags of x at bit 7 of each byte (exact: no carries cross bytes).
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
 
+// Byte-equality mask of a lane's 16-byte narrow slice against its packed
+// targets: bit n = destination cbase + 16*lane + n.  Dword k byte b is
+// destination 4k + b; shifting dword k's zero-byte flags right by 3 - k puts
+// it at bit 8b + 4 + k (high nibbles), a shift-or and a byte permute pack the
+// nibbles to bit 4b + k, and two delta swaps transpose that 4x4 bit matrix
+// to bit 4k + b.
 __device__ __forceinline__ uint32_t eq_mask16(const uint4& a, const uint4& t) {
-  return eq_nibble(a.x, t.x) | eq_nibble(a.y, t.y) << 4 | eq_nibble(a.z, t.z) << 8 |
-         eq_nibble(a.w, t.w) << 12;
+  const uint32_t z = (zero_bytes(a.x ^ t.x) >> 3) | (zero_bytes(a.y ^ t.y) >> 2) |
+                     (zero_bytes(a.z ^ t.z) >> 1) | zero_bytes(a.w ^ t.w);
+  uint32_t x = __builtin_amdgcn_perm(0u, z | (z << 4), 0x0c0c0301u);
+  uint32_t d = (x ^ (x >> 3)) & 0x0A0Au;
+  x ^= d ^ (d << 3);
+  d = (x ^ (x >> 6)) & 0x00CCu;
+  return x ^ d ^ (d << 6);
 }
 
 // Lane t (< 32) of the wave keeps dword t of the 16 ballots (q = t / 2).
@@ -456,18 +464,24 @@ __device__ __forceinline__ uint32_t put_mask(uint32_t out, uint64_t m, int q, ui
   return (lane >> 1) == (uint32_t)q ? pick : out;
 }
 
+// nb_row[nb_row_off[i] + j]: byte offset in Dn (row * npitch) of the narrow
+// row of the request's source i's neighbour j (ascending id) -- the D row
+// itself for plans without narrow rows -- or `dead` if it is drained: the
+// offset of an all-0xFF row after the plan's narrow rows (kInf without them).
+// Each source's list starts 16-byte aligned and is padded with `dead` to
+// roundup(k, 8) + 8 entries (the pipelined loads run one group ahead).  nb_drained[i] counts the drained neighbours.
+// Every per-neighbour quantity is wave-uniform and read with scalar loads:
+// no LDS staging, no workgroup barriers -- a wave is independent.
 template <bool NARROW>
 __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     const uint8_t* __restrict__ Dn, uint32_t npitch, const uint32_t* __restrict__ D,
     uint32_t pitch, uint32_t N, const uint32_t* __restrict__ req_src,
     const uint32_t* __restrict__ row_of, const uint32_t* __restrict__ nb_ptr,
     const uint32_t* __restrict__ nb_id, const uint32_t* __restrict__ nb_w,
-    const uint8_t* __restrict__ ovl, uint32_t hop, const uint64_t* __restrict__ nh_off,
-    uint32_t* __restrict__ nh, uint32_t chunks, uint32_t n_src) {
-  __shared__ uint32_t s_row[kNbTile];  // row of neighbour, or kInf if drained
-  __shared__ uint32_t s_w[kNbTile];
-  __shared__ uint32_t s_id[kNbTile];
-
+    const uint32_t* __restrict__ nb_row, const uint32_t* __restrict__ nb_row_off,
+    const uint32_t* __restrict__ nb_drained, uint32_t dead, uint32_t hop,
+    const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh, uint32_t chunks,
+    uint32_t n_src) {
   // Sources are dealt round-robin over the 8 XCD groups (block b runs on the
   // XCD group b % 8): every XCD gets the same mix of switch roles (work per
   // source ~ its neighbour count), and inside a group the sources come in id
@@ -478,104 +492,112 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
   if (i >= n_src) return;
   const uint32_t s = req_src[i];
   const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
-  if (k == 0) return;  // isolated source: no bitmaps at all
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t cbase = (c * kEcmpWaves + (threadIdx.x >> 6)) * kEcmpChunk;
-  const bool live = cbase < N;  // wave-uniform
+  if (k == 0 || cbase >= N) return;  // whole wave: no barriers below
   const uint32_t srow = row_of[s];
   const uint32_t wpm = pitch / 32;  // u32 words per bitmap
-  uint32_t* out_base = nh + nh_off[i] + cbase / 32 + lane;
-  const bool store_lane = lane < 32 && cbase / 32 + lane < wpm;
-  // fast path: even lane 2t stores word t
-  uint32_t* out_base2 = nh + nh_off[i] + cbase / 32 + lane / 2;
-  const bool store_lane2 = (lane & 1u) == 0 && cbase / 32 + lane / 2 < wpm;
+  const uint32_t* offs = nb_row + nb_row_off[i];
+  uint32_t* out_w = nh + nh_off[i] + cbase / 32;  // word base of bitmap 0
 
-  // NARROW: the u8 value a neighbour must hold at this lane's 16
-  // destinations (cbase + 16*lane + k), packed four per dword; 0xFE = none
-  // (never held by a non-drained neighbour where the source row is not
-  // saturated: d_x(s) = w(x, s) < 0xFE, and a node s cannot reach no
-  // neighbour reaches either)
+  // NARROW: the u8 value a neighbour must hold at this lane's 16 slice
+  // bytes, packed like the row; 0xFE = none (never held by a non-drained
+  // neighbour where the source row is not saturated: d_x(s) = w(x, s) < 0xFE,
+  // and a node s cannot reach no neighbour reaches either)
   uint4 tg = make_uint4(0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu);
   bool exact = !NARROW;
-  if (live && NARROW) {
+  if (NARROW) {
     const uint4 raw = *reinterpret_cast<const uint4*>(Dn + (size_t)srow * npitch + cbase + lane * 16);
+    const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+    uint32_t t[4];
     bool sat = false;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       uint32_t o = 0;
 #pragma unroll
       for (int bq = 0; bq < 4; ++bq) {
-        const uint32_t x = ((&raw.x)[w] >> (8 * bq)) & 0xFFu;
+        const uint32_t x = (rw[w] >> (8 * bq)) & 0xFFu;
         sat |= x == 0xFEu;
         o |= ((x == 0u || x >= 0xFEu) ? 0xFEu : x - 1u) << (8 * bq);  // d_x = d_s - 1
       }
-      (&tg.x)[w] = o;
+      t[w] = o;
     }
+    tg = make_uint4(t[0], t[1], t[2], t[3]);
     exact = __ballot(sat) != 0;
   }
 
-  for (uint32_t t0 = 0; t0 < k; t0 += kNbTile) {
-    const uint32_t tk = min(kNbTile, k - t0);
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < tk; j += kEcmpThreads) {
-      const uint32_t x = nb_id[nb0 + t0 + j];
-      s_id[j] = x;
-      s_w[j] = hop ? 1u : nb_w[nb0 + t0 + j];
-      s_row[j] = ovl[x] ? kInf : row_of[x];
-    }
-    __syncthreads();
-    if (!live) continue;
-    uint32_t* out = out_base + (size_t)t0 * wpm;
-    uint32_t* out2 = out_base2 + (size_t)t0 * wpm;
-    if (!exact) {
-      // fast path: kEcmpUnroll neighbour rows in flight; a drained neighbour's
-      // row reads as "unreachable" (0xFF never equals a target) and its single
-      // possible bit is patched below
-      for (uint32_t j0 = 0; j0 < tk; j0 += kEcmpUnroll) {
-        uint4 raw[kEcmpUnroll];
+  if (!exact) {
+    // fast path: lane l stores the 16-bit slice of destinations
+    // cbase + 16l .. +15; two groups of kEcmpUnroll neighbour rows in flight
+    // (ping-pong); a drained neighbour's row reads as "unreachable" (0xFF
+    // never equals a target) and its single possible bit is patched below
+    const bool st = cbase / 16 + lane < pitch / 16;
+    const uint32_t loff = lane * 16;
+    const uint8_t* dn_c = Dn + cbase;
+    // unconditional loads (drained neighbours and list padding point at the
+    // all-0xFF dead row), so the waits count exactly: group B's loads stay in
+    // flight while group A is matched
+    auto load_group = [&](uint32_t j0, uint4* r) {
+      const uint4 o4 = *reinterpret_cast<const uint4*>(offs + j0);  // one scalar load
+      const uint32_t o[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
-        for (int u = 0; u < kEcmpUnroll; ++u) {
-          const uint32_t rj = j0 + u < tk ? s_row[j0 + u] : kInf;
-          raw[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
-          if (rj != kInf)
-            raw[u] = *reinterpret_cast<const uint4*>(Dn + (size_t)rj * npitch + cbase + lane * 16);
-        }
+      for (int u = 0; u < kEcmpUnroll; ++u) r[u] = *reinterpret_cast<const uint4*>(dn_c + o[u] + loff);
+    };
+    auto match_group = [&](uint32_t j0, const uint4* r) {
 #pragma unroll
-        for (int u = 0; u < kEcmpUnroll; ++u) {
-          if (j0 + u >= tk) break;
-          const uint32_t m = eq_mask16(raw[u], tg);
-          const uint32_t word = m | (uint32_t)__shfl_xor((int)m, 1, 64) << 16;
-          if (store_lane2) out2[(size_t)(j0 + u) * wpm] = word;
-        }
+      for (int u = 0; u < kEcmpUnroll; ++u) {
+        if (j0 + u >= k) break;
+        const uint32_t m = eq_mask16(r[u], tg);
+        uint16_t* o = reinterpret_cast<uint16_t*>(out_w + (size_t)(j0 + u) * wpm);
+        if (st) o[lane] = (uint16_t)m;
       }
-    } else {
-      for (uint32_t j = 0; j < tk; ++j) {
-        const uint32_t rj = s_row[j], wj = s_w[j];
-        uint32_t word = 0;
-        if (rj != kInf) {
-          uint32_t a[16], b[16];
+    };
+    uint4 ra[kEcmpUnroll], rb[kEcmpUnroll];
+    load_group(0, ra);
+    for (uint32_t j0 = 0; j0 < k; j0 += 2 * kEcmpUnroll) {
+      load_group(j0 + kEcmpUnroll, rb);
+      match_group(j0, ra);
+      load_group(j0 + 2 * kEcmpUnroll, ra);
+      match_group(j0 + kEcmpUnroll, rb);
+    }
+  } else {
+    // exact rows: 16 ballots over destinations cbase + q*64 + lane, four
+    // at a time (both rows' loads in flight); lane t < 32 stores word t
+    const uint32_t* Ds = D + (size_t)srow * pitch;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t oj = offs[j], wj = hop ? 1u : nb_w[nb0 + j];
+      uint32_t word = 0;
+      if (oj != dead) {
+        const uint32_t rj = NARROW ? oj / npitch : oj;
+        const uint32_t* Dx = D + (size_t)rj * pitch;
 #pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const uint32_t v = cbase + q * 64 + lane;
-            a[q] = v < N ? D[(size_t)rj * pitch + v] : kInf;
-            b[q] = v < N ? D[(size_t)srow * pitch + v] : kInf;
+        for (int q0 = 0; q0 < 16; q0 += 4) {
+          uint32_t a[4], b[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t v = cbase + (q0 + u) * 64 + lane;
+            a[u] = v < N ? Dx[v] : kInf;
+            b[u] = v < N ? Ds[v] : kInf;
           }
 #pragma unroll
-          for (int q = 0; q < 16; ++q)
-            word = put_mask(word, __ballot(a[q] != kInf && b[q] != kInf && a[q] + wj == b[q]), q,
-                            lane);
+          for (int u = 0; u < 4; ++u)
+            word = put_mask(word, __ballot(a[u] != kInf && b[u] != kInf && a[u] + wj == b[u]),
+                            q0 + u, lane);
         }
-        if (store_lane) out[(size_t)j * wpm] = word;
       }
+      if (lane < 32 && cbase / 32 + lane < wpm) out_w[(size_t)j * wpm + lane] = word;
     }
-    // drained neighbour x: its bitmap is empty except, possibly, x itself --
-    // reached directly over the link when d_s(x) == w(s, x)
-    for (uint32_t j = 0; j < tk; ++j) {
-      if (s_row[j] != kInf) continue;
-      const uint32_t x = s_id[j];
+  }
+  // drained neighbour x: its bitmap is empty except, possibly, x itself --
+  // reached directly over the link when d_s(x) == w(s, x)
+  if (nb_drained[i]) {
+    for (uint32_t j = 0; j < k; ++j) {
+      if (offs[j] != dead) continue;
+      const uint32_t x = nb_id[nb0 + j];
       if (x < cbase || x >= cbase + kEcmpChunk) continue;
-      if (lane == (x - cbase) / 32 && D[(size_t)srow * pitch + x] == s_w[j])
-        out[(size_t)j * wpm] = 1u << (x & 31);
+      const uint32_t wj = hop ? 1u : nb_w[nb0 + j];
+      if (lane == (x - cbase) / 32 && D[(size_t)srow * pitch + x] == wj)
+        out_w[(size_t)j * wpm + lane] = 1u << (x & 31);
     }
   }
 }
@@ -903,13 +925,37 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   HIP_TRY(c, p->d_row_of.upload(row_of.data(), N, c->stream));
   HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
-  if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
+  {
+    // per-source neighbour rows for the next-hop pass (kInf = drained)
+    std::vector<uint32_t> nb_row, nb_row_off(n_src), nb_drained(n_src, 0);
+    const uint32_t dead = p->ms ? (uint32_t)p->closure.size() * c->npitch : kInf;
+    p->dead = dead;
+    for (uint32_t i = 0; i < n_src; ++i) {
+      nb_row_off[i] = (uint32_t)nb_row.size();
+      for (uint32_t e = c->nb_ptr[srcs[i]]; e < c->nb_ptr[srcs[i] + 1]; ++e) {
+        const uint32_t x = c->nb_id[e];
+        const bool dr = c->ovl[x] != 0;
+        nb_row.push_back(dr ? dead : p->ms ? row_of[x] * c->npitch : row_of[x]);
+        nb_drained[i] += dr;
+      }
+      const size_t k = nb_row.size() - nb_row_off[i];
+      nb_row.resize(nb_row_off[i] + (k + 7) / 8 * 8 + 8, dead);
+    }
+    HIP_TRY(c, p->d_nb_row.upload(nb_row.data(), nb_row.size(), c->stream));
+    HIP_TRY(c, p->d_nb_row_off.upload(nb_row_off.data(), n_src, c->stream));
+    HIP_TRY(c, p->d_nb_drained.upload(nb_drained.data(), n_src, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors end here
+  }
+  if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
   if (!p->ms && p->lds_bytes > kMaxLds)
     return fail(c, SPF_E_UNSUPPORTED,
                 "batched plans keep a distance row per source in LDS: %u nodes do not fit "
                 "(single-source spf_sssp and what-if batches handle large graphs)", N);
-  if (p->ms) HIP_TRY(c, p->d_Dn.alloc((size_t)p->closure.size() * c->npitch));
+  if (p->ms) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
+    HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
+    HIP_TRY(c, hipMemsetAsync(p->d_Dn.p + p->closure.size() * c->npitch, 0xFF, c->npitch, c->stream));
+  }
   {
     const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
     if (st != SPF_OK) return st;
@@ -1012,7 +1058,8 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
   const uint32_t nb = chunks * ((p->n_src + 7) / 8) * 8;
   hipLaunchKernelGGL((ecmp_kernel<NARROW>), dim3(nb), dim3(kEcmpThreads), 0, s, Dn, c->npitch, D,
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
-                     c->d_nb_w.p, c->d_ovl.p, hop ? 1u : 0u, p->d_nh_off.p, d_nh, chunks, p->n_src);
+                     c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead, hop ? 1u : 0u,
+                     p->d_nh_off.p, d_nh, chunks, p->n_src);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
