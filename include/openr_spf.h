@@ -80,6 +80,28 @@ const char* spf_global_error(void);
 
 /* Copies the graph to the device (replaces any previous graph). */
 spf_status spf_graph_load(spf_ctx* ctx, const spf_graph* g);
+
+/* In-place patches of the loaded graph: the CSR
+ * structure (nodes, up edges, their order) stays, so no spf_graph_load is
+ * needed when an adjacency-database update only toggles node overload bits or
+ * changes metrics of up links -- the reference re-runs updateAdjacencyDatabase
+ * (openr/decision/LinkState.cpp:564-719) and clears its SPF memo
+ * (:509-512, :714-717) on every such publication.
+ *   spf_graph_set_overload: overloaded[i] != 0 drains node nodes[i]
+ *     (LinkState::updateNodeOverloaded, LinkState.cpp:480-493).
+ *   spf_graph_set_metric: new metric of directed edge edges[i] (CSR edge id),
+ *     i.e. Link::getMetricFromNode of its tail (LinkState.cpp:195-204).
+ * Every change bumps spf_graph_epoch(); SPF plans (spf_plan_*) re-derive
+ * their internal state on their next execute (same output layout); KSP2 and
+ * what-if plans return SPF_E_STATE and must be recreated; any plan returns
+ * SPF_E_STATE after a spf_graph_load. */
+spf_status spf_graph_set_overload(spf_ctx* ctx, const uint32_t* nodes, const uint8_t* overloaded,
+                                  uint32_t n);
+spf_status spf_graph_set_metric(spf_ctx* ctx, const uint32_t* edges, const int32_t* metric,
+                                uint32_t n);
+uint64_t spf_graph_epoch(const spf_ctx* ctx);
+/* Number of spf_graph_load calls so far (patches do not count). */
+uint64_t spf_graph_loads(const spf_ctx* ctx);
 uint32_t spf_row_pitch(const spf_ctx* ctx);
 /* 1 when the loaded graph has an up edge with metric <= 0 (weighted solves of
  * such graphs return SPF_E_UNSUPPORTED: zero-cost plateaus make the reference's
@@ -110,6 +132,10 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
  * synchronisation, no allocation: capturable into a hipGraph. */
 spf_status spf_plan_execute(spf_plan* plan, uint32_t* d_dist, uint32_t* d_nh,
                             void* stream);
+/* spf_plan_execute into host buffers: dist [n_src][n_nodes] (dense, no row
+ * padding) and the next-hop words (spf_plan_nh_words of them); either may be
+ * NULL.  Device staging is owned by the plan. */
+spf_status spf_plan_execute_host(spf_plan* plan, uint32_t* dist, uint32_t* nh);
 
 /* Kernel timing with HIP events recorded on the execute stream: after
  * spf_plan_enable_timing(plan, K), each of the next K executes records events

@@ -142,6 +142,10 @@ PROTOTYPES = {
     "spf_last_error": (C.c_char_p, [_vp]),
     "spf_global_error": (C.c_char_p, []),
     "spf_graph_load": (C.c_int, [_vp, C.POINTER(SpfGraph)]),
+    "spf_graph_set_overload": (C.c_int, [_vp, _u32p, _u8p, C.c_uint32]),
+    "spf_graph_set_metric": (C.c_int, [_vp, _u32p, _i32p, C.c_uint32]),
+    "spf_graph_epoch": (C.c_uint64, [_vp]),
+    "spf_graph_loads": (C.c_uint64, [_vp]),
     "spf_row_pitch": (C.c_uint32, [_vp]),
     "spf_graph_has_nonpositive_metric": (C.c_int, [_vp]),
     "spf_src_neighbors": (C.c_int, [_vp, C.c_uint32, _u32p, C.c_uint32, _u32p]),
@@ -151,6 +155,7 @@ PROTOTYPES = {
     "spf_plan_nh_layout": (C.c_int, [_vp, _u64p, _u32p]),
     "spf_plan_closure_rows": (C.c_uint32, [_vp]),
     "spf_plan_execute": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "spf_plan_execute_host": (C.c_int, [_vp, _u32p, _u32p]),
     "spf_plan_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_plan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
     "spf_solve": (C.c_int, [_vp, _u32p, C.c_uint32, C.c_uint32, _u32p, _u32p]),

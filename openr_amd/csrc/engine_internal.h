@@ -55,6 +55,8 @@ struct spf_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   uint64_t solves = 0;
+  uint64_t shape = 0;  // bumped by spf_graph_load (CSR structure)
+  uint64_t epoch = 0;  // bumped by every graph change (load or in-place patch)
   // graph
   bool loaded = false;
   uint32_t N = 0, E = 0, pitch = 0;
@@ -80,6 +82,7 @@ struct spf_ctx {
 struct spf_plan {
   spf_ctx* ctx = nullptr;
   uint32_t n_src = 0, flags = 0;
+  uint64_t shape = 0, epoch = 0;  // graph state the plan was derived from
   std::vector<uint32_t> srcs, closure;
   std::vector<uint64_t> nh_off;
   std::vector<uint32_t> words;
@@ -91,6 +94,9 @@ struct spf_plan {
   spfi::DevBuf<uint64_t> d_nh_off;
   spfi::DevBuf<uint32_t> d_nb_row, d_nb_row_off, d_nb_drained;  // next-hop pass inputs
   uint32_t dead = 0;  // nb_row value of a drained neighbour
+  spfi::DevBuf<uint32_t> d_slot_src;  // next-hop blocks: source per (slot, XCD)
+  spfi::DevBuf<uint32_t> h_dist, h_nh;  // spf_plan_execute_host staging
+  size_t slots = 0;
   size_t lds_bytes = 0;
   bool q16 = true;
   // optional per-kernel timing: 3 events per execute (before SSSP, between,

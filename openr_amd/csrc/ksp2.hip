@@ -444,6 +444,7 @@ size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw,
 struct spf_ksp2_plan {
   spf_ctx* ctx = nullptr;
   uint32_t n_src = 0, lw = 0;
+  uint64_t epoch = 0;  // graph state the plan was derived from
   std::vector<uint32_t> srcs;
   DevBuf<uint32_t> d_srcs, d_D, d_H, d_all, d_wt_rev;
   DevBuf<uint8_t> d_no_drain;
@@ -516,6 +517,7 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 32, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  p->epoch = c->epoch;
   *out = p.release();
   return SPF_OK;
 }
@@ -527,6 +529,8 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
   if (!p) return fail(nullptr, SPF_E_INVALID, "spf_ksp2_execute: NULL plan");
   spf_ctx* c = p->ctx;
   if (!c->loaded) return fail(c, SPF_E_STATE, "graph no longer loaded");
+  if (p->epoch != c->epoch)
+    return fail(c, SPF_E_STATE, "graph changed since the plan was created: recreate it");
   if (!d_pairs || !d_counters || (pool_words && !d_pool))
     return fail(c, SPF_E_INVALID, "spf_ksp2_execute: NULL output buffer");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;

@@ -195,7 +195,9 @@ struct ls_state {
   std::vector<uint32_t> free_ids;
 
   // flattened graph
-  bool dirty = true;
+  bool dirty = true;                 // links changed: re-flatten (patch or reload)
+  bool engine_loaded = false;        // the engine holds the flattened graph below
+  std::vector<uint32_t> pending_ovl;  // name ids whose overload bit flipped since the last flatten
   std::vector<uint32_t> csr_name;   // csr id -> name id
   std::vector<uint32_t> csr_of;     // name id -> csr id (kNone)
   std::vector<uint32_t> row_ptr, col, link_id, edge_tail;
@@ -237,9 +239,13 @@ spf_status eng_fail(ls_state* ls, spf_status st) {
   return st;
 }
 
-void clear_memo(ls_state* ls) {
+void clear_results(ls_state* ls) {
   ls->spf_memo.clear();
   ls->ksp_memo.clear();
+}
+
+void clear_memo(ls_state* ls) {
+  clear_results(ls);
   ls->dirty = true;
 }
 
@@ -337,6 +343,7 @@ bool node_overloaded(const ls_state* ls, uint32_t node) {
 spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric down,
                     ls_change* out) {
   bool topo = false, attrs = false, label;
+  const bool known = ls->dbs.count(node) != 0;
   DbIn& slot = ls->dbs[node];
   const int32_t prior_label = slot.node_label;
   slot = std::move(db);
@@ -356,7 +363,8 @@ spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric do
               return a->before(*b);
             });
 
-  topo |= set_node_overload(ls, node, cur.overload, up, down);
+  // a node overload flip alone keeps the CSR: the engine patches one byte
+  const bool node_flip = set_node_overload(ls, node, cur.overload, up, down);
   label = prior_label != cur.node_label;
 
   size_t i = 0, j = 0;
@@ -407,14 +415,49 @@ spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric do
     ++i;
     ++j;
   }
-  if (topo) clear_memo(ls);
-  put_change(out, topo, attrs, label);
+  if (topo) {
+    clear_memo(ls);
+  } else if (node_flip) {
+    clear_results(ls);
+    ls->pending_ovl.push_back(node);
+  }
+  // a new node joins the CSR on the next flatten; like the reference, its
+  // first database signals no topology change and keeps the memo
+  if (!known) ls->dirty = true;
+  put_change(out, topo || node_flip, attrs, label);
   return SPF_OK;
 }
 
 // CSR flatten: ids in ascending name order, edges in linksFromNode order.
 spf_status flatten(ls_state* ls) {
-  if (!ls->dirty) return SPF_OK;
+  if (!ls->dirty) {
+    // only node overload bits changed: patch them in place
+    std::vector<uint32_t> nodes;
+    std::vector<uint8_t> vals;
+    for (uint32_t nm : ls->pending_ovl) {
+      const uint32_t u = nm < ls->csr_of.size() ? ls->csr_of[nm] : kNone;
+      if (u == kNone) continue;
+      const uint8_t v = node_overloaded(ls, nm);
+      if (ls->ovl[u] == v) continue;
+      ls->ovl[u] = v;
+      nodes.push_back(u);
+      vals.push_back(v);
+    }
+    ls->pending_ovl.clear();
+    if (!nodes.empty() && ls->eng && ls->engine_loaded) {
+      const spf_status st =
+          spf_graph_set_overload(ls->eng, nodes.data(), vals.data(), (uint32_t)nodes.size());
+      if (st != SPF_OK) return eng_fail(ls, st);
+    }
+    return SPF_OK;
+  }
+  ls->pending_ovl.clear();
+  // keep the flattened graph the engine holds, to patch it if only metrics
+  // and overload bits differ
+  const std::vector<uint32_t> old_name = ls->csr_name, old_rp = ls->row_ptr, old_col = ls->col,
+                              old_lid = ls->link_id;
+  const std::vector<int32_t> old_metric = ls->metric;
+  const std::vector<uint8_t> old_ovl = ls->ovl;
   std::vector<uint32_t> ids;
   ids.reserve(ls->dbs.size());
   for (const auto& kv : ls->dbs) ids.push_back(kv.first);
@@ -447,6 +490,33 @@ spf_status flatten(ls_state* ls) {
     }
     ls->row_ptr[u + 1] = (uint32_t)ls->col.size();
   }
+  if (N > 0 && ls->eng && ls->engine_loaded && ls->csr_name == old_name &&
+      ls->row_ptr == old_rp && ls->col == old_col && ls->link_id == old_lid) {
+    // same CSR structure: patch metrics and overload bits in place
+    std::vector<uint32_t> edges, nodes;
+    std::vector<int32_t> mets;
+    std::vector<uint8_t> vals;
+    for (uint32_t e = 0; e < (uint32_t)ls->metric.size(); ++e)
+      if (ls->metric[e] != old_metric[e]) {
+        edges.push_back(e);
+        mets.push_back(ls->metric[e]);
+      }
+    for (uint32_t u = 0; u < N; ++u)
+      if (ls->ovl[u] != old_ovl[u]) {
+        nodes.push_back(u);
+        vals.push_back(ls->ovl[u]);
+      }
+    spf_status st = spf_graph_set_metric(ls->eng, edges.data(), mets.data(), (uint32_t)edges.size());
+    if (st == SPF_OK)
+      st = spf_graph_set_overload(ls->eng, nodes.data(), vals.data(), (uint32_t)nodes.size());
+    if (st != SPF_OK) {
+      ls->engine_loaded = false;
+      return eng_fail(ls, st);
+    }
+    ls->dirty = false;
+    return SPF_OK;
+  }
+  ls->engine_loaded = false;
   if (N > 0 && ls->eng) {
     spf_graph g;
     g.n_nodes = N;
@@ -458,6 +528,7 @@ spf_status flatten(ls_state* ls) {
     g.overloaded = ls->ovl.data();
     const spf_status st = spf_graph_load(ls->eng, &g);
     if (st != SPF_OK) return eng_fail(ls, st);
+    ls->engine_loaded = true;
   }
   ls->dirty = false;
   return SPF_OK;

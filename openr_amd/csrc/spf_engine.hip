@@ -436,6 +436,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 constexpr int kEcmpUnroll = 4;         // neighbour rows per group (two groups in flight)
 constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
 constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
+constexpr uint32_t kEcmpRunsPerXcd = 64;  // source runs dealt to each XCD
 
 // Zero-byte flags of x at bit 7 of each byte (exact: no carries cross bytes).
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
@@ -481,15 +482,15 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     const uint32_t* __restrict__ nb_row, const uint32_t* __restrict__ nb_row_off,
     const uint32_t* __restrict__ nb_drained, uint32_t dead, uint32_t hop,
     const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh, uint32_t chunks,
-    uint32_t n_src) {
-  // Sources are dealt round-robin over the 8 XCD groups (block b runs on the
-  // XCD group b % 8): every XCD gets the same mix of switch roles (work per
-  // source ~ its neighbour count), and inside a group the sources come in id
-  // order, so e.g. the racks of one pod -- same neighbour rows -- share an L2.
+    const uint32_t* __restrict__ slot_src) {
+  // Block b runs on XCD b % 8.  slot_src (spf_plan_create) lists each XCD's
+  // sources: runs of consecutive request sources (the racks of one pod, the
+  // spines of one plane -- the same neighbour rows, shared in that XCD's L2)
+  // dealt to the XCDs by work; a source's chunks are consecutive blocks.
   const uint32_t grp = blockIdx.x & 7, pos = blockIdx.x >> 3;
-  const uint32_t i = (pos / chunks) * 8 + grp;
+  const uint32_t i = slot_src[(pos / chunks) * 8 + grp];
   const uint32_t c = pos % chunks;
-  if (i >= n_src) return;
+  if (i == kInf) return;
   const uint32_t s = req_src[i];
   const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
   const uint32_t lane = threadIdx.x & 63;
@@ -835,8 +836,95 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->loaded = true;
+  ++c->shape;
+  ++c->epoch;
   return SPF_OK;
 }
+
+// In-place graph patches.  The reference reacts to
+// every adjacency-database publication by re-running updateAdjacencyDatabase
+// (LinkState.cpp:564-719) and dropping its SPF memo; the common cases -- a node
+// toggling its overload bit (the per-iteration perturbation of
+// BM_DecisionFabric, RoutingBenchmarkUtils.cpp:453-479) or a link metric
+// change -- leave the CSR structure intact, so only the affected bytes are
+// rewritten here instead of a full spf_graph_load.
+spf_status spf_graph_set_overload(spf_ctx* c, const uint32_t* nodes, const uint8_t* overloaded,
+                                  uint32_t n) {
+  if (!c || (n && (!nodes || !overloaded)))
+    return fail(c, SPF_E_INVALID, "spf_graph_set_overload: NULL argument");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  for (uint32_t i = 0; i < n; ++i)
+    if (nodes[i] >= c->N) return fail(c, SPF_E_INVALID, "node %u out of range", nodes[i]);
+  bool changed = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t v = overloaded[i] ? 1 : 0;
+    if (c->ovl[nodes[i]] != v) {
+      c->ovl[nodes[i]] = v;
+      changed = true;
+    }
+  }
+  if (!changed) return SPF_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, c->d_ovl.upload(c->ovl.data(), c->N, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  ++c->epoch;
+  return SPF_OK;
+}
+
+spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t* metric,
+                                uint32_t n) {
+  if (!c || (n && (!edges || !metric)))
+    return fail(c, SPF_E_INVALID, "spf_graph_set_metric: NULL argument");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  for (uint32_t i = 0; i < n; ++i)
+    if (edges[i] >= c->E) return fail(c, SPF_E_INVALID, "edge %u out of range", edges[i]);
+  std::vector<uint32_t> wt = c->wt;
+  bool changed = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t w = metric[i] > 0 ? (uint32_t)metric[i] : 0u;
+    changed |= wt[edges[i]] != w;
+    wt[edges[i]] = w;
+  }
+  if (!changed) return SPF_OK;
+  bool nonpos = false;
+  uint32_t max_metric = 0;
+  for (uint32_t e = 0; e < c->E; ++e) {
+    nonpos |= wt[e] == 0;
+    max_metric = std::max(max_metric, wt[e]);
+  }
+  if ((uint64_t)max_metric * (uint64_t)(c->N - 1) >= (uint64_t)kInf)
+    return fail(c, SPF_E_UNSUPPORTED, "max metric %u x %u hops overflows 32-bit distances",
+                max_metric, c->N - 1);
+  c->wt.swap(wt);
+  c->nonpos = nonpos;
+  c->max_metric = max_metric;
+  c->unit = !nonpos && max_metric <= 1;
+  // min metric per distinct neighbour of every tail touched
+  std::vector<uint32_t> tails;
+  for (uint32_t i = 0; i < n; ++i)
+    tails.push_back((uint32_t)(std::upper_bound(c->row_ptr.begin(), c->row_ptr.end(), edges[i]) -
+                               c->row_ptr.begin()) - 1);
+  std::sort(tails.begin(), tails.end());
+  tails.erase(std::unique(tails.begin(), tails.end()), tails.end());
+  for (uint32_t u : tails) {
+    const uint32_t b = c->nb_ptr[u], e = c->nb_ptr[u + 1];
+    for (uint32_t j = b; j < e; ++j) c->nb_w[j] = kInf;
+    for (uint32_t k = c->row_ptr[u]; k < c->row_ptr[u + 1]; ++k) {
+      const uint32_t j = (uint32_t)(std::lower_bound(c->nb_id.begin() + b, c->nb_id.begin() + e,
+                                                     c->col[k]) - c->nb_id.begin());
+      c->nb_w[j] = std::min(c->nb_w[j], c->wt[k]);
+    }
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, c->d_wt.upload(c->wt.data(), c->E, c->stream));
+  HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  ++c->epoch;
+  return SPF_OK;
+}
+
+uint64_t spf_graph_epoch(const spf_ctx* c) { return c ? c->epoch : 0; }
+uint64_t spf_graph_loads(const spf_ctx* c) { return c ? c->shape : 0; }
 
 spf_status spf_src_neighbors(const spf_ctx* c, uint32_t src, uint32_t* out,
                              uint32_t cap, uint32_t* count) {
@@ -848,27 +936,28 @@ spf_status spf_src_neighbors(const spf_ctx* c, uint32_t src, uint32_t* out,
   return SPF_OK;
 }
 
-spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
-                           uint32_t flags, spf_plan** out) {
-  if (!c || !out) return fail(c, SPF_E_INVALID, "spf_plan_create: NULL argument");
-  *out = nullptr;
-  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
-  if (n_src == 0 || !srcs) return fail(c, SPF_E_INVALID, "empty source list");
-  const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
+}  // extern "C"
+
+namespace {
+
+// Everything a plan derives from the graph's current state (closure over
+// non-drained neighbours, narrow/exact mode, next-hop row tables).  Run at
+// creation and again by spf_plan_execute after an in-place graph patch
+// (spf_graph_set_overload / spf_graph_set_metric); the output layout
+// (nh_off, words) depends only on the CSR structure, which patches keep.
+spf_status build_plan(spf_ctx* c, spf_plan* p) {
+  const uint32_t n_src = p->n_src;
+  const uint32_t* srcs = p->srcs.data();
+  const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
   if (!hop && c->nonpos)
     return fail(c, SPF_E_UNSUPPORTED,
                 "graph has up links with metric <= 0; weighted SPF over zero/negative "
                 "metrics is outside the exact-parity envelope");
   const uint32_t N = c->N;
-  auto p = std::make_unique<spf_plan>();
-  p->ctx = c;
-  p->n_src = n_src;
-  p->flags = flags;
-  p->srcs.assign(srcs, srcs + n_src);
+  p->closure.clear();
   std::vector<uint32_t> row_of(N, kInf);
   bool distinct = true;
   for (uint32_t i = 0; i < n_src; ++i) {
-    if (srcs[i] >= N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
     if (row_of[srcs[i]] != kInf) distinct = false;
     else row_of[srcs[i]] = i;
   }
@@ -945,6 +1034,37 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
     HIP_TRY(c, p->d_nb_row.upload(nb_row.data(), nb_row.size(), c->stream));
     HIP_TRY(c, p->d_nb_row_off.upload(nb_row_off.data(), n_src, c->stream));
     HIP_TRY(c, p->d_nb_drained.upload(nb_drained.data(), n_src, c->stream));
+    // next-hop blocks per XCD: runs of consecutive sources of about
+    // 1/(8 * runs) of the work each, every run to the XCD with the least
+    // work so far (runs come in request order: the heavy spine and fabric
+    // switches first)
+    const char* env = std::getenv("SPF_ECMP_RUNS");
+    const uint32_t runs = env ? (uint32_t)atoi(env) : kEcmpRunsPerXcd;
+    std::vector<uint32_t> lists[8];
+    if (runs == 0) {  // plain round-robin
+      for (uint32_t i = 0; i < n_src; ++i) lists[i % 8].push_back(i);
+    } else {
+      uint64_t total = 0, load[8] = {};
+      for (uint32_t i = 0; i < n_src; ++i) total += p->words[i] + 1;
+      const uint64_t target = std::max<uint64_t>(1, total / (8ull * runs));
+      for (uint32_t i = 0; i < n_src;) {
+        uint32_t e = i;
+        uint64_t w = 0;
+        while (e < n_src && w < target) w += p->words[e++] + 1;
+        const int g = (int)(std::min_element(load, load + 8) - load);
+        load[g] += w;
+        for (uint32_t t = i; t < e; ++t) lists[g].push_back(t);
+        i = e;
+      }
+    }
+    size_t most = 0;
+    for (auto& l : lists) most = std::max(most, l.size());
+    std::vector<uint32_t> slot(most * 8, kInf);
+    for (int g = 0; g < 8; ++g)
+      for (size_t t = 0; t < lists[g].size(); ++t) slot[t * 8 + g] = lists[g][t];
+    p->slots = slot.size();
+    if (slot.empty()) slot.push_back(kInf);
+    HIP_TRY(c, p->d_slot_src.upload(slot.data(), slot.size(), c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors end here
   }
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
@@ -961,9 +1081,34 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
     if (st != SPF_OK) return st;
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  p->epoch = c->epoch;
+  return SPF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
+                           uint32_t flags, spf_plan** out) {
+  if (!c || !out) return fail(c, SPF_E_INVALID, "spf_plan_create: NULL argument");
+  *out = nullptr;
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (n_src == 0 || !srcs) return fail(c, SPF_E_INVALID, "empty source list");
+  for (uint32_t i = 0; i < n_src; ++i)
+    if (srcs[i] >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
+  auto p = std::make_unique<spf_plan>();
+  p->ctx = c;
+  p->n_src = n_src;
+  p->flags = flags;
+  p->srcs.assign(srcs, srcs + n_src);
+  p->shape = c->shape;
+  const spf_status st = build_plan(c, p.get());
+  if (st != SPF_OK) return st;
   *out = p.release();
   return SPF_OK;
 }
+
 
 void spf_plan_destroy(spf_plan* p) { delete p; }
 uint64_t spf_plan_nh_words(const spf_plan* p) { return p ? p->nh_total : 0; }
@@ -1055,11 +1200,11 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
                        uint32_t* d_nh, hipStream_t s) {
   const uint32_t per_block = kEcmpChunk * kEcmpWaves;
   const uint32_t chunks = (c->N + per_block - 1) / per_block;
-  const uint32_t nb = chunks * ((p->n_src + 7) / 8) * 8;
+  const uint32_t nb = chunks * (uint32_t)p->slots;
   hipLaunchKernelGGL((ecmp_kernel<NARROW>), dim3(nb), dim3(kEcmpThreads), 0, s, Dn, c->npitch, D,
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
                      c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead, hop ? 1u : 0u,
-                     p->d_nh_off.p, d_nh, chunks, p->n_src);
+                     p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -1114,6 +1259,12 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   if (!c->loaded) return fail(c, SPF_E_STATE, "graph no longer loaded");
   if (!d_dist || (p->nh_total && !d_nh))
     return fail(c, SPF_E_INVALID, "spf_plan_execute: NULL output buffer");
+  if (p->shape != c->shape)
+    return fail(c, SPF_E_STATE, "graph reloaded since the plan was created: recreate it");
+  if (p->epoch != c->epoch) {  // patched in place: re-derive, same output layout
+    const spf_status st = build_plan(c, p);
+    if (st != SPF_OK) return st;
+  }
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint32_t pitch = c->pitch;
   const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
@@ -1175,26 +1326,32 @@ spf_status spf_plan_timing(spf_plan* p, double* sssp_ms, double* ecmp_ms, uint32
   return SPF_OK;
 }
 
+spf_status spf_plan_execute_host(spf_plan* p, uint32_t* dist_out, uint32_t* nh_out) {
+  if (!p) return fail(nullptr, SPF_E_INVALID, "spf_plan_execute_host: NULL plan");
+  spf_ctx* c = p->ctx;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, p->h_dist.alloc((size_t)p->n_src * c->pitch));
+  HIP_TRY(c, p->h_nh.alloc(std::max<uint64_t>(p->nh_total, 1)));
+  const spf_status st = spf_plan_execute(p, p->h_dist.p, p->h_nh.p, nullptr);
+  if (st != SPF_OK) return st;
+  if (dist_out) {
+    HIP_TRY(c, hipMemcpy2DAsync(dist_out, (size_t)c->N * 4, p->h_dist.p, (size_t)c->pitch * 4,
+                                (size_t)c->N * 4, p->n_src, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (nh_out && p->nh_total) {
+    HIP_TRY(c, hipMemcpyAsync(nh_out, p->h_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SPF_OK;
+}
+
 spf_status spf_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
                      uint32_t* dist_out, uint32_t* nh_out) {
   spf_plan* raw = nullptr;
   spf_status st = spf_plan_create(c, srcs, n_src, flags, &raw);
   if (st != SPF_OK) return st;
   std::unique_ptr<spf_plan> p(raw);
-  DevBuf<uint32_t> d_dist, d_nh;
-  HIP_TRY(c, d_dist.alloc((size_t)n_src * c->pitch));
-  HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(p->nh_total, 1)));
-  st = spf_plan_execute(p.get(), d_dist.p, d_nh.p, nullptr);
-  if (st != SPF_OK) return st;
-  if (dist_out) {
-    HIP_TRY(c, hipMemcpy2DAsync(dist_out, (size_t)c->N * 4, d_dist.p, (size_t)c->pitch * 4,
-                                (size_t)c->N * 4, n_src, hipMemcpyDeviceToHost, c->stream));
-  }
-  if (nh_out && p->nh_total) {
-    HIP_TRY(c, hipMemcpyAsync(nh_out, d_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
-  }
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return SPF_OK;
+  return spf_plan_execute_host(p.get(), dist_out, nh_out);
 }
 
 spf_status spf_debug_stamps(spf_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n) {

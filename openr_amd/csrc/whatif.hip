@@ -827,6 +827,7 @@ __global__ void base_digest_kernel(spf_whatif_digest* o, const unsigned long lon
 struct spf_whatif_plan {
   spf_ctx* ctx = nullptr;
   uint32_t src = 0, n_fail = 0, W = 0, wave_teams = 0;
+  uint64_t epoch = 0;  // graph state the plan was derived from
   DevBuf<uint32_t> d_fails, d_link_edge, d_nbr_bit, d_dist, d_q, d_q2, d_bm, d_nhb, d_ctr;
   DevBuf<uint32_t> d_lvl, d_order, d_misc;
   DevBuf<unsigned long long> d_H;
@@ -942,6 +943,7 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
     HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 16 * bt * 8, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  p->epoch = c->epoch;
   *out = p.release();
   return SPF_OK;
 }
@@ -961,6 +963,8 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   if (!p || !d_out) return fail(p ? p->ctx : nullptr, SPF_E_INVALID, "spf_whatif_execute: NULL");
   spf_ctx* c = p->ctx;
   if (!c->loaded) return fail(c, SPF_E_STATE, "graph no longer loaded");
+  if (p->epoch != c->epoch)
+    return fail(c, SPF_E_STATE, "graph changed since the plan was created: recreate it");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint32_t N = c->N;
   hipEvent_t* ev = nullptr;

@@ -75,6 +75,14 @@ class SpfPlan:
         self._eng._err(N.lib.spf_plan_execute(self._h, C.c_void_p(d_dist), C.c_void_p(d_nh),
                                               C.c_void_p(stream) if stream else None))
 
+    def execute_host(self) -> "SolveResult":
+        """Execute into host arrays (spf_plan_execute_host)."""
+        n = self._eng.n_nodes
+        dist = np.zeros((self.n_src, n), np.uint32)
+        nh = np.zeros(max(1, self.nh_words), np.uint32)
+        self._eng._err(N.lib.spf_plan_execute_host(self._h, N.ptr(dist), N.ptr(nh)))
+        return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
+
     def enable_timing(self, max_executes: int) -> None:
         self._eng._err(N.lib.spf_plan_enable_timing(self._h, max_executes))
 
@@ -236,6 +244,39 @@ class SpfEngine:
         g.overloaded = N.ptr(arrs[4], C.c_uint8)
         self._err(N.lib.spf_graph_load(self._h, C.byref(g)))
         self._graph = arrs
+
+    def set_overload(self, nodes, overloaded) -> None:
+        """Drain / undrain nodes in place (spf_graph_set_overload): SPF plans
+        re-derive on their next execute, KSP2 / what-if plans must be recreated."""
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        vals = np.ascontiguousarray(overloaded, np.uint8)
+        if len(nodes) != len(vals):
+            raise ValueError("nodes / overloaded length mismatch")
+        self._err(N.lib.spf_graph_set_overload(self._h, N.ptr(nodes), N.ptr(vals, C.c_uint8),
+                                               len(nodes)))
+        if self._graph is not None:
+            self._graph[4][nodes] = vals
+
+    def set_metric(self, edges, metric) -> None:
+        """New metrics of directed CSR edges in place (spf_graph_set_metric)."""
+        edges = np.ascontiguousarray(edges, np.uint32)
+        mets = np.ascontiguousarray(metric, np.int32)
+        if len(edges) != len(mets):
+            raise ValueError("edges / metric length mismatch")
+        self._err(N.lib.spf_graph_set_metric(self._h, N.ptr(edges), N.ptr(mets, C.c_int32),
+                                             len(edges)))
+        if self._graph is not None:
+            self._graph[2][edges] = mets
+
+    @property
+    def epoch(self) -> int:
+        """Graph version: bumped by every load and in-place patch."""
+        return int(N.lib.spf_graph_epoch(self._h))
+
+    @property
+    def loads(self) -> int:
+        """spf_graph_load calls so far (in-place patches do not count)."""
+        return int(N.lib.spf_graph_loads(self._h))
 
     @property
     def pitch(self) -> int:
