@@ -123,6 +123,12 @@ spf_status ls_get_spf_result(ls_state* ls, const char* node, int use_link_metric
                              ls_spf_view* out);
 spf_status ls_get_kth_paths(ls_state* ls, const char* src, const char* dst,
                             uint64_t k, ls_paths_view* out);
+/* Batch fill of the getKthPaths memo: (src, d, 1) and (src, d, 2) for every
+ * node d in one KSP2 launch.  Later ls_get_kth_paths calls for src return the
+ * prefetched paths; spf_runs still counts as if each pair were queried on its
+ * own (LinkState.cpp:778-779, 815).  Used by SpfSolver's KSP2_ED_ECMP route
+ * build (Decision.cpp:895-1018). */
+spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src);
 spf_status ls_get_metric_a_to_b(ls_state* ls, const char* a, const char* b,
                                 int use_link_metric, uint64_t* metric,
                                 int* has_value);

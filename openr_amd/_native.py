@@ -200,6 +200,7 @@ PROTOTYPES = {
     "ls_links_from_node": (C.c_int, [_vp, C.c_char_p, _u32p, C.c_uint32, _u32p]),
     "ls_link_info": (C.c_int, [_vp, C.c_uint32, C.POINTER(LsLinkDesc)]),
     "ls_get_spf_result": (C.c_int, [_vp, C.c_char_p, C.c_int, C.POINTER(LsSpfView)]),
+    "ls_prefetch_kth_paths": (C.c_int, [_vp, C.c_char_p]),
     "ls_get_kth_paths": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_uint64,
                                    C.POINTER(LsPathsView)]),
     "ls_get_metric_a_to_b": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_int, _u64p,

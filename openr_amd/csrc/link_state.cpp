@@ -168,6 +168,11 @@ struct SpfMemo {
 };
 struct PathMemo {
   std::vector<uint32_t> path_ptr{0}, link;
+  // filled by ls_prefetch_kth_paths: the reference's side effects of
+  // computing it (getSpfResult(src) for k = 1, one runSpf for k = 2 with
+  // k = 1 paths) are applied on first access, so spf_runs counts as if the
+  // pair had been queried alone
+  uint8_t pending = 0;
 };
 
 }  // namespace
@@ -627,7 +632,21 @@ spf_status kth_paths(ls_state* ls, uint32_t src, uint32_t dst, uint64_t k, const
   auto key = std::make_tuple(src, dst, k);
   auto it = ls->ksp_memo.find(key);
   if (it != ls->ksp_memo.end()) {
-    *out = &it->second;
+    PathMemo& m = it->second;
+    if (m.pending) {  // prefetched: settle the reference's side effects
+      m.pending = 0;
+      if (k == 1) {
+        const SpfMemo* sm = nullptr;
+        const spf_status st = spf_result(ls, src, true, &sm);
+        if (st != SPF_OK) return st;
+      } else {
+        const PathMemo* k1 = nullptr;
+        const spf_status st = kth_paths(ls, src, dst, 1, &k1);
+        if (st != SPF_OK) return st;
+        if (!k1->link.empty()) ls->spf_runs++;  // LinkState.cpp:778-779
+      }
+    }
+    *out = &m;
     return SPF_OK;
   }
   std::vector<uint32_t> ignore;
@@ -898,6 +917,47 @@ spf_status ls_get_kth_paths(ls_state* ls, const char* src, const char* dst, uint
   out->n_paths = (uint32_t)pm->path_ptr.size() - 1;
   out->path_ptr = pm->path_ptr.data();
   out->link = pm->link.data();
+  return SPF_OK;
+}
+
+// getKthPaths(src, d, 1) and (src, d, 2) for every node d in one batched
+// KSP2 launch (spf_ksp2_solve), stored in the memo; SpfSolver calls it
+// before building KSP2_ED_ECMP routes (Decision.cpp:895-1018 queries every
+// advertiser of every such prefix).
+spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src_c) {
+  if (!ls || !src_c) return SPF_E_INVALID;
+  spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  if (!ls->eng) return lfail(ls, SPF_E_NO_DEVICE, "LinkState created host-only (device < 0)");
+  const uint32_t src = ls->intern(src_c);
+  const uint32_t s = src < ls->csr_of.size() ? ls->csr_of[src] : kNone;
+  if (s == kNone) return SPF_OK;  // not in the graph: every query is empty anyway
+  const uint32_t N = (uint32_t)ls->csr_name.size();
+  std::vector<spf_ksp2_pair> pairs(N);
+  std::vector<uint32_t> pool;
+  uint64_t used = 0;
+  st = spf_ksp2_solve(ls->eng, &s, 1, pairs.data(), nullptr, 0, &used);
+  if (st != SPF_OK && st != SPF_E_NOMEM) return eng_fail(ls, st);
+  pool.resize(std::max<uint64_t>(used, 1));
+  st = spf_ksp2_solve(ls->eng, &s, 1, pairs.data(), pool.data(), pool.size(), &used);
+  if (st != SPF_OK) return eng_fail(ls, st);
+  for (uint32_t d = 0; d < N; ++d) {
+    const uint32_t dst = ls->csr_name[d];
+    for (uint32_t k = 1; k <= 2; ++k) {
+      auto key = std::make_tuple(src, dst, (uint64_t)k);
+      if (ls->ksp_memo.count(key)) continue;
+      PathMemo m;
+      uint32_t at = pairs[d].first[k - 1];
+      for (uint32_t p = 0; p < pairs[d].n_paths[k - 1] && at != SPF_KSP2_NONE; ++p) {
+        const uint32_t n = pool[at], next = pool[at + 1];
+        m.link.insert(m.link.end(), pool.begin() + at + 2, pool.begin() + at + 2 + n);
+        m.path_ptr.push_back((uint32_t)m.link.size());
+        at = next;
+      }
+      m.pending = 1;
+      ls->ksp_memo.emplace(key, std::move(m));
+    }
+  }
   return SPF_OK;
 }
 

@@ -317,6 +317,11 @@ class LinkState:
         self._ksp_cache[key] = paths
         return paths
 
+    def prefetchKthPaths(self, src: str) -> None:
+        """Fill the getKthPaths memo for (src, *, 1) and (src, *, 2) with one
+        batched KSP2 launch (ls_prefetch_kth_paths)."""
+        self._err(N.lib.ls_prefetch_kth_paths(self._h, src.encode()))
+
     def getMetricFromAToB(self, a: str, b: str, useLinkMetric: bool = True) -> Optional[int]:
         m = C.c_uint64()
         has = C.c_int()

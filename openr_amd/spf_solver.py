@@ -16,14 +16,25 @@ Covered, single area, over the MI355X engine:
     one SPF plan for me (+ every neighbour with LFA) and a next-hop selection
     kernel, one wavefront per destination set.
 
+  * SR_MPLS forwarding (selectBestPathsSpf with perDestination, :829-893 and
+    the push-label branch of getNextHopsThrift :1260-1290) over the memoised
+    SPF results of me (and, with LFA, of every neighbour);
+  * KSP2_ED_ECMP (selectBestPathsKsp2 :895-1018):
+    k = 1 / k = 2 edge-disjoint paths to every advertiser from ONE batched
+    KSP2 launch (LinkState.prefetchKthPaths -> ls_prefetch_kth_paths), the
+    anycast filter LinkState.pathAInPathB, label stacks with PHP and prepend
+    labels;
+  * addBestPaths (:1020-1080): min-nexthop threshold, static next hops of a
+    self-advertised prefix with a prepend label.
+
 Not covered yet (raise NotImplementedError): multiple areas, BGP / best-route
-selection by PrefixMetrics, SR_MPLS forwarding and KSP2_ED_ECMP prefixes
-(SURVEY.md §8(f) rank 3).
+selection by PrefixMetrics.
 """
 
 from __future__ import annotations
 
 import ctypes as C
+from collections import deque
 from dataclasses import dataclass, field
 from typing import Dict, FrozenSet, List, Optional, Sequence, Set, Tuple
 
@@ -80,6 +91,7 @@ class PrefixEntry:
     forwardingType: str = "IP"
     forwardingAlgorithm: str = "SP_ECMP"
     prependLabel: Optional[int] = None
+    minNexthop: Optional[int] = None
 
     @property
     def isV4(self) -> bool:
@@ -133,6 +145,28 @@ class DecisionRouteDb:
         self.mplsRoutes[r.label] = r
 
 
+# enum values of OpenrConfig.thrift:77-85 (getPrefixForwardingTypeAndAlgorithm
+# takes the minimum over the best entries)
+_FWD_TYPE = {"IP": 0, "SR_MPLS": 1}
+_FWD_ALGO = {"SP_ECMP": 0, "KSP2_ED_ECMP": 1}
+
+
+def getPrefixForwardingTypeAndAlgorithm(entries: Dict[Tuple[str, str], "PrefixEntry"],
+                                        best: Set[Tuple[str, str]]) -> Tuple[str, str]:
+    """openr/common/Util.cpp:617-643."""
+    if not entries:
+        return "IP", "SP_ECMP"
+    t, a = 1, 1
+    for na, e in entries.items():
+        if na not in best:
+            continue
+        t = min(t, _FWD_TYPE[e.forwardingType])
+        a = min(a, _FWD_ALGO[e.forwardingAlgorithm])
+        if t == 0 and a == 0:
+            break
+    return ("IP", "SR_MPLS")[t], ("SP_ECMP", "KSP2_ED_ECMP")[a]
+
+
 @dataclass
 class _SetResult:
     min_metric: Optional[int]
@@ -148,8 +182,18 @@ class SpfSolver:
         self.myNodeName = myNodeName
         self.enableV4 = enableV4
         self.computeLfaPaths = computeLfaPaths
+        self.bgpDryRun = bgpDryRun
+        self.staticMplsRoutes: Dict[int, List[NextHopThrift]] = {}
         if enableBestRouteSelection:
             raise NotImplementedError("best route selection by PrefixMetrics")
+
+    def updateStaticMplsRoutes(self, routesToUpdate: Dict[int, List[NextHopThrift]],
+                               routesToDelete: Sequence[int] = ()) -> None:
+        """SpfSolver::updateStaticMplsRoutes (Decision.cpp): label -> next hops."""
+        for label, nhs in routesToUpdate.items():
+            self.staticMplsRoutes[label] = list(nhs)
+        for label in routesToDelete:
+            self.staticMplsRoutes.pop(label, None)
 
     # -- batched next-hop selection (getMinCostNodes/..WithMetric/..Thrift) ----
     def _select(self, ls: LinkState, me: str, sets: Sequence[Sequence[str]]) -> List[_SetResult]:
@@ -200,6 +244,135 @@ class SpfSolver:
                                   link.getArea(), nb))
         return out
 
+    # -- SR_MPLS SP_ECMP: getNextHopsWithMetric / getNextHopsThrift with
+    #    perDestination = true (Decision.cpp:829-893, 1107-1305) --------------------
+    def _srSpfNextHops(self, ls: LinkState, me: str, area: str, best: List[Tuple[str, str]],
+                       ents: Dict[Tuple[str, str], PrefixEntry], isV4: bool,
+                       labels: Dict[str, int]) -> Set[NextHopThrift]:
+        dsts = list(best)
+        if any(na[0] == me for na in best):  # :848-857
+            for na, e in ents.items():
+                if na[0] == me and e.prependLabel is not None:
+                    if na in dsts:
+                        dsts.remove(na)
+                    break
+        dstSet = set(dsts)
+        mine = ls.getSpfResult(me)
+        shortest, minCost = (1 << 64) - 1, set()
+        for d, _ in sorted(dsts):  # getMinCostNodes (:1082-1105)
+            if d not in mine:
+                continue
+            m = mine[d].metric()
+            if shortest >= m:
+                if shortest > m:
+                    shortest, minCost = m, set()
+                minCost.add(d)
+        nextHopNodes: Dict[Tuple[str, str], int] = {}
+        for d in minCost:
+            for nh in mine[d].nextHops():
+                nextHopNodes[(nh, d)] = shortest - ls.getMetricFromAToB(me, nh)
+        if self.computeLfaPaths and minCost:
+            for link in ls.linksFromNode(me):
+                if not link.isUp():
+                    continue
+                nb = link.getOtherNodeName(me)
+                fromNb = ls.getSpfResult(nb)
+                nbToHere = fromNb[me].metric()
+                for d, a in sorted(dsts):
+                    if a != area or d not in fromNb:
+                        continue
+                    dn = fromNb[d].metric()
+                    if dn < shortest + nbToHere:  # RFC 5286 (:1180)
+                        key = (nb, d)
+                        if key not in nextHopNodes or nextHopNodes[key] > dn:
+                            nextHopNodes[key] = dn
+        out: Set[NextHopThrift] = set()
+        if not nextHopNodes:
+            return out
+        for link in ls.linksFromNode(me):
+            nb = link.getOtherNodeName(me)
+            for d, a in sorted(dsts):
+                if a != area:
+                    continue
+                via = nextHopNodes.get((nb, d))
+                if via is None or not link.isUp():
+                    continue
+                if (nb, area) in dstSet and nb != d:
+                    continue
+                over = link.getMetricFromNode(me) + via
+                if not self.computeLfaPaths and over != shortest:
+                    continue
+                push: List[int] = []
+                pe = ents[(d, area)]
+                if pe.prependLabel is not None:
+                    push.append(pe.prependLabel)
+                    if not isMplsLabelValid(push[-1]):
+                        continue
+                if d != nb:
+                    push.append(labels.get(d, 0))
+                    if not isMplsLabelValid(push[-1]):
+                        continue
+                action = MplsAction("PUSH", None, tuple(push)) if push else None
+                addr = link.getNhV4FromNode(me) if isV4 else link.getNhV6FromNode(me)
+                out.add(createNextHop(addr, link.getIfaceFromNode(me), over, action,
+                                      link.getArea(), nb))
+        return out
+
+    # -- KSP2_ED_ECMP: selectBestPathsKsp2 (Decision.cpp:895-1018) -------------------
+    def _ksp2NextHops(self, ls: LinkState, me: str, area: str, best: List[Tuple[str, str]],
+                      ents: Dict[Tuple[str, str], PrefixEntry], isV4: bool,
+                      labels: Dict[str, int]) -> Set[NextHopThrift]:
+        paths = []
+        for node, a in sorted(best):
+            if node == me and a == area:
+                continue
+            paths.extend(ls.getKthPaths(me, node, 1))
+        first = len(paths)
+        for node, a in sorted(best):
+            if a != area:
+                continue
+            for sec in ls.getKthPaths(me, node, 2):
+                # anycast: drop a second path that contains a shortest one
+                if not any(LinkState.pathAInPathB(paths[i], sec) for i in range(first)):
+                    paths.append(sec)
+        out: Set[NextHopThrift] = set()
+        for path in paths:
+            cost, stack, nxt = 0, deque(), me
+            for link in path:
+                cost += link.getMetricFromNode(nxt)
+                nxt = link.getOtherNodeName(nxt)
+                stack.appendleft(labels.get(nxt, 0))
+            stack.pop()  # the first hop's label: PHP
+            pe = ents[(nxt, area)]
+            if pe.prependLabel is not None:
+                stack.appendleft(pe.prependLabel)  # bottom of the stack
+            head = path[0]
+            action = MplsAction("PUSH", None, tuple(stack)) if stack else None
+            addr = head.getNhV4FromNode(me) if isV4 else head.getNhV6FromNode(me)
+            out.add(createNextHop(addr, head.getIfaceFromNode(me), cost, action, head.getArea(),
+                                  head.getOtherNodeName(me)))
+        return out
+
+    # -- addBestPaths (Decision.cpp:1020-1080) ---------------------------------------
+    def _addBestPaths(self, me: str, prefix: str, best: List[Tuple[str, str]],
+                      bestNA: Tuple[str, str], ents: Dict[Tuple[str, str], PrefixEntry],
+                      nhs: Set[NextHopThrift]) -> Optional[RibUnicastEntry]:
+        need = None
+        for na in best:  # getMinNextHopThreshold: the largest minNexthop
+            m = ents[na].minNexthop
+            if m is not None and (need is None or m > need):
+                need = m
+        if need is not None and need > len(nhs):
+            return None  # min-nexthop requirement not met
+        if any(na[0] == me for na in best):
+            prepend = next((e.prependLabel for na, e in ents.items()
+                            if na[0] == me and e.prependLabel is not None), None)
+            assert prepend is not None, "self route must carry a prepend label"
+            nhs = set(nhs)
+            for nh in self.staticMplsRoutes.get(prepend, []):
+                nhs.add(createNextHop(nh.address, None, 0, None))
+        return RibUnicastEntry(prefix, nhs, ents[bestNA], bestNA[1])
+
     # -- buildRouteDb (Decision.cpp:557-722) ----------------------------------------
     def buildRouteDb(self, myNodeName: str, areaLinkStates: Dict[str, LinkState],
                      prefixState: PrefixState) -> Optional[DecisionRouteDb]:
@@ -213,7 +386,10 @@ class SpfSolver:
         mine = ls.getSpfResult(me)  # memoised: reachability for prefix filtering
 
         # ---- unicast: destination set per prefix (createRouteForPrefix) ----
-        uni: List[Tuple[str, Dict[Tuple[str, str], PrefixEntry], List[str]]] = []
+        labels = ls.getAdjacencyDatabaseLabels()
+        uni: List[Tuple[str, Dict[Tuple[str, str], PrefixEntry], List[str], Tuple[str, str]]] = []
+        sr: List[Tuple[str, Dict[Tuple[str, str], PrefixEntry], List[Tuple[str, str]],
+                       Tuple[str, str], str]] = []
         for prefix, entries in prefixState.prefixes().items():
             ents = {na: e for na, e in entries.items() if na[1] == area and na[0] in mine}
             if not ents:
@@ -223,22 +399,24 @@ class SpfSolver:
                 continue
             if any(e.type == "BGP" for e in ents.values()):
                 raise NotImplementedError("BGP prefixes / metric-vector selection")
-            if any(e.forwardingType != "IP" or e.forwardingAlgorithm != "SP_ECMP"
-                   for e in ents.values()):
-                raise NotImplementedError("SR_MPLS / KSP2_ED_ECMP forwarding")
-            # openr routes: every advertiser is best; drop drained ones unless
-            # all are (maybeFilterDrainedNodes)
-            best = sorted(ents)
-            undrained = [na for na in best if not ls.isNodeOverloaded(na[0])]
-            best = undrained or best
+            # openr routes: every advertiser is best (selectBestRoutes), the
+            # best node-area the first of them; drop drained ones unless all
+            # are (maybeFilterDrainedNodes :766-789 -- which keeps the
+            # unfiltered bestNodeArea)
+            allNA = sorted(ents)
+            bestNA = allNA[0]
+            best = [na for na in allNA if not ls.isNodeOverloaded(na[0])] or allNA
             hasSelfPrepend = all(e.prependLabel is not None
                                  for na, e in ents.items() if na[0] == me)
             if any(na[0] == me for na in best) and not hasSelfPrepend:
                 continue  # self-advertised
-            uni.append((prefix, ents, [na[0] for na in best]))
+            ftype, falgo = getPrefixForwardingTypeAndAlgorithm(ents, set(best))
+            if falgo == "SP_ECMP" and ftype == "IP":
+                uni.append((prefix, ents, [na[0] for na in best], bestNA))
+            else:
+                sr.append((prefix, ents, best, bestNA, falgo))
 
         # ---- node labels (collisions: Decision.cpp:605-617) ----
-        labels = ls.getAdjacencyDatabaseLabels()
         label_to_node: Dict[int, str] = {}
         for node, label in labels.items():
             if label == 0 or not isMplsLabelValid(label):
@@ -248,16 +426,34 @@ class SpfSolver:
                 continue
             label_to_node[label] = node
 
-        sets = [dsts for _, _, dsts in uni] + [[n] for n in label_to_node.values()]
+        sets = [dsts for _, _, dsts, _ in uni] + [[n] for n in label_to_node.values()]
         sel = self._select(ls, me, sets)
 
-        for (prefix, ents, dsts), res in zip(uni, sel[: len(uni)]):
+        for (prefix, ents, dsts, bestNA), res in zip(uni, sel[: len(uni)]):
             if not res.hops:
                 continue  # no route to prefix
             isV4 = next(iter(ents.values())).isV4
-            bestNA = (sorted(dsts)[0], area)
             nhs = self._next_hops(ls, me, area, res, isV4, set(dsts), None)
-            db.addUnicastRoute(RibUnicastEntry(prefix, nhs, ents[bestNA], area))
+            r = self._addBestPaths(me, prefix, [(d, area) for d in dsts], bestNA, ents, nhs)
+            if r is not None:
+                db.addUnicastRoute(r)
+
+        # ---- SR_MPLS prefixes: per-destination SP_ECMP or KSP2_ED_ECMP ----
+        if any(falgo == "KSP2_ED_ECMP" for *_, falgo in sr):
+            ls.prefetchKthPaths(me)  # one batched KSP2 launch for every advertiser
+        for prefix, ents, best, bestNA, falgo in sr:
+            isV4 = next(iter(ents.values())).isV4
+            if falgo == "KSP2_ED_ECMP":
+                if any(ents[na].forwardingType != "SR_MPLS" for na in best):
+                    continue  # incompatible forwarding type (Decision.cpp:905-913)
+                nhs = self._ksp2NextHops(ls, me, area, best, ents, isV4, labels)
+            else:
+                nhs = self._srSpfNextHops(ls, me, area, best, ents, isV4, labels)
+            if not nhs:
+                continue  # no route to prefix
+            r = self._addBestPaths(me, prefix, best, bestNA, ents, nhs)
+            if r is not None:
+                db.addUnicastRoute(r)
 
         for (label, node), res in zip(label_to_node.items(), sel[len(uni):]):
             if node == me:

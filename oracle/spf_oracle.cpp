@@ -26,6 +26,7 @@
 //  reference's own test expectations (tests/golden/, tests/test_oracle_*.py).
 // ============================================================================
 #include <algorithm>
+#include <deque>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -1135,6 +1136,162 @@ const char* orc_ls_nexthops_json(orc_ls* p, const char* me_c, const char* const*
   for (const auto& r : rows) {
     if (!first) o += ',';
     first = false;
+    o += r;
+  }
+  o += "]}";
+  return o.c_str();
+}
+
+// ---- SR_MPLS next hops (one area) --------------------------------------------
+// For `me` and the best advertiser set `dsts` (already drained-filtered) of
+// one SR_MPLS prefix, prepend[i] = prependLabel of dsts[i]'s entry (< 0 none):
+//   algo 0 -> selectBestPathsSpf with perDestination = true
+//             (Decision.cpp:829-893): self removed when it carries a prepend
+//             label, getNextHopsWithMetric keyed (neighbour, dst) (:1107-1196),
+//             getNextHopsThrift push labels [prepend?, dst node label if the
+//             dst is not the neighbour] (:1198-1305);
+//   algo 1 -> selectBestPathsKsp2 (:895-1018): k = 1 paths to every dst but
+//             me, k = 2 paths not containing a k = 1 path (pathAInPathB,
+//             LinkState.h:395-410), label stack of the path's node labels
+//             minus the first hop (PHP) with the prepend label at the bottom.
+// Output JSON: {"nh": [[ifName, metric(i32), neighbour, addrHex,
+//                       action|null, [push labels]|null], ...]} (sorted)
+static bool pathAInPathB(const orc::Path& a, const orc::Path& b) {
+  if (a.size() > b.size()) return false;
+  for (size_t i = 0; i < b.size() - a.size() + 1; ++i) {
+    size_t ai = 0, bi = i;
+    while (ai < a.size() && a[ai] == b[bi]) {
+      ++ai;
+      ++bi;
+    }
+    if (ai == a.size()) return true;
+  }
+  return false;
+}
+static bool labelValid(int64_t l) { return (l & ~int64_t(0xFFFFF)) == 0; }
+static std::string srRow(const orc::Link& l, const std::string& me, orc::Metric metric, int v4,
+                         const std::vector<int32_t>& push) {
+  std::string r = "[";
+  json_str(r, l.ifaceFrom(me));
+  r += "," + std::to_string((int32_t)metric) + ",";
+  json_str(r, l.other(me));
+  r += ",";
+  json_str(r, hexOf(v4 ? l.v4From(me) : l.v6From(me)));
+  if (push.empty()) {
+    r += ",null,null]";
+  } else {
+    r += ",\"PUSH\",[";
+    for (size_t i = 0; i < push.size(); ++i) r += (i ? "," : "") + std::to_string(push[i]);
+    r += "]]";
+  }
+  return r;
+}
+const char* orc_ls_sr_nexthops_json(orc_ls* p, const char* me_c, const char* const* dsts_c,
+                                    const int64_t* prepend, uint32_t n_dsts, int lfa, int v4,
+                                    int algo) {
+  const orc::LinkState& ls = p->ls;
+  const std::string me(me_c);
+  std::map<std::string, int64_t> pre;  // dst -> prepend label (-1 none)
+  for (uint32_t i = 0; i < n_dsts; ++i) pre[dsts_c[i]] = prepend ? prepend[i] : -1;
+  auto nodeLabel = [&](const std::string& n) -> int32_t { return ls.dbs().at(n).nodeLabel; };
+  std::set<std::string> rows;
+  if (algo == 1) {
+    std::vector<orc::Path> paths;
+    for (const auto& kv : pre) {
+      if (kv.first == me) continue;
+      for (const auto& path : ls.kthPaths(me, kv.first, 1)) paths.push_back(path);
+    }
+    const size_t first = paths.size();
+    for (const auto& kv : pre) {
+      for (const auto& sec : ls.kthPaths(me, kv.first, 2)) {
+        bool add = true;
+        for (size_t i = 0; i < first && add; ++i)
+          if (pathAInPathB(paths[i], sec)) add = false;
+        if (add) paths.push_back(sec);
+      }
+    }
+    for (const auto& path : paths) {
+      orc::Metric cost = 0;
+      std::deque<int32_t> labels;
+      std::string nxt = me;
+      for (const auto& l : path) {
+        cost += l->metricFrom(nxt);
+        nxt = l->other(nxt);
+        labels.push_front(nodeLabel(nxt));
+      }
+      labels.pop_back();
+      const int64_t pl = pre.at(nxt);
+      if (pl >= 0) labels.push_front((int32_t)pl);
+      rows.insert(srRow(*path.front(), me, cost, v4,
+                        std::vector<int32_t>(labels.begin(), labels.end())));
+    }
+  } else {
+    std::set<std::string> dstSet;
+    for (const auto& kv : pre) dstSet.insert(kv.first);
+    if (dstSet.count(me) && pre.at(me) >= 0) dstSet.erase(me);
+    const auto& mine = ls.getSpfResult(me, true);
+    orc::Metric shortest = std::numeric_limits<orc::Metric>::max();
+    std::set<std::string> minCost;
+    for (const auto& d : dstSet) {
+      auto it = mine.find(d);
+      if (it == mine.end()) continue;
+      if (shortest >= it->second.metric) {
+        if (shortest > it->second.metric) {
+          shortest = it->second.metric;
+          minCost.clear();
+        }
+        minCost.insert(d);
+      }
+    }
+    std::map<std::pair<std::string, std::string>, orc::Metric> nh;
+    for (const auto& d : minCost)
+      for (const auto& n : mine.at(d).nextHops) nh[{n, d}] = shortest - mine.at(n).metric;
+    if (lfa && !minCost.empty()) {
+      for (const auto& l : ls.linksFrom(me)) {
+        if (!l->isUp()) continue;
+        const std::string& nb = l->other(me);
+        const auto& fromNb = ls.getSpfResult(nb, true);
+        const orc::Metric back = fromNb.at(me).metric;
+        for (const auto& d : dstSet) {
+          auto it = fromNb.find(d);
+          if (it == fromNb.end()) continue;
+          if (it->second.metric < shortest + back) {
+            auto f = nh.find({nb, d});
+            if (f == nh.end()) nh.emplace(std::make_pair(nb, d), it->second.metric);
+            else if (f->second > it->second.metric) f->second = it->second.metric;
+          }
+        }
+      }
+    }
+    for (const auto& l : ls.linksFrom(me)) {
+      const std::string& nb = l->other(me);
+      for (const auto& d : dstSet) {
+        auto f = nh.find({nb, d});
+        if (f == nh.end() || !l->isUp()) continue;
+        if (dstSet.count(nb) && nb != d) continue;
+        const orc::Metric over = l->metricFrom(me) + f->second;
+        if (!lfa && over != shortest) continue;
+        std::vector<int32_t> push;
+        bool ok = true;
+        if (pre.at(d) >= 0) {
+          push.push_back((int32_t)pre.at(d));
+          ok &= labelValid(pre.at(d));
+        }
+        if (ok && d != nb) {
+          push.push_back(nodeLabel(d));
+          ok &= labelValid(nodeLabel(d));
+        }
+        if (!ok) continue;
+        rows.insert(srRow(*l, me, over, v4, push));
+      }
+    }
+  }
+  std::string& o = p->scratch;
+  o = "{\"nh\":[";
+  bool firstRow = true;
+  for (const auto& r : rows) {
+    if (!firstRow) o += ',';
+    firstRow = false;
     o += r;
   }
   o += "]}";

@@ -17,6 +17,20 @@ class _Replay:
             getattr(other, op)(arg)
         return other
 
+    def node_names(self) -> List[str]:
+        """Nodes with a database, from the update history."""
+        names: Dict[str, None] = {}
+        for op, arg in self.history:
+            if op == "update":
+                for d in arg:
+                    names[d.thisNodeName] = None
+            elif op == "update_packed":
+                for o, n in zip(arg.dbs["name_off"], arg.dbs["name_len"]):
+                    names[bytes(arg.blob[o: o + n]).decode()] = None
+            elif op == "delete":
+                names.pop(arg, None)
+        return sorted(names)
+
 
 class OracleAdapter(_Replay):
     def __init__(self) -> None:
@@ -75,6 +89,31 @@ class OracleAdapter(_Replay):
             if r["nh"]:
                 out[f"label:{x}"] = sorted(r["nh"], key=str)
         return out
+
+
+    def ksp2_routes(self, me, v4, lfa=True) -> Dict[str, list]:
+        """{dst: rows} of every other node's SR_MPLS + KSP2_ED_ECMP loopback:
+        the restated selectBestPathsKsp2 (Decision.cpp:895-1018)."""
+        from oracle import sr_nexthops
+
+        out = {}
+        for x in self.node_names():
+            if x == me or x not in self.spf(me):
+                continue
+            rows = sr_nexthops(self.ls, me, {x: None}, lfa, v4, True)
+            if rows:
+                out[x] = sorted(rows, key=str)
+        return out
+
+    def ksp2_route_build(self, me, lfa=True) -> None:
+        """The SPF work of buildRouteDb(me) with every node advertising a
+        KSP2_ED_ECMP loopback: KSP2 next hops + node-label routes."""
+        from oracle import nexthops
+
+        self.ksp2_routes(me, False, lfa)
+        for x in self.node_names():
+            if x != me:
+                nexthops(self.ls, me, [x], lfa, False, 1)
 
 
 class ProductAdapter(_Replay):
@@ -152,6 +191,44 @@ class ProductAdapter(_Replay):
             if r is not None:
                 out[f"label:{x}"] = rows(r.nexthops)
         return out
+
+
+def _ksp2_db(ls, me, v4, lfa):
+    from openr_amd.spf_solver import PrefixEntry, PrefixState, SpfSolver
+
+    ps = PrefixState()
+    pfx = {}
+    names = sorted(ls.getAdjacencyDatabaseLabels())
+    for i, x in enumerate(names):
+        pfx[x] = f"10.0.{i // 250}.{i % 250 + 1}/32" if v4 else f"fc00::{i + 1:x}/128"
+        ps.updatePrefix(x, ls.getArea(), PrefixEntry(pfx[x], forwardingType="SR_MPLS",
+                                                     forwardingAlgorithm="KSP2_ED_ECMP"))
+    return SpfSolver(me, True, lfa).buildRouteDb(me, {ls.getArea(): ls}, ps), pfx
+
+
+def _ksp2_methods(cls):
+    def ksp2_routes(self, me, v4, lfa=True):
+        db, pfx = _ksp2_db(self.ls, me, v4, lfa)
+        out = {}
+        for x, p in pfx.items():
+            r = db.unicastRoutes.get(p)
+            if x == me or r is None or not r.nexthops:
+                continue
+            out[x] = sorted(([n.ifName, n.metric, n.neighborNodeName, n.address.hex(),
+                              n.mplsAction.action if n.mplsAction else None,
+                              list(n.mplsAction.pushLabels) if n.mplsAction else None]
+                             for n in r.nexthops), key=str)
+        return out
+
+    def ksp2_route_build(self, me, lfa=True):
+        _ksp2_db(self.ls, me, False, lfa)
+
+    cls.ksp2_routes = ksp2_routes
+    cls.ksp2_route_build = ksp2_route_build
+    return cls
+
+
+_ksp2_methods(ProductAdapter)
 
 
 class HostOnlyProductAdapter(ProductAdapter):

@@ -393,6 +393,79 @@ cases.append({
                 "cite": "DecisionTest.cpp:3386-3528"}],
 })
 
+# ---------------- KSP2_ED_ECMP routes (DecisionTest.cpp) ----------------
+# Every node advertises its loopback as SR_MPLS + KSP2_ED_ECMP
+# (createPrefixDbWithKspfAlgo, DecisionTest.cpp:161-197); rows
+# [ifName, metric, neighbour, addrHex, "PUSH"|None, [push labels]|None].
+
+
+def ksp2_hop(D, adj, metric, push, v4):
+    a = D[adj]
+    return [a.ifName, metric, a.otherNodeName, (a.nextHopV4 if v4 else a.nextHopV6).hex(),
+            "PUSH" if push else None, push]
+
+
+def ksp2_routes(D, spec, v4):
+    return {me: {dst: sorted((ksp2_hop(D, a, m, push, v4) for a, m, push in hops), key=str)
+                 for dst, hops in dsts.items()}
+            for me, dsts in spec.items()}
+
+
+RING_KSP2 = {
+    "1": {"4": [("adj12", 20, [4]), ("adj13", 20, [4])],
+          "3": [("adj13", 10, None), ("adj12", 30, [3, 4])],
+          "2": [("adj12", 10, None), ("adj13", 30, [2, 4])]},
+    "2": {"4": [("adj24", 10, None), ("adj21", 30, [4, 3])],
+          "3": [("adj21", 20, [3]), ("adj24", 20, [3])],
+          "1": [("adj21", 10, None), ("adj24", 30, [1, 3])]},
+    "3": {"4": [("adj34", 10, None), ("adj31", 30, [4, 2])],
+          "2": [("adj31", 20, [2]), ("adj34", 20, [2])],
+          "1": [("adj31", 10, None), ("adj34", 30, [1, 2])]},
+    "4": {"3": [("adj43", 10, None), ("adj42", 30, [3, 1])],
+          "2": [("adj42", 10, None), ("adj43", 30, [2, 1])],
+          "1": [("adj42", 20, [1]), ("adj43", 20, [1])]},
+}
+for v4 in (False, True):
+    cases.append({
+        "name": f"decision_ring_ksp2_routes_{'v4' if v4 else 'v6'}",
+        "cite": "DecisionTest.cpp:2290-2476 (SimpleRingTopologyFixture, Ksp2EdEcmp)",
+        "steps": ring_steps,
+        "checks": [{"type": "ksp2_routes", "v4": v4, "expect": ksp2_routes(R, RING_KSP2, v4),
+                    "cite": "DecisionTest.cpp:2328-2470"},
+                   {"type": "ksp2_route_build_spf_runs", "nodes": ["1", "2", "3", "4"],
+                    "expect": 16, "cite": "DecisionTest.cpp:2302-2303"}],
+    })
+
+M = dict(R)
+M["adj14"] = create_adjacency("4", "1/4", "4/1", "fe80::4", "192.168.0.4", 10, 100004)
+M["adj41"] = create_adjacency("1", "4/1", "1/4", "fe80::1", "192.168.0.1", 10, 100001)
+mesh = [create_adj_db("1", [M["adj12"], M["adj13"], M["adj14"]], 1),
+        create_adj_db("2", [M["adj21"], M["adj23"], M["adj24"]], 2),
+        create_adj_db("3", [M["adj31"], M["adj32"], M["adj34"]], 3),
+        create_adj_db("4", [M["adj41"], M["adj42"], M["adj43"]], 4)]
+mesh3_drained = create_adj_db("3", [M["adj31"], M["adj32"], M["adj34"]], 3)
+mesh3_drained.isOverloaded = True
+MESH_KSP2 = {"1": {"4": [("adj14", 10, None), ("adj12", 20, [4]), ("adj13", 20, [4])],
+                   "3": [("adj13", 10, None), ("adj12", 20, [3]), ("adj14", 20, [3])],
+                   "2": [("adj12", 10, None), ("adj13", 20, [2]), ("adj14", 20, [2])]}}
+MESH_KSP2_DRAINED = {"1": {"4": [("adj14", 10, None), ("adj12", 20, [4])]}}
+for v4 in (False, True):
+    cases.append({
+        "name": f"decision_mesh_ksp2_routes_{'v4' if v4 else 'v6'}",
+        "cite": "DecisionTest.cpp:1607-1675 (SimpleRingMeshTopologyFixture, Ksp2EdEcmp)",
+        "steps": [
+            {"update": [db_json(d) for d in mesh],
+             "checks": [{"type": "ksp2_routes", "v4": v4,
+                         "expect": ksp2_routes(M, MESH_KSP2, v4),
+                         "cite": "DecisionTest.cpp:1640-1660"}]},
+            {"update": [db_json(mesh3_drained)], "expect_change": [[True, False, False]],
+             "checks": [{"type": "ksp2_routes", "v4": v4,
+                         "expect": ksp2_routes(M, MESH_KSP2_DRAINED, v4),
+                         "cite": "DecisionTest.cpp:1665-1674"}]},
+        ],
+        "checks": [],
+    })
+
 out = HERE / "reference_expectations.json"
 out.write_text(json.dumps({"source": "fredxia/openr openr/decision/tests", "cases": cases},
                           indent=1, sort_keys=False))

@@ -233,3 +233,22 @@ def nexthops(orc: "OracleLinkState", me: str, dsts: Sequence[str], lfa: bool = F
     raw = lib.orc_ls_nexthops_json(orc._h, me.encode(), arr, len(dsts), int(lfa), int(v4),
                                    -1 if swap_label is None else swap_label)
     return json.loads(raw)
+
+
+lib.orc_ls_sr_nexthops_json.restype = C.c_char_p
+lib.orc_ls_sr_nexthops_json.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_char_p),
+                                        C.POINTER(C.c_int64), C.c_uint32, C.c_int, C.c_int,
+                                        C.c_int]
+
+
+def sr_nexthops(orc: "OracleLinkState", me: str, dsts: Dict[str, Optional[int]], lfa: bool,
+                v4: bool, ksp2: bool) -> List[list]:
+    """SR_MPLS next hops of one prefix (Decision.cpp:829-1018): `dsts` maps
+    each best advertiser to its entry's prependLabel.  Sorted rows [ifName,
+    metric, neighbour, addrHex, "PUSH"|None, [labels]|None]."""
+    names = sorted(dsts)
+    arr = (C.c_char_p * max(1, len(names)))(*[d.encode() for d in names])
+    pre = (C.c_int64 * max(1, len(names)))(*[-1 if dsts[d] is None else dsts[d] for d in names])
+    raw = lib.orc_ls_sr_nexthops_json(orc._h, me.encode(), arr, pre, len(names), int(lfa),
+                                      int(v4), int(ksp2))
+    return json.loads(raw)["nh"]

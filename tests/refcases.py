@@ -173,5 +173,16 @@ def _check(chk: dict, ad, dbs, case) -> None:
             got = ad.routes(me, chk["lfa"], chk["v4"], labels)
             for key, rows in exp.items():
                 assert got.get(key) == sorted(rows, key=str), (where, me, key, got.get(key), rows)
+    elif t == "ksp2_routes":
+        for me, exp in chk["expect"].items():
+            got = ad.ksp2_routes(me, chk["v4"])
+            for dst, rows in exp.items():
+                assert got.get(dst) == rows, (where, me, dst, got.get(dst), rows)
+    elif t == "ksp2_route_build_spf_runs":
+        fresh = ad.fresh()
+        before = fresh.spf_runs()
+        for n in chk["nodes"]:
+            fresh.ksp2_route_build(n)
+        assert fresh.spf_runs() - before == chk["expect"], (where, fresh.spf_runs() - before)
     else:
         raise AssertionError(f"unknown check {t}")
