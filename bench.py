@@ -98,6 +98,16 @@ class AllSources:
         n, e = self.n, self.e
         self.bytes_launch = int(n * (4 * (n + 1) + 8 * e + n + 4 * n)
                                 + n * int(np.sum((nbr + 7) // 8)))
+        # the kernels the plan runs: multi-source BFS for unit metrics
+        # (N <= 16384), per-source SSSP otherwise
+        unit = bool(np.all(met == 1)) and n <= 16384
+        self.kernels = ("msbfs_kernel" if unit else "sssp_kernel", "ecmp_kernel")
+        # compulsory HBM traffic of one pass: the outputs (dist rows, next-hop
+        # bitmaps) plus, on the BFS path, the u8 narrow rows written once and
+        # read at least once
+        npitch = (n + 1023) // 1024 * 1024
+        self.floor_launch = int(n * eng.pitch * 4 + self.plan.nh_words * 4
+                                + (2 * n * npitch if unit else 0))
         self.parallelism = (f"source-sharded over {world} rank(s): one LSDB snapshot per rank, "
                             "no data-path collective")
 
@@ -109,7 +119,7 @@ class AllSources:
 
     def kernel_ms(self):
         a, b, cnt = self.plan.timing()
-        return {"sssp_kernel": a / max(cnt, 1), "ecmp_kernel": b / max(cnt, 1)}
+        return {self.kernels[0]: a / max(cnt, 1), "ecmp_kernel": b / max(cnt, 1)}
 
     def edges_per_unit(self) -> int:
         return self.e
@@ -427,6 +437,12 @@ def main() -> None:
         },
         "cpu_baseline": None,
     }
+    floor = getattr(wl, "floor_launch", None)
+    if floor:
+        # the outputs alone over the same launch time: how far the pass is
+        # from the bytes it must move whatever the algorithm
+        out["roofline"]["compulsory_bytes_per_launch"] = floor
+        out["roofline"]["compulsory_frac"] = floor / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
     if isinstance(wl, WhatIfAllLinks):
         out["config"]["hot_failures_per_rank"] = wl.n_hot
         out["config"]["workgroup_team_failures_per_rank"] = wl.n_big
