@@ -88,7 +88,8 @@ struct spf_plan {
   std::vector<uint32_t> words;
   uint64_t nh_total = 0;
   bool direct = false;  // closure == srcs: D is the caller's dist buffer
-  bool ms = false;      // unit metrics: multi-source BFS + u8 narrow copy
+  bool ms = false;      // unit metrics: multi-source BFS
+  bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
   spfi::DevBuf<uint8_t> d_Dn;
   spfi::DevBuf<uint64_t> d_nh_off;

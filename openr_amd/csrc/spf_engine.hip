@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
         const uint32_t s = __ffsll((unsigned long long)m) - 1;
         if ((nv[i] >> s) & 1ull) {
           D[(size_t)(row0 + s) * pitch + v] = L;
-          Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
+          if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
         }
       }
     }
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const uint32_t v = tid + i * kMsThreads;
       if (v < N && !((vis[i] >> s) & 1ull)) {
         drow[v] = kInf;
-        nrow[v] = 0xFF;
+        if (Dn) nrow[v] = 0xFF;
       }
     }
   }
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
     for (uint32_t v = N + tid; v < npitch; v += kMsThreads) {
       if (v < pitch) drow[v] = kInf;
-      nrow[v] = 0xFF;
+      if (Dn) nrow[v] = 0xFF;
     }
   }
   MS_STAMP();
@@ -562,31 +562,42 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
       match_group(j0 + kEcmpUnroll, rb);
     }
   } else {
-    // exact rows: 16 ballots over destinations cbase + q*64 + lane, four
-    // at a time (both rows' loads in flight); lane t < 32 stores word t
-    const uint32_t* Ds = D + (size_t)srow * pitch;
+    // exact u32 rows ("wide"): lane l holds the source's distances of
+    // destinations cbase + 16l .. +15 in registers and, per neighbour, compares
+    // four 16-byte loads of the neighbour's row: bit k set iff
+    // d_x(v) + w(s, x) == d_s(v) (d_x finite; then the sum stays below kInf).
+    // Same 16-bit lane stores as the narrow path.
+    const bool st = cbase / 16 + lane < pitch / 16;
+    uint32_t b[16];
+    {
+      const uint4* Ds = reinterpret_cast<const uint4*>(D + (size_t)srow * pitch + cbase) + lane * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 t = st ? Ds[q] : make_uint4(kInf, kInf, kInf, kInf);
+        b[4 * q] = t.x;
+        b[4 * q + 1] = t.y;
+        b[4 * q + 2] = t.z;
+        b[4 * q + 3] = t.w;
+      }
+    }
     for (uint32_t j = 0; j < k; ++j) {
       const uint32_t oj = offs[j], wj = hop ? 1u : nb_w[nb0 + j];
-      uint32_t word = 0;
-      if (oj != dead) {
+      uint32_t m = 0;
+      if (oj != dead && st) {
         const uint32_t rj = NARROW ? oj / npitch : oj;
-        const uint32_t* Dx = D + (size_t)rj * pitch;
+        const uint4* Dx = reinterpret_cast<const uint4*>(D + (size_t)rj * pitch + cbase) + lane * 4;
+        uint4 t[4];
 #pragma unroll
-        for (int q0 = 0; q0 < 16; q0 += 4) {
-          uint32_t a[4], b[4];
+        for (int q = 0; q < 4; ++q) t[q] = Dx[q];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const uint32_t v = cbase + (q0 + u) * 64 + lane;
-            a[u] = v < N ? Dx[v] : kInf;
-            b[u] = v < N ? Ds[v] : kInf;
-          }
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t a[4] = {t[q].x, t[q].y, t[q].z, t[q].w};
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            word = put_mask(word, __ballot(a[u] != kInf && b[u] != kInf && a[u] + wj == b[u]),
-                            q0 + u, lane);
+          for (int e = 0; e < 4; ++e)
+            m |= (uint32_t)(a[e] != kInf && a[e] + wj == b[4 * q + e]) << (4 * q + e);
         }
       }
-      if (lane < 32 && cbase / 32 + lane < wpm) out_w[(size_t)j * wpm + lane] = word;
+      if (st) reinterpret_cast<uint16_t*>(out_w + (size_t)j * wpm)[lane] = (uint16_t)m;
     }
   }
   // drained neighbour x: its bitmap is empty except, possibly, x itself --
@@ -940,6 +951,19 @@ spf_status spf_src_neighbors(const spf_ctx* c, uint32_t src, uint32_t* out,
 
 namespace {
 
+// u8 narrow rows for the next-hop pass: 4x fewer bytes per neighbour row
+// read, paid for by a second store per (source, slice, level) in the BFS.
+// Worth it when next-hop work (sum of neighbour counts) outweighs the BFS
+// store work, which grows with the number of levels: dense fabrics (degree
+// ~23, 5 levels) yes, grids (degree 4, 198 levels) no.  SPF_NARROW=0/1
+// overrides (experiments).
+bool use_narrow(const spf_ctx* c, const spf_plan* p) {
+  if (const char* e = std::getenv("SPF_NARROW")) return e[0] == '1';
+  uint64_t nb = 0;
+  for (uint32_t i = 0; i < p->n_src; ++i) nb += p->words[i];
+  return nb >= 8ull * p->n_src;  // average distinct degree >= 8
+}
+
 // Everything a plan derives from the graph's current state (closure over
 // non-drained neighbours, narrow/exact mode, next-hop row tables).  Run at
 // creation and again by spf_plan_execute after an in-place graph patch
@@ -1015,17 +1039,18 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
+  p->narrow = p->ms && use_narrow(c, p);
   {
     // per-source neighbour rows for the next-hop pass (kInf = drained)
     std::vector<uint32_t> nb_row, nb_row_off(n_src), nb_drained(n_src, 0);
-    const uint32_t dead = p->ms ? (uint32_t)p->closure.size() * c->npitch : kInf;
+    const uint32_t dead = p->narrow ? (uint32_t)p->closure.size() * c->npitch : kInf;
     p->dead = dead;
     for (uint32_t i = 0; i < n_src; ++i) {
       nb_row_off[i] = (uint32_t)nb_row.size();
       for (uint32_t e = c->nb_ptr[srcs[i]]; e < c->nb_ptr[srcs[i] + 1]; ++e) {
         const uint32_t x = c->nb_id[e];
         const bool dr = c->ovl[x] != 0;
-        nb_row.push_back(dr ? dead : p->ms ? row_of[x] * c->npitch : row_of[x]);
+        nb_row.push_back(dr ? dead : p->narrow ? row_of[x] * c->npitch : row_of[x]);
         nb_drained[i] += dr;
       }
       const size_t k = nb_row.size() - nb_row_off[i];
@@ -1072,7 +1097,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     return fail(c, SPF_E_UNSUPPORTED,
                 "batched plans keep a distance row per source in LDS: %u nodes do not fit "
                 "(single-source spf_sssp and what-if batches handle large graphs)", N);
-  if (p->ms) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
+  if (p->narrow) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
     HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
     HIP_TRY(c, hipMemsetAsync(p->d_Dn.p + p->closure.size() * c->npitch, 0xFF, c->npitch, c->stream));
   }
@@ -1276,12 +1301,12 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     ++p->timing_n;
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
-  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->d_Dn.p, s)
+  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr, s)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   if (p->nh_total) {
-    st = p->ms ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
+    st = p->narrow ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
                : launch_ecmp<false>(c, p, nullptr, D, hop, d_nh, s);
     if (st != SPF_OK) return st;
   }

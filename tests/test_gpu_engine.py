@@ -122,3 +122,28 @@ def test_zero_metric_is_rejected_loudly():
     with pytest.raises(UnsupportedInput):
         eng.solve([0])
     eng.solve([0], hop=True)  # hop counts ignore metrics: fine
+
+
+@pytest.mark.parametrize("narrow", ["0", "1"])
+@pytest.mark.parametrize("name,make", [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("grid12", lambda: T.grid(12)),
+    ("rand_drained", lambda: T.random_graph(60, 150, 7, max_metric=1, overload_frac=0.15)),
+], ids=["fabric", "grid", "rand"])
+def test_next_hop_pass_both_row_widths(name, make, narrow, monkeypatch):
+    """The BFS plans' next-hop pass on u8 narrow rows and on the exact u32 rows
+    (the plan picks one by average degree; SPF_NARROW forces it)."""
+    monkeypatch.setenv("SPF_NARROW", narrow)
+    names, eng, orc = load(make())
+    compare(names, eng, orc, list(range(len(names))), hop=True)
+
+
+def test_saturated_narrow_rows_fall_back_to_exact(monkeypatch):
+    """Hop distances >= 254 saturate the u8 copy: those waves decide on the
+    u32 rows.  A 700-node ring has distances up to 350."""
+    monkeypatch.setenv("SPF_NARROW", "1")
+    topo = T.wan(700, 0, seed=1)  # ring only
+    names, eng, orc = load(topo)
+    rng = np.random.default_rng(5)
+    compare(names, eng, orc, sorted(int(x) for x in rng.choice(len(names), 40, replace=False)),
+            hop=True)
