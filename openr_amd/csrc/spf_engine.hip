@@ -235,6 +235,7 @@ constexpr uint32_t kMsBatch = 64;
 constexpr int kMsMaxOwn = 16;
 constexpr uint32_t kMsMaxNodes = kMsThreads * kMsMaxOwn;  // 16384 (F: 128 KiB of LDS)
 constexpr int kMsUnroll = 8;
+constexpr uint32_t kMsLaneStoreRatio = 4;  // per-lane stores when 4 * max per-node count < #sources
 constexpr uint32_t kSliceW = 64;  // nodes per sliced-ELL slice (= wave width)
 
 // Narrow (u8) distance rows: npitch bytes (a multiple of 1024), node v at
@@ -326,6 +327,29 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
       uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
       const uint32_t v = tid + i * kMsThreads;
+      // Two ways to cover the (source, node) pairs of the slice: one
+      // coalesced store per source (row-major; best when a source discovers
+      // many nodes of the slice at once -- dense fabrics), or each lane
+      // walking its own new sources (scattered stores; best when every source
+      // discovers a node or two per level -- grids, rings).  Trip counts:
+      // #sources vs the largest per-node count.
+      const uint32_t nsrc = (uint32_t)__popcll(((uint64_t)mhi << 32) | mlo);
+      uint32_t maxpop = (uint32_t)__popcll(nv[i]);
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) maxpop = max(maxpop, (uint32_t)__shfl_xor((int)maxpop, d, 64));
+      maxpop = __builtin_amdgcn_readfirstlane(maxpop);
+      if (maxpop * kMsLaneStoreRatio < nsrc) {
+        uint64_t m = nv[i];
+        for (uint32_t it = 0; it < maxpop; ++it) {
+          if (m) {
+            const uint32_t s = __ffsll((unsigned long long)m) - 1;
+            D[(size_t)(row0 + s) * pitch + v] = L;
+            if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
+            m &= m - 1;
+          }
+        }
+        continue;
+      }
       for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
         const uint32_t s = __ffsll((unsigned long long)m) - 1;
         if ((nv[i] >> s) & 1ull) {
