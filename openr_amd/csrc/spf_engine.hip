@@ -253,10 +253,14 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-template <int OWN>
+//   LCOL: the sliced-ELL columns are staged once in LDS as u16 (when they fit
+//   beside F -- low-degree graphs such as grids), so the pull sweep issues no
+//   global loads: no vmcnt wait, and a level's stores drain in the background
+//   instead of stalling the next sweep's first column load.
+template <int OWN, bool LCOL>
 __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
-    const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
+    uint32_t n_col, const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
     uint32_t n_rows, uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch,
     uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
     unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
@@ -265,6 +269,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   uint32_t* o_node = reinterpret_cast<uint32_t*>(F + N + 1);   // [64] drained batch sources
   uint32_t* o_cnt = o_node + kMsBatch;                         // [1]
   uint32_t* flag = o_cnt + 1;                                  // [2] per-parity progress
+  uint16_t* lcol = reinterpret_cast<uint16_t*>(flag + 2);      // [n_col] (LCOL)
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t row0 = blockIdx.x * bs;  // bs <= 64 sources per workgroup
@@ -282,6 +287,8 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   MS_STAMP();
 
   for (uint32_t v = tid; v <= N; v += kMsThreads) F[v] = 0;
+  if (LCOL)
+    for (uint32_t t = tid; t < n_col; t += kMsThreads) lcol[t] = (uint16_t)sell_col[t];
   if (tid == 0) {
     *o_cnt = 0;
     flag[0] = flag[1] = 0;
@@ -369,6 +376,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const bool need = v < N && vis[i] != all;
       if (__ballot(need)) {  // wave-uniform: the slice has unfinished nodes
         const uint32_t* cp = sell_col + sb[i] + lane;
+        const uint16_t* lp = lcol + sb[i] + lane;
         const uint32_t w = sw[i];
         uint64_t acc = 0;
         for (uint32_t j = 0; j < w; j += kMsUnroll) {
@@ -376,7 +384,8 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
           // padding index N reads F[N] = 0
           uint32_t c[kMsUnroll];
 #pragma unroll
-          for (int u = 0; u < kMsUnroll; ++u) c[u] = j + u < w ? cp[(j + u) * kSliceW] : N;
+          for (int u = 0; u < kMsUnroll; ++u)
+            c[u] = j + u < w ? (LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW]) : N;
 #pragma unroll
           for (int u = 0; u < kMsUnroll; ++u) acc |= F[c[u]];
         }
@@ -1211,19 +1220,27 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 
 namespace {
 
-size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 4); }
+size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 3); }
 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
                   hipStream_t s) {
+  const uint32_t n_col = c->sell_ptr.back();
+  const size_t lds = msbfs_lds_bytes(c->N), lds_col = lds + 2ull * n_col;
+  const bool lcol = lds_col <= kMaxLds;
   // one workgroup per CU per round: a batch costs one edge sweep per level
   // whatever its size, but its stores scale with it, so spread the sources
   // over every CU rather than fill 64-source batches on fewer CUs
   const uint32_t rounds = (rows + kMsBatch * c->n_cu - 1) / (kMsBatch * c->n_cu);
   const uint32_t bs = std::min<uint32_t>(kMsBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
-  hipLaunchKernelGGL((msbfs_kernel<OWN>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
-                     msbfs_lds_bytes(c->N), s, c->d_sell_ptr.p, c->d_sell_col.p, c->d_ovl.p,
-                     rows_src, rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
+  if (lcol)
+    hipLaunchKernelGGL((msbfs_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
+                       lds_col, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
+                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
+  else
+    hipLaunchKernelGGL((msbfs_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
+                       lds, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
+                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
@@ -1267,10 +1284,9 @@ spf_status set_lds_limits(spf_ctx* c) {
   if (done) return SPF_OK;
   const void* fns[] = {(const void*)sssp_kernel<uint16_t, true>, (const void*)sssp_kernel<uint16_t, false>,
                        (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>,
-                       (const void*)msbfs_kernel<1>, (const void*)msbfs_kernel<2>,
-                       (const void*)msbfs_kernel<4>, (const void*)msbfs_kernel<8>,
-                       (const void*)msbfs_kernel<10>, (const void*)msbfs_kernel<12>,
-                       (const void*)msbfs_kernel<16>};
+#define MSB(o) (const void*)msbfs_kernel<o, false>, (const void*)msbfs_kernel<o, true>
+                       MSB(1), MSB(2), MSB(4), MSB(8), MSB(10), MSB(12), MSB(16)};
+#undef MSB
   for (const void* f : fns)
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
   done = true;
