@@ -98,16 +98,17 @@ class AllSources:
         n, e = self.n, self.e
         self.bytes_launch = int(n * (4 * (n + 1) + 8 * e + n + 4 * n)
                                 + n * int(np.sum((nbr + 7) // 8)))
-        # the kernels the plan runs: multi-source BFS for unit metrics
-        # (N <= 16384), per-source SSSP otherwise
-        unit = bool(np.all(met == 1)) and n <= 16384
-        self.kernels = ("msbfs_kernel" if unit else "sssp_kernel", "ecmp_kernel")
+        # the kernels the plan runs (multi-source BFS for unit metrics, one of
+        # two variants; per-source SSSP otherwise) and the next-hop row width
+        bfs, narrow = self.plan.kernels()
+        self.kernels = (bfs, "ecmp_kernel")
+        self.narrow = narrow
         # compulsory HBM traffic of one pass: the outputs (dist rows, next-hop
-        # bitmaps) plus, on the BFS path, the u8 narrow rows written once and
-        # read at least once
+        # bitmaps) plus the u8 narrow rows, when used, written once and read
+        # at least once
         npitch = (n + 1023) // 1024 * 1024
         self.floor_launch = int(n * eng.pitch * 4 + self.plan.nh_words * 4
-                                + (2 * n * npitch if unit else 0))
+                                + (2 * n * npitch if narrow else 0))
         self.parallelism = (f"source-sharded over {world} rank(s): one LSDB snapshot per rank, "
                             "no data-path collective")
 

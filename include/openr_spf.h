@@ -126,6 +126,12 @@ uint64_t spf_plan_nh_words(const spf_plan* plan);     /* total u32 words   */
 spf_status spf_plan_nh_layout(const spf_plan* plan, uint64_t* nh_off,
                               uint32_t* words);       /* n_src entries each */
 uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved */
+/* Which kernels the next execute runs (diagnostics, benchmarks):
+ * *bfs = 0 sssp_kernel (weighted, per source), 1 msbfs_kernel (64 sources per
+ * sweep, per-level stores), 2 msbfs_planes_kernel (32 sources, register bit
+ * planes, rows written once); *narrow = 1 when the next-hop pass reads u8 rows.
+ * No reference counterpart (engine introspection). */
+spf_status spf_plan_kernels(const spf_plan* plan, uint32_t* bfs, uint32_t* narrow);
 
 /* Execute on device buffers: d_dist = [n_src][pitch] u32, d_nh = nh words.
  * Enqueued on `stream` (a hipStream_t, NULL = the context's stream); no host

@@ -71,6 +71,8 @@ struct spf_ctx {
   uint32_t npitch = 0;                       // narrow (u8) row pitch
   std::vector<uint32_t> sell_ptr, sell_col;  // sliced-ELL columns (64-node slices)
   spfi::DevBuf<uint32_t> d_sell_ptr, d_sell_col;
+  std::vector<uint32_t> sell4_ptr, sell4;  // packed u16x4 columns (uint2 entries), planes BFS
+  spfi::DevBuf<uint32_t> d_sell4_ptr, d_sell4;
   spfi::DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
   spfi::DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds

@@ -379,15 +379,29 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
         const uint16_t* lp = lcol + sb[i] + lane;
         const uint32_t w = sw[i];
         uint64_t acc = 0;
-        for (uint32_t j = 0; j < w; j += kMsUnroll) {
-          // kMsUnroll column loads in flight; past the slice width the
-          // padding index N reads F[N] = 0
+        uint32_t j = 0;
+        // kMsUnroll column loads in flight, then the remainder in groups of
+        // 4, 2, 1 (w is wave-uniform: scalar branches, no F reads wasted on
+        // padding -- the LDS port is what bounds the sweep)
+        for (; j + kMsUnroll <= w; j += kMsUnroll) {
           uint32_t c[kMsUnroll];
 #pragma unroll
           for (int u = 0; u < kMsUnroll; ++u)
-            c[u] = j + u < w ? (LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW]) : N;
+            c[u] = LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW];
 #pragma unroll
           for (int u = 0; u < kMsUnroll; ++u) acc |= F[c[u]];
+        }
+#pragma unroll
+        for (int g = kMsUnroll / 2; g >= 1; g >>= 1) {
+          if (j + g <= w) {
+            uint32_t c[kMsUnroll / 2];
+#pragma unroll
+            for (int u = 0; u < g; ++u)
+              c[u] = LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW];
+#pragma unroll
+            for (int u = 0; u < g; ++u) acc |= F[c[u]];
+            j += g;
+          }
         }
         if (need) {
           nx[i] = acc & ~vis[i];
@@ -452,6 +466,175 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 }
 
 // ---------------------------------------------------------------------------
+//  1c. multi-source BFS with register-resident distances (bit planes)
+// ---------------------------------------------------------------------------
+// msbfs_kernel writes every (source, node) distance at the level it is found:
+// on a large-diameter graph (grid100: 198 levels) a 64-node slice of a source
+// row is found over dozens of levels, so its lines leave L2 partially written
+// again and again (PMC: 3.1 GB written for a 0.4 GB result).  This variant
+// keeps the distances on chip and writes each row once, coalesced:
+//   * <= 32 sources per workgroup, u32 masks (F in LDS is 4 B/node);
+//   * for every owned node, 8 bit planes: bit s of plane b = bit b of
+//     d(source s, node) -- a level L ORs the new mask into the planes of L's
+//     set bits (uniform branches, popcount(L) ORs per node);
+//   * at the end, per source, lane v assembles its distance from the planes
+//     and the wave stores 64 consecutive entries of the row (and of the u8
+//     copy when the next-hop pass reads narrow rows).
+// Planes hold 255 levels (a window); a search deeper than that flushes the
+// window, marks the entries found so far and starts the next window.
+// Register budget: 8 planes + visited + new per owned node = 10 VGPRs, so
+// OWN <= 10 (N <= 10240); the host picks msbfs_kernel otherwise.
+constexpr uint32_t kPlBatch = 32;
+constexpr int kPlanes = 8;
+constexpr uint32_t kPlWindow = (1u << kPlanes) - 1;  // relative levels 0..254, 255 = marker
+//   Columns: SELL-64 packed four u16 byte offsets (4 * id) per lane (uint2), every live slice
+//   at least one group wide (padding id N, F[N] == 0), staged in LDS when
+//   they fit.  Group 0 of all owned slices is straight-line code (a grid's
+//   whole sweep: one 8-byte column load and four F loads per node); lanes
+//   whose node is finished read F[N] (a broadcast).
+//   F is double-buffered: one barrier per level.
+
+template <int OWN, bool LCOL>
+__global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
+    const uint32_t* __restrict__ sell4_ptr, const uint2* __restrict__ sell4, uint32_t n4,
+    const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src, uint32_t n_rows,
+    uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch, uint32_t* __restrict__ D,
+    uint8_t* __restrict__ Dn) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint2* lcol = reinterpret_cast<uint2*>(smem);                   // [n4] (LCOL)
+  uint32_t* F0 = reinterpret_cast<uint32_t*>(smem + (LCOL ? 8ull * n4 : 0));  // [N + 1]
+  uint32_t* F1 = F0 + N + 1;                                      // [N + 1]
+  uint32_t* o_node = F1 + N + 1;                                  // [32] drained batch sources
+  uint32_t* o_cnt = o_node + kPlBatch;                            // [1]
+  uint32_t* flag = o_cnt + 1;                                     // [3] progress, L mod 3
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t row0 = blockIdx.x * bs;  // bs <= 32
+  const uint32_t nb = min(bs, n_rows - row0);
+  const uint32_t all = nb == 32 ? ~0u : ((1u << nb) - 1u);
+
+  for (uint32_t v = tid; v <= N; v += kMsThreads) F0[v] = F1[v] = 0;
+  if (LCOL)
+    for (uint32_t t = tid; t < n4; t += kMsThreads) lcol[t] = sell4[t];
+  if (tid == 0) {
+    *o_cnt = 0;
+    flag[0] = flag[1] = flag[2] = 0;
+  }
+  __syncthreads();
+  if (tid < nb) {
+    const uint32_t src = rows_src[row0 + tid];
+    F0[src] = 1u << tid;  // sources of a batch are distinct
+    if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
+  }
+  __syncthreads();
+  const uint32_t n_osrc = *o_cnt;
+
+  uint32_t vis[OWN], P[OWN][kPlanes];
+  uint32_t dslices = 0;  // bit i: owned slice i holds a drained node (wave-uniform)
+  uint32_t sb[OWN], sg[OWN];  // owned slice i: first packed entry, groups (wave-uniform)
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const uint32_t v = tid + i * kMsThreads;
+    vis[i] = v < N ? F0[v] : 0u;
+#pragma unroll
+    for (int b = 0; b < kPlanes; ++b) P[i][b] = 0u;
+    if (__ballot(v < N && ovl[v])) dslices |= 1u << i;
+    const uint32_t slice = (tid - lane + i * kMsThreads) / kSliceW;
+    const bool live = slice * kSliceW < N;
+    const uint32_t b = live ? sell4_ptr[slice] : 0u;
+    const uint32_t e = live ? sell4_ptr[slice + 1] : kSliceW;
+    sb[i] = __builtin_amdgcn_readfirstlane(b);
+    sg[i] = __builtin_amdgcn_readfirstlane((e - b) / kSliceW);
+  }
+
+  uint32_t base = 0;  // level of relative value 0 in the current window
+  for (uint32_t L = 1;; ++L) {
+    const uint32_t* Fc = (L & 1) ? F0 : F1;  // frontier of level L - 1
+    uint32_t* Fn = (L & 1) ? F1 : F0;        // frontier of level L
+    // opaque lane id, recomputed per level: hoisting the owned slices'
+    // addresses out of the level loop would spill
+    uint32_t ln = tid;
+    asm volatile("" : "+v"(ln));
+    ln &= 63u;
+    const uint32_t rel = L - base;  // relative level recorded in the planes
+    uint32_t any = 0;
+    const unsigned char* Fb = reinterpret_cast<const unsigned char*>(Fc);
+#define PL_F(off) (*reinterpret_cast<const uint32_t*>(Fb + (off)))
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const uint32_t v = tid + i * kMsThreads;
+      uint32_t nx = 0;
+      // a uniform branch per slice: skips finished slices and keeps the
+      // scheduler from hoisting ten slices' loads (register pressure).
+      // No per-lane masking: a finished node gets nx = 0 from ~vis, a node
+      // past N has only padding columns (F[N] == 0).
+      if (__ballot(vis[i] != all)) {
+        const uint2 q = LCOL ? lcol[sb[i] + ln] : sell4[sb[i] + ln];
+        uint32_t acc = PL_F(q.x & 0xFFFFu) | PL_F(q.x >> 16) | PL_F(q.y & 0xFFFFu) | PL_F(q.y >> 16);
+#pragma unroll 1
+        for (uint32_t g = 1; g < sg[i]; ++g) {  // wider slices: the remaining groups
+          const uint2 r = LCOL ? lcol[sb[i] + g * kSliceW + ln] : sell4[sb[i] + g * kSliceW + ln];
+          acc |= PL_F(r.x & 0xFFFFu) | PL_F(r.x >> 16) | PL_F(r.y & 0xFFFFu) | PL_F(r.y >> 16);
+        }
+        nx = acc & ~vis[i];
+        vis[i] |= nx;
+        any |= nx;
+#pragma unroll
+        for (int b = 0; b < kPlanes; ++b)
+          if ((rel >> b) & 1u) P[i][b] |= nx;
+      }
+      uint32_t f = nx;
+      if ((dslices >> i) & 1u) {  // the slice holds a drained node (uniform test)
+        if (v < N && ovl[v]) {    // drained: expands only as its own source
+          uint32_t own = 0;
+          for (uint32_t k = 0; k < n_osrc; ++k)
+            if ((o_node[k] & 0xFFFFFFu) == v) own = 1u << (o_node[k] >> 24);
+          f &= own;
+        }
+      }
+      if (v < N) Fn[v] = f;  // every level: the buffer still holds level L - 2
+    }
+#undef PL_F
+    // flag[L mod 3]: set during level L, read after its barrier; cleared
+    // during level L - 2 (its last reader finished before barrier L - 1)
+    if (any) flag[L % 3] = 1;
+    if (tid == 0) flag[(L + 1) % 3] = 0;
+    __syncthreads();
+    const bool done = !flag[L % 3];
+    if (done || rel == kPlWindow - 1) {
+      // Flush the window.  The first one writes every entry of the batch's
+      // rows (unreached = kInf, row padding); a later one (searches deeper
+      // than 254 levels) only the entries found in it -- entries of earlier
+      // windows carry the marker value kPlWindow in their planes.
+      const bool first = base == 0;
+      for (uint32_t s = 0; s < nb; ++s) {
+        uint32_t* drow = D + (size_t)(row0 + s) * pitch;
+        uint8_t* nrow = Dn ? Dn + (size_t)(row0 + s) * npitch : nullptr;
+#pragma unroll
+        for (int i = 0; i < OWN; ++i) {
+          const uint32_t v = tid + i * kMsThreads;
+          uint32_t r = 0;
+#pragma unroll
+          for (int b = 0; b < kPlanes; ++b) r |= ((P[i][b] >> s) & 1u) << b;
+          const bool seen = v < N && ((vis[i] >> s) & 1u);
+          const uint32_t d = seen ? base + r : kInf;
+          if (first || (seen && r != kPlWindow)) {
+            if (v < pitch) drow[v] = d;
+            if (nrow && v < npitch) nrow[v] = d == kInf ? 0xFFu : (uint8_t)min(d, 254u);
+          }
+        }
+      }
+      if (done) break;
+#pragma unroll
+      for (int i = 0; i < OWN; ++i)
+#pragma unroll
+        for (int b = 0; b < kPlanes; ++b) P[i][b] |= vis[i];
+      base += kPlWindow;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 //  2. next-hop (ECMP) pass
 // ---------------------------------------------------------------------------
 // Output: per source, one destination bitmap per distinct up neighbour x
@@ -490,12 +673,6 @@ __device__ __forceinline__ uint32_t eq_mask16(const uint4& a, const uint4& t) {
   x ^= d ^ (d << 3);
   d = (x ^ (x >> 6)) & 0x00CCu;
   return x ^ d ^ (d << 6);
-}
-
-// Lane t (< 32) of the wave keeps dword t of the 16 ballots (q = t / 2).
-__device__ __forceinline__ uint32_t put_mask(uint32_t out, uint64_t m, int q, uint32_t lane) {
-  const uint32_t pick = (lane & 1u) ? (uint32_t)(m >> 32) : (uint32_t)m;
-  return (lane >> 1) == (uint32_t)q ? pick : out;
 }
 
 // nb_row[nb_row_off[i] + j]: byte offset in Dn (row * npitch) of the narrow
@@ -877,6 +1054,36 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     }
     HIP_TRY(c, c->d_sell_ptr.upload(c->sell_ptr.data(), c->sell_ptr.size(), c->stream));
     HIP_TRY(c, c->d_sell_col.upload(c->sell_col.data(), c->sell_col.size(), c->stream));
+    // the same columns packed four u16 ids per lane (groups of 4 per slice,
+    // at least one), for msbfs_planes_kernel (N <= 10240)
+    c->sell4_ptr.assign(n_slices + 1, 0);
+    c->sell4.clear();
+    if (4ull * N < 65536) {
+      for (uint32_t sl = 0; sl < n_slices; ++sl) {
+        const uint32_t w = (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / kSliceW;
+        const uint32_t groups = std::max(1u, (w + 3) / 4);
+        c->sell4_ptr[sl + 1] = c->sell4_ptr[sl] + groups * kSliceW;
+      }
+      c->sell4.assign(2ull * c->sell4_ptr[n_slices], 0);
+      for (uint32_t sl = 0; sl < n_slices; ++sl) {
+        const uint32_t w = (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / kSliceW;
+        const uint32_t groups = (c->sell4_ptr[sl + 1] - c->sell4_ptr[sl]) / kSliceW;
+        for (uint32_t g = 0; g < groups; ++g)
+          for (uint32_t ln = 0; ln < kSliceW; ++ln) {
+            uint32_t id[4];
+            for (uint32_t k = 0; k < 4; ++k) {
+              const uint32_t j = 4 * g + k;
+              id[k] = j < w ? c->sell_col[c->sell_ptr[sl] + j * kSliceW + ln] : N;
+            }
+            const size_t e = 2ull * (c->sell4_ptr[sl] + g * kSliceW + ln);
+            // byte offsets into the BFS frontier array (4 B per node)
+            c->sell4[e] = 4 * id[0] | (4 * id[1] << 16);
+            c->sell4[e + 1] = 4 * id[2] | (4 * id[3] << 16);
+          }
+      }
+      HIP_TRY(c, c->d_sell4_ptr.upload(c->sell4_ptr.data(), c->sell4_ptr.size(), c->stream));
+      HIP_TRY(c, c->d_sell4.upload(c->sell4.data(), c->sell4.size(), c->stream));
+    }
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->loaded = true;
@@ -985,13 +1192,18 @@ spf_status spf_src_neighbors(const spf_ctx* c, uint32_t src, uint32_t* out,
 namespace {
 
 // u8 narrow rows for the next-hop pass: 4x fewer bytes per neighbour row
-// read, paid for by a second store per (source, slice, level) in the BFS.
-// Worth it when next-hop work (sum of neighbour counts) outweighs the BFS
-// store work, which grows with the number of levels: dense fabrics (degree
-// ~23, 5 levels) yes, grids (degree 4, 198 levels) no.  SPF_NARROW=0/1
-// overrides (experiments).
+// read, paid for by a second store per (source, slice, level) in
+// msbfs_kernel.  Worth it when next-hop work (sum of neighbour counts)
+// outweighs the BFS store work, which grows with the number of levels:
+// dense fabrics (degree ~23, 5 levels) yes; always with the register-plane
+// BFS (one coalesced store per row).  SPF_NARROW=0/1 overrides (experiments).
+bool use_planes(const spf_ctx* c);
+
 bool use_narrow(const spf_ctx* c, const spf_plan* p) {
   if (const char* e = std::getenv("SPF_NARROW")) return e[0] == '1';
+  // the register-plane BFS writes each row once, coalesced: the u8 copy
+  // costs one more row store and the next-hop pass reads 4x fewer bytes
+  if (use_planes(c)) return true;
   uint64_t nb = 0;
   for (uint32_t i = 0; i < p->n_src; ++i) nb += p->words[i];
   return nb >= 8ull * p->n_src;  // average distinct degree >= 8
@@ -1172,6 +1384,13 @@ void spf_plan_destroy(spf_plan* p) { delete p; }
 uint64_t spf_plan_nh_words(const spf_plan* p) { return p ? p->nh_total : 0; }
 uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->closure.size() : 0; }
 
+spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
+  if (!p || !bfs || !narrow) return SPF_E_INVALID;
+  *bfs = !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
+  *narrow = p->narrow ? 1u : 0u;
+  return SPF_OK;
+}
+
 spf_status spf_plan_nh_layout(const spf_plan* p, uint64_t* nh_off, uint32_t* words) {
   if (!p) return SPF_E_INVALID;
   for (uint32_t i = 0; i < p->n_src; ++i) {
@@ -1243,6 +1462,37 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
                        rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
 }
 
+size_t planes_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kPlBatch + 4); }
+
+template <int OWN>
+void planes_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
+                   hipStream_t s) {
+  const uint32_t n4 = c->sell4_ptr.back();
+  const size_t lds = planes_lds_bytes(c->N), lds_col = lds + 8ull * n4;
+  const bool lcol = lds_col <= kMaxLds;
+  const uint32_t rounds = (rows + kPlBatch * c->n_cu - 1) / (kPlBatch * c->n_cu);
+  const uint32_t bs = std::min<uint32_t>(kPlBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
+  const uint2* col4 = reinterpret_cast<const uint2*>(c->d_sell4.p);
+  if (lcol)
+    hipLaunchKernelGGL((msbfs_planes_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
+                       lds_col, s, c->d_sell4_ptr.p, col4, n4, c->d_ovl.p, rows_src, rows, bs, c->N,
+                       c->pitch, c->npitch, D, Dn);
+  else
+    hipLaunchKernelGGL((msbfs_planes_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
+                       lds, s, c->d_sell4_ptr.p, col4, n4, c->d_ovl.p, rows_src, rows, bs, c->N,
+                       c->pitch, c->npitch, D, Dn);
+}
+
+// Which BFS variant: the register-plane kernel needs N <= 10240; it wins
+// when levels are many (partial-line rewrites dominate msbfs_kernel) and
+// loses when the edge sweep dominates (it runs 32 sources per sweep, not
+// 64).  SPF_MSBFS=planes|masks overrides (experiments).
+bool use_planes(const spf_ctx* c) {
+  if (c->N > 10 * (uint32_t)kMsThreads || c->sell4.empty()) return false;
+  if (const char* e = std::getenv("SPF_MSBFS")) return e[0] == 'p';
+  return c->sell_ptr.back() <= 8ull * c->N;  // sliced-ELL width <= 8 on average
+}
+
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
                         uint8_t* Dn, hipStream_t s) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
@@ -1250,6 +1500,15 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
   }
   const uint32_t own = (c->N + kMsThreads - 1) / kMsThreads;
+  if (use_planes(c)) {
+    if (own <= 1) planes_launch<1>(c, rows_src, rows, D, Dn, s);
+    else if (own <= 2) planes_launch<2>(c, rows_src, rows, D, Dn, s);
+    else if (own <= 4) planes_launch<4>(c, rows_src, rows, D, Dn, s);
+    else if (own <= 8) planes_launch<8>(c, rows_src, rows, D, Dn, s);
+    else planes_launch<10>(c, rows_src, rows, D, Dn, s);
+    HIP_TRY(c, hipGetLastError());
+    return SPF_OK;
+  }
   if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, s);
   else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, s);
   else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, s);
@@ -1285,7 +1544,10 @@ spf_status set_lds_limits(spf_ctx* c) {
   const void* fns[] = {(const void*)sssp_kernel<uint16_t, true>, (const void*)sssp_kernel<uint16_t, false>,
                        (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>,
 #define MSB(o) (const void*)msbfs_kernel<o, false>, (const void*)msbfs_kernel<o, true>
-                       MSB(1), MSB(2), MSB(4), MSB(8), MSB(10), MSB(12), MSB(16)};
+                       MSB(1), MSB(2), MSB(4), MSB(8), MSB(10), MSB(12), MSB(16),
+#define PLB(o) (const void*)msbfs_planes_kernel<o, false>, (const void*)msbfs_planes_kernel<o, true>
+                       PLB(1), PLB(2), PLB(4), PLB(8), PLB(10)};
+#undef PLB
 #undef MSB
   for (const void* f : fns)
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));

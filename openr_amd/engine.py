@@ -83,6 +83,15 @@ class SpfPlan:
         self._eng._err(N.lib.spf_plan_execute_host(self._h, N.ptr(dist), N.ptr(nh)))
         return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
 
+    BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel")
+
+    def kernels(self) -> Tuple[str, bool]:
+        """(distance kernel name, next-hop pass reads u8 narrow rows) of the
+        next execute (spf_plan_kernels)."""
+        bfs, narrow = C.c_uint32(), C.c_uint32()
+        self._eng._err(N.lib.spf_plan_kernels(self._h, C.byref(bfs), C.byref(narrow)))
+        return self.BFS_KERNELS[bfs.value], bool(narrow.value)
+
     def enable_timing(self, max_executes: int) -> None:
         self._eng._err(N.lib.spf_plan_enable_timing(self._h, max_executes))
 

@@ -147,3 +147,22 @@ def test_saturated_narrow_rows_fall_back_to_exact(monkeypatch):
     rng = np.random.default_rng(5)
     compare(names, eng, orc, sorted(int(x) for x in rng.choice(len(names), 40, replace=False)),
             hop=True)
+
+
+@pytest.mark.parametrize("variant", ["planes", "masks"])
+@pytest.mark.parametrize("name,make", [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("grid30", lambda: T.grid(30)),
+    ("rand_drained", lambda: T.random_graph(60, 150, 7, max_metric=1, overload_frac=0.15)),
+    ("ring1200", lambda: T.wan(1200, 0, seed=1)),  # 600 levels: three plane windows
+    ("ring_drained", lambda: T.random_graph(400, 400, 3, max_metric=1, overload_frac=0.05)),
+], ids=["fabric", "grid", "rand", "ring1200", "sparse_drained"])
+def test_bfs_variants_exact(name, make, variant, monkeypatch):
+    """Both multi-source BFS kernels (register bit planes, 32 sources per
+    workgroup; per-level mask stores, 64 sources), with both next-hop row
+    widths; SPF_MSBFS / SPF_NARROW force the choice the plan makes by degree."""
+    monkeypatch.setenv("SPF_MSBFS", variant)
+    names, eng, orc = load(make())
+    for narrow in ("0", "1"):
+        monkeypatch.setenv("SPF_NARROW", narrow)
+        compare(names, eng, orc, list(range(len(names))), hop=True)
