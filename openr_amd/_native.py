@@ -14,6 +14,8 @@ from pathlib import Path
 import numpy as np
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libopenr_spf.so"
+if os.environ.get("OPENR_SPF_LIB"):  # experiments: an alternative in-tree build
+    LIB_PATH = Path(os.environ["OPENR_SPF_LIB"]).resolve()
 
 SPF_OK = 0
 SPF_E_INVALID = 1

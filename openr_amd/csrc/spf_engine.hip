@@ -502,9 +502,12 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
     uint8_t* __restrict__ Dn) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint2* lcol = reinterpret_cast<uint2*>(smem);                   // [n4] (LCOL)
-  uint32_t* F0 = reinterpret_cast<uint32_t*>(smem + (LCOL ? 8ull * n4 : 0));  // [N + 1]
-  uint32_t* F1 = F0 + N + 1;                                      // [N + 1]
-  uint32_t* o_node = F1 + N + 1;                                  // [32] drained batch sources
+  // F0/F1: one word per owned node slot (OWN * 1024 >= N + 1); slots past
+  // N keep F = 0 (their vis is `all`), so every slot is written unconditionally
+  constexpr uint32_t kF = OWN * kMsThreads;
+  uint32_t* F0 = reinterpret_cast<uint32_t*>(smem + (LCOL ? 8ull * n4 : 0));  // [kF]
+  uint32_t* F1 = F0 + kF;                                         // [kF]
+  uint32_t* o_node = F1 + kF;                                     // [32] drained batch sources
   uint32_t* o_cnt = o_node + kPlBatch;                            // [1]
   uint32_t* flag = o_cnt + 1;                                     // [3] progress, L mod 3
 
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
   const uint32_t nb = min(bs, n_rows - row0);
   const uint32_t all = nb == 32 ? ~0u : ((1u << nb) - 1u);
 
-  for (uint32_t v = tid; v <= N; v += kMsThreads) F0[v] = F1[v] = 0;
+  for (uint32_t v = tid; v < kF; v += kMsThreads) F0[v] = F1[v] = 0;
   if (LCOL)
     for (uint32_t t = tid; t < n4; t += kMsThreads) lcol[t] = sell4[t];
   if (tid == 0) {
@@ -535,7 +538,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     const uint32_t v = tid + i * kMsThreads;
-    vis[i] = v < N ? F0[v] : 0u;
+    vis[i] = v < N ? F0[v] : all;
 #pragma unroll
     for (int b = 0; b < kPlanes; ++b) P[i][b] = 0u;
     if (__ballot(v < N && ovl[v])) dslices |= 1u << i;
@@ -560,16 +563,19 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
     uint32_t any = 0;
     const unsigned char* Fb = reinterpret_cast<const unsigned char*>(Fc);
 #define PL_F(off) (*reinterpret_cast<const uint32_t*>(Fb + (off)))
+    uint2 qn = LCOL ? lcol[sb[0] + ln] : sell4[sb[0] + ln];
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = tid + i * kMsThreads;
       uint32_t nx = 0;
+      const uint2 q = qn;
+      // group 0 of slice i + 1 is loaded while slice i waits for its F reads
+      if (i + 1 < OWN) qn = LCOL ? lcol[sb[i + 1] + ln] : sell4[sb[i + 1] + ln];
       // a uniform branch per slice: skips finished slices and keeps the
       // scheduler from hoisting ten slices' loads (register pressure).
-      // No per-lane masking: a finished node gets nx = 0 from ~vis, a node
+      // No per-lane masking: a finished node gets nx = 0 from ~vis, a slot
       // past N has only padding columns (F[N] == 0).
       if (__ballot(vis[i] != all)) {
-        const uint2 q = LCOL ? lcol[sb[i] + ln] : sell4[sb[i] + ln];
         uint32_t acc = PL_F(q.x & 0xFFFFu) | PL_F(q.x >> 16) | PL_F(q.y & 0xFFFFu) | PL_F(q.y >> 16);
 #pragma unroll 1
         for (uint32_t g = 1; g < sg[i]; ++g) {  // wider slices: the remaining groups
@@ -592,7 +598,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
           f &= own;
         }
       }
-      if (v < N) Fn[v] = f;  // every level: the buffer still holds level L - 2
+      Fn[v] = f;
     }
 #undef PL_F
     // flag[L mod 3]: set during level L, read after its barrier; cleared
@@ -1462,13 +1468,13 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
                        rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
 }
 
-size_t planes_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kPlBatch + 4); }
+size_t planes_lds_bytes(uint32_t own) { return 8ull * own * kMsThreads + 4ull * (kPlBatch + 4); }
 
 template <int OWN>
 void planes_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
                    hipStream_t s) {
   const uint32_t n4 = c->sell4_ptr.back();
-  const size_t lds = planes_lds_bytes(c->N), lds_col = lds + 8ull * n4;
+  const size_t lds = planes_lds_bytes(OWN), lds_col = lds + 8ull * n4;
   const bool lcol = lds_col <= kMaxLds;
   const uint32_t rounds = (rows + kPlBatch * c->n_cu - 1) / (kPlBatch * c->n_cu);
   const uint32_t bs = std::min<uint32_t>(kPlBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
