@@ -92,6 +92,8 @@ typedef struct ls_paths_view {
 spf_status ls_create(const char* area, int device, ls_state** out);
 void ls_destroy(ls_state* ls);
 const char* ls_last_error(const ls_state* ls);
+/* LinkState::getArea (LinkState.h:356-359) */
+const char* ls_get_area(const ls_state* ls);
 
 spf_status ls_update_adjacency_databases(ls_state* ls, const openr_lsdb* lsdb,
                                          uint64_t hold_up_ttl,

@@ -188,6 +188,7 @@ PROTOTYPES = {
     "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "ls_destroy": (None, [_vp]),
     "ls_last_error": (C.c_char_p, [_vp]),
+    "ls_get_area": (C.c_char_p, [_vp]),
     "ls_update_adjacency_databases": (C.c_int, [_vp, C.POINTER(OpenrLsdb), C.c_uint64,
                                                 C.c_uint64, C.POINTER(LsChange)]),
     "ls_delete_adjacency_database": (C.c_int, [_vp, C.c_char_p, C.POINTER(LsChange)]),
@@ -214,6 +215,18 @@ PROTOTYPES = {
     "ls_flatten": (C.c_int, [_vp, _u32p, _u32p]),
     "ls_graph_node_names": (C.c_int, [_vp, _u32p]),
     "ls_graph_csr": (C.c_int, [_vp, _u32p, _u32p, _i32p, _u32p, _u8p]),
+    # LSDB wire ingest (openr_wire.h)
+    "openr_wire_decode_adjdb": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp)]),
+    "openr_wire_decode_publication": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp)]),
+    "openr_wire_view": (C.POINTER(OpenrLsdb), [_vp]),
+    "openr_wire_area": (C.c_char_p, [_vp]),
+    "openr_wire_n_expired": (C.c_uint32, [_vp]),
+    "openr_wire_expired": (C.c_char_p, [_vp, C.c_uint32]),
+    "openr_wire_n_skipped": (C.c_uint32, [_vp]),
+    "openr_wire_free": (None, [_vp]),
+    "openr_wire_last_error": (C.c_char_p, []),
+    "ls_apply_publication": (C.c_int, [_vp, C.c_char_p, C.c_size_t, _u32p, _u32p,
+                                       C.POINTER(LsChange)]),
 }
 
 

@@ -2,8 +2,9 @@
 
     python -m openr_amd.build [--force]
 
-Sources: openr_amd/csrc/spf_engine.hip (HIP kernels + engine C-ABI) and
-openr_amd/csrc/link_state.cpp (LinkState facade C-ABI); headers in include/.
+Sources: every openr_amd/csrc/*.hip (HIP kernels + engine C-ABI) and *.cpp
+(link_state.cpp: LinkState facade C-ABI; lsdb_wire.cpp: LSDB wire ingest);
+headers in include/.
 """
 
 from __future__ import annotations

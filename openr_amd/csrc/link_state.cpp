@@ -767,6 +767,8 @@ const char* ls_last_error(const ls_state* ls) {
   return ls ? ls->err.c_str() : spf_global_error();
 }
 
+const char* ls_get_area(const ls_state* ls) { return ls ? ls->area.c_str() : nullptr; }
+
 spf_status ls_update_adjacency_databases(ls_state* ls, const openr_lsdb* lsdb, uint64_t up,
                                          uint64_t down, ls_change* changes) {
   if (!ls || !lsdb) return SPF_E_INVALID;

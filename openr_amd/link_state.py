@@ -227,6 +227,23 @@ class LinkState:
         self._topology(res)
         return res
 
+    def processPublication(self, publication: bytes) -> LinkStateChange:
+        """The link-state half of ``Decision::processPublication``
+        (Decision.cpp:1709-1817) for this area: a serialized
+        thrift::Publication (CompactProtocol); every ``"adj:"`` value is
+        decoded and applied, every expired ``"adj:"`` key deletes its node's
+        database.  Returns the OR of the steps' LinkStateChanges; the counts
+        of applied / deleted databases land in ``lastPublicationCounts``."""
+        nu, nd, c = C.c_uint32(), C.c_uint32(), N.LsChange()
+        st = N.lib.ls_apply_publication(self._h, publication, len(publication), C.byref(nu),
+                                        C.byref(nd), C.byref(c))
+        N.raise_for(st, (N.lib.openr_wire_last_error() or b"").decode())
+        self.lastPublicationCounts = (int(nu.value), int(nd.value))
+        res = _change(c)
+        self._link_cache.clear()
+        self._topology([res])
+        return res
+
     def deleteAdjacencyDatabase(self, nodeName: str) -> LinkStateChange:
         c = N.LsChange()
         self._err(N.lib.ls_delete_adjacency_database(self._h, nodeName.encode(), C.byref(c)))
