@@ -25,6 +25,7 @@
 //  fbthrift, fb303, glog); parity of this restatement is pinned against the
 //  reference's own test expectations (tests/golden/, tests/test_oracle_*.py).
 // ============================================================================
+#include <atomic>
 #include <algorithm>
 #include <deque>
 #include <cstdint>
@@ -263,7 +264,8 @@ struct NodeResult {
 using SpfResult = std::unordered_map<std::string, NodeResult>;
 using Path = std::vector<LinkPtr>;
 
-static uint64_t g_spf_runs = 0;
+// atomic: the benchmark's multi-core CPU baseline runs one LinkState per thread
+static std::atomic<uint64_t> g_spf_runs{0};
 
 // ---- Dijkstra priority queue (LinkState.h:475-535) -------------------------
 struct QNode {
@@ -679,7 +681,7 @@ static std::string str_at(const char* blob, uint32_t off, uint32_t len) {
 
 orc_ls* orc_ls_new(const char* area) { return new orc_ls(area); }
 void orc_ls_free(orc_ls* p) { delete p; }
-uint64_t orc_spf_runs(void) { return orc::g_spf_runs; }
+uint64_t orc_spf_runs(void) { return orc::g_spf_runs.load(); }
 
 static void put_change(const orc::Change& c, uint8_t* out) {
   if (!out) return;
