@@ -101,6 +101,7 @@ struct WiBase {
 // ---------------------------------------------------------------------------
 namespace cg = cooperative_groups;
 constexpr int kCoopThreads = 512;  // one block per CU: always co-resident
+constexpr uint32_t kCoopHubDeg = 32;  // nodes above this degree get a whole wave
 
 struct CoopSssp {
   const uint32_t* row_ptr;
@@ -122,7 +123,8 @@ struct CoopSssp {
 // other workgroups is read with agent-scope atomics (ld) or atomicExch.
 __device__ void coop_sssp(cg::grid_group& grid, const CoopSssp& a) {
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t gsz = gridDim.x * blockDim.x;
+  const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t bm_words = (a.N + 31) / 32;
   for (uint32_t v = gtid; v < a.N; v += gsz) st(&a.dist[v], v == a.src ? 0u : kInf);
   for (uint32_t i = gtid; i < bm_words; i += gsz) st(&a.bm[i], 0u);
@@ -140,15 +142,34 @@ __device__ void coop_sssp(cg::grid_group& grid, const CoopSssp& a) {
     uint32_t* nxt = (it & 1) ? a.qa : a.qb;
     uint32_t* nctr = &a.ctr[(it + 1) % 3];
     if (gtid == 0) st(&a.ctr[(it + 2) % 3], 0u);  // read last at iteration it - 1
-    for (uint32_t i = gtid; i < len; i += gsz) {
-      const uint32_t u = ld(&cur[i]);
-      if (a.ovl[u] && u != a.src) continue;  // drained: recorded, not expanded
-      const uint32_t du = ld(&a.dist[u]);
-      for (uint32_t e = a.row_ptr[u]; e < a.row_ptr[u + 1]; ++e) {
-        if (a.ign && ((a.ign[a.link[e] >> 5] >> (a.link[e] & 31)) & 1u)) continue;
-        const uint32_t v = a.col[e];
-        const uint32_t nd = du + (a.hop ? 1u : a.wt[e]);
-        if (nd < atomicMin(&a.dist[v], nd)) atomicOr(&a.bm[v >> 5], 1u << (v & 31));
+    // wave-uniform sweep over the frontier: a lane expands its own node
+    // unless the node is a hub (degree > kCoopHubDeg), whose edges the whole
+    // wave then relaxes together -- one thread walking a scale-free hub's
+    // thousands of returning atomics serially was the critical path
+    auto relax = [&](uint32_t e, uint32_t du) {
+      if (a.ign && ((a.ign[a.link[e] >> 5] >> (a.link[e] & 31)) & 1u)) return;
+      const uint32_t v = a.col[e];
+      const uint32_t nd = du + (a.hop ? 1u : a.wt[e]);
+      if (nd < atomicMin(&a.dist[v], nd)) atomicOr(&a.bm[v >> 5], 1u << (v & 31));
+    };
+    for (uint32_t b = gtid - lane; b < len; b += gsz) {
+      const uint32_t i = b + lane;
+      uint32_t e0 = 0, e1 = 0, du = 0;
+      if (i < len) {
+        const uint32_t u = ld(&cur[i]);
+        if (!a.ovl[u] || u == a.src) {  // drained: recorded, not expanded
+          du = ld(&a.dist[u]);
+          e0 = a.row_ptr[u];
+          e1 = a.row_ptr[u + 1];
+        }
+      }
+      const bool hub = e1 - e0 > kCoopHubDeg;
+      if (!hub)
+        for (uint32_t e = e0; e < e1; ++e) relax(e, du);
+      for (uint64_t hubs = __ballot(hub); hubs; hubs &= hubs - 1) {
+        const int l = __builtin_ctzll(hubs);
+        const uint32_t hb = __shfl(e0, l, 64), he = __shfl(e1, l, 64), hd = __shfl(du, l, 64);
+        for (uint32_t e = hb + lane; e < he; e += 64) relax(e, hd);
       }
     }
     grid.sync();
@@ -186,13 +207,17 @@ struct BaseArgs {
   uint32_t* order;      // [N] nodes by distance
   uint32_t* misc;       // [8]: 0 max dist, 1 nonempty levels, 2..4 flags
   unsigned long long* H;
+  unsigned long long* prof;  // SPF_WHATIF_PROF: [16] phase clocks of block 0
 };
 
+// word j of nh(v) from v's in-edges first, first + stride, ... (a wave
+// splits a hub's edges over its lanes and ORs the parts)
 __device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* dist,
-                                            const uint32_t* nhb, uint32_t v, uint32_t j) {
+                                            const uint32_t* nhb, uint32_t v, uint32_t j,
+                                            uint32_t first = 0, uint32_t stride = 1) {
   const uint32_t dv = dist[v];
   uint32_t acc = 0;
-  for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
+  for (uint32_t e = g.row_ptr[v] + first; e < g.row_ptr[v + 1]; e += stride) {
     const uint32_t u = g.col[e];
     if (g.ovl[u] && u != g.src) continue;
     const uint32_t du = ld(&dist[u]);
@@ -207,10 +232,45 @@ __device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* di
   return acc;
 }
 
+// nh(v) of a hub by one wave: lanes test v's in-edges 64 at a time, then
+// every tight predecessor's W words are ORed in with lane = word (a (v, j)
+// item per thread would rescan the hub's edges W times)
+__device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, uint32_t v,
+                       uint32_t lane) {
+  const uint32_t dv = dist[v], W = g.W;
+  const uint32_t e0 = g.row_ptr[v], e1 = g.row_ptr[v + 1];
+  for (uint32_t j0 = 0; j0 < W; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    uint32_t acc = 0;
+    for (uint32_t eb = e0; eb < e1; eb += 64) {
+      const uint32_t e = eb + lane;
+      uint32_t u = kInf;
+      if (e < e1) {
+        const uint32_t cu = g.col[e];
+        if (!g.ovl[cu] || cu == g.src) {
+          const uint32_t du = ld(&dist[cu]);
+          if (du != kInf && du + g.wt[g.rev[e]] == dv) u = cu;
+        }
+      }
+      for (uint64_t t = __ballot(u != kInf); t; t &= t - 1) {
+        const uint32_t tu = __shfl(u, __builtin_ctzll(t), 64);
+        if (tu == g.src) {
+          const uint32_t jb = g.nbr_bit[v];
+          if (j == (jb >> 5)) acc |= 1u << (jb & 31);
+        } else if (j < W) {
+          acc |= ld(&nhb[(size_t)tu * W + j]);
+        }
+      }
+    }
+    if (j < W) st(&nhb[(size_t)v * W + j], acc);
+  }
+}
+
 __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
   cg::grid_group grid = cg::this_grid();
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t gsz = gridDim.x * blockDim.x;
+  const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
+  const uint32_t lane = threadIdx.x & 63;
   const WiGraph& g = a.g;
   const uint32_t N = g.N, W = g.W;
   const uint64_t NW = (uint64_t)N * W;
@@ -220,7 +280,10 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
     for (int i = 0; i < 8; ++i) st(&a.misc[i], 0u);
     *a.H = 0;
   }
+  const bool stamp = a.prof && gtid == 0;
+  if (stamp) a.prof[0] = wall_clock64();
   coop_sssp(grid, a.sp);  // starts and ends with a grid barrier
+  if (stamp) a.prof[1] = wall_clock64();
   const uint32_t* dist = a.sp.dist;
   // ---- distance range and per-value counts ----
   for (uint32_t v = gtid; v < N; v += gsz) {
@@ -278,10 +341,19 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
       const uint32_t end = ld(&a.lvl[d]);
       if (end == begin) continue;  // empty level: uniform skip
       const uint64_t items = (uint64_t)(end - begin) * W;
-      for (uint64_t x = gtid; x < items; x += gsz) {
-        const uint32_t v = ld(&a.order[begin + (uint32_t)(x / W)]);
-        const uint32_t j = (uint32_t)(x % W);
-        st(&a.nhb[(size_t)v * W + j], nh_word(g, dist, a.nhb, v, j));
+      for (uint64_t b = gtid - lane; b < items; b += gsz) {  // wave-uniform
+        const uint64_t x = b + lane;
+        uint32_t v = 0, j = 0;
+        bool hub = false;
+        if (x < items) {
+          v = ld(&a.order[begin + (uint32_t)(x / W)]);
+          j = (uint32_t)(x % W);
+          hub = g.row_ptr[v + 1] - g.row_ptr[v] > kCoopHubDeg;
+          if (!hub) st(&a.nhb[(size_t)v * W + j], nh_word(g, dist, a.nhb, v, j));
+        }
+        // a hub's W words are made once, by the wave, at its j = 0 item
+        for (uint64_t hubs = __ballot(hub && j == 0); hubs; hubs &= hubs - 1)
+          hub_nh(g, dist, a.nhb, __shfl(v, __builtin_ctzll(hubs), 64), lane);
       }
       begin = end;
       grid.sync();
@@ -305,6 +377,11 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
       if (!ld(&a.misc[2 + it % 3])) break;
     }
   }
+  if (stamp) {
+    a.prof[2] = wall_clock64();
+    a.prof[4] = ld(&a.misc[0]);
+    a.prof[5] = ld(&a.misc[1]);
+  }
   // ---- result hash ----
   uint64_t h = 0;
   for (uint32_t v = gtid; v < N; v += gsz) {
@@ -325,6 +402,7 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
     hi = (uint32_t)(t >> 32);
   }
   if ((threadIdx.x & 63) == 0 && (lo | hi)) atomicAdd(a.H, ((unsigned long long)hi << 32) | lo);
+  if (stamp) a.prof[3] = wall_clock64();
 }
 
 // ---------------------------------------------------------------------------
@@ -939,8 +1017,8 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
   if (std::getenv("SPF_WHATIF_PROF")) {
-    HIP_TRY(c, p->d_prof.alloc(16 * bt));
-    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 16 * bt * 8, c->stream));
+    HIP_TRY(c, p->d_prof.alloc(16 * (bt + 1)));
+    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 16 * (bt + 1) * 8, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   p->epoch = c->epoch;
@@ -979,7 +1057,8 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   {
     BaseArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr,
                         N, p->src, 0u, p->d_dist.p, p->d_q.p, p->d_q2.p, p->d_bm.p, p->d_ctr.p},
-               g, p->d_nhb.p, p->d_lvl.p, p->d_order.p, p->d_misc.p, p->d_H.p};
+               g, p->d_nhb.p, p->d_lvl.p, p->d_order.p, p->d_misc.p, p->d_H.p,
+               p->d_prof.p ? p->d_prof.p + 16ull * p->big_teams : nullptr};
     void* args[] = {&a};
     HIP_TRY(c, hipLaunchCooperativeKernel((const void*)whatif_base_kernel, dim3(coop_blocks(c)),
                                           dim3(kCoopThreads), args, 0, s));
@@ -1004,7 +1083,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     HIP_TRY(c, hipGetLastError());
   }
   if (p->d_prof.p) {  // diagnostics: phase times of the workgroup teams
-    std::vector<unsigned long long> h(16ull * p->big_teams);
+    std::vector<unsigned long long> h(16ull * (p->big_teams + 1));
     HIP_TRY(c, hipMemcpyAsync(h.data(), p->d_prof.p, h.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     for (uint32_t t = 0; t < p->big_teams; ++t) {
@@ -1014,6 +1093,9 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
                    "fallback=%llu digest=%llu (x10ns)\n", t, r[8], r[9], (r[1] - r[0]) / 1,
                    r[2] - r[1], r[3] - r[2], r[4] - r[3], r[5] - r[4]);
     }
+    const unsigned long long* r = &h[16ull * p->big_teams];
+    std::fprintf(stderr, "whatif base sssp=%llu nh=%llu hash=%llu (x10ns) maxd=%llu levels=%llu W=%u\n",
+                 r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4], r[5], p->W);
   }
   if (d_base) {
     // the unfailed digest: nothing changed, hash = H
