@@ -208,6 +208,8 @@ struct BaseArgs {
   uint32_t* misc;       // [8]: 0 max dist, 1 nonempty levels, 2..4 flags
   unsigned long long* H;
   unsigned long long* prof;  // SPF_WHATIF_PROF: [16] phase clocks of block 0
+  uint32_t* parent;     // [N] one tight expanded predecessor (levels path)
+  uint32_t* sub;        // [N] subtree sizes of the parent tree, 0 without levels
 };
 
 // word j of nh(v) from v's in-edges first, first + stride, ... (a wave
@@ -232,13 +234,27 @@ __device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* di
   return acc;
 }
 
+// the first tight expanded predecessor of v in CSR order (v reachable, != src)
+__device__ __forceinline__ uint32_t first_tight_pred(const WiGraph& g, const uint32_t* dist,
+                                                     uint32_t v) {
+  const uint32_t dv = dist[v];
+  for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
+    const uint32_t u = g.col[e];
+    if (g.ovl[u] && u != g.src) continue;
+    const uint32_t du = ld(&dist[u]);
+    if (du != kInf && du + g.wt[g.rev[e]] == dv) return u;
+  }
+  return kInf;
+}
+
 // nh(v) of a hub by one wave: lanes test v's in-edges 64 at a time, then
 // every tight predecessor's W words are ORed in with lane = word (a (v, j)
 // item per thread would rescan the hub's edges W times)
-__device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, uint32_t v,
-                       uint32_t lane) {
+__device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, uint32_t* parent,
+                       uint32_t v, uint32_t lane) {
   const uint32_t dv = dist[v], W = g.W;
   const uint32_t e0 = g.row_ptr[v], e1 = g.row_ptr[v + 1];
+  bool have_parent = false;
   for (uint32_t j0 = 0; j0 < W; j0 += 64) {
     const uint32_t j = j0 + lane;
     uint32_t acc = 0;
@@ -252,7 +268,13 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
           if (du != kInf && du + g.wt[g.rev[e]] == dv) u = cu;
         }
       }
-      for (uint64_t t = __ballot(u != kInf); t; t &= t - 1) {
+      const uint64_t tight = __ballot(u != kInf);
+      if (tight && !have_parent) {  // wave-uniform
+        have_parent = true;
+        const uint32_t first = __shfl(u, __builtin_ctzll(tight), 64);
+        if (lane == 0) st(&parent[v], first);
+      }
+      for (uint64_t t = tight; t; t &= t - 1) {
         const uint32_t tu = __shfl(u, __builtin_ctzll(t), 64);
         if (tu == g.src) {
           const uint32_t jb = g.nbr_bit[v];
@@ -276,6 +298,7 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
   const uint64_t NW = (uint64_t)N * W;
   for (uint64_t x = gtid; x < NW; x += gsz) st(&a.nhb[x], 0u);
   for (uint32_t i = gtid; i <= kLevelCap; i += gsz) st(&a.lvl[i], 0u);
+  for (uint32_t v = gtid; v < N; v += gsz) st(&a.sub[v], 0u);
   if (gtid == 0) {
     for (int i = 0; i < 8; ++i) st(&a.misc[i], 0u);
     *a.H = 0;
@@ -349,13 +372,32 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
           v = ld(&a.order[begin + (uint32_t)(x / W)]);
           j = (uint32_t)(x % W);
           hub = g.row_ptr[v + 1] - g.row_ptr[v] > kCoopHubDeg;
-          if (!hub) st(&a.nhb[(size_t)v * W + j], nh_word(g, dist, a.nhb, v, j));
+          if (!hub) {
+            st(&a.nhb[(size_t)v * W + j], nh_word(g, dist, a.nhb, v, j));
+            if (j == 0) st(&a.parent[v], first_tight_pred(g, dist, v));
+          }
         }
         // a hub's W words are made once, by the wave, at its j = 0 item
         for (uint64_t hubs = __ballot(hub && j == 0); hubs; hubs &= hubs - 1)
-          hub_nh(g, dist, a.nhb, __shfl(v, __builtin_ctzll(hubs), 64), lane);
+          hub_nh(g, dist, a.nhb, a.parent, __shfl(v, __builtin_ctzll(hubs), 64), lane);
       }
       begin = end;
+      grid.sync();
+    }
+    // subtree sizes of the parent tree, deepest level first: a lower bound
+    // on the DAG descendants a failure of the tree edge into v can change,
+    // used to hand big repairs to workgroup teams up front
+    for (uint32_t v = gtid; v < N; v += gsz)
+      if (ld(&dist[v]) != kInf) atomicAdd(&a.sub[v], 1u);
+    grid.sync();
+    for (uint32_t d = maxd; d >= 1; --d) {
+      const uint32_t lo = ld(&a.lvl[d - 1]), hi = ld(&a.lvl[d]);
+      if (lo == hi) continue;  // empty level: uniform skip
+      for (uint32_t x = lo + gtid; x < hi; x += gsz) {
+        const uint32_t v = ld(&a.order[x]);
+        const uint32_t pu = ld(&a.parent[v]);
+        if (pu != kInf) atomicAdd(&a.sub[pu], ld(&a.sub[v]));
+      }
       grid.sync();
     }
   } else {
@@ -412,7 +454,9 @@ __global__ void classify_kernel(WiGraph g, const uint32_t* __restrict__ dist,
                                 const unsigned long long* __restrict__ H,
                                 const uint32_t* __restrict__ fails, uint32_t n_fail,
                                 const uint32_t* __restrict__ link_edge,
-                                spf_whatif_digest* out, uint2* hot, uint32_t* n_hot) {
+                                const uint32_t* __restrict__ sub, uint32_t wave_cap,
+                                spf_whatif_digest* out, uint2* hot, uint32_t* n_hot,
+                                uint2* big, uint32_t* n_big) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n_fail) return;
   const uint32_t e0 = link_edge[fails[f]];
@@ -427,6 +471,8 @@ __global__ void classify_kernel(WiGraph g, const uint32_t* __restrict__ dist,
   }
   if (tight == kInf) {
     out[f] = spf_whatif_digest{0u, 0u, (uint64_t)*H};
+  } else if (sub[g.col[tight]] > wave_cap) {  // |D| >= subtree: a workgroup's repair
+    big[atomicAdd(n_big, 1u)] = make_uint2(f, tight);
   } else {
     hot[atomicAdd(n_hot, 1u)] = make_uint2(f, tight);
   }
@@ -909,16 +955,23 @@ struct spf_whatif_plan {
   DevBuf<uint32_t> d_fails, d_link_edge, d_nbr_bit, d_dist, d_q, d_q2, d_bm, d_nhb, d_ctr;
   DevBuf<uint32_t> d_lvl, d_order, d_misc;
   DevBuf<unsigned long long> d_H;
-  DevBuf<uint2> d_hot, d_big;
-  DevBuf<uint32_t> d_cnt;  // [0] n_hot, [1] cursor, [2] n_big
+  DevBuf<uint2> d_hot, d_big, d_big0;
+  DevBuf<uint32_t> d_cnt;  // [0] n_hot, [1] cursor, [2] n_big (overflow), [3] n_big0 (classified)
+  DevBuf<uint32_t> d_parent, d_sub;
+  hipStream_t s2 = nullptr;  // workgroup teams of the classified big failures
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint32_t big_teams = 0;
   DevBuf<unsigned long long> d_prof;  // SPF_WHATIF_PROF diagnostics
   DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
   DevBuf<uint32_t> b_mark, b_dlist, b_dnew, b_nhn, b_lvl, b_ord;  // workgroup-team scratch
+  DevBuf<uint32_t> c_mark, c_dlist, c_dnew, c_nhn, c_lvl, c_ord;  // same, concurrent set
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
   ~spf_whatif_plan() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (s2) (void)hipStreamDestroy(s2);
   }
 };
 
@@ -994,6 +1047,12 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->d_H.alloc(1));
   HIP_TRY(c, p->d_hot.alloc(std::max<uint32_t>(1, p->n_fail)));
   HIP_TRY(c, p->d_big.alloc(std::max<uint32_t>(1, p->n_fail)));
+  HIP_TRY(c, p->d_big0.alloc(std::max<uint32_t>(1, p->n_fail)));
+  HIP_TRY(c, p->d_parent.alloc(N));
+  HIP_TRY(c, p->d_sub.alloc(N));
+  HIP_TRY(c, hipStreamCreateWithFlags(&p->s2, hipStreamNonBlocking));
+  HIP_TRY(c, hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+  HIP_TRY(c, hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
   HIP_TRY(c, p->d_cnt.alloc(4));
   const size_t wt = p->wave_teams;
   HIP_TRY(c, p->w_mark.alloc(wt * N));
@@ -1013,6 +1072,13 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->b_nhn.alloc(bt * N * p->W));
   HIP_TRY(c, p->b_lvl.alloc(bt * (N + 1)));
   HIP_TRY(c, p->b_ord.alloc(bt * 2 * N));
+  HIP_TRY(c, p->c_mark.alloc(bt * N));
+  HIP_TRY(c, p->c_dlist.alloc(bt * N));
+  HIP_TRY(c, p->c_dnew.alloc(bt * N));
+  HIP_TRY(c, p->c_nhn.alloc(bt * N * p->W));
+  HIP_TRY(c, p->c_lvl.alloc(bt * (N + 1)));
+  HIP_TRY(c, p->c_ord.alloc(bt * 2 * N));
+  HIP_TRY(c, hipMemsetAsync(p->c_mark.p, 0xFF, bt * N * 4, c->stream));
   // marks start (and are always left) at kInf
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
@@ -1058,7 +1124,8 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     BaseArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr,
                         N, p->src, 0u, p->d_dist.p, p->d_q.p, p->d_q2.p, p->d_bm.p, p->d_ctr.p},
                g, p->d_nhb.p, p->d_lvl.p, p->d_order.p, p->d_misc.p, p->d_H.p,
-               p->d_prof.p ? p->d_prof.p + 16ull * p->big_teams : nullptr};
+               p->d_prof.p ? p->d_prof.p + 16ull * p->big_teams : nullptr, p->d_parent.p,
+               p->d_sub.p};
     void* args[] = {&a};
     HIP_TRY(c, hipLaunchCooperativeKernel((const void*)whatif_base_kernel, dim3(coop_blocks(c)),
                                           dim3(kCoopThreads), args, 0, s));
@@ -1068,10 +1135,21 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   HIP_TRY(c, hipMemsetAsync(p->d_cnt.p, 0, 16, s));
   if (p->n_fail) {
     hipLaunchKernelGGL(classify_kernel, dim3((p->n_fail + 255) / 256), dim3(256), 0, s, g,
-                       p->d_dist.p, p->d_H.p, p->d_fails.p, p->n_fail, p->d_link_edge.p, d_out,
-                       p->d_hot.p, p->d_cnt.p);
+                       p->d_dist.p, p->d_H.p, p->d_fails.p, p->n_fail, p->d_link_edge.p,
+                       p->d_sub.p, kWaveCap, d_out, p->d_hot.p, p->d_cnt.p, p->d_big0.p,
+                       p->d_cnt.p + 3);
     HIP_TRY(c, hipGetLastError());
     WiBase B{p->d_dist.p, p->d_nhb.p, p->d_H.p};
+    // failures classified big (parent subtree > kWaveCap) go to workgroup
+    // teams on a second stream right away, beside the wave teams; separate
+    // scratch, separate list, no dependence between the two grids
+    HIP_TRY(c, hipEventRecord(p->ev_fork, s));
+    HIP_TRY(c, hipStreamWaitEvent(p->s2, p->ev_fork, 0));
+    hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, p->s2, g, B,
+                       p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
+                       p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, nullptr);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(p->ev_join, p->s2));
     hipLaunchKernelGGL(repair_wave_kernel, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                        p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
                        p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p, p->w_ord.p,
@@ -1081,6 +1159,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
                        p->b_lvl.p, p->b_ord.p, d_out, p->d_prof.p);
     HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamWaitEvent(s, p->ev_join, 0));
   }
   if (p->d_prof.p) {  // diagnostics: phase times of the workgroup teams
     std::vector<unsigned long long> h(16ull * (p->big_teams + 1));
@@ -1112,8 +1191,8 @@ spf_status spf_whatif_stats(spf_whatif_plan* p, uint32_t* n_hot, uint32_t* n_big
   spf_ctx* c = p->ctx;
   uint32_t cnt[4];
   HIP_TRY(c, hipMemcpy(cnt, p->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost));
-  if (n_hot) *n_hot = cnt[0];
-  if (n_big) *n_big = cnt[2];
+  if (n_hot) *n_hot = cnt[0] + cnt[3];  // wave list + classified big
+  if (n_big) *n_big = cnt[2] + cnt[3];  // wave overflow + classified big
   return SPF_OK;
 }
 
