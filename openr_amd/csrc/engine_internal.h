@@ -53,6 +53,8 @@ struct spf_ctx {
   int device = 0;
   uint32_t n_cu = 256;  // compute units (BFS batch sizing)
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;  // what-if workgroup teams (lazily created, lives with the ctx)
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
   std::string err;
   uint64_t solves = 0;
   uint64_t shape = 0;  // bumped by spf_graph_load (CSR structure)

@@ -951,6 +951,12 @@ void spf_ctx_destroy(spf_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
   }
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
+  if (c->side_fork) (void)hipEventDestroy(c->side_fork);
+  if (c->side_join) (void)hipEventDestroy(c->side_join);
   delete c;
 }
 

@@ -958,8 +958,6 @@ struct spf_whatif_plan {
   DevBuf<uint2> d_hot, d_big, d_big0;
   DevBuf<uint32_t> d_cnt;  // [0] n_hot, [1] cursor, [2] n_big (overflow), [3] n_big0 (classified)
   DevBuf<uint32_t> d_parent, d_sub;
-  hipStream_t s2 = nullptr;  // workgroup teams of the classified big failures
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint32_t big_teams = 0;
   DevBuf<unsigned long long> d_prof;  // SPF_WHATIF_PROF diagnostics
   DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
@@ -969,9 +967,6 @@ struct spf_whatif_plan {
   uint32_t timing_cap = 0, timing_n = 0;
   ~spf_whatif_plan() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (s2) (void)hipStreamDestroy(s2);
   }
 };
 
@@ -1050,9 +1045,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->d_big0.alloc(std::max<uint32_t>(1, p->n_fail)));
   HIP_TRY(c, p->d_parent.alloc(N));
   HIP_TRY(c, p->d_sub.alloc(N));
-  HIP_TRY(c, hipStreamCreateWithFlags(&p->s2, hipStreamNonBlocking));
-  HIP_TRY(c, hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-  HIP_TRY(c, hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+  if (!c->side) {  // the classified big failures' workgroup teams run here
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming));
+  }
   HIP_TRY(c, p->d_cnt.alloc(4));
   const size_t wt = p->wave_teams;
   HIP_TRY(c, p->w_mark.alloc(wt * N));
@@ -1143,13 +1140,16 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     // failures classified big (parent subtree > kWaveCap) go to workgroup
     // teams on a second stream right away, beside the wave teams; separate
     // scratch, separate list, no dependence between the two grids
-    HIP_TRY(c, hipEventRecord(p->ev_fork, s));
-    HIP_TRY(c, hipStreamWaitEvent(p->s2, p->ev_fork, 0));
-    hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, p->s2, g, B,
+    hipStream_t side = c->side ? c->side : s;
+    if (c->side) {
+      HIP_TRY(c, hipEventRecord(c->side_fork, s));
+      HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_fork, 0));
+    }
+    hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, side, g, B,
                        p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
                        p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, nullptr);
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipEventRecord(p->ev_join, p->s2));
+    if (c->side) HIP_TRY(c, hipEventRecord(c->side_join, c->side));
     hipLaunchKernelGGL(repair_wave_kernel, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                        p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
                        p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p, p->w_ord.p,
@@ -1159,7 +1159,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
                        p->b_lvl.p, p->b_ord.p, d_out, p->d_prof.p);
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipStreamWaitEvent(s, p->ev_join, 0));
+    if (c->side) HIP_TRY(c, hipStreamWaitEvent(s, c->side_join, 0));
   }
   if (p->d_prof.p) {  // diagnostics: phase times of the workgroup teams
     std::vector<unsigned long long> h(16ull * (p->big_teams + 1));
