@@ -246,7 +246,11 @@ uint32_t spf_whatif_plan_failures(const spf_whatif_plan* plan);
 spf_status spf_whatif_plan_links(const spf_whatif_plan* plan, uint32_t* links /* [n_fail] */);
 /* d_out = [n_fail] digests, d_base = 1 digest (may be NULL).  Enqueued on
  * `stream` (cooperative launch for the unfailed solve); no host
- * synchronisation. */
+ * synchronisation.  Failures with a large affected region are repaired on a
+ * side stream owned by the ctx, forked from and joined back into `stream`
+ * with events, so all work is ordered after earlier work on `stream` and
+ * complete before later work on it.  Executes of plans sharing one ctx must
+ * not overlap (one host thread per ctx, as elsewhere). */
 spf_status spf_whatif_execute(spf_whatif_plan* plan, spf_whatif_digest* d_out,
                               spf_whatif_digest* d_base, void* stream);
 /* After an execute: failures that needed a re-solve (tight links) and those
