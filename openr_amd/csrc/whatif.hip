@@ -927,6 +927,9 @@ __global__ __launch_bounds__(1024) void repair_block_kernel(
     uint32_t* mark, uint32_t* dlist, uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord,
     spf_whatif_digest* out, unsigned long long* prof) {
   __shared__ TeamCtl ctl;
+  // the largest repairs are the critical path of a batch and share their CU
+  // with wave teams running concurrently: win the issue arbitration
+  __builtin_amdgcn_s_setprio(3);
   const size_t team = blockIdx.x;
   mark += team * g.N;
   dlist += team * g.N;
