@@ -653,7 +653,21 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         row[jb >> 5] |= 1u << (jb & 31);
       } else {
         const uint32_t* from = mu != kInf ? nhn + (size_t)mu * W : B.nhb + (size_t)u * W;
-        for (uint32_t j = 0; j < W; ++j) row[j] |= from[j];
+        // row and from may alias as far as the compiler knows: batches of 8
+        // loads ahead of their stores keep the loads in flight together
+        // instead of one load-OR-store round trip per word
+        uint32_t j = 0;
+        if (TEAM == 1024)  // workgroup teams only: costs the wave teams occupancy
+          for (; j + 8 <= W; j += 8) {
+            uint32_t f[8], r[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = from[j + q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) r[q] = row[j + q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) row[j + q] = r[q] | f[q];
+          }
+        for (; j < W; ++j) row[j] |= from[j];
       }
     }
   };
@@ -1150,7 +1164,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     }
     hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, side, g, B,
                        p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
-                       p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, nullptr);
+                       p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p);
     HIP_TRY(c, hipGetLastError());
     if (c->side) HIP_TRY(c, hipEventRecord(c->side_join, c->side));
     hipLaunchKernelGGL(repair_wave_kernel, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
@@ -1160,7 +1174,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     HIP_TRY(c, hipGetLastError());
     hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
-                       p->b_lvl.p, p->b_ord.p, d_out, p->d_prof.p);
+                       p->b_lvl.p, p->b_ord.p, d_out, nullptr);
     HIP_TRY(c, hipGetLastError());
     if (c->side) HIP_TRY(c, hipStreamWaitEvent(s, c->side_join, 0));
   }
