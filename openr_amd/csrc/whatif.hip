@@ -498,6 +498,15 @@ __device__ __forceinline__ void team_sync() {
 }
 
 // Returns false (nothing written, scratch clean) when |D| exceeds cap.
+// a team's scratch (mark, dlist, dnew, level lists) is private to one
+// workgroup: workgroup-scope accesses may be served by the CU's L1
+__device__ __forceinline__ uint32_t ldw(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void stw(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int TEAM>
 __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
                        uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, uint32_t cap,
@@ -521,7 +530,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
     ctl->ndist = ctl->nnh = ctl->dh = 0;
     dlist[0] = b;
-    st(&mark[b], 0);
+    stw(&mark[b], 0);
   }
   team_sync<TEAM>();
   // ---- D = descendants of b in the unfailed DAG (level by level) ----
@@ -539,9 +548,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       const uint32_t idx = atomicAdd(&ctl->n, 1u);
       if (idx < cap) {
         dlist[idx] = c;
-        st(&mark[c], idx);
+        stw(&mark[c], idx);
       } else {
-        st(&mark[c], kInf);
+        stw(&mark[c], kInf);
         ctl->ovf = 1;
       }
     };
@@ -550,7 +559,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.ovl[v]) continue;  // drained (v != src): no DAG children
       const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
       if (b1 - b0 > kHubDeg) {
-        st(&ord[atomicAdd(&ctl->hub, 1u)], i);
+        stw(&ord[atomicAdd(&ctl->hub, 1u)], i);
         continue;
       }
       const uint32_t dv = B.dist[v];
@@ -560,7 +569,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     {
       const uint32_t nh_ = ctl->hub;
       for (uint32_t k = wv; k < nh_; k += kWaves) {
-        const uint32_t v = dlist[ld(&ord[k])];
+        const uint32_t v = dlist[ldw(&ord[k])];
         const uint32_t dv = B.dist[v];
         for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) child(dv, e);
       }
@@ -576,7 +585,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   if (prof && tt == 0) prof[8] = n;
   team_sync<TEAM>();
   if (ovf) {
-    for (uint32_t i = tt; i < n; i += TEAM) st(&mark[dlist[i]], kInf);
+    for (uint32_t i = tt; i < n; i += TEAM) stw(&mark[dlist[i]], kInf);
     team_sync<TEAM>();
     return false;
   }
@@ -584,7 +593,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   auto seed_edge = [&](uint32_t e) -> uint32_t {
     if (g.link[e] == l) return kInf;
     const uint32_t u = g.col[e];
-    if (ld(&mark[u]) != kInf) return kInf;
+    if (ldw(&mark[u]) != kInf) return kInf;
     if (g.ovl[u] && u != g.src) return kInf;
     const uint32_t du = B.dist[u];
     return du == kInf ? kInf : du + g.wt[g.rev[e]];
@@ -593,24 +602,24 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     const uint32_t v = dlist[i];
     const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
     if (b1 - b0 > kHubDeg) {
-      st(&ord[atomicAdd(&ctl->hub, 1u)], i);
+      stw(&ord[atomicAdd(&ctl->hub, 1u)], i);
       continue;
     }
     uint32_t best = kInf;
     for (uint32_t e = b0; e < b1; ++e) best = min(best, seed_edge(e));
-    st(&dnew[i], best);
+    stw(&dnew[i], best);
   }
   team_sync<TEAM>();
   {
     const uint32_t nh_ = ctl->hub;
     for (uint32_t k = wv; k < nh_; k += kWaves) {
-      const uint32_t i = ld(&ord[k]);
+      const uint32_t i = ldw(&ord[k]);
       const uint32_t v = dlist[i];
       uint32_t best = kInf;
       for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64)
         best = min(best, seed_edge(e));
       best = wave_min32(best);
-      if (lane == 0) st(&dnew[i], best);
+      if (lane == 0) stw(&dnew[i], best);
     }
   }
   team_sync<TEAM>();
@@ -619,14 +628,14 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   // used by the fixed-point fallback
   auto nh_of = [&](uint32_t i, uint32_t j) -> uint32_t {
     const uint32_t v = dlist[i];
-    const uint32_t dv = ld(&dnew[i]);
+    const uint32_t dv = ldw(&dnew[i]);
     uint32_t acc = 0;
     for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
       if (g.link[e] == l) continue;
       const uint32_t u = g.col[e];
       if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = ld(&mark[u]);
-      const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
+      const uint32_t mu = ldw(&mark[u]);
+      const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
       if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
       if (u == g.src) {
         const uint32_t jb = g.nbr_bit[v];
@@ -645,8 +654,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.link[e] == l) continue;
       const uint32_t u = g.col[e];
       if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = ld(&mark[u]);
-      const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
+      const uint32_t mu = ldw(&mark[u]);
+      const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
       if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
       if (u == g.src) {
         const uint32_t jb = g.nbr_bit[v];
@@ -681,7 +690,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   team_sync<TEAM>();
   {
     uint32_t m = kInf;
-    for (uint32_t i = tt; i < n; i += TEAM) m = min(m, ld(&dnew[i]));
+    for (uint32_t i = tt; i < n; i += TEAM) m = min(m, ldw(&dnew[i]));
     if (m != kInf) atomicMin(&ctl->dmin, m);
   }
   team_sync<TEAM>();
@@ -705,8 +714,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     // (a) the level's nodes (their distance is final) into ord
     uint32_t m = kInf;
     for (uint32_t i = tt; i < n; i += TEAM) {
-      const uint32_t d = ld(&dnew[i]);
-      if (d == t) st(&ord[atomicAdd(cnt, 1u)], i);
+      const uint32_t d = ldw(&dnew[i]);
+      if (d == t) stw(&ord[atomicAdd(cnt, 1u)], i);
       else if (d != kInf && d > t) m = min(m, d);
     }
     team_sync<TEAM>();
@@ -718,17 +727,17 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     uint32_t* hub_cnt = &ctl->lc[(it + 2) % 3];  // free this level
     auto relax = [&](uint32_t v, uint32_t e) {
       if (g.link[e] == l) return;
-      const uint32_t ic = ld(&mark[g.col[e]]);
+      const uint32_t ic = ldw(&mark[g.col[e]]);
       if (ic == kInf) return;
       const uint32_t nd = t + g.wt[e];
       if (nd < atomicMin(&dnew[ic], nd)) m = min(m, nd);
     };
     for (uint32_t k = tt; k < K; k += TEAM) {
-      const uint32_t i = ld(&ord[k]);
+      const uint32_t i = ldw(&ord[k]);
       const uint32_t v = dlist[i];
       const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
       if (b1 - b0 > kHubDeg) {
-        st(&hubs[atomicAdd(hub_cnt, 1u)], i);
+        stw(&hubs[atomicAdd(hub_cnt, 1u)], i);
         continue;
       }
       nh_row(i, v, t);
@@ -738,7 +747,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     team_sync<TEAM>();
     const uint32_t H_ = *hub_cnt;
     for (uint32_t k = wv; k < H_; k += kWaves) {
-      const uint32_t i = ld(&hubs[k]);
+      const uint32_t i = ldw(&hubs[k]);
       const uint32_t v = dlist[i];
       uint32_t* row = nhn + (size_t)i * W;
       const uint32_t jb = g.nbr_bit[v];
@@ -750,8 +759,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         if (e < g.row_ptr[v + 1] && g.link[e] != l) {
           u = g.col[e];
           if (!(g.ovl[u] && u != g.src)) {
-            mu = ld(&mark[u]);
-            const uint32_t du = mu != kInf ? ld(&dnew[mu]) : B.dist[u];
+            mu = ldw(&mark[u]);
+            const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
             tight = du != kInf && du + g.wt[g.rev[e]] == t;
           }
         }
@@ -782,11 +791,11 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       bool any = false;
       for (uint32_t i = tt; i < n; i += TEAM) {
         const uint32_t v = dlist[i];
-        const uint32_t dv = ld(&dnew[i]);
+        const uint32_t dv = ldw(&dnew[i]);
         if (dv == kInf || g.ovl[v]) continue;
         for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
           if (g.link[e] == l) continue;
-          const uint32_t ic = ld(&mark[g.col[e]]);
+          const uint32_t ic = ldw(&mark[g.col[e]]);
           if (ic == kInf) continue;
           const uint32_t nd = dv + g.wt[e];
           if (nd < atomicMin(&dnew[ic], nd)) any = true;
@@ -807,7 +816,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }
     team_sync<TEAM>();
     for (uint32_t i = tt; i < n; i += TEAM) {
-      const uint32_t d = ld(&dnew[i]);
+      const uint32_t d = ldw(&dnew[i]);
       if (d != kInf) {
         atomicMin(&ctl->dmin, d);
         atomicMax(&ctl->dmax, d);
@@ -819,10 +828,10 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     if (nlev <= cap) {
       // counting sort of D by new distance; a predecessor always sits in a
       // lower level (positive metrics), so one pass per level is exact
-      for (uint32_t b = tt; b < nlev; b += TEAM) st(&lvl[b], 0u);
+      for (uint32_t b = tt; b < nlev; b += TEAM) stw(&lvl[b], 0u);
       team_sync<TEAM>();
       for (uint32_t i = tt; i < n; i += TEAM) {
-        const uint32_t d = ld(&dnew[i]);
+        const uint32_t d = ldw(&dnew[i]);
         if (d != kInf) atomicAdd(&lvl[d - dmin], 1u);
       }
       team_sync<TEAM>();
@@ -830,29 +839,29 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         uint32_t carry = 0;
         for (uint32_t base = 0; base < nlev; base += 64) {
           const uint32_t b = base + tt;
-          const uint32_t x = b < nlev ? ld(&lvl[b]) : 0u;
+          const uint32_t x = b < nlev ? ldw(&lvl[b]) : 0u;
           uint32_t inc = x;
           for (int d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(inc, d, 64);
             if (tt >= (uint32_t)d) inc += y;
           }
-          if (b < nlev) st(&lvl[b], carry + inc - x);
+          if (b < nlev) stw(&lvl[b], carry + inc - x);
           carry += __shfl(inc, 63, 64);
         }
       }
       team_sync<TEAM>();
       for (uint32_t i = tt; i < n; i += TEAM) {
-        const uint32_t d = ld(&dnew[i]);
-        if (d != kInf) st(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
+        const uint32_t d = ldw(&dnew[i]);
+        if (d != kInf) stw(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
       }
       team_sync<TEAM>();
       uint32_t begin = 0;
       for (uint32_t b = 0; b < nlev; ++b) {
-        const uint32_t end = ld(&lvl[b]);
+        const uint32_t end = ldw(&lvl[b]);
         if (end == begin) continue;
         const uint32_t items = (end - begin) * W;
         for (uint32_t x = tt; x < items; x += TEAM) {
-          const uint32_t i = ld(&ord[begin + x / W]), j = x % W;
+          const uint32_t i = ldw(&ord[begin + x / W]), j = x % W;
           nhn[(size_t)i * W + j] = nh_of(i, j);
         }
         begin = end;
@@ -864,7 +873,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         bool any = false;
         for (uint32_t x = tt; x < nw; x += TEAM) {
           const uint32_t i = x / W, j = x % W;
-          if (ld(&dnew[i]) == kInf) continue;
+          if (ldw(&dnew[i]) == kInf) continue;
           const uint32_t acc = nh_of(i, j);
           if (acc != nhn[x]) {
             nhn[x] = acc;
@@ -884,7 +893,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   uint64_t dh = 0;
   for (uint32_t i = tt; i < n; i += TEAM) {
     const uint32_t v = dlist[i];
-    const uint32_t d1 = ld(&dnew[i]), d0 = B.dist[v];
+    const uint32_t d1 = ldw(&dnew[i]), d0 = B.dist[v];
     const uint32_t* h0 = B.nhb + (size_t)v * W;
     const uint32_t* h1 = nhn + (size_t)i * W;
     nd_ += d1 != d0;
@@ -892,7 +901,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     for (uint32_t w = 0; w < W && !diff; ++w) diff = h0[w] != h1[w];
     nn_ += diff;
     dh += (d1 == kInf ? 0ull : node_hash(v, d1, h1, W)) - node_hash(v, d0, h0, W);
-    st(&mark[v], kInf);
+    stw(&mark[v], kInf);
   }
   if (nd_) atomicAdd(&ctl->ndist, (unsigned long long)nd_);
   if (nn_) atomicAdd(&ctl->nnh, (unsigned long long)nn_);
