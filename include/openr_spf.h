@@ -254,7 +254,8 @@ spf_status spf_whatif_plan_links(const spf_whatif_plan* plan, uint32_t* links /*
 spf_status spf_whatif_execute(spf_whatif_plan* plan, spf_whatif_digest* d_out,
                               spf_whatif_digest* d_base, void* stream);
 /* After an execute: failures that needed a re-solve (tight links) and those
- * re-solved by whole workgroups (large affected region). */
+ * re-solved by whole workgroups (large affected region).  Waits for the last
+ * execute's stream (SPF_E_STATE before the first execute). */
 spf_status spf_whatif_stats(spf_whatif_plan* plan, uint32_t* n_hot, uint32_t* n_big);
 spf_status spf_whatif_enable_timing(spf_whatif_plan* plan, uint32_t max_executes);
 /* summed ms of the unfailed solve (SPF + next hops + hash) and of the failures */

@@ -48,7 +48,12 @@ spf_status openr_wire_decode_adjdb(const uint8_t* buf, size_t len, openr_wire_ls
  * with "adj:" and carries a value becomes a database (area = the
  * publication's area); every expired "adj:" key contributes its node name
  * (getNodeNameFromKey, openr/common/Util.cpp:1013-1020).  Other keys
- * (prefix:, fibTime:) are not link state and are ignored. */
+ * (prefix:, fibTime:) are not link state and are ignored.  Databases come
+ * out in the iteration order of the keyVals container the reference
+ * deserialises into (std::unordered_map<std::string, Value>,
+ * KvStore.thrift:43-44, reserved for the map size and filled in wire order),
+ * which is the order Decision::processPublication applies them in
+ * (Decision.cpp:1726). */
 spf_status openr_wire_decode_publication(const uint8_t* buf, size_t len,
                                          openr_wire_lsdb** out);
 
@@ -67,6 +72,15 @@ const char* openr_wire_last_error(void);
  * *n_updated / *n_deleted count them (any pointer may be NULL). */
 spf_status ls_apply_publication(ls_state* ls, const uint8_t* buf, size_t len,
                                 uint32_t* n_updated, uint32_t* n_deleted, ls_change* agg);
+/* The same with enable_ordered_fib_programming (Decision.cpp:1750-1758):
+ * my_node != NULL applies the databases one at a time, each with hold-up
+ * TTL = getHopsFromAToB(my_node, originator) and hold-down TTL =
+ * getMaxHopsToNode(originator) - hold-up (0/0 when the originator is not
+ * reachable), read before that database is applied; needs a device-backed
+ * LinkState.  my_node == NULL is ls_apply_publication. */
+spf_status ls_apply_publication_ordered(ls_state* ls, const uint8_t* buf, size_t len,
+                                        const char* my_node, uint32_t* n_updated,
+                                        uint32_t* n_deleted, ls_change* agg);
 
 #ifdef __cplusplus
 }

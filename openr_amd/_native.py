@@ -7,8 +7,10 @@ no fallback: if the library is missing, importing this module raises.
 
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import weakref
 from pathlib import Path
 
 import numpy as np
@@ -227,6 +229,8 @@ PROTOTYPES = {
     "openr_wire_last_error": (C.c_char_p, []),
     "ls_apply_publication": (C.c_int, [_vp, C.c_char_p, C.c_size_t, _u32p, _u32p,
                                        C.POINTER(LsChange)]),
+    "ls_apply_publication_ordered": (C.c_int, [_vp, C.c_char_p, C.c_size_t, C.c_char_p, _u32p,
+                                               _u32p, C.POINTER(LsChange)]),
 }
 
 
@@ -265,3 +269,56 @@ def lsdb_struct(packed) -> OpenrLsdb:
     s.n_dbs = len(packed.dbs)
     s.adjs = packed.adjs.ctypes.data if len(packed.adjs) else None
     return s
+
+
+# ---- lifetime of native handles -------------------------------------------------
+class NativeHandle:
+    """Owner of one C-ABI object (plan or context) with an explicit close().
+
+    Device memory, streams and events are released by close() -- or by the
+    context manager -- in a defined order: plans before the context they were
+    created on.  Handles still open when the interpreter exits are closed by
+    an atexit hook in the same order, before the HIP runtime's own teardown
+    runs (destroying them from a garbage-collector finaliser after that point
+    is what crashed profiled runs at exit)."""
+
+    _LEVEL = 0  # closed in ascending level at exit: plans 0, contexts 1
+    _destroy = ""
+
+    def _adopt(self, h: C.c_void_p) -> None:
+        self._h = h
+        _LIVE.add(self)
+
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        lib = globals().get("lib")  # None during interpreter shutdown
+        if h is not None and h.value and lib is not None and getattr(self, "_owned", True):
+            getattr(lib, self._destroy)(h)
+        self._h = C.c_void_p()
+        _LIVE.discard(self)
+
+    @property
+    def closed(self) -> bool:
+        h = getattr(self, "_h", None)
+        return h is None or not h.value
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self) -> None:
+        self.close()
+
+
+_LIVE: "weakref.WeakSet[NativeHandle]" = weakref.WeakSet()
+
+
+def close_all() -> None:
+    """Close every open plan, then every open context (registered atexit)."""
+    for obj in sorted(list(_LIVE), key=lambda o: o._LEVEL):
+        obj.close()
+
+
+atexit.register(close_all)

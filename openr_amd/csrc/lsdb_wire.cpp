@@ -24,6 +24,7 @@
 // ============================================================================
 #include <algorithm>
 #include <cstring>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <string_view>
@@ -200,7 +201,7 @@ void decode_adjacency(Reader& r, Packed& pk, openr_adj_rec& a) {
 // adjacencies appended to pk.  Returns the node name (for the key check).
 std::string decode_adjdb(Reader& r, Packed& pk, const std::string* area_override) {
   openr_db_rec d{};
-  std::string_view name, area = "0";  // 6: string area (KvStore.kDefaultArea)
+  std::string_view name, area;  // 6: string area, no declared default (Lsdb.thrift:128)
   std::vector<openr_adj_rec> adjs;
   int16_t id = 0; int t;
   while (r.ok && r.field(id, t)) {
@@ -297,23 +298,34 @@ spf_status openr_wire_decode_publication(const uint8_t* buf, size_t len, openr_w
       if (!r.ok || n == 0) continue;
       const uint8_t kv = r.byte();
       if ((kv >> 4) != kBinary || (kv & 0x0F) != kStruct) { r.fail(); break; }
+      // The reference walks keyVals as the std::unordered_map<std::string,
+      // Value> fbthrift deserialises it into (KvStore.thrift:43-44,
+      // Decision.cpp:1726): reserved for the map's size, then filled in wire
+      // order.  The order databases are applied decides the order links
+      // enter the per-node link sets, hence linksFromNode order and the
+      // KSP2 / pathLinks tie-breaks -- so build the same container here
+      // (libstdc++ on both sides) and iterate it.
+      struct Entry { bool adj = false, has_value = false; std::string_view value; };
+      std::unordered_map<std::string, Entry> key_vals;
+      key_vals.reserve(n);
       for (uint64_t i = 0; i < n && r.ok; ++i) {
         const std::string_view key = r.binary();
-        bool has_value = false;
-        std::string_view value;
+        Entry e;
         int16_t vid = 0; int vt;
         while (r.ok && r.field(vid, vt)) {  // thrift::Value (KvStore.thrift:21-41)
           if (vid == 2 && vt == kBinary) {
-            value = r.binary();
-            has_value = true;
+            e.value = r.binary();
+            e.has_value = true;
           } else {
             r.skip(vt, false);
           }
         }
-        // a TTL update carries no value (Decision.cpp:1728-1732)
-        if (r.ok && has_value && key.substr(0, kAdjDbMarker.size()) == kAdjDbMarker)
-          vals.push_back({node_from_key(key), value});
+        e.adj = key.substr(0, kAdjDbMarker.size()) == kAdjDbMarker;
+        if (r.ok) key_vals.emplace(std::string(key), e);
       }
+      for (const auto& kvp : key_vals)  // a TTL update carries no value (Decision.cpp:1728-1732)
+        if (kvp.second.adj && kvp.second.has_value)
+          vals.push_back({node_from_key(kvp.first), kvp.second.value});
     } else if (id == 3 && t == kList) {  // expiredKeys: list<string>
       uint32_t n; int et;
       r.list(n, et);
@@ -362,8 +374,9 @@ uint32_t openr_wire_n_skipped(const openr_wire_lsdb* w) { return w ? w->skipped 
 void openr_wire_free(openr_wire_lsdb* w) { delete w; }
 const char* openr_wire_last_error(void) { return g_wire_err.c_str(); }
 
-spf_status ls_apply_publication(ls_state* ls, const uint8_t* buf, size_t len, uint32_t* n_updated,
-                                uint32_t* n_deleted, ls_change* agg) {
+spf_status ls_apply_publication_ordered(ls_state* ls, const uint8_t* buf, size_t len,
+                                        const char* my_node, uint32_t* n_updated,
+                                        uint32_t* n_deleted, ls_change* agg) {
   if (!ls) return wire_fail(SPF_E_INVALID, "null LinkState");
   openr_wire_lsdb* w = nullptr;
   spf_status st = openr_wire_decode_publication(buf, len, &w);
@@ -376,8 +389,34 @@ spf_status ls_apply_publication(ls_state* ls, const uint8_t* buf, size_t len, ui
                                         "' applied to the LinkState of area '" + ls_area + "'");
   const uint32_t n = w->view.n_dbs;
   std::vector<ls_change> ch(n ? n : 1);
-  st = ls_update_adjacency_databases(ls, &w->view, 0, 0, ch.data());
-  if (st != SPF_OK) return wire_fail(st, ls_last_error(ls));
+  if (!my_node) {
+    st = ls_update_adjacency_databases(ls, &w->view, 0, 0, ch.data());
+    if (st != SPF_OK) return wire_fail(st, ls_last_error(ls));
+  } else {
+    // enable_ordered_fib_programming (Decision.cpp:1750-1758): each database
+    // is held for the hop count from this node to its originator (hold up)
+    // and the rest of the originator's eccentricity (hold down), both read
+    // from the link state as it stands before that database is applied.
+    for (uint32_t i = 0; i < n; ++i) {
+      const openr_db_rec& d = w->view.dbs[i];
+      const std::string node(w->view.blob + d.name_off, d.name_len);
+      uint64_t up = 0, down = 0, hops = 0, max_hops = 0;
+      int has = 0;
+      st = ls_get_metric_a_to_b(ls, my_node, node.c_str(), 0, &hops, &has);
+      if (st != SPF_OK) return wire_fail(st, ls_last_error(ls));
+      if (has) {
+        st = ls_get_max_hops_to_node(ls, node.c_str(), &max_hops);
+        if (st != SPF_OK) return wire_fail(st, ls_last_error(ls));
+        up = hops;
+        down = max_hops - hops;
+      }
+      openr_lsdb one = w->view;
+      one.dbs = w->view.dbs + i;
+      one.n_dbs = 1;
+      st = ls_update_adjacency_databases(ls, &one, up, down, &ch[i]);
+      if (st != SPF_OK) return wire_fail(st, ls_last_error(ls));
+    }
+  }
   ls_change one{};
   for (const std::string& node : w->expired) {
     st = ls_delete_adjacency_database(ls, node.c_str(), &one);
@@ -393,6 +432,11 @@ spf_status ls_apply_publication(ls_state* ls, const uint8_t* buf, size_t len, ui
   if (n_updated) *n_updated = n;
   if (n_deleted) *n_deleted = (uint32_t)w->expired.size();
   return SPF_OK;
+}
+
+spf_status ls_apply_publication(ls_state* ls, const uint8_t* buf, size_t len, uint32_t* n_updated,
+                                uint32_t* n_deleted, ls_change* agg) {
+  return ls_apply_publication_ordered(ls, buf, len, nullptr, n_updated, n_deleted, agg);
 }
 
 }  // extern "C"

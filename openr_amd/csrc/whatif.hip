@@ -991,6 +991,7 @@ struct spf_whatif_plan {
   DevBuf<uint32_t> c_mark, c_dlist, c_dnew, c_nhn, c_lvl, c_ord;  // same, concurrent set
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
+  hipStream_t last = nullptr;  // stream of the last execute (spf_whatif_stats waits on it)
   ~spf_whatif_plan() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
@@ -1133,6 +1134,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   if (p->epoch != c->epoch)
     return fail(c, SPF_E_STATE, "graph changed since the plan was created: recreate it");
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  p->last = s;
   const uint32_t N = c->N;
   hipEvent_t* ev = nullptr;
   if (p->timing_cap) {
@@ -1215,8 +1217,12 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
 spf_status spf_whatif_stats(spf_whatif_plan* p, uint32_t* n_hot, uint32_t* n_big) {
   if (!p) return SPF_E_INVALID;
   spf_ctx* c = p->ctx;
-  uint32_t cnt[4];
-  HIP_TRY(c, hipMemcpy(cnt, p->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost));
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  if (!p->last) return fail(c, SPF_E_STATE, "spf_whatif_stats: no execute yet");
+  // the counters are written on the execute stream (non-blocking, so the
+  // null stream does not order after it): copy on that stream and wait
+  HIP_TRY(c, hipMemcpyAsync(cnt, p->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, p->last));
+  HIP_TRY(c, hipStreamSynchronize(p->last));
   if (n_hot) *n_hot = cnt[0] + cnt[3];  // wave list + classified big
   if (n_big) *n_big = cnt[2] + cnt[3];  // wave overflow + classified big
   return SPF_OK;

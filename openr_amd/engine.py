@@ -11,12 +11,16 @@ synchronisation, so it can be timed with HIP events or captured in a graph.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _native as N
+from ._native import NativeHandle, close_all  # noqa: F401
+
+
 
 HOP_COUNT = N.SPF_FLAG_HOP_COUNT
 UNREACHABLE = N.SPF_UNREACHABLE
@@ -44,7 +48,9 @@ def nh_matrix(nh: np.ndarray, off: int, k: int, pitch: int, n: int) -> np.ndarra
     return bits[:, :n].astype(bool)
 
 
-class SpfPlan:
+class SpfPlan(NativeHandle):
+    _destroy = "spf_plan_destroy"
+
     def __init__(self, eng: "SpfEngine", srcs: Sequence[int], flags: int) -> None:
         self._eng = eng
         self.srcs = np.ascontiguousarray(srcs, np.uint32)
@@ -52,19 +58,12 @@ class SpfPlan:
         h = C.c_void_p()
         eng._err(N.lib.spf_plan_create(eng._h, N.ptr(self.srcs), len(self.srcs), flags,
                                        C.byref(h)))
-        self._h = h
+        self._adopt(h)
         self.nh_words = int(N.lib.spf_plan_nh_words(h))
         self.closure_rows = int(N.lib.spf_plan_closure_rows(h))
         self.nh_off = np.zeros(len(self.srcs), np.uint64)
         self.words = np.zeros(len(self.srcs), np.uint32)
         N.lib.spf_plan_nh_layout(h, N.ptr(self.nh_off, C.c_uint64), N.ptr(self.words))
-
-    def __del__(self) -> None:
-        h = getattr(self, "_h", None)
-        lib = getattr(N, "lib", None)  # None during interpreter shutdown
-        if h is not None and h.value and lib is not None:
-            lib.spf_plan_destroy(h)
-            self._h = C.c_void_p()
 
     @property
     def n_src(self) -> int:
@@ -137,22 +136,17 @@ class Ksp2Result:
         return out
 
 
-class Ksp2Plan:
+class Ksp2Plan(NativeHandle):
     """A fixed source batch for batched KSP2 (``spf_ksp2_plan``)."""
+
+    _destroy = "spf_ksp2_plan_destroy"
 
     def __init__(self, eng: "SpfEngine", srcs: Sequence[int]) -> None:
         self._eng = eng
         self.srcs = np.ascontiguousarray(srcs, np.uint32)
         h = C.c_void_p()
         eng._err(N.lib.spf_ksp2_plan_create(eng._h, N.ptr(self.srcs), len(self.srcs), C.byref(h)))
-        self._h = h
-
-    def __del__(self) -> None:
-        h = getattr(self, "_h", None)
-        lib = getattr(N, "lib", None)
-        if h is not None and h.value and lib is not None:
-            lib.spf_ksp2_plan_destroy(h)
-            self._h = C.c_void_p()
+        self._adopt(h)
 
     def execute(self, d_pairs: int, d_pool: int, pool_words: int, d_counters: int,
                 stream: int = 0) -> None:
@@ -173,8 +167,10 @@ DIGEST_DTYPE = np.dtype([("n_dist_changed", "<u4"), ("n_nh_changed", "<u4"),
                          ("hash", "<u8")])  # spf_whatif_digest
 
 
-class WhatIfPlan:
+class WhatIfPlan(NativeHandle):
     """One source, a list of single-link failures (``spf_whatif_plan``)."""
+
+    _destroy = "spf_whatif_plan_destroy"
 
     def __init__(self, eng: "SpfEngine", src: int, links: Optional[Sequence[int]]) -> None:
         self._eng = eng
@@ -182,18 +178,11 @@ class WhatIfPlan:
         arr = None if links is None else np.ascontiguousarray(links, np.uint32)
         eng._err(N.lib.spf_whatif_plan_create(eng._h, src, None if arr is None else N.ptr(arr),
                                               0 if arr is None else len(arr), C.byref(h)))
-        self._h = h
+        self._adopt(h)
         self.n_fail = int(N.lib.spf_whatif_plan_failures(h))
         self.links = np.zeros(max(1, self.n_fail), np.uint32)
         eng._err(N.lib.spf_whatif_plan_links(h, N.ptr(self.links)))
         self.links = self.links[: self.n_fail]
-
-    def __del__(self) -> None:
-        h = getattr(self, "_h", None)
-        lib = getattr(N, "lib", None)
-        if h is not None and h.value and lib is not None:
-            lib.spf_whatif_plan_destroy(h)
-            self._h = C.c_void_p()
 
     def execute(self, d_out: int, d_base: int = 0, stream: int = 0) -> None:
         self._eng._err(N.lib.spf_whatif_execute(self._h, C.c_void_p(d_out),
@@ -214,26 +203,34 @@ class WhatIfPlan:
         return a.value, b.value, n.value
 
 
-class SpfEngine:
-    """An engine context with one graph loaded (``spf_ctx``)."""
+class SpfEngine(NativeHandle):
+    """An engine context with one graph loaded (``spf_ctx``).  ``close()``
+    (or ``with SpfEngine(0) as eng:``) first closes the plans created on it,
+    then destroys the context (its streams, events and device buffers)."""
+
+    _LEVEL = 1
+    _destroy = "spf_ctx_destroy"
 
     def __init__(self, device: int = 0, handle: Optional[C.c_void_p] = None) -> None:
         self._owned = handle is None
+        self._plans: "weakref.WeakSet[NativeHandle]" = weakref.WeakSet()
         if handle is None:
             h = C.c_void_p()
             st = N.lib.spf_ctx_create(device, C.byref(h))
             N.raise_for(st, N.global_error())
-            self._h = h
+            self._adopt(h)
         else:
             self._h = handle
         self._graph = None
 
-    def __del__(self) -> None:
-        h = getattr(self, "_h", None)
-        lib = getattr(N, "lib", None)
-        if getattr(self, "_owned", False) and h is not None and h.value and lib is not None:
-            lib.spf_ctx_destroy(h)
-            self._h = C.c_void_p()
+    def close(self) -> None:
+        for p in list(getattr(self, "_plans", ())):
+            p.close()
+        super().close()
+
+    def _track(self, plan):
+        self._plans.add(plan)
+        return plan
 
     def _err(self, st: int) -> None:
         N.raise_for(st, (N.lib.spf_last_error(self._h) or b"").decode())
@@ -315,7 +312,7 @@ class SpfEngine:
 
     # ---- solves -----------------------------------------------------------------
     def plan(self, srcs: Sequence[int], hop: bool = False) -> SpfPlan:
-        return SpfPlan(self, srcs, HOP_COUNT if hop else 0)
+        return self._track(SpfPlan(self, srcs, HOP_COUNT if hop else 0))
 
     def solve(self, srcs: Sequence[int], hop: bool = False) -> SolveResult:
         p = self.plan(srcs, hop)
@@ -327,7 +324,7 @@ class SpfEngine:
         return SolveResult(dist, nh, p.nh_off, p.words, self.pitch)
 
     def ksp2_plan(self, srcs: Sequence[int]) -> Ksp2Plan:
-        return Ksp2Plan(self, srcs)
+        return self._track(Ksp2Plan(self, srcs))
 
     def ksp2(self, srcs: Sequence[int]) -> Ksp2Result:
         """getKthPaths(s, d, 1) and (s, d, 2) for every s in srcs, every d."""
@@ -348,7 +345,7 @@ class SpfEngine:
         return Ksp2Result(srcs, n, pairs, pool)
 
     def whatif_plan(self, src: int, links: Optional[Sequence[int]] = None) -> WhatIfPlan:
-        return WhatIfPlan(self, src, links)
+        return self._track(WhatIfPlan(self, src, links))
 
     def whatif(self, src: int, links: Optional[Sequence[int]] = None):
         """Digests of runSpf(src, true, {l}) for each failed link l (every up

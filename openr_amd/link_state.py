@@ -153,31 +153,28 @@ def _change(c: N.LsChange) -> LinkStateChange:
                            bool(c.node_label_changed))
 
 
-class LinkState:
+class LinkState(N.NativeHandle):
     """``openr::LinkState`` (LinkState.h:177-469) on the MI355X engine.
 
     ``device`` selects the GPU; ``device=-1`` builds a host-only state (LSDB
-    bookkeeping and graph flatten, no shortest-path queries).
+    bookkeeping and graph flatten, no shortest-path queries).  ``close()``
+    (or a ``with`` block) releases the engine context it owns.
     """
+
+    _LEVEL = 1
+    _destroy = "ls_destroy"
 
     def __init__(self, area: str = K_DEFAULT_AREA, device: int = 0) -> None:
         h = C.c_void_p()
         st = N.lib.ls_create(area.encode(), device, C.byref(h))
         N.raise_for(st, N.global_error())
-        self._h = h
+        self._adopt(h)
         self._area = area
         self._names: List[Optional[str]] = []
         self._gen = 0
         self._spf_cache: Dict[Tuple[str, bool], SpfResult] = {}
         self._ksp_cache: Dict[Tuple[str, str, int], List[Path]] = {}
         self._link_cache: Dict[int, Link] = {}
-
-    def __del__(self) -> None:
-        h = getattr(self, "_h", None)
-        lib = getattr(N, "lib", None)  # None during interpreter shutdown
-        if h is not None and h.value and lib is not None:
-            lib.ls_destroy(h)
-            self._h = C.c_void_p()
 
     # -- helpers ---------------------------------------------------------------
     def _err(self, st: int) -> None:
@@ -227,16 +224,23 @@ class LinkState:
         self._topology(res)
         return res
 
-    def processPublication(self, publication: bytes) -> LinkStateChange:
+    def processPublication(self, publication: bytes,
+                           orderedFibNode: Optional[str] = None) -> LinkStateChange:
         """The link-state half of ``Decision::processPublication``
         (Decision.cpp:1709-1817) for this area: a serialized
         thrift::Publication (CompactProtocol); every ``"adj:"`` value is
-        decoded and applied, every expired ``"adj:"`` key deletes its node's
-        database.  Returns the OR of the steps' LinkStateChanges; the counts
-        of applied / deleted databases land in ``lastPublicationCounts``."""
+        decoded and applied (in the reference's keyVals iteration order),
+        every expired ``"adj:"`` key deletes its node's database.  With
+        ``orderedFibNode`` (this node's name, enable_ordered_fib_programming)
+        each database carries the hold-up / hold-down TTLs of
+        Decision.cpp:1750-1758.  Returns the OR of the steps'
+        LinkStateChanges; the counts of applied / deleted databases land in
+        ``lastPublicationCounts``."""
         nu, nd, c = C.c_uint32(), C.c_uint32(), N.LsChange()
-        st = N.lib.ls_apply_publication(self._h, publication, len(publication), C.byref(nu),
-                                        C.byref(nd), C.byref(c))
+        st = N.lib.ls_apply_publication_ordered(
+            self._h, publication, len(publication),
+            orderedFibNode.encode() if orderedFibNode is not None else None, C.byref(nu),
+            C.byref(nd), C.byref(c))
         N.raise_for(st, (N.lib.openr_wire_last_error() or b"").decode())
         self.lastPublicationCounts = (int(nu.value), int(nd.value))
         res = _change(c)

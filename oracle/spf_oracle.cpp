@@ -39,6 +39,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <unordered_set>
@@ -1298,6 +1299,461 @@ const char* orc_ls_sr_nexthops_json(orc_ls* p, const char* me_c, const char* con
   }
   o += "]}";
   return o.c_str();
+}
+
+// ============================================================================
+//  Full-size parity digests (tests/golden/make_fullsize_digests.py,
+//  tests/test_gpu_fullsize.py).  One 64-bit value per source (all-sources
+//  SPF + ECMP), per source over all destinations (KSP2), per failure (what-if),
+//  so that every output the GPU produces at BASELINE size is compared, not a
+//  sample.  The result hash is the what-if hash above:
+//    H(result) = sum over reachable v of mix64(mix64(v + 1) + metric(v)) ^ fnv(nh(v))
+//  nh(v) = u32 words of the bitset over src's distinct up neighbours (by name).
+//  The orc_digest_* functions apply the same hashes to the GPU's output
+//  layouts (include/openr_spf.h) so both sides are reduced by one routine.
+// ============================================================================
+}  // extern "C"
+
+namespace orc {
+
+static inline uint64_t fnvWords(const uint32_t* w, uint32_t n) {
+  uint64_t f = 0xcbf29ce484222325ULL;
+  for (uint32_t i = 0; i < n; ++i) {
+    f ^= w[i];
+    f *= 0x100000001b3ULL;
+  }
+  return f;
+}
+static inline uint64_t nodeTerm(uint32_t v, uint64_t metric, const uint32_t* nh, uint32_t words) {
+  return mix64(mix64((uint64_t)v + 1) + metric) ^ fnvWords(nh, words);
+}
+static inline uint64_t fnvFeed(uint64_t h, uint64_t x) { return (h ^ x) * 0x100000001b3ULL; }
+
+static uint64_t keyHash(const std::string& a, const std::string& b, const std::string& c,
+                        const std::string& d) {
+  uint64_t f = 0xcbf29ce484222325ULL;
+  for (const std::string* s : {&a, &b, &c, &d}) {
+    for (unsigned char ch : *s) f = (f ^ ch) * 0x100000001b3ULL;
+    f = (f ^ 0x01) * 0x100000001b3ULL;
+  }
+  return mix64(f);
+}
+static uint64_t linkKeyHash(const Link& l) {
+  const auto& k = l.key();
+  return keyHash(k.first.first, k.first.second, k.second.first, k.second.second);
+}
+
+// Digest of the k = 1 and k = 2 path lists of one (src, dst) pair.
+static uint64_t pairDigest(const std::vector<Path>* lists /* [2] */) {
+  uint64_t h = 0xcbf29ce484222325ULL;
+  for (int k = 0; k < 2; ++k) {
+    h = fnvFeed(h, 0x1000 + lists[k].size());
+    for (const auto& p : lists[k]) {
+      h = fnvFeed(h, 0x2000 + p.size());
+      for (const auto& l : p) h = fnvFeed(h, linkKeyHash(*l));
+    }
+  }
+  return h;
+}
+
+// Node table of the caller (names ascending = engine node ids).
+struct NameIds {
+  std::vector<std::string> names;
+  std::unordered_map<std::string, uint32_t> id;
+  NameIds(const char* blob, const uint32_t* off, const uint32_t* len, uint32_t n) : names(n) {
+    id.reserve(2 * n);
+    for (uint32_t i = 0; i < n; ++i) {
+      names[i].assign(blob + off[i], len[i]);
+      id.emplace(names[i], i);
+    }
+  }
+};
+
+// Distinct up neighbours of src, ascending name -> bit index.
+static std::unordered_map<std::string, uint32_t> nbrBits(const LinkState& ls,
+                                                         const std::string& s) {
+  std::set<std::string> nbrSet;
+  for (const auto& l : ls.linksFrom(s))
+    if (l->isUp()) nbrSet.insert(l->other(s));
+  std::unordered_map<std::string, uint32_t> bitOf;
+  uint32_t b = 0;
+  for (const auto& n : nbrSet) bitOf[n] = b++;
+  return bitOf;
+}
+
+// ---- runSpf restated on an integer CSR --------------------------------------
+// The same algorithm as LinkState::runSpf (LinkState.cpp:808-882) and
+// runSpfFast above: nodes pop in (metric, name) order (ids ascend with names,
+// so (metric, id)), drained nodes other than the source are not expanded
+// (:831-838), every up, non-ignored link to an unsettled node relaxes with
+// the metric its tail advertises (:844-851), a strictly better label resets
+// the next hops, an equal or better one unions the tail's next hops and, when
+// the union is empty (tail = source), inserts the head itself (:857-873).
+// Links are visited in linksFromNode order.  Next hops are kept as bitsets
+// over the source's distinct up neighbours instead of string sets.  Used for
+// graphs where the string-keyed restatement needs minutes per source (the
+// 250k-node what-if graph); pinned to runSpf / runSpfFast by
+// tests/test_oracle_fullsize.py.
+struct IntGraph {
+  uint32_t n = 0;
+  std::vector<uint32_t> rp, col, lk;
+  std::vector<Metric> w;
+  std::vector<uint8_t> up, ovl;
+  std::vector<const Link*> links;  // lk -> Link
+  Metric minW = UINT64_MAX, maxW = 0;   // over up edges
+  IntGraph(const LinkState& ls, const NameIds& t) : n((uint32_t)t.names.size()) {
+    std::unordered_map<const Link*, uint32_t> lid;
+    rp.assign(n + 1, 0);
+    for (uint32_t u = 0; u < n; ++u) {
+      const std::string& un = t.names[u];
+      for (const auto& l : ls.linksFrom(un)) {
+        auto it = t.id.find(l->other(un));
+        if (it == t.id.end()) continue;
+        auto ins = lid.emplace(l.get(), (uint32_t)links.size());
+        if (ins.second) links.push_back(l.get());
+        col.push_back(it->second);
+        lk.push_back(ins.first->second);
+        w.push_back(l->metricFrom(un));
+        up.push_back(l->isUp());
+        if (l->isUp()) {
+          minW = std::min(minW, w.back());
+          maxW = std::max(maxW, w.back());
+        }
+      }
+      rp[u + 1] = (uint32_t)col.size();
+      ovl.push_back(ls.nodeOverloaded(un));
+    }
+  }
+};
+
+struct IntSpf {
+  std::vector<Metric> dist;
+  std::vector<uint32_t> nh;  // [n][words]
+  std::vector<uint8_t> settled, open;
+  std::vector<std::pair<Metric, uint32_t>> heap;
+  std::vector<std::vector<uint32_t>> buckets;  // Dial's circular buckets
+  uint32_t words = 0;
+
+  // Pops follow (metric, id).  With positive metrics bounded by maxW a node
+  // is never relaxed into the distance being settled, so a circular array of
+  // maxW + 1 buckets, each sorted by id when its distance is reached, pops in
+  // exactly the heap's order; otherwise a lazy-deletion binary heap.
+  void run(const IntGraph& g, uint32_t src, uint32_t ignore, bool useLinkMetric,
+           const std::vector<int32_t>& bitOf /* [n], -1 = not a neighbour */) {
+    const uint32_t n = g.n;
+    dist.assign(n, UINT64_MAX);
+    nh.resize((size_t)n * words);
+    settled.assign(n, 0);
+    open.assign(n, 0);
+    heap.clear();
+    const bool dial = !useLinkMetric || (g.minW >= 1 && g.maxW <= 65536);
+    const Metric nb = useLinkMetric ? g.maxW + 1 : 2;
+    if (dial) {
+      buckets.resize(nb);
+      for (auto& b : buckets) b.clear();
+    }
+    size_t pending = 0;
+    auto cmp = std::greater<std::pair<Metric, uint32_t>>();
+    auto zero = [&](uint32_t v) {
+      std::fill(nh.begin() + (size_t)v * words, nh.begin() + (size_t)(v + 1) * words, 0u);
+    };
+    auto push = [&](Metric d, uint32_t v) {
+      if (dial) {
+        buckets[d % nb].push_back(v);
+        ++pending;
+      } else {
+        heap.emplace_back(d, v);
+        std::push_heap(heap.begin(), heap.end(), cmp);
+      }
+    };
+    auto settle = [&](uint32_t u, Metric du) {
+      settled[u] = 1;
+      if (g.ovl[u] && u != src) return;
+      const uint32_t* nu = &nh[(size_t)u * words];
+      for (uint32_t e = g.rp[u]; e < g.rp[u + 1]; ++e) {
+        const uint32_t v = g.col[e];
+        if (!g.up[e] || settled[v] || g.lk[e] == ignore) continue;
+        const Metric nd = du + (useLinkMetric ? g.w[e] : 1);
+        if (!open[v]) {
+          open[v] = 1;
+          dist[v] = nd;
+          zero(v);
+        }
+        if (dist[v] < nd) continue;
+        if (dist[v] > nd) {
+          dist[v] = nd;
+          zero(v);
+        }
+        uint32_t* nv = &nh[(size_t)v * words];
+        uint32_t any = 0;
+        for (uint32_t i = 0; i < words; ++i) any |= (nv[i] |= nu[i]);
+        if (!any && bitOf[v] >= 0) nv[bitOf[v] >> 5] |= 1u << (bitOf[v] & 31);
+        push(dist[v], v);
+      }
+    };
+    dist[src] = 0;
+    open[src] = 1;
+    zero(src);
+    ++g_spf_runs;
+    if (dial) {
+      push(0, src);
+      std::vector<uint32_t> cur;
+      for (Metric d = 0; pending; ++d) {
+        auto& b = buckets[d % nb];
+        if (b.empty()) continue;
+        cur.swap(b);
+        b.clear();
+        pending -= cur.size();
+        std::sort(cur.begin(), cur.end());
+        for (uint32_t u : cur)
+          if (!settled[u] && dist[u] == d) settle(u, d);
+        cur.clear();
+      }
+    } else {
+      heap.emplace_back(0, src);
+      while (!heap.empty()) {
+        std::pop_heap(heap.begin(), heap.end(), cmp);
+        const auto top = heap.back();
+        heap.pop_back();
+        if (settled[top.second] || dist[top.second] != top.first) continue;
+        settle(top.second, top.first);
+      }
+    }
+    for (uint32_t v = 0; v < n; ++v)
+      if (!settled[v]) {
+        dist[v] = UINT64_MAX;
+        zero(v);
+      }
+  }
+};
+
+template <class F>
+static void parallelFor(uint32_t n, int threads, F&& f) {
+  threads = std::max(1, std::min<int>(threads, (int)n));
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      for (uint32_t i = t; i < n; i += threads) f(i, t);
+    });
+  for (auto& th : ts) th.join();
+}
+
+}  // namespace orc
+
+extern "C" {
+
+// Iteration order of thrift::Publication.keyVals as the reference holds it:
+// a std::unordered_map<std::string, Value> (KvStore.thrift:43-44) reserved for
+// the map size and filled in wire order by the deserialiser, walked by
+// Decision::processPublication (Decision.cpp:1726).  perm_out[i] = wire index
+// of the i-th entry visited; returns the number of distinct keys.
+uint32_t orc_keyvals_order(const char* const* keys, uint32_t n, uint32_t* perm_out) {
+  std::unordered_map<std::string, uint32_t> m;
+  m.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) m.emplace(keys[i], i);
+  uint32_t k = 0;
+  for (const auto& kv : m) perm_out[k++] = kv.second;
+  return k;
+}
+
+uint64_t orc_link_keyhash(const char* n1, const char* if1, const char* n2, const char* if2) {
+  return orc::keyHash(n1, if1, n2, if2);
+}
+
+// Per-source digests H(runSpf(src, ulm)) of all sources in srcs.
+// int_path != 0 uses the integer-CSR restatement (same result, pinned by
+// tests/test_oracle_fullsize.py).  Runs on `threads` host threads.
+int orc_ls_source_digests(orc_ls* p, const char* blob, const uint32_t* off, const uint32_t* len,
+                          uint32_t n, const uint32_t* srcs, uint32_t n_src, int ulm, int int_path,
+                          int threads, uint64_t* out) {
+  const orc::NameIds t(blob, off, len, n);
+  const orc::LinkState& ls = p->ls;
+  std::unique_ptr<orc::IntGraph> g;
+  if (int_path) g.reset(new orc::IntGraph(ls, t));
+  std::vector<orc::IntSpf> scratch(std::max(1, threads));
+  orc::parallelFor(n_src, threads, [&](uint32_t i, int th) {
+    const std::string& s = t.names[srcs[i]];
+    const auto bitOf = orc::nbrBits(ls, s);
+    const uint32_t words = ((uint32_t)bitOf.size() + 31) / 32;
+    uint64_t h = 0;
+    if (int_path) {
+      std::vector<int32_t> bits(n, -1);
+      for (const auto& kv : bitOf) bits[t.id.at(kv.first)] = (int32_t)kv.second;
+      orc::IntSpf& sp = scratch[th];
+      sp.words = words;
+      sp.run(*g, srcs[i], UINT32_MAX, ulm != 0, bits);
+      for (uint32_t v = 0; v < n; ++v)
+        if (sp.dist[v] != UINT64_MAX)
+          h += orc::nodeTerm(v, sp.dist[v], &sp.nh[(size_t)v * words], words);
+    } else {
+      const orc::SpfResult r = ls.runSpf(s, ulm != 0);
+      std::vector<uint32_t> w(words);
+      for (const auto& kv : r) {
+        auto it = t.id.find(kv.first);
+        if (it == t.id.end()) continue;
+        std::fill(w.begin(), w.end(), 0u);
+        for (const auto& x : kv.second.nextHops) {
+          const uint32_t j = bitOf.at(x);
+          w[j >> 5] |= 1u << (j & 31);
+        }
+        h += orc::nodeTerm(it->second, kv.second.metric, w.data(), words);
+      }
+    }
+    out[i] = h;
+  });
+  return 0;
+}
+
+// The same digest over GPU output (include/openr_spf.h plan layout): dist =
+// [n_src][n] u32 (0xFFFFFFFF unreachable), next hops planar: neighbour j of
+// source i in nh(v) <=> nh[nh_off[i] + j*(pitch/32) + v/32] bit v%32, k[i]
+// neighbours.
+int orc_digest_planar(uint32_t n_src, uint32_t n, uint32_t pitch, const uint32_t* dist,
+                      const uint32_t* nh, const uint64_t* nh_off, const uint32_t* k,
+                      int threads, uint64_t* out) {
+  orc::parallelFor(n_src, threads, [&](uint32_t i, int) {
+    const uint32_t words = (k[i] + 31) / 32;
+    const uint32_t wpm = pitch / 32;
+    std::vector<uint32_t> w(words);
+    uint64_t h = 0;
+    for (uint32_t v = 0; v < n; ++v) {
+      const uint32_t d = dist[(size_t)i * n + v];
+      if (d == 0xFFFFFFFFu) continue;
+      std::fill(w.begin(), w.end(), 0u);
+      for (uint32_t j = 0; j < k[i]; ++j)
+        if ((nh[nh_off[i] + (size_t)j * wpm + v / 32] >> (v % 32)) & 1u) w[j >> 5] |= 1u << (j & 31);
+      h += orc::nodeTerm(v, d, w.data(), words);
+    }
+    out[i] = h;
+  });
+  return 0;
+}
+
+// KSP2 digests: for each source, getKthPaths(src, d, 1) and (src, d, 2)
+// (LinkState.cpp:762-791) for every d of the node table, each pair reduced
+// with pairDigest, the source's value = sum over d of
+// mix64(pairDigest + mix64(d + 1)).  pair_out (may be NULL) = [n_src][n].
+// k = 1 traces the source's SPF; k = 2 re-runs it without every link of the
+// k = 1 paths -- what kthPaths does, without its memo, so threads can share
+// the (read-only) LinkState.
+int orc_ls_ksp2_digests(orc_ls* p, const char* blob, const uint32_t* off, const uint32_t* len,
+                        uint32_t n, const uint32_t* srcs, uint32_t n_src, int threads,
+                        uint64_t* src_out, uint64_t* pair_out) {
+  const orc::NameIds t(blob, off, len, n);
+  const orc::LinkState& ls = p->ls;
+  orc::parallelFor(n_src, threads, [&](uint32_t i, int) {
+    const std::string& s = t.names[srcs[i]];
+    const orc::SpfResult r1 = ls.runSpf(s, true);
+    uint64_t acc = 0;
+    for (uint32_t d = 0; d < n; ++d) {
+      const std::string& dst = t.names[d];
+      std::vector<orc::Path> lists[2];
+      auto traceAll = [&](const orc::SpfResult& r, std::vector<orc::Path>& outp) {
+        if (!r.count(dst)) return;
+        orc::LinkSet visited;
+        auto pth = ls.trace(s, dst, r, visited);
+        while (pth && !pth->empty()) {
+          outp.push_back(std::move(*pth));
+          pth = ls.trace(s, dst, r, visited);
+        }
+      };
+      traceAll(r1, lists[0]);
+      orc::LinkSet ignore;
+      for (const auto& pth : lists[0])
+        for (const auto& l : pth) ignore.insert(l);
+      if (ignore.empty()) {
+        traceAll(r1, lists[1]);
+      } else {
+        traceAll(ls.runSpf(s, true, ignore), lists[1]);
+      }
+      const uint64_t pd = orc::pairDigest(lists);
+      if (pair_out) pair_out[(size_t)i * n + d] = pd;
+      acc += mix64(pd + mix64((uint64_t)d + 1));
+    }
+    src_out[i] = acc;
+  });
+  return 0;
+}
+
+// The same reduction over GPU KSP2 output (spf_ksp2_pair records + path pool
+// of link ids; link_hash[id] = orc_link_keyhash of that link's ordered key).
+int orc_digest_ksp2(uint32_t n_src, uint32_t n, const uint32_t* pairs /* [n_src*n][4] */,
+                    const uint32_t* pool, const uint64_t* link_hash, int threads,
+                    uint64_t* src_out, uint64_t* pair_out) {
+  orc::parallelFor(n_src, threads, [&](uint32_t i, int) {
+    uint64_t acc = 0;
+    for (uint32_t d = 0; d < n; ++d) {
+      const uint32_t* rec = pairs + ((size_t)i * n + d) * 4;
+      uint64_t h = 0xcbf29ce484222325ULL;
+      for (int k = 0; k < 2; ++k) {
+        h = orc::fnvFeed(h, 0x1000 + rec[2 + k]);
+        uint32_t at = rec[k];
+        for (uint32_t q = 0; q < rec[2 + k]; ++q) {
+          const uint32_t len = pool[at];
+          h = orc::fnvFeed(h, 0x2000 + len);
+          for (uint32_t x = 0; x < len; ++x) h = orc::fnvFeed(h, link_hash[pool[at + 2 + x]]);
+          at = pool[at + 1];
+        }
+      }
+      if (pair_out) pair_out[(size_t)i * n + d] = h;
+      acc += mix64(h + mix64((uint64_t)d + 1));
+    }
+    src_out[i] = acc;
+  });
+  return 0;
+}
+
+// What-if digests on the integer restatement (same contract as
+// orc_ls_whatif_digests with fast != 0), `threads` host threads.
+int orc_ls_whatif_int(orc_ls* p, const char* blob, const uint32_t* off, const uint32_t* len,
+                      uint32_t n, const char* src, const char* const* fail_nodes,
+                      const char* const* fail_ifs, uint32_t n_fail, int threads,
+                      orc_digest* base_out, orc_digest* out) {
+  const orc::NameIds t(blob, off, len, n);
+  const orc::LinkState& ls = p->ls;
+  const orc::IntGraph g(ls, t);
+  std::unordered_map<const orc::Link*, uint32_t> lidx;
+  for (uint32_t i = 0; i < g.links.size(); ++i) lidx.emplace(g.links[i], i);
+  std::vector<uint32_t> fail(n_fail);
+  for (uint32_t i = 0; i < n_fail; ++i) {
+    fail[i] = UINT32_MAX;
+    for (const auto& l : ls.linksFrom(fail_nodes[i]))
+      if (l->ifaceFrom(fail_nodes[i]) == fail_ifs[i]) {
+        fail[i] = lidx.at(l.get());
+        break;
+      }
+    if (fail[i] == UINT32_MAX) return -1 - (int)i;
+  }
+  const std::string s(src);
+  const uint32_t sid = t.id.at(s);
+  const auto bitOf = orc::nbrBits(ls, s);
+  const uint32_t words = ((uint32_t)bitOf.size() + 31) / 32;
+  std::vector<int32_t> bits(n, -1);
+  for (const auto& kv : bitOf) bits[t.id.at(kv.first)] = (int32_t)kv.second;
+  orc::IntSpf base;
+  base.words = words;
+  base.run(g, sid, UINT32_MAX, true, bits);
+  auto digest = [&](const orc::IntSpf& b, const orc::IntSpf& f) {
+    orc_digest dg{0, 0, 0};
+    for (uint32_t v = 0; v < n; ++v) {
+      const uint32_t* a = &b.nh[(size_t)v * words];
+      const uint32_t* c = &f.nh[(size_t)v * words];
+      if (b.dist[v] != f.dist[v]) ++dg.n_dist_changed;
+      if ((b.dist[v] == UINT64_MAX) != (f.dist[v] == UINT64_MAX) || !std::equal(a, a + words, c))
+        ++dg.n_nh_changed;
+      if (f.dist[v] != UINT64_MAX) dg.hash += orc::nodeTerm(v, f.dist[v], c, words);
+    }
+    return dg;
+  };
+  if (base_out) *base_out = digest(base, base);
+  std::vector<orc::IntSpf> scratch(std::max(1, threads));
+  orc::parallelFor(n_fail, threads, [&](uint32_t i, int th) {
+    orc::IntSpf& sp = scratch[th];
+    sp.words = words;
+    sp.run(g, sid, fail[i], true, bits);
+    out[i] = digest(base, sp);
+  });
+  return 0;
 }
 
 }  // extern "C"

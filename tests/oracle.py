@@ -252,3 +252,120 @@ def sr_nexthops(orc: "OracleLinkState", me: str, dsts: Dict[str, Optional[int]],
     raw = lib.orc_ls_sr_nexthops_json(orc._h, me.encode(), arr, pre, len(names), int(lfa),
                                       int(v4), int(ksp2))
     return json.loads(raw)["nh"]
+
+
+# ---- full-size parity digests (oracle/spf_oracle.cpp, "Full-size parity digests") ----
+_u32p, _u64p = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+lib.orc_link_keyhash.restype = C.c_uint64
+lib.orc_link_keyhash.argtypes = [C.c_char_p] * 4
+lib.orc_ls_source_digests.restype = C.c_int
+lib.orc_ls_source_digests.argtypes = [C.c_void_p, C.c_char_p, _u32p, _u32p, C.c_uint32, _u32p,
+                                      C.c_uint32, C.c_int, C.c_int, C.c_int, _u64p]
+lib.orc_digest_planar.restype = C.c_int
+lib.orc_digest_planar.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p, _u64p, _u32p,
+                                  C.c_int, _u64p]
+lib.orc_ls_ksp2_digests.restype = C.c_int
+lib.orc_ls_ksp2_digests.argtypes = [C.c_void_p, C.c_char_p, _u32p, _u32p, C.c_uint32, _u32p,
+                                    C.c_uint32, C.c_int, _u64p, _u64p]
+lib.orc_digest_ksp2.restype = C.c_int
+lib.orc_digest_ksp2.argtypes = [C.c_uint32, C.c_uint32, _u32p, _u32p, _u64p, C.c_int, _u64p, _u64p]
+lib.orc_ls_whatif_int.restype = C.c_int
+lib.orc_ls_whatif_int.argtypes = [C.c_void_p, C.c_char_p, _u32p, _u32p, C.c_uint32, C.c_char_p,
+                                  C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_uint32,
+                                  C.c_int, C.POINTER(OrcDigest), C.POINTER(OrcDigest)]
+
+
+def host_threads() -> int:
+    import os
+
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1),
+                      os.cpu_count() or 1, 16))
+
+
+def link_keyhash(key: Sequence[str]) -> int:
+    """Hash of a link's ordered key [n1, if1, n2, if2] (helpers.link_key)."""
+    return int(lib.orc_link_keyhash(*[s.encode() for s in key]))
+
+
+def source_digests(orc: "OracleLinkState", table: NameTable, srcs: Sequence[int],
+                   ulm: bool = True, int_path: bool = False, threads: int = 0) -> np.ndarray:
+    """u64 digest of runSpf(src) per source (ids into `table`)."""
+    srcs = np.ascontiguousarray(srcs, np.uint32)
+    out = np.zeros(max(1, len(srcs)), np.uint64)
+    lib.orc_ls_source_digests(orc._h, table.blob, _p(table.offs), _p(table.lens), table.n,
+                              _p(srcs), len(srcs), int(ulm), int(int_path),
+                              threads or host_threads(), _p(out, C.c_uint64))
+    return out[: len(srcs)]
+
+
+def digest_planar(dist: np.ndarray, nh: np.ndarray, nh_off: np.ndarray, k: np.ndarray,
+                  pitch: int, threads: int = 0) -> np.ndarray:
+    """The same digest over the engine's output layout (dist [n_src, n] u32)."""
+    dist = np.ascontiguousarray(dist, np.uint32)
+    nh = np.ascontiguousarray(nh, np.uint32)
+    nh_off = np.ascontiguousarray(nh_off, np.uint64)
+    k = np.ascontiguousarray(k, np.uint32)
+    n_src, n = dist.shape
+    out = np.zeros(max(1, n_src), np.uint64)
+    lib.orc_digest_planar(n_src, n, pitch, _p(dist), _p(nh), _p(nh_off, C.c_uint64), _p(k),
+                          threads or host_threads(), _p(out, C.c_uint64))
+    return out[:n_src]
+
+
+def ksp2_digests(orc: "OracleLinkState", table: NameTable, srcs: Sequence[int],
+                 pairs: bool = False, threads: int = 0):
+    """Per-source digest of getKthPaths(src, d, 1|2) over every d; with
+    pairs=True also the per-pair digests [n_src, n]."""
+    srcs = np.ascontiguousarray(srcs, np.uint32)
+    out = np.zeros(max(1, len(srcs)), np.uint64)
+    pout = np.zeros((len(srcs), table.n), np.uint64) if pairs else None
+    lib.orc_ls_ksp2_digests(orc._h, table.blob, _p(table.offs), _p(table.lens), table.n,
+                            _p(srcs), len(srcs), threads or host_threads(), _p(out, C.c_uint64),
+                            _p(pout, C.c_uint64) if pairs else None)
+    return (out[: len(srcs)], pout) if pairs else out[: len(srcs)]
+
+
+def digest_ksp2(pairs: np.ndarray, pool: np.ndarray, n_src: int, n: int,
+                link_hash: np.ndarray, with_pairs: bool = False, threads: int = 0):
+    """The same reduction over engine KSP2 output (spf_ksp2_pair records)."""
+    pr = np.ascontiguousarray(pairs).view(np.uint32)
+    pool = np.ascontiguousarray(pool, np.uint32)
+    if pool.size == 0:
+        pool = np.zeros(1, np.uint32)
+    lh = np.ascontiguousarray(link_hash, np.uint64)
+    out = np.zeros(max(1, n_src), np.uint64)
+    pout = np.zeros((n_src, n), np.uint64) if with_pairs else None
+    lib.orc_digest_ksp2(n_src, n, _p(pr), _p(pool), _p(lh, C.c_uint64), threads or host_threads(),
+                        _p(out, C.c_uint64), _p(pout, C.c_uint64) if with_pairs else None)
+    return (out[:n_src], pout) if with_pairs else out[:n_src]
+
+
+def whatif_digests_int(orc: "OracleLinkState", table: NameTable, src: str,
+                       fails: Sequence[tuple], threads: int = 0):
+    """whatif_digests on the integer-CSR restatement, multi-threaded; returns
+    (base tuple, structured DIGEST array [n])."""
+    n = len(fails)
+    fn = (C.c_char_p * max(1, n))(*[f[0].encode() for f in fails])
+    fi = (C.c_char_p * max(1, n))(*[f[1].encode() for f in fails])
+    base = OrcDigest()
+    out = (OrcDigest * max(1, n))()
+    rc = lib.orc_ls_whatif_int(orc._h, table.blob, _p(table.offs), _p(table.lens), table.n,
+                               src.encode(), fn, fi, n, threads or host_threads(), C.byref(base),
+                               out)
+    assert rc == 0, f"failed link {-rc - 1} not found"
+    arr = np.frombuffer(out, dtype=np.dtype([("n_dist_changed", "<u4"), ("n_nh_changed", "<u4"),
+                                             ("hash", "<u8")]), count=n).copy()
+    return (int(base.n_dist_changed), int(base.n_nh_changed), int(base.hash)), arr
+
+
+lib.orc_keyvals_order.restype = C.c_uint32
+lib.orc_keyvals_order.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, _u32p]
+
+
+def keyvals_order(keys: Sequence[str]) -> List[int]:
+    """Wire indices of a publication's keyVals in the order the reference's
+    std::unordered_map visits them (Decision.cpp:1726)."""
+    arr = (C.c_char_p * max(1, len(keys)))(*[k.encode() for k in keys])
+    out = np.zeros(max(1, len(keys)), np.uint32)
+    k = lib.orc_keyvals_order(arr, len(keys), _p(out))
+    return [int(x) for x in out[:k]]

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from helpers import link_key, spf_canonical
-from oracle import OracleLinkState
+from oracle import OracleLinkState, keyvals_order
 from openr_amd import topology as T
 from openr_amd.link_state import LinkState
 from openr_amd.lsdb import pack
@@ -20,6 +20,12 @@ pytestmark = pytest.mark.gpu
 def _pub(dbs, expired=()):
     return encode_publication([(f"adj:{d.thisNodeName}", encode_adjacency_database(d)) for d in dbs],
                               expired=[f"adj:{n}" for n in expired])
+
+
+def _ref_order(dbs):
+    """The databases of one publication in the order the reference applies
+    them (its keyVals unordered_map, Decision.cpp:1726)."""
+    return [dbs[i] for i in keyvals_order([f"adj:{d.thisNodeName}" for d in dbs])]
 
 
 @pytest.mark.parametrize("name,make", [
@@ -37,7 +43,8 @@ def test_link_state_from_publications_matches_oracle(name, make):
     for i in range(0, len(dbs), 64):
         ls.processPublication(_pub(dbs[i:i + 64]))
     orc = OracleLinkState()
-    orc.update_packed(topo.lsdb)
+    for i in range(0, len(dbs), 64):
+        orc.update_packed(pack(_ref_order(dbs[i:i + 64])))
     rng = np.random.default_rng(2)
     sample = [topo.nodes[int(i)] for i in rng.choice(len(topo.nodes), min(8, len(topo.nodes)), replace=False)]
     for s in sample:
@@ -58,3 +65,39 @@ def test_link_state_from_publications_matches_oracle(name, make):
         if s in gone:
             continue
         assert spf_canonical(ls.getSpfResult(s)) == orc.spf(s), s
+
+
+def test_ordered_fib_holds_match_oracle():
+    """enable_ordered_fib_programming (Decision.cpp:1750-1758): a publication
+    that changes metrics and drains a node is applied with per-database
+    hold-up = hops(me, originator), hold-down = maxHops(originator) - hold-up;
+    until the holds expire SPF still sees the old values."""
+    topo = T.random_graph(40, 90, 8, max_metric=6, parallel_frac=0.2)
+    dbs = unpack(topo.lsdb)
+    for d in dbs:
+        d.area = "0"
+    me = dbs[0].thisNodeName
+    ls = LinkState()
+    ls.processPublication(_pub(dbs))
+    orc = OracleLinkState()
+    orc.update_packed(pack(_ref_order(dbs)))
+    changed = []
+    for d in dbs[3:9]:
+        for a in d.adjacencies:
+            a.metric += 2
+        changed.append(d)
+    changed[1].isOverloaded = True
+    ls.processPublication(_pub(changed), orderedFibNode=me)
+    for d in _ref_order(changed):
+        hops = orc.metric_a_to_b(me, d.thisNodeName, False)
+        up = hops if hops is not None else 0
+        down = orc.max_hops(d.thisNodeName) - up if hops is not None else 0
+        orc.update_packed(pack([d]), up, down)
+    assert ls.hasHolds() == orc.has_holds()
+    for step in range(8):
+        for s in (me, dbs[5].thisNodeName, dbs[20].thisNodeName):
+            assert spf_canonical(ls.getSpfResult(s)) == orc.spf(s), (step, s)
+        if not orc.has_holds():
+            break
+        c = ls.decrementHolds()
+        assert (c.topologyChanged, ) == (orc.decrement_holds()[0], )

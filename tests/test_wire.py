@@ -40,7 +40,7 @@ def test_known_answer_adjacency_database():
     ])
     db = decode_adjacency_database(buf)
     assert db.thisNodeName == "a" and db.isOverloaded and db.nodeLabel == 300
-    assert db.area == "0"  # IDL default
+    assert db.area == ""  # no declared default (Lsdb.thrift:128)
     (a,) = db.adjacencies
     assert (a.otherNodeName, a.ifName, a.metric) == ("b", "i1", -3)
     # field 11 arrived with a foreign type (i32, not string): skipped, default kept
@@ -129,10 +129,12 @@ def test_publication_semantics():
         flood_root="r")
     p = decode_publication(pub)
     assert p.area == "spine" and p.skipped == 1
-    assert [d.thisNodeName for d in p.adjacencyDbs] == ["n1", "n2"]
-    for got, want in zip(p.adjacencyDbs, (d1, d2)):
+    # keyVals iteration order of the reference (see the order test below)
+    got = {d.thisNodeName: d for d in p.adjacencyDbs}
+    assert sorted(got) == ["n1", "n2"]
+    for name, want in (("n1", d1), ("n2", d2)):
         want.area = "spine"
-        assert got == want
+        assert got[name] == want
     assert p.expiredNodes == ["gone", ""]
     # area before the key-values (non-IDL order) and the IDL default area
     assert decode_publication(encode_publication([("adj:n1", encode_adjacency_database(d1))],
@@ -162,11 +164,15 @@ def test_link_state_from_publications_equals_direct_updates():
     topo = T.fabric(1000, full=False)
     from openr_amd.wire import unpack
 
+    from oracle import keyvals_order
+
     dbs = unpack(topo.lsdb)
     direct = LinkState(device=-1)
-    direct.updateAdjacencyDatabases(dbs)
     wire = LinkState(device=-1)
     chunks = [dbs[i:i + 97] for i in range(0, len(dbs), 97)]
+    for ch in chunks:  # each publication in the reference's keyVals order
+        direct.updateAdjacencyDatabases(
+            [ch[i] for i in keyvals_order([f"adj:{d.thisNodeName}" for d in ch])])
     for ch in chunks:
         pub = encode_publication([(f"adj:{d.thisNodeName}", encode_adjacency_database(d)) for d in ch])
         c = wire.processPublication(pub)
@@ -185,3 +191,27 @@ def test_link_state_from_publications_equals_direct_updates():
     # a publication of another area is refused
     with pytest.raises(N.SpfError, match="area"):
         wire.processPublication(encode_publication([], area="other"))
+
+
+def test_publication_databases_follow_reference_keyvals_order():
+    """Databases come out in the iteration order of the reference's
+    keyVals container (std::unordered_map<std::string, Value>,
+    KvStore.thrift:43-44, Decision.cpp:1726), not in wire order; TTL-only and
+    non-adj keys take part in the container but yield no database."""
+    from oracle import keyvals_order
+
+    rng = np.random.default_rng(11)
+    for n in (1, 2, 5, 13, 14, 40, 97):
+        names = [f"node{int(x)}" for x in rng.choice(10 ** 6, n, replace=False)]
+        kv = []
+        for i, nm in enumerate(names):
+            db = AdjacencyDatabase(thisNodeName=nm, adjacencies=[], nodeLabel=i, area="0")
+            kv.append((f"adj:{nm}", encode_adjacency_database(db)))
+            if i % 3 == 0:
+                kv.append((f"prefix:{nm}", b"x"))
+            if i % 4 == 1:
+                kv.append((f"adj:ttl{nm}", None))
+        pub = decode_publication(encode_publication(kv))
+        want = [kv[i][0][4:] for i in keyvals_order([k for k, _ in kv])
+                if kv[i][0].startswith("adj:") and kv[i][1] is not None]
+        assert [d.thisNodeName for d in pub.adjacencyDbs] == want

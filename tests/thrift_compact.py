@@ -184,7 +184,7 @@ def encode_adjacency_database(db, omit_defaults: bool = False, unknown: bool = F
         w.f_i64(3, 1600000000000)
         w.struct_end()
         w.struct_end()
-    if not (omit_defaults and db.area == "0"):
+    if not (omit_defaults and db.area == ""):
         w.f_binary(6, db.area)
     if unknown:
         _unknown_fields(w, 20)
