@@ -4,16 +4,21 @@ fabric (BASELINE.json configs[2]; metric "all-sources SPF solves/sec + GTEPS,
 10k-node fabric, 1/2/4/8 MI355X").
 
 Default workload (fabric_full): a step = one all-sources pass, every node of
-the rank's LSDB snapshot solved as a source (distances + ECMP next-hop
-bitsets, bit-exact with the reference's LinkState::runSpf,
-openr/decision/LinkState.cpp:808-882), results resident in HBM.  Scaling is
-weak: rank r solves its own LSDB snapshot -- the fabric with rack switch r's
-overload bit toggled, the perturbation the reference's BM_DecisionFabric
-applies per iteration (RoutingBenchmarkUtils.cpp:406-447) -- so per-GPU work
-is fixed and no collective touches the data path.
+the fabric solved as a source (distances + ECMP next-hop bitsets, bit-exact
+with the reference's LinkState::runSpf, openr/decision/LinkState.cpp:808-882).
+With --gpus N the sources are split over the N ranks (contiguous id blocks
+balanced by next-hop work, sharding.AllSourcesLayout) and every rank's
+distance rows and next-hop bitmaps are gathered to rank 0 over RCCL inside
+the step, so rank 0 holds the whole-graph result (strong scaling: the work
+per step is fixed).  --scaling weak instead gives rank r its own LSDB
+snapshot (rack switch r drained, BM_DecisionFabric's per-iteration
+perturbation, RoutingBenchmarkUtils.cpp:406-447) and leaves results on each
+GPU.
 
 Other BASELINE configs (--workload):
-  grid100    configs[1]: all-sources SPF + ECMP on grid 100x100 (weak, as above)
+  grid100    configs[1]: all-sources SPF + ECMP on grid 100x100 (as above)
+  fabric_ref the reference generator's fabric (per-pod emplace quirk kept)
+  fabric_rtt fabric_full wiring with RTT-derived metrics: the weighted path
   wan_ksp2   configs[3]: getKthPaths(s, d, 1) and (s, d, 2) for ALL pairs of the
              2000-node WAN graph; sources sharded over ranks (strong scaling),
              every rank's paths gathered to rank 0 with RCCL inside the step.
@@ -59,17 +64,27 @@ def oracle():
 
 
 class AllSources:
-    """configs[1]/[2]: one all-sources SPF + ECMP pass per step (weak scaling)."""
+    """configs[1]/[2]: one all-sources SPF + ECMP pass per step.
 
-    scaling = "weak"
+    strong (default): one LSDB, its sources split over the ranks in
+    contiguous id blocks balanced by next-hop work
+    (sharding.AllSourcesLayout), each rank writing its results straight into
+    a send buffer that is gathered to rank 0 over RCCL inside the step -- the
+    whole-graph result (every source's distance row and next-hop bitmaps)
+    ends on rank 0.  Send buffers alternate between two steps, so step t+1's
+    kernels overlap step t's gather; the timed region ends after the last
+    gather.  weak (--scaling weak): rank r solves its own LSDB snapshot
+    (rack switch r drained, BM_DecisionFabric's per-iteration perturbation,
+    RoutingBenchmarkUtils.cpp:406-447), results stay on each GPU."""
+
     unit = "solves/s"
-    kernels = ("sssp_kernel", "ecmp_kernel")
 
-    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb,
+                 scaling: str = "strong"):
         import torch
 
         from openr_amd import topology as T
-        from openr_amd.sharding import snapshot_for_rank
+        from openr_amd.sharding import AllSourcesLayout, snapshot_for_rank
 
         if name == "fabric_full":
             topo = T.fabric(10000, full=True)
@@ -77,43 +92,79 @@ class AllSources:
         elif name == "fabric_ref":
             topo = T.fabric(10000, full=False)
             self.desc = "fabric_ref numOfSws=10000 (reference generator incl. per-pod emplace quirk)"
+        elif name == "fabric_rtt":
+            sys.path.insert(0, str(ROOT / "tests" / "golden"))
+            from make_fullsize_digests import fabric_rtt
+
+            topo = fabric_rtt()
+            self.desc = ("fabric_full wiring, per-direction metrics max(rtt/100,1) from seeded RTTs "
+                         "(LinkMonitor.cpp:44-47), weighted SPF")
         else:
             topo = T.grid(100)
             self.desc = "grid 100x100 (RoutingBenchmarkUtils.cpp:161-240)"
-        # rank r's snapshot: one node drained, as BM_Decision* toggles per iteration
-        topo.lsdb = snapshot_for_rank(topo.lsdb, rank)
+        self.scaling = scaling
+        if scaling == "weak":  # rank r's snapshot: one node drained
+            topo.lsdb = snapshot_for_rank(topo.lsdb, rank)
         self.topo = topo
         names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
         self.n, self.e = len(names), len(col)
         eng = eng_cls(dev.index)
         eng.load(rp, col, met, lid, ovl)
-        self.eng = eng
-        self.plan = eng.plan(list(range(self.n)))
-        self.d_dist = torch.empty(self.n * eng.pitch, dtype=torch.int32, device=dev)
-        self.d_nh = torch.empty(max(1, self.plan.nh_words), dtype=torch.int32, device=dev)
-        self.units = self.n
-        self.world = world
-        # B_solve = 4(N+1) + 8E + N + 4N + N*ceil(deg(src)/8)
-        nbr = np.array([len(eng.neighbors(s)) for s in range(self.n)], np.int64)
+        self.eng, self.rank, self.world, self.dev = eng, rank, world, dev
+        k = np.array([len(eng.neighbors(s)) for s in range(self.n)], np.int64)
+        pitch = eng.pitch
+        gather = scaling == "strong" and world > 1
+        self.layout = AllSourcesLayout(k, pitch, world if gather else 1)
+        srcs = self.layout.srcs[rank if gather else 0]
+        self.plan = eng.plan(srcs)
+        assert np.array_equal(self.plan.nh_off, self.layout.plan_nh_off(rank if gather else 0))
+        cap = self.layout.cap
+        self.dist_words = len(srcs) * pitch
+        self.nbuf = 2 if gather else 1
+        self.send = [torch.zeros(max(1, cap), dtype=torch.int32, device=dev)
+                     for _ in range(self.nbuf)]
+        self.recv = ([torch.zeros((world, max(1, cap)), dtype=torch.int32, device=dev)
+                      for _ in range(self.nbuf)] if gather and rank == 0 else None)
+        self.works = [None] * self.nbuf
+        self.gather = gather
+        self.i = 0
+        self.units = len(srcs)
+        self.gather_bytes = 4 * sum(self.layout.words) if gather else 0
+        # SURVEY.md §8(d) per-solve figure (one CSR sweep charged per solve)
         n, e = self.n, self.e
-        self.bytes_launch = int(n * (4 * (n + 1) + 8 * e + n + 4 * n)
-                                + n * int(np.sum((nbr + 7) // 8)))
-        # the kernels the plan runs (multi-source BFS for unit metrics, one of
-        # two variants; per-source SSSP otherwise) and the next-hop row width
+        self.survey_bytes = int(len(srcs) * (4 * (n + 1) + 8 * e + n + 4 * n)
+                                + len(srcs) * int(np.sum((k[srcs] + 7) // 8)))
         bfs, narrow = self.plan.kernels()
         self.kernels = (bfs, "ecmp_kernel")
         self.narrow = narrow
-        # compulsory HBM traffic of one pass: the outputs (dist rows, next-hop
-        # bitmaps) plus the u8 narrow rows, when used, written once and read
-        # at least once
-        npitch = (n + 1023) // 1024 * 1024
-        self.floor_launch = int(n * eng.pitch * 4 + self.plan.nh_words * 4
-                                + (2 * n * npitch if narrow else 0))
-        self.parallelism = (f"source-sharded over {world} rank(s): one LSDB snapshot per rank, "
-                            "no data-path collective")
+        tb, te = self.plan.traffic()
+        self.kernel_bytes = {bfs: tb, "ecmp_kernel": te}
+        self.parallelism = (
+            f"sources in contiguous id blocks over {world} rank(s) (one LSDB), plan closure "
+            f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source dist rows + "
+            f"next-hop bitmaps gathered to rank 0 over RCCL in the step "
+            f"({self.gather_bytes / 1e6:.0f} MB/step, send buffers double-buffered)"
+            if gather else
+            "one rank, all sources" if scaling == "strong" else
+            f"weak: one LSDB snapshot per rank ({world} ranks), results stay on each GPU")
 
     def step(self, stream) -> None:
-        self.plan.execute_torch(self.d_dist, self.d_nh, stream)
+        import torch.distributed as dist
+
+        b = self.i % self.nbuf
+        self.i += 1
+        if self.works[b] is not None:  # the gather that last read this buffer
+            self.works[b].wait()
+        buf = self.send[b]
+        self.plan.execute(buf.data_ptr(), buf.data_ptr() + 4 * self.dist_words, stream.cuda_stream)
+        if self.gather:
+            out = list(self.recv[b].unbind(0)) if self.rank == 0 else None
+            self.works[b] = dist.gather(buf, out, dst=0, async_op=True)
+
+    def finish(self) -> None:
+        for w in self.works:
+            if w is not None:
+                w.wait()
 
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
@@ -229,7 +280,7 @@ class Ksp2AllPairs:
         # + 4 B per output link; the k = 1 SPF rows are charged per source.
         n, e = self.n, self.e
         self.b_solve = 4 * (n + 1) + 8 * e + n + 4 * n
-        self.bytes_launch = None  # known after the first execute (output links)
+        self.survey_bytes = None  # known after the first execute (output links)
         self.parallelism = (f"sources dealt round-robin over {world} rank(s), graph replicated; "
                             "pair headers + path pools gathered to rank 0 (RCCL gather) in the step")
 
@@ -256,9 +307,19 @@ class Ksp2AllPairs:
         if cnt_h[2] & 1:
             raise SystemExit("KSP2 path pool overflowed: raise pool_words")
         # path pool words = records [len, next, links]; output links ~ words
-        self.bytes_launch = int(self.units * self.b_solve + len(self.srcs) * self.b_solve
+        self.survey_bytes = int(self.units * self.b_solve + len(self.srcs) * self.b_solve
                                 + 4 * int(cnt_h[0]))
         self.k2_runs = int(cnt_h[1])
+        # compulsory bytes: the k = 1 SPF reads the CSR once per source and
+        # writes a distance row; the KSP2 kernel stages the graph once per
+        # block (destination x 64-source chunk) and writes the pair records
+        # and path pool once
+        n, e = self.n, self.e
+        csr = 4 * (n + 1) + 12 * e
+        blocks = n * ((len(self.srcs) + 63) // 64)
+        self.kernel_bytes = {
+            "sssp_kernel": len(self.srcs) * (4 * (n + 1) + 8 * e + n + 4 * self.eng.pitch),
+            "ksp2_kernel": blocks * csr + 16 * self.units + 4 * int(cnt_h[0])}
         return {"sssp_kernel": a / max(cnt, 1), "ksp2_kernel": b / max(cnt, 1)}
 
     def edges_per_unit(self) -> int:
@@ -321,7 +382,16 @@ class WhatIfAllLinks:
         # a what-if solve is B_solve with a 24 B digest in
         # place of the dense result: 4(N+1) + 8E + N + 24
         n, e = self.n, self.e
-        self.bytes_launch = int((self.units + 1) * (4 * (n + 1) + 8 * e + n + 24))
+        self.survey_bytes = int((self.units + 1) * (4 * (n + 1) + 8 * e + n + 24))
+        # compulsory bytes: the unfailed pass reads the CSR (row_ptr, col,
+        # metric, link id) once and writes distances + next-hop rows; the
+        # failure pass reads the failure list and the CSR once and writes a
+        # 16-byte digest per failure (affected regions re-read the CSR, which
+        # is repair work, not charged)
+        csr = 4 * (n + 1) + 12 * e + n
+        words = (len(eng.neighbors(self.src)) + 31) // 32
+        self.kernel_bytes = {"base": csr + 4 * n + 4 * words * n,
+                             "failures": csr + 4 * self.units + 16 * self.units}
         self.parallelism = (f"failures dealt round-robin over {world} rank(s), graph replicated, "
                             "unfailed SPF recomputed per rank; digests gathered to rank 0 "
                             "(RCCL gather) in the step")
@@ -369,6 +439,7 @@ class WhatIfAllLinks:
 
 
 WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
+             "fabric_rtt": AllSources,
              "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks}
 
 
@@ -380,6 +451,10 @@ def main() -> None:
     ap.add_argument("--workload", default="fabric_full", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of CPU-baseline sampling (0 disables)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="all-sources workloads: split one LSDB's sources over ranks and "
+                         "gather the results to rank 0 (strong), or one LSDB snapshot per "
+                         "rank with results left on each GPU (weak)")
     args = ap.parse_args()
 
     import torch
@@ -395,11 +470,16 @@ def main() -> None:
 
     from openr_amd.engine import SpfEngine, graph_from_lsdb
 
-    wl = WORKLOADS[args.workload](args.workload, rank, world, dev, SpfEngine, graph_from_lsdb)
+    cls = WORKLOADS[args.workload]
+    if cls is AllSources:
+        wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb, scaling=args.scaling)
+    else:
+        wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb)
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
         wl.step(stream)
+    getattr(wl, "finish", lambda: None)()
     torch.cuda.synchronize(dev)
     wl.enable_timing(max(1, args.steps))
 
@@ -409,6 +489,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step(stream)
+    getattr(wl, "finish", lambda: None)()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -429,13 +510,21 @@ def main() -> None:
     value = units * args.steps / elapsed
     gteps = units * wl.edges_per_unit() * args.steps / elapsed / 1e9
 
-    achieved = wl.bytes_launch / (launch_ms * 1e-3) / 1e9
+    # roofline of the dominant kernel: the bytes it must move (its structure's
+    # compulsory traffic, wl.kernel_bytes) over its HIP-event time
     dominant = max(kms, key=kms.get)
-    traffic = None
+    kbytes = wl.kernel_bytes
+    achieved = kbytes[dominant] / (kms[dominant] * 1e-3) / 1e9
+    traffic, traffic_src = None, None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            pj = json.loads(pmc.read_text())
+            for kname, kv in pj.get("per_kernel", {}).items():
+                if kname.startswith(dominant):
+                    traffic = kv["fetch_bytes_x2"] + kv["write_bytes"]
+                    traffic_src = (f"{pmc.relative_to(ROOT)} ({pj.get('source', 'rocprofv3 --pmc')}"
+                                   f"; kernel {kname}; FETCH_SIZE x2 + WRITE_SIZE)")
         except Exception:  # noqa: BLE001
             traffic = None
 
@@ -470,23 +559,21 @@ def main() -> None:
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "+".join(wl.kernels) + " (one execute)",
-            "dominant": dominant,
+            "traffic_source": traffic_src,
+            "kernel": dominant,
             "kernel_ms": kms,
-            "algorithmic_bytes_per_launch": wl.bytes_launch,
-            # measured HBM bytes (PMC, profiles/pmc_<workload>.json) over the
-            # same launch time: the real DRAM-side utilisation
-            "traffic_gbs": traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
-            "traffic_frac": traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "kernel_bytes": kbytes,
+            # the whole execute: every kernel's compulsory bytes over their summed time
+            "execute_frac": sum(kbytes.values()) / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            # SURVEY.md §8(d)'s per-solve figure (a full CSR sweep charged to every
+            # solve) over the compulsory bytes: how much sweep work batching shares
+            "survey_bytes_per_launch": wl.survey_bytes,
+            "reuse_factor": wl.survey_bytes / sum(kbytes.values()),
         },
         "cpu_baseline": None,
     }
-    floor = getattr(wl, "floor_launch", None)
-    if floor:
-        # the outputs alone over the same launch time: how far the pass is
-        # from the bytes it must move whatever the algorithm
-        out["roofline"]["compulsory_bytes_per_launch"] = floor
-        out["roofline"]["compulsory_frac"] = floor / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    if getattr(wl, "gather", False):
+        out["config"]["gather_bytes_per_step"] = wl.gather_bytes
     if isinstance(wl, WhatIfAllLinks):
         out["config"]["hot_failures_per_rank"] = wl.n_hot
         out["config"]["workgroup_team_failures_per_rank"] = wl.n_big

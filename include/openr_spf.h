@@ -132,6 +132,12 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
  * planes, rows written once); *narrow = 1 when the next-hop pass reads u8 rows.
  * No reference counterpart (engine introspection). */
 spf_status spf_plan_kernels(const spf_plan* plan, uint32_t* bfs, uint32_t* narrow);
+/* Bytes the distance kernel and the next-hop kernel of one execute must move
+ * to or from HBM (compulsory traffic given each kernel's structure: one
+ * column sweep per BFS workgroup or per SSSP source, every output written
+ * once, every compared distance row read once).  Denominator-free roofline
+ * input for benchmarks; no reference counterpart. */
+spf_status spf_plan_traffic(const spf_plan* plan, uint64_t* bfs_bytes, uint64_t* ecmp_bytes);
 
 /* Execute on device buffers: d_dist = [n_src][pitch] u32, d_nh = nh words.
  * Enqueued on `stream` (a hipStream_t, NULL = the context's stream); no host

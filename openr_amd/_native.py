@@ -159,6 +159,7 @@ PROTOTYPES = {
     "spf_plan_nh_layout": (C.c_int, [_vp, _u64p, _u32p]),
     "spf_plan_closure_rows": (C.c_uint32, [_vp]),
     "spf_plan_kernels": (C.c_int, [_vp, _u32p, _u32p]),
+    "spf_plan_traffic": (C.c_int, [_vp, _u64p, _u64p]),
     "spf_plan_execute": (C.c_int, [_vp, _vp, _vp, _vp]),
     "spf_plan_execute_host": (C.c_int, [_vp, _u32p, _u32p]),
     "spf_plan_enable_timing": (C.c_int, [_vp, C.c_uint32]),

@@ -1403,6 +1403,41 @@ spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) 
   return SPF_OK;
 }
 
+// Bytes each kernel of one execute must move between HBM and the CUs, given
+// the kernel's own structure: what `roofline.achieved` in bench.py divides by
+// the kernel's measured time (no credit for on-chip reuse).
+//   BFS (msbfs / planes): one read of the sliced-ELL columns and the drain
+//     bytes per workgroup (a batch of sources shares one sweep per level;
+//     repeated levels hit the L2), plus the distance rows (u32, pitch) and,
+//     in narrow mode, the u8 rows (npitch) written once.
+//   SSSP (weighted, one workgroup per source): one read of row_ptr, col,
+//     metric and drain bytes per source, plus the distance row written.
+//   ECMP: every distance row it compares read once (u8 rows in narrow mode,
+//     u32 rows otherwise) plus the next-hop bitmaps written once.
+spf_status spf_plan_traffic(const spf_plan* p, uint64_t* bfs_bytes, uint64_t* ecmp_bytes) {
+  if (!p || !bfs_bytes || !ecmp_bytes) return SPF_E_INVALID;
+  const spf_ctx* c = p->ctx;
+  const uint64_t N = c->N, E = c->E, rows = p->closure.size();
+  uint64_t bfs = 0;
+  if (p->ms) {
+    const bool planes = use_planes(c);
+    const uint32_t batch = planes ? kPlBatch : kMsBatch;
+    const uint64_t rounds = (rows + (uint64_t)batch * c->n_cu - 1) / ((uint64_t)batch * c->n_cu);
+    const uint64_t bs = std::min<uint64_t>(batch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
+    const uint64_t groups = (rows + bs - 1) / bs;
+    const uint64_t n_slices = c->sell_ptr.size() - 1;
+    const uint64_t csr = planes ? 8ull * c->sell4_ptr.back() + 4ull * (n_slices + 1)
+                                : 4ull * c->sell_ptr.back() + 4ull * (n_slices + 1);
+    bfs = groups * (csr + N) + rows * c->pitch * 4ull + (p->narrow ? rows * c->npitch : 0ull);
+  } else {
+    bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch);
+  }
+  const uint64_t row_bytes = p->narrow ? c->npitch : 4ull * c->pitch;
+  *bfs_bytes = bfs;
+  *ecmp_bytes = p->nh_total ? rows * row_bytes + 4ull * p->nh_total : 0ull;
+  return SPF_OK;
+}
+
 spf_status spf_plan_nh_layout(const spf_plan* p, uint64_t* nh_off, uint32_t* words) {
   if (!p) return SPF_E_INVALID;
   for (uint32_t i = 0; i < p->n_src; ++i) {

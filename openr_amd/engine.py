@@ -91,6 +91,13 @@ class SpfPlan(NativeHandle):
         self._eng._err(N.lib.spf_plan_kernels(self._h, C.byref(bfs), C.byref(narrow)))
         return self.BFS_KERNELS[bfs.value], bool(narrow.value)
 
+    def traffic(self) -> Tuple[int, int]:
+        """Compulsory HBM bytes of (distance kernel, next-hop kernel) per
+        execute (spf_plan_traffic)."""
+        a, b = C.c_uint64(), C.c_uint64()
+        self._eng._err(N.lib.spf_plan_traffic(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def enable_timing(self, max_executes: int) -> None:
         self._eng._err(N.lib.spf_plan_enable_timing(self._h, max_executes))
 

@@ -1,20 +1,24 @@
 """Multi-GPU sharding of SPF batches (one process per GPU, torch.distributed).
 
-Two ways a node's worth of SPF work spreads over ranks:
+All-sources SPF + ECMP (the ``bench.py`` default):
+one LSDB replicated on every GPU, its sources split over ranks
+(:class:`AllSourcesLayout`), every rank solving its share and the per-source
+results -- distance rows and next-hop bitmaps in the engine's layout --
+gathered to rank 0 over RCCL (``Decision::getDecisionRouteDb`` for every
+node, Decision.cpp:1480-1500, answered from one place).  Sources go to ranks
+in contiguous blocks of node-id order balanced by next-hop work: a source's
+next hops need the distance rows of its neighbours, which the rank computes
+too (the plan's closure), and contiguous blocks keep that closure small
+where interleaving would pull in nearly every row of a fabric.
 
-* ``weak``: each rank owns an independent LSDB snapshot and solves all of its
-  sources -- the what-if / per-iteration pattern of ``BM_DecisionFabric``
-  (RoutingBenchmarkUtils.cpp:406-447: every iteration drains one rack
-  switch).  Snapshot r drains node ``(r * 7919) mod N`` (r > 0).
-* ``strong``: one LSDB, its sources interleaved over ranks (source i -> rank
-  i mod world) so per-rank cost is balanced across switch roles.
+Weak scaling over per-rank LSDB snapshots (``snapshot_for_rank``, the
+per-iteration drain of ``BM_DecisionFabric``, RoutingBenchmarkUtils.cpp:
+406-447) stays available as a labelled extra (``bench.py --scaling weak``).
 
-For all-sources SPF neither puts a collective on the data path: results stay
-in each GPU's HBM; only timings (MAX) and, for verification, 64-bit digests of
-per-source results (all_gather) cross ranks.  KSP2 (sources dealt over ranks)
-and what-if batches (failed links dealt over ranks) end with one exchange:
-``gather_padded`` moves every rank's variable-length result buffer to rank 0
-(RCCL on GPU tensors, gloo on CPU tensors in the tests).
+KSP2 (sources dealt over ranks) and what-if batches (failed links dealt over
+ranks) end with one exchange too: ``gather_padded`` moves every rank's
+variable-length result buffer to rank 0 (RCCL on GPU tensors, gloo on CPU
+tensors in the tests).
 """
 
 from __future__ import annotations
@@ -41,8 +45,83 @@ def victim_node(n_nodes: int, rank: int) -> int:
 
 
 def source_shard(n_sources: int, rank: int, world: int) -> np.ndarray:
-    """Interleaved source ids owned by `rank` (strong scaling)."""
+    """Interleaved source ids owned by `rank`."""
     return np.arange(rank, n_sources, world, dtype=np.uint32)
+
+
+class AllSourcesLayout:
+    """Where every source's result lives when the all-sources pass is split
+    over `world` ranks and gathered to rank 0.
+
+    ``k[v]`` = distinct up neighbours of v (the number of next-hop bitmaps of
+    source v, ``spf_src_neighbors``), ``pitch`` = the engine's row pitch.
+    Rank r solves ``srcs[r]`` (one plan, sources in ascending id) and writes
+    its results into one contiguous send buffer of u32 words:
+    ``[dist rows: len(srcs[r]) x pitch][next-hop bitmaps: nh_words[r]]`` --
+    exactly the plan's own output layout (``spf_plan_nh_layout``), so the
+    kernels write the send buffer directly.  Buffers are padded to
+    ``cap`` words so one ``gather`` moves them; rank 0 ends up with
+    ``world x cap`` words from which :meth:`dist_row` / :meth:`nh_block`
+    read any source's result."""
+
+    def __init__(self, k: np.ndarray, pitch: int, world: int) -> None:
+        k = np.asarray(k, np.int64)
+        n = len(k)
+        self.n, self.pitch, self.world = n, pitch, world
+        self.k = k
+        wpm = pitch // 32
+        # contiguous blocks balanced by next-hop work (k + 1 bitmaps-ish per source)
+        cost = np.cumsum(k + 1, dtype=np.float64)
+        total = cost[-1] if n else 0.0
+        bounds = [0] + [int(np.searchsorted(cost, total * r / world, side="right"))
+                        for r in range(1, world)] + [n]
+        self.srcs = [np.arange(bounds[r], bounds[r + 1], dtype=np.uint32) for r in range(world)]
+        self.rank_of = np.zeros(n, np.int64)
+        self.index_of = np.zeros(n, np.int64)
+        self.nh_off = np.zeros(n, np.int64)  # word offset within the rank's send buffer
+        self.dist_off = np.zeros(n, np.int64)
+        self.words = []
+        for r, ss in enumerate(self.srcs):
+            m = len(ss)
+            self.rank_of[ss] = r
+            self.index_of[ss] = np.arange(m)
+            self.dist_off[ss] = np.arange(m, dtype=np.int64) * pitch
+            nh_local = np.concatenate([[0], np.cumsum(k[ss] * wpm)[:-1]]).astype(np.int64) \
+                if m else np.zeros(0, np.int64)
+            self.nh_off[ss] = m * pitch + nh_local
+            self.words.append(int(m * pitch + (k[ss] * wpm).sum()))
+        self.cap = max(self.words) if self.words else 0
+
+    def plan_nh_off(self, rank: int) -> np.ndarray:
+        """The plan-relative next-hop offsets rank `rank`'s plan must report."""
+        ss = self.srcs[rank]
+        return (self.nh_off[ss] - len(ss) * self.pitch).astype(np.uint64)
+
+    def dist_row(self, recv: Sequence, s: int):
+        r = int(self.rank_of[s])
+        o = int(self.dist_off[s])
+        return recv[r][o: o + self.n]
+
+    def nh_block(self, recv: Sequence, s: int):
+        """Next-hop bitmaps of source s: k[s] rows of pitch/32 words."""
+        r = int(self.rank_of[s])
+        o = int(self.nh_off[s])
+        return recv[r][o: o + int(self.k[s]) * (self.pitch // 32)]
+
+    def dense(self, recv: Sequence):
+        """Rank 0's gathered buffers as whole-graph arrays (host numpy):
+        dist [n, n] u32 and the next-hop words with per-source offsets
+        (nh_off, k) -- the layout a single-rank plan over all sources has."""
+        dist = np.zeros((self.n, self.n), np.uint32)
+        wpm = self.pitch // 32
+        nh_off = np.concatenate([[0], np.cumsum(self.k * wpm)[:-1]]).astype(np.uint64)
+        nh = np.zeros(max(1, int((self.k * wpm).sum())), np.uint32)
+        host = [np.asarray(b.cpu() if hasattr(b, "cpu") else b).view(np.uint32) for b in recv]
+        for s in range(self.n):
+            dist[s] = self.dist_row(host, s)
+            blk = self.nh_block(host, s)
+            nh[int(nh_off[s]): int(nh_off[s]) + len(blk)] = blk
+        return dist, nh, nh_off, self.k.astype(np.uint32)
 
 
 _M1 = np.uint64(0x9E3779B97F4A7C15)

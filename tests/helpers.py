@@ -69,3 +69,23 @@ def spf_canonical(res) -> dict:
         }
         for node, r in sorted(res.items())
     }
+
+
+def planar_rows(ks, dist, mats, pitch):
+    """Oracle dense results (dist [m, n] u64, mats[i] bool [>= k_i, n]) in the
+    engine's plan layout: dist rows u32 padded to `pitch` (unreachable =
+    0xFFFFFFFF, padding 0) and next-hop bitmaps, k_i rows of pitch/32 words
+    per source, concatenated in source order."""
+    import numpy as np
+
+    m, n = dist.shape
+    d32 = np.zeros((m, pitch), np.uint32)
+    d32[:, :n] = np.where(dist == np.iinfo(np.uint64).max, 0xFFFFFFFF, dist).astype(np.uint32)
+    rows = []
+    for i in range(m):
+        for j in range(int(ks[i])):
+            row = np.zeros(pitch, bool)
+            row[:n] = mats[i][j]
+            rows.append(np.packbits(row, bitorder="little").view(np.uint32))
+    nh = np.concatenate(rows) if rows else np.zeros(0, np.uint32)
+    return d32, nh

@@ -244,3 +244,84 @@ def test_two_rank_ksp2_and_whatif_exchange_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok
+
+
+# ---- all-sources split + gather to rank 0 ------------
+def _all_sources_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    here = Path(__file__).resolve().parent
+    sys.path.insert(0, str(here))
+    sys.path.insert(0, str(here.parent))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from helpers import planar_rows
+    from oracle import OracleLinkState
+    from openr_amd import topology as T
+    from openr_amd.engine import graph_from_lsdb
+    from openr_amd.sharding import AllSourcesLayout
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        topo = T.fabric(700, full=True)
+        names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+        n = len(names)
+        pitch = (n + 63) // 64 * 64
+        k = np.array([len(set(col[rp[v]:rp[v + 1]].tolist())) for v in range(n)])
+        lay = AllSourcesLayout(k, pitch, world)
+        orc = OracleLinkState()
+        orc.update_packed(topo.lsdb)
+        # this rank's share, in the plan layout, written into the send buffer
+        srcs = lay.srcs[rank]
+        d, mats = orc.dense(names, list(srcs))
+        d32, nh = planar_rows(k[srcs], d, mats, pitch)
+        send = torch.zeros(lay.cap, dtype=torch.int32)
+        flat = np.concatenate([d32.ravel(), nh]).view(np.int32)
+        assert len(flat) == lay.words[rank]
+        send[: len(flat)] = torch.from_numpy(flat)
+        recv = [torch.zeros(lay.cap, dtype=torch.int32) for _ in range(world)] if rank == 0 else None
+        dist.gather(send, recv, dst=0)
+        if rank == 0:
+            got_d, got_nh, got_off, got_k = lay.dense(recv)
+            # the single-rank answer: every source in one plan layout
+            d_all, mats_all = orc.dense(names, list(range(n)))
+            e32, enh = planar_rows(k, d_all, mats_all, pitch)
+            q.put((np.array_equal(got_d, e32[:, :n]), np.array_equal(got_nh[: len(enh)], enh),
+                   sorted(np.concatenate(lay.srcs).tolist()) == list(range(n))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_sources_split_and_gather_reassembles_single_rank_result(world):
+    """One LSDB, sources split over ranks, every rank's dist rows + next-hop
+    bitmaps gathered to rank 0 (gloo here, RCCL in bench.py): rank 0's
+    reassembled arrays equal the single-rank all-sources result bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_all_sources_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == (True, True, True)
+
+
+def test_all_sources_layout_blocks_balance_next_hop_work():
+    from openr_amd.sharding import AllSourcesLayout
+
+    rng = np.random.default_rng(0)
+    k = rng.integers(1, 200, 9976)
+    for world in (1, 2, 4, 8):
+        lay = AllSourcesLayout(k, 10048, world)
+        assert np.array_equal(np.concatenate(lay.srcs), np.arange(9976))
+        work = [int((k[s] + 1).sum()) for s in lay.srcs]
+        assert max(work) - min(work) <= 2 * k.max() + 2
+        assert lay.cap == max(lay.words)
