@@ -443,7 +443,19 @@ WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": All
              "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks}
 
 
+def _dump_maps_at_exit(path: str) -> None:
+    """Diagnostics: copy /proc/self/maps when the interpreter finalises, so
+    addresses in a native crash during exit-time teardown can be attributed
+    to a library (BENCH_DUMP_MAPS=<file>)."""
+    import atexit
+    import shutil
+
+    atexit.register(lambda: shutil.copy("/proc/self/maps", path))
+
+
 def main() -> None:
+    if os.environ.get("BENCH_DUMP_MAPS"):
+        _dump_maps_at_exit(os.environ["BENCH_DUMP_MAPS"])
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
