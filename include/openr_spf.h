@@ -22,9 +22,15 @@
  *     appear in linksFromNode(u) iteration order.
  *   - overloaded[u] != 0: u is recorded but never expanded unless it is the
  *     source (LinkState.cpp:831-838).
- *   - Distances are u32.  spf_graph_load rejects graphs whose longest possible
- *     path (max metric x (n_nodes-1)) does not fit; such graphs are out of
- *     scope for this engine (SPF_E_UNSUPPORTED).
+ *   - Distances are u32 unless the plan asks for SPF_FLAG_DIST64 (u64, the
+ *     reference's LinkStateMetric).  Weighted solves of graphs whose longest
+ *     possible path (max metric x (n_nodes-1)) does not fit 32 bits, or with
+ *     a negative metric (the reference's i32 -> u64 conversion wraps), need
+ *     SPF_FLAG_DIST64.
+ *   - Zero or negative metrics, u64 distances and graphs too large for the
+ *     LDS-resident kernels run the exact kernel (exact.hip): runSpf replayed
+ *     step for step, one wavefront per source, heap pop order (metric, id)
+ *     reproduced -- the next-hop sets under zero-cost plateaus depend on it.
  *   - Row pitch: dist and next-hop rows are stored with pitch
  *     spf_row_pitch() = n_nodes rounded up to a multiple of 64.
  *
@@ -57,6 +63,11 @@ typedef enum spf_status {
 
 /* solve flags */
 #define SPF_FLAG_HOP_COUNT 0x1u /* useLinkMetric == false: every edge costs 1 */
+/* Distance rows are u64 (LinkStateMetric, LinkState.h:22): pitch entries of
+ * 8 bytes, UINT64_MAX = unreachable.  Required for weighted solves of graphs
+ * with a negative metric or max metric x (n_nodes-1) >= 2^32 - 1. */
+#define SPF_FLAG_DIST64 0x2u
+#define SPF_UNREACHABLE64 0xFFFFFFFFFFFFFFFFull
 
 typedef struct spf_ctx spf_ctx;
 typedef struct spf_plan spf_plan;
@@ -103,10 +114,12 @@ uint64_t spf_graph_epoch(const spf_ctx* ctx);
 /* Number of spf_graph_load calls so far (patches do not count). */
 uint64_t spf_graph_loads(const spf_ctx* ctx);
 uint32_t spf_row_pitch(const spf_ctx* ctx);
-/* 1 when the loaded graph has an up edge with metric <= 0 (weighted solves of
- * such graphs return SPF_E_UNSUPPORTED: zero-cost plateaus make the reference's
- * next-hop sets depend on heap pop order, not implemented yet). */
+/* 1 when the loaded graph has an up edge with metric <= 0 (weighted solves
+ * of such graphs run the exact kernel, which reproduces the heap pop order the
+ * reference's next-hop sets depend on under zero-cost plateaus). */
 int spf_graph_has_nonpositive_metric(const spf_ctx* ctx);
+/* 1 when weighted solves need u64 distances (SPF_FLAG_DIST64). */
+int spf_graph_needs_dist64(const spf_ctx* ctx);
 
 /* Distinct up neighbours of `src` in ascending id: the bit order of its
  * next-hop sets.  Writes min(count, cap) ids; *count = total. */
@@ -148,6 +161,7 @@ spf_status spf_plan_execute(spf_plan* plan, uint32_t* d_dist, uint32_t* d_nh,
  * padding) and the next-hop words (spf_plan_nh_words of them); either may be
  * NULL.  Device staging is owned by the plan. */
 spf_status spf_plan_execute_host(spf_plan* plan, uint32_t* dist, uint32_t* nh);
+/* (with SPF_FLAG_DIST64, `dist` is read as uint64_t[n_src][n_nodes]) */
 
 /* Kernel timing with HIP events recorded on the execute stream: after
  * spf_plan_enable_timing(plan, K), each of the next K executes records events
@@ -170,6 +184,19 @@ spf_status spf_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
 spf_status spf_sssp(spf_ctx* ctx, uint32_t src, uint32_t flags,
                     const uint32_t* ignore_links, uint32_t n_ignore,
                     uint32_t* dist_out);
+
+/* runSpf(src, useLinkMetric, linksToIgnore) on the exact kernel, into host
+ * buffers: distances as u64 (dist64_out, UINT64_MAX unreachable) when
+ * dist32_out is NULL, else as u32; next-hop bitmaps in the plan layout
+ * (spf_src_neighbors(src) bitmaps of pitch/32 words); pop_out[v] = the
+ * position of v in the reference's Dijkstra pop order (UINT32_MAX
+ * unreachable), from which pathLinks follow: the tight up in-edges (u -> v)
+ * of expanded u with pop(u) < pop(v), ordered by (pop(u), linksFromNode
+ * order).  Any pointer but one distance buffer may be NULL. */
+spf_status spf_solve_exact(spf_ctx* ctx, uint32_t src, uint32_t flags,
+                           const uint32_t* ignore_links, uint32_t n_ignore,
+                           uint64_t* dist64_out, uint32_t* dist32_out, uint32_t* nh_out,
+                           uint32_t* pop_out);
 
 /* Predecessor ("pathLinks") lists of one source given its distance row `dist`
  * (from spf_solve / spf_sssp with the same flags and ignore set), in the

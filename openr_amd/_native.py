@@ -28,6 +28,8 @@ SPF_E_NOMEM = 5
 SPF_E_STATE = 6
 SPF_UNREACHABLE = 0xFFFFFFFF
 SPF_FLAG_HOP_COUNT = 0x1
+SPF_FLAG_DIST64 = 0x2
+SPF_UNREACHABLE64 = 0xFFFFFFFFFFFFFFFF
 SPF_KSP2_NONE = 0xFFFFFFFF
 SPF_ROUTE_LFA = 0x1
 
@@ -166,6 +168,9 @@ PROTOTYPES = {
     "spf_plan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
     "spf_solve": (C.c_int, [_vp, _u32p, C.c_uint32, C.c_uint32, _u32p, _u32p]),
     "spf_sssp": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u32p]),
+    "spf_solve_exact": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u64p, _u32p,
+                                  _u32p, _u32p]),
+    "spf_graph_needs_dist64": (C.c_int, [_vp]),
     "spf_preds": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u32p,
                             _u32p, _u32p, C.c_uint32, _u32p]),
     "spf_solves": (C.c_uint64, [_vp]),

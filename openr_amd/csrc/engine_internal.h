@@ -63,8 +63,13 @@ struct spf_ctx {
   bool loaded = false;
   uint32_t N = 0, E = 0, pitch = 0;
   bool nonpos = false;
+  bool needs64 = false;  // a negative metric or max metric x (N-1) >= 2^32 - 1: u64 labels
   uint32_t max_metric = 0;
   std::vector<uint32_t> row_ptr, col, wt, rev, link;
+  std::vector<int32_t> met;  // metrics as advertised (exact kernel)
+  spfi::DevBuf<int32_t> d_met;
+  spfi::DevBuf<uint8_t> d_exact;      // exact kernel: per-wave heap/labels/next hops
+  spfi::DevBuf<uint32_t> d_exact_ctr;
   std::vector<uint8_t> ovl;
   std::vector<uint32_t> nb_ptr, nb_id, nb_w;  // distinct up neighbours
   uint32_t big_nodes = 0;                    // nodes with degree > kBigDeg
@@ -94,6 +99,8 @@ struct spf_plan {
   bool direct = false;  // closure == srcs: D is the caller's dist buffer
   bool ms = false;      // unit metrics: multi-source BFS
   bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
+  bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
+  uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
   spfi::DevBuf<uint8_t> d_Dn;
   spfi::DevBuf<uint64_t> d_nh_off;
@@ -140,6 +147,11 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 // size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
                         hipStream_t s);
+// The exact kernel (exact.hip) over n_src sources: dist rows (u32 or u64,
+// pitch entries), planar next-hop bitmaps at nh_off, optional pop ranks.
+spf_status launch_exact(spf_ctx* c, const uint32_t* d_srcs, uint32_t n_src, const uint64_t* d_nh_off,
+                        uint32_t Wmax, bool hop, bool dist64, const uint32_t* ign, void* d_dist,
+                        uint32_t* d_nh, uint32_t* d_pop, hipStream_t s);
 // Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
 spf_status set_lds_limits(spf_ctx* c);
 

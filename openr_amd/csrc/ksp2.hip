@@ -466,9 +466,10 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   *out = nullptr;
   if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
   if (n_src == 0 || !srcs) return fail(c, SPF_E_INVALID, "empty source list");
-  if (c->nonpos)
+  if (c->nonpos || c->needs64)
     return fail(c, SPF_E_UNSUPPORTED,
-                "graph has up links with metric <= 0 (KSP2 runs weighted SPF)");
+                "graph has up links with metric <= 0 or needs u64 distances (the batched KSP2 "
+                "kernel runs u32 weighted SPF; LinkState.getKthPaths takes the exact path)");
   if (c->N > 65535) return fail(c, SPF_E_UNSUPPORTED, "KSP2 kernel supports <= 65535 nodes");
   auto p = std::make_unique<spf_ksp2_plan>();
   p->ctx = c;

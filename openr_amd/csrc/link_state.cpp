@@ -550,6 +550,49 @@ void fill_view(const SpfMemo& m, ls_spf_view* out) {
   out->pl_prev = m.pl_prev.data();
 }
 
+// Weighted solves the data-parallel kernels cannot answer exactly (zero or
+// negative metrics, u64 distances) run the engine's exact kernel, which also
+// reports the Dijkstra pop order; pathLinks follow from it.
+bool needs_exact(const ls_state* ls, bool ulm) {
+  return ulm && (spf_graph_has_nonpositive_metric(ls->eng) || spf_graph_needs_dist64(ls->eng));
+}
+
+// runSpf(s, ulm, ignore) on the exact kernel: u64 distances (UINT64_MAX =
+// unreachable), next-hop bitmaps (nh may be NULL) and pathLinks as csr edge
+// ids: the tight up in-edges (u -> v) of expanded u popped before v, in
+// (pop order of u, linksFromNode order) -- LinkState.cpp:857-873.
+spf_status exact_spf(ls_state* ls, uint32_t s, bool ulm, const std::vector<uint32_t>& ignore,
+                     std::vector<uint64_t>& dist, std::vector<uint32_t>* nh,
+                     std::vector<uint32_t>& pred_ptr, std::vector<uint32_t>& pred_edge) {
+  const uint32_t N = (uint32_t)ls->csr_name.size();
+  const uint32_t flags = ulm ? 0u : SPF_FLAG_HOP_COUNT;
+  std::vector<uint32_t> pop(N);
+  dist.assign(N, 0);
+  spf_status st = spf_solve_exact(ls->eng, s, flags, ignore.empty() ? nullptr : ignore.data(),
+                                  (uint32_t)ignore.size(), dist.data(), nullptr,
+                                  nh ? nh->data() : nullptr, pop.data());
+  if (st != SPF_OK) return eng_fail(ls, st);
+  std::unordered_set<uint32_t> ign(ignore.begin(), ignore.end());
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> in(N);  // (pop(u), edge)
+  for (uint32_t u = 0; u < N; ++u) {
+    if (pop[u] == SPF_UNREACHABLE || (ls->ovl[u] && u != s)) continue;  // not expanded
+    for (uint32_t e = ls->row_ptr[u]; e < ls->row_ptr[u + 1]; ++e) {
+      const uint32_t v = ls->col[e];
+      if (pop[v] == SPF_UNREACHABLE || pop[v] <= pop[u] || ign.count(ls->link_id[e])) continue;
+      const uint64_t w = ulm ? (uint64_t)(int64_t)ls->metric[e] : 1ull;
+      if (dist[u] + w == dist[v]) in[v].emplace_back(pop[u], e);
+    }
+  }
+  pred_ptr.assign(N + 1, 0);
+  pred_edge.clear();
+  for (uint32_t v = 0; v < N; ++v) {
+    std::sort(in[v].begin(), in[v].end());
+    for (const auto& pe : in[v]) pred_edge.push_back(pe.second);
+    pred_ptr[v + 1] = (uint32_t)pred_edge.size();
+  }
+  return SPF_OK;
+}
+
 // getSpfResult (LinkState.cpp:793-803) -> memo entry
 spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out) {
   auto key = std::make_pair(node, (int)ulm);
@@ -582,20 +625,29 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
     const uint64_t words = (uint64_t)k * wpm;
     m.dist.resize(N);
     std::vector<uint32_t> nh(std::max<uint64_t>(words, 1));
-    st = spf_solve(ls->eng, &s, 1, flags, m.dist.data(), nh.data());
-    if (st != SPF_OK) return eng_fail(ls, st);
-    uint32_t npred = 0;
-    m.pred_ptr.resize(N + 1);
-    st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(), nullptr, 0, &npred);
-    if (st != SPF_OK) return eng_fail(ls, st);
-    m.pred_edge.resize(npred);
-    st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(),
-                   m.pred_edge.data(), npred, &npred);
-    if (st != SPF_OK) return eng_fail(ls, st);
+    std::vector<uint64_t> d64;
+    if (needs_exact(ls, ulm)) {
+      st = exact_spf(ls, s, ulm, {}, d64, &nh, m.pred_ptr, m.pred_edge);
+      if (st != SPF_OK) return st;
+      for (uint32_t v = 0; v < N; ++v)  // csr-indexed reachability for path tracing
+        m.dist[v] = d64[v] == SPF_UNREACHABLE64 ? SPF_UNREACHABLE : 0u;
+    } else {
+      st = spf_solve(ls->eng, &s, 1, flags, m.dist.data(), nh.data());
+      if (st != SPF_OK) return eng_fail(ls, st);
+      uint32_t npred = 0;
+      m.pred_ptr.resize(N + 1);
+      st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(), nullptr, 0,
+                     &npred);
+      if (st != SPF_OK) return eng_fail(ls, st);
+      m.pred_edge.resize(npred);
+      st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(),
+                     m.pred_edge.data(), npred, &npred);
+      if (st != SPF_OK) return eng_fail(ls, st);
+    }
     for (uint32_t v = 0; v < N; ++v) {
       if (m.dist[v] == SPF_UNREACHABLE) continue;
       m.node.push_back(ls->csr_name[v]);
-      m.metric.push_back(m.dist[v]);
+      m.metric.push_back(d64.empty() ? (uint64_t)m.dist[v] : d64[v]);
       for (uint32_t j = 0; j < k; ++j)  // bitmap j: destinations routed via neighbour j
         if ((nh[(size_t)j * wpm + (v >> 5)] >> (v & 31)) & 1u)
           m.nh_node.push_back(ls->csr_name[nbr[j]]);
@@ -686,10 +738,19 @@ spf_status kth_paths(ls_state* ls, uint32_t src, uint32_t dst, uint64_t k, const
     ls->spf_runs++;  // the un-memoised runSpf of LinkState.cpp:778-779
     const uint32_t N = (uint32_t)ls->csr_name.size();
     dist.resize(N);
-    st = spf_sssp(ls->eng, s, 0, ignore.data(), (uint32_t)ignore.size(), dist.data());
-    if (st != SPF_OK) return eng_fail(ls, st);
-    reachable = dist[d] != SPF_UNREACHABLE;
-    if (reachable) {
+    if (needs_exact(ls, true)) {
+      std::vector<uint64_t> d64;
+      st = exact_spf(ls, s, true, ignore, d64, nullptr, my_ptr, my_edge);
+      if (st != SPF_OK) return st;
+      reachable = d64[d] != SPF_UNREACHABLE64;
+      pptr = &my_ptr;
+      pedge = &my_edge;
+    } else {
+      st = spf_sssp(ls->eng, s, 0, ignore.data(), (uint32_t)ignore.size(), dist.data());
+      if (st != SPF_OK) return eng_fail(ls, st);
+      reachable = dist[d] != SPF_UNREACHABLE;
+    }
+    if (reachable && !pptr) {
       uint32_t np = 0;
       my_ptr.resize(N + 1);
       st = spf_preds(ls->eng, s, 0, ignore.data(), (uint32_t)ignore.size(), dist.data(),
@@ -934,6 +995,9 @@ spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src_c) {
   const uint32_t src = ls->intern(src_c);
   const uint32_t s = src < ls->csr_of.size() ? ls->csr_of[src] : kNone;
   if (s == kNone) return SPF_OK;  // not in the graph: every query is empty anyway
+  // outside the batched kernel's envelope (zero / negative metrics, u64):
+  // nothing to prefetch, getKthPaths answers pair by pair on the exact kernel
+  if (needs_exact(ls, true)) return SPF_OK;
   const uint32_t N = (uint32_t)ls->csr_name.size();
   std::vector<spf_ksp2_pair> pairs(N);
   std::vector<uint32_t> pool;

@@ -918,6 +918,7 @@ const char* spf_last_error(const spf_ctx* c) { return c ? c->err.c_str() : g_err
 uint64_t spf_solves(const spf_ctx* c) { return c ? c->solves : 0; }
 uint32_t spf_row_pitch(const spf_ctx* c) { return c ? c->pitch : 0; }
 int spf_graph_has_nonpositive_metric(const spf_ctx* c) { return c && c->nonpos; }
+int spf_graph_needs_dist64(const spf_ctx* c) { return c && c->needs64; }
 
 spf_status spf_ctx_create(int device, spf_ctx** out) {
   if (!out) return fail(nullptr, SPF_E_INVALID, "spf_ctx_create: out is NULL");
@@ -978,7 +979,9 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   c->link.assign(g->link_id, g->link_id + E);
   c->ovl.assign(g->overloaded, g->overloaded + N);
   c->wt.resize(E);
+  c->met.assign(g->metric, g->metric + E);
   c->nonpos = false;
+  c->needs64 = false;
   c->max_metric = 0;
   for (uint32_t u = 0; u < N; ++u) {
     if (c->row_ptr[u] > c->row_ptr[u + 1])
@@ -988,13 +991,14 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     if (c->col[e] >= N) return fail(c, SPF_E_INVALID, "edge %u head %u out of range", e, c->col[e]);
     const int32_t m = g->metric[e];
     if (m <= 0) c->nonpos = true;
+    if (m < 0) c->needs64 = true;  // i32 -> u64 wraps (LinkState.h:22)
     c->wt[e] = m > 0 ? (uint32_t)m : 0u;
     c->max_metric = std::max(c->max_metric, c->wt[e]);
   }
   c->unit = !c->nonpos && c->max_metric <= 1;
-  if ((uint64_t)c->max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf)
-    return fail(c, SPF_E_UNSUPPORTED,
-                "max metric %u x %u hops overflows 32-bit distances", c->max_metric, N - 1);
+  // longest possible path beyond 32 bits: weighted solves take the exact
+  // kernel's u64 labels (SPF_FLAG_DIST64)
+  if ((uint64_t)c->max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf) c->needs64 = true;
   // reverse edge of every directed edge (same link id, swapped ends)
   c->rev.assign(E, kInf);
   {
@@ -1038,6 +1042,7 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   HIP_TRY(c, c->d_row_ptr.upload(c->row_ptr.data(), N + 1, c->stream));
   HIP_TRY(c, c->d_col.upload(c->col.data(), E, c->stream));
   HIP_TRY(c, c->d_wt.upload(c->wt.data(), E, c->stream));
+  HIP_TRY(c, c->d_met.upload(c->met.data(), E, c->stream));
   HIP_TRY(c, c->d_rev.upload(c->rev.data(), E, c->stream));
   HIP_TRY(c, c->d_link.upload(c->link.data(), E, c->stream));
   c->max_link = 0;
@@ -1142,23 +1147,25 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
   for (uint32_t i = 0; i < n; ++i)
     if (edges[i] >= c->E) return fail(c, SPF_E_INVALID, "edge %u out of range", edges[i]);
   std::vector<uint32_t> wt = c->wt;
+  std::vector<int32_t> met = c->met;
   bool changed = false;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t w = metric[i] > 0 ? (uint32_t)metric[i] : 0u;
-    changed |= wt[edges[i]] != w;
+    changed |= met[edges[i]] != metric[i];
     wt[edges[i]] = w;
+    met[edges[i]] = metric[i];
   }
   if (!changed) return SPF_OK;
-  bool nonpos = false;
+  bool nonpos = false, neg = false;
   uint32_t max_metric = 0;
   for (uint32_t e = 0; e < c->E; ++e) {
-    nonpos |= wt[e] == 0;
+    nonpos |= met[e] <= 0;
+    neg |= met[e] < 0;
     max_metric = std::max(max_metric, wt[e]);
   }
-  if ((uint64_t)max_metric * (uint64_t)(c->N - 1) >= (uint64_t)kInf)
-    return fail(c, SPF_E_UNSUPPORTED, "max metric %u x %u hops overflows 32-bit distances",
-                max_metric, c->N - 1);
   c->wt.swap(wt);
+  c->met.swap(met);
+  c->needs64 = neg || (uint64_t)max_metric * (uint64_t)(c->N - 1) >= (uint64_t)kInf;
   c->nonpos = nonpos;
   c->max_metric = max_metric;
   c->unit = !nonpos && max_metric <= 1;
@@ -1180,6 +1187,7 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
   }
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, c->d_wt.upload(c->wt.data(), c->E, c->stream));
+  HIP_TRY(c, c->d_met.upload(c->met.data(), c->E, c->stream));
   HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   ++c->epoch;
@@ -1230,11 +1238,42 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   const uint32_t n_src = p->n_src;
   const uint32_t* srcs = p->srcs.data();
   const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
-  if (!hop && c->nonpos)
+  const bool d64 = (p->flags & SPF_FLAG_DIST64) != 0;
+  if (!hop && c->needs64 && !d64)
     return fail(c, SPF_E_UNSUPPORTED,
-                "graph has up links with metric <= 0; weighted SPF over zero/negative "
-                "metrics is outside the exact-parity envelope");
+                "weighted distances of this graph may exceed 32 bits (negative metric or max "
+                "metric x hops >= 2^32): create the plan with SPF_FLAG_DIST64");
   const uint32_t N = c->N;
+  // the exact kernel replays runSpf step for step: zero-metric plateaus
+  // (pop order), u64 labels, and graphs whose distance rows do not fit the
+  // LDS-resident kernels
+  const bool ms_ok = (hop || c->unit) && N <= kMsMaxNodes;
+  const bool lds_ok = sssp_lds_bytes(N, c->pitch, c->big_nodes, N <= 65535) <= kMaxLds;
+  p->exact = d64 || (!hop && c->nonpos) || (!ms_ok && !lds_ok);
+  if (p->exact) {
+    p->closure = p->srcs;
+    p->direct = true;
+    p->ms = false;
+    p->narrow = false;
+    p->nh_off.resize(n_src);
+    p->words.resize(n_src);
+    uint64_t off = 0;
+    p->wmax = 1;
+    for (uint32_t i = 0; i < n_src; ++i) {
+      const uint32_t k = c->nb_ptr[srcs[i] + 1] - c->nb_ptr[srcs[i]];
+      p->words[i] = k;
+      p->nh_off[i] = off;
+      off += (uint64_t)k * (c->pitch / 32);
+      p->wmax = std::max(p->wmax, (k + 31) / 32);
+    }
+    p->nh_total = off;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
+    HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    p->epoch = c->epoch;
+    return SPF_OK;
+  }
   p->closure.clear();
   std::vector<uint32_t> row_of(N, kInf);
   bool distinct = true;
@@ -1350,10 +1389,6 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors end here
   }
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
-  if (!p->ms && p->lds_bytes > kMaxLds)
-    return fail(c, SPF_E_UNSUPPORTED,
-                "batched plans keep a distance row per source in LDS: %u nodes do not fit "
-                "(single-source spf_sssp and what-if batches handle large graphs)", N);
   if (p->narrow) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
     HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
     HIP_TRY(c, hipMemsetAsync(p->d_Dn.p + p->closure.size() * c->npitch, 0xFF, c->npitch, c->stream));
@@ -1398,7 +1433,7 @@ uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->clos
 
 spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
-  *bfs = !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
+  *bfs = p->exact ? 3u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
   *narrow = p->narrow ? 1u : 0u;
   return SPF_OK;
 }
@@ -1419,6 +1454,13 @@ spf_status spf_plan_traffic(const spf_plan* p, uint64_t* bfs_bytes, uint64_t* ec
   const spf_ctx* c = p->ctx;
   const uint64_t N = c->N, E = c->E, rows = p->closure.size();
   uint64_t bfs = 0;
+  if (p->exact) {  // per source: the CSR once, the labels, the outputs
+    const uint64_t lab = (p->flags & SPF_FLAG_DIST64) ? 8ull : 4ull;
+    *bfs_bytes = rows * (4ull * (N + 1) + 12ull * E + N + 17ull * N + lab * c->pitch) +
+                 4ull * p->nh_total;
+    *ecmp_bytes = 0;
+    return SPF_OK;
+  }
   if (p->ms) {
     const bool planes = use_planes(c);
     const uint32_t batch = planes ? kPlBatch : kMsBatch;
@@ -1642,6 +1684,24 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint32_t pitch = c->pitch;
   const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
+  if (p->exact) {
+    hipEvent_t* ev = nullptr;
+    if (p->timing_cap) {
+      ev = &p->ev[3 * (p->timing_n % p->timing_cap)];
+      ++p->timing_n;
+      HIP_TRY(c, hipEventRecord(ev[0], s));
+    }
+    const spf_status st = launch_exact(c, p->d_srcs.p, p->n_src, p->d_nh_off.p, p->wmax, hop,
+                                       (p->flags & SPF_FLAG_DIST64) != 0, nullptr, d_dist, d_nh,
+                                       nullptr, s);
+    if (st != SPF_OK) return st;
+    if (ev) {
+      HIP_TRY(c, hipEventRecord(ev[1], s));
+      HIP_TRY(c, hipEventRecord(ev[2], s));
+    }
+    c->solves += p->n_src;
+    return SPF_OK;
+  }
   uint32_t* D = p->direct ? d_dist : p->d_D.p;
   const uint32_t rows = (uint32_t)p->closure.size();
   hipEvent_t* ev = nullptr;
@@ -1704,13 +1764,14 @@ spf_status spf_plan_execute_host(spf_plan* p, uint32_t* dist_out, uint32_t* nh_o
   if (!p) return fail(nullptr, SPF_E_INVALID, "spf_plan_execute_host: NULL plan");
   spf_ctx* c = p->ctx;
   HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, p->h_dist.alloc((size_t)p->n_src * c->pitch));
+  const size_t lab = (p->flags & SPF_FLAG_DIST64) ? 8 : 4;
+  HIP_TRY(c, p->h_dist.alloc((size_t)p->n_src * c->pitch * (lab / 4)));
   HIP_TRY(c, p->h_nh.alloc(std::max<uint64_t>(p->nh_total, 1)));
   const spf_status st = spf_plan_execute(p, p->h_dist.p, p->h_nh.p, nullptr);
   if (st != SPF_OK) return st;
   if (dist_out) {
-    HIP_TRY(c, hipMemcpy2DAsync(dist_out, (size_t)c->N * 4, p->h_dist.p, (size_t)c->pitch * 4,
-                                (size_t)c->N * 4, p->n_src, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpy2DAsync(dist_out, (size_t)c->N * lab, p->h_dist.p, (size_t)c->pitch * lab,
+                                (size_t)c->N * lab, p->n_src, hipMemcpyDeviceToHost, c->stream));
   }
   if (nh_out && p->nh_total) {
     HIP_TRY(c, hipMemcpyAsync(nh_out, p->h_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1745,8 +1806,12 @@ spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ig
   if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
   if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
   const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
-  if (!hop && c->nonpos)
-    return fail(c, SPF_E_UNSUPPORTED, "graph has up links with metric <= 0");
+  if (!hop && (c->nonpos || c->needs64)) {  // the exact kernel (u32 rows when they fit)
+    if (c->needs64)
+      return fail(c, SPF_E_UNSUPPORTED, "weighted distances may exceed 32 bits: use spf_solve_exact");
+    return spf_solve_exact(c, src, flags, ignore_links, n_ignore, nullptr, dist_out, nullptr,
+                           nullptr);
+  }
   spf_status st = set_lds_limits(c);
   if (st != SPF_OK) return st;
   const uint32_t* ign = nullptr;
@@ -1761,6 +1826,45 @@ spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ig
   }
   if (st != SPF_OK) return st;
   HIP_TRY(c, hipMemcpyAsync(dist_out, c->d_row.p, 4ull * c->N, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->solves += 1;
+  return SPF_OK;
+}
+
+spf_status spf_solve_exact(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ignore_links,
+                           uint32_t n_ignore, uint64_t* dist64_out, uint32_t* dist32_out,
+                           uint32_t* nh_out, uint32_t* pop_out) {
+  if (!c) return fail(c, SPF_E_INVALID, "spf_solve_exact: NULL context");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
+  const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
+  if (dist32_out && !hop && c->needs64)
+    return fail(c, SPF_E_UNSUPPORTED, "weighted distances may exceed 32 bits: ask for u64 rows");
+  const uint32_t* ign = nullptr;
+  spf_status st = upload_ignore(c, ignore_links, n_ignore, &ign);
+  if (st != SPF_OK) return st;
+  const uint32_t k = c->nb_ptr[src + 1] - c->nb_ptr[src];
+  const uint64_t wpm = c->pitch / 32, nh_words = (uint64_t)k * wpm;
+  const bool d64 = dist32_out == nullptr;
+  DevBuf<uint32_t> d_dist, d_nh, d_pop;
+  DevBuf<uint64_t> d_off;
+  const uint64_t zero = 0;
+  HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
+  HIP_TRY(c, d_off.upload(&zero, 1, c->stream));
+  HIP_TRY(c, d_dist.alloc((size_t)c->pitch * (d64 ? 2 : 1)));
+  HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(nh_words, 1)));
+  if (pop_out) HIP_TRY(c, d_pop.alloc(c->pitch));
+  st = launch_exact(c, c->d_one_src.p, 1, d_off.p, std::max<uint32_t>(1, (k + 31) / 32), hop, d64,
+                    ign, d_dist.p, d_nh.p, pop_out ? d_pop.p : nullptr, c->stream);
+  if (st != SPF_OK) return st;
+  if (d64 && dist64_out)
+    HIP_TRY(c, hipMemcpyAsync(dist64_out, d_dist.p, 8ull * c->N, hipMemcpyDeviceToHost, c->stream));
+  if (!d64)
+    HIP_TRY(c, hipMemcpyAsync(dist32_out, d_dist.p, 4ull * c->N, hipMemcpyDeviceToHost, c->stream));
+  if (nh_out && nh_words)
+    HIP_TRY(c, hipMemcpyAsync(nh_out, d_nh.p, 4ull * nh_words, hipMemcpyDeviceToHost, c->stream));
+  if (pop_out)
+    HIP_TRY(c, hipMemcpyAsync(pop_out, d_pop.p, 4ull * c->N, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->solves += 1;
   return SPF_OK;

@@ -1026,8 +1026,10 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   *out = nullptr;
   if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
   if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
-  if (c->nonpos)
-    return fail(c, SPF_E_UNSUPPORTED, "graph has up links with metric <= 0 (what-if runs weighted SPF)");
+  if (c->nonpos || c->needs64)
+    return fail(c, SPF_E_UNSUPPORTED,
+                "graph has up links with metric <= 0 or needs u64 distances (what-if batches "
+                "run u32 weighted SPF with positive metrics)");
   auto p = std::make_unique<spf_whatif_plan>();
   p->ctx = c;
   p->src = src;

@@ -23,12 +23,14 @@ from ._native import NativeHandle, close_all  # noqa: F401
 
 
 HOP_COUNT = N.SPF_FLAG_HOP_COUNT
+DIST64 = N.SPF_FLAG_DIST64
 UNREACHABLE = N.SPF_UNREACHABLE
+UNREACHABLE64 = N.SPF_UNREACHABLE64
 
 
 @dataclass
 class SolveResult:
-    dist: np.ndarray  # [n_src, n_nodes] uint32 (UNREACHABLE)
+    dist: np.ndarray  # [n_src, n_nodes] uint32 (UNREACHABLE), uint64 for dist64 plans
     nh: np.ndarray  # destination bitmaps, one per (source, neighbour)
     nh_off: np.ndarray  # [n_src] uint64 word offset of each source's bitmaps
     words: np.ndarray  # [n_src] number of bitmaps (= distinct up neighbours)
@@ -77,12 +79,12 @@ class SpfPlan(NativeHandle):
     def execute_host(self) -> "SolveResult":
         """Execute into host arrays (spf_plan_execute_host)."""
         n = self._eng.n_nodes
-        dist = np.zeros((self.n_src, n), np.uint32)
+        dist = np.zeros((self.n_src, n), np.uint64 if self.flags & DIST64 else np.uint32)
         nh = np.zeros(max(1, self.nh_words), np.uint32)
         self._eng._err(N.lib.spf_plan_execute_host(self._h, N.ptr(dist), N.ptr(nh)))
         return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
 
-    BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel")
+    BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel")
 
     def kernels(self) -> Tuple[str, bool]:
         """(distance kernel name, next-hop pass reads u8 narrow rows) of the
@@ -318,17 +320,35 @@ class SpfEngine(NativeHandle):
         return int(N.lib.spf_solves(self._h))
 
     # ---- solves -----------------------------------------------------------------
-    def plan(self, srcs: Sequence[int], hop: bool = False) -> SpfPlan:
-        return self._track(SpfPlan(self, srcs, HOP_COUNT if hop else 0))
+    @property
+    def needs_dist64(self) -> bool:
+        """Weighted solves of this graph need u64 distances (spf_graph_needs_dist64)."""
+        return bool(N.lib.spf_graph_needs_dist64(self._h))
 
-    def solve(self, srcs: Sequence[int], hop: bool = False) -> SolveResult:
-        p = self.plan(srcs, hop)
+    def plan(self, srcs: Sequence[int], hop: bool = False, dist64: bool = False) -> SpfPlan:
+        return self._track(SpfPlan(self, srcs, (HOP_COUNT if hop else 0) |
+                                   (DIST64 if dist64 else 0)))
+
+    def solve(self, srcs: Sequence[int], hop: bool = False, dist64: bool = False) -> SolveResult:
+        """All of `srcs` in one plan, results on the host.  dist64: u64
+        distance rows (the exact kernel; needed when needs_dist64)."""
+        with self.plan(srcs, hop, dist64) as p:
+            return p.execute_host()
+
+    def solve_exact(self, src: int, hop: bool = False,
+                    ignore_links: Optional[Sequence[int]] = None):
+        """runSpf on the exact kernel (spf_solve_exact): (dist u64 [N],
+        next-hop bitmaps [k, N] bool, pop rank [N] u32)."""
+        ign = np.ascontiguousarray(ignore_links if ignore_links is not None else [], np.uint32)
         n = self.n_nodes
-        dist = np.zeros((p.n_src, n), np.uint32)
-        nh = np.zeros(max(1, p.nh_words), np.uint32)
-        self._err(N.lib.spf_solve(self._h, N.ptr(p.srcs), p.n_src, p.flags, N.ptr(dist),
-                                  N.ptr(nh)))
-        return SolveResult(dist, nh, p.nh_off, p.words, self.pitch)
+        k = len(self.neighbors(src))
+        dist = np.zeros(n, np.uint64)
+        nh = np.zeros(max(1, k * self.pitch // 32), np.uint32)
+        pop = np.zeros(n, np.uint32)
+        self._err(N.lib.spf_solve_exact(self._h, src, HOP_COUNT if hop else 0,
+                                        N.ptr(ign) if len(ign) else None, len(ign),
+                                        N.ptr(dist, C.c_uint64), None, N.ptr(nh), N.ptr(pop)))
+        return dist, nh_matrix(nh, 0, k, self.pitch, n), pop
 
     def ksp2_plan(self, srcs: Sequence[int]) -> Ksp2Plan:
         return self._track(Ksp2Plan(self, srcs))

@@ -111,17 +111,16 @@ def test_baseline_size_sampled_exact_and_all_sources_properties(which):
             assert np.array_equal(mat[j], d[x].astype(np.int64) + 1 == d[s])
 
 
-def test_zero_metric_is_rejected_loudly():
-    from openr_amd._native import UnsupportedInput
-
+def test_zero_metric_runs_the_exact_kernel():
+    """A zero-metric link routes weighted plans to the exact kernel
+    (test_gpu_exact.py covers it in depth); hop counts stay on the BFS."""
     topo = T.random_graph(20, 30, 2)
     topo.lsdb.adjs["metric"][0] = 0
-    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
-    eng = SpfEngine(0)
-    eng.load(rp, col, met, lid, ovl)
-    with pytest.raises(UnsupportedInput):
-        eng.solve([0])
-    eng.solve([0], hop=True)  # hop counts ignore metrics: fine
+    names, eng, orc = load(topo)
+    assert eng.plan([0]).kernels()[0] == "exact_spf_kernel"
+    assert eng.plan([0], hop=True).kernels()[0] != "exact_spf_kernel"
+    compare(names, eng, orc, list(range(len(names))))
+    compare(names, eng, orc, list(range(len(names))), hop=True)
 
 
 @pytest.mark.parametrize("narrow", ["0", "1"])

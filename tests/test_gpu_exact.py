@@ -1,0 +1,160 @@
+"""The exact-envelope kernel (csrc/exact.hip) on the MI355X against the oracle:
+inputs the data-parallel kernels used to refuse (VERDICT r01 missing #3).
+
+* zero-metric links: next-hop sets follow the reference's heap pop order
+  (metric, name) on zero-cost plateaus (LinkState.cpp:857-873,
+  LinkState.h:488-498) -- every source, with parallel links, drained nodes
+  and drained links;
+* negative metrics: the reference's i32 -> u64 conversion wraps
+  (LinkState.h:22, LinkState.cpp:151-152): u64 labels, compared raw;
+* u64 distances: max metric x hops beyond 2^32 (SPF_FLAG_DIST64);
+* the LinkState facade on such graphs: getSpfResult incl. pathLinks order,
+  getKthPaths k = 1, 2;
+* the exact kernel forced on ordinary graphs equals the fast kernels.
+"""
+
+import numpy as np
+import pytest
+
+from helpers import link_key, spf_canonical
+from oracle import OracleLinkState
+from openr_amd import topology as T
+from openr_amd._native import UnsupportedInput
+from openr_amd.engine import SpfEngine, graph_from_lsdb
+from openr_amd.link_state import LinkState
+
+pytestmark = pytest.mark.gpu
+
+U64_INF = np.iinfo(np.uint64).max
+
+
+def with_metrics(topo, fn, seed):
+    rng = np.random.default_rng(seed)
+    m = topo.lsdb.adjs["metric"]
+    topo.lsdb.adjs["metric"] = fn(m, rng).astype(np.int32)
+    return topo
+
+
+def zero_frac(frac):
+    return lambda m, rng: np.where(rng.random(len(m)) < frac, 0, m)
+
+
+def load(topo):
+    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+    eng = SpfEngine(0)
+    eng.load(rp, col, met, lid, ovl)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    return names, eng, orc
+
+
+def compare(names, eng, orc, srcs, dist64, hop=False):
+    res = eng.solve(srcs, hop=hop, dist64=dist64)
+    dist, mats = orc.dense(names, srcs, ulm=not hop)
+    if dist64:
+        assert np.array_equal(res.dist, dist), "distance mismatch"
+    else:
+        exp = np.where(dist == U64_INF, 0xFFFFFFFF, dist).astype(np.uint32)
+        assert np.array_equal(res.dist, exp), "distance mismatch"
+    for i, s in enumerate(srcs):
+        k = len(eng.neighbors(s))
+        got, want = res.nh_matrix(i), mats[i][:k]
+        assert not mats[i][k:].any()
+        if not np.array_equal(got, want):
+            j, v = (int(x[0]) for x in np.nonzero(got != want))
+            raise AssertionError(f"next-hop mismatch src {names[s]} dst {names[v]} nbr j={j}: "
+                                 f"gpu {bool(got[j, v])} oracle {bool(want[j, v])}")
+
+
+ZERO = [(f"zero{s}", (lambda s: lambda: with_metrics(T.random_graph(
+    60, 150, 70 + s, max_metric=3, parallel_frac=0.2, overload_frac=0.1,
+    link_overload_frac=0.05), zero_frac(0.35), s))(s)) for s in range(5)] + [
+    ("zero_grid", lambda: with_metrics(T.grid(9), zero_frac(0.5), 9)),
+    ("all_zero", lambda: with_metrics(T.random_graph(40, 90, 3, parallel_frac=0.2),
+                                      lambda m, rng: 0 * m, 1)),
+]
+
+
+@pytest.mark.parametrize("name,make", ZERO, ids=[z[0] for z in ZERO])
+def test_zero_metric_plateaus_every_source(name, make):
+    names, eng, orc = load(make())
+    assert not eng.needs_dist64
+    srcs = list(range(len(names)))
+    compare(names, eng, orc, srcs, dist64=False)
+    compare(names, eng, orc, srcs, dist64=True)
+    compare(names, eng, orc, srcs, dist64=False, hop=True)
+
+
+def test_negative_metrics_wrap_like_the_reference():
+    topo = with_metrics(T.random_graph(40, 100, 12, max_metric=6, parallel_frac=0.1),
+                        lambda m, rng: np.where(rng.random(len(m)) < 0.1, -rng.integers(1, 5, len(m)), m), 4)
+    names, eng, orc = load(topo)
+    assert eng.needs_dist64
+    with pytest.raises(UnsupportedInput):
+        eng.solve([0])  # u32 rows cannot hold wrapped u64 labels
+    compare(names, eng, orc, list(range(len(names))), dist64=True)
+
+
+def test_u64_distances_beyond_32_bits():
+    topo = with_metrics(T.wan(30, 10, seed=4),
+                        lambda m, rng: rng.integers(2 ** 30, 2 ** 31 - 1, len(m)), 5)
+    names, eng, orc = load(topo)
+    assert eng.needs_dist64
+    res = eng.solve([0], dist64=True)
+    assert int(res.dist.max()) > 2 ** 32  # really beyond u32
+    compare(names, eng, orc, list(range(len(names))), dist64=True)
+
+
+@pytest.mark.parametrize("name,make", [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("wan300", lambda: T.wan(300, 150, seed=3)),
+    ("rand", lambda: T.random_graph(60, 150, 7, max_metric=8, parallel_frac=0.2,
+                                    overload_frac=0.1, link_overload_frac=0.05)),
+], ids=["fabric", "wan", "rand"])
+def test_exact_kernel_equals_fast_kernels(name, make):
+    names, eng, orc = load(make())
+    srcs = list(range(len(names)))
+    fast = eng.solve(srcs)
+    ex = eng.solve(srcs, dist64=True)
+    assert np.array_equal(ex.dist, np.where(fast.dist == 0xFFFFFFFF, U64_INF, fast.dist))
+    assert np.array_equal(ex.nh[: fast.nh.size], fast.nh)
+    compare(names, eng, orc, srcs[:: max(1, len(srcs) // 40)], dist64=True)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_linkstate_facade_on_zero_metric_graph(seed):
+    """getSpfResult (metric, nextHops, pathLinks in the reference's order) and
+    getKthPaths k = 1, 2 through the product LinkState."""
+    topo = with_metrics(T.random_graph(30, 70, 90 + seed, max_metric=3, parallel_frac=0.3,
+                                       overload_frac=0.1), zero_frac(0.3), seed)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    with LinkState() as ls:
+        ls.updateAdjacencyDatabases(topo.lsdb)
+        names = ls.flatten()[0]
+        for s in names:
+            assert spf_canonical(ls.getSpfResult(s)) == orc.spf(s), s
+        for s in names[:6]:
+            for d in names:
+                for k in (1, 2):
+                    got = [[link_key(l) for l in p] for p in ls.getKthPaths(s, d, k)]
+                    assert got == orc.kth_paths(s, d, k), (s, d, k)
+
+
+def test_single_source_exact_pop_order_and_ignore_set():
+    topo = with_metrics(T.random_graph(50, 120, 33, max_metric=3, parallel_frac=0.2),
+                        zero_frac(0.3), 2)
+    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+    with SpfEngine(0) as eng:
+        eng.load(rp, col, met, lid, ovl)
+        dist, nh, pop = eng.solve_exact(0)
+        reach = dist != U64_INF
+        # pop ranks: a permutation of the reached nodes, non-decreasing in distance
+        assert sorted(pop[reach].tolist()) == list(range(int(reach.sum())))
+        order = np.argsort(pop[reach])
+        assert (np.diff(dist[reach][order].astype(np.int64)) >= 0).all()
+        # ignoring links: the same as the engine's u32 single-source path
+        ign = sorted(set(int(x) for x in lid))[::5]
+        d2, _, _ = eng.solve_exact(0, ignore_links=ign)
+        assert np.array_equal(eng.sssp(0, ignore_links=ign),
+                              np.where(d2 == U64_INF, 0xFFFFFFFF, d2).astype(np.uint32))
