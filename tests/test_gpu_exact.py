@@ -116,7 +116,9 @@ def test_exact_kernel_equals_fast_kernels(name, make):
     srcs = list(range(len(names)))
     fast = eng.solve(srcs)
     ex = eng.solve(srcs, dist64=True)
-    assert np.array_equal(ex.dist, np.where(fast.dist == 0xFFFFFFFF, U64_INF, fast.dist))
+    want = fast.dist.astype(np.uint64)
+    want[fast.dist == 0xFFFFFFFF] = U64_INF
+    assert np.array_equal(ex.dist, want)
     assert np.array_equal(ex.nh[: fast.nh.size], fast.nh)
     compare(names, eng, orc, srcs[:: max(1, len(srcs) // 40)], dist64=True)
 
