@@ -596,6 +596,19 @@ def main() -> None:
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    from openr_amd.engine import close_all
+
+    close_all()  # plans before contexts, while the HIP runtime is up
+    if os.environ.get("BENCH_FAST_EXIT"):
+        # Profiled runs only.  Under rocprofv3 this process holds two HSA
+        # runtimes -- the profiler's (/opt/rocm-7.2.0) and the one bundled with
+        # torch's HIP runtime (torch/lib) -- and torch's libamdhip64 teardown
+        # in exit() calls into the profiler's libhsa-runtime64 and faults
+        # (addresses resolved against /proc/self/maps).  Every
+        # result and profile is written by now; skip the C exit handlers.
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

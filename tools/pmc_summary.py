@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
 ap.add_argument("--json")
 ap.add_argument("--kernels", default="")
+ap.add_argument("--source", default="", help="provenance tag stored in the JSON")
 args = ap.parse_args()
 
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -44,10 +45,18 @@ if args.json:
         write = cs.get("WRITE_SIZE", 0.0) * 1024
         hit, miss = cs.get("TCC_HIT_sum", 0.0), cs.get("TCC_MISS_sum", 0.0)
         per[k] = {"fetch_bytes_x2": fetch, "write_bytes": write,
-                  "l2_hit_rate": hit / (hit + miss) if hit + miss else None}
+                  "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
+                  "counters_per_dispatch": cs}
+        busy = cs.get("SQ_BUSY_CYCLES")
+        if busy:  # issue-side shares (per SQ, summed over SEs): what bounds the kernel
+            for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
+                      "SQ_WAIT_ANY", "SQ_ACTIVE_INST_LDS"):
+                if c in cs and cs.get("SQ_WAVE_CYCLES"):
+                    per[k][c.lower() + "_per_wave_cycle"] = cs[c] / cs["SQ_WAVE_CYCLES"]
         total += fetch + write
-    out = {"hbm_bytes_per_launch": total, "per_kernel": per,
-           "note": "FETCH_SIZE doubled (gfx950 wide-read correction); WRITE_SIZE as counted"}
+    out = {"hbm_bytes_per_launch": total, "per_kernel": per, "source": args.source,
+           "note": "FETCH_SIZE doubled (gfx950 wide-read correction); WRITE_SIZE as counted; "
+                   "SQ_* per dispatch, *_per_wave_cycle = counter / SQ_WAVE_CYCLES"}
     with open(args.json, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
