@@ -22,7 +22,7 @@ for w in ${WORKLOADS:-fabric_full}; do
   done <<< "${PMC_GROUPS:-FETCH_SIZE
 WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES
-SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT}"
+SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT}"
   python3 tools/pmc_summary.py "$OUT" --json "gpurun_out/$TAG/pmc_$w.json" --source "$TAG" > "$OUT/summary.txt" 2>&1 \
     || { tail -5 "$OUT/summary.txt"; exit 1; }
 done

@@ -50,7 +50,7 @@ if args.json:
         busy = cs.get("SQ_BUSY_CYCLES")
         if busy:  # issue-side shares (per SQ, summed over SEs): what bounds the kernel
             for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
-                      "SQ_WAIT_ANY", "SQ_ACTIVE_INST_LDS"):
+                      "SQ_WAIT_ANY"):
                 if c in cs and cs.get("SQ_WAVE_CYCLES"):
                     per[k][c.lower() + "_per_wave_cycle"] = cs[c] / cs["SQ_WAVE_CYCLES"]
         total += fetch + write
