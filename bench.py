@@ -63,6 +63,74 @@ def oracle():
     return OracleLinkState
 
 
+class Buf:
+    """A device buffer: `ptr` for the C-ABI, `t` the torch tensor on
+    multi-rank runs (collectives), numpy() a host copy."""
+
+    def __init__(self, dev, n: int, dtype, zero: bool) -> None:
+        self.n, self.dtype = int(n), np.dtype(dtype)
+        if dev.torch is not None:
+            tt = {np.dtype(np.int32): dev.torch.int32, np.dtype(np.int64): dev.torch.int64}[self.dtype]
+            mk = dev.torch.zeros if zero else dev.torch.empty
+            self.t = mk(max(1, self.n), dtype=tt, device=dev.device)
+            self.ptr = self.t.data_ptr()
+            self.h = None
+        else:
+            from openr_amd.hiprt import DeviceArray
+
+            self.t = None
+            self.h = DeviceArray(self.n, self.dtype, zero=zero)
+            self.ptr = self.h.ptr
+
+    def numpy(self) -> np.ndarray:
+        return self.t.cpu().numpy() if self.t is not None else self.h.numpy()
+
+    def free(self) -> None:
+        if self.h is not None:
+            self.h.free()
+        self.t = None
+
+
+class Dev:
+    """Device plumbing.  One rank: openr_amd.hiprt (the HIP runtime
+    libopenr_spf.so links, no torch in the process).  Several ranks: torch,
+    for torch.distributed over RCCL; kernels go on torch's current stream."""
+
+    def __init__(self, local: int, world: int) -> None:
+        self.index, self.world = local, world
+        self.bufs = []
+        if world > 1:
+            import torch
+
+            torch.cuda.set_device(local)
+            self.torch, self.device = torch, torch.device("cuda", local)
+        else:
+            from openr_amd import hiprt
+
+            hiprt.set_device(local)
+            self.torch, self.device, self.hip = None, None, hiprt
+
+    def buf(self, n: int, dtype=np.int32, zero: bool = False) -> Buf:
+        b = Buf(self, n, dtype, zero)
+        self.bufs.append(b)
+        return b
+
+    def stream(self) -> int:
+        """hipStream_t for the engine's execute calls (0 = the engine's own)."""
+        return self.torch.cuda.current_stream(self.device).cuda_stream if self.torch else 0
+
+    def sync(self) -> None:
+        if self.torch:
+            self.torch.cuda.synchronize(self.device)
+        else:
+            self.hip.synchronize()
+
+    def close(self) -> None:
+        for b in self.bufs:
+            b.free()
+        self.bufs = []
+
+
 class AllSources:
     """configs[1]/[2]: one all-sources SPF + ECMP pass per step.
 
@@ -81,8 +149,6 @@ class AllSources:
 
     def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb,
                  scaling: str = "strong"):
-        import torch
-
         from openr_amd import topology as T
         from openr_amd.sharding import AllSourcesLayout, snapshot_for_rank
 
@@ -93,10 +159,7 @@ class AllSources:
             topo = T.fabric(10000, full=False)
             self.desc = "fabric_ref numOfSws=10000 (reference generator incl. per-pod emplace quirk)"
         elif name == "fabric_rtt":
-            sys.path.insert(0, str(ROOT / "tests" / "golden"))
-            from make_fullsize_digests import fabric_rtt
-
-            topo = fabric_rtt()
+            topo = T.fabric_rtt()
             self.desc = ("fabric_full wiring, per-direction metrics max(rtt/100,1) from seeded RTTs "
                          "(LinkMonitor.cpp:44-47), weighted SPF")
         else:
@@ -121,9 +184,9 @@ class AllSources:
         cap = self.layout.cap
         self.dist_words = len(srcs) * pitch
         self.nbuf = 2 if gather else 1
-        self.send = [torch.zeros(max(1, cap), dtype=torch.int32, device=dev)
-                     for _ in range(self.nbuf)]
-        self.recv = ([torch.zeros((world, max(1, cap)), dtype=torch.int32, device=dev)
+        self.send = [dev.buf(max(1, cap), zero=True) for _ in range(self.nbuf)]
+        self.recv = ([dev.torch.zeros((world, max(1, cap)), dtype=dev.torch.int32,
+                                      device=dev.device)
                       for _ in range(self.nbuf)] if gather and rank == 0 else None)
         self.works = [None] * self.nbuf
         self.gather = gather
@@ -148,18 +211,18 @@ class AllSources:
             "one rank, all sources" if scaling == "strong" else
             f"weak: one LSDB snapshot per rank ({world} ranks), results stay on each GPU")
 
-    def step(self, stream) -> None:
-        import torch.distributed as dist
-
+    def step(self) -> None:
         b = self.i % self.nbuf
         self.i += 1
         if self.works[b] is not None:  # the gather that last read this buffer
             self.works[b].wait()
         buf = self.send[b]
-        self.plan.execute(buf.data_ptr(), buf.data_ptr() + 4 * self.dist_words, stream.cuda_stream)
+        self.plan.execute(buf.ptr, buf.ptr + 4 * self.dist_words, self.dev.stream())
         if self.gather:
+            import torch.distributed as dist
+
             out = list(self.recv[b].unbind(0)) if self.rank == 0 else None
-            self.works[b] = dist.gather(buf, out, dst=0, async_op=True)
+            self.works[b] = dist.gather(buf.t, out, dst=0, async_op=True)
 
     def finish(self) -> None:
         for w in self.works:
@@ -247,8 +310,6 @@ class Ksp2AllPairs:
     kernels = ("sssp_kernel", "ksp2_kernel")
 
     def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
-        import torch
-
         from openr_amd import topology as T
         from openr_amd.engine import PAIR_DTYPE
 
@@ -264,17 +325,16 @@ class Ksp2AllPairs:
         n_pairs = len(self.srcs) * self.n
         self.units = n_pairs
         self.pair_words = PAIR_DTYPE.itemsize // 4
-        self.d_pairs = torch.empty(n_pairs * self.pair_words, dtype=torch.int32, device=dev)
-        self.d_cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.d_pairs = dev.buf(n_pairs * self.pair_words)
+        self.d_cnt = dev.buf(4, np.int64, zero=True)
         # size the path pool with one untimed sizing run (the counter keeps
         # counting past an overflow)
         self.pool_words = 1 << 20
-        self.d_pool = torch.empty(self.pool_words, dtype=torch.int32, device=dev)
-        self.plan.execute(self.d_pairs.data_ptr(), self.d_pool.data_ptr(), self.pool_words,
-                          self.d_cnt.data_ptr(), 0)
-        torch.cuda.synchronize(dev)
-        self.pool_words = int(int(self.d_cnt[0].item()) * 1.05) + (1 << 22)
-        self.d_pool = torch.empty(self.pool_words, dtype=torch.int32, device=dev)
+        pool0 = dev.buf(self.pool_words)
+        self.plan.execute(self.d_pairs.ptr, pool0.ptr, self.pool_words, self.d_cnt.ptr, 0)
+        dev.sync()
+        self.pool_words = int(int(self.d_cnt.numpy()[0]) * 1.05) + (1 << 22)
+        self.d_pool = dev.buf(self.pool_words)
         self.gathered = 0
         # one k = 2 solve per pair (B_solve without next hops)
         # + 4 B per output link; the k = 1 SPF rows are charged per source.
@@ -284,26 +344,23 @@ class Ksp2AllPairs:
         self.parallelism = (f"sources dealt round-robin over {world} rank(s), graph replicated; "
                             "pair headers + path pools gathered to rank 0 (RCCL gather) in the step")
 
-    def step(self, stream) -> None:
-        import torch
-        import torch.distributed as dist
-
-        self.plan.execute(self.d_pairs.data_ptr(), self.d_pool.data_ptr(), self.pool_words,
-                          self.d_cnt.data_ptr(), stream.cuda_stream)
+    def step(self) -> None:
+        self.plan.execute(self.d_pairs.ptr, self.d_pool.ptr, self.pool_words, self.d_cnt.ptr,
+                          self.dev.stream())
         if self.world > 1:
             # one exchange: every rank's pair headers and path pool to rank 0
             from openr_amd.sharding import gather_padded
 
-            used = int(self.d_cnt[0].item())
-            gather_padded(self.d_pairs, self.d_pairs.numel())
-            gather_padded(self.d_pool, used)
+            used = int(self.d_cnt.t[0].item())
+            gather_padded(self.d_pairs.t, self.d_pairs.t.numel())
+            gather_padded(self.d_pool.t, used)
 
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
 
     def kernel_ms(self):
         a, b, cnt = self.plan.timing()
-        cnt_h = self.d_cnt.cpu().numpy()
+        cnt_h = self.d_cnt.numpy()
         if cnt_h[2] & 1:
             raise SystemExit("KSP2 path pool overflowed: raise pool_words")
         # path pool words = records [len, next, links]; output links ~ words
@@ -354,8 +411,6 @@ class WhatIfAllLinks:
     kernels = ("base", "failures")
 
     def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
-        import torch
-
         from openr_amd import topology as T
         from openr_amd.engine import DIGEST_DTYPE
         from openr_amd.link_state import LinkState
@@ -376,9 +431,8 @@ class WhatIfAllLinks:
         self.links = all_links[rank::world]
         self.plan = eng.whatif_plan(self.src, self.links)
         self.units = len(self.links)
-        self.d_out = torch.empty(max(1, self.units) * DIGEST_DTYPE.itemsize // 8,
-                                 dtype=torch.int64, device=dev)
-        self.d_base = torch.empty(2, dtype=torch.int64, device=dev)
+        self.d_out = dev.buf(max(1, self.units) * DIGEST_DTYPE.itemsize // 8, np.int64)
+        self.d_base = dev.buf(2, np.int64)
         # a what-if solve is B_solve with a 24 B digest in
         # place of the dense result: 4(N+1) + 8E + N + 24
         n, e = self.n, self.e
@@ -396,15 +450,12 @@ class WhatIfAllLinks:
                             "unfailed SPF recomputed per rank; digests gathered to rank 0 "
                             "(RCCL gather) in the step")
 
-    def step(self, stream) -> None:
-        import torch
-        import torch.distributed as dist
-
-        self.plan.execute(self.d_out.data_ptr(), self.d_base.data_ptr(), stream.cuda_stream)
+    def step(self) -> None:
+        self.plan.execute(self.d_out.ptr, self.d_base.ptr, self.dev.stream())
         if self.world > 1:  # one exchange: every rank's digests to rank 0
             from openr_amd.sharding import gather_padded
 
-            gather_padded(self.d_out, self.d_out.numel())
+            gather_padded(self.d_out.t, self.d_out.t.numel())
 
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
@@ -469,16 +520,16 @@ def main() -> None:
                          "rank with results left on each GPU (weak)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
     if world > 1:
+        import torch
+        import torch.distributed as dist
+
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = Dev(local, world)
 
     from openr_amd.engine import SpfEngine, graph_from_lsdb
 
@@ -487,36 +538,34 @@ def main() -> None:
         wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb, scaling=args.scaling)
     else:
         wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb)
-    stream = torch.cuda.current_stream(dev)
-
     for _ in range(args.warmup):
-        wl.step(stream)
+        wl.step()
     getattr(wl, "finish", lambda: None)()
-    torch.cuda.synchronize(dev)
+    dev.sync()
     wl.enable_timing(max(1, args.steps))
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    dev.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        wl.step(stream)
+        wl.step()
     getattr(wl, "finish", lambda: None)()
-    torch.cuda.synchronize(dev)
+    dev.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+        elapsed = float(t.item())
     kms = wl.kernel_ms()
     launch_ms = sum(kms.values())
 
     # whole-job units: weak = every rank did `units`; strong = ranks split them
     units = wl.units
     if world > 1:
-        u = torch.tensor([units], dtype=torch.float64, device=dev)
+        u = torch.tensor([units], dtype=torch.float64, device=dev.device)
         dist.all_reduce(u)
         units = float(u.item())
     value = units * args.steps / elapsed
@@ -599,16 +648,7 @@ def main() -> None:
     from openr_amd.engine import close_all
 
     close_all()  # plans before contexts, while the HIP runtime is up
-    if os.environ.get("BENCH_FAST_EXIT"):
-        # Profiled runs only.  Under rocprofv3 this process holds two HSA
-        # runtimes -- the profiler's (/opt/rocm-7.2.0) and the one bundled with
-        # torch's HIP runtime (torch/lib) -- and torch's libamdhip64 teardown
-        # in exit() calls into the profiler's libhsa-runtime64 and faults
-        # (addresses resolved against /proc/self/maps).  Every
-        # result and profile is written by now; skip the C exit handlers.
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
+    dev.close()
 
 
 if __name__ == "__main__":

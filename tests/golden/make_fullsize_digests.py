@@ -51,21 +51,7 @@ from openr_amd import topology as T  # noqa: E402
 from openr_amd.link_state import LinkState  # noqa: E402
 
 
-def fabric_rtt(seed: int = 7) -> T.Topology:
-    """fabric_full wiring with per-direction metrics max(rtt/100, 1)
-    (LinkMonitor.cpp:44-47), rtt in microseconds drawn per adjacency:
-    intra-pod 40-400 us, pod-to-spine 200-3000 us (seeded)."""
-    topo = T.fabric(10000, full=True)
-    rng = np.random.default_rng(seed)
-    src, dst = topo.adj_src, topo.adj_dst
-    spine = np.array([n.startswith("1-") for n in topo.nodes])
-    far = spine[src] | spine[dst]
-    rtt = np.where(far, rng.integers(200, 3001, len(src)), rng.integers(40, 401, len(src)))
-    metric = np.maximum(rtt // 100, 1).astype(np.int32)
-    topo.lsdb.adjs["metric"] = metric
-    topo.metric = metric
-    topo.name = "fabric_rtt"
-    return topo
+fabric_rtt = T.fabric_rtt  # openr_amd/topology.py (same seeded generator)
 
 
 WORKLOADS = {

@@ -5,7 +5,7 @@
 #   TAG=r02_v4 WORKLOADS="fabric_full grid100" bash tools/pmc_round.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-export TMPDIR=/tmp BENCH_FAST_EXIT=1
+export TMPDIR=/tmp
 TAG=${TAG:-pmc}
 for w in ${WORKLOADS:-fabric_full}; do
   OUT=gpurun_out/$TAG/pmc_$w
