@@ -649,6 +649,8 @@ def main() -> None:
 
     close_all()  # plans before contexts, while the HIP runtime is up
     dev.close()
+    if world == 1 and os.environ.get("BENCH_DEVICE_RESET"):
+        dev.hip.device_reset()
 
 
 if __name__ == "__main__":

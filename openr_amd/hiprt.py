@@ -40,6 +40,11 @@ def synchronize() -> None:
     _check(_lib.hipDeviceSynchronize(), "hipDeviceSynchronize")
 
 
+def device_reset() -> None:
+    """Release every device resource of this process now (hipDeviceReset)."""
+    _check(_lib.hipDeviceReset(), "hipDeviceReset")
+
+
 class DeviceArray:
     """A device allocation of `n` elements of `dtype` (no torch)."""
 
