@@ -147,6 +147,50 @@ spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids /* [n_nodes] */)
 spf_status ls_graph_csr(ls_state* ls, uint32_t* row_ptr, uint32_t* col, int32_t* metric,
                         uint32_t* link_id, uint8_t* overloaded);
 
+/* ---- standalone value types of LinkState.h ------------------------------ */
+/* openr::Link (LinkState.h:82-175): a link built outside a LinkState, as
+ * LinkTest constructs one -- Link(area, node1, adj1, node2, adj2),
+ * LinkState.cpp:127-186.  Side accessors take a node name and fail with
+ * SPF_E_INVALID for a node not on the link (the reference throws
+ * std::invalid_argument, LinkState.cpp:163-172). */
+typedef struct ls_link ls_link;
+spf_status ls_link_create(const char* area, const char* node1, const char* if1, int32_t metric1,
+                          int32_t adj_label1, int overload1, const char* node2, const char* if2,
+                          int32_t metric2, int32_t adj_label2, int overload2, ls_link** out);
+void ls_link_destroy(ls_link* link);
+const char* ls_link_area(const ls_link* link);                 /* getArea           */
+uint64_t ls_link_hash(const ls_link* link);                    /* Link::hash        */
+int ls_link_is_up(const ls_link* link);                        /* isUp              */
+int ls_link_equal(const ls_link* a, const ls_link* b);         /* operator==        */
+int ls_link_less(const ls_link* a, const ls_link* b);          /* operator<         */
+spf_status ls_link_other_node(const ls_link* link, const char* node, const char** out);
+spf_status ls_link_iface(const ls_link* link, const char* node, const char** out);
+spf_status ls_link_metric(const ls_link* link, const char* node, uint64_t* out);
+spf_status ls_link_adj_label(const ls_link* link, const char* node, int32_t* out);
+spf_status ls_link_overload(const ls_link* link, const char* node, int* out);
+/* setMetricFromNode / setOverloadFromNode (LinkState.cpp:253-286): *changed =
+ * the effective metric changed now / the link's up state changed. */
+spf_status ls_link_set_metric(ls_link* link, const char* node, uint64_t metric,
+                              uint64_t hold_up, uint64_t hold_down, int* changed);
+spf_status ls_link_set_overload(ls_link* link, const char* node, int overload,
+                                uint64_t hold_up, uint64_t hold_down, int* changed);
+
+/* LinkState::pathAInPathB (static, LinkState.h:395-410) over paths given as
+ * link ids of one LinkState (ls_get_kth_paths): 1 when a is a contiguous
+ * run of b. */
+int ls_path_a_in_path_b(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb);
+
+/* HoldableValue<bool> / HoldableValue<LinkStateMetric> (LinkState.h:36-58,
+ * LinkState.cpp:54-125). */
+typedef struct ls_holdable ls_holdable;
+ls_holdable* ls_holdable_create(int is_bool, uint64_t value);
+void ls_holdable_destroy(ls_holdable* h);
+uint64_t ls_holdable_value(const ls_holdable* h);
+int ls_holdable_has_hold(const ls_holdable* h);
+int ls_holdable_decrement_ttl(ls_holdable* h);
+int ls_holdable_update_value(ls_holdable* h, uint64_t value, uint64_t hold_up_ttl,
+                             uint64_t hold_down_ttl);
+
 #ifdef __cplusplus
 }
 #endif

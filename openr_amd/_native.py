@@ -235,6 +235,31 @@ PROTOTYPES = {
     "openr_wire_last_error": (C.c_char_p, []),
     "ls_apply_publication": (C.c_int, [_vp, C.c_char_p, C.c_size_t, _u32p, _u32p,
                                        C.POINTER(LsChange)]),
+    "ls_link_create": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32,
+                                 C.c_int, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, C.c_int,
+                                 C.POINTER(_vp)]),
+    "ls_link_destroy": (None, [_vp]),
+    "ls_link_area": (C.c_char_p, [_vp]),
+    "ls_link_hash": (C.c_uint64, [_vp]),
+    "ls_link_is_up": (C.c_int, [_vp]),
+    "ls_link_equal": (C.c_int, [_vp, _vp]),
+    "ls_link_less": (C.c_int, [_vp, _vp]),
+    "ls_link_other_node": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_char_p)]),
+    "ls_link_iface": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_char_p)]),
+    "ls_link_metric": (C.c_int, [_vp, C.c_char_p, _u64p]),
+    "ls_link_adj_label": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_int32)]),
+    "ls_link_overload": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_int)]),
+    "ls_link_set_metric": (C.c_int, [_vp, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                     C.POINTER(C.c_int)]),
+    "ls_link_set_overload": (C.c_int, [_vp, C.c_char_p, C.c_int, C.c_uint64, C.c_uint64,
+                                       C.POINTER(C.c_int)]),
+    "ls_path_a_in_path_b": (C.c_int, [_u32p, C.c_uint32, _u32p, C.c_uint32]),
+    "ls_holdable_create": (_vp, [C.c_int, C.c_uint64]),
+    "ls_holdable_destroy": (None, [_vp]),
+    "ls_holdable_value": (C.c_uint64, [_vp]),
+    "ls_holdable_has_hold": (C.c_int, [_vp]),
+    "ls_holdable_decrement_ttl": (C.c_int, [_vp]),
+    "ls_holdable_update_value": (C.c_int, [_vp, C.c_uint64, C.c_uint64, C.c_uint64]),
     "ls_apply_publication_ordered": (C.c_int, [_vp, C.c_char_p, C.c_size_t, C.c_char_p, _u32p,
                                                _u32p, C.POINTER(LsChange)]),
 }

@@ -1096,4 +1096,139 @@ spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids) {
   return SPF_OK;
 }
 
+
+// ---- standalone Link / HoldableValue / pathAInPathB (LinkState.h) ------------
+struct ls_link {
+  std::string area;
+  std::string name[2];
+  LinkObj obj;
+  int side(const char* n) const {
+    if (name[0] == n) return 0;
+    if (name[1] == n) return 1;
+    return -1;
+  }
+};
+
+struct ls_holdable {
+  bool is_bool;
+  Holdable<bool> b{false};
+  Holdable<Metric> m{0};
+};
+
+spf_status ls_link_create(const char* area, const char* node1, const char* if1, int32_t metric1,
+                          int32_t adj_label1, int overload1, const char* node2, const char* if2,
+                          int32_t metric2, int32_t adj_label2, int overload2, ls_link** out) {
+  if (!area || !node1 || !if1 || !node2 || !if2 || !out) return SPF_E_INVALID;
+  auto l = std::make_unique<ls_link>();
+  l->area = area;
+  l->name[0] = node1;
+  l->name[1] = node2;
+  const char* ifs[2] = {if1, if2};
+  const int32_t met[2] = {metric1, metric2}, lab[2] = {adj_label1, adj_label2};
+  const int ovl[2] = {overload1, overload2};
+  for (int i = 0; i < 2; ++i) {
+    Side& sd = l->obj.s[i];
+    sd.node = (uint32_t)i;
+    sd.ifname = ifs[i];
+    sd.metric.set((Metric)(int64_t)met[i]);  // i32 -> u64 like the reference
+    sd.overload.set(ovl[i] != 0);
+    sd.label = lab[i];
+  }
+  l->obj.names = std::minmax(std::make_pair(l->name[0], std::string(if1)),
+                             std::make_pair(l->name[1], std::string(if2)));
+  const auto& nm = l->obj.names;
+  l->obj.hash = folly_mix(folly_mix(std::hash<std::string>()(nm.first.first),
+                                    std::hash<std::string>()(nm.first.second)),
+                          folly_mix(std::hash<std::string>()(nm.second.first),
+                                    std::hash<std::string>()(nm.second.second)));
+  *out = l.release();
+  return SPF_OK;
+}
+void ls_link_destroy(ls_link* l) { delete l; }
+const char* ls_link_area(const ls_link* l) { return l ? l->area.c_str() : nullptr; }
+uint64_t ls_link_hash(const ls_link* l) { return l ? l->obj.hash : 0; }
+int ls_link_is_up(const ls_link* l) { return l && l->obj.up(); }
+int ls_link_equal(const ls_link* a, const ls_link* b) { return a && b && a->obj.same(b->obj); }
+int ls_link_less(const ls_link* a, const ls_link* b) { return a && b && a->obj.before(b->obj); }
+
+#define LS_SIDE(l, node)                                   \
+  const int sd_ = (l && node) ? (l)->side(node) : -1;       \
+  if (sd_ < 0) return SPF_E_INVALID; /* std::invalid_argument */
+
+spf_status ls_link_other_node(const ls_link* l, const char* node, const char** out) {
+  LS_SIDE(l, node);
+  *out = l->name[1 - sd_].c_str();
+  return SPF_OK;
+}
+spf_status ls_link_iface(const ls_link* l, const char* node, const char** out) {
+  LS_SIDE(l, node);
+  *out = l->obj.s[sd_].ifname.c_str();
+  return SPF_OK;
+}
+spf_status ls_link_metric(const ls_link* l, const char* node, uint64_t* out) {
+  LS_SIDE(l, node);
+  *out = l->obj.s[sd_].metric.get();
+  return SPF_OK;
+}
+spf_status ls_link_adj_label(const ls_link* l, const char* node, int32_t* out) {
+  LS_SIDE(l, node);
+  *out = l->obj.s[sd_].label;
+  return SPF_OK;
+}
+spf_status ls_link_overload(const ls_link* l, const char* node, int* out) {
+  LS_SIDE(l, node);
+  *out = l->obj.s[sd_].overload.get() ? 1 : 0;
+  return SPF_OK;
+}
+// Link::setMetricFromNode / setOverloadFromNode (LinkState.cpp:253-286):
+// *changed = the metric changed now / the link's up-state changed
+spf_status ls_link_set_metric(ls_link* l, const char* node, uint64_t metric, uint64_t hold_up,
+                              uint64_t hold_down, int* changed) {
+  LS_SIDE(l, node);
+  const bool c = l->obj.s[sd_].metric.update(metric, hold_up, hold_down);
+  if (changed) *changed = c;
+  return SPF_OK;
+}
+spf_status ls_link_set_overload(ls_link* l, const char* node, int overload, uint64_t hold_up,
+                                uint64_t hold_down, int* changed) {
+  LS_SIDE(l, node);
+  const bool was_up = l->obj.up();
+  l->obj.s[sd_].overload.update(overload != 0, hold_up, hold_down);
+  if (changed) *changed = was_up != l->obj.up();
+  return SPF_OK;
+}
+#undef LS_SIDE
+
+// LinkState::pathAInPathB (LinkState.h:395-410): a occurs in b as a contiguous
+// run of equal links (Link::operator==; link ids of one LinkState identify
+// links).
+int ls_path_a_in_path_b(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) {
+  if (na > nb) return 0;
+  for (uint32_t i = 0; i < nb - na + 1; ++i) {
+    uint32_t ai = 0, bi = i;
+    while (ai < na && a[ai] == b[bi]) {
+      ++ai;
+      ++bi;
+    }
+    if (ai == na) return 1;
+  }
+  return 0;
+}
+
+ls_holdable* ls_holdable_create(int is_bool, uint64_t value) {
+  auto* h = new ls_holdable{is_bool != 0};
+  if (h->is_bool) h->b.set(value != 0);
+  else h->m.set(value);
+  return h;
+}
+void ls_holdable_destroy(ls_holdable* h) { delete h; }
+uint64_t ls_holdable_value(const ls_holdable* h) {
+  return h->is_bool ? (uint64_t)h->b.get() : h->m.get();
+}
+int ls_holdable_has_hold(const ls_holdable* h) { return h->is_bool ? h->b.has_hold() : h->m.has_hold(); }
+int ls_holdable_decrement_ttl(ls_holdable* h) { return h->is_bool ? h->b.tick() : h->m.tick(); }
+int ls_holdable_update_value(ls_holdable* h, uint64_t v, uint64_t hold_up, uint64_t hold_down) {
+  return h->is_bool ? h->b.update(v != 0, hold_up, hold_down) : h->m.update(v, hold_up, hold_down);
+}
+
 }  // extern "C"

@@ -32,9 +32,10 @@ class Link:
     """Snapshot of ``openr::Link`` (LinkState.h:82-175) taken at query time."""
 
     __slots__ = ("_n1", "_n2", "_if1", "_if2", "_m1", "_m2", "_l1", "_l2",
-                 "_o1", "_o2", "_up", "hash", "_key", "_area", "_v4", "_v6")
+                 "_o1", "_o2", "_up", "hash", "_key", "_area", "_v4", "_v6", "_ident")
 
-    def __init__(self, ls: "LinkState", d: N.LsLinkDesc) -> None:
+    def __init__(self, ls: "LinkState", d: N.LsLinkDesc, link_id: int = -1) -> None:
+        self._ident = (id(ls), link_id)  # pathAInPathB identity (one link of one LinkState)
         name = ls._name
         self._n1, self._n2 = name(d.node1), name(d.node2)
         self._if1, self._if2 = d.if1.decode(), d.if2.decode()
@@ -201,7 +202,7 @@ class LinkState(N.NativeHandle):
         if lk is None:
             d = N.LsLinkDesc()
             self._err(N.lib.ls_link_info(self._h, link_id, C.byref(d)))
-            lk = Link(self, d)
+            lk = Link(self, d, link_id)
             self._link_cache[link_id] = lk
         return lk
 
@@ -359,15 +360,21 @@ class LinkState(N.NativeHandle):
         return int(m.value)
 
     @staticmethod
-    def pathAInPathB(a: Sequence[Link], b: Sequence[Link]) -> bool:
-        """``LinkState::pathAInPathB`` (LinkState.h:395-410): a is a contiguous
-        sub-path of b."""
-        if len(a) > len(b):
-            return False
-        for i in range(len(b) - len(a) + 1):
-            if all(a[j] == b[i + j] for j in range(len(a))):
-                return True
-        return False
+    def pathAInPathB(a: Sequence, b: Sequence) -> bool:
+        """``LinkState::pathAInPathB`` (LinkState.h:395-410) through the C-ABI
+        (``ls_path_a_in_path_b``): a is a contiguous run of b.  Links compare
+        by identity, as the reference's shared_ptr<Link> elements do: the same
+        link of one LinkState, or the same standalone ``OwnedLink``."""
+        import numpy as np
+
+        ids: Dict[object, int] = {}
+
+        def enc(p):
+            return np.array([ids.setdefault(getattr(l, "_ident", None) or ("obj", id(l)), len(ids))
+                             for l in p] or [0], np.uint32)
+
+        ea, eb = enc(a), enc(b)
+        return bool(N.lib.ls_path_a_in_path_b(N.ptr(ea), len(a), N.ptr(eb), len(b)))
 
     # -- batch access to the flattened graph ---------------------------------------
     def flatten(self):
@@ -392,3 +399,98 @@ class LinkState(N.NativeHandle):
 
     def engine_handle(self) -> C.c_void_p:
         return C.c_void_p(N.lib.ls_engine(self._h))
+
+
+class OwnedLink(N.NativeHandle):
+    """A standalone ``openr::Link`` (LinkState.h:82-175) built from two
+    adjacencies, as ``Link(area, n1, adj1, n2, adj2)`` (LinkState.cpp:127-186)
+    -- the C-ABI ``ls_link_*`` object.  Side accessors raise ValueError for a
+    node not on the link (std::invalid_argument in the reference)."""
+
+    _destroy = "ls_link_destroy"
+
+    def __init__(self, area: str, node1: str, adj1, node2: str, adj2) -> None:
+        h = C.c_void_p()
+        N.raise_for(N.lib.ls_link_create(
+            area.encode(), node1.encode(), adj1.ifName.encode(), adj1.metric, adj1.adjLabel,
+            int(adj1.isOverloaded), node2.encode(), adj2.ifName.encode(), adj2.metric,
+            adj2.adjLabel, int(adj2.isOverloaded), C.byref(h)), "ls_link_create")
+        self._adopt(h)
+
+    def _side(self, fn, node: str, out):
+        if fn(self._h, node.encode(), C.byref(out)) != N.SPF_OK:
+            raise ValueError(node)
+        return out.value
+
+    def getArea(self) -> str:
+        return N.lib.ls_link_area(self._h).decode()
+
+    @property
+    def hash(self) -> int:
+        return int(N.lib.ls_link_hash(self._h))
+
+    def getOtherNodeName(self, node: str) -> str:
+        return self._side(N.lib.ls_link_other_node, node, C.c_char_p()).decode()
+
+    def getIfaceFromNode(self, node: str) -> str:
+        return self._side(N.lib.ls_link_iface, node, C.c_char_p()).decode()
+
+    def getMetricFromNode(self, node: str) -> int:
+        return int(self._side(N.lib.ls_link_metric, node, C.c_uint64()))
+
+    def getAdjLabelFromNode(self, node: str) -> int:
+        return int(self._side(N.lib.ls_link_adj_label, node, C.c_int32()))
+
+    def getOverloadFromNode(self, node: str) -> bool:
+        return bool(self._side(N.lib.ls_link_overload, node, C.c_int()))
+
+    def isUp(self) -> bool:
+        return bool(N.lib.ls_link_is_up(self._h))
+
+    def setMetricFromNode(self, node: str, metric: int, holdUpTtl: int, holdDownTtl: int) -> bool:
+        ch = C.c_int()
+        if N.lib.ls_link_set_metric(self._h, node.encode(), metric, holdUpTtl, holdDownTtl,
+                                    C.byref(ch)) != N.SPF_OK:
+            raise ValueError(node)
+        return bool(ch.value)
+
+    def setOverloadFromNode(self, node: str, overload: bool, holdUpTtl: int,
+                            holdDownTtl: int) -> bool:
+        ch = C.c_int()
+        if N.lib.ls_link_set_overload(self._h, node.encode(), int(overload), holdUpTtl,
+                                      holdDownTtl, C.byref(ch)) != N.SPF_OK:
+            raise ValueError(node)
+        return bool(ch.value)
+
+    def __eq__(self, other: object) -> bool:
+        return isinstance(other, OwnedLink) and bool(N.lib.ls_link_equal(self._h, other._h))
+
+    def __lt__(self, other: "OwnedLink") -> bool:
+        return bool(N.lib.ls_link_less(self._h, other._h))
+
+    def __hash__(self) -> int:  # equal links have equal Link::hash
+        return self.hash
+
+
+class HoldableValue(N.NativeHandle):
+    """``openr::HoldableValue<bool>`` / ``<LinkStateMetric>`` (LinkState.h:36-58,
+    LinkState.cpp:54-125), the C-ABI ``ls_holdable_*`` object."""
+
+    _destroy = "ls_holdable_destroy"
+
+    def __init__(self, value) -> None:
+        self._bool = isinstance(value, bool)
+        self._adopt(C.c_void_p(N.lib.ls_holdable_create(int(self._bool), int(value))))
+
+    def value(self):
+        v = int(N.lib.ls_holdable_value(self._h))
+        return bool(v) if self._bool else v
+
+    def hasHold(self) -> bool:
+        return bool(N.lib.ls_holdable_has_hold(self._h))
+
+    def decrementTtl(self) -> bool:
+        return bool(N.lib.ls_holdable_decrement_ttl(self._h))
+
+    def updateValue(self, value, holdUpTtl: int, holdDownTtl: int) -> bool:
+        return bool(N.lib.ls_holdable_update_value(self._h, int(value), holdUpTtl, holdDownTtl))

@@ -49,14 +49,14 @@ class Topology:
 
 
 def _build(name, nodes, src, dst, metric, if_fmt=None, ifs=None, oifs=None,
-           adj_label=None, node_overloaded=None) -> Topology:
+           adj_label=None, node_overloaded=None, node_label=None) -> Topology:
     src = np.asarray(src, np.int64)
     dst = np.asarray(dst, np.int64)
     if ifs is None:
         ifs = [if_fmt(nodes[a], nodes[b]) for a, b in zip(src.tolist(), dst.tolist())]
         oifs = [if_fmt(nodes[b], nodes[a]) for a, b in zip(src.tolist(), dst.tolist())]
     packed = pack_fast(nodes, src, dst, ifs, oifs, metric, node_overloaded=node_overloaded,
-                       adj_label=adj_label)
+                       adj_label=adj_label, node_label=node_label)
     return Topology(name, list(nodes), src, dst, np.asarray(metric, np.int32), packed)
 
 
@@ -91,7 +91,8 @@ def decision_test_grid(n: int) -> Topology:
                     ifs.append(a)
                     oifs.append(b)
     return _build(f"dtgrid{n}", nodes, src, dst, np.ones(len(src), np.int32), ifs=ifs,
-                  oifs=oifs, adj_label=100001 + np.asarray(dst))
+                  oifs=oifs, adj_label=100001 + np.asarray(dst),
+                  node_label=np.arange(1, n * n + 1))  # createAdjDb(name, adjs, node + 1)
 
 
 def fabric(num_sws: int = 10000, full: bool = True,

@@ -88,3 +88,40 @@ def test_pop_and_adjacency_label_routes():
             (nh,) = db.mplsRoutes[lab].nexthops
             assert nh.mplsAction.action == "PHP" and nh.ifName == link.getIfaceFromNode(me)
             assert nh.metric == link.getMetricFromNode(me)
+
+
+@pytest.mark.parametrize("n", [2, 4, 6, 8])
+def test_grid_route_count_and_distances(n):
+    """DecisionTest.cpp:4301-4356 (GridTopologyFixture.ShortestPathTest): every
+    node's buildRouteDb over the n x n grid (createGrid, :4238-4264: node
+    label node + 1, one v6 loopback per node) programs n^2 (n^2 - 1) unicast,
+    n^2 * n^2 node-label and 4n (n - 1) adjacency-label routes in total,
+    2n^4 + 3n^2 - 4n (:4313), and corner-to-corner / any-pair metrics are the
+    Manhattan distances."""
+    from openr_amd.spf_solver import PrefixEntry, PrefixState
+
+    topo = T.decision_test_grid(n)
+    ps = PrefixState()
+    pfx = {}
+    for node in range(n * n):
+        pfx[node] = f"::ffff:10.1.{node // 256}.{node % 256}/128"  # nodeToPrefixV6
+        ps.updatePrefix(str(node), "0", PrefixEntry(pfx[node]))
+    with LinkState() as ls:
+        ls.updateAdjacencyDatabases(topo.lsdb)
+        total, dbs = 0, {}
+        for node in range(n * n):
+            me = str(node)
+            db = SpfSolver(me, False, False).buildRouteDb(me, {ls.getArea(): ls}, ps)
+            total += len(db.unicastRoutes) + len(db.mplsRoutes)
+            dbs[node] = db
+        assert total == 2 * n ** 4 + 3 * n ** 2 - 4 * n
+
+        def grid_distance(a, b):
+            return abs(a % n - b % n) + abs(a // n - b // n)
+
+        rng = np.random.default_rng(n)
+        pairs = [(0, n * n - 1), (n - 1, n * (n - 1))] + \
+            [tuple(int(x) for x in rng.choice(n * n, 2, replace=False)) for _ in range(8)]
+        for src, dst in pairs:
+            nhs = dbs[src].unicastRoutes[pfx[dst]].nexthops
+            assert {h.metric for h in nhs} == {grid_distance(src, dst)}
