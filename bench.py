@@ -198,8 +198,10 @@ class AllSources:
         self.survey_bytes = int(len(srcs) * (4 * (n + 1) + 8 * e + n + 4 * n)
                                 + len(srcs) * int(np.sum((k[srcs] + 7) // 8)))
         bfs, narrow = self.plan.kernels()
-        self.kernels = (bfs, self.plan.ecmp_kernel() or "ecmp_kernel")
+        self.kernels = (bfs, "ecmp_kernel")
         self.narrow = narrow
+        tb, te = self.plan.traffic()
+        self.kernel_bytes = {bfs: tb, "ecmp_kernel": te}
         self.parallelism = (
             f"sources in contiguous id blocks over {world} rank(s) (one LSDB), plan closure "
             f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source dist rows + "
@@ -232,9 +234,7 @@ class AllSources:
 
     def kernel_ms(self):
         a, b, cnt = self.plan.timing()
-        tb, te = self.plan.traffic()  # after an execute: level-bitmap reads are known
-        self.kernel_bytes = {self.kernels[0]: tb, self.kernels[1]: te}
-        return {self.kernels[0]: a / max(cnt, 1), self.kernels[1]: b / max(cnt, 1)}
+        return {self.kernels[0]: a / max(cnt, 1), "ecmp_kernel": b / max(cnt, 1)}
 
     def edges_per_unit(self) -> int:
         return self.e

@@ -100,9 +100,6 @@ struct spf_plan {
   bool ms = false;      // unit metrics: multi-source BFS
   bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
-  bool levels = false;  // msbfs writes level bitmaps, ecmp_levels_kernel reads them
-  spfi::DevBuf<unsigned long long> d_LB;  // [rows][kLbLevels][n_slices] level bitmaps
-  spfi::DevBuf<uint32_t> d_ecc;           // [rows] last BFS level of each row
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
   spfi::DevBuf<uint8_t> d_Dn;

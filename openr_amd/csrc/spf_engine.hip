@@ -237,7 +237,6 @@ constexpr uint32_t kMsMaxNodes = kMsThreads * kMsMaxOwn;  // 16384 (F: 128 KiB o
 constexpr int kMsUnroll = 8;
 constexpr uint32_t kMsLaneStoreRatio = 4;  // per-lane stores when 4 * max per-node count < #sources
 constexpr uint32_t kSliceW = 64;  // nodes per sliced-ELL slice (= wave width)
-constexpr uint32_t kLbLevels = 8;  // level bitmaps kept per row (levels 0..7)
 
 // Narrow (u8) distance rows: npitch bytes (a multiple of 1024), node v at
 // byte v -- a level's stores are 64 consecutive bytes per (source, slice),
@@ -264,12 +263,10 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     uint32_t n_col, const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
     uint32_t n_rows, uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch,
     uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
-    unsigned long long* __restrict__ LB, uint32_t* __restrict__ ecc, uint32_t lvls,
     unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* F = reinterpret_cast<uint64_t*>(smem);             // [N + 1]
-  unsigned long long* lvl_or = reinterpret_cast<unsigned long long*>(F + N + 1);  // [2] LB mode
-  uint32_t* o_node = reinterpret_cast<uint32_t*>(lvl_or + 2);  // [64] drained batch sources
+  uint32_t* o_node = reinterpret_cast<uint32_t*>(F + N + 1);   // [64] drained batch sources
   uint32_t* o_cnt = o_node + kMsBatch;                         // [1]
   uint32_t* flag = o_cnt + 1;                                  // [2] per-parity progress
   uint16_t* lcol = reinterpret_cast<uint16_t*>(flag + 2);      // [n_col] (LCOL)
@@ -292,15 +289,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   for (uint32_t v = tid; v <= N; v += kMsThreads) F[v] = 0;
   if (LCOL)
     for (uint32_t t = tid; t < n_col; t += kMsThreads) lcol[t] = (uint16_t)sell_col[t];
-  const uint32_t n_slices = (N + kSliceW - 1) / kSliceW;
-  if (LB) {  // level bitmaps of this batch's rows start empty
-    unsigned long long* lb = LB + (size_t)row0 * lvls * n_slices;
-    for (size_t t = tid; t < (size_t)nb * lvls * n_slices; t += kMsThreads) lb[t] = 0ull;
-  }
   if (tid == 0) {
     *o_cnt = 0;
     flag[0] = flag[1] = 0;
-    lvl_or[0] = lvl_or[1] = 0ull;
   }
   __syncthreads();
   if (tid < nb) {
@@ -312,7 +303,6 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   const uint32_t n_osrc = *o_cnt;
 
   uint64_t vis[OWN], nv[OWN];
-  uint32_t my_ecc = 0;   // thread s < nb: last level source s found a node at
   uint32_t drained = 0;  // bit i: owned node i is drained
   uint32_t sb[OWN], sw[OWN];  // owned slice i: column base, width (wave-uniform)
 #pragma unroll
@@ -344,20 +334,6 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
       uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
       const uint32_t v = tid + i * kMsThreads;
-      if (LB) {
-        // level bitmaps for the next-hop pass: per source of the slice, one
-        // ballot = the slice's 64 nodes found at level L (a 64x64 bit
-        // transpose of the new masks), one 8-byte store
-        if (lane == 0) atomicOr(&lvl_or[L & 1], ((unsigned long long)mhi << 32) | mlo);
-        if (L < lvls) {
-          const uint32_t slice = (tid - lane + i * kMsThreads) / kSliceW;
-          for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
-            const uint32_t src = __ffsll((unsigned long long)m) - 1;
-            const uint64_t bits = __ballot((nv[i] >> src) & 1ull);
-            if (lane == 0) LB[((size_t)(row0 + src) * lvls + L) * n_slices + slice] = bits;
-          }
-        }
-      }
       // Two ways to cover the (source, node) pairs of the slice: one
       // coalesced store per source (row-major; best when a source discovers
       // many nodes of the slice at once -- dense fabrics), or each lane
@@ -437,10 +413,6 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     MS_STAMP();
     __syncthreads();  // every read of F for this level is done
     MS_STAMP();
-    if (LB) {
-      if (tid < nb && ((lvl_or[L & 1] >> tid) & 1ull)) my_ecc = L;
-      if (tid == 0) lvl_or[(L + 1) & 1] = 0ull;  // read at level L - 1, written at L + 1
-    }
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = tid + i * kMsThreads;
@@ -462,7 +434,6 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     if (!flag[L & 1]) break;
   }
   MS_STAMP();
-  if (LB && tid < nb) ecc[row0 + tid] = my_ecc;
   // ---- unreachable (s, v) pairs and row padding ----
   uint64_t miss = 0;
 #pragma unroll
@@ -688,7 +659,7 @@ constexpr int kEcmpUnroll = 4;         // neighbour rows per group (two groups i
 constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
 constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
 constexpr uint32_t kEcmpRunsPerXcd = 64;  // source runs dealt to each XCD
-constexpr uint32_t kEcmpBlocksPerCu = 0;  // r02_v10 A/B: 2-12 all slower  // long-lived next-hop blocks (0 = one per item)
+constexpr uint32_t kEcmpBlocksPerCu = 6;  // long-lived next-hop blocks (0 = one per item)
 
 // Zero-byte flags of x at bit 7 of each byte (exact: no carries cross bytes).
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
@@ -865,111 +836,6 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     }
   }
   }  // pos
-}
-
-// ---------------------------------------------------------------------------
-//  2b. next-hop pass over level bitmaps (unit metrics, shallow graphs)
-// ---------------------------------------------------------------------------
-// With unit metrics the triangle inequality gives d_x(v) >= d_s(v) - 1 for
-// every expanded neighbour x of s, so the ECMP test d_x(v) = d_s(v) - 1 is
-// d_x(v) <= d_s(v) - 1:
-//     x in nh_s(v)  <=>  v in  U_l ( L_s^l  &  C_x^{l-1} ),
-// L_r^l = the nodes row r reaches at level l (msbfs_kernel's level bitmaps),
-// C_x^l = L_x^0 | ... | L_x^l.  A lane owns one u32 word (32 destinations),
-// a wave 2048 destinations; per neighbour the pass costs ecc_s word loads and
-// ~3 bit operations per level -- no byte compares, no bit transposes, the
-// output word comes out in place.  Rows deeper than the kept levels
-// (ecc >= lvls) decide on the exact u32 rows instead.
-constexpr uint32_t kLvChunk = 2048;  // destinations per wave
-constexpr int kLvGroup = 4;          // neighbours whose loads are in flight together
-
-__global__ __launch_bounds__(kEcmpThreads) void ecmp_levels_kernel(
-    const uint32_t* __restrict__ LB, uint32_t lvls, const uint32_t* __restrict__ ecc,
-    const uint32_t* __restrict__ D, uint32_t pitch, uint32_t N,
-    const uint32_t* __restrict__ req_src, const uint32_t* __restrict__ row_of,
-    const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
-    const uint8_t* __restrict__ ovl, const uint64_t* __restrict__ nh_off,
-    uint32_t* __restrict__ nh, uint32_t chunks, const uint32_t* __restrict__ slot_src) {
-  const uint32_t grp = blockIdx.x & 7, pos = blockIdx.x >> 3;
-  const uint32_t i = slot_src[(pos / chunks) * 8 + grp];
-  const uint32_t c = pos % chunks;
-  if (i == kInf) return;
-  const uint32_t s = req_src[i];
-  const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wpm = pitch / 32;  // u32 words per bitmap = per level row
-  const uint32_t w0 = (c * kEcmpWaves + (threadIdx.x >> 6)) * (kLvChunk / 32);
-  if (k == 0 || w0 >= wpm) return;  // whole wave
-  const uint32_t w = w0 + lane;
-  const bool live = w < wpm;
-  const uint32_t srow = row_of[s];
-  const uint32_t es = ecc[srow];
-  uint32_t* out = nh + nh_off[i] + w;
-  auto exact_word = [&](uint32_t rx) {  // d_x(v) + 1 == d_s(v), 32 destinations
-    uint32_t m = 0;
-    const uint4* ds = reinterpret_cast<const uint4*>(D + (size_t)srow * pitch + 32 * w);
-    const uint4* dx = reinterpret_cast<const uint4*>(D + (size_t)rx * pitch + 32 * w);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 a = dx[q], b = ds[q];
-      const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) m |= (uint32_t)(av[e] != kInf && av[e] + 1 == bv[e]) << (4 * q + e);
-    }
-    return m;
-  };
-  if (es >= lvls) {  // the source row itself is deeper than the kept levels
-    for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t x = nb_id[nb0 + j];
-      uint32_t m = 0;
-      if (live) {
-        if (ovl[x]) m = (x / 32 == w && D[(size_t)srow * pitch + x] == 1u) ? 1u << (x & 31) : 0u;
-        else m = exact_word(row_of[x]);
-        out[(size_t)j * wpm] = m;
-      }
-    }
-    return;
-  }
-  const uint32_t* Ls_base = LB + (size_t)srow * lvls * wpm + w;
-  uint32_t Ls[kLbLevels];
-#pragma unroll
-  for (uint32_t l = 0; l < kLbLevels; ++l) Ls[l] = (l <= es && l < lvls && live) ? Ls_base[(size_t)l * wpm] : 0u;
-  for (uint32_t j0 = 0; j0 < k; j0 += kLvGroup) {
-    uint32_t Lx[kLvGroup][kLbLevels];
-    uint32_t ex[kLvGroup], xs[kLvGroup];
-#pragma unroll
-    for (int g = 0; g < kLvGroup; ++g) {  // issue the group's loads
-      const uint32_t j = j0 + g;
-      xs[g] = j < k ? nb_id[nb0 + j] : kInf;
-      const bool dead = xs[g] == kInf || ovl[xs[g]];
-      const uint32_t rx = dead ? 0u : row_of[xs[g]];
-      ex[g] = dead ? kInf : ecc[rx];
-      const uint32_t* Lx_base = LB + (size_t)rx * lvls * wpm + w;
-#pragma unroll
-      for (uint32_t l = 0; l + 1 < kLbLevels; ++l)
-        Lx[g][l] = (!dead && l < es && l <= ex[g] && live) ? Lx_base[(size_t)l * wpm] : 0u;
-    }
-#pragma unroll
-    for (int g = 0; g < kLvGroup; ++g) {
-      const uint32_t j = j0 + g;
-      if (j >= k) break;
-      const uint32_t x = xs[g];
-      uint32_t m = 0;
-      if (ovl[x]) {  // drained neighbour: only x itself, over the direct link
-        m = (live && x / 32 == w && D[(size_t)srow * pitch + x] == 1u) ? 1u << (x & 31) : 0u;
-      } else if (ex[g] >= lvls) {
-        if (live) m = exact_word(row_of[x]);
-      } else {
-        uint32_t cx = 0;
-#pragma unroll
-        for (uint32_t l = 1; l < kLbLevels; ++l) {
-          cx |= Lx[g][l - 1];
-          m |= Ls[l] & cx;
-        }
-      }
-      if (live) out[(size_t)j * wpm] = m;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1477,14 +1343,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
-  // level-bitmap next hops: the per-level-store BFS (not the register-plane
-  // one, whose graphs are deep) on graphs dense enough for the byte-row pass
-  // to have paid (SPF_LEVELS=0/1 overrides, experiments and tests)
-  {
-    const char* e = std::getenv("SPF_LEVELS");
-    p->levels = p->ms && !use_planes(c) && (e ? e[0] == '1' : use_narrow(c, p));
-  }
-  p->narrow = p->ms && !p->levels && use_narrow(c, p);
+  p->narrow = p->ms && use_narrow(c, p);
   {
     // per-source neighbour rows for the next-hop pass (kInf = drained)
     std::vector<uint32_t> nb_row, nb_row_off(n_src), nb_drained(n_src, 0);
@@ -1538,11 +1397,6 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors end here
   }
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
-  if (p->levels) {
-    const size_t n_slices = (N + kSliceW - 1) / kSliceW;
-    HIP_TRY(c, p->d_LB.alloc(p->closure.size() * kLbLevels * n_slices));
-    HIP_TRY(c, p->d_ecc.alloc(p->closure.size()));
-  }
   if (p->narrow) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
     HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
     HIP_TRY(c, hipMemsetAsync(p->d_Dn.p + p->closure.size() * c->npitch, 0xFF, c->npitch, c->stream));
@@ -1588,7 +1442,7 @@ uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->clos
 spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
   *bfs = p->exact ? 3u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
-  *narrow = p->levels ? 2u : p->narrow ? 1u : 0u;
+  *narrow = p->narrow ? 1u : 0u;
   return SPF_OK;
 }
 
@@ -1624,21 +1478,13 @@ spf_status spf_plan_traffic(const spf_plan* p, uint64_t* bfs_bytes, uint64_t* ec
     const uint64_t n_slices = c->sell_ptr.size() - 1;
     const uint64_t csr = planes ? 8ull * c->sell4_ptr.back() + 4ull * (n_slices + 1)
                                 : 4ull * c->sell_ptr.back() + 4ull * (n_slices + 1);
-    const uint64_t lb = p->levels ? rows * kLbLevels * ((N + kSliceW - 1) / kSliceW) * 8ull : 0ull;
-    bfs = groups * (csr + N) + rows * c->pitch * 4ull + (p->narrow ? rows * c->npitch : 0ull) + lb;
+    bfs = groups * (csr + N) + rows * c->pitch * 4ull + (p->narrow ? rows * c->npitch : 0ull);
   } else {
     bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch);
   }
-  uint64_t row_bytes_total = rows * (p->narrow ? c->npitch : 4ull * c->pitch);
-  if (p->levels) {  // the level bitmaps each row's search reached, read once
-    std::vector<uint32_t> ecc(rows);
-    HIP_TRY(p->ctx, hipMemcpy(ecc.data(), p->d_ecc.p, 4ull * rows, hipMemcpyDeviceToHost));
-    row_bytes_total = 0;
-    for (uint32_t e : ecc)
-      row_bytes_total += (e < kLbLevels ? e + 1ull : 4ull * 32) * (c->pitch / 8);  // deep: u32 row
-  }
+  const uint64_t row_bytes = p->narrow ? c->npitch : 4ull * c->pitch;
   *bfs_bytes = bfs;
-  *ecmp_bytes = p->nh_total ? row_bytes_total + 4ull * p->nh_total : 0ull;
+  *ecmp_bytes = p->nh_total ? rows * row_bytes + 4ull * p->nh_total : 0ull;
   return SPF_OK;
 }
 
@@ -1690,11 +1536,11 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 
 namespace {
 
-size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 16ull + 4ull * (kMsBatch + 3); }
+size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 3); }
 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
-                  unsigned long long* LB, uint32_t* ecc, hipStream_t s) {
+                  hipStream_t s) {
   const uint32_t n_col = c->sell_ptr.back();
   const size_t lds = msbfs_lds_bytes(c->N), lds_col = lds + 2ull * n_col;
   const bool lcol = lds_col <= kMaxLds;
@@ -1706,13 +1552,11 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
   if (lcol)
     hipLaunchKernelGGL((msbfs_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds_col, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
-                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, LB, ecc, kLbLevels,
-                       c->d_stamps.p);
+                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
   else
     hipLaunchKernelGGL((msbfs_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
-                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, LB, ecc, kLbLevels,
-                       c->d_stamps.p);
+                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
 }
 
 size_t planes_lds_bytes(uint32_t own) { return 8ull * own * kMsThreads + 4ull * (kPlBatch + 4); }
@@ -1747,7 +1591,7 @@ bool use_planes(const spf_ctx* c) {
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
-                        uint8_t* Dn, unsigned long long* LB, uint32_t* ecc, hipStream_t s) {
+                        uint8_t* Dn, hipStream_t s) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
     HIP_TRY(c, c->d_stamps.alloc(64 * 16));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
@@ -1762,13 +1606,13 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
     HIP_TRY(c, hipGetLastError());
     return SPF_OK;
   }
-  if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, LB, ecc, s);
-  else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, LB, ecc, s);
-  else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, LB, ecc, s);
-  else if (own <= 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, LB, ecc, s);
-  else if (own <= 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, LB, ecc, s);
-  else if (own <= 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, LB, ecc, s);
-  else msbfs_launch<16>(c, rows_src, rows, D, Dn, LB, ecc, s);
+  if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, s);
+  else if (own <= 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, s);
+  else msbfs_launch<16>(c, rows_src, rows, D, Dn, s);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -1788,19 +1632,6 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
                      c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead, hop ? 1u : 0u,
                      p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p, n_pos);
-  HIP_TRY(c, hipGetLastError());
-  return SPF_OK;
-}
-
-spf_status launch_ecmp_levels(spf_ctx* c, spf_plan* p, const uint32_t* D, uint32_t* d_nh,
-                              hipStream_t s) {
-  const uint32_t per_block = kLvChunk * kEcmpWaves;
-  const uint32_t chunks = (c->pitch + per_block - 1) / per_block;
-  const uint32_t nb = chunks * (uint32_t)p->slots;
-  hipLaunchKernelGGL(ecmp_levels_kernel, dim3(nb), dim3(kEcmpThreads), 0, s,
-                     reinterpret_cast<const uint32_t*>(p->d_LB.p), kLbLevels, p->d_ecc.p, D,
-                     c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
-                     c->d_ovl.p, p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -1892,15 +1723,12 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     ++p->timing_n;
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
-  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
-                                       p->levels ? p->d_LB.p : nullptr,
-                                       p->levels ? p->d_ecc.p : nullptr, s)
+  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr, s)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   if (p->nh_total) {
-    st = p->levels ? launch_ecmp_levels(c, p, D, d_nh, s)
-       : p->narrow ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
+    st = p->narrow ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
                : launch_ecmp<false>(c, p, nullptr, D, hop, d_nh, s);
     if (st != SPF_OK) return st;
   }

@@ -91,16 +91,7 @@ class SpfPlan(NativeHandle):
         next execute (spf_plan_kernels)."""
         bfs, narrow = C.c_uint32(), C.c_uint32()
         self._eng._err(N.lib.spf_plan_kernels(self._h, C.byref(bfs), C.byref(narrow)))
-        return self.BFS_KERNELS[bfs.value], narrow.value == 1
-
-    def ecmp_kernel(self) -> str:
-        """Name of the next-hop kernel the next execute runs ("" for the exact
-        kernel, which derives next hops inline)."""
-        bfs, narrow = C.c_uint32(), C.c_uint32()
-        self._eng._err(N.lib.spf_plan_kernels(self._h, C.byref(bfs), C.byref(narrow)))
-        if bfs.value == 3:
-            return ""
-        return "ecmp_levels_kernel" if narrow.value == 2 else "ecmp_kernel"
+        return self.BFS_KERNELS[bfs.value], bool(narrow.value)
 
     def traffic(self) -> Tuple[int, int]:
         """Compulsory HBM bytes of (distance kernel, next-hop kernel) per

@@ -133,7 +133,6 @@ def test_next_hop_pass_both_row_widths(name, make, narrow, monkeypatch):
     """The BFS plans' next-hop pass on u8 narrow rows and on the exact u32 rows
     (the plan picks one by average degree; SPF_NARROW forces it)."""
     monkeypatch.setenv("SPF_NARROW", narrow)
-    monkeypatch.setenv("SPF_LEVELS", "0")
     names, eng, orc = load(make())
     compare(names, eng, orc, list(range(len(names))), hop=True)
 
@@ -142,7 +141,6 @@ def test_saturated_narrow_rows_fall_back_to_exact(monkeypatch):
     """Hop distances >= 254 saturate the u8 copy: those waves decide on the
     u32 rows.  A 700-node ring has distances up to 350."""
     monkeypatch.setenv("SPF_NARROW", "1")
-    monkeypatch.setenv("SPF_LEVELS", "0")
     topo = T.wan(700, 0, seed=1)  # ring only
     names, eng, orc = load(topo)
     rng = np.random.default_rng(5)
@@ -164,29 +162,6 @@ def test_bfs_variants_exact(name, make, variant, monkeypatch):
     widths; SPF_MSBFS / SPF_NARROW force the choice the plan makes by degree."""
     monkeypatch.setenv("SPF_MSBFS", variant)
     names, eng, orc = load(make())
-    for narrow, levels in (("0", "0"), ("1", "0"), ("0", "1")):
+    for narrow in ("0", "1"):
         monkeypatch.setenv("SPF_NARROW", narrow)
-        monkeypatch.setenv("SPF_LEVELS", levels)
         compare(names, eng, orc, list(range(len(names))), hop=True)
-
-
-@pytest.mark.parametrize("name,make", [
-    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
-    ("fabric_drained", lambda: T.random_graph(300, 2000, 9, max_metric=1, overload_frac=0.1,
-                                              link_overload_frac=0.05)),
-    ("ring1200", lambda: T.wan(1200, 0, seed=1)),  # every row deeper than the kept levels
-    ("wan_mixed", lambda: T.wan(400, 300, seed=2, max_metric=1)),  # some rows deep, some not
-], ids=["fabric", "drained", "deep", "mixed"])
-def test_level_bitmap_next_hops_exact(name, make, monkeypatch):
-    """msbfs_kernel's level bitmaps + ecmp_levels_kernel (forced with
-    SPF_LEVELS=1): shallow rows through the bitmaps, rows deeper than the kept
-    levels through the exact u32 fallback, drained neighbours, both metrics."""
-    monkeypatch.setenv("SPF_MSBFS", "masks")
-    monkeypatch.setenv("SPF_LEVELS", "1")
-    names, eng, orc = load(make())
-    p = eng.plan([0])
-    assert p.ecmp_kernel() == "ecmp_levels_kernel"
-    srcs = list(range(len(names)))
-    compare(names, eng, orc, srcs, hop=True)
-    if name != "ring1200":
-        compare(names, eng, orc, srcs)
