@@ -659,7 +659,6 @@ constexpr int kEcmpUnroll = 4;         // neighbour rows per group (two groups i
 constexpr uint32_t kEcmpChunk = 1024;  // destinations per wave
 constexpr uint32_t kEcmpWaves = kEcmpThreads / 64;
 constexpr uint32_t kEcmpRunsPerXcd = 64;  // source runs dealt to each XCD
-constexpr uint32_t kEcmpBlocksPerCu = 6;  // long-lived next-hop blocks (0 = one per item)
 
 // Zero-byte flags of x at bit 7 of each byte (exact: no carries cross bytes).
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
@@ -699,26 +698,22 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     const uint32_t* __restrict__ nb_row, const uint32_t* __restrict__ nb_row_off,
     const uint32_t* __restrict__ nb_drained, uint32_t dead, uint32_t hop,
     const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh, uint32_t chunks,
-    const uint32_t* __restrict__ slot_src, uint32_t n_pos) {
+    const uint32_t* __restrict__ slot_src) {
   // Block b runs on XCD b % 8.  slot_src (spf_plan_create) lists each XCD's
   // sources: runs of consecutive request sources (the racks of one pod, the
   // spines of one plane -- the same neighbour rows, shared in that XCD's L2)
-  // dealt to the XCDs by work; a source's chunks are consecutive positions.
-  // Waves are long-lived: a block walks positions pos, pos + gridDim/8, ...
-  // of its XCD's list (one (source, chunk) item per pass).  Launching a
-  // block per item made the waves so short (~2.4 us) that the wave launch
-  // rate, not the memory system, set the resident wave count (PMC: ~1.2
-  // waves per SIMD on average, profiles/r02_v9).
-  const uint32_t grp = blockIdx.x & 7;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t pos = blockIdx.x >> 3; pos < n_pos; pos += gridDim.x >> 3) {
+  // dealt to the XCDs by work; a source's chunks are consecutive blocks.
+  // (Long-lived blocks walking the list were slower at every size tried,
+  // profiles/r02_v10_ab_ecmp_blocks.txt.)
+  const uint32_t grp = blockIdx.x & 7, pos = blockIdx.x >> 3;
   const uint32_t i = slot_src[(pos / chunks) * 8 + grp];
   const uint32_t c = pos % chunks;
-  if (i == kInf) continue;
+  if (i == kInf) return;
   const uint32_t s = req_src[i];
   const uint32_t nb0 = nb_ptr[s], k = nb_ptr[s + 1] - nb0;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t cbase = (c * kEcmpWaves + (threadIdx.x >> 6)) * kEcmpChunk;
-  if (k == 0 || cbase >= N) continue;  // whole wave: no barriers below
+  if (k == 0 || cbase >= N) return;  // whole wave: no barriers below
   const uint32_t srow = row_of[s];
   const uint32_t wpm = pitch / 32;  // u32 words per bitmap
   const uint32_t* offs = nb_row + nb_row_off[i];
@@ -835,7 +830,6 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
         out_w[(size_t)j * wpm + lane] = 1u << (x & 31);
     }
   }
-  }  // pos
 }
 
 // ---------------------------------------------------------------------------
@@ -1622,16 +1616,11 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
                        uint32_t* d_nh, hipStream_t s) {
   const uint32_t per_block = kEcmpChunk * kEcmpWaves;
   const uint32_t chunks = (c->N + per_block - 1) / per_block;
-  const uint32_t n_pos = chunks * (uint32_t)(p->slots / 8);  // positions per XCD list
-  // long-lived blocks: kEcmpBlocksPerCu per CU, dealt over the 8 XCDs
-  static const uint32_t per_cu = std::getenv("SPF_ECMP_BPC") ? (uint32_t)atoi(std::getenv("SPF_ECMP_BPC"))
-                                                             : kEcmpBlocksPerCu;
-  const uint32_t nb = per_cu == 0 ? n_pos * 8
-                                  : std::min<uint32_t>(n_pos, std::max<uint32_t>(1, per_cu * c->n_cu / 8)) * 8;
+  const uint32_t nb = chunks * (uint32_t)p->slots;
   hipLaunchKernelGGL((ecmp_kernel<NARROW>), dim3(nb), dim3(kEcmpThreads), 0, s, Dn, c->npitch, D,
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
                      c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead, hop ? 1u : 0u,
-                     p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p, n_pos);
+                     p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
