@@ -63,7 +63,6 @@ using namespace spfi;
 
 namespace {
 
-constexpr int kSsspThreads = 256;
 constexpr int kEcmpThreads = 256;
 constexpr uint32_t kBigDeg = 24;  // > kBigDeg: expanded by a whole wave
 constexpr size_t kMaxLds = 160 * 1024;
@@ -96,8 +95,12 @@ enum { C_QLEN = 0, C_NBIG = 1, C_NWORDS = 4 };
 // ---------------------------------------------------------------------------
 //  1. single-source shortest paths, one workgroup per source row
 // ---------------------------------------------------------------------------
-template <typename QT, bool UNIT>
-__global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
+//   THREADS: a workgroup's distance row sits in LDS, so a large graph fits
+//   only one or two workgroups per CU; those then get 1024 threads, so the
+//   CU still holds 32 waves of relaxations in flight (PMC r02_v9, fabric_rtt
+//   with 256 threads: 75 % of wave cycles waiting, ~8 waves per CU).
+template <typename QT, bool UNIT, int THREADS>
+__global__ __launch_bounds__(THREADS) void sssp_kernel(
     const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
     const uint32_t* __restrict__ wt, const uint8_t* __restrict__ ovl,
     const uint32_t* __restrict__ link, const uint32_t* __restrict__ ign,
@@ -113,12 +116,12 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t wave = tid >> 6;
-  constexpr uint32_t kWaves = kSsspThreads / 64;
+  constexpr uint32_t kWaves = THREADS / 64;
   const uint32_t row = blockIdx.x;
   const uint32_t src = rows_src[row];
 
-  for (uint32_t v = tid; v < pitch; v += kSsspThreads) dist[v] = kInf;
-  for (uint32_t i = tid; i < bm_words; i += kSsspThreads) bm[i] = 0;
+  for (uint32_t v = tid; v < pitch; v += THREADS) dist[v] = kInf;
+  for (uint32_t i = tid; i < bm_words; i += THREADS) bm[i] = 0;
   if (tid == 0) {
     ctl[C_QLEN] = 0;
     ctl[C_NBIG] = 0;
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
   uint32_t qlen = 1;
   while (qlen != 0) {
     // ---- expand: small-degree nodes one per thread, big ones per wave ----
-    for (uint32_t i = tid; i < qlen; i += kSsspThreads) {
+    for (uint32_t i = tid; i < qlen; i += THREADS) {
       const uint32_t u = q[i];
       if (ovl[u] && u != src) continue;  // drained node: recorded, not expanded
       const uint32_t b = row_ptr[u], e = row_ptr[u + 1];
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
     if (tid == 0) ctl[C_NBIG] = 0;  // every thread has read nbig by now
 
     // ---- compact the next-frontier bitmap into q (wave ballot/scan) ----
-    for (uint32_t base = 0; base < bm_words; base += kSsspThreads) {
+    for (uint32_t base = 0; base < bm_words; base += THREADS) {
       const uint32_t i = base + tid;
       uint32_t word = 0;
       if (i < bm_words) {
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(kSsspThreads) void sssp_kernel(
   // ---- write the distance row (16-byte stores) ----
   uint4* out = reinterpret_cast<uint4*>(D + (size_t)row * pitch);
   const uint4* in = reinterpret_cast<const uint4*>(dist);
-  for (uint32_t i = tid; i < pitch / 4; i += kSsspThreads) out[i] = in[i];
+  for (uint32_t i = tid; i < pitch / 4; i += THREADS) out[i] = in[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1509,18 +1512,29 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
   const bool q16 = N <= 65535;
   const size_t lds = sssp_lds_bytes(N, pitch, c->big_nodes, q16);
   const bool unit = hop || c->max_metric == 1;
-  const dim3 g(rows), b(kSsspThreads);
-#define SSSP_LAUNCH(QT, U)                                                                \
-  hipLaunchKernelGGL((sssp_kernel<QT, U>), g, b, lds, s, c->d_row_ptr.p, c->d_col.p,       \
-                     wt, ovl, c->d_link.p, ign, rows_src, N, pitch, bm_words,             \
+  // threads per workgroup from how many workgroups the LDS row lets a CU hold
+  // (SPF_SSSP_THREADS overrides, experiments)
+  uint32_t threads = lds > kMaxLds / 3 ? 1024u : lds > kMaxLds / 6 ? 512u : 256u;
+  if (const char* e = std::getenv("SPF_SSSP_THREADS")) threads = (uint32_t)atoi(e);
+  const dim3 g(rows);
+#define SSSP_LAUNCH(QT, U, TH)                                                            \
+  hipLaunchKernelGGL((sssp_kernel<QT, U, TH>), g, dim3(TH), lds, s, c->d_row_ptr.p,       \
+                     c->d_col.p, wt, ovl, c->d_link.p, ign, rows_src, N, pitch, bm_words,  \
                      c->big_nodes, D)
+#define SSSP_TH(QT, U)                                  \
+  do {                                                  \
+    if (threads >= 1024) SSSP_LAUNCH(QT, U, 1024);      \
+    else if (threads >= 512) SSSP_LAUNCH(QT, U, 512);   \
+    else SSSP_LAUNCH(QT, U, 256);                       \
+  } while (0)
   if (q16) {
-    if (unit) SSSP_LAUNCH(uint16_t, true);
-    else SSSP_LAUNCH(uint16_t, false);
+    if (unit) SSSP_TH(uint16_t, true);
+    else SSSP_TH(uint16_t, false);
   } else {
-    if (unit) SSSP_LAUNCH(uint32_t, true);
-    else SSSP_LAUNCH(uint32_t, false);
+    if (unit) SSSP_TH(uint32_t, true);
+    else SSSP_TH(uint32_t, false);
   }
+#undef SSSP_TH
 #undef SSSP_LAUNCH
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
@@ -1632,14 +1646,16 @@ namespace spfi {
 spf_status set_lds_limits(spf_ctx* c) {
   static bool done = false;
   if (done) return SPF_OK;
-  const void* fns[] = {(const void*)sssp_kernel<uint16_t, true>, (const void*)sssp_kernel<uint16_t, false>,
-                       (const void*)sssp_kernel<uint32_t, true>, (const void*)sssp_kernel<uint32_t, false>,
+#define SSK(QT, U) (const void*)sssp_kernel<QT, U, 256>, (const void*)sssp_kernel<QT, U, 512>, \
+                   (const void*)sssp_kernel<QT, U, 1024>
+  const void* fns[] = {SSK(uint16_t, true), SSK(uint16_t, false), SSK(uint32_t, true), SSK(uint32_t, false),
 #define MSB(o) (const void*)msbfs_kernel<o, false>, (const void*)msbfs_kernel<o, true>
                        MSB(1), MSB(2), MSB(4), MSB(8), MSB(10), MSB(12), MSB(16),
 #define PLB(o) (const void*)msbfs_planes_kernel<o, false>, (const void*)msbfs_planes_kernel<o, true>
                        PLB(1), PLB(2), PLB(4), PLB(8), PLB(10)};
 #undef PLB
 #undef MSB
+#undef SSK
   for (const void* f : fns)
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
   done = true;
