@@ -489,9 +489,79 @@ class WhatIfAllLinks:
                           "this graph)"}
 
 
+class FacadeLfa:
+    """CS-1 latency through the LinkState facade (the C-ABI drop-in): after an
+    adjacency-database publication that drains (or undrains) one rack switch
+    -- BM_DecisionFabric's per-iteration perturbation,
+    RoutingBenchmarkUtils.cpp:406-447 -- the SPFs a route build with LFA
+    needs: getSpfResult(me) and getSpfResult(n) for every neighbour n
+    (Decision.cpp:1107-1196), each a full SpfResult (metrics, next hops,
+    pathLinks) in host memory.  A step = one publication + those 1 + deg(me)
+    results; value = steps per second, ms_per_step = the latency."""
+
+    scaling = "replicas"
+    unit = "lfa_spf_sets/s"
+    kernels = ("facade",)
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        from openr_amd import topology as T
+        from openr_amd.link_state import LinkState
+        from openr_amd.wire import unpack
+
+        self.topo = T.fabric(10000, full=True)
+        self.desc = ("fabric_full numOfSws=10000; me = rack switch 3-0-0; per step one publication "
+                     "toggling rack switch 3-1-0's overload bit, then getSpfResult(me) + "
+                     "getSpfResult(neighbour) for each of me's neighbours (LFA)")
+        self.ls = LinkState(device=dev.index)
+        self.ls.updateAdjacencyDatabases(self.topo.lsdb)
+        self.me = "3-0-0"
+        self.nbrs = sorted({l.getOtherNodeName(self.me) for l in self.ls.linksFromNode(self.me)})
+        names = self.ls.flatten()[0]
+        self.n, self.e = len(names), len(self.ls.flatten()[2])
+        dbs = {d.thisNodeName: d for d in unpack(self.topo.lsdb)}
+        self.victim = dbs["3-1-0"]
+        self.units = 1
+        self.world = world
+        self.i = 0
+        self.kernel_bytes = {"facade": 1}
+        self.survey_bytes = 0
+        self.parallelism = "one LinkState per process (replicas)"
+        self.lat = []
+
+    def step(self) -> None:
+        t0 = time.perf_counter()
+        self.victim.isOverloaded = not self.victim.isOverloaded
+        self.ls.updateAdjacencyDatabase(self.victim)
+        for node in [self.me] + self.nbrs:
+            r = self.ls.getSpfResult(node)
+            assert r
+        self.lat.append(time.perf_counter() - t0)
+
+    def enable_timing(self, k: int) -> None:
+        self.lat = []
+
+    def kernel_ms(self):
+        return {"facade": 1e3 * float(np.mean(self.lat)) if self.lat else 0.0}
+
+    def edges_per_unit(self) -> int:
+        return self.e * (1 + len(self.nbrs))
+
+    def cpu_baseline(self, budget_s: float):
+        orc = oracle()()
+        orc.update_packed(self.topo.lsdb)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            orc.time_sources([self.me] + self.nbrs)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "lfa_spf_sets/s", "cores": 1, "kind": "port",
+                "sample": f"{done} x (runSpf(me) + runSpf(each of {len(self.nbrs)} neighbours)) "
+                          f"({dt:.1f} s on 1 core of {cpu_model()}; oracle/spf_oracle.cpp)"}
+
+
 WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
              "fabric_rtt": AllSources,
-             "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks}
+             "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks, "fabric_lfa": FacadeLfa}
 
 
 def _dump_maps_at_exit(path: str) -> None:
@@ -593,6 +663,8 @@ def main() -> None:
         "metric": METRIC if isinstance(wl, AllSources) else (
             "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN"
             if isinstance(wl, Ksp2AllPairs) else
+            "LinkState facade: publication + getSpfResult(me and every LFA neighbour) per sec"
+            if isinstance(wl, FacadeLfa) else
             "what-if single-link-failure SPF reruns/sec, 1M-link scale-free graph"),
         "value": value,
         "unit": wl.unit,
