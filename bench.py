@@ -529,12 +529,14 @@ class FacadeLfa:
         self.lat = []
 
     def step(self) -> None:
+        # the C-ABI the C++ binding calls: the results are
+        # the LinkState's memo arrays (ls_spf_view); no Python objects built
         t0 = time.perf_counter()
         self.victim.isOverloaded = not self.victim.isOverloaded
         self.ls.updateAdjacencyDatabase(self.victim)
         for node in [self.me] + self.nbrs:
-            r = self.ls.getSpfResult(node)
-            assert r
+            v = self.ls._spf_view(node)
+            assert v.n > 0
         self.lat.append(time.perf_counter() - t0)
 
     def enable_timing(self, k: int) -> None:

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
+from collections.abc import Mapping
 from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple, Union
 
 from . import _native as N
@@ -152,6 +153,58 @@ Path = List[Link]
 def _change(c: N.LsChange) -> LinkStateChange:
     return LinkStateChange(bool(c.topology_changed), bool(c.link_attributes_changed),
                            bool(c.node_label_changed))
+
+
+class _LazySpfResult(Mapping):
+    """SpfResult (unordered_map<string, NodeSpfResult>) backed by numpy
+    copies of the C-ABI view; a NodeSpfResult is built when first read."""
+
+    def __init__(self, ls: "LinkState", v: "N.LsSpfView") -> None:
+        import numpy as np
+
+        def arr(ptr, n, dt):
+            return np.ctypeslib.as_array(ptr, (n,)).astype(dt) if n else np.zeros(0, dt)
+
+        n = int(v.n)
+        self._ls = ls
+        self._node = arr(v.node, n, np.uint32)
+        self._metric = arr(v.metric, n, np.uint64)
+        self._nh_ptr = arr(v.nh_ptr, n + 1, np.uint32)
+        self._nh_node = arr(v.nh_node, int(self._nh_ptr[-1]) if n else 0, np.uint32)
+        self._pl_ptr = arr(v.pl_ptr, n + 1, np.uint32)
+        m = int(self._pl_ptr[-1]) if n else 0
+        self._pl_link = arr(v.pl_link, m, np.uint32)
+        self._pl_prev = arr(v.pl_prev, m, np.uint32)
+        self._index: Optional[Dict[str, int]] = None
+        self._made: Dict[str, NodeSpfResult] = {}
+
+    def _idx(self) -> Dict[str, int]:
+        if self._index is None:
+            name = self._ls._name
+            self._index = {name(int(x)): i for i, x in enumerate(self._node)}
+        return self._index
+
+    def __getitem__(self, key: str) -> NodeSpfResult:
+        r = self._made.get(key)
+        if r is None:
+            i = self._idx()[key]
+            ls = self._ls
+            a, b = int(self._nh_ptr[i]), int(self._nh_ptr[i + 1])
+            nh = {ls._name(int(x)) for x in self._nh_node[a:b]}
+            a, b = int(self._pl_ptr[i]), int(self._pl_ptr[i + 1])
+            pl = [PathLink(ls._link(int(l)), ls._name(int(p)))
+                  for l, p in zip(self._pl_link[a:b], self._pl_prev[a:b])]
+            r = self._made[key] = NodeSpfResult(int(self._metric[i]), nh, pl)
+        return r
+
+    def __iter__(self):
+        return iter(self._idx())
+
+    def __len__(self) -> int:
+        return len(self._node)
+
+    def __contains__(self, key: object) -> bool:
+        return key in self._idx()
 
 
 class LinkState(N.NativeHandle):
@@ -309,21 +362,25 @@ class LinkState(N.NativeHandle):
 
     # -- shortest paths ----------------------------------------------------------
     def getSpfResult(self, nodeName: str, useLinkMetric: bool = True) -> SpfResult:
+        """``getSpfResult`` (LinkState.cpp:793-803): a read-only mapping node
+        name -> NodeSpfResult over the C-ABI's result arrays (copied once);
+        entries are materialised on access."""
         key = (nodeName, bool(useLinkMetric))
         hit = self._spf_cache.get(key)
         if hit is not None:
             return hit
+        v = self._spf_view(nodeName, useLinkMetric)
+        res = _LazySpfResult(self, v)
+        self._spf_cache[key] = res
+        return res
+
+    def _spf_view(self, nodeName: str, useLinkMetric: bool = True) -> "N.LsSpfView":
+        """The raw C-ABI result (ls_get_spf_result): arrays owned by the
+        LinkState's memo, valid until the next topology change."""
         v = N.LsSpfView()
         self._err(N.lib.ls_get_spf_result(self._h, nodeName.encode(), int(bool(useLinkMetric)),
                                           C.byref(v)))
-        res: SpfResult = {}
-        for i in range(v.n):
-            nh = {self._name(v.nh_node[j]) for j in range(v.nh_ptr[i], v.nh_ptr[i + 1])}
-            pl = [PathLink(self._link(v.pl_link[j]), self._name(v.pl_prev[j]))
-                  for j in range(v.pl_ptr[i], v.pl_ptr[i + 1])]
-            res[self._name(v.node[i])] = NodeSpfResult(int(v.metric[i]), nh, pl)
-        self._spf_cache[key] = res
-        return res
+        return v
 
     def getKthPaths(self, src: str, dest: str, k: int) -> List[Path]:
         key = (src, dest, int(k))
