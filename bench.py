@@ -197,11 +197,12 @@ class AllSources:
         n, e = self.n, self.e
         self.survey_bytes = int(len(srcs) * (4 * (n + 1) + 8 * e + n + 4 * n)
                                 + len(srcs) * int(np.sum((k[srcs] + 7) // 8)))
-        bfs, narrow = self.plan.kernels()
-        self.kernels = (bfs, "ecmp_kernel")
-        self.narrow = narrow
-        tb, te = self.plan.traffic()
-        self.kernel_bytes = {bfs: tb, "ecmp_kernel": te}
+        # the execute's timed phases: distance kernel, row slicing (sliced
+        # next-hop plans), next-hop kernel
+        self.phases = self.plan.phase_kernels()
+        self.kernels = tuple(k for k in self.phases if k)
+        self.narrow = self.plan.row_mode()
+        self._phase_bytes()
         self.parallelism = (
             f"sources in contiguous id blocks over {world} rank(s) (one LSDB), plan closure "
             f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source dist rows + "
@@ -232,9 +233,14 @@ class AllSources:
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
 
+    def _phase_bytes(self) -> None:
+        tb = self.plan.traffic_phases()  # sliced plans: planes of the last execute
+        self.kernel_bytes = {k: b for k, b in zip(self.phases, tb) if k}
+
     def kernel_ms(self):
-        a, b, cnt = self.plan.timing()
-        return {self.kernels[0]: a / max(cnt, 1), "ecmp_kernel": b / max(cnt, 1)}
+        ms, cnt = self.plan.timing_phases()
+        self._phase_bytes()
+        return {k: t / max(cnt, 1) for k, t in zip(self.phases, ms) if k}
 
     def edges_per_unit(self) -> int:
         return self.e
@@ -709,6 +715,8 @@ def main() -> None:
     }
     if getattr(wl, "gather", False):
         out["config"]["gather_bytes_per_step"] = wl.gather_bytes
+    if isinstance(wl, AllSources):
+        out["config"]["next_hop_rows"] = wl.narrow  # u32 | u8 | sliced (bit planes)
     if isinstance(wl, WhatIfAllLinks):
         out["config"]["hot_failures_per_rank"] = wl.n_hot
         out["config"]["workgroup_team_failures_per_rank"] = wl.n_big

@@ -32,7 +32,8 @@
  *     step for step, one wavefront per source, heap pop order (metric, id)
  *     reproduced -- the next-hop sets under zero-cost plateaus depend on it.
  *   - Row pitch: dist and next-hop rows are stored with pitch
- *     spf_row_pitch() = n_nodes rounded up to a multiple of 64.
+ *     spf_row_pitch() = n_nodes rounded up to a multiple of 1024 (every
+ *     next-hop bitmap then starts on a 128-byte line).
  *
  * Errors: every call returns spf_status; spf_last_error() describes the last
  * failure.  No exceptions cross the ABI.  All calls on one context must come
@@ -142,7 +143,10 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
 /* Which kernels the next execute runs (diagnostics, benchmarks):
  * *bfs = 0 sssp_kernel (weighted, per source), 1 msbfs_kernel (64 sources per
  * sweep, per-level stores), 2 msbfs_planes_kernel (32 sources, register bit
- * planes, rows written once); *narrow = 1 when the next-hop pass reads u8 rows.
+ * planes, rows written once), 3 exact_spf_kernel; *narrow = 0 when the
+ * next-hop pass (ecmp_kernel) reads the u32 rows, 1 when it reads u8 rows,
+ * 2 when slice_rows_kernel turns the u8 rows into bit planes and
+ * ecmp_sliced_kernel matches those.
  * No reference counterpart (engine introspection). */
 spf_status spf_plan_kernels(const spf_plan* plan, uint32_t* bfs, uint32_t* narrow);
 /* Bytes the distance kernel and the next-hop kernel of one execute must move
@@ -151,6 +155,10 @@ spf_status spf_plan_kernels(const spf_plan* plan, uint32_t* bfs, uint32_t* narro
  * once, every compared distance row read once).  Denominator-free roofline
  * input for benchmarks; no reference counterpart. */
 spf_status spf_plan_traffic(const spf_plan* plan, uint64_t* bfs_bytes, uint64_t* ecmp_bytes);
+/* The same per phase: bytes[0] distance kernel, bytes[1] row slicing (0
+ * unless *narrow == 2), bytes[2] next-hop kernel.  For sliced plans the
+ * plane count comes from the last execute's deepest level (a 4-byte read). */
+spf_status spf_plan_traffic_phases(const spf_plan* plan, uint64_t* bytes);
 
 /* Execute on device buffers: d_dist = [n_src][pitch] u32, d_nh = nh words.
  * Enqueued on `stream` (a hipStream_t, NULL = the context's stream); no host
@@ -170,6 +178,9 @@ spf_status spf_plan_execute_host(spf_plan* plan, uint32_t* dist, uint32_t* nh);
  * (then resets the count). */
 spf_status spf_plan_enable_timing(spf_plan* plan, uint32_t max_executes);
 spf_status spf_plan_timing(spf_plan* plan, double* sssp_ms, double* ecmp_ms, uint32_t* n);
+/* The same per phase: ms[0] distance kernel, ms[1] row slicing, ms[2]
+ * next-hop kernel (spf_plan_timing's ecmp_ms = ms[1] + ms[2]). */
+spf_status spf_plan_timing_phases(spf_plan* plan, double* ms, uint32_t* n);
 
 /* Convenience: plan + execute + copy back to host buffers.
  * dist_out = [n_src][n_nodes] (dense, no pitch); nh_out sized by

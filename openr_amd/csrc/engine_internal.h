@@ -99,10 +99,14 @@ struct spf_plan {
   bool direct = false;  // closure == srcs: D is the caller's dist buffer
   bool ms = false;      // unit metrics: multi-source BFS
   bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
+  bool sliced = false;  // ... and the next-hop pass on its bit-sliced form
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
   spfi::DevBuf<uint8_t> d_Dn;
+  spfi::DevBuf<uint32_t> d_S, d_maxd;  // sliced rows (+ dead row); deepest BFS level + 8 counters
+  spfi::DevBuf<uint32_t> d_units, d_unit_off;  // sliced pass: uint4 work units per XCD
+  uint32_t max_xcd_units = 0;
   spfi::DevBuf<uint64_t> d_nh_off;
   spfi::DevBuf<uint32_t> d_nb_row, d_nb_row_off, d_nb_drained;  // next-hop pass inputs
   uint32_t dead = 0;  // nb_row value of a drained neighbour
@@ -111,8 +115,9 @@ struct spf_plan {
   size_t slots = 0;
   size_t lds_bytes = 0;
   bool q16 = true;
-  // optional per-kernel timing: 3 events per execute (before SSSP, between,
-  // after ECMP), ring of `timing_cap` executes
+  // optional per-kernel timing: 4 events per execute (before the distance
+  // kernel, after it, after the row slicing, after ECMP), ring of
+  // `timing_cap` executes
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
   ~spf_plan() {

@@ -38,6 +38,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "engine_internal.h"
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
     uint32_t n_col, const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
     uint32_t n_rows, uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch,
-    uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
+    uint32_t* __restrict__ D, uint8_t* __restrict__ Dn, uint32_t* __restrict__ maxd,
     unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* F = reinterpret_cast<uint64_t*>(smem);             // [N + 1]
@@ -323,6 +324,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   }
 
   MS_STAMP();
+  uint32_t last = 0;  // deepest level of the batch
   for (uint32_t L = 0;; ++L) {
     // ---- record level L: D[s][v] = L for every new (s, v) ----
     // per owned slice, only the sources with a new node in it (wave OR);
@@ -434,8 +436,13 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     if (any) flag[L & 1] = 1;
     if (tid == 0) flag[(L + 1) & 1] = 0;
     __syncthreads();
-    if (!flag[L & 1]) break;
+    if (!flag[L & 1]) {
+      last = L;
+      break;
+    }
   }
+  // the plan's deepest level: how many bit planes the sliced rows need
+  if (maxd && tid == 0) atomicMax(maxd, last);
   MS_STAMP();
   // ---- unreachable (s, v) pairs and row padding ----
   uint64_t miss = 0;
@@ -836,6 +843,243 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
 }
 
 // ---------------------------------------------------------------------------
+//  2b. next-hop pass over bit-sliced rows (msbfs_kernel plans)
+// ---------------------------------------------------------------------------
+// A row's distances as P bit planes: word w of plane b holds bit b of the
+// distances of nodes 32w .. 32w + 31 (bit t = node 32w + t); all-ones =
+// unreachable.  P = the bits of maxd + 1 (maxd = the plan's deepest BFS
+// level, from msbfs_kernel), so every finite distance stays below the
+// all-ones code: a fabric (4-5 levels) needs 3 planes, 3/8 of the u8 row.
+// With unit metrics (w(s, x) = 1) the test of 32 destinations against one
+// neighbour row is OR_b (x_b ^ t_b) == 0 with t = d_s - 1, decremented
+// bit-sliced once per source word: ~2 bit operations per plane and
+// neighbour word where the byte compare of narrow rows spends ~30 per 16
+// destinations, and the result is already the output word (bit v of word
+// v / 32 of bitmap j).  When maxd reaches the u8 copy's saturation (254)
+// the planes stay unwritten and the pass decides on the u32 rows.
+constexpr uint32_t kSlChunk = 2048;  // destinations per pass of a wave: one word per lane
+constexpr uint32_t kSlSlots = 8;     // plane slots per word of a sliced row
+constexpr uint32_t kSlSat = 254;     // maxd at which the u8 copy saturates
+
+// Sliced row r starts at S + r * kSlSlots * wpm; word w's P planes sit at
+// w * P .. w * P + P - 1, so a lane's planes are one P-dword load and a
+// wave's 64 loads cover 64 * P consecutive dwords.
+
+// u8 narrow rows -> bit-sliced rows; one thread per (row, word): two 16-byte
+// loads, P words stored.
+__global__ __launch_bounds__(256) void slice_rows_kernel(const uint8_t* __restrict__ Dn,
+                                                         uint32_t npitch, uint32_t rows, uint32_t wpm,
+                                                         const uint32_t* __restrict__ maxd,
+                                                         uint32_t* __restrict__ S) {
+  const uint32_t md = *maxd;
+  if (md >= kSlSat) return;
+  const uint32_t P = 32u - __clz(md + 1u);
+  const uint64_t total = (uint64_t)rows * wpm;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = (uint32_t)(t / wpm), w = (uint32_t)(t % wpm);
+    const uint4* in = reinterpret_cast<const uint4*>(Dn + (size_t)r * npitch + 32ull * w);
+    const uint4 a = in[0], b = in[1];
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t* out = S + (size_t)r * kSlSlots * wpm + (size_t)w * P;
+    for (uint32_t pl = 0; pl < P; ++pl) {
+      uint32_t word = 0;
+      // bit pl of bytes 4q .. 4q + 3 -> bits 4q .. 4q + 3 (the multiply moves
+      // byte i's bit to bit 24 + i; no cross term lands in bits 24..31)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        word |= ((((d[q] >> pl) & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+      out[pl] = word;
+    }
+  }
+}
+
+template <int P>
+struct Planes {
+  uint32_t v[P];
+};
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// N consecutive dwords by buffer loads: wave-uniform byte offset in soff (an
+// SGPR), the lane's in voff -- no 64-bit vector addresses
+template <int N>
+__device__ __forceinline__ void bload(uint32_t* d, __amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                      uint32_t soff) {
+  if constexpr (N >= 4) {
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w;
+    if constexpr (N > 4) bload<N - 4>(d + 4, r, voff + 16, soff);
+  } else if constexpr (N == 3) {
+    const u32x3 a = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, (int)soff, 0);
+    d[0] = a.x, d[1] = a.y, d[2] = a.z;
+  } else if constexpr (N == 2) {
+    const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    d[0] = a.x, d[1] = a.y;
+  } else {
+    d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+  }
+}
+
+// The sliced match of one 64-word chunk: lane = output word w.  Loads are
+// unconditional (rows are padded past the last lane's word), stores
+// predicated on `live`.  Two groups of U neighbour rows in flight, one
+// P-dword load per row (U * P <= 16 keeps the registers low).
+//   rs: the sliced rows (S); ro: the source's bitmaps (nh + nh_off[i]).
+//   offs/k: the unit's neighbour range (its row offsets, its length); jb:
+//   the range's first neighbour index (the bitmap the first result goes to).
+template <int P, int U = (P <= 4 ? 4 : 2)>
+__device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t ro,
+                                            uint32_t wpm, uint32_t srow,
+                                            const uint32_t* __restrict__ offs, uint32_t k,
+                                            uint32_t jb, uint32_t w, bool live) {
+  const uint32_t wpb = w * P * 4;  // the lane's plane bytes inside any row
+  Planes<P> sv;
+  bload<P>(sv.v, rs, wpb, srow * kSlSlots * wpm * 4);
+  uint32_t t[P];
+  uint32_t ones = ~0u, zeros = ~0u, borrow = ~0u;
+#pragma unroll
+  for (int b = 0; b < P; ++b) {
+    const uint32_t x = sv.v[b];
+    ones &= x;
+    zeros &= ~x;
+    t[b] = x ^ borrow;  // t = d_s - 1
+    borrow &= ~x;
+  }
+  // the source itself (d = 0) and unreachable destinations take no next hop;
+  // elsewhere t is finite and never the all-ones code of a drained (dead) row
+  const uint32_t valid = ~(ones | zeros);
+  auto load_group = [&](uint32_t j0, Planes<P> (&r)[U]) {
+    uint32_t o[U];  // one scalar load of U row offsets
+    if constexpr (U == 4) {
+      const uint4 o4 = *reinterpret_cast<const uint4*>(offs + j0);
+      o[0] = o4.x, o[1] = o4.y, o[2] = o4.z, o[3] = o4.w;
+    } else {
+      const uint2 o2 = *reinterpret_cast<const uint2*>(offs + j0);
+      o[0] = o2.x, o[1] = o2.y;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) bload<P>(r[u].v, rs, wpb, o[u] * 4);
+  };
+  auto match_group = [&](uint32_t j0, const Planes<P> (&r)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (j0 + u >= k) break;
+      uint32_t diff = 0;
+#pragma unroll
+      for (int b = 0; b < P; ++b) diff |= r[u].v[b] ^ t[b];
+      if (live)
+        __builtin_amdgcn_raw_buffer_store_b32(~diff & valid, ro, (int)(w * 4),
+                                              (int)((jb + j0 + u) * wpm * 4), 0);
+    }
+  };
+  Planes<P> ra[U], rb[U];
+  load_group(0, ra);
+  for (uint32_t j0 = 0; j0 < k; j0 += 2 * U) {
+    load_group(j0 + U, rb);
+    match_group(j0, ra);
+    load_group(j0 + 2 * U, ra);
+    match_group(j0 + U, rb);
+  }
+}
+
+// Work units: (source i, chunks [c0, c1) of 64 words, neighbours [j0, j1)),
+// at most about kSlUnit neighbour-chunk matches each (spf_plan_create keeps
+// light sources whole and cuts heavy ones per chunk and neighbour range),
+// one wave per unit, units of an XCD's source runs on that XCD.  A wave's
+// matches are latency-bound (two groups of row loads in flight), so one wave
+// per source left the spine switches (173 neighbours x 5 chunks) running
+// long after the rest; one wave per (source, chunk) was bound by wave launch;
+// persistent waves pulling units through per-XCD atomic counters serialised
+// on the counters (r02_v20: 2.4x slower); sc1 bitmap stores (lines leave L2)
+// changed nothing (r02_v22).
+constexpr uint32_t kSlUnit = 128;  // neighbour-chunk matches per unit (at most, about)
+
+__global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
+    const uint32_t* __restrict__ S, const uint32_t* __restrict__ maxd,
+    const uint32_t* __restrict__ D, uint32_t pitch,
+    const uint32_t* __restrict__ req_src, const uint32_t* __restrict__ row_of,
+    const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
+    const uint32_t* __restrict__ nb_w, const uint32_t* __restrict__ nb_row,
+    const uint32_t* __restrict__ nb_row_off, const uint32_t* __restrict__ nb_drained,
+    uint32_t dead, uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
+    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes) {
+  const uint32_t g = blockIdx.x & 7;  // this block's XCD (round-robin placement)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wpm = pitch / 32;
+  const uint32_t md = *maxd;
+  const uint32_t P = md < kSlSat ? 32u - __clz(md + 1u) : 0u;  // 0: saturated
+  const uint32_t rstride = kSlSlots * wpm;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(S), 0, (int)s_bytes, 0x00020000);
+  // wave-uniform to the compiler too (readfirstlane): the unit's values then
+  // live in SGPRs and its row offsets arrive by scalar loads
+  const uint32_t t = (blockIdx.x >> 3) * kEcmpWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t u_begin = unit_off[g];
+  if (t >= unit_off[g + 1] - u_begin) return;  // whole wave: no barriers below
+  {
+    const uint4 u = units[u_begin + t];
+    const uint32_t i = u.x, c0 = u.y & 0xFFFFu, c1 = u.y >> 16, j0 = u.z, j1 = u.w;
+    const uint32_t s = req_src[i];
+    const uint32_t nb0 = nb_ptr[s], k = j1 - j0;
+    const uint32_t srow = row_of[s];
+    const uint32_t* offs = nb_row + nb_row_off[i];
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        nh + nh_off[i], 0, (int)((nb_ptr[s + 1] - nb0) * wpm * 4), 0x00020000);
+    for (uint32_t c = c0; c < c1; ++c) {
+      const uint32_t w0 = c * 64, w = w0 + lane;
+      const bool live = w < wpm;
+      switch (P) {
+        case 1: sliced_pass<1>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 2: sliced_pass<2>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 3: sliced_pass<3>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 4: sliced_pass<4>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 5: sliced_pass<5>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 6: sliced_pass<6>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 7: sliced_pass<7>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        case 8: sliced_pass<8>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        default: {
+          uint32_t* out = nh + nh_off[i] + w;
+          // saturated: exact u32 rows, 32 destinations per lane (offsets are
+          // sliced-row offsets, row = offset / rstride)
+          for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t oj = offs[j], wj = hop ? 1u : nb_w[nb0 + j];
+            uint32_t m = 0;
+            if (oj != dead && live) {
+              const uint4* Dx = reinterpret_cast<const uint4*>(D + (size_t)(oj / rstride) * pitch + 32ull * w);
+              const uint4* Ds = reinterpret_cast<const uint4*>(D + (size_t)srow * pitch + 32ull * w);
+#pragma unroll 1
+              for (int q = 0; q < 8; ++q) {
+                const uint4 a4 = Dx[q], b4 = Ds[q];
+                const uint32_t a[4] = {a4.x, a4.y, a4.z, a4.w}, b[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) m |= (uint32_t)(a[e] != kInf && a[e] + wj == b[e]) << (4 * q + e);
+              }
+            }
+            if (live) out[(size_t)j * wpm] = m;
+          }
+        }
+      }
+      // drained neighbour x: only x itself, reached directly when d_s(x) == w(s, x)
+      if (nb_drained[i]) {
+        uint32_t* out = nh + nh_off[i] + w;
+        const uint32_t cbase = w0 * 32;
+        for (uint32_t j = j0; j < j1; ++j) {
+          if (offs[j] != dead) continue;
+          const uint32_t x = nb_id[nb0 + j];
+          if (x < cbase || x >= cbase + kSlChunk) continue;
+          const uint32_t wj = hop ? 1u : nb_w[nb0 + j];
+          if (lane == (x - cbase) / 32 && D[(size_t)srow * pitch + x] == wj)
+            out[(size_t)j * wpm] = 1u << (x & 31);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 //  copy selected D rows into the caller's dense output (non-direct plans)
 // ---------------------------------------------------------------------------
 __global__ void gather_rows_kernel(const uint32_t* __restrict__ D, uint32_t pitch,
@@ -977,7 +1221,14 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   c->loaded = false;
   c->N = N;
   c->E = E;
-  c->pitch = (N + 63) & ~63u;      // dist rows / bitmap rows: whole u64 words
+  // dist rows / bitmap rows: whole 1024-node chunks, so every next-hop
+  // bitmap (pitch / 8 bytes) starts on a 128-byte line and no line of the
+  // output is written partially by two waves (SPF_PITCH_ALIGN: A/B only)
+  {
+    const char* e = std::getenv("SPF_PITCH_ALIGN");
+    const uint32_t a = e ? (uint32_t)atoi(e) : 1024u;  // a power of two >= 64
+    c->pitch = (N + a - 1) & ~(a - 1);
+  }
   c->npitch = (N + 1023) & ~1023u;  // narrow rows: whole 1024-node chunks
   c->row_ptr.assign(g->row_ptr, g->row_ptr + N + 1);
   c->col.assign(g->col, g->col + E);
@@ -1225,7 +1476,7 @@ namespace {
 bool use_planes(const spf_ctx* c);
 
 bool use_narrow(const spf_ctx* c, const spf_plan* p) {
-  if (const char* e = std::getenv("SPF_NARROW")) return e[0] == '1';
+  if (const char* e = std::getenv("SPF_NARROW")) return e[0] != '0';
   // the register-plane BFS writes each row once, coalesced: the u8 copy
   // costs one more row store and the next-hop pass reads 4x fewer bytes
   if (use_planes(c)) return true;
@@ -1341,17 +1592,31 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
   p->narrow = p->ms && use_narrow(c, p);
+  // bit-sliced rows behind the per-level-store BFS (it reports the deepest
+  // level); the register-plane BFS serves deep graphs, where planes would
+  // not pay.  SPF_NARROW=1 keeps the byte-row pass (experiments, tests).
+  {
+    const char* e = std::getenv("SPF_NARROW");
+    p->sliced = p->narrow && !use_planes(c) && !(e && e[0] == '1');
+  }
+  const uint32_t wpm = c->pitch / 32;
+  const uint64_t rstride = (uint64_t)kSlSlots * wpm;  // sliced row: words
   {
     // per-source neighbour rows for the next-hop pass (kInf = drained)
     std::vector<uint32_t> nb_row, nb_row_off(n_src), nb_drained(n_src, 0);
-    const uint32_t dead = p->narrow ? (uint32_t)p->closure.size() * c->npitch : kInf;
+    const uint32_t dead = p->sliced   ? (uint32_t)(p->closure.size() * rstride)
+                          : p->narrow ? (uint32_t)p->closure.size() * c->npitch
+                                      : kInf;
     p->dead = dead;
     for (uint32_t i = 0; i < n_src; ++i) {
       nb_row_off[i] = (uint32_t)nb_row.size();
       for (uint32_t e = c->nb_ptr[srcs[i]]; e < c->nb_ptr[srcs[i] + 1]; ++e) {
         const uint32_t x = c->nb_id[e];
         const bool dr = c->ovl[x] != 0;
-        nb_row.push_back(dr ? dead : p->narrow ? row_of[x] * c->npitch : row_of[x]);
+        nb_row.push_back(dr          ? dead
+                         : p->sliced ? (uint32_t)(row_of[x] * rstride)
+                         : p->narrow ? row_of[x] * c->npitch
+                                     : row_of[x]);
         nb_drained[i] += dr;
       }
       const size_t k = nb_row.size() - nb_row_off[i];
@@ -1383,6 +1648,40 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
         i = e;
       }
     }
+    if (p->sliced) {
+      // sliced-pass work units per XCD, in the XCD's source order: a source
+      // whose neighbour-chunk matches fit kSlUnit is one unit, a heavier one
+      // is cut per chunk and per neighbour range (multiples of 8: the row
+      // offset lists are read 16-byte aligned)
+      const uint32_t chunks = (wpm + 63) / 64;
+      const char* ue = std::getenv("SPF_SLICED_UNIT");  // A/B knob
+      const uint32_t unit = ue ? (uint32_t)atoi(ue) : kSlUnit;
+      std::vector<uint32_t> units, unit_off(9, 0);
+      p->max_xcd_units = 0;
+      for (int g = 0; g < 8; ++g) {
+        unit_off[g] = (uint32_t)(units.size() / 4);
+        for (uint32_t i : lists[g]) {
+          const uint32_t k = p->words[i];
+          if (k == 0) continue;
+          if ((uint64_t)k * chunks <= unit) {
+            units.insert(units.end(), {i, 0u | (chunks << 16), 0u, k});
+            continue;
+          }
+          // per chunk, k split into equal ranges of <= unit neighbours
+          // (multiples of 8)
+          const uint32_t parts = (k + unit - 1) / unit;
+          const uint32_t jstep = ((k + parts - 1) / parts + 7) / 8 * 8;
+          for (uint32_t ch = 0; ch < chunks; ++ch)
+            for (uint32_t j = 0; j < k; j += jstep)
+              units.insert(units.end(), {i, ch | ((ch + 1) << 16), j, std::min(k, j + jstep)});
+        }
+        p->max_xcd_units = std::max(p->max_xcd_units, (uint32_t)(units.size() / 4) - unit_off[g]);
+      }
+      unit_off[8] = (uint32_t)(units.size() / 4);
+      if (units.empty()) units.assign(4, 0);
+      HIP_TRY(c, p->d_units.upload(units.data(), units.size(), c->stream));
+      HIP_TRY(c, p->d_unit_off.upload(unit_off.data(), 9, c->stream));
+    }
     size_t most = 0;
     for (auto& l : lists) most = std::max(most, l.size());
     std::vector<uint32_t> slot(most * 8, kInf);
@@ -1397,6 +1696,16 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   if (p->narrow) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
     HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
     HIP_TRY(c, hipMemsetAsync(p->d_Dn.p + p->closure.size() * c->npitch, 0xFF, c->npitch, c->stream));
+  }
+  if (p->sliced) {  // sliced rows + the dead row (all planes all-ones) + padding
+    const size_t rows = p->closure.size();
+    // a wave's last chunk reads up to 64 * kSlSlots words past a row's end
+    const size_t pad = 64 * kSlSlots + 64;
+    if (((rows + 1) * rstride + pad) * 4 >= (1ull << 31))  // buffer byte offsets
+      return fail(c, SPF_E_UNSUPPORTED, "sliced rows exceed 32-bit offsets");
+    HIP_TRY(c, p->d_S.alloc((rows + 1) * rstride + pad));
+    HIP_TRY(c, hipMemsetAsync(p->d_S.p + rows * rstride, 0xFF, (rstride + pad) * 4, c->stream));
+    HIP_TRY(c, p->d_maxd.alloc(1));
   }
   {
     const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
@@ -1439,7 +1748,7 @@ uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->clos
 spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
   *bfs = p->exact ? 3u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
-  *narrow = p->narrow ? 1u : 0u;
+  *narrow = p->sliced ? 2u : p->narrow ? 1u : 0u;
   return SPF_OK;
 }
 
@@ -1456,6 +1765,21 @@ spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) 
 //     u32 rows otherwise) plus the next-hop bitmaps written once.
 spf_status spf_plan_traffic(const spf_plan* p, uint64_t* bfs_bytes, uint64_t* ecmp_bytes) {
   if (!p || !bfs_bytes || !ecmp_bytes) return SPF_E_INVALID;
+  uint64_t b[3];
+  const spf_status st = spf_plan_traffic_phases(p, b);
+  if (st != SPF_OK) return st;
+  *bfs_bytes = b[0];
+  *ecmp_bytes = b[1] + b[2];
+  return SPF_OK;
+}
+
+//   Slicing (sliced plans): the u8 rows read, P planes per row written; the
+//     sliced next-hop pass then reads P planes per row and writes the bitmaps.
+spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
+  if (!p || !bytes) return SPF_E_INVALID;
+  uint64_t* bfs_bytes = &bytes[0];
+  uint64_t* ecmp_bytes = &bytes[2];
+  bytes[1] = 0;
   const spf_ctx* c = p->ctx;
   const uint64_t N = c->N, E = c->E, rows = p->closure.size();
   uint64_t bfs = 0;
@@ -1479,8 +1803,22 @@ spf_status spf_plan_traffic(const spf_plan* p, uint64_t* bfs_bytes, uint64_t* ec
   } else {
     bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch);
   }
-  const uint64_t row_bytes = p->narrow ? c->npitch : 4ull * c->pitch;
   *bfs_bytes = bfs;
+  if (p->sliced && p->nh_total) {
+    // planes in use: from the last execute's deepest level (one 4-byte read)
+    uint32_t md = 0;
+    HIP_TRY(p->ctx, hipMemcpy(&md, p->d_maxd.p, 4, hipMemcpyDeviceToHost));
+    const uint64_t wbytes = 4ull * (c->pitch / 32);
+    if (md < kSlSat) {
+      const uint64_t P = 32u - __builtin_clz(md + 1u);
+      bytes[1] = rows * c->npitch + rows * P * wbytes;
+      *ecmp_bytes = rows * P * wbytes + 4ull * p->nh_total;
+    } else {
+      *ecmp_bytes = rows * 4ull * c->pitch + 4ull * p->nh_total;
+    }
+    return SPF_OK;
+  }
+  const uint64_t row_bytes = p->narrow ? c->npitch : 4ull * c->pitch;
   *ecmp_bytes = p->nh_total ? rows * row_bytes + 4ull * p->nh_total : 0ull;
   return SPF_OK;
 }
@@ -1548,7 +1886,7 @@ size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 
 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
-                  hipStream_t s) {
+                  uint32_t* maxd, hipStream_t s) {
   const uint32_t n_col = c->sell_ptr.back();
   const size_t lds = msbfs_lds_bytes(c->N), lds_col = lds + 2ull * n_col;
   const bool lcol = lds_col <= kMaxLds;
@@ -1560,11 +1898,11 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
   if (lcol)
     hipLaunchKernelGGL((msbfs_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds_col, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
-                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
+                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, maxd, c->d_stamps.p);
   else
     hipLaunchKernelGGL((msbfs_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
-                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, c->d_stamps.p);
+                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, maxd, c->d_stamps.p);
 }
 
 size_t planes_lds_bytes(uint32_t own) { return 8ull * own * kMsThreads + 4ull * (kPlBatch + 4); }
@@ -1599,7 +1937,7 @@ bool use_planes(const spf_ctx* c) {
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
-                        uint8_t* Dn, hipStream_t s) {
+                        uint8_t* Dn, uint32_t* maxd, hipStream_t s) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
     HIP_TRY(c, c->d_stamps.alloc(64 * 16));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
@@ -1614,13 +1952,13 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
     HIP_TRY(c, hipGetLastError());
     return SPF_OK;
   }
-  if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, s);
-  else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, s);
-  else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, s);
-  else if (own <= 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, s);
-  else if (own <= 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, s);
-  else if (own <= 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, s);
-  else msbfs_launch<16>(c, rows_src, rows, D, Dn, s);
+  if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, maxd, s);
+  else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, maxd, s);
+  else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, maxd, s);
+  else if (own <= 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, maxd, s);
+  else if (own <= 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, maxd, s);
+  else if (own <= 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, maxd, s);
+  else msbfs_launch<16>(c, rows_src, rows, D, Dn, maxd, s);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -1635,6 +1973,32 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
                      c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead, hop ? 1u : 0u,
                      p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p);
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
+spf_status launch_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool hop, uint32_t* d_nh,
+                         hipStream_t s) {
+  const uint32_t wpm = c->pitch / 32;
+  const uint32_t rows = (uint32_t)p->closure.size();
+  const uint64_t words = (uint64_t)rows * wpm;
+  const uint32_t sb = (uint32_t)std::min<uint64_t>((words + 255) / 256, 16ull * c->n_cu);
+  hipLaunchKernelGGL(slice_rows_kernel, dim3(std::max(sb, 1u)), dim3(256), 0, s, p->d_Dn.p, c->npitch,
+                     rows, wpm, p->d_maxd.p, p->d_S.p);
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
+spf_status launch_ecmp_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool hop, uint32_t* d_nh,
+                              hipStream_t s) {
+  // one wave per unit; block b serves XCD b % 8 (round-robin placement)
+  const uint32_t blocks = 8 * std::max(1u, (p->max_xcd_units + kEcmpWaves - 1) / kEcmpWaves);
+  hipLaunchKernelGGL(ecmp_sliced_kernel, dim3(blocks), dim3(kEcmpThreads), 0, s, p->d_S.p,
+                     p->d_maxd.p, D, c->pitch, p->d_srcs.p, p->d_row_of.p,
+                     c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p,
+                     p->d_nb_drained.p, p->dead, hop ? 1u : 0u, p->d_nh_off.p, d_nh,
+                     reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p,
+                     (uint32_t)(p->d_S.n * 4));
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -1705,7 +2069,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   if (p->exact) {
     hipEvent_t* ev = nullptr;
     if (p->timing_cap) {
-      ev = &p->ev[3 * (p->timing_n % p->timing_cap)];
+      ev = &p->ev[4 * (p->timing_n % p->timing_cap)];
       ++p->timing_n;
       HIP_TRY(c, hipEventRecord(ev[0], s));
     }
@@ -1713,31 +2077,38 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
                                        (p->flags & SPF_FLAG_DIST64) != 0, nullptr, d_dist, d_nh,
                                        nullptr, s);
     if (st != SPF_OK) return st;
-    if (ev) {
-      HIP_TRY(c, hipEventRecord(ev[1], s));
-      HIP_TRY(c, hipEventRecord(ev[2], s));
-    }
+    if (ev)
+      for (int e = 1; e < 4; ++e) HIP_TRY(c, hipEventRecord(ev[e], s));
     c->solves += p->n_src;
     return SPF_OK;
   }
   uint32_t* D = p->direct ? d_dist : p->d_D.p;
   const uint32_t rows = (uint32_t)p->closure.size();
+  const bool sliced = p->sliced && p->nh_total;
+  if (sliced) HIP_TRY(c, hipMemsetAsync(p->d_maxd.p, 0, 4, s));  // msbfs_kernel's atomicMax target
   hipEvent_t* ev = nullptr;
   if (p->timing_cap) {
-    ev = &p->ev[3 * (p->timing_n % p->timing_cap)];
+    ev = &p->ev[4 * (p->timing_n % p->timing_cap)];
     ++p->timing_n;
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
-  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr, s)
+  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
+                                       sliced ? p->d_maxd.p : nullptr, s)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
-  if (p->nh_total) {
-    st = p->narrow ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
-               : launch_ecmp<false>(c, p, nullptr, D, hop, d_nh, s);
+  if (sliced) {
+    st = launch_sliced(c, p, D, hop, d_nh, s);
     if (st != SPF_OK) return st;
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+  if (p->nh_total) {
+    st = sliced     ? launch_ecmp_sliced(c, p, D, hop, d_nh, s)
+         : p->narrow ? launch_ecmp<true>(c, p, p->d_Dn.p, D, hop, d_nh, s)
+                     : launch_ecmp<false>(c, p, nullptr, D, hop, d_nh, s);
+    if (st != SPF_OK) return st;
+  }
+  if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
   if (!p->direct) {
     hipLaunchKernelGGL(gather_rows_kernel, dim3(std::min<uint32_t>((pitch / 4 + 255) / 256, 64), p->n_src),
                        dim3(256), 0, s, D, pitch, p->d_req_rows.p, d_dist);
@@ -1751,30 +2122,37 @@ spf_status spf_plan_enable_timing(spf_plan* p, uint32_t max_executes) {
   if (!p) return SPF_E_INVALID;
   spf_ctx* c = p->ctx;
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
-  p->ev.assign(3ull * max_executes, nullptr);
+  p->ev.assign(4ull * max_executes, nullptr);
   for (auto& e : p->ev) HIP_TRY(c, hipEventCreate(&e));
   p->timing_cap = max_executes;
   p->timing_n = 0;
   return SPF_OK;
 }
 
-spf_status spf_plan_timing(spf_plan* p, double* sssp_ms, double* ecmp_ms, uint32_t* n) {
-  if (!p || !p->timing_cap) return SPF_E_STATE;
+spf_status spf_plan_timing_phases(spf_plan* p, double* ms, uint32_t* n) {
+  if (!p || !p->timing_cap || !ms) return SPF_E_STATE;
   spf_ctx* c = p->ctx;
   const uint32_t cnt = std::min(p->timing_n, p->timing_cap);
-  double a = 0, b = 0;
+  ms[0] = ms[1] = ms[2] = 0;
   for (uint32_t i = 0; i < cnt; ++i) {
-    float t0 = 0, t1 = 0;
-    HIP_TRY(c, hipEventSynchronize(p->ev[3 * i + 2]));
-    HIP_TRY(c, hipEventElapsedTime(&t0, p->ev[3 * i], p->ev[3 * i + 1]));
-    HIP_TRY(c, hipEventElapsedTime(&t1, p->ev[3 * i + 1], p->ev[3 * i + 2]));
-    a += t0;
-    b += t1;
+    HIP_TRY(c, hipEventSynchronize(p->ev[4 * i + 3]));
+    for (int ph = 0; ph < 3; ++ph) {
+      float t = 0;
+      HIP_TRY(c, hipEventElapsedTime(&t, p->ev[4 * i + ph], p->ev[4 * i + ph + 1]));
+      ms[ph] += t;
+    }
   }
-  if (sssp_ms) *sssp_ms = a;
-  if (ecmp_ms) *ecmp_ms = b;
   if (n) *n = cnt;
   p->timing_n = 0;
+  return SPF_OK;
+}
+
+spf_status spf_plan_timing(spf_plan* p, double* sssp_ms, double* ecmp_ms, uint32_t* n) {
+  double ms[3];
+  const spf_status st = spf_plan_timing_phases(p, ms, n);
+  if (st != SPF_OK) return st;
+  if (sssp_ms) *sssp_ms = ms[0];
+  if (ecmp_ms) *ecmp_ms = ms[1] + ms[2];
   return SPF_OK;
 }
 

@@ -85,20 +85,46 @@ class SpfPlan(NativeHandle):
         return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
 
     BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel")
+    ROW_MODES = ("u32", "u8", "sliced")
 
     def kernels(self) -> Tuple[str, bool]:
-        """(distance kernel name, next-hop pass reads u8 narrow rows) of the
-        next execute (spf_plan_kernels)."""
+        """(distance kernel name, next-hop pass reads u8 narrow rows or their
+        bit-sliced form) of the next execute (spf_plan_kernels)."""
+        bfs, narrow = self._kernel_codes()
+        return self.BFS_KERNELS[bfs], bool(narrow)
+
+    def _kernel_codes(self) -> Tuple[int, int]:
         bfs, narrow = C.c_uint32(), C.c_uint32()
         self._eng._err(N.lib.spf_plan_kernels(self._h, C.byref(bfs), C.byref(narrow)))
-        return self.BFS_KERNELS[bfs.value], bool(narrow.value)
+        return bfs.value, narrow.value
+
+    def row_mode(self) -> str:
+        """Rows the next-hop pass reads: "u32", "u8" or "sliced" (bit planes)."""
+        return self.ROW_MODES[self._kernel_codes()[1]]
+
+    def phase_kernels(self) -> Tuple[str, Optional[str], Optional[str]]:
+        """Kernel names of the execute's three timed phases (distance kernel,
+        row slicing, next-hop pass); None where a phase launches nothing."""
+        bfs, narrow = self._kernel_codes()
+        name = self.BFS_KERNELS[bfs]
+        if bfs == 3 or not self.nh_words:
+            return name, None, None
+        if narrow == 2:
+            return name, "slice_rows_kernel", "ecmp_sliced_kernel"
+        return name, None, "ecmp_kernel"
 
     def traffic(self) -> Tuple[int, int]:
-        """Compulsory HBM bytes of (distance kernel, next-hop kernel) per
-        execute (spf_plan_traffic)."""
+        """Compulsory HBM bytes of (distance kernel, next-hop pass incl. row
+        slicing) per execute (spf_plan_traffic)."""
         a, b = C.c_uint64(), C.c_uint64()
         self._eng._err(N.lib.spf_plan_traffic(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    def traffic_phases(self) -> Tuple[int, int, int]:
+        """Compulsory bytes per phase (distance kernel, slicing, next hops)."""
+        b = (C.c_uint64 * 3)()
+        self._eng._err(N.lib.spf_plan_traffic_phases(self._h, b))
+        return b[0], b[1], b[2]
 
     def enable_timing(self, max_executes: int) -> None:
         self._eng._err(N.lib.spf_plan_enable_timing(self._h, max_executes))
@@ -108,6 +134,13 @@ class SpfPlan(NativeHandle):
         a, b, n = C.c_double(), C.c_double(), C.c_uint32()
         self._eng._err(N.lib.spf_plan_timing(self._h, C.byref(a), C.byref(b), C.byref(n)))
         return a.value, b.value, n.value
+
+    def timing_phases(self) -> Tuple[Tuple[float, float, float], int]:
+        """((distance, slicing, next-hop) summed ms, executes) since
+        enable/last call (spf_plan_timing_phases)."""
+        ms, n = (C.c_double * 3)(), C.c_uint32()
+        self._eng._err(N.lib.spf_plan_timing_phases(self._h, ms, C.byref(n)))
+        return (ms[0], ms[1], ms[2]), n.value
 
     def execute_torch(self, dist, nh, stream=None) -> None:
         """dist: int32/uint32 tensor [n_src, pitch] on the engine's device;

@@ -215,6 +215,20 @@ def barabasi_albert(n: int = 250_000, m: int = 4, seed: int = 1,
     return _undirected_to_adj(nodes, links, fwd, rev, f"ba{n}")
 
 
+def clique_with_tail(k: int, depth: int) -> Topology:
+    """A k-clique with a path of depth - 1 nodes hanging off clique node 0,
+    unit metrics: the graph's diameter (deepest BFS level over all sources)
+    is exactly `depth` (k >= 2, depth >= 1)."""
+    nodes = [f"c{i:02d}" for i in range(k)] + [f"t{i:03d}" for i in range(depth - 1)]
+    links = [(a, b) for a in range(k) for b in range(a + 1, k)]
+    prev = 0
+    for i in range(depth - 1):
+        links.append((prev, k + i))
+        prev = k + i
+    ones = np.ones(len(links), np.int64)
+    return _undirected_to_adj(nodes, links, ones, ones, f"clique{k}_tail{depth}")
+
+
 def random_graph(n: int, n_links: int, seed: int, max_metric: int = 10,
                  parallel_frac: float = 0.0, overload_frac: float = 0.0,
                  link_overload_frac: float = 0.0) -> Topology:

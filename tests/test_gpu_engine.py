@@ -123,29 +123,54 @@ def test_zero_metric_runs_the_exact_kernel():
     compare(names, eng, orc, list(range(len(names))), hop=True)
 
 
-@pytest.mark.parametrize("narrow", ["0", "1"])
+ROW_MODES = {"0": "u32", "1": "u8", "2": "sliced"}
+
+
+@pytest.mark.parametrize("narrow", ["0", "1", "2"])
 @pytest.mark.parametrize("name,make", [
     ("fabric_full1000", lambda: T.fabric(1000, full=True)),
     ("grid12", lambda: T.grid(12)),
     ("rand_drained", lambda: T.random_graph(60, 150, 7, max_metric=1, overload_frac=0.15)),
-], ids=["fabric", "grid", "rand"])
-def test_next_hop_pass_both_row_widths(name, make, narrow, monkeypatch):
-    """The BFS plans' next-hop pass on u8 narrow rows and on the exact u32 rows
-    (the plan picks one by average degree; SPF_NARROW forces it)."""
+    ("fabric_drained", lambda: T.random_graph(300, 3000, 11, max_metric=1, overload_frac=0.1)),
+], ids=["fabric", "grid", "rand", "dense_drained"])
+def test_next_hop_pass_every_row_form(name, make, narrow, monkeypatch):
+    """The BFS plans' next-hop pass on the exact u32 rows, on u8 narrow rows
+    and on their bit-sliced planes (the plan picks by degree and BFS kernel;
+    SPF_NARROW=0/1/2 forces it), unit metrics and hop counts."""
     monkeypatch.setenv("SPF_NARROW", narrow)
+    monkeypatch.setenv("SPF_MSBFS", "masks")  # the per-level BFS reports the depth slicing needs
     names, eng, orc = load(make())
+    assert eng.plan([0], hop=True).row_mode() == ROW_MODES[narrow]
     compare(names, eng, orc, list(range(len(names))), hop=True)
+    compare(names, eng, orc, list(range(len(names))))
 
 
-def test_saturated_narrow_rows_fall_back_to_exact(monkeypatch):
-    """Hop distances >= 254 saturate the u8 copy: those waves decide on the
-    u32 rows.  A 700-node ring has distances up to 350."""
-    monkeypatch.setenv("SPF_NARROW", "1")
+@pytest.mark.parametrize("narrow", ["1", "2"])
+def test_saturated_narrow_rows_fall_back_to_exact(narrow, monkeypatch):
+    """Hop distances >= 254 saturate the u8 copy: the byte pass decides those
+    waves on the u32 rows, the sliced pass the whole plan.  A 700-node ring
+    has distances up to 350."""
+    monkeypatch.setenv("SPF_NARROW", narrow)
+    monkeypatch.setenv("SPF_MSBFS", "masks")
     topo = T.wan(700, 0, seed=1)  # ring only
     names, eng, orc = load(topo)
     rng = np.random.default_rng(5)
     compare(names, eng, orc, sorted(int(x) for x in rng.choice(len(names), 40, replace=False)),
             hop=True)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 6, 7, 14, 15, 30, 31, 126, 127, 253])
+def test_sliced_plane_counts(depth, monkeypatch):
+    """Every plane count of the sliced pass: a dense core with a path tail
+    whose length sets the deepest level (P = bits of maxd + 1 changes at
+    maxd = 1, 3, 7, ... 127; 253 is the last depth before the u8 copy
+    saturates)."""
+    monkeypatch.setenv("SPF_NARROW", "2")
+    monkeypatch.setenv("SPF_MSBFS", "masks")
+    names, eng, orc = load(T.clique_with_tail(12, depth))
+    p = eng.plan([0], hop=True)
+    assert p.row_mode() == "sliced"
+    compare(names, eng, orc, list(range(len(names))), hop=True)
 
 
 @pytest.mark.parametrize("variant", ["planes", "masks"])
@@ -162,6 +187,6 @@ def test_bfs_variants_exact(name, make, variant, monkeypatch):
     widths; SPF_MSBFS / SPF_NARROW force the choice the plan makes by degree."""
     monkeypatch.setenv("SPF_MSBFS", variant)
     names, eng, orc = load(make())
-    for narrow in ("0", "1"):
+    for narrow in ("0", "1", "2"):
         monkeypatch.setenv("SPF_NARROW", narrow)
         compare(names, eng, orc, list(range(len(names))), hop=True)
