@@ -143,7 +143,9 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
 /* Which kernels the next execute runs (diagnostics, benchmarks):
  * *bfs = 0 sssp_kernel (weighted, per source), 1 msbfs_kernel (64 sources per
  * sweep, per-level stores), 2 msbfs_planes_kernel (32 sources, register bit
- * planes, rows written once), 3 exact_spf_kernel; *narrow = 0 when the
+ * planes, rows written once), 3 exact_spf_kernel, 4 spf_big_kernel (graphs
+ * beyond the LDS-resident kernels: one source at a time on the whole chip,
+ * next hops inside); *narrow = 0 when the
  * next-hop pass (ecmp_kernel) reads the u32 rows, 1 when it reads u8 rows,
  * 2 when slice_rows_kernel turns the u8 rows into bit planes and
  * ecmp_sliced_kernel matches those.

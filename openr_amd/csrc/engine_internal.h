@@ -107,6 +107,8 @@ struct spf_plan {
   spfi::DevBuf<uint32_t> d_S, d_maxd;  // sliced rows (+ dead row); deepest BFS level + 8 counters
   spfi::DevBuf<uint32_t> d_units, d_unit_off;  // sliced pass: uint4 work units per XCD
   uint32_t max_xcd_units = 0;
+  bool big = false;  // spf_big_kernel (whatif.hip): graphs beyond the LDS kernels
+  spfi::DevBuf<uint32_t> b_q, b_q2, b_bm, b_ctr, b_nbr_bit, b_nhb, b_lvl, b_order, b_misc, b_parent;
   spfi::DevBuf<uint64_t> d_nh_off;
   spfi::DevBuf<uint32_t> d_nb_row, d_nb_row_off, d_nb_drained;  // next-hop pass inputs
   uint32_t dead = 0;  // nb_row value of a drained neighbour
@@ -157,6 +159,11 @@ spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
 spf_status launch_exact(spf_ctx* c, const uint32_t* d_srcs, uint32_t n_src, const uint64_t* d_nh_off,
                         uint32_t Wmax, bool hop, bool dist64, const uint32_t* ign, void* d_dist,
                         uint32_t* d_nh, uint32_t* d_pop, hipStream_t s);
+// spf_big_kernel (whatif.hip): the plan's sources one after another on the
+// whole chip -- frontier SSSP into the dist rows, next hops in distance
+// order, transposed into the plan's bitmaps.  Positive metrics or hop counts.
+spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, bool hop,
+                      hipStream_t s);
 // Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
 spf_status set_lds_limits(spf_ctx* c);
 

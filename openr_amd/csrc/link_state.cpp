@@ -644,13 +644,27 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
                      m.pred_edge.data(), npred, &npred);
       if (st != SPF_OK) return eng_fail(ls, st);
     }
+    // next hops per destination from the per-neighbour bitmaps (bitmap j:
+    // destinations routed via neighbour j): set bits counted, then placed
+    // in neighbour order -- O(k * N/32 + bits), not O(k * N)
+    const uint32_t nw = (N + 31) / 32, nv = nw * 32;  // bitmap words / nodes they cover
+    std::vector<uint32_t> at(nv + 1, 0);
+    for (uint32_t j = 0; j < k; ++j)
+      for (uint32_t w = 0; w < nw; ++w)
+        for (uint32_t x = nh[(size_t)j * wpm + w]; x; x &= x - 1) ++at[w * 32 + __builtin_ctz(x) + 1];
+    for (uint32_t v = 0; v < nv; ++v) at[v + 1] += at[v];
+    std::vector<uint32_t> nh_of(at[nv]);
+    {
+      std::vector<uint32_t> fill(at.begin(), at.end() - 1);
+      for (uint32_t j = 0; j < k; ++j)
+        for (uint32_t w = 0; w < nw; ++w)
+          for (uint32_t x = nh[(size_t)j * wpm + w]; x; x &= x - 1) nh_of[fill[w * 32 + __builtin_ctz(x)]++] = j;
+    }
     for (uint32_t v = 0; v < N; ++v) {
       if (m.dist[v] == SPF_UNREACHABLE) continue;
       m.node.push_back(ls->csr_name[v]);
       m.metric.push_back(d64.empty() ? (uint64_t)m.dist[v] : d64[v]);
-      for (uint32_t j = 0; j < k; ++j)  // bitmap j: destinations routed via neighbour j
-        if ((nh[(size_t)j * wpm + (v >> 5)] >> (v & 31)) & 1u)
-          m.nh_node.push_back(ls->csr_name[nbr[j]]);
+      for (uint32_t t = at[v]; t < at[v + 1]; ++t) m.nh_node.push_back(ls->csr_name[nbr[nh_of[t]]]);
       m.nh_ptr.push_back((uint32_t)m.nh_node.size());
       for (uint32_t p = m.pred_ptr[v]; p < m.pred_ptr[v + 1]; ++p) {
         const uint32_t e = m.pred_edge[p];

@@ -261,10 +261,18 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
 //   beside F -- low-degree graphs such as grids), so the pull sweep issues no
 //   global loads: no vmcnt wait, and a level's stores drain in the background
 //   instead of stalling the next sweep's first column load.
+//   Level 0 is pushed, not pulled: its frontier is the batch's own sources,
+//   so each wave ORs its sources' bits into their neighbours' F entries
+//   (LDS 64-bit atomics over the sources' CSR rows) where a pull would sweep
+//   every column of the graph (~1/5 of a fabric batch's time, r02 stamps).
+//   Links are up in both directions or neither, so CSR out-neighbours are
+//   the in-neighbours the pull reads.  (Pushing later levels, whose
+//   frontiers live in the owners' registers, spilled msbfs_kernel<10>.)
 template <int OWN, bool LCOL>
 __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
-    uint32_t n_col, const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
+    uint32_t n_col, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+    const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
     uint32_t n_rows, uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch,
     uint32_t* __restrict__ D, uint8_t* __restrict__ Dn, uint32_t* __restrict__ maxd,
     unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
@@ -273,7 +281,8 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   uint32_t* o_node = reinterpret_cast<uint32_t*>(F + N + 1);   // [64] drained batch sources
   uint32_t* o_cnt = o_node + kMsBatch;                         // [1]
   uint32_t* flag = o_cnt + 1;                                  // [2] per-parity progress
-  uint16_t* lcol = reinterpret_cast<uint16_t*>(flag + 2);      // [n_col] (LCOL)
+  uint32_t* src_l = flag + 2;                                  // [64] the batch's sources
+  uint16_t* lcol = reinterpret_cast<uint16_t*>(src_l + kMsBatch);  // [n_col] (LCOL)
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t row0 = blockIdx.x * bs;  // bs <= 64 sources per workgroup
@@ -299,21 +308,42 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   }
   __syncthreads();
   if (tid < nb) {
-    const uint32_t src = rows_src[row0 + tid];
-    F[src] = 1ull << tid;  // sources of a batch are distinct
+    const uint32_t src = rows_src[row0 + tid];  // sources of a batch are distinct
+    src_l[tid] = src;
     if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
+    D[(size_t)(row0 + tid) * pitch + src] = 0;  // level 0
+    if (Dn) Dn[(size_t)(row0 + tid) * npitch + src] = 0;
+  }
+  // ---- level 1 by push: each source's bit ORed into its neighbours' F (a
+  // source expands even when drained), a wave per source ----
+  for (uint32_t b = tid >> 6; b < nb; b += kMsThreads / 64) {
+    const uint32_t u = rows_src[row0 + b];
+    const uint32_t e1 = row_ptr[u + 1];
+    for (uint32_t e = row_ptr[u] + lane; e < e1; e += 64)
+      atomicOr(reinterpret_cast<unsigned long long*>(&F[col[e]]), 1ull << b);
   }
   __syncthreads();
   const uint32_t n_osrc = *o_cnt;
+  // the part of mask x a drained node v may expand: its own source bit
+  auto own_bits = [&](uint32_t v, uint64_t x) {
+    uint64_t own = 0;
+    for (uint32_t k = 0; k < n_osrc; ++k)
+      if ((o_node[k] & 0xFFFFFFu) == v) own = 1ull << (o_node[k] >> 24);
+    return x & own;
+  };
 
   uint64_t vis[OWN], nv[OWN];
   uint32_t drained = 0;  // bit i: owned node i is drained
   uint32_t sb[OWN], sw[OWN];  // owned slice i: column base, width (wave-uniform)
+  uint64_t any1 = 0;
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     const uint32_t v = tid + i * kMsThreads;
-    nv[i] = v < N ? F[v] : 0ull;
-    vis[i] = nv[i];
+    uint64_t self = 0;  // v's own source bit, if v is one of the batch's sources
+    for (uint32_t b = 0; b < nb; ++b) self |= (uint64_t)(src_l[b] == v) << b;
+    nv[i] = v < N ? F[v] & ~self : 0ull;  // level 1
+    vis[i] = self | nv[i];
+    any1 |= nv[i];
     if (v < N && ovl[v]) drained |= 1u << i;
     const uint32_t slice = (tid - lane + i * kMsThreads) / kSliceW;
     const bool live = slice * kSliceW < N;
@@ -322,10 +352,19 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     sb[i] = __builtin_amdgcn_readfirstlane(b);
     sw[i] = __builtin_amdgcn_readfirstlane((e - b) / kSliceW);
   }
+  __syncthreads();  // every read of the pushed F is done
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const uint32_t v = tid + i * kMsThreads;
+    if (v < N) F[v] = ((drained >> i) & 1u) ? own_bits(v, nv[i]) : nv[i];
+  }
+  if (any1) flag[0] = 1;  // level 1 is not empty (flag[1] stays 0 for level 1's sweep)
+  __syncthreads();
+  const bool level1 = flag[0] != 0;  // read before level 1 resets flag[0]
 
   MS_STAMP();
   uint32_t last = 0;  // deepest level of the batch
-  for (uint32_t L = 0;; ++L) {
+  for (uint32_t L = 1; level1; ++L) {
     // ---- record level L: D[s][v] = L for every new (s, v) ----
     // per owned slice, only the sources with a new node in it (wave OR);
     // one store covers 64 consecutive nodes of one source row
@@ -371,9 +410,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       }
     }
     MS_STAMP();
-    // ---- pull sweep for level L+1 ----
     uint64_t any = 0;
     uint64_t nx[OWN];
+    // ---- pull sweep for level L+1 ----
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       nx[i] = 0;
@@ -423,12 +462,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const uint32_t v = tid + i * kMsThreads;
       if (v < N) {
         uint64_t f = nx[i];
-        if ((drained >> i) & 1u) {  // drained: expands only as its own source
-          uint64_t own = 0;
-          for (uint32_t k = 0; k < n_osrc; ++k)
-            if ((o_node[k] & 0xFFFFFFu) == v) own = 1ull << (o_node[k] >> 24);
-          f &= own;
-        }
+        if ((drained >> i) & 1u) f = own_bits(v, f);  // drained: expands only as its own source
         F[v] = f;
       }
       nv[i] = nx[i];
@@ -1505,12 +1539,19 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   // LDS-resident kernels
   const bool ms_ok = (hop || c->unit) && N <= kMsMaxNodes;
   const bool lds_ok = sssp_lds_bytes(N, c->pitch, c->big_nodes, N <= 65535) <= kMaxLds;
-  p->exact = d64 || (!hop && c->nonpos) || (!ms_ok && !lds_ok);
-  if (p->exact) {
+  p->exact = d64 || (!hop && c->nonpos);
+  // graphs beyond the LDS-resident kernels: the whole chip per source
+  // (spf_big_kernel); SPF_BIG=0 sends them to the exact kernel, SPF_BIG=1
+  // sends every plan it can take there (tests)
+  const char* be = std::getenv("SPF_BIG");
+  p->big = !p->exact && ((!ms_ok && !lds_ok) ? !(be && be[0] == '0') : (be && be[0] == '1'));
+  if (!ms_ok && !lds_ok && !p->big) p->exact = true;
+  if (p->exact || p->big) {
     p->closure = p->srcs;
     p->direct = true;
     p->ms = false;
     p->narrow = false;
+    p->sliced = false;
     p->nh_off.resize(n_src);
     p->words.resize(n_src);
     uint64_t off = 0;
@@ -1747,7 +1788,7 @@ uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->clos
 
 spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
-  *bfs = p->exact ? 3u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
+  *bfs = p->big ? 4u : p->exact ? 3u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
   *narrow = p->sliced ? 2u : p->narrow ? 1u : 0u;
   return SPF_OK;
 }
@@ -1783,6 +1824,11 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
   const spf_ctx* c = p->ctx;
   const uint64_t N = c->N, E = c->E, rows = p->closure.size();
   uint64_t bfs = 0;
+  if (p->big) {  // per source: the CSR a few sweeps (counted once), the row, scratch + bitmaps
+    *bfs_bytes = rows * (4ull * (N + 1) + 12ull * E + N + 4ull * c->pitch) + 4ull * p->nh_total;
+    *ecmp_bytes = 0;
+    return SPF_OK;
+  }
   if (p->exact) {  // per source: the CSR once, the labels, the outputs
     const uint64_t lab = (p->flags & SPF_FLAG_DIST64) ? 8ull : 4ull;
     *bfs_bytes = rows * (4ull * (N + 1) + 12ull * E + N + 17ull * N + lab * c->pitch) +
@@ -1882,7 +1928,7 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 
 namespace {
 
-size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (kMsBatch + 3); }
+size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (2 * kMsBatch + 3); }
 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
@@ -1897,12 +1943,14 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
   const uint32_t bs = std::min<uint32_t>(kMsBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
   if (lcol)
     hipLaunchKernelGGL((msbfs_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
-                       lds_col, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
-                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, maxd, c->d_stamps.p);
+                       lds_col, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_row_ptr.p, c->d_col.p,
+                       c->d_ovl.p, rows_src, rows, bs, c->N, c->pitch, c->npitch, D, Dn,
+                       maxd, c->d_stamps.p);
   else
     hipLaunchKernelGGL((msbfs_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
-                       lds, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_ovl.p, rows_src,
-                       rows, bs, c->N, c->pitch, c->npitch, D, Dn, maxd, c->d_stamps.p);
+                       lds, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_row_ptr.p, c->d_col.p,
+                       c->d_ovl.p, rows_src, rows, bs, c->N, c->pitch, c->npitch, D, Dn,
+                       maxd, c->d_stamps.p);
 }
 
 size_t planes_lds_bytes(uint32_t own) { return 8ull * own * kMsThreads + 4ull * (kPlBatch + 4); }
@@ -2066,16 +2114,17 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint32_t pitch = c->pitch;
   const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
-  if (p->exact) {
+  if (p->exact || p->big) {
     hipEvent_t* ev = nullptr;
     if (p->timing_cap) {
       ev = &p->ev[4 * (p->timing_n % p->timing_cap)];
       ++p->timing_n;
       HIP_TRY(c, hipEventRecord(ev[0], s));
     }
-    const spf_status st = launch_exact(c, p->d_srcs.p, p->n_src, p->d_nh_off.p, p->wmax, hop,
-                                       (p->flags & SPF_FLAG_DIST64) != 0, nullptr, d_dist, d_nh,
-                                       nullptr, s);
+    const spf_status st =
+        p->big ? launch_big(c, p, d_dist, d_nh, hop, s)
+               : launch_exact(c, p->d_srcs.p, p->n_src, p->d_nh_off.p, p->wmax, hop,
+                              (p->flags & SPF_FLAG_DIST64) != 0, nullptr, d_dist, d_nh, nullptr, s);
     if (st != SPF_OK) return st;
     if (ev)
       for (int e = 1; e < 4; ++e) HIP_TRY(c, hipEventRecord(ev[e], s));

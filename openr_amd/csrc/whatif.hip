@@ -88,7 +88,13 @@ struct WiGraph {
   const uint8_t* ovl;
   const uint32_t* nbr_bit;  // [N] j if v is the src's j-th distinct neighbour, else kInf
   uint32_t N, src, W;
+  uint32_t hop = 0;  // hop counts: every up link weighs 1 (useLinkMetric = false)
 };
+
+// directed weight of the edge reverse to e (tail -> head of the in-edge)
+__device__ __forceinline__ uint32_t in_w(const WiGraph& g, uint32_t e) {
+  return g.hop ? 1u : g.wt[g.rev[e]];
+}
 
 struct WiBase {
   const uint32_t* dist;  // [N] unfailed distances
@@ -223,7 +229,7 @@ __device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* di
     const uint32_t u = g.col[e];
     if (g.ovl[u] && u != g.src) continue;
     const uint32_t du = ld(&dist[u]);
-    if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
+    if (du == kInf || du + in_w(g, e) != dv) continue;
     if (u == g.src) {
       const uint32_t jb = g.nbr_bit[v];
       if ((jb >> 5) == j) acc |= 1u << (jb & 31);
@@ -242,7 +248,7 @@ __device__ __forceinline__ uint32_t first_tight_pred(const WiGraph& g, const uin
     const uint32_t u = g.col[e];
     if (g.ovl[u] && u != g.src) continue;
     const uint32_t du = ld(&dist[u]);
-    if (du != kInf && du + g.wt[g.rev[e]] == dv) return u;
+    if (du != kInf && du + in_w(g, e) == dv) return u;
   }
   return kInf;
 }
@@ -265,7 +271,7 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
         const uint32_t cu = g.col[e];
         if (!g.ovl[cu] || cu == g.src) {
           const uint32_t du = ld(&dist[cu]);
-          if (du != kInf && du + g.wt[g.rev[e]] == dv) u = cu;
+          if (du != kInf && du + in_w(g, e) == dv) u = cu;
         }
       }
       const uint64_t tight = __ballot(u != kInf);
@@ -288,11 +294,125 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
   }
 }
 
+// Next-hop bitsets nhb[v][W] of the SPF in `dist` (every distance final,
+// after coop_sssp): nodes bucketed by distance value and settled level by
+// level (every tight predecessor of a level-d node sits at a lower level)
+// when at most kMaxLevels distinct values occur, fixed-point sweeps of the
+// monotone union otherwise.  nhb must be zero and lvl[0..kLevelCap],
+// misc[0..7] zero on entry.  Returns whether the level path ran (then
+// lvl[d] = end of bucket d in `order`).  Starts and ends with a grid barrier.
+__device__ bool level_nh(cg::grid_group& grid, const WiGraph& g, const uint32_t* dist,
+                         uint32_t* nhb, uint32_t* lvl, uint32_t* order, uint32_t* misc,
+                         uint32_t* parent) {
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t N = g.N, W = g.W;
+  const uint64_t NW = (uint64_t)N * W;
+  grid.sync();
+  // ---- distance range and per-value counts ----
+  for (uint32_t v = gtid; v < N; v += gsz) {
+    const uint32_t d = ld(&dist[v]);
+    if (d != kInf) atomicMax(&misc[0], d);
+  }
+  grid.sync();
+  const uint32_t maxd = ld(&misc[0]);
+  bool levels = maxd < kLevelCap;
+  if (levels) {
+    for (uint32_t v = gtid; v < N; v += gsz) {
+      const uint32_t d = ld(&dist[v]);
+      if (d != kInf && atomicAdd(&lvl[d], 1u) == 0) atomicAdd(&misc[1], 1u);
+    }
+    grid.sync();
+    levels = ld(&misc[1]) <= kMaxLevels;
+  }
+  if (levels) {
+    // exclusive scan of the counts by block 0 (maxd + 1 <= kLevelCap entries)
+    if (blockIdx.x == 0) {
+      __shared__ uint32_t carry;
+      if (threadIdx.x == 0) carry = 0;
+      __syncthreads();
+      for (uint32_t base = 0; base <= maxd; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t x = i <= maxd ? ld(&lvl[i]) : 0u;
+        // block scan through LDS
+        __shared__ uint32_t buf[kCoopThreads];
+        buf[threadIdx.x] = x;
+        __syncthreads();
+        for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
+          const uint32_t y = threadIdx.x >= d ? buf[threadIdx.x - d] : 0u;
+          __syncthreads();
+          buf[threadIdx.x] += y;
+          __syncthreads();
+        }
+        const uint32_t incl = buf[threadIdx.x] + carry;
+        if (i <= maxd) st(&lvl[i], incl - x);
+        __syncthreads();
+        if (threadIdx.x == blockDim.x - 1) carry = incl;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) st(&lvl[maxd + 1], carry);
+    }
+    grid.sync();
+    // scatter nodes into distance order (lvl[d] advances to the bucket end)
+    for (uint32_t v = gtid; v < N; v += gsz) {
+      const uint32_t d = ld(&dist[v]);
+      if (d != kInf) st(&order[atomicAdd(&lvl[d], 1u)], v);
+    }
+    grid.sync();
+    // level by level: every predecessor of a level-d node sits at a lower level
+    uint32_t begin = ld(&lvl[0]);  // bucket 0 (the source) ends here
+    for (uint32_t d = 1; d <= maxd; ++d) {
+      const uint32_t end = ld(&lvl[d]);
+      if (end == begin) continue;  // empty level: uniform skip
+      const uint64_t items = (uint64_t)(end - begin) * W;
+      for (uint64_t b = gtid - lane; b < items; b += gsz) {  // wave-uniform
+        const uint64_t x = b + lane;
+        uint32_t v = 0, j = 0;
+        bool hub = false;
+        if (x < items) {
+          v = ld(&order[begin + (uint32_t)(x / W)]);
+          j = (uint32_t)(x % W);
+          hub = g.row_ptr[v + 1] - g.row_ptr[v] > kCoopHubDeg;
+          if (!hub) {
+            st(&nhb[(size_t)v * W + j], nh_word(g, dist, nhb, v, j));
+            if (j == 0) st(&parent[v], first_tight_pred(g, dist, v));
+          }
+        }
+        // a hub's W words are made once, by the wave, at its j = 0 item
+        for (uint64_t hubs = __ballot(hub && j == 0); hubs; hubs &= hubs - 1)
+          hub_nh(g, dist, nhb, parent, __shfl(v, __builtin_ctzll(hubs), 64), lane);
+      }
+      begin = end;
+      grid.sync();
+    }
+  } else {
+    // fixed-point sweeps (monotone union over the DAG), flags rotate by 3
+    for (uint32_t it = 0;; ++it) {
+      bool any = false;
+      for (uint64_t x = gtid; x < NW; x += gsz) {
+        const uint32_t v = (uint32_t)(x / W), j = (uint32_t)(x % W);
+        if (v == g.src || ld(&dist[v]) == kInf) continue;
+        const uint32_t acc = nh_word(g, dist, nhb, v, j);
+        if (acc != ld(&nhb[x])) {
+          st(&nhb[x], acc);
+          any = true;
+        }
+      }
+      if (any) st(&misc[2 + it % 3], 1u);
+      if (gtid == 0) st(&misc[2 + (it + 1) % 3], 0u);
+      grid.sync();
+      if (!ld(&misc[2 + it % 3])) break;
+    }
+  }
+  grid.sync();
+  return levels;
+}
+
 __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
   cg::grid_group grid = cg::this_grid();
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
-  const uint32_t lane = threadIdx.x & 63;
   const WiGraph& g = a.g;
   const uint32_t N = g.N, W = g.W;
   const uint64_t NW = (uint64_t)N * W;
@@ -308,82 +428,9 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
   coop_sssp(grid, a.sp);  // starts and ends with a grid barrier
   if (stamp) a.prof[1] = wall_clock64();
   const uint32_t* dist = a.sp.dist;
-  // ---- distance range and per-value counts ----
-  for (uint32_t v = gtid; v < N; v += gsz) {
-    const uint32_t d = ld(&dist[v]);
-    if (d != kInf) atomicMax(&a.misc[0], d);
-  }
-  grid.sync();
-  const uint32_t maxd = ld(&a.misc[0]);
-  bool levels = maxd < kLevelCap;
+  const bool levels = level_nh(grid, g, dist, a.nhb, a.lvl, a.order, a.misc, a.parent);
   if (levels) {
-    for (uint32_t v = gtid; v < N; v += gsz) {
-      const uint32_t d = ld(&dist[v]);
-      if (d != kInf && atomicAdd(&a.lvl[d], 1u) == 0) atomicAdd(&a.misc[1], 1u);
-    }
-    grid.sync();
-    levels = ld(&a.misc[1]) <= kMaxLevels;
-  }
-  if (levels) {
-    // exclusive scan of the counts by block 0 (maxd + 1 <= kLevelCap entries)
-    if (blockIdx.x == 0) {
-      __shared__ uint32_t carry;
-      if (threadIdx.x == 0) carry = 0;
-      __syncthreads();
-      for (uint32_t base = 0; base <= maxd; base += blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t x = i <= maxd ? ld(&a.lvl[i]) : 0u;
-        // block scan through LDS
-        __shared__ uint32_t buf[kCoopThreads];
-        buf[threadIdx.x] = x;
-        __syncthreads();
-        for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
-          const uint32_t y = threadIdx.x >= d ? buf[threadIdx.x - d] : 0u;
-          __syncthreads();
-          buf[threadIdx.x] += y;
-          __syncthreads();
-        }
-        const uint32_t incl = buf[threadIdx.x] + carry;
-        if (i <= maxd) st(&a.lvl[i], incl - x);
-        __syncthreads();
-        if (threadIdx.x == blockDim.x - 1) carry = incl;
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) st(&a.lvl[maxd + 1], carry);
-    }
-    grid.sync();
-    // scatter nodes into distance order (lvl[d] advances to the bucket end)
-    for (uint32_t v = gtid; v < N; v += gsz) {
-      const uint32_t d = ld(&dist[v]);
-      if (d != kInf) st(&a.order[atomicAdd(&a.lvl[d], 1u)], v);
-    }
-    grid.sync();
-    // level by level: every predecessor of a level-d node sits at a lower level
-    uint32_t begin = ld(&a.lvl[0]);  // bucket 0 (the source) ends here
-    for (uint32_t d = 1; d <= maxd; ++d) {
-      const uint32_t end = ld(&a.lvl[d]);
-      if (end == begin) continue;  // empty level: uniform skip
-      const uint64_t items = (uint64_t)(end - begin) * W;
-      for (uint64_t b = gtid - lane; b < items; b += gsz) {  // wave-uniform
-        const uint64_t x = b + lane;
-        uint32_t v = 0, j = 0;
-        bool hub = false;
-        if (x < items) {
-          v = ld(&a.order[begin + (uint32_t)(x / W)]);
-          j = (uint32_t)(x % W);
-          hub = g.row_ptr[v + 1] - g.row_ptr[v] > kCoopHubDeg;
-          if (!hub) {
-            st(&a.nhb[(size_t)v * W + j], nh_word(g, dist, a.nhb, v, j));
-            if (j == 0) st(&a.parent[v], first_tight_pred(g, dist, v));
-          }
-        }
-        // a hub's W words are made once, by the wave, at its j = 0 item
-        for (uint64_t hubs = __ballot(hub && j == 0); hubs; hubs &= hubs - 1)
-          hub_nh(g, dist, a.nhb, a.parent, __shfl(v, __builtin_ctzll(hubs), 64), lane);
-      }
-      begin = end;
-      grid.sync();
-    }
+    const uint32_t maxd = ld(&a.misc[0]);
     // subtree sizes of the parent tree, deepest level first: a lower bound
     // on the DAG descendants a failure of the tree edge into v can change,
     // used to hand big repairs to workgroup teams up front
@@ -399,24 +446,6 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
         if (pu != kInf) atomicAdd(&a.sub[pu], ld(&a.sub[v]));
       }
       grid.sync();
-    }
-  } else {
-    // fixed-point sweeps (monotone union over the DAG), flags rotate by 3
-    for (uint32_t it = 0;; ++it) {
-      bool any = false;
-      for (uint64_t x = gtid; x < NW; x += gsz) {
-        const uint32_t v = (uint32_t)(x / W), j = (uint32_t)(x % W);
-        if (v == g.src || ld(&dist[v]) == kInf) continue;
-        const uint32_t acc = nh_word(g, dist, a.nhb, v, j);
-        if (acc != ld(&a.nhb[x])) {
-          st(&a.nhb[x], acc);
-          any = true;
-        }
-      }
-      if (any) st(&a.misc[2 + it % 3], 1u);
-      if (gtid == 0) st(&a.misc[2 + (it + 1) % 3], 0u);
-      grid.sync();
-      if (!ld(&a.misc[2 + it % 3])) break;
     }
   }
   if (stamp) {
@@ -445,6 +474,88 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
   }
   if ((threadIdx.x & 63) == 0 && (lo | hi)) atomicAdd(a.H, ((unsigned long long)hi << 32) | lo);
   if (stamp) a.prof[3] = wall_clock64();
+}
+
+// ---------------------------------------------------------------------------
+//  batched SPF + next hops beyond the LDS-resident kernels (plans on graphs
+//  too large for them, positive metrics or hop counts)
+// ---------------------------------------------------------------------------
+// One cooperative launch walks the plan's sources one after another, the
+// whole chip on each: frontier SSSP straight into the source's output row
+// (coop_sssp), next hops per node in distance order (level_nh, node-major
+// scratch nhb[v][W]), then a transpose into the plan's bitmap layout (bit v
+// of word v/32 of neighbour j's bitmap): a wave holds the scratch word w of
+// 64 consecutive nodes, one ballot per bit j of it is the 64-node slice of
+// bitmap 32w + j, and lanes 0..31 store the 32 slices as 8-byte words.
+struct BigArgs {
+  CoopSssp sp;  // src and dist set per source
+  WiGraph g;    // src, W set per source; g.nbr_bit = nbr_bit below
+  const uint32_t* srcs;
+  uint32_t n_src;
+  const uint32_t* nb_ptr;  // distinct up neighbours (ascending id)
+  const uint32_t* nb_id;
+  uint32_t* D;  // [n_src][pitch] output rows
+  uint32_t pitch;
+  uint32_t* nh;  // output bitmaps
+  const uint64_t* nh_off;
+  uint32_t* nbr_bit;  // [N] scratch, kInf between sources
+  uint32_t* nhb;      // [N][W] scratch
+  uint32_t* lvl;      // [kLevelCap + 1]
+  uint32_t* order;    // [N]
+  uint32_t* misc;     // [8]
+  uint32_t* parent;   // [N]
+};
+
+__global__ __launch_bounds__(kCoopThreads) void spf_big_kernel(BigArgs a) {
+  cg::grid_group grid = cg::this_grid();
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t N = a.g.N, wpm = a.pitch / 32;
+  for (uint32_t i = 0; i < a.n_src; ++i) {
+    const uint32_t s = a.srcs[i];
+    const uint32_t nb0 = a.nb_ptr[s], k = a.nb_ptr[s + 1] - nb0;
+    const uint32_t W = k ? (k + 31) / 32 : 1u;
+    WiGraph g = a.g;
+    g.src = s;
+    g.W = W;
+    CoopSssp sp = a.sp;
+    sp.src = s;
+    sp.dist = a.D + (size_t)i * a.pitch;
+    // per-source state (the previous source's readers finished at its last barrier)
+    for (uint32_t j = gtid; j < k; j += gsz) st(&a.nbr_bit[a.nb_id[nb0 + j]], j);
+    const uint64_t NW = (uint64_t)N * W;
+    for (uint64_t x = gtid; x < NW; x += gsz) st(&a.nhb[x], 0u);
+    for (uint32_t d = gtid; d <= kLevelCap; d += gsz) st(&a.lvl[d], 0u);
+    if (gtid < 8) st(&a.misc[gtid], 0u);
+    for (uint32_t v = N + gtid; v < a.pitch; v += gsz) st(&sp.dist[v], kInf);  // row padding
+    coop_sssp(grid, sp);  // starts and ends with a grid barrier
+    level_nh(grid, g, sp.dist, a.nhb, a.lvl, a.order, a.misc, a.parent);
+    // transpose into the plan's bitmaps: items (64-node group, scratch word)
+    if (k) {
+      uint32_t* out = a.nh + a.nh_off[i];
+      const uint32_t groups = a.pitch / 64;
+      const uint64_t items = (uint64_t)groups * W;
+      for (uint64_t t = (gtid >> 6); t < items; t += gsz / 64) {  // a wave per item
+        const uint32_t grp = (uint32_t)(t / W), w = (uint32_t)(t % W);
+        const uint32_t v = grp * 64 + lane;
+        const uint32_t x = v < N ? ld(&a.nhb[(size_t)v * W + w]) : 0u;
+        uint64_t mine = 0;
+#pragma unroll 4
+        for (uint32_t jj = 0; jj < 32; ++jj) {
+          const uint64_t m = __ballot((x >> jj) & 1u);
+          if (lane == jj) mine = m;
+        }
+        const uint32_t j = w * 32 + lane;
+        if (lane < 32 && j < k) {
+          uint2* o = reinterpret_cast<uint2*>(out + (size_t)j * wpm + grp * 2);
+          *o = make_uint2((uint32_t)mine, (uint32_t)(mine >> 32));
+        }
+      }
+    }
+    for (uint32_t j = gtid; j < k; j += gsz) st(&a.nbr_bit[a.nb_id[nb0 + j]], kInf);
+    grid.sync();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -636,7 +747,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.ovl[u] && u != g.src) continue;
       const uint32_t mu = ldw(&mark[u]);
       const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
-      if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
+      if (du == kInf || du + in_w(g, e) != dv) continue;
       if (u == g.src) {
         const uint32_t jb = g.nbr_bit[v];
         if ((jb >> 5) == j) acc |= 1u << (jb & 31);
@@ -656,7 +767,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.ovl[u] && u != g.src) continue;
       const uint32_t mu = ldw(&mark[u]);
       const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
-      if (du == kInf || du + g.wt[g.rev[e]] != dv) continue;
+      if (du == kInf || du + in_w(g, e) != dv) continue;
       if (u == g.src) {
         const uint32_t jb = g.nbr_bit[v];
         row[jb >> 5] |= 1u << (jb & 31);
@@ -1012,6 +1123,35 @@ spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
              hop ? 1u : 0u, dist, c->d_gq.p, c->d_gq2.p, c->d_gbm.p, c->d_gctr.p};
   void* args[] = {&a};
   HIP_TRY(c, hipLaunchCooperativeKernel((const void*)gsssp_coop_kernel, dim3(coop_blocks(c)),
+                                        dim3(kCoopThreads), args, 0, s));
+  return SPF_OK;
+}
+
+spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, bool hop,
+                      hipStream_t s) {
+  const uint32_t N = c->N;
+  HIP_TRY(c, p->b_q.alloc(N));
+  HIP_TRY(c, p->b_q2.alloc(N));
+  HIP_TRY(c, p->b_bm.alloc((N + 31) / 32));
+  HIP_TRY(c, p->b_ctr.alloc(4));
+  if (!p->b_nbr_bit.p) {
+    HIP_TRY(c, p->b_nbr_bit.alloc(N));
+    HIP_TRY(c, hipMemsetAsync(p->b_nbr_bit.p, 0xFF, 4ull * N, s));
+  }
+  HIP_TRY(c, p->b_nhb.alloc((size_t)N * p->wmax));
+  HIP_TRY(c, p->b_lvl.alloc(kLevelCap + 1));
+  HIP_TRY(c, p->b_order.alloc(N));
+  HIP_TRY(c, p->b_misc.alloc(8));
+  HIP_TRY(c, p->b_parent.alloc(N));
+  WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
+            p->b_nbr_bit.p, N, 0u, 1u, hop ? 1u : 0u};
+  BigArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr, N,
+                     0u, hop ? 1u : 0u, d_dist, p->b_q.p, p->b_q2.p, p->b_bm.p, p->b_ctr.p},
+            g, p->d_srcs.p, p->n_src, c->d_nb_ptr.p, c->d_nb_id.p, d_dist, c->pitch, d_nh,
+            p->d_nh_off.p, p->b_nbr_bit.p, p->b_nhb.p, p->b_lvl.p, p->b_order.p, p->b_misc.p,
+            p->b_parent.p};
+  void* args[] = {&a};
+  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)spf_big_kernel, dim3(coop_blocks(c)),
                                         dim3(kCoopThreads), args, 0, s));
   return SPF_OK;
 }

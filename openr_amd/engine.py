@@ -84,7 +84,8 @@ class SpfPlan(NativeHandle):
         self._eng._err(N.lib.spf_plan_execute_host(self._h, N.ptr(dist), N.ptr(nh)))
         return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
 
-    BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel")
+    BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel",
+                   "spf_big_kernel")
     ROW_MODES = ("u32", "u8", "sliced")
 
     def kernels(self) -> Tuple[str, bool]:
@@ -107,7 +108,7 @@ class SpfPlan(NativeHandle):
         row slicing, next-hop pass); None where a phase launches nothing."""
         bfs, narrow = self._kernel_codes()
         name = self.BFS_KERNELS[bfs]
-        if bfs == 3 or not self.nh_words:
+        if bfs >= 3 or not self.nh_words:  # exact / big kernels: next hops inside
             return name, None, None
         if narrow == 2:
             return name, "slice_rows_kernel", "ecmp_sliced_kernel"

@@ -121,6 +121,7 @@ def test_zero_metric_runs_the_exact_kernel():
     assert eng.plan([0], hop=True).kernels()[0] != "exact_spf_kernel"
     compare(names, eng, orc, list(range(len(names))))
     compare(names, eng, orc, list(range(len(names))), hop=True)
+    compare(names, eng, orc, [3, 1, 3, 0])  # unsorted, duplicated sources
 
 
 ROW_MODES = {"0": "u32", "1": "u8", "2": "sliced"}
@@ -190,3 +191,17 @@ def test_bfs_variants_exact(name, make, variant, monkeypatch):
     for narrow in ("0", "1", "2"):
         monkeypatch.setenv("SPF_NARROW", narrow)
         compare(names, eng, orc, list(range(len(names))), hop=True)
+
+
+@pytest.mark.parametrize("name,make", SMALL, ids=[n for n, _ in SMALL])
+def test_big_graph_kernel_exact(name, make, monkeypatch):
+    """spf_big_kernel (the plans on graphs beyond the LDS-resident kernels:
+    cooperative frontier SSSP, next hops in distance order, transpose to the
+    bitmap layout) forced onto small graphs (SPF_BIG=1), every source,
+    weighted and hop counts, against the oracle."""
+    monkeypatch.setenv("SPF_BIG", "1")
+    names, eng, orc = load(make())
+    assert eng.plan([0]).kernels()[0] == "spf_big_kernel"
+    compare(names, eng, orc, list(range(len(names))))
+    compare(names, eng, orc, list(range(len(names))), hop=True)
+    compare(names, eng, orc, [3, 1, 3, 0])  # unsorted, duplicated sources

@@ -113,13 +113,21 @@ def test_whatif_ba250k_16k_failures_match_oracle():
     assert int(g["n_nh_changed"].max()) > 50_000
 
 
-def test_large_graph_spf_ecmp_ba250k_matches_oracle():
-    """N2: batched SPF + ECMP next hops beyond the LDS-resident kernels."""
+@pytest.mark.parametrize("big", ["1", "0"], ids=["big_kernel", "exact_kernel"])
+def test_large_graph_spf_ecmp_ba250k_matches_oracle(big, monkeypatch):
+    """N2: batched SPF + ECMP next hops beyond the LDS-resident kernels, on
+    spf_big_kernel (the default) and on the exact kernel (SPF_BIG=0; 16 of
+    the sources, it is the slow envelope)."""
+    monkeypatch.setenv("SPF_BIG", big)
     meta, g = golden("ba250k_spf")
     ls, names, csr, cd = _make("ba250k_spf")
     assert cd == meta["csr_digest"]
-    srcs = g["srcs"]
+    n = len(g["srcs"]) if big == "1" else 16
+    srcs = g["srcs"][:n]
     with _engine(csr) as eng:
+        p = eng.plan(srcs)
+        assert p.kernels()[0] == ("spf_big_kernel" if big == "1" else "exact_spf_kernel")
+        p.close()
         res = eng.solve(srcs)
         got = digest_planar(res.dist, res.nh, res.nh_off, res.words, res.pitch)
-    _report(got, g["digest"], "ba250k per-source digests", [names[int(s)] for s in srcs])
+    _report(got, g["digest"][:n], "ba250k per-source digests", [names[int(s)] for s in srcs])
