@@ -664,8 +664,11 @@ def main() -> None:
                     traffic = kv["fetch_bytes_x2"] + kv["write_bytes"]
                     traffic_src = (f"{pmc.relative_to(ROOT)} ({pj.get('source', 'rocprofv3 --pmc')}"
                                    f"; kernel {kname}; FETCH_SIZE x2 + WRITE_SIZE)")
-        except Exception:  # noqa: BLE001
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: no PMC traffic from {pmc}: {e!r}", file=sys.stderr)
             traffic = None
+    elif rank == 0:
+        print(f"bench: {pmc} not found: roofline.traffic is null", file=sys.stderr)
 
     out = {
         "metric": METRIC if isinstance(wl, AllSources) else (

@@ -274,8 +274,11 @@ spf_status spf_ksp2_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
  *                   mod 2^64, mix = splitmix64's finaliser, nh(v) = bitset over
  *                   the distinct up neighbours of src in the unfailed graph
  *                   (ascending id), ceil(k/32) words.
- * The unfailed result's digest is {0, 0, hash}.  Works on graphs of any size
- * (global-memory kernels); weighted metrics must be positive. */
+ * The unfailed result's digest is {0, 0, hash}.  Global-memory kernels, no
+ * LDS size limit: repair scratch is sized from fixed HBM budgets (4 GB of
+ * wave teams, 8 GB of workgroup teams, fewer teams on bigger graphs) plus
+ * O(N) per plan; an allocation failure returns SPF_E_NOMEM.  Weighted
+ * metrics must be positive. */
 typedef struct spf_whatif_digest {
   uint32_t n_dist_changed;
   uint32_t n_nh_changed;

@@ -135,7 +135,8 @@ spf_status fail(spf_ctx* c, spf_status st, const char* fmt, ...);
   do {                                                                       \
     const hipError_t e_ = (expr);                                            \
     if (e_ != hipSuccess)                                                    \
-      return fail(ctx, SPF_E_HIP, "%s: %s (%s:%d)", #expr,                   \
+      return fail(ctx, e_ == hipErrorOutOfMemory ? SPF_E_NOMEM : SPF_E_HIP,   \
+                  "%s: %s (%s:%d)", #expr,                                   \
                   hipGetErrorString(e_), __FILE__, __LINE__);                \
   } while (0)
 

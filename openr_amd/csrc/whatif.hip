@@ -46,7 +46,8 @@ namespace {
 
 constexpr uint32_t kBusy = 0xFFFFFFFEu;
 constexpr uint32_t kWaveCap = 1024;            // |D| a wave team can hold
-constexpr size_t kBigScratch = 8ull << 30;     // HBM budget of the workgroup teams
+constexpr size_t kBigScratch = 8ull << 30;     // HBM budget of the workgroup teams (both sets)
+constexpr size_t kWaveScratch = 4ull << 30;    // HBM budget of the wave teams
 constexpr uint32_t kDialLevels = 1024;         // distinct distances settled bucket by bucket
 constexpr uint32_t kHubDeg = 32;               // nodes above this degree get a whole wave
 
@@ -791,8 +792,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       }
     }
   };
-  const uint32_t nw = n * W;
-  for (uint32_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
+  const size_t nw = (size_t)n * W;
+  for (size_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
   if (tt == 0) {
     ctl->dmin = kInf;
     ctl->nxt[0] = kInf;
@@ -918,8 +919,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (!ctl->flag[it % 3]) break;
     }
 
-    const uint32_t nw = n * W;
-    for (uint32_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
+    const size_t nw = (size_t)n * W;
+    for (size_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
     if (tt == 0) {
       ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
       ctl->dmin = kInf;
@@ -970,9 +971,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       for (uint32_t b = 0; b < nlev; ++b) {
         const uint32_t end = ldw(&lvl[b]);
         if (end == begin) continue;
-        const uint32_t items = (end - begin) * W;
-        for (uint32_t x = tt; x < items; x += TEAM) {
-          const uint32_t i = ldw(&ord[begin + x / W]), j = x % W;
+        const size_t items = (size_t)(end - begin) * W;
+        for (size_t x = tt; x < items; x += TEAM) {
+          const uint32_t i = ldw(&ord[begin + x / W]), j = (uint32_t)(x % W);
           nhn[(size_t)i * W + j] = nh_of(i, j);
         }
         begin = end;
@@ -1194,7 +1195,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   const uint32_t k = c->nb_ptr[src + 1] - c->nb_ptr[src];
   for (uint32_t j = 0; j < k; ++j) nbr_bit[c->nb_id[c->nb_ptr[src] + j]] = j;
   p->W = std::max<uint32_t>(1, (k + 31) / 32);
-  p->wave_teams = 4 * 2 * c->n_cu;
+  {  // wave teams: 8 per CU (2 waves per SIMD) within the scratch budget
+    const size_t per_team = 4ull * (N + kWaveCap * (4ull + p->W) + kWaveCap + 1);
+    const size_t fit = std::max<size_t>(4, kWaveScratch / per_team) & ~size_t(3);
+    p->wave_teams = (uint32_t)std::min<size_t>(4ull * 2 * c->n_cu, fit);
+  }
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, p->d_fails.upload(fails.data(), fails.size(), c->stream));
   HIP_TRY(c, p->d_link_edge.upload(link_edge.data(), link_edge.size(), c->stream));
@@ -1227,9 +1232,9 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->w_nhn.alloc(wt * kWaveCap * p->W));
   HIP_TRY(c, p->w_lvl.alloc(wt * (kWaveCap + 1)));
   HIP_TRY(c, p->w_ord.alloc(wt * 2 * kWaveCap));
-  {  // workgroup teams: one per CU within the scratch budget
+  {  // workgroup teams: one per CU, two sets (b_*, c_*) within the scratch budget
     const size_t per_team = 4ull * ((size_t)N * (6 + p->W) + 1);
-    p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / per_team));
+    p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / 2 / per_team));
   }
   const size_t bt = p->big_teams;
   HIP_TRY(c, p->b_mark.alloc(bt * N));

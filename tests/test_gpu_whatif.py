@@ -79,6 +79,41 @@ def test_whatif_explicit_link_list_and_drained_source():
     assert [as_tuple(d) for d in got] == want
 
 
+WIDE = [
+    # U[1, 1000] metrics on a 3000-node WAN: the big repairs hold far more than
+    # kDialLevels (1024) distinct distances, so the workgroup teams leave the
+    # Dial loop for label-correcting sweeps + the level sort (whatif.hip:899-980)
+    ("wan3000_m1e3", lambda: T.wan(3000, 1500, seed=2), 1_000),
+    # U[1, 1e5]: the unfailed distances pass kLevelCap (65536), so the base
+    # pass takes its fixed-point path (whatif.hip:321) and the repairs' level
+    # span exceeds their cap (fixed-point sweeps, whatif.hip:981)
+    ("wan1500_m1e5", lambda: T.wan(1500, 800, seed=3, max_metric=100_000), 100_000),
+]
+
+
+@pytest.mark.parametrize("name,make,max_metric", WIDE, ids=[w[0] for w in WIDE])
+def test_whatif_wide_metrics_fallback_paths(name, make, max_metric):
+    """graphs whose distances leave the bucketed (levels / Dial)
+    paths; the hottest failures plus a random sample, each against the
+    oracle's full re-run."""
+    ls, names, eng, orc, _ = setup(make())
+    s = 0
+    links, got, base = eng.whatif(s)
+    d = eng.sssp(s)
+    if max_metric >= 65536:
+        assert int(d[d != 0xFFFFFFFF].max()) >= 65536  # base: non-levels path
+    size = got["n_dist_changed"].astype(np.int64)
+    assert size.max() > 1024  # a repair beyond the Dial level budget
+    order = np.argsort(-size)
+    rng = np.random.default_rng(3)
+    pick = list(order[:12]) + list(rng.choice(len(links), 120, replace=False))
+    obase, want = whatif_digests(orc, NameTable(names), names[s],
+                                 [fail_of(ls, links[i]) for i in pick])
+    assert as_tuple(base) == obase
+    for i, w in zip(pick, want):
+        assert as_tuple(got[i]) == w, (name, fail_of(ls, links[i]))
+
+
 @pytest.fixture(scope="module")
 def ba250k():
     return setup(T.barabasi_albert(250_000, 4, seed=1))
