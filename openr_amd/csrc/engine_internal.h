@@ -78,6 +78,7 @@ struct spf_ctx {
   uint32_t npitch = 0;                       // narrow (u8) row pitch
   std::vector<uint32_t> sell_ptr, sell_col;  // sliced-ELL columns (64-node slices)
   spfi::DevBuf<uint32_t> d_sell_ptr, d_sell_col;
+  spfi::DevBuf<uint32_t> d_ms_smap;  // msbfs_kernel: slice of (wave, slot), balanced by width
   std::vector<uint32_t> sell4_ptr, sell4;  // packed u16x4 columns (uint2 entries), planes BFS
   spfi::DevBuf<uint32_t> d_sell4_ptr, d_sell4;
   spfi::DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
@@ -100,6 +101,8 @@ struct spf_plan {
   bool ms = false;      // unit metrics: multi-source BFS
   bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
   bool sliced = false;  // ... and the next-hop pass on its bit-sliced form
+  bool expand = false;  // ... the u32 rows expanded from the u8 ones (BFS stores bytes only)
+  bool any_drained_nb = false;  // some source has a drained neighbour (next-hop pass reads D)
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;

@@ -241,6 +241,14 @@ constexpr uint32_t kMsMaxNodes = kMsThreads * kMsMaxOwn;  // 16384 (F: 128 KiB o
 constexpr int kMsUnroll = 8;
 constexpr uint32_t kMsLaneStoreRatio = 4;  // per-lane stores when 4 * max per-node count < #sources
 constexpr uint32_t kSliceW = 64;  // nodes per sliced-ELL slice (= wave width)
+constexpr uint32_t kNoSlice = 0x03FFFFFFu;  // unused slot: its nodes (kNoSlice * 64 + lane) lie past N
+
+// owned slots per thread of msbfs_kernel (the template instances: 1, 2, 4, 8,
+// 10, 12, 16) for an N-node graph
+inline uint32_t ms_own(uint32_t N) {
+  const uint32_t own = (N + kMsThreads - 1) / kMsThreads;
+  return own <= 1 ? 1 : own <= 2 ? 2 : own <= 4 ? 4 : own <= 8 ? 8 : own <= 10 ? 10 : own <= 12 ? 12 : 16;
+}
 
 // Narrow (u8) distance rows: npitch bytes (a multiple of 1024), node v at
 // byte v -- a level's stores are 64 consecutive bytes per (source, slice),
@@ -268,21 +276,25 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
 //   Links are up in both directions or neither, so CSR out-neighbours are
 //   the in-neighbours the pull reads.  (Pushing later levels, whose
 //   frontiers live in the owners' registers, spilled msbfs_kernel<10>.)
-template <int OWN, bool LCOL>
+template <int OWN, bool LCOL, bool DB = false>
 __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ sell_col,
     uint32_t n_col, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src,
     uint32_t n_rows, uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch,
     uint32_t* __restrict__ D, uint8_t* __restrict__ Dn, uint32_t* __restrict__ maxd,
+    uint32_t d_from, const uint32_t* __restrict__ smap,
     unsigned long long* __restrict__ stamps /* diagnostics, usually null */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* F = reinterpret_cast<uint64_t*>(smem);             // [N + 1]
-  uint32_t* o_node = reinterpret_cast<uint32_t*>(F + N + 1);   // [64] drained batch sources
+  uint64_t* F2 = F + (DB ? N + 1 : 0);                         // [N + 1] (DB) second frontier
+  uint32_t* o_node = reinterpret_cast<uint32_t*>(F2 + N + 1);  // [64] drained batch sources
   uint32_t* o_cnt = o_node + kMsBatch;                         // [1]
-  uint32_t* flag = o_cnt + 1;                                  // [2] per-parity progress
-  uint32_t* src_l = flag + 2;                                  // [64] the batch's sources
-  uint16_t* lcol = reinterpret_cast<uint16_t*>(src_l + kMsBatch);  // [n_col] (LCOL)
+  uint32_t* flag = o_cnt + 1;                                  // [3] progress flags
+  uint32_t* src_l = flag + 3;                                  // [64] the batch's sources
+  uint32_t* e_base = src_l + kMsBatch;                         // [64] their first CSR edge
+  uint32_t* e_pre = e_base + kMsBatch;                         // [65] degree prefix sums
+  uint16_t* lcol = reinterpret_cast<uint16_t*>(e_pre + kMsBatch + 1);  // [n_col] (LCOL)
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t row0 = blockIdx.x * bs;  // bs <= 64 sources per workgroup
@@ -290,7 +302,8 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
   // diagnostics: lane 0 of every wave of workgroup 0 logs phase clocks into
   // stamps[wave * 64 + 1 ..], the count into stamps[wave * 64]
-  const bool stamp = stamps && blockIdx.x == 0 && lane == 0;
+  // (the workgroup logged: stamps[1024], SPF_STAMPS=<workgroup>)
+  const bool stamp = stamps && blockIdx.x == (uint32_t)stamps[64 * 16] && lane == 0;
   unsigned long long* my_stamps = stamps + (tid >> 6) * 64;
   uint32_t n_stamp = 0;
 #define MS_STAMP()                                                   \
@@ -302,25 +315,32 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   for (uint32_t v = tid; v <= N; v += kMsThreads) F[v] = 0;
   if (LCOL)
     for (uint32_t t = tid; t < n_col; t += kMsThreads) lcol[t] = (uint16_t)sell_col[t];
+  if (DB)
+    for (uint32_t v = N + tid; v <= N; v += kMsThreads) F2[v] = 0;  // the padding target
   if (tid == 0) {
     *o_cnt = 0;
-    flag[0] = flag[1] = 0;
+    flag[0] = flag[1] = flag[2] = 0;
   }
   __syncthreads();
-  if (tid < nb) {
-    const uint32_t src = rows_src[row0 + tid];  // sources of a batch are distinct
-    src_l[tid] = src;
-    if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
-    D[(size_t)(row0 + tid) * pitch + src] = 0;  // level 0
-    if (Dn) Dn[(size_t)(row0 + tid) * npitch + src] = 0;
-  }
-  // ---- level 1 by push: each source's bit ORed into its neighbours' F (a
-  // source expands even when drained), a wave per source ----
-  for (uint32_t b = tid >> 6; b < nb; b += kMsThreads / 64) {
-    const uint32_t u = rows_src[row0 + b];
-    const uint32_t e1 = row_ptr[u + 1];
-    for (uint32_t e = row_ptr[u] + lane; e < e1; e += 64)
-      atomicOr(reinterpret_cast<unsigned long long*>(&F[col[e]]), 1ull << b);
+  // ---- the batch's sources (wave 0): level 0, drained sources, their CSR
+  // rows as one flat edge list (exclusive scan of the degrees), and their own
+  // bits marked in F for the owners to pick up ----
+  if (tid < 64) {
+    uint32_t deg = 0;
+    if (tid < nb) {
+      const uint32_t src = rows_src[row0 + tid];  // sources of a batch are distinct
+      src_l[tid] = src;
+      if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
+      if (D && d_from == 0) D[(size_t)(row0 + tid) * pitch + src] = 0;  // level 0
+      if (Dn) Dn[(size_t)(row0 + tid) * npitch + src] = 0;
+      e_base[tid] = row_ptr[src];
+      deg = row_ptr[src + 1] - e_base[tid];
+      F[src] = 1ull << tid;
+    }
+    uint32_t total;
+    const uint32_t ex = wave_excl_scan(deg, &total);
+    e_pre[tid] = ex;
+    if (tid == 0) e_pre[64] = total;
   }
   __syncthreads();
   const uint32_t n_osrc = *o_cnt;
@@ -332,30 +352,59 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     return x & own;
   };
 
+  // owned slices: slot i of this wave holds slice smap[wave * OWN + i] (the
+  // host deals slices to waves balanced by column width; an unused slot's
+  // nodes lie past N)
+  const uint32_t wv = tid >> 6;
+  uint32_t sv[OWN];  // first node of owned slice i (wave-uniform)
   uint64_t vis[OWN], nv[OWN];
   uint32_t drained = 0;  // bit i: owned node i is drained
   uint32_t sb[OWN], sw[OWN];  // owned slice i: column base, width (wave-uniform)
-  uint64_t any1 = 0;
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
-    const uint32_t v = tid + i * kMsThreads;
-    uint64_t self = 0;  // v's own source bit, if v is one of the batch's sources
-    for (uint32_t b = 0; b < nb; ++b) self |= (uint64_t)(src_l[b] == v) << b;
-    nv[i] = v < N ? F[v] & ~self : 0ull;  // level 1
-    vis[i] = self | nv[i];
-    any1 |= nv[i];
+    sv[i] = __builtin_amdgcn_readfirstlane(smap[wv * OWN + i]) * kSliceW;
+    const uint32_t v = sv[i] + lane;
+    vis[i] = v < N ? F[v] : 0ull;  // the node's own source bit, if it is a source
     if (v < N && ovl[v]) drained |= 1u << i;
-    const uint32_t slice = (tid - lane + i * kMsThreads) / kSliceW;
-    const bool live = slice * kSliceW < N;
+    const bool live = sv[i] < N;
+    const uint32_t slice = live ? sv[i] / kSliceW : 0u;
     const uint32_t b = live ? sell_ptr[slice] : 0u;
     const uint32_t e = live ? sell_ptr[slice + 1] : 0u;
     sb[i] = __builtin_amdgcn_readfirstlane(b);
     sw[i] = __builtin_amdgcn_readfirstlane((e - b) / kSliceW);
   }
+  __syncthreads();  // the self marks are read
+  if (tid < nb) F[src_l[tid]] = 0;
+  __syncthreads();
+  // ---- level 1 by push: each source's bit ORed into its neighbours' F (a
+  // source expands even when drained); the batch's edges dealt over the
+  // whole workgroup, their loads all independent ----
+  {
+    const uint32_t n_e = e_pre[64];
+    for (uint32_t t = tid; t < n_e; t += kMsThreads) {
+      uint32_t lo = 0, hi = nb;  // the source b with e_pre[b] <= t < e_pre[b + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (e_pre[mid] <= t) lo = mid;
+        else hi = mid;
+      }
+      atomicOr(reinterpret_cast<unsigned long long*>(&F[col[e_base[lo] + t - e_pre[lo]]]),
+               1ull << lo);
+    }
+  }
+  __syncthreads();
+  uint64_t any1 = 0;
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const uint32_t v = sv[i] + lane;
+    nv[i] = v < N ? F[v] & ~vis[i] : 0ull;  // level 1
+    vis[i] |= nv[i];
+    any1 |= nv[i];
+  }
   __syncthreads();  // every read of the pushed F is done
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
-    const uint32_t v = tid + i * kMsThreads;
+    const uint32_t v = sv[i] + lane;
     if (v < N) F[v] = ((drained >> i) & 1u) ? own_bits(v, nv[i]) : nv[i];
   }
   if (any1) flag[0] = 1;  // level 1 is not empty (flag[1] stays 0 for level 1's sweep)
@@ -363,116 +412,153 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   const bool level1 = flag[0] != 0;  // read before level 1 resets flag[0]
 
   MS_STAMP();
-  uint32_t last = 0;  // deepest level of the batch
-  for (uint32_t L = 1; level1; ++L) {
-    // ---- record level L: D[s][v] = L for every new (s, v) ----
-    // per owned slice, only the sources with a new node in it (wave OR);
-    // one store covers 64 consecutive nodes of one source row
+  // ---- record a level: D[s][v] = L for every new (s, v) of owned slice i
+  // (mask x); only the sources with a new node in the slice (wave OR) ----
+  auto record = [&](int i, uint64_t x, uint32_t L) {
+    // most slices have no new node at a given level: one ballot skips them
+    if (__ballot(x != 0ull) == 0ull) return;
     const uint32_t nl = min(L, 254u);
+    uint32_t* const DL = L >= d_from ? D : nullptr;  // u32 rows this level (uniform)
+    // the wave-uniform mask lives in SGPRs: row addressing is scalar work
+    const uint64_t wm = wave_or64(x);
+    uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
+    uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
+    const uint32_t v = sv[i] + lane;
+    // Two ways to cover the (source, node) pairs of the slice: one
+    // coalesced store per source (row-major; best when a source discovers
+    // many nodes of the slice at once -- dense fabrics), or each lane
+    // walking its own new sources (scattered stores; best when every source
+    // discovers a node or two per level -- grids, rings).  Trip counts:
+    // #sources vs the largest per-node count.
+    const uint32_t nsrc = (uint32_t)__popcll(((uint64_t)mhi << 32) | mlo);
+    uint32_t maxpop = (uint32_t)__popcll(x);
 #pragma unroll
-    for (int i = 0; i < OWN; ++i) {
-      // most slices have no new node at a given level: one ballot skips them
-      if (__ballot(nv[i] != 0ull) == 0ull) continue;
-      // the wave-uniform mask lives in SGPRs: row addressing is scalar work
-      const uint64_t wm = wave_or64(nv[i]);
-      uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
-      uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
-      const uint32_t v = tid + i * kMsThreads;
-      // Two ways to cover the (source, node) pairs of the slice: one
-      // coalesced store per source (row-major; best when a source discovers
-      // many nodes of the slice at once -- dense fabrics), or each lane
-      // walking its own new sources (scattered stores; best when every source
-      // discovers a node or two per level -- grids, rings).  Trip counts:
-      // #sources vs the largest per-node count.
-      const uint32_t nsrc = (uint32_t)__popcll(((uint64_t)mhi << 32) | mlo);
-      uint32_t maxpop = (uint32_t)__popcll(nv[i]);
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) maxpop = max(maxpop, (uint32_t)__shfl_xor((int)maxpop, d, 64));
-      maxpop = __builtin_amdgcn_readfirstlane(maxpop);
-      if (maxpop * kMsLaneStoreRatio < nsrc) {
-        uint64_t m = nv[i];
-        for (uint32_t it = 0; it < maxpop; ++it) {
-          if (m) {
-            const uint32_t s = __ffsll((unsigned long long)m) - 1;
-            D[(size_t)(row0 + s) * pitch + v] = L;
-            if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
-            m &= m - 1;
-          }
-        }
-        continue;
-      }
-      for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
-        const uint32_t s = __ffsll((unsigned long long)m) - 1;
-        if ((nv[i] >> s) & 1ull) {
-          D[(size_t)(row0 + s) * pitch + v] = L;
+    for (int d = 1; d < 64; d <<= 1) maxpop = max(maxpop, (uint32_t)__shfl_xor((int)maxpop, d, 64));
+    maxpop = __builtin_amdgcn_readfirstlane(maxpop);
+    if (maxpop * kMsLaneStoreRatio < nsrc) {
+      uint64_t m = x;
+      for (uint32_t it = 0; it < maxpop; ++it) {
+        if (m) {
+          const uint32_t s = __ffsll((unsigned long long)m) - 1;
+          if (DL) DL[(size_t)(row0 + s) * pitch + v] = L;
           if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
+          m &= m - 1;
         }
+      }
+      return;
+    }
+    for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
+      const uint32_t s = __ffsll((unsigned long long)m) - 1;
+      if ((x >> s) & 1ull) {
+        if (DL) DL[(size_t)(row0 + s) * pitch + v] = L;
+        if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
       }
     }
-    MS_STAMP();
-    uint64_t any = 0;
-    uint64_t nx[OWN];
-    // ---- pull sweep for level L+1 ----
+  };
+  // ---- pull of owned slice i from frontier Fc: the slice's unfinished
+  // nodes OR their neighbours' frontier masks; returns the new bits ----
+  auto pull = [&](int i, const uint64_t* Fc) -> uint64_t {
+    const uint32_t v = sv[i] + lane;
+    const bool need = v < N && vis[i] != all;
+    uint64_t nx = 0;
+    if (__ballot(need)) {  // wave-uniform: the slice has unfinished nodes
+      const uint32_t* cp = sell_col + sb[i] + lane;
+      const uint16_t* lp = lcol + sb[i] + lane;
+      const uint32_t w = sw[i];
+      uint64_t acc = 0;
+      uint32_t j = 0;
+      // kMsUnroll column loads in flight, then the remainder in groups of
+      // 4, 2, 1 (w is wave-uniform: scalar branches, no F reads wasted on
+      // padding -- the LDS port is what bounds the sweep)
+      for (; j + kMsUnroll <= w; j += kMsUnroll) {
+        uint32_t c[kMsUnroll];
 #pragma unroll
-    for (int i = 0; i < OWN; ++i) {
-      nx[i] = 0;
-      const uint32_t v = tid + i * kMsThreads;
-      const bool need = v < N && vis[i] != all;
-      if (__ballot(need)) {  // wave-uniform: the slice has unfinished nodes
-        const uint32_t* cp = sell_col + sb[i] + lane;
-        const uint16_t* lp = lcol + sb[i] + lane;
-        const uint32_t w = sw[i];
-        uint64_t acc = 0;
-        uint32_t j = 0;
-        // kMsUnroll column loads in flight, then the remainder in groups of
-        // 4, 2, 1 (w is wave-uniform: scalar branches, no F reads wasted on
-        // padding -- the LDS port is what bounds the sweep)
-        for (; j + kMsUnroll <= w; j += kMsUnroll) {
-          uint32_t c[kMsUnroll];
+        for (int u = 0; u < kMsUnroll; ++u)
+          c[u] = LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW];
 #pragma unroll
-          for (int u = 0; u < kMsUnroll; ++u)
+        for (int u = 0; u < kMsUnroll; ++u) acc |= Fc[c[u]];
+      }
+#pragma unroll
+      for (int g = kMsUnroll / 2; g >= 1; g >>= 1) {
+        if (j + g <= w) {
+          uint32_t c[kMsUnroll / 2];
+#pragma unroll
+          for (int u = 0; u < g; ++u)
             c[u] = LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW];
 #pragma unroll
-          for (int u = 0; u < kMsUnroll; ++u) acc |= F[c[u]];
-        }
-#pragma unroll
-        for (int g = kMsUnroll / 2; g >= 1; g >>= 1) {
-          if (j + g <= w) {
-            uint32_t c[kMsUnroll / 2];
-#pragma unroll
-            for (int u = 0; u < g; ++u)
-              c[u] = LCOL ? (uint32_t)lp[(j + u) * kSliceW] : cp[(j + u) * kSliceW];
-#pragma unroll
-            for (int u = 0; u < g; ++u) acc |= F[c[u]];
-            j += g;
-          }
-        }
-        if (need) {
-          nx[i] = acc & ~vis[i];
-          vis[i] |= nx[i];
-          any |= nx[i];
+          for (int u = 0; u < g; ++u) acc |= Fc[c[u]];
+          j += g;
         }
       }
-    }
-    MS_STAMP();
-    __syncthreads();  // every read of F for this level is done
-    MS_STAMP();
-#pragma unroll
-    for (int i = 0; i < OWN; ++i) {
-      const uint32_t v = tid + i * kMsThreads;
-      if (v < N) {
-        uint64_t f = nx[i];
-        if ((drained >> i) & 1u) f = own_bits(v, f);  // drained: expands only as its own source
-        F[v] = f;
+      if (need) {
+        nx = acc & ~vis[i];
+        vis[i] |= nx;
       }
-      nv[i] = nx[i];
     }
-    if (any) flag[L & 1] = 1;
-    if (tid == 0) flag[(L + 1) & 1] = 0;
-    __syncthreads();
-    if (!flag[L & 1]) {
-      last = L;
-      break;
+    return nx;
+  };
+  uint32_t last = 0;  // deepest level of the batch
+  if constexpr (DB) {
+    // Double-buffered frontier (graphs whose two F arrays fit in LDS): a
+    // slice is pulled from level L's frontier, its level L + 1 bits go
+    // straight into the other buffer and its stores are issued at once --
+    // one barrier per level, no per-slice state kept across it.
+    // flag[L mod 3]: set during level L, read after its barrier, cleared
+    // during level L + 2's predecessor (its last readers passed a barrier).
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) record(i, nv[i], 1);
+    uint64_t* Fc = F;
+    uint64_t* Fn = F2;
+    for (uint32_t L = 1; level1; ++L) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int i = 0; i < OWN; ++i) {
+        const uint64_t nx = pull(i, Fc);
+        const uint32_t v = sv[i] + lane;
+        if (v < N) Fn[v] = ((drained >> i) & 1u) ? own_bits(v, nx) : nx;
+        any |= nx;
+        record(i, nx, L + 1);
+      }
+      if (any) flag[L % 3] = 1;
+      if (tid == 0) flag[(L + 1) % 3] = 0;
+      MS_STAMP();
+      __syncthreads();
+      MS_STAMP();
+      if (!flag[L % 3]) {
+        last = L;
+        break;
+      }
+      uint64_t* t = Fc;
+      Fc = Fn;
+      Fn = t;
+    }
+  } else {
+    for (uint32_t L = 1; level1; ++L) {
+#pragma unroll
+      for (int i = 0; i < OWN; ++i) record(i, nv[i], L);
+      MS_STAMP();
+      uint64_t any = 0;
+      // ---- pull sweep for level L+1 ----
+#pragma unroll
+      for (int i = 0; i < OWN; ++i) {
+        nv[i] = pull(i, F);
+        any |= nv[i];
+      }
+      MS_STAMP();
+      __syncthreads();  // every read of F for this level is done
+      MS_STAMP();
+#pragma unroll
+      for (int i = 0; i < OWN; ++i) {
+        const uint32_t v = sv[i] + lane;
+        if (v < N) F[v] = ((drained >> i) & 1u) ? own_bits(v, nv[i]) : nv[i];  // drained: own source only
+      }
+      if (any) flag[L & 1] = 1;
+      if (tid == 0) flag[(L + 1) & 1] = 0;
+      __syncthreads();
+      if (!flag[L & 1]) {
+        last = L;
+        break;
+      }
     }
   }
   // the plan's deepest level: how many bit planes the sliced rows need
@@ -482,16 +568,16 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   uint64_t miss = 0;
 #pragma unroll
   for (int i = 0; i < OWN; ++i)
-    if (tid + i * kMsThreads < N) miss |= ~vis[i] & all;
+    if (sv[i] + lane < N) miss |= ~vis[i] & all;
   for (uint64_t m = wave_or64(miss); m; m &= m - 1) {
     const uint32_t s = __ffsll((unsigned long long)m) - 1;
     uint32_t* drow = D + (size_t)(row0 + s) * pitch;
     uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
-      const uint32_t v = tid + i * kMsThreads;
+      const uint32_t v = sv[i] + lane;
       if (v < N && !((vis[i] >> s) & 1ull)) {
-        drow[v] = kInf;
+        if (D && d_from == 0) drow[v] = kInf;
         if (Dn) nrow[v] = 0xFF;
       }
     }
@@ -500,7 +586,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     uint32_t* drow = D + (size_t)(row0 + s) * pitch;
     uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
     for (uint32_t v = N + tid; v < npitch; v += kMsThreads) {
-      if (v < pitch) drow[v] = kInf;
+      if (D && d_from == 0 && v < pitch) drow[v] = kInf;
       if (Dn) nrow[v] = 0xFF;
     }
   }
@@ -900,13 +986,24 @@ constexpr uint32_t kSlSat = 254;     // maxd at which the u8 copy saturates
 // wave's 64 loads cover 64 * P consecutive dwords.
 
 // u8 narrow rows -> bit-sliced rows; one thread per (row, word): two 16-byte
-// loads, P words stored.
+// loads, P words stored.  With D (expand plans, whose BFS stores only the u8
+// rows) the same thread also writes the row's u32 distances of its 32 nodes:
+// byte b < 254 is the distance, 255 unreachable (kInf, also the row padding),
+// and 254 -- saturated, level >= 254 -- keeps the exact value the BFS wrote
+// into D for those levels only.
 __global__ __launch_bounds__(256) void slice_rows_kernel(const uint8_t* __restrict__ Dn,
                                                          uint32_t npitch, uint32_t rows, uint32_t wpm,
                                                          const uint32_t* __restrict__ maxd,
-                                                         uint32_t* __restrict__ S) {
+                                                         uint32_t* __restrict__ S,
+                                                         uint32_t* __restrict__ D, uint32_t pitch,
+                                                         uint32_t ecmp_expands) {
   const uint32_t md = *maxd;
-  if (md >= kSlSat) return;
+  const bool planes = md < kSlSat;
+  // unsaturated rows are expanded by the next-hop pass itself when it can
+  // (ecmp_sliced_kernel's expansion blocks, overlapping its latency-bound
+  // matches); saturated ones here, before the pass reads them
+  if (ecmp_expands && planes) D = nullptr;
+  if (!planes && !D) return;
   const uint32_t P = 32u - __clz(md + 1u);
   const uint64_t total = (uint64_t)rows * wpm;
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
@@ -915,15 +1012,39 @@ __global__ __launch_bounds__(256) void slice_rows_kernel(const uint8_t* __restri
     const uint4* in = reinterpret_cast<const uint4*>(Dn + (size_t)r * npitch + 32ull * w);
     const uint4 a = in[0], b = in[1];
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t* out = S + (size_t)r * kSlSlots * wpm + (size_t)w * P;
-    for (uint32_t pl = 0; pl < P; ++pl) {
-      uint32_t word = 0;
-      // bit pl of bytes 4q .. 4q + 3 -> bits 4q .. 4q + 3 (the multiply moves
-      // byte i's bit to bit 24 + i; no cross term lands in bits 24..31)
+    if (planes) {
+      uint32_t* out = S + (size_t)r * kSlSlots * wpm + (size_t)w * P;
+      for (uint32_t pl = 0; pl < P; ++pl) {
+        uint32_t word = 0;
+        // bit pl of bytes 4q .. 4q + 3 -> bits 4q .. 4q + 3 (the multiply moves
+        // byte i's bit to bit 24 + i; no cross term lands in bits 24..31)
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        word |= ((((d[q] >> pl) & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
-      out[pl] = word;
+        for (int q = 0; q < 8; ++q)
+          word |= ((((d[q] >> pl) & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+        out[pl] = word;
+      }
+    }
+    if (D) {
+      uint4* o = reinterpret_cast<uint4*>(D + (size_t)r * pitch + 32ull * w);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t y = (d[q] >> (8 * k)) & 0xFFu;
+          x[k] = y == 0xFFu ? kInf : y;
+        }
+        // saturated bytes (254) keep the BFS's exact u32 (rare: deep graphs)
+        const uint32_t z = d[q] ^ 0xFEFEFEFEu;  // a zero byte where d[q] holds 254
+        if (__builtin_expect(((z - 0x01010101u) & ~z & 0x80808080u) != 0, 0)) {
+          const uint4 old = o[q];
+          const uint32_t ov[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (((d[q] >> (8 * k)) & 0xFFu) == 0xFEu) x[k] = ov[k];
+        }
+        o[q] = make_uint4(x[0], x[1], x[2], x[3]);
+      }
     }
   }
 }
@@ -1039,18 +1160,42 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     const uint32_t* __restrict__ nb_w, const uint32_t* __restrict__ nb_row,
     const uint32_t* __restrict__ nb_row_off, const uint32_t* __restrict__ nb_drained,
     uint32_t dead, uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
-    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes) {
-  const uint32_t g = blockIdx.x & 7;  // this block's XCD (round-robin placement)
+    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes,
+    const uint8_t* __restrict__ Dn, uint32_t* __restrict__ Dx, uint32_t x_rows, uint32_t x_blocks) {
+  const uint32_t md = *maxd;
+  if (blockIdx.x < x_blocks) {
+    // expansion blocks (expand plans whose rows did not saturate): the u32
+    // rows from the u8 ones (255 = unreachable), 4 nodes per lane, a wave's
+    // 1 KB of stores contiguous -- streaming stores beside the matches below,
+    // which are bound by load latency, not bandwidth (pitch == npitch)
+    if (!Dx || md >= kSlSat) return;
+    const uint64_t n4 = (uint64_t)x_rows * pitch / 4;
+    const uint32_t* in = reinterpret_cast<const uint32_t*>(Dn);
+    uint4* out = reinterpret_cast<uint4*>(Dx);
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+         q += (uint64_t)x_blocks * blockDim.x) {
+      const uint32_t b = in[q];
+      uint32_t x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t y = (b >> (8 * k)) & 0xFFu;
+        x[k] = y == 0xFFu ? kInf : y;
+      }
+      out[q] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    return;
+  }
+  const uint32_t bid = blockIdx.x - x_blocks;  // x_blocks is a multiple of 8
+  const uint32_t g = bid & 7;  // this block's XCD (round-robin placement)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wpm = pitch / 32;
-  const uint32_t md = *maxd;
   const uint32_t P = md < kSlSat ? 32u - __clz(md + 1u) : 0u;  // 0: saturated
   const uint32_t rstride = kSlSlots * wpm;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(S), 0, (int)s_bytes, 0x00020000);
   // wave-uniform to the compiler too (readfirstlane): the unit's values then
   // live in SGPRs and its row offsets arrive by scalar loads
-  const uint32_t t = (blockIdx.x >> 3) * kEcmpWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t t = (bid >> 3) * kEcmpWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t u_begin = unit_off[g];
   if (t >= unit_off[g + 1] - u_begin) return;  // whole wave: no barriers below
   {
@@ -1361,6 +1506,33 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     }
     HIP_TRY(c, c->d_sell_ptr.upload(c->sell_ptr.data(), c->sell_ptr.size(), c->stream));
     HIP_TRY(c, c->d_sell_col.upload(c->sell_col.data(), c->sell_col.size(), c->stream));
+    // msbfs_kernel's slices per wave: a level's pull sweep costs each wave the
+    // column groups of its slices and the workgroup waits for the slowest, so
+    // slices are dealt widest first to the wave with the fewest groups that
+    // still has a free slot (OWN slots per wave; unused slots = kNoSlice)
+    if (N <= kMsMaxNodes) {
+      const uint32_t own = ms_own(N), waves = kMsThreads / 64;
+      std::vector<uint32_t> order(n_slices), load(waves, 0), used(waves, 0);
+      std::iota(order.begin(), order.end(), 0u);
+      auto width = [&](uint32_t sl) { return (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / kSliceW; };
+      std::stable_sort(order.begin(), order.end(),
+                       [&](uint32_t a, uint32_t b) { return width(a) > width(b); });
+      std::vector<uint32_t> smap((size_t)waves * own, kNoSlice);
+      for (uint32_t sl : order) {
+        uint32_t best = waves;
+        for (uint32_t w = 0; w < waves; ++w)
+          if (used[w] < own && (best == waves || load[w] < load[best])) best = w;
+        smap[(size_t)best * own + used[best]++] = sl;
+        load[best] += std::max(1u, width(sl));
+      }
+      if (std::getenv("SPF_SMAP_STRIDED"))  // A/B: slot i of wave w = slice 16 i + w
+        for (uint32_t w = 0; w < waves; ++w)
+          for (uint32_t i = 0; i < own; ++i) {
+            const uint32_t sl = i * waves + w;
+            smap[(size_t)w * own + i] = sl < n_slices ? sl : kNoSlice;
+          }
+      HIP_TRY(c, c->d_ms_smap.upload(smap.data(), smap.size(), c->stream));
+    }
     // the same columns packed four u16 ids per lane (groups of 4 per slice,
     // at least one), for msbfs_planes_kernel (N <= 10240)
     c->sell4_ptr.assign(n_slices + 1, 0);
@@ -1552,6 +1724,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     p->ms = false;
     p->narrow = false;
     p->sliced = false;
+    p->expand = false;
     p->nh_off.resize(n_src);
     p->words.resize(n_src);
     uint64_t off = 0;
@@ -1639,6 +1812,10 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   {
     const char* e = std::getenv("SPF_NARROW");
     p->sliced = p->narrow && !use_planes(c) && !(e && e[0] == '1');
+    // the BFS stores u8 rows only and the slicing pass expands them into the
+    // u32 rows (SPF_EXPAND=0: the BFS stores both, A/B)
+    const char* x = std::getenv("SPF_EXPAND");
+    p->expand = p->sliced && c->pitch <= c->npitch && !(x && x[0] == '0');
   }
   const uint32_t wpm = c->pitch / 32;
   const uint64_t rstride = (uint64_t)kSlSlots * wpm;  // sliced row: words
@@ -1666,6 +1843,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     HIP_TRY(c, p->d_nb_row.upload(nb_row.data(), nb_row.size(), c->stream));
     HIP_TRY(c, p->d_nb_row_off.upload(nb_row_off.data(), n_src, c->stream));
     HIP_TRY(c, p->d_nb_drained.upload(nb_drained.data(), n_src, c->stream));
+    p->any_drained_nb = std::any_of(nb_drained.begin(), nb_drained.end(), [](uint32_t x) { return x; });
     // next-hop blocks per XCD: runs of consecutive sources of about
     // 1/(8 * runs) of the work each, every run to the XCD with the least
     // work so far (runs come in request order: the heavy spine and fabric
@@ -1814,8 +1992,9 @@ spf_status spf_plan_traffic(const spf_plan* p, uint64_t* bfs_bytes, uint64_t* ec
   return SPF_OK;
 }
 
-//   Slicing (sliced plans): the u8 rows read, P planes per row written; the
-//     sliced next-hop pass then reads P planes per row and writes the bitmaps.
+//   Slicing (sliced plans): the u8 rows read, P planes per row written (and,
+//     in expand plans, the u32 rows); the sliced next-hop pass then reads P
+//     planes per row and writes the bitmaps.
 spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
   if (!p || !bytes) return SPF_E_INVALID;
   uint64_t* bfs_bytes = &bytes[0];
@@ -1845,7 +2024,9 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
     const uint64_t n_slices = c->sell_ptr.size() - 1;
     const uint64_t csr = planes ? 8ull * c->sell4_ptr.back() + 4ull * (n_slices + 1)
                                 : 4ull * c->sell_ptr.back() + 4ull * (n_slices + 1);
-    bfs = groups * (csr + N) + rows * c->pitch * 4ull + (p->narrow ? rows * c->npitch : 0ull);
+    // expand plans: the u32 rows are written by the slicing pass instead
+    bfs = groups * (csr + N) + (p->expand ? 0ull : rows * c->pitch * 4ull) +
+          (p->narrow ? rows * c->npitch : 0ull);
   } else {
     bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch);
   }
@@ -1855,11 +2036,13 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
     uint32_t md = 0;
     HIP_TRY(p->ctx, hipMemcpy(&md, p->d_maxd.p, 4, hipMemcpyDeviceToHost));
     const uint64_t wbytes = 4ull * (c->pitch / 32);
+    const uint64_t expand = p->expand ? rows * 4ull * c->pitch : 0ull;  // u32 rows written
     if (md < kSlSat) {
       const uint64_t P = 32u - __builtin_clz(md + 1u);
-      bytes[1] = rows * c->npitch + rows * P * wbytes;
+      bytes[1] = rows * c->npitch + rows * P * wbytes + expand;
       *ecmp_bytes = rows * P * wbytes + 4ull * p->nh_total;
     } else {
+      bytes[1] = expand ? rows * c->npitch + expand : 0ull;
       *ecmp_bytes = rows * 4ull * c->pitch + 4ull * p->nh_total;
     }
     return SPF_OK;
@@ -1928,11 +2111,22 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 
 namespace {
 
-size_t msbfs_lds_bytes(uint32_t N) { return 8ull * (N + 1) + 4ull * (2 * kMsBatch + 3); }
+size_t msbfs_lds_bytes(uint32_t N, bool db = false) {
+  return 8ull * (N + 1) * (db ? 2 : 1) + 4ull * (4 * kMsBatch + 5);
+}
+
+// msbfs_kernel with a double-buffered frontier: when the columns do not fit
+// in LDS beside one F array but two F arrays do (SPF_MSBFS_DB=0: single, A/B)
+bool ms_double_buffer(const spf_ctx* c) {
+  const char* e = std::getenv("SPF_MSBFS_DB");
+  if (e && e[0] == '0') return false;
+  const size_t n_col = c->sell_ptr.back();
+  return msbfs_lds_bytes(c->N) + 2ull * n_col > kMaxLds && msbfs_lds_bytes(c->N, true) <= kMaxLds;
+}
 
 template <int OWN>
 void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
-                  uint32_t* maxd, hipStream_t s) {
+                  uint32_t* maxd, uint32_t d_from, hipStream_t s) {
   const uint32_t n_col = c->sell_ptr.back();
   const size_t lds = msbfs_lds_bytes(c->N), lds_col = lds + 2ull * n_col;
   const bool lcol = lds_col <= kMaxLds;
@@ -1945,12 +2139,17 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
     hipLaunchKernelGGL((msbfs_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds_col, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_row_ptr.p, c->d_col.p,
                        c->d_ovl.p, rows_src, rows, bs, c->N, c->pitch, c->npitch, D, Dn,
-                       maxd, c->d_stamps.p);
+                       maxd, d_from, c->d_ms_smap.p, c->d_stamps.p);
+  else if (ms_double_buffer(c))
+    hipLaunchKernelGGL((msbfs_kernel<OWN, false, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
+                       msbfs_lds_bytes(c->N, true), s, c->d_sell_ptr.p, c->d_sell_col.p, n_col,
+                       c->d_row_ptr.p, c->d_col.p, c->d_ovl.p, rows_src, rows, bs, c->N, c->pitch,
+                       c->npitch, D, Dn, maxd, d_from, c->d_ms_smap.p, c->d_stamps.p);
   else
     hipLaunchKernelGGL((msbfs_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds, s, c->d_sell_ptr.p, c->d_sell_col.p, n_col, c->d_row_ptr.p, c->d_col.p,
                        c->d_ovl.p, rows_src, rows, bs, c->N, c->pitch, c->npitch, D, Dn,
-                       maxd, c->d_stamps.p);
+                       maxd, d_from, c->d_ms_smap.p, c->d_stamps.p);
 }
 
 size_t planes_lds_bytes(uint32_t own) { return 8ull * own * kMsThreads + 4ull * (kPlBatch + 4); }
@@ -1985,12 +2184,15 @@ bool use_planes(const spf_ctx* c) {
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
-                        uint8_t* Dn, uint32_t* maxd, hipStream_t s) {
+                        uint8_t* Dn, uint32_t* maxd, hipStream_t s, uint32_t d_from = 0) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
-    HIP_TRY(c, c->d_stamps.alloc(64 * 16));
+    HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
+    const unsigned long long wg = std::strtoull(std::getenv("SPF_STAMPS"), nullptr, 10);
+    HIP_TRY(c, hipMemcpyAsync(c->d_stamps.p + 64 * 16, &wg, 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
   }
-  const uint32_t own = (c->N + kMsThreads - 1) / kMsThreads;
+  const uint32_t own = ms_own(c->N);
   if (use_planes(c)) {
     if (own <= 1) planes_launch<1>(c, rows_src, rows, D, Dn, s);
     else if (own <= 2) planes_launch<2>(c, rows_src, rows, D, Dn, s);
@@ -2000,13 +2202,13 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
     HIP_TRY(c, hipGetLastError());
     return SPF_OK;
   }
-  if (own <= 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, maxd, s);
-  else if (own <= 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, maxd, s);
-  else if (own <= 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, maxd, s);
-  else if (own <= 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, maxd, s);
-  else if (own <= 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, maxd, s);
-  else if (own <= 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, maxd, s);
-  else msbfs_launch<16>(c, rows_src, rows, D, Dn, maxd, s);
+  if (own == 1) msbfs_launch<1>(c, rows_src, rows, D, Dn, maxd, d_from, s);
+  else if (own == 2) msbfs_launch<2>(c, rows_src, rows, D, Dn, maxd, d_from, s);
+  else if (own == 4) msbfs_launch<4>(c, rows_src, rows, D, Dn, maxd, d_from, s);
+  else if (own == 8) msbfs_launch<8>(c, rows_src, rows, D, Dn, maxd, d_from, s);
+  else if (own == 10) msbfs_launch<10>(c, rows_src, rows, D, Dn, maxd, d_from, s);
+  else if (own == 12) msbfs_launch<12>(c, rows_src, rows, D, Dn, maxd, d_from, s);
+  else msbfs_launch<16>(c, rows_src, rows, D, Dn, maxd, d_from, s);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2025,6 +2227,15 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
   return SPF_OK;
 }
 
+// Expand plans: the next-hop pass expands the unsaturated u32 rows itself
+// unless it reads them (a drained neighbour's direct-hop test reads the
+// source's u32 row) or the row pitches differ (SPF_EXPAND=2: always the
+// slicing pass, A/B)
+bool ecmp_expands(const spf_ctx* c, const spf_plan* p) {
+  const char* x = std::getenv("SPF_EXPAND");
+  return p->expand && c->pitch == c->npitch && !p->any_drained_nb && !(x && x[0] == '2');
+}
+
 spf_status launch_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool hop, uint32_t* d_nh,
                          hipStream_t s) {
   const uint32_t wpm = c->pitch / 32;
@@ -2032,7 +2243,8 @@ spf_status launch_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool hop, u
   const uint64_t words = (uint64_t)rows * wpm;
   const uint32_t sb = (uint32_t)std::min<uint64_t>((words + 255) / 256, 16ull * c->n_cu);
   hipLaunchKernelGGL(slice_rows_kernel, dim3(std::max(sb, 1u)), dim3(256), 0, s, p->d_Dn.p, c->npitch,
-                     rows, wpm, p->d_maxd.p, p->d_S.p);
+                     rows, wpm, p->d_maxd.p, p->d_S.p, p->expand ? const_cast<uint32_t*>(D) : nullptr,
+                     c->pitch, ecmp_expands(c, p) ? 1u : 0u);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2041,12 +2253,16 @@ spf_status launch_ecmp_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool h
                               hipStream_t s) {
   // one wave per unit; block b serves XCD b % 8 (round-robin placement)
   const uint32_t blocks = 8 * std::max(1u, (p->max_xcd_units + kEcmpWaves - 1) / kEcmpWaves);
-  hipLaunchKernelGGL(ecmp_sliced_kernel, dim3(blocks), dim3(kEcmpThreads), 0, s, p->d_S.p,
+  // expansion blocks first (dispatched at once, beside the match blocks)
+  const bool xp = ecmp_expands(c, p);
+  const uint32_t x_blocks = xp ? 2 * c->n_cu : 0u;
+  hipLaunchKernelGGL(ecmp_sliced_kernel, dim3(x_blocks + blocks), dim3(kEcmpThreads), 0, s, p->d_S.p,
                      p->d_maxd.p, D, c->pitch, p->d_srcs.p, p->d_row_of.p,
                      c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p,
                      p->d_nb_drained.p, p->dead, hop ? 1u : 0u, p->d_nh_off.p, d_nh,
                      reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p,
-                     (uint32_t)(p->d_S.n * 4));
+                     (uint32_t)(p->d_S.n * 4), p->d_Dn.p, xp ? const_cast<uint32_t*>(D) : nullptr,
+                     (uint32_t)p->closure.size(), x_blocks);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2061,7 +2277,8 @@ spf_status set_lds_limits(spf_ctx* c) {
 #define SSK(QT, U) (const void*)sssp_kernel<QT, U, 256>, (const void*)sssp_kernel<QT, U, 512>, \
                    (const void*)sssp_kernel<QT, U, 1024>
   const void* fns[] = {SSK(uint16_t, true), SSK(uint16_t, false), SSK(uint32_t, true), SSK(uint32_t, false),
-#define MSB(o) (const void*)msbfs_kernel<o, false>, (const void*)msbfs_kernel<o, true>
+#define MSB(o) (const void*)msbfs_kernel<o, false>, (const void*)msbfs_kernel<o, true>, \
+               (const void*)msbfs_kernel<o, false, true>
                        MSB(1), MSB(2), MSB(4), MSB(8), MSB(10), MSB(12), MSB(16),
 #define PLB(o) (const void*)msbfs_planes_kernel<o, false>, (const void*)msbfs_planes_kernel<o, true>
                        PLB(1), PLB(2), PLB(4), PLB(8), PLB(10)};
@@ -2142,7 +2359,8 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
   spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
-                                       sliced ? p->d_maxd.p : nullptr, s)
+                                       sliced ? p->d_maxd.p : nullptr, s,
+                                       sliced && p->expand ? kSlSat : 0u)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));

@@ -205,3 +205,26 @@ def test_big_graph_kernel_exact(name, make, monkeypatch):
     compare(names, eng, orc, list(range(len(names))))
     compare(names, eng, orc, list(range(len(names))), hop=True)
     compare(names, eng, orc, [3, 1, 3, 0])  # unsorted, duplicated sources
+
+
+@pytest.mark.parametrize("expand", ["0", "1", "2"])
+@pytest.mark.parametrize("name,make", [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("ring700", lambda: T.wan(700, 0, seed=1)),  # distances to 350: saturated u8 bytes
+    ("rand_drained", lambda: T.random_graph(300, 3000, 11, max_metric=1, overload_frac=0.1)),
+], ids=["fabric", "ring700", "dense_drained"])
+def test_expanded_u32_rows(name, make, expand, monkeypatch):
+    """Sliced plans whose BFS stores only the u8 rows and the u32 rows are
+    expanded from them -- by the next-hop pass's expansion blocks (default;
+    the slicing pass when rows saturate or a source has a drained
+    neighbour), always by the slicing pass (SPF_EXPAND=2) -- and the BFS
+    writing both (SPF_EXPAND=0): every source's rows and next hops against
+    the oracle, including the saturated levels (>= 254) the BFS still writes
+    as u32."""
+    monkeypatch.setenv("SPF_EXPAND", expand)
+    monkeypatch.setenv("SPF_NARROW", "2")
+    monkeypatch.setenv("SPF_MSBFS", "masks")
+    names, eng, orc = load(make())
+    assert eng.plan([0], hop=True).row_mode() == "sliced"
+    compare(names, eng, orc, list(range(len(names))), hop=True)
+    compare(names, eng, orc, list(range(0, len(names), 3)))

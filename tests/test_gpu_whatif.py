@@ -87,7 +87,7 @@ WIDE = [
     # U[1, 1e5]: the unfailed distances pass kLevelCap (65536), so the base
     # pass takes its fixed-point path (whatif.hip:321) and the repairs' level
     # span exceeds their cap (fixed-point sweeps, whatif.hip:981)
-    ("wan1500_m1e5", lambda: T.wan(1500, 800, seed=3, max_metric=100_000), 100_000),
+    ("wan3000_m1e5", lambda: T.wan(3000, 1500, seed=3, max_metric=100_000), 100_000),
 ]
 
 

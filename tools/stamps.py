@@ -1,12 +1,12 @@
 """Per-phase cycle breakdown of the BFS kernel (workgroup 0, every wave).
 
-Diagnostic only: SPF_STAMPS=1 makes msbfs_kernel log s_memtime at each phase
-boundary.  Prints, per level, the min/max over the 16 waves of the store phase,
+Diagnostic only: SPF_STAMPS=<workgroup> makes msbfs_kernel log s_memtime at
+each phase boundary of that workgroup (default 0).  Prints, per level, the min/max over the 16 waves of the store phase,
 pull phase and barrier wait, and which wave is the slowest.
 """
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["SPF_STAMPS"] = "1"
+os.environ.setdefault("SPF_STAMPS", "0")  # the workgroup logged
 import numpy as np
 import torch
 from openr_amd import topology as T
@@ -28,13 +28,9 @@ n = min(len(x) for x in waves)
 st = np.stack([x[:n] for x in waves])  # [W, n]
 t0 = st[:, 0].min()
 print(f"{which}: {st.shape[0]} waves, {n} stamps, total cycles {int(st[:, -1].max() - t0)}")
-n_lv = (n - 3) // 3
-prev = st[:, 1]
-print("init max", int((st[:, 1] - st[:, 0]).max()))
-for L in range(n_lv):
-    A, B, Cc = st[:, 2 + 3 * L], st[:, 3 + 3 * L], st[:, 4 + 3 * L]
-    sto, pul, bar = A - prev, B - A, Cc - B
-    print(f"level {L:3d}: stores {sto.min():7d}..{sto.max():7d} (w{sto.argmax():2d})  "
-          f"pull {pul.min():7d}..{pul.max():7d} (w{pul.argmax():2d})  barrier {bar.min():7d}..{bar.max():7d}")
-    prev = Cc
-print("tail max", int((st[:, -1] - prev).max()))
+# consecutive stamp intervals (min..max over the waves, slowest wave):
+# single-buffered kernel: init | per level: stores, pull, barrier | tail;
+# double-buffered: init | per level: pull+stores, barrier | tail
+for k in range(1, n):
+    d = st[:, k] - st[:, k - 1]
+    print(f"interval {k:3d}: {int(d.min()):8d}..{int(d.max()):8d} (w{int(d.argmax()):2d})")
