@@ -177,12 +177,21 @@ class AllSources:
         k = np.array([len(eng.neighbors(s)) for s in range(self.n)], np.int64)
         pitch = eng.pitch
         gather = scaling == "strong" and world > 1
-        self.layout = AllSourcesLayout(k, pitch, world if gather else 1)
-        srcs = self.layout.srcs[rank if gather else 0]
+        # the gathered distance rows: the plans' u8 rows when every rank's
+        # are lossless (checked once below), a quarter of the u32 bytes
+        layout = AllSourcesLayout(k, pitch, world if gather else 1)
+        srcs = layout.srcs[rank if gather else 0]
         self.plan = eng.plan(srcs)
+        self.dist_bytes = 4
+        if gather and self.plan.row_mode() != "u32" and self._narrow_lossless(dev, len(srcs), pitch):
+            self.dist_bytes = 1
+            layout = AllSourcesLayout(k, pitch, world, dist_bytes=1)
+        self.layout = layout
         assert np.array_equal(self.plan.nh_off, self.layout.plan_nh_off(rank if gather else 0))
         cap = self.layout.cap
-        self.dist_words = len(srcs) * pitch
+        self.dist_words = self.layout.dist_words[rank if gather else 0]
+        # u8 rows on the wire: the plan's u32 rows go to a scratch buffer
+        self.d32 = dev.buf(max(1, len(srcs) * pitch)) if self.dist_bytes == 1 else None
         self.nbuf = 2 if gather else 1
         self.send = [dev.buf(max(1, cap), zero=True) for _ in range(self.nbuf)]
         self.recv = ([dev.torch.zeros((world, max(1, cap)), dtype=dev.torch.int32,
@@ -193,6 +202,8 @@ class AllSources:
         self.i = 0
         self.units = len(srcs)
         self.gather_bytes = 4 * sum(self.layout.words) if gather else 0
+        self.wire = ("u8 distance rows (lossless: every distance < 254) + next-hop bitmaps"
+                     if self.dist_bytes == 1 else "u32 distance rows + next-hop bitmaps")
         # SURVEY.md §8(d) per-solve figure (one CSR sweep charged per solve)
         n, e = self.n, self.e
         self.survey_bytes = int(len(srcs) * (4 * (n + 1) + 8 * e + n + 4 * n)
@@ -205,8 +216,8 @@ class AllSources:
         self._phase_bytes()
         self.parallelism = (
             f"sources in contiguous id blocks over {world} rank(s) (one LSDB), plan closure "
-            f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source dist rows + "
-            f"next-hop bitmaps gathered to rank 0 over RCCL in the step "
+            f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source results "
+            f"({self.wire}) gathered to rank 0 over RCCL in the step "
             f"({self.gather_bytes / 1e6:.0f} MB/step, send buffers double-buffered)"
             if gather else
             "one rank, all sources" if scaling == "strong" else
@@ -218,12 +229,37 @@ class AllSources:
         if self.works[b] is not None:  # the gather that last read this buffer
             self.works[b].wait()
         buf = self.send[b]
-        self.plan.execute(buf.ptr, buf.ptr + 4 * self.dist_words, self.dev.stream())
+        if self.d32 is None:
+            self.plan.execute(buf.ptr, buf.ptr + 4 * self.dist_words, self.dev.stream())
+        else:
+            self.plan.execute(self.d32.ptr, buf.ptr + 4 * self.dist_words, self.dev.stream())
+            self.plan.copy_narrow_rows(buf.ptr, self.dev.stream())
         if self.gather:
             import torch.distributed as dist
 
             out = list(self.recv[b].unbind(0)) if self.rank == 0 else None
             self.works[b] = dist.gather(buf.t, out, dst=0, async_op=True)
+
+    def _narrow_lossless(self, dev, m: int, pitch: int) -> bool:
+        """One untimed execute: are this rank's u8 rows exact (no distance
+        >= 254)?  Agreed over all ranks (every rank must ship the same form)."""
+        import torch
+        import torch.distributed as dist
+
+        d32 = dev.buf(max(1, m * pitch))
+        nh = dev.buf(max(1, int(self.plan.nh_words)))
+        d8 = dev.buf(max(1, m * pitch // 4))
+        self.plan.execute(d32.ptr, nh.ptr, dev.stream())
+        self.plan.copy_narrow_rows(d8.ptr, dev.stream())
+        a = d32.t[: m * pitch].to(torch.int64) & 0xFFFFFFFF
+        b = d8.t.view(torch.uint8)[: m * pitch].to(torch.int64)
+        inf = 0xFFFFFFFF
+        ok = bool(((a == inf) | (a < 254)).all()) and bool(torch.equal(torch.where(a == inf, 255, a), b))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        for x in (d32, nh, d8):
+            x.free()
+        return bool(flag.item())
 
     def finish(self) -> None:
         for w in self.works:

@@ -167,6 +167,16 @@ spf_status spf_plan_traffic_phases(const spf_plan* plan, uint64_t* bytes);
  * synchronisation, no allocation: capturable into a hipGraph. */
 spf_status spf_plan_execute(spf_plan* plan, uint32_t* d_dist, uint32_t* d_nh,
                             void* stream);
+/* The narrow (u8) distance rows of the plan's last execute, for plans whose
+ * distance kernel keeps them (spf_plan_kernels: *narrow != 0): row i (source
+ * srcs[i]) byte v = d(srcs[i], v) when below 254, 254 when d >= 254, 255
+ * when unreachable or v >= n_nodes -- lossless when every finite distance of
+ * the execute is below 254 (unit-metric fabrics: 4 levels; grid 100x100:
+ * 198).  n_src rows of spf_row_pitch bytes are copied to d_out on `stream`
+ * (after the execute on that stream).  SPF_E_UNSUPPORTED for plans without
+ * them.  Used to ship rows compactly (multi-GPU gather); no reference
+ * counterpart (the reference's metric is u64, LinkState.h:22). */
+spf_status spf_plan_copy_narrow_rows(spf_plan* plan, uint8_t* d_out, void* stream);
 /* spf_plan_execute into host buffers: dist [n_src][n_nodes] (dense, no row
  * padding) and the next-hop words (spf_plan_nh_words of them); either may be
  * NULL.  Device staging is owned by the plan. */

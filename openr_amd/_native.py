@@ -164,6 +164,7 @@ PROTOTYPES = {
     "spf_plan_traffic": (C.c_int, [_vp, _u64p, _u64p]),
     "spf_plan_traffic_phases": (C.c_int, [_vp, _u64p]),
     "spf_plan_execute": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "spf_plan_copy_narrow_rows": (C.c_int, [_vp, _vp, _vp]),
     "spf_plan_execute_host": (C.c_int, [_vp, _u32p, _u32p]),
     "spf_plan_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_plan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),

@@ -102,7 +102,6 @@ struct spf_plan {
   bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
   bool sliced = false;  // ... and the next-hop pass on its bit-sliced form
   bool expand = false;  // ... the u32 rows expanded from the u8 ones (BFS stores bytes only)
-  bool any_drained_nb = false;  // some source has a drained neighbour (next-hop pass reads D)
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;

@@ -986,8 +986,9 @@ constexpr uint32_t kSlSat = 254;     // maxd at which the u8 copy saturates
 // wave's 64 loads cover 64 * P consecutive dwords.
 
 // u8 narrow rows -> bit-sliced rows; one thread per (row, word): two 16-byte
-// loads, P words stored.  With D (expand plans, whose BFS stores only the u8
-// rows) the same thread also writes the row's u32 distances of its 32 nodes:
+// loads, P words stored.  With D (expand plans, SPF_EXPAND=1, whose BFS
+// stores only the u8 rows) the same thread also writes the row's u32
+// distances of its 32 nodes:
 // byte b < 254 is the distance, 255 unreachable (kInf, also the row padding),
 // and 254 -- saturated, level >= 254 -- keeps the exact value the BFS wrote
 // into D for those levels only.
@@ -995,14 +996,9 @@ __global__ __launch_bounds__(256) void slice_rows_kernel(const uint8_t* __restri
                                                          uint32_t npitch, uint32_t rows, uint32_t wpm,
                                                          const uint32_t* __restrict__ maxd,
                                                          uint32_t* __restrict__ S,
-                                                         uint32_t* __restrict__ D, uint32_t pitch,
-                                                         uint32_t ecmp_expands) {
+                                                         uint32_t* __restrict__ D, uint32_t pitch) {
   const uint32_t md = *maxd;
   const bool planes = md < kSlSat;
-  // unsaturated rows are expanded by the next-hop pass itself when it can
-  // (ecmp_sliced_kernel's expansion blocks, overlapping its latency-bound
-  // matches); saturated ones here, before the pass reads them
-  if (ecmp_expands && planes) D = nullptr;
   if (!planes && !D) return;
   const uint32_t P = 32u - __clz(md + 1u);
   const uint64_t total = (uint64_t)rows * wpm;
@@ -1160,33 +1156,9 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     const uint32_t* __restrict__ nb_w, const uint32_t* __restrict__ nb_row,
     const uint32_t* __restrict__ nb_row_off, const uint32_t* __restrict__ nb_drained,
     uint32_t dead, uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
-    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes,
-    const uint8_t* __restrict__ Dn, uint32_t* __restrict__ Dx, uint32_t x_rows, uint32_t x_blocks) {
+    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes) {
   const uint32_t md = *maxd;
-  if (blockIdx.x < x_blocks) {
-    // expansion blocks (expand plans whose rows did not saturate): the u32
-    // rows from the u8 ones (255 = unreachable), 4 nodes per lane, a wave's
-    // 1 KB of stores contiguous -- streaming stores beside the matches below,
-    // which are bound by load latency, not bandwidth (pitch == npitch)
-    if (!Dx || md >= kSlSat) return;
-    const uint64_t n4 = (uint64_t)x_rows * pitch / 4;
-    const uint32_t* in = reinterpret_cast<const uint32_t*>(Dn);
-    uint4* out = reinterpret_cast<uint4*>(Dx);
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
-         q += (uint64_t)x_blocks * blockDim.x) {
-      const uint32_t b = in[q];
-      uint32_t x[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t y = (b >> (8 * k)) & 0xFFu;
-        x[k] = y == 0xFFu ? kInf : y;
-      }
-      out[q] = make_uint4(x[0], x[1], x[2], x[3]);
-    }
-    return;
-  }
-  const uint32_t bid = blockIdx.x - x_blocks;  // x_blocks is a multiple of 8
-  const uint32_t g = bid & 7;  // this block's XCD (round-robin placement)
+  const uint32_t g = blockIdx.x & 7;  // this block's XCD (round-robin placement)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wpm = pitch / 32;
   const uint32_t P = md < kSlSat ? 32u - __clz(md + 1u) : 0u;  // 0: saturated
@@ -1195,7 +1167,7 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
       const_cast<uint32_t*>(S), 0, (int)s_bytes, 0x00020000);
   // wave-uniform to the compiler too (readfirstlane): the unit's values then
   // live in SGPRs and its row offsets arrive by scalar loads
-  const uint32_t t = (bid >> 3) * kEcmpWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t t = (blockIdx.x >> 3) * kEcmpWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t u_begin = unit_off[g];
   if (t >= unit_off[g + 1] - u_begin) return;  // whole wave: no barriers below
   {
@@ -1261,6 +1233,17 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
 // ---------------------------------------------------------------------------
 //  copy selected D rows into the caller's dense output (non-direct plans)
 // ---------------------------------------------------------------------------
+// u8 rows (npitch bytes, a multiple of 16): row rows[i] -> out row i
+__global__ void gather_rows_u8_kernel(const uint8_t* __restrict__ Dn, uint32_t npitch,
+                                      const uint32_t* __restrict__ rows, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.y;
+  const uint4* in = reinterpret_cast<const uint4*>(Dn + (size_t)rows[i] * npitch);
+  uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * npitch);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < npitch / 16;
+       t += gridDim.x * blockDim.x)
+    o[t] = in[t];
+}
+
 __global__ void gather_rows_kernel(const uint32_t* __restrict__ D, uint32_t pitch,
                                    const uint32_t* __restrict__ rows,
                                    uint32_t* __restrict__ out) {
@@ -1812,10 +1795,14 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   {
     const char* e = std::getenv("SPF_NARROW");
     p->sliced = p->narrow && !use_planes(c) && !(e && e[0] == '1');
-    // the BFS stores u8 rows only and the slicing pass expands them into the
-    // u32 rows (SPF_EXPAND=0: the BFS stores both, A/B)
+    // SPF_EXPAND=1 (A/B; measured slower): the BFS stores the u8
+    // rows only and the slicing pass expands them into the u32 rows.  By
+    // default the BFS stores both: its u32 stores drain behind its
+    // latency-bound sweeps (+0.06 ms on fabric_full) where a separate
+    // streaming pass costs 0.14 ms and a fused one 0.14 ms of the next-hop
+    // kernel's time (r02_v25/r02_v26)
     const char* x = std::getenv("SPF_EXPAND");
-    p->expand = p->sliced && c->pitch <= c->npitch && !(x && x[0] == '0');
+    p->expand = p->sliced && c->pitch <= c->npitch && x && x[0] == '1';
   }
   const uint32_t wpm = c->pitch / 32;
   const uint64_t rstride = (uint64_t)kSlSlots * wpm;  // sliced row: words
@@ -1843,7 +1830,6 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     HIP_TRY(c, p->d_nb_row.upload(nb_row.data(), nb_row.size(), c->stream));
     HIP_TRY(c, p->d_nb_row_off.upload(nb_row_off.data(), n_src, c->stream));
     HIP_TRY(c, p->d_nb_drained.upload(nb_drained.data(), n_src, c->stream));
-    p->any_drained_nb = std::any_of(nb_drained.begin(), nb_drained.end(), [](uint32_t x) { return x; });
     // next-hop blocks per XCD: runs of consecutive sources of about
     // 1/(8 * runs) of the work each, every run to the XCD with the least
     // work so far (runs come in request order: the heavy spine and fabric
@@ -2227,15 +2213,6 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
   return SPF_OK;
 }
 
-// Expand plans: the next-hop pass expands the unsaturated u32 rows itself
-// unless it reads them (a drained neighbour's direct-hop test reads the
-// source's u32 row) or the row pitches differ (SPF_EXPAND=2: always the
-// slicing pass, A/B)
-bool ecmp_expands(const spf_ctx* c, const spf_plan* p) {
-  const char* x = std::getenv("SPF_EXPAND");
-  return p->expand && c->pitch == c->npitch && !p->any_drained_nb && !(x && x[0] == '2');
-}
-
 spf_status launch_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool hop, uint32_t* d_nh,
                          hipStream_t s) {
   const uint32_t wpm = c->pitch / 32;
@@ -2244,7 +2221,7 @@ spf_status launch_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool hop, u
   const uint32_t sb = (uint32_t)std::min<uint64_t>((words + 255) / 256, 16ull * c->n_cu);
   hipLaunchKernelGGL(slice_rows_kernel, dim3(std::max(sb, 1u)), dim3(256), 0, s, p->d_Dn.p, c->npitch,
                      rows, wpm, p->d_maxd.p, p->d_S.p, p->expand ? const_cast<uint32_t*>(D) : nullptr,
-                     c->pitch, ecmp_expands(c, p) ? 1u : 0u);
+                     c->pitch);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2253,16 +2230,12 @@ spf_status launch_ecmp_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool h
                               hipStream_t s) {
   // one wave per unit; block b serves XCD b % 8 (round-robin placement)
   const uint32_t blocks = 8 * std::max(1u, (p->max_xcd_units + kEcmpWaves - 1) / kEcmpWaves);
-  // expansion blocks first (dispatched at once, beside the match blocks)
-  const bool xp = ecmp_expands(c, p);
-  const uint32_t x_blocks = xp ? 2 * c->n_cu : 0u;
-  hipLaunchKernelGGL(ecmp_sliced_kernel, dim3(x_blocks + blocks), dim3(kEcmpThreads), 0, s, p->d_S.p,
+  hipLaunchKernelGGL(ecmp_sliced_kernel, dim3(blocks), dim3(kEcmpThreads), 0, s, p->d_S.p,
                      p->d_maxd.p, D, c->pitch, p->d_srcs.p, p->d_row_of.p,
                      c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p,
                      p->d_nb_drained.p, p->dead, hop ? 1u : 0u, p->d_nh_off.p, d_nh,
                      reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p,
-                     (uint32_t)(p->d_S.n * 4), p->d_Dn.p, xp ? const_cast<uint32_t*>(D) : nullptr,
-                     (uint32_t)p->closure.size(), x_blocks);
+                     (uint32_t)(p->d_S.n * 4));
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2382,6 +2355,20 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     HIP_TRY(c, hipGetLastError());
   }
   c->solves += p->n_src;
+  return SPF_OK;
+}
+
+spf_status spf_plan_copy_narrow_rows(spf_plan* p, uint8_t* d_out, void* stream) {
+  if (!p || !d_out) return fail(p ? p->ctx : nullptr, SPF_E_INVALID, "spf_plan_copy_narrow_rows: NULL");
+  spf_ctx* c = p->ctx;
+  if (p->exact || p->big || !p->narrow || !p->d_Dn.p)
+    return fail(c, SPF_E_UNSUPPORTED, "spf_plan_copy_narrow_rows: the plan keeps no u8 rows");
+  if (c->npitch != c->pitch)
+    return fail(c, SPF_E_UNSUPPORTED, "spf_plan_copy_narrow_rows: u8 and u32 row pitches differ");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipLaunchKernelGGL(gather_rows_u8_kernel, dim3(std::min<uint32_t>((c->npitch / 16 + 255) / 256, 64), p->n_src),
+                     dim3(256), 0, s, p->d_Dn.p, c->npitch, p->d_req_rows.p, d_out);
+  HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
 

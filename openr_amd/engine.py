@@ -76,6 +76,12 @@ class SpfPlan(NativeHandle):
         self._eng._err(N.lib.spf_plan_execute(self._h, C.c_void_p(d_dist), C.c_void_p(d_nh),
                                               C.c_void_p(stream) if stream else None))
 
+    def copy_narrow_rows(self, d_out: int, stream: int = 0) -> None:
+        """Enqueue a copy of the last execute's u8 rows (n_src x pitch bytes,
+        254 = saturated, 255 = unreachable) to d_out (spf_plan_copy_narrow_rows)."""
+        self._eng._err(N.lib.spf_plan_copy_narrow_rows(self._h, C.c_void_p(d_out),
+                                                       C.c_void_p(stream) if stream else None))
+
     def execute_host(self) -> "SolveResult":
         """Execute into host arrays (spf_plan_execute_host)."""
         n = self._eng.n_nodes

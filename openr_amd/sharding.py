@@ -59,15 +59,21 @@ class AllSourcesLayout:
     its results into one contiguous send buffer of u32 words:
     ``[dist rows: len(srcs[r]) x pitch][next-hop bitmaps: nh_words[r]]`` --
     exactly the plan's own output layout (``spf_plan_nh_layout``), so the
-    kernels write the send buffer directly.  Buffers are padded to
+    kernels write the send buffer directly.  With ``dist_bytes=1`` the
+    distance rows are the plan's u8 rows (``spf_plan_copy_narrow_rows``,
+    a quarter of the bytes on the wire; lossless while every distance is
+    below 254, which the caller checks).  Buffers are padded to
     ``cap`` words so one ``gather`` moves them; rank 0 ends up with
     ``world x cap`` words from which :meth:`dist_row` / :meth:`nh_block`
     read any source's result."""
 
-    def __init__(self, k: np.ndarray, pitch: int, world: int) -> None:
+    def __init__(self, k: np.ndarray, pitch: int, world: int, dist_bytes: int = 4) -> None:
         k = np.asarray(k, np.int64)
         n = len(k)
+        assert dist_bytes in (1, 4) and (pitch * dist_bytes) % 4 == 0
         self.n, self.pitch, self.world = n, pitch, world
+        self.dist_bytes = dist_bytes
+        row_words = pitch * dist_bytes // 4  # a distance row in u32 words
         self.k = k
         wpm = pitch // 32
         # contiguous blocks balanced by next-hop work (k + 1 bitmaps-ish per source)
@@ -85,22 +91,29 @@ class AllSourcesLayout:
             m = len(ss)
             self.rank_of[ss] = r
             self.index_of[ss] = np.arange(m)
-            self.dist_off[ss] = np.arange(m, dtype=np.int64) * pitch
+            self.dist_off[ss] = np.arange(m, dtype=np.int64) * row_words
             nh_local = np.concatenate([[0], np.cumsum(k[ss] * wpm)[:-1]]).astype(np.int64) \
                 if m else np.zeros(0, np.int64)
-            self.nh_off[ss] = m * pitch + nh_local
-            self.words.append(int(m * pitch + (k[ss] * wpm).sum()))
+            self.nh_off[ss] = m * row_words + nh_local
+            self.words.append(int(m * row_words + (k[ss] * wpm).sum()))
+        self.dist_words = [len(ss) * row_words for ss in self.srcs]
         self.cap = max(self.words) if self.words else 0
 
     def plan_nh_off(self, rank: int) -> np.ndarray:
         """The plan-relative next-hop offsets rank `rank`'s plan must report."""
         ss = self.srcs[rank]
-        return (self.nh_off[ss] - len(ss) * self.pitch).astype(np.uint64)
+        return (self.nh_off[ss] - self.dist_words[rank]).astype(np.uint64)
 
     def dist_row(self, recv: Sequence, s: int):
+        """Source s's distances (u32, SPF_UNREACHABLE) from host buffers; u8
+        rows (dist_bytes 1: the engine's narrow rows, lossless below 254)
+        are widened, 255 -> unreachable."""
         r = int(self.rank_of[s])
         o = int(self.dist_off[s])
-        return recv[r][o: o + self.n]
+        if self.dist_bytes == 4:
+            return recv[r][o: o + self.n]
+        b = np.asarray(recv[r]).view(np.uint8)[4 * o: 4 * o + self.n]
+        return np.where(b == 255, np.uint32(0xFFFFFFFF), b.astype(np.uint32))
 
     def nh_block(self, recv: Sequence, s: int):
         """Next-hop bitmaps of source s: k[s] rows of pitch/32 words."""

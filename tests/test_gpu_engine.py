@@ -207,20 +207,18 @@ def test_big_graph_kernel_exact(name, make, monkeypatch):
     compare(names, eng, orc, [3, 1, 3, 0])  # unsorted, duplicated sources
 
 
-@pytest.mark.parametrize("expand", ["0", "1", "2"])
+@pytest.mark.parametrize("expand", ["0", "1"])
 @pytest.mark.parametrize("name,make", [
     ("fabric_full1000", lambda: T.fabric(1000, full=True)),
     ("ring700", lambda: T.wan(700, 0, seed=1)),  # distances to 350: saturated u8 bytes
     ("rand_drained", lambda: T.random_graph(300, 3000, 11, max_metric=1, overload_frac=0.1)),
 ], ids=["fabric", "ring700", "dense_drained"])
 def test_expanded_u32_rows(name, make, expand, monkeypatch):
-    """Sliced plans whose BFS stores only the u8 rows and the u32 rows are
-    expanded from them -- by the next-hop pass's expansion blocks (default;
-    the slicing pass when rows saturate or a source has a drained
-    neighbour), always by the slicing pass (SPF_EXPAND=2) -- and the BFS
-    writing both (SPF_EXPAND=0): every source's rows and next hops against
-    the oracle, including the saturated levels (>= 254) the BFS still writes
-    as u32."""
+    """Sliced plans whose BFS writes both row forms (default) and whose BFS
+    stores only the u8 rows, the slicing pass expanding them into the u32
+    rows (SPF_EXPAND=1): every source's rows and next hops against the
+    oracle, including the saturated levels (>= 254) the BFS still writes as
+    u32 in the second mode."""
     monkeypatch.setenv("SPF_EXPAND", expand)
     monkeypatch.setenv("SPF_NARROW", "2")
     monkeypatch.setenv("SPF_MSBFS", "masks")
@@ -228,3 +226,39 @@ def test_expanded_u32_rows(name, make, expand, monkeypatch):
     assert eng.plan([0], hop=True).row_mode() == "sliced"
     compare(names, eng, orc, list(range(len(names))), hop=True)
     compare(names, eng, orc, list(range(0, len(names), 3)))
+
+
+@pytest.mark.parametrize("name,make,srcs", [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True), slice(0, None)),
+    ("grid30", lambda: T.grid(30), slice(0, None)),
+    ("fabric_block", lambda: T.fabric(1000, full=True), slice(300, 500)),  # closure != sources
+    ("ring700", lambda: T.wan(700, 0, seed=1), slice(0, 40)),  # distances past 254 saturate
+], ids=["fabric", "grid", "fabric_block", "ring700"])
+def test_copy_narrow_rows(name, make, srcs, monkeypatch):
+    """spf_plan_copy_narrow_rows (the u8 rows the multi-GPU gather ships):
+    byte = min(d, 254), 255 = unreachable and row padding, rows in plan
+    source order, against the same execute's u32 rows."""
+    from openr_amd.hiprt import DeviceArray, synchronize
+
+    if name == "ring700":  # a sparse ring's plans read u32 rows unless told
+        monkeypatch.setenv("SPF_NARROW", "2")
+        monkeypatch.setenv("SPF_MSBFS", "masks")
+    names, eng, orc = load(make())
+    ids = list(range(len(names)))[srcs]
+    plan = eng.plan(ids)
+    assert plan.row_mode() != "u32"
+    pitch, m = eng.pitch, len(ids)
+    d32 = DeviceArray(m * pitch, np.uint32)
+    nh = DeviceArray(max(1, plan.nh_words), np.uint32)
+    d8 = DeviceArray(m * pitch, np.uint8)
+    try:
+        plan.execute(d32.ptr, nh.ptr)
+        plan.copy_narrow_rows(d8.ptr)
+        synchronize()
+        a = d32.numpy().reshape(m, pitch)
+        b = d8.numpy().reshape(m, pitch)
+        want = np.where(a == 0xFFFFFFFF, 255, np.minimum(a, 254)).astype(np.uint8)
+        assert np.array_equal(b, want)
+    finally:
+        for x in (d32, nh, d8):
+            x.free()

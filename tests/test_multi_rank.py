@@ -247,7 +247,7 @@ def test_two_rank_ksp2_and_whatif_exchange_gloo():
 
 
 # ---- all-sources split + gather to rank 0 ------------
-def _all_sources_worker(rank, world, port, q):
+def _all_sources_worker(rank, world, port, q, dist_bytes=4):
     import sys
     from pathlib import Path
 
@@ -271,13 +271,16 @@ def _all_sources_worker(rank, world, port, q):
         n = len(names)
         pitch = (n + 63) // 64 * 64
         k = np.array([len(set(col[rp[v]:rp[v + 1]].tolist())) for v in range(n)])
-        lay = AllSourcesLayout(k, pitch, world)
+        lay = AllSourcesLayout(k, pitch, world, dist_bytes)
         orc = OracleLinkState()
         orc.update_packed(topo.lsdb)
         # this rank's share, in the plan layout, written into the send buffer
         srcs = lay.srcs[rank]
         d, mats = orc.dense(names, list(srcs))
         d32, nh = planar_rows(k[srcs], d, mats, pitch)
+        if dist_bytes == 1:  # the engine's narrow rows: min(d, 254), 255 = unreachable
+            rows = np.where(d32 == 0xFFFFFFFF, 255, np.minimum(d32, 254)).astype(np.uint8)
+            d32 = rows.ravel().view(np.uint32)
         send = torch.zeros(lay.cap, dtype=torch.int32)
         flat = np.concatenate([d32.ravel(), nh]).view(np.int32)
         assert len(flat) == lay.words[rank]
@@ -295,15 +298,16 @@ def _all_sources_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_all_sources_split_and_gather_reassembles_single_rank_result(world):
-    """One LSDB, sources split over ranks, every rank's dist rows + next-hop
-    bitmaps gathered to rank 0 (gloo here, RCCL in bench.py): rank 0's
-    reassembled arrays equal the single-rank all-sources result bit for bit."""
+@pytest.mark.parametrize("world,dist_bytes", [(2, 4), (3, 4), (2, 1), (3, 1)])
+def test_all_sources_split_and_gather_reassembles_single_rank_result(world, dist_bytes):
+    """One LSDB, sources split over ranks, every rank's dist rows (u32, or
+    the engine's u8 rows) + next-hop bitmaps gathered to rank 0 (gloo here,
+    RCCL in bench.py): rank 0's reassembled arrays equal the single-rank
+    all-sources result bit for bit."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_all_sources_worker, args=(r, world, port, q))
+    procs = [ctx.Process(target=_all_sources_worker, args=(r, world, port, q, dist_bytes))
              for r in range(world)]
     for p in procs:
         p.start()
