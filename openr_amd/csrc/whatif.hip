@@ -596,11 +596,34 @@ __global__ void classify_kernel(WiGraph g, const uint32_t* __restrict__ dist,
 struct TeamCtl {
   uint32_t n, ovf, flag[3], dmin, dmax, nxt[3], lc[3], hub;
   unsigned long long ndist, nnh, dh;
+  uint32_t bar;   // group teams: arrivals at the team barrier (monotonic)
+  uint32_t next;  // group teams: the failure the team takes next
 };
 
-template <int TEAM>
-__device__ __forceinline__ void team_sync() {
-  if (TEAM == 64) {
+// A team is a wave (64), a workgroup (1024) or a group of TEAM / 1024
+// workgroups of one cooperative launch on one XCD (team_sync = the agent-scope
+// release -> arrival counter -> poll -> acquire hand-off of
+// MI355X_MICROARCH.md §Workgroup dispatch; the counter only grows, so the
+// barrier of the k-th call completes at k * G arrivals)
+template <int TEAM, bool GROUP = false>
+__device__ __forceinline__ void team_sync(TeamCtl* ctl) {
+  if constexpr (GROUP) {
+    const uint32_t G = TEAM / blockDim.x;  // workgroups per team
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t ticket =
+          __hip_atomic_fetch_add(&ctl->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t target = (ticket / G + 1) * G;
+      while (__hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  } else if constexpr (TEAM == 64) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -610,16 +633,21 @@ __device__ __forceinline__ void team_sync() {
 }
 
 // Returns false (nothing written, scratch clean) when |D| exceeds cap.
-// a team's scratch (mark, dlist, dnew, level lists) is private to one
-// workgroup: workgroup-scope accesses may be served by the CU's L1
+// a wave's or workgroup's scratch (mark, dlist, dnew, level lists) is private
+// to one workgroup: workgroup-scope accesses may be served by the CU's L1; a
+// group team's is shared by several CUs: agent scope (L1 bypassed)
+template <bool GROUP>
 __device__ __forceinline__ uint32_t ldw(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if constexpr (GROUP) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+template <bool GROUP>
 __device__ __forceinline__ void stw(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if constexpr (GROUP) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int TEAM>
+template <int TEAM, bool GROUP = false>
 __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
                        uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, uint32_t cap,
                        TeamCtl* ctl, uint32_t tt, uint32_t e_fail, spf_whatif_digest* out,
@@ -642,14 +670,14 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
     ctl->ndist = ctl->nnh = ctl->dh = 0;
     dlist[0] = b;
-    stw(&mark[b], 0);
+    stw<GROUP>(&mark[b], 0);
   }
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   // ---- D = descendants of b in the unfailed DAG (level by level) ----
   uint32_t lo = 0;
   for (;;) {
     const uint32_t n = ctl->n;
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     if (lo >= n || ctl->ovf) break;
     // a thread per frontier node; hubs (thousands of edges) are queued in
     // ord and expanded by a whole wave each
@@ -660,9 +688,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       const uint32_t idx = atomicAdd(&ctl->n, 1u);
       if (idx < cap) {
         dlist[idx] = c;
-        stw(&mark[c], idx);
+        stw<GROUP>(&mark[c], idx);
       } else {
-        stw(&mark[c], kInf);
+        stw<GROUP>(&mark[c], kInf);
         ctl->ovf = 1;
       }
     };
@@ -671,41 +699,41 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.ovl[v]) continue;  // drained (v != src): no DAG children
       const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
       if (b1 - b0 > kHubDeg) {
-        stw(&ord[atomicAdd(&ctl->hub, 1u)], i);
+        stw<GROUP>(&ord[atomicAdd(&ctl->hub, 1u)], i);
         continue;
       }
       const uint32_t dv = B.dist[v];
       for (uint32_t e = b0; e < b1; ++e) child(dv, e);
     }
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     {
       const uint32_t nh_ = ctl->hub;
       for (uint32_t k = wv; k < nh_; k += kWaves) {
-        const uint32_t v = dlist[ldw(&ord[k])];
+        const uint32_t v = dlist[ldw<GROUP>(&ord[k])];
         const uint32_t dv = B.dist[v];
         for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) child(dv, e);
       }
     }
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     if (tt == 0) ctl->hub = 0;
     lo = n;
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
   }
   const uint32_t n = min(ctl->n, cap);
   const bool ovf = ctl->ovf != 0;
   WI_STAMP(1);
   if (prof && tt == 0) prof[8] = n;
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   if (ovf) {
-    for (uint32_t i = tt; i < n; i += TEAM) stw(&mark[dlist[i]], kInf);
-    team_sync<TEAM>();
+    for (uint32_t i = tt; i < n; i += TEAM) stw<GROUP>(&mark[dlist[i]], kInf);
+    team_sync<TEAM, GROUP>(ctl);
     return false;
   }
   // ---- seeds: best in-edge from outside D (unchanged distances) ----
   auto seed_edge = [&](uint32_t e) -> uint32_t {
     if (g.link[e] == l) return kInf;
     const uint32_t u = g.col[e];
-    if (ldw(&mark[u]) != kInf) return kInf;
+    if (ldw<GROUP>(&mark[u]) != kInf) return kInf;
     if (g.ovl[u] && u != g.src) return kInf;
     const uint32_t du = B.dist[u];
     return du == kInf ? kInf : du + g.wt[g.rev[e]];
@@ -714,40 +742,40 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     const uint32_t v = dlist[i];
     const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
     if (b1 - b0 > kHubDeg) {
-      stw(&ord[atomicAdd(&ctl->hub, 1u)], i);
+      stw<GROUP>(&ord[atomicAdd(&ctl->hub, 1u)], i);
       continue;
     }
     uint32_t best = kInf;
     for (uint32_t e = b0; e < b1; ++e) best = min(best, seed_edge(e));
-    stw(&dnew[i], best);
+    stw<GROUP>(&dnew[i], best);
   }
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   {
     const uint32_t nh_ = ctl->hub;
     for (uint32_t k = wv; k < nh_; k += kWaves) {
-      const uint32_t i = ldw(&ord[k]);
+      const uint32_t i = ldw<GROUP>(&ord[k]);
       const uint32_t v = dlist[i];
       uint32_t best = kInf;
       for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64)
         best = min(best, seed_edge(e));
       best = wave_min32(best);
-      if (lane == 0) stw(&dnew[i], best);
+      if (lane == 0) stw<GROUP>(&dnew[i], best);
     }
   }
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   if (tt == 0) ctl->hub = 0;
   // nh word j of a D node from its tight expanded predecessors (D or not);
   // used by the fixed-point fallback
   auto nh_of = [&](uint32_t i, uint32_t j) -> uint32_t {
     const uint32_t v = dlist[i];
-    const uint32_t dv = ldw(&dnew[i]);
+    const uint32_t dv = ldw<GROUP>(&dnew[i]);
     uint32_t acc = 0;
     for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
       if (g.link[e] == l) continue;
       const uint32_t u = g.col[e];
       if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = ldw(&mark[u]);
-      const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
+      const uint32_t mu = ldw<GROUP>(&mark[u]);
+      const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
       if (du == kInf || du + in_w(g, e) != dv) continue;
       if (u == g.src) {
         const uint32_t jb = g.nbr_bit[v];
@@ -766,8 +794,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.link[e] == l) continue;
       const uint32_t u = g.col[e];
       if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = ldw(&mark[u]);
-      const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
+      const uint32_t mu = ldw<GROUP>(&mark[u]);
+      const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
       if (du == kInf || du + in_w(g, e) != dv) continue;
       if (u == g.src) {
         const uint32_t jb = g.nbr_bit[v];
@@ -778,7 +806,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         // loads ahead of their stores keep the loads in flight together
         // instead of one load-OR-store round trip per word
         uint32_t j = 0;
-        if (TEAM == 1024)  // workgroup teams only: costs the wave teams occupancy
+        if (TEAM >= 512)  // workgroup / group teams only: costs the wave teams occupancy
           for (; j + 8 <= W; j += 8) {
             uint32_t f[8], r[8];
 #pragma unroll
@@ -799,13 +827,13 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     ctl->nxt[0] = kInf;
     ctl->lc[0] = 0;
   }
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   {
     uint32_t m = kInf;
-    for (uint32_t i = tt; i < n; i += TEAM) m = min(m, ldw(&dnew[i]));
+    for (uint32_t i = tt; i < n; i += TEAM) m = min(m, ldw<GROUP>(&dnew[i]));
     if (m != kInf) atomicMin(&ctl->dmin, m);
   }
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   WI_STAMP(2);
   // ---- Dial: settle D one distance value at a time (metrics are positive:
   // a node holding the smallest pending value is final), next hops inline ----
@@ -826,11 +854,11 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     // (a) the level's nodes (their distance is final) into ord
     uint32_t m = kInf;
     for (uint32_t i = tt; i < n; i += TEAM) {
-      const uint32_t d = ldw(&dnew[i]);
-      if (d == t) stw(&ord[atomicAdd(cnt, 1u)], i);
+      const uint32_t d = ldw<GROUP>(&dnew[i]);
+      if (d == t) stw<GROUP>(&ord[atomicAdd(cnt, 1u)], i);
       else if (d != kInf && d > t) m = min(m, d);
     }
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     // (b) level nodes: next hops from their tight predecessors, then relax
     // their edges.  A thread per node; hubs (queued after the level list)
     // by a whole wave: ballot over the in-edges, coalesced row ORs.
@@ -839,27 +867,27 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     uint32_t* hub_cnt = &ctl->lc[(it + 2) % 3];  // free this level
     auto relax = [&](uint32_t v, uint32_t e) {
       if (g.link[e] == l) return;
-      const uint32_t ic = ldw(&mark[g.col[e]]);
+      const uint32_t ic = ldw<GROUP>(&mark[g.col[e]]);
       if (ic == kInf) return;
       const uint32_t nd = t + g.wt[e];
       if (nd < atomicMin(&dnew[ic], nd)) m = min(m, nd);
     };
     for (uint32_t k = tt; k < K; k += TEAM) {
-      const uint32_t i = ldw(&ord[k]);
+      const uint32_t i = ldw<GROUP>(&ord[k]);
       const uint32_t v = dlist[i];
       const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
       if (b1 - b0 > kHubDeg) {
-        stw(&hubs[atomicAdd(hub_cnt, 1u)], i);
+        stw<GROUP>(&hubs[atomicAdd(hub_cnt, 1u)], i);
         continue;
       }
       nh_row(i, v, t);
       if (!g.ovl[v])
         for (uint32_t e = b0; e < b1; ++e) relax(v, e);
     }
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     const uint32_t H_ = *hub_cnt;
     for (uint32_t k = wv; k < H_; k += kWaves) {
-      const uint32_t i = ldw(&hubs[k]);
+      const uint32_t i = ldw<GROUP>(&hubs[k]);
       const uint32_t v = dlist[i];
       uint32_t* row = nhn + (size_t)i * W;
       const uint32_t jb = g.nbr_bit[v];
@@ -871,8 +899,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         if (e < g.row_ptr[v + 1] && g.link[e] != l) {
           u = g.col[e];
           if (!(g.ovl[u] && u != g.src)) {
-            mu = ldw(&mark[u]);
-            const uint32_t du = mu != kInf ? ldw(&dnew[mu]) : B.dist[u];
+            mu = ldw<GROUP>(&mark[u]);
+            const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
             tight = du != kInf && du + g.wt[g.rev[e]] == t;
           }
         }
@@ -892,7 +920,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) relax(v, e);
     }
     if (m != kInf) atomicMin(next, m);
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     t = *next;
     if (prof && tt == 0) prof[9] = it + 1;
   }
@@ -903,11 +931,11 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       bool any = false;
       for (uint32_t i = tt; i < n; i += TEAM) {
         const uint32_t v = dlist[i];
-        const uint32_t dv = ldw(&dnew[i]);
+        const uint32_t dv = ldw<GROUP>(&dnew[i]);
         if (dv == kInf || g.ovl[v]) continue;
         for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
           if (g.link[e] == l) continue;
-          const uint32_t ic = ldw(&mark[g.col[e]]);
+          const uint32_t ic = ldw<GROUP>(&mark[g.col[e]]);
           if (ic == kInf) continue;
           const uint32_t nd = dv + g.wt[e];
           if (nd < atomicMin(&dnew[ic], nd)) any = true;
@@ -915,7 +943,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       }
       if (any) ctl->flag[it % 3] = 1;
       if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
-      team_sync<TEAM>();
+      team_sync<TEAM, GROUP>(ctl);
       if (!ctl->flag[it % 3]) break;
     }
 
@@ -926,58 +954,58 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       ctl->dmin = kInf;
       ctl->dmax = 0;
     }
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     for (uint32_t i = tt; i < n; i += TEAM) {
-      const uint32_t d = ldw(&dnew[i]);
+      const uint32_t d = ldw<GROUP>(&dnew[i]);
       if (d != kInf) {
         atomicMin(&ctl->dmin, d);
         atomicMax(&ctl->dmax, d);
       }
     }
-    team_sync<TEAM>();
+    team_sync<TEAM, GROUP>(ctl);
     const uint32_t dmin = ctl->dmin;
     const uint32_t nlev = dmin == kInf ? 0u : ctl->dmax - dmin + 1;
     if (nlev <= cap) {
       // counting sort of D by new distance; a predecessor always sits in a
       // lower level (positive metrics), so one pass per level is exact
-      for (uint32_t b = tt; b < nlev; b += TEAM) stw(&lvl[b], 0u);
-      team_sync<TEAM>();
+      for (uint32_t b = tt; b < nlev; b += TEAM) stw<GROUP>(&lvl[b], 0u);
+      team_sync<TEAM, GROUP>(ctl);
       for (uint32_t i = tt; i < n; i += TEAM) {
-        const uint32_t d = ldw(&dnew[i]);
+        const uint32_t d = ldw<GROUP>(&dnew[i]);
         if (d != kInf) atomicAdd(&lvl[d - dmin], 1u);
       }
-      team_sync<TEAM>();
+      team_sync<TEAM, GROUP>(ctl);
       if (tt < 64) {  // exclusive scan by the team's first wave
         uint32_t carry = 0;
         for (uint32_t base = 0; base < nlev; base += 64) {
           const uint32_t b = base + tt;
-          const uint32_t x = b < nlev ? ldw(&lvl[b]) : 0u;
+          const uint32_t x = b < nlev ? ldw<GROUP>(&lvl[b]) : 0u;
           uint32_t inc = x;
           for (int d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(inc, d, 64);
             if (tt >= (uint32_t)d) inc += y;
           }
-          if (b < nlev) stw(&lvl[b], carry + inc - x);
+          if (b < nlev) stw<GROUP>(&lvl[b], carry + inc - x);
           carry += __shfl(inc, 63, 64);
         }
       }
-      team_sync<TEAM>();
+      team_sync<TEAM, GROUP>(ctl);
       for (uint32_t i = tt; i < n; i += TEAM) {
-        const uint32_t d = ldw(&dnew[i]);
-        if (d != kInf) stw(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
+        const uint32_t d = ldw<GROUP>(&dnew[i]);
+        if (d != kInf) stw<GROUP>(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
       }
-      team_sync<TEAM>();
+      team_sync<TEAM, GROUP>(ctl);
       uint32_t begin = 0;
       for (uint32_t b = 0; b < nlev; ++b) {
-        const uint32_t end = ldw(&lvl[b]);
+        const uint32_t end = ldw<GROUP>(&lvl[b]);
         if (end == begin) continue;
         const size_t items = (size_t)(end - begin) * W;
         for (size_t x = tt; x < items; x += TEAM) {
-          const uint32_t i = ldw(&ord[begin + x / W]), j = (uint32_t)(x % W);
+          const uint32_t i = ldw<GROUP>(&ord[begin + x / W]), j = (uint32_t)(x % W);
           nhn[(size_t)i * W + j] = nh_of(i, j);
         }
         begin = end;
-        team_sync<TEAM>();
+        team_sync<TEAM, GROUP>(ctl);
       }
     } else {
       // fixed-point sweeps (monotone union over the DAG)
@@ -985,7 +1013,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         bool any = false;
         for (uint32_t x = tt; x < nw; x += TEAM) {
           const uint32_t i = x / W, j = x % W;
-          if (ldw(&dnew[i]) == kInf) continue;
+          if (ldw<GROUP>(&dnew[i]) == kInf) continue;
           const uint32_t acc = nh_of(i, j);
           if (acc != nhn[x]) {
             nhn[x] = acc;
@@ -994,7 +1022,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         }
         if (any) ctl->flag[it % 3] = 1;
         if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
-        team_sync<TEAM>();
+        team_sync<TEAM, GROUP>(ctl);
         if (!ctl->flag[it % 3]) break;
       }
     }
@@ -1005,7 +1033,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   uint64_t dh = 0;
   for (uint32_t i = tt; i < n; i += TEAM) {
     const uint32_t v = dlist[i];
-    const uint32_t d1 = ldw(&dnew[i]), d0 = B.dist[v];
+    const uint32_t d1 = ldw<GROUP>(&dnew[i]), d0 = B.dist[v];
     const uint32_t* h0 = B.nhb + (size_t)v * W;
     const uint32_t* h1 = nhn + (size_t)i * W;
     nd_ += d1 != d0;
@@ -1013,16 +1041,16 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     for (uint32_t w = 0; w < W && !diff; ++w) diff = h0[w] != h1[w];
     nn_ += diff;
     dh += (d1 == kInf ? 0ull : node_hash(v, d1, h1, W)) - node_hash(v, d0, h0, W);
-    stw(&mark[v], kInf);
+    stw<GROUP>(&mark[v], kInf);
   }
   if (nd_) atomicAdd(&ctl->ndist, (unsigned long long)nd_);
   if (nn_) atomicAdd(&ctl->nnh, (unsigned long long)nn_);
   if (dh) atomicAdd(&ctl->dh, (unsigned long long)dh);
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   if (tt == 0)
     *out = spf_whatif_digest{(uint32_t)ctl->ndist, (uint32_t)ctl->nnh,
                              (uint64_t)(*B.H + ctl->dh)};
-  team_sync<TEAM>();
+  team_sync<TEAM, GROUP>(ctl);
   WI_STAMP(5);
 #undef WI_STAMP
   return true;
@@ -1080,6 +1108,100 @@ __global__ __launch_bounds__(1024) void repair_block_kernel(
   }
 }
 
+// The classified big failures, largest subtree first (the order the group
+// teams pull them in): a rank sort by one workgroup; lists longer than
+// kSortCap keep their order.
+constexpr uint32_t kSortCap = 8192;
+__global__ __launch_bounds__(1024) void sort_big_kernel(const uint2* __restrict__ in,
+                                                        const uint32_t* __restrict__ n_in,
+                                                        const uint32_t* __restrict__ sub,
+                                                        const uint32_t* __restrict__ col,
+                                                        uint2* __restrict__ out) {
+  const uint32_t n = *n_in;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (n > kSortCap) {
+      out[i] = in[i];
+      continue;
+    }
+    const uint32_t ki = sub[col[in[i].y]];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t kj = sub[col[in[j].y]];
+      r += kj > ki || (kj == ki && j < i);
+    }
+    out[r] = in[i];
+  }
+}
+
+// Group teams of G workgroups of kGroupWg threads (one cooperative launch, a
+// workgroup per CU): the largest repairs get G CUs each.  Half-size
+// workgroups (8 waves, 2 per SIMD) co-reside with the wave teams' blocks, so
+// both progress from the start.  Members of a team sit on one XCD (blocks x
+// and x + 8 share one); teams pull failures, largest first.
+constexpr int kGroupWg = 512;
+template <int G>
+__global__ __launch_bounds__(kGroupWg) void repair_group_kernel(
+    WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
+    uint32_t* cursor, TeamCtl* ctls, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
+    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out,
+    unsigned long long* prof) {
+  constexpr int TEAM = kGroupWg * G;
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t idx = blockIdx.x >> 3;
+  const uint32_t member = idx % G;
+  const size_t team = (size_t)(idx / G) * 8 + (blockIdx.x & 7);
+  TeamCtl* ctl = ctls + team;
+  const uint32_t tt = member * kGroupWg + threadIdx.x;
+  mark += team * g.N;
+  dlist += team * g.N;
+  dnew += team * g.N;
+  nhn += team * (size_t)g.N * g.W;
+  lvl += team * ((size_t)g.N + 1);
+  ord += team * 2 * (size_t)g.N;
+  const uint32_t total = *n_big;
+  for (;;) {
+    if (tt == 0) ctl->next = atomicAdd(cursor, 1u);
+    team_sync<TEAM, true>(ctl);
+    const uint32_t k = ldw<true>(&ctl->next);
+    if (k >= total) break;  // team-uniform
+    const uint2 h = big[k];
+    repair<TEAM, true>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, ctl, tt, h.y, out + h.x,
+                       prof ? prof + team * 16 : nullptr);
+  }
+}
+
+struct GroupArgs {
+  WiGraph g;
+  WiBase B;
+  const uint2* big;
+  const uint32_t* n_big;
+  uint32_t* cursor;
+  TeamCtl* ctls;
+  uint32_t *mark, *dlist, *dnew, *nhn, *lvl, *ord;
+  spf_whatif_digest* out;
+  unsigned long long* prof;
+};
+
+template <int G>
+hipError_t launch_group_g(GroupArgs& a, uint32_t n_cu, hipStream_t s) {
+  void* args[] = {&a.g, &a.B, &a.big, &a.n_big, &a.cursor, &a.ctls, &a.mark, &a.dlist, &a.dnew,
+                  &a.nhn, &a.lvl, &a.ord, &a.out, &a.prof};
+  return hipLaunchCooperativeKernel((const void*)repair_group_kernel<G>, dim3(n_cu),
+                                    dim3(kGroupWg), args, 0, s);
+}
+
+// one cooperative launch, a workgroup per CU (every member of every team
+// resident at once: the team barrier's precondition)
+hipError_t launch_group(uint32_t G, GroupArgs& a, uint32_t n_cu, hipStream_t s) {
+  switch (G) {
+    case 2: return launch_group_g<2>(a, n_cu, s);
+    case 4: return launch_group_g<4>(a, n_cu, s);
+    case 8: return launch_group_g<8>(a, n_cu, s);
+    case 16: return launch_group_g<16>(a, n_cu, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 __global__ void base_digest_kernel(spf_whatif_digest* o, const unsigned long long* H) {
   *o = spf_whatif_digest{0u, 0u, (uint64_t)*H};
 }
@@ -1093,8 +1215,12 @@ struct spf_whatif_plan {
   DevBuf<uint32_t> d_fails, d_link_edge, d_nbr_bit, d_dist, d_q, d_q2, d_bm, d_nhb, d_ctr;
   DevBuf<uint32_t> d_lvl, d_order, d_misc;
   DevBuf<unsigned long long> d_H;
-  DevBuf<uint2> d_hot, d_big, d_big0;
-  DevBuf<uint32_t> d_cnt;  // [0] n_hot, [1] cursor, [2] n_big (overflow), [3] n_big0 (classified)
+  DevBuf<uint2> d_hot, d_big, d_big0, d_big1;  // d_big1: d_big0 largest first
+  // [0] n_hot, [1] cursor, [2] n_big (overflow), [3] n_big0 (classified),
+  // [4] group teams' cursor
+  DevBuf<uint32_t> d_cnt;
+  DevBuf<unsigned char> d_ctl;  // group teams' TeamCtl
+  uint32_t group = 0, group_teams = 0;  // workgroups per group team (0: one-workgroup teams)
   DevBuf<uint32_t> d_parent, d_sub;
   uint32_t big_teams = 0;
   DevBuf<unsigned long long> d_prof;  // SPF_WHATIF_PROF diagnostics
@@ -1196,9 +1322,12 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   for (uint32_t j = 0; j < k; ++j) nbr_bit[c->nb_id[c->nb_ptr[src] + j]] = j;
   p->W = std::max<uint32_t>(1, (k + 31) / 32);
   {  // wave teams: 8 per CU (2 waves per SIMD) within the scratch budget
+     // (SPF_WHATIF_WAVES=<per CU>, a multiple of 4: A/B)
+    const char* e = std::getenv("SPF_WHATIF_WAVES");
+    const size_t per_cu = e ? std::max(4, atoi(e) & ~3) : 8;
     const size_t per_team = 4ull * (N + kWaveCap * (4ull + p->W) + kWaveCap + 1);
     const size_t fit = std::max<size_t>(4, kWaveScratch / per_team) & ~size_t(3);
-    p->wave_teams = (uint32_t)std::min<size_t>(4ull * 2 * c->n_cu, fit);
+    p->wave_teams = (uint32_t)std::min<size_t>(per_cu * c->n_cu, fit);
   }
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, p->d_fails.upload(fails.data(), fails.size(), c->stream));
@@ -1217,6 +1346,7 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->d_hot.alloc(std::max<uint32_t>(1, p->n_fail)));
   HIP_TRY(c, p->d_big.alloc(std::max<uint32_t>(1, p->n_fail)));
   HIP_TRY(c, p->d_big0.alloc(std::max<uint32_t>(1, p->n_fail)));
+  HIP_TRY(c, p->d_big1.alloc(std::max<uint32_t>(1, p->n_fail)));
   HIP_TRY(c, p->d_parent.alloc(N));
   HIP_TRY(c, p->d_sub.alloc(N));
   if (!c->side) {  // the classified big failures' workgroup teams run here
@@ -1224,7 +1354,7 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
     HIP_TRY(c, hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming));
     HIP_TRY(c, hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming));
   }
-  HIP_TRY(c, p->d_cnt.alloc(4));
+  HIP_TRY(c, p->d_cnt.alloc(8));
   const size_t wt = p->wave_teams;
   HIP_TRY(c, p->w_mark.alloc(wt * N));
   HIP_TRY(c, p->w_dlist.alloc(wt * kWaveCap));
@@ -1237,6 +1367,20 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
     p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / 2 / per_team));
   }
   const size_t bt = p->big_teams;
+  {  // group teams over the concurrent (c_*) scratch sets: G workgroups each,
+     // n_cu / G teams (a multiple of 8: members share an XCD), no more teams
+     // than scratch sets (SPF_WHATIF_GROUP=1: one-workgroup teams, A/B)
+    const char* e = std::getenv("SPF_WHATIF_GROUP");
+    uint32_t G = e ? (uint32_t)atoi(e) : 4u;
+    if (G > 1) {
+      while (G <= 16 && (c->n_cu / G > bt || (c->n_cu / G) % 8)) G *= 2;
+      if (G <= 16 && c->n_cu % (8 * G) == 0 && c->n_cu / G >= 8) {
+        p->group = G;
+        p->group_teams = c->n_cu / G;
+        HIP_TRY(c, p->d_ctl.alloc(sizeof(TeamCtl) * p->group_teams));
+      }
+    }
+  }
   HIP_TRY(c, p->b_mark.alloc(bt * N));
   HIP_TRY(c, p->b_dlist.alloc(bt * N));
   HIP_TRY(c, p->b_dnew.alloc(bt * N));
@@ -1304,7 +1448,8 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   // 2. failures
-  HIP_TRY(c, hipMemsetAsync(p->d_cnt.p, 0, 16, s));
+  HIP_TRY(c, hipMemsetAsync(p->d_cnt.p, 0, 32, s));
+  if (p->group) HIP_TRY(c, hipMemsetAsync(p->d_ctl.p, 0, sizeof(TeamCtl) * p->group_teams, s));
   if (p->n_fail) {
     hipLaunchKernelGGL(classify_kernel, dim3((p->n_fail + 255) / 256), dim3(256), 0, s, g,
                        p->d_dist.p, p->d_H.p, p->d_fails.p, p->n_fail, p->d_link_edge.p,
@@ -1320,6 +1465,18 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
       HIP_TRY(c, hipEventRecord(c->side_fork, s));
       HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_fork, 0));
     }
+    bool grouped = false;
+    if (p->group) {
+      hipLaunchKernelGGL(sort_big_kernel, dim3(1), dim3(1024), 0, side, p->d_big0.p, p->d_cnt.p + 3,
+                         p->d_sub.p, c->d_col.p, p->d_big1.p);
+      HIP_TRY(c, hipGetLastError());
+      GroupArgs ga{g, B, p->d_big1.p, p->d_cnt.p + 3, p->d_cnt.p + 4,
+                   reinterpret_cast<TeamCtl*>(p->d_ctl.p), p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
+                   p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p};
+      grouped = launch_group(p->group, ga, c->n_cu, side) == hipSuccess;
+      if (!grouped) (void)hipGetLastError();  // fall back to one-workgroup teams
+    }
+    if (!grouped)
     hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, side, g, B,
                        p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
                        p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p);
