@@ -1321,10 +1321,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   const uint32_t k = c->nb_ptr[src + 1] - c->nb_ptr[src];
   for (uint32_t j = 0; j < k; ++j) nbr_bit[c->nb_id[c->nb_ptr[src] + j]] = j;
   p->W = std::max<uint32_t>(1, (k + 31) / 32);
-  {  // wave teams: 8 per CU (2 waves per SIMD) within the scratch budget
-     // (SPF_WHATIF_WAVES=<per CU>, a multiple of 4: A/B)
+  {  // wave teams: 12 per CU (3 waves per SIMD beside the group teams' 2;
+     // 8: 23.3 ms, 12: 20.1, 16: 22.7 on the 1M-link graph, r02_v30) within
+     // the scratch budget (SPF_WHATIF_WAVES=<per CU>, a multiple of 4: A/B)
     const char* e = std::getenv("SPF_WHATIF_WAVES");
-    const size_t per_cu = e ? std::max(4, atoi(e) & ~3) : 8;
+    const size_t per_cu = e ? std::max(4, atoi(e) & ~3) : 12;
     const size_t per_team = 4ull * (N + kWaveCap * (4ull + p->W) + kWaveCap + 1);
     const size_t fit = std::max<size_t>(4, kWaveScratch / per_team) & ~size_t(3);
     p->wave_teams = (uint32_t)std::min<size_t>(per_cu * c->n_cu, fit);

@@ -245,7 +245,7 @@ def test_copy_narrow_rows(name, make, srcs, monkeypatch):
         monkeypatch.setenv("SPF_MSBFS", "masks")
     names, eng, orc = load(make())
     ids = list(range(len(names)))[srcs]
-    plan = eng.plan(ids)
+    plan = eng.plan(ids, hop=True)  # the ring's metrics are not unit: hop counts
     assert plan.row_mode() != "u32"
     pitch, m = eng.pitch, len(ids)
     d32 = DeviceArray(m * pitch, np.uint32)
