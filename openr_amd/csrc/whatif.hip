@@ -224,19 +224,42 @@ struct BaseArgs {
 __device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* dist,
                                             const uint32_t* nhb, uint32_t v, uint32_t j,
                                             uint32_t first = 0, uint32_t stride = 1) {
+  // edges in groups of 4, each stage's loads issued together: the column and
+  // reverse-edge ids, then the tails' distances / drain bytes / metrics, then
+  // the tight tails' words -- three memory round trips per group where an
+  // edge-at-a-time loop made three per edge
   const uint32_t dv = dist[v];
   uint32_t acc = 0;
-  for (uint32_t e = g.row_ptr[v] + first; e < g.row_ptr[v + 1]; e += stride) {
-    const uint32_t u = g.col[e];
-    if (g.ovl[u] && u != g.src) continue;
-    const uint32_t du = ld(&dist[u]);
-    if (du == kInf || du + in_w(g, e) != dv) continue;
-    if (u == g.src) {
-      const uint32_t jb = g.nbr_bit[v];
-      if ((jb >> 5) == j) acc |= 1u << (jb & 31);
-    } else {
-      acc |= ld(&nhb[(size_t)u * g.W + j]);
+  const uint32_t e1 = g.row_ptr[v + 1];
+  for (uint32_t e = g.row_ptr[v] + first; e < e1; e += 4 * stride) {
+    uint32_t u[4], r[4], du[4], w[4], x[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t ek = e + k * stride;
+      ok[k] = ek < e1;
+      u[k] = ok[k] ? g.col[ek] : 0u;
+      r[k] = ok[k] && !g.hop ? g.rev[ek] : 0u;
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      du[k] = ok[k] ? ld(&dist[u[k]]) : kInf;
+      w[k] = ok[k] ? (g.hop ? 1u : g.wt[r[k]]) : 0u;
+      if (ok[k] && g.ovl[u[k]] && u[k] != g.src) du[k] = kInf;  // drained: not expanded
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = 0;
+      if (du[k] != kInf && du[k] + w[k] == dv) {
+        if (u[k] == g.src) {
+          const uint32_t jb = g.nbr_bit[v];
+          if ((jb >> 5) == j) x[k] = 1u << (jb & 31);
+        } else {
+          x[k] = ld(&nhb[(size_t)u[k] * g.W + j]);
+        }
+      }
+    }
+    acc |= x[0] | x[1] | x[2] | x[3];
   }
   return acc;
 }
@@ -281,13 +304,27 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
         const uint32_t first = __shfl(u, __builtin_ctzll(tight), 64);
         if (lane == 0) st(&parent[v], first);
       }
-      for (uint64_t t = tight; t; t &= t - 1) {
-        const uint32_t tu = __shfl(u, __builtin_ctzll(t), 64);
-        if (tu == g.src) {
-          const uint32_t jb = g.nbr_bit[v];
-          if (j == (jb >> 5)) acc |= 1u << (jb & 31);
-        } else if (j < W) {
-          acc |= ld(&nhb[(size_t)tu * W + j]);
+      // the tight tails' words 8 at a time, their loads issued together
+      for (uint64_t t = tight; t;) {
+        uint32_t tu[8], x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          tu[q] = kInf;
+          if (t) {  // wave-uniform
+            tu[q] = __shfl(u, __builtin_ctzll(t), 64);
+            t &= t - 1;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          x[q] = tu[q] != kInf && tu[q] != g.src && j < W ? ld(&nhb[(size_t)tu[q] * W + j]) : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          acc |= x[q];
+          if (tu[q] == g.src) {
+            const uint32_t jb = g.nbr_bit[v];
+            if (j == (jb >> 5)) acc |= 1u << (jb & 31);
+          }
         }
       }
     }
@@ -805,8 +842,10 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         // row and from may alias as far as the compiler knows: batches of 8
         // loads ahead of their stores keep the loads in flight together
         // instead of one load-OR-store round trip per word
+        // (wave teams: batches of 4, the registers they can spare beside the
+        // group teams sharing their SIMDs)
         uint32_t j = 0;
-        if (TEAM >= 512)  // workgroup / group teams only: costs the wave teams occupancy
+        if (TEAM >= 512)
           for (; j + 8 <= W; j += 8) {
             uint32_t f[8], r[8];
 #pragma unroll
@@ -816,6 +855,15 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
 #pragma unroll
             for (int q = 0; q < 8; ++q) row[j + q] = r[q] | f[q];
           }
+        for (; j + 4 <= W; j += 4) {
+          uint32_t f[4], r[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) f[q] = from[j + q];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) r[q] = row[j + q];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) row[j + q] = r[q] | f[q];
+        }
         for (; j < W; ++j) row[j] |= from[j];
       }
     }
