@@ -152,7 +152,8 @@ spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
 // metrics and no drains for distances TO the rows' nodes).
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
                        const uint32_t* ign, uint32_t* D, hipStream_t s,
-                       const uint32_t* wt = nullptr, const uint8_t* ovl = nullptr);
+                       const uint32_t* wt = nullptr, const uint8_t* ovl = nullptr,
+                       uint8_t* Dn = nullptr);
 // Single-source SSSP in global memory, one cooperative grid (any graph
 // size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,

@@ -106,7 +106,8 @@ __global__ __launch_bounds__(THREADS) void sssp_kernel(
     const uint32_t* __restrict__ wt, const uint8_t* __restrict__ ovl,
     const uint32_t* __restrict__ link, const uint32_t* __restrict__ ign,
     const uint32_t* __restrict__ rows_src, uint32_t N, uint32_t pitch,
-    uint32_t bm_words, uint32_t big_cap, uint32_t* __restrict__ D) {
+    uint32_t bm_words, uint32_t big_cap, uint32_t* __restrict__ D,
+    uint8_t* __restrict__ Dn /* optional u8 copy (npitch == pitch) */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* dist = reinterpret_cast<uint32_t*>(smem);  // [pitch]
   uint32_t* bm = dist + pitch;                         // [bm_words] next frontier
@@ -210,10 +211,21 @@ __global__ __launch_bounds__(THREADS) void sssp_kernel(
   }
   __syncthreads();
 
-  // ---- write the distance row (16-byte stores) ----
+  // ---- write the distance row (16-byte stores) and, for narrow plans, its
+  // u8 copy (min(d, 254), 255 = unreachable) for the next-hop pass ----
   uint4* out = reinterpret_cast<uint4*>(D + (size_t)row * pitch);
   const uint4* in = reinterpret_cast<const uint4*>(dist);
-  for (uint32_t i = tid; i < pitch / 4; i += THREADS) out[i] = in[i];
+  for (uint32_t i = tid; i < pitch / 4; i += THREADS) {
+    const uint4 d = in[i];
+    out[i] = d;
+    if (Dn) {
+      const uint32_t x[4] = {d.x, d.y, d.z, d.w};
+      uint32_t b = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) b |= (x[k] == kInf ? 0xFFu : min(x[k], 254u)) << (8 * k);
+      reinterpret_cast<uint32_t*>(Dn + (size_t)row * pitch)[i] = b;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -811,6 +823,31 @@ __device__ __forceinline__ uint32_t eq_mask16(const uint4& a, const uint4& t) {
   return x ^ d ^ (d << 6);
 }
 
+// Weighted narrow match: byte targets d_s(v) - w of the lane's 16
+// destinations (word q, byte b = destination 4q + b) and the mask of those
+// with a target at all, in eq_mask16's bit order: d_s(v) >= w (v is neither
+// the source nor closer than the link) and d_s(v) < 254 (the wave takes the
+// exact u32 path when any byte of its source slice saturated).  A neighbour
+// byte equals a valid target (< 254) only if it is that exact distance.
+__device__ __forceinline__ uint32_t weighted_targets16(const uint4& raw, uint32_t w, uint4* t) {
+  const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+  uint32_t tt[4], valid = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t x = (rw[q] >> (8 * b)) & 0xFFu;
+      const bool ok = x >= w && x < 0xFEu;
+      o |= (ok ? x - w : 0xFEu) << (8 * b);
+      valid |= (uint32_t)ok << (4 * q + b);
+    }
+    tt[q] = o;
+  }
+  *t = make_uint4(tt[0], tt[1], tt[2], tt[3]);
+  return valid;
+}
+
 // nb_row[nb_row_off[i] + j]: byte offset in Dn (row * npitch) of the narrow
 // row of the request's source i's neighbour j (ascending id) -- the D row
 // itself for plans without narrow rows -- or `dead` if it is drained: the
@@ -826,7 +863,7 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     const uint32_t* __restrict__ row_of, const uint32_t* __restrict__ nb_ptr,
     const uint32_t* __restrict__ nb_id, const uint32_t* __restrict__ nb_w,
     const uint32_t* __restrict__ nb_row, const uint32_t* __restrict__ nb_row_off,
-    const uint32_t* __restrict__ nb_drained, uint32_t dead, uint32_t hop,
+    const uint32_t* __restrict__ nb_drained, uint32_t dead, uint32_t hop, uint32_t weighted,
     const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh, uint32_t chunks,
     const uint32_t* __restrict__ slot_src) {
   // Block b runs on XCD b % 8.  slot_src (spf_plan_create) lists each XCD's
@@ -854,9 +891,10 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
   // neighbour where the source row is not saturated: d_x(s) = w(x, s) < 0xFE,
   // and a node s cannot reach no neighbour reaches either)
   uint4 tg = make_uint4(0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu, 0xFEFEFEFEu);
+  uint4 raw = tg;  // the source's 16 bytes (weighted matches derive targets per neighbour)
   bool exact = !NARROW;
   if (NARROW) {
-    const uint4 raw = *reinterpret_cast<const uint4*>(Dn + (size_t)srow * npitch + cbase + lane * 16);
+    raw = *reinterpret_cast<const uint4*>(Dn + (size_t)srow * npitch + cbase + lane * 16);
     const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
     uint32_t t[4];
     bool sat = false;
@@ -896,7 +934,14 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
 #pragma unroll
       for (int u = 0; u < kEcmpUnroll; ++u) {
         if (j0 + u >= k) break;
-        const uint32_t m = eq_mask16(r[u], tg);
+        uint32_t m;
+        if (weighted) {  // wave-uniform: targets d_s - w(s, x) per neighbour
+          uint4 tw;
+          const uint32_t valid = weighted_targets16(raw, nb_w[nb0 + j0 + u], &tw);
+          m = eq_mask16(r[u], tw) & valid;
+        } else {
+          m = eq_mask16(r[u], tg);
+        }
         uint16_t* o = reinterpret_cast<uint16_t*>(out_w + (size_t)(j0 + u) * wpm);
         if (st) o[lane] = (uint16_t)m;
       }
@@ -1788,13 +1833,16 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
-  p->narrow = p->ms && use_narrow(c, p);
+  // weighted plans keep a u8 copy too when the pitches agree (the sssp
+  // kernel writes it beside the u32 row; the next-hop pass compares bytes and
+  // falls back to u32 rows per wave where the source's row saturates)
+  p->narrow = (p->ms || c->pitch == c->npitch) && use_narrow(c, p);
   // bit-sliced rows behind the per-level-store BFS (it reports the deepest
   // level); the register-plane BFS serves deep graphs, where planes would
   // not pay.  SPF_NARROW=1 keeps the byte-row pass (experiments, tests).
   {
     const char* e = std::getenv("SPF_NARROW");
-    p->sliced = p->narrow && !use_planes(c) && !(e && e[0] == '1');
+    p->sliced = p->ms && p->narrow && !use_planes(c) && !(e && e[0] == '1');
     // SPF_EXPAND=1 (A/B; measured slower): the BFS stores the u8
     // rows only and the slicing pass expands them into the u32 rows.  By
     // default the BFS stores both: its u32 stores drain behind its
@@ -2014,7 +2062,7 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
     bfs = groups * (csr + N) + (p->expand ? 0ull : rows * c->pitch * 4ull) +
           (p->narrow ? rows * c->npitch : 0ull);
   } else {
-    bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch);
+    bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch + (p->narrow ? c->npitch : 0ull));
   }
   *bfs_bytes = bfs;
   if (p->sliced && p->nh_total) {
@@ -2058,7 +2106,7 @@ namespace spfi {
 // Launch the SSSP kernel over `rows` closure rows (device list rows_src).
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
                        const uint32_t* ign, uint32_t* D, hipStream_t s, const uint32_t* wt,
-                       const uint8_t* ovl) {
+                       const uint8_t* ovl, uint8_t* Dn) {
   if (!wt) wt = c->d_wt.p;
   if (!ovl) ovl = c->d_ovl.p;
   const uint32_t N = c->N, pitch = c->pitch, bm_words = (N + 31) / 32;
@@ -2073,7 +2121,7 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 #define SSSP_LAUNCH(QT, U, TH)                                                            \
   hipLaunchKernelGGL((sssp_kernel<QT, U, TH>), g, dim3(TH), lds, s, c->d_row_ptr.p,       \
                      c->d_col.p, wt, ovl, c->d_link.p, ign, rows_src, N, pitch, bm_words,  \
-                     c->big_nodes, D)
+                     c->big_nodes, D, Dn)
 #define SSSP_TH(QT, U)                                  \
   do {                                                  \
     if (threads >= 1024) SSSP_LAUNCH(QT, U, 1024);      \
@@ -2205,9 +2253,11 @@ spf_status launch_ecmp(spf_ctx* c, spf_plan* p, const uint8_t* Dn, const uint32_
   const uint32_t per_block = kEcmpChunk * kEcmpWaves;
   const uint32_t chunks = (c->N + per_block - 1) / per_block;
   const uint32_t nb = chunks * (uint32_t)p->slots;
+  const uint32_t weighted = NARROW && !hop && !c->unit ? 1u : 0u;
   hipLaunchKernelGGL((ecmp_kernel<NARROW>), dim3(nb), dim3(kEcmpThreads), 0, s, Dn, c->npitch, D,
                      c->pitch, c->N, p->d_srcs.p, p->d_row_of.p, c->d_nb_ptr.p, c->d_nb_id.p,
-                     c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead, hop ? 1u : 0u,
+                     c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p, p->d_nb_drained.p, p->dead,
+                     hop ? 1u : 0u, weighted,
                      p->d_nh_off.p, d_nh, chunks, p->d_slot_src.p);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
@@ -2334,7 +2384,8 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                        sliced ? p->d_maxd.p : nullptr, s,
                                        sliced && p->expand ? kSlSat : 0u)
-                        : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s);
+                        : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s, nullptr,
+                                      nullptr, p->narrow ? p->d_Dn.p : nullptr);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   if (sliced) {

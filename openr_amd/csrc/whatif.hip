@@ -288,16 +288,30 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
   for (uint32_t j0 = 0; j0 < W; j0 += 64) {
     const uint32_t j = j0 + lane;
     uint32_t acc = 0;
-    for (uint32_t eb = e0; eb < e1; eb += 64) {
-      const uint32_t e = eb + lane;
-      uint32_t u = kInf;
-      if (e < e1) {
-        const uint32_t cu = g.col[e];
-        if (!g.ovl[cu] || cu == g.src) {
-          const uint32_t du = ld(&dist[cu]);
-          if (du != kInf && du + in_w(g, e) == dv) u = cu;
-        }
+    // 4 chunks of 64 in-edges per pass, each stage's loads issued together
+    // (ids, then the tails' distances / drains / metrics): a hub's scan was
+    // one dependent round trip chain per 64 edges and set its level's time
+    for (uint32_t eb4 = e0; eb4 < e1; eb4 += 256) {
+    uint32_t cu4[4], r4[4], u4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t e = eb4 + q * 64 + lane;
+      cu4[q] = e < e1 ? g.col[e] : kInf;
+      r4[q] = e < e1 && !g.hop ? g.rev[e] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      u4[q] = kInf;
+      if (cu4[q] != kInf) {
+        const uint32_t cu = cu4[q];
+        const uint32_t du = ld(&dist[cu]);
+        const uint32_t w = g.hop ? 1u : g.wt[r4[q]];
+        if ((!g.ovl[cu] || cu == g.src) && du != kInf && du + w == dv) u4[q] = cu;
       }
+    }
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {  // chunks in CSR order: the first tight tail is the parent
+      const uint32_t u = u4[c4];
       const uint64_t tight = __ballot(u != kInf);
       if (tight && !have_parent) {  // wave-uniform
         have_parent = true;
@@ -327,6 +341,7 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
           }
         }
       }
+    }
     }
     if (j < W) st(&nhb[(size_t)v * W + j], acc);
   }

@@ -262,3 +262,21 @@ def test_copy_narrow_rows(name, make, srcs, monkeypatch):
     finally:
         for x in (d32, nh, d8):
             x.free()
+
+
+@pytest.mark.parametrize("narrow", ["0", "1"])
+@pytest.mark.parametrize("name,make", [
+    ("fabric_rtt600", lambda: T.fabric_rtt(num_sws=600)),
+    ("wan_dense", lambda: T.random_graph(400, 3200, 5, max_metric=40, overload_frac=0.05)),
+    ("wan_deep", lambda: T.random_graph(500, 2600, 9, max_metric=600)),  # rows saturate at 254
+], ids=["fabric_rtt", "dense_drained", "deep"])
+def test_weighted_narrow_rows(name, make, narrow, monkeypatch):
+    """Weighted plans with a u8 copy of the rows (the next-hop pass matches
+    bytes against d_s - w(s, x) per neighbour, exact u32 rows where a
+    source slice saturates) and without (SPF_NARROW=0): every source's
+    distances and next hops against the oracle."""
+    monkeypatch.setenv("SPF_NARROW", narrow)
+    names, eng, orc = load(make())
+    plan = eng.plan([0])
+    assert plan.row_mode() == ("u8" if narrow == "1" else "u32")
+    compare(names, eng, orc, list(range(len(names))))
