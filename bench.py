@@ -696,7 +696,8 @@ def main() -> None:
         try:
             pj = json.loads(pmc.read_text())
             for kname, kv in pj.get("per_kernel", {}).items():
-                if kname.startswith(dominant):
+                # (the staged-graph KSP2 kernel is ksp2_lds_kernel)
+                if kname.startswith(dominant) or kname.replace("_lds", "").startswith(dominant):
                     traffic = kv["fetch_bytes_x2"] + kv["write_bytes"]
                     traffic_src = (f"{pmc.relative_to(ROOT)} ({pj.get('source', 'rocprofv3 --pmc')}"
                                    f"; kernel {kname}; FETCH_SIZE x2 + WRITE_SIZE)")
