@@ -41,7 +41,7 @@ namespace {
 constexpr int kKspThreads = 256;             // 4 waves, one pair each
 constexpr int kKspWaves = kKspThreads / 64;
 constexpr int kKspLdsMaxThreads = 1024;      // staged-graph kernel: up to 16 waves
-constexpr uint32_t kKspChunk = 64;          // destinations per workgroup
+constexpr uint32_t kKspChunk = 64;          // sources per workgroup (default; SPF_KSP2_CHUNK)
 constexpr uint32_t kPoolGrab = 2048;        // words a wave reserves at a time
 constexpr size_t kMaxLdsKsp = 160 * 1024;
 
@@ -217,10 +217,18 @@ __device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint3
 // expanded.  Every node with exact D + H <= the final D[dst] -- all the
 // nodes a trace to dst can inspect as tight tails -- ends exact (induction
 // along its shortest path, whose nodes all satisfy the same bound).
+// Expansion is ordered by f = D + H in buckets of width `delta`: a pending
+// node with f > T stays pending (its bitmap bit is set again), and when a
+// sweep expands nothing T moves to the smallest pending f + the width, which
+// doubles on each move.  Without
+// the order the sweep is a hop-synchronous Bellman-Ford that reaches dst only
+// after expanding every node within dst's hop count (bound D[dst] = inf
+// until then); with it, only nodes with f < d2(dst) + delta are expanded.
+// The fixpoint -- and so every distance the trace reads -- is the same.
 template <class G>
 __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, uint32_t bm_words,
                           const uint32_t* ign, uint32_t src, uint32_t dst, uint32_t pitch,
-                          const uint32_t* H) {
+                          const uint32_t* H, uint32_t delta) {
   const uint32_t lane = __lane_id();
   for (uint32_t v = lane; v < pitch; v += 64) D[v] = kInf;
   for (uint32_t i = lane; i < bm_words; i += 64) bm[i] = 0;
@@ -231,13 +239,24 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
   }
   wave_sync();
   uint32_t qlen = 1;
+  uint64_t width = delta;
+  uint64_t T = (uint64_t)H[src] + width;  // expand pending nodes with f <= T
   while (qlen) {
+    uint64_t defer_f = ~0ull;  // smallest f left pending by this lane
+    bool expanded = false;
     for (uint32_t i = lane; i < qlen; i += 64) {
       const uint32_t u = q[i];
       if (g.ovl(u) && u != src) continue;  // drained: recorded, not expanded
       const uint32_t du = D[u];
       const uint32_t bound = D[dst];
-      if ((uint64_t)du + H[u] > bound || u == dst) continue;
+      const uint64_t f = (uint64_t)du + H[u];
+      if (f > bound || u == dst) continue;
+      if (f > T) {  // a later bucket: stays pending
+        atomicOr(&bm[u >> 5], 1u << (u & 31));
+        defer_f = min(defer_f, f);
+        continue;
+      }
+      expanded = true;
       const uint32_t e_end = g.rp(u + 1);
       for (uint32_t e = g.rp(u); e < e_end; ++e) {
         if (bit(ign, g.link(e))) continue;
@@ -246,6 +265,13 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
         const uint32_t hv = H[v];
         if (hv == kInf || (uint64_t)nd + hv > bound) continue;
         if (nd < atomicMin(&D[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+      }
+    }
+    if (!__ballot(expanded)) {  // everything pending lies past T: next bucket,
+      const uint64_t m = wave_min64(defer_f);  // twice as wide (a long detour or
+      if (m != ~0ull) {                        // an unreachable dst: log2 raises)
+        width = min(2ull * width, 0xFFFFFFFFull);
+        T = m + width;
       }
     }
     wave_sync();
@@ -275,7 +301,8 @@ struct KspArgs {
   const uint32_t* Dsrc;   // [n_src][pitch] SPF rows of the sources
   const uint32_t* Hrows;  // [N][pitch] distances TO each node (transposed SPF)
   const uint32_t* srcs;
-  uint32_t n_src, pitch, lw, chunks;
+  uint32_t n_src, pitch, lw, chunks, chunk;
+  uint32_t delta;  // bucket width of the k = 2 SPF's f = D + H order
   spf_ksp2_pair* pairs;
   uint32_t* pool;
   uint64_t cap;
@@ -309,7 +336,7 @@ __device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint
 
   const uint32_t d = blockIdx.x / a.chunks;
   const uint32_t c = blockIdx.x % a.chunks;
-  const uint32_t i_end = min(a.n_src, (c + 1) * kKspChunk);
+  const uint32_t i_end = min(a.n_src, (c + 1) * a.chunk);
   unsigned long long* used = a.counters;
   uint32_t* overflow = reinterpret_cast<uint32_t*>(a.counters + 2);
   PoolCursor pc;
@@ -352,7 +379,7 @@ __device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint
       if (n1) {
         ++k2_runs;
         wave_sync();
-        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch, H);
+        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch, H, a.delta);
         if (a.prof) t2 = __builtin_amdgcn_s_memtime();
         if (Dw[d] != kInf) {
           for (uint32_t j = lane; j < lw; j += 64) vis[j] = 0;
@@ -384,7 +411,7 @@ __device__ void stage_heuristic_row(const KspArgs& a, uint32_t* H, uint32_t* ctl
   const uint4* in = reinterpret_cast<const uint4*>(a.Hrows + (size_t)d * a.pitch);
   uint4* o = reinterpret_cast<uint4*>(H);
   for (uint32_t t = threadIdx.x; t < a.pitch / 4; t += blockDim.x) o[t] = in[t];
-  if (threadIdx.x == 0) ctl[0] = c * kKspChunk;
+  if (threadIdx.x == 0) ctl[0] = c * a.chunk;
 }
 
 // Graph in HBM: 4 waves per workgroup, 32-bit DFS stack.
@@ -444,6 +471,8 @@ size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw,
 struct spf_ksp2_plan {
   spf_ctx* ctx = nullptr;
   uint32_t n_src = 0, lw = 0;
+  uint32_t delta = 0;  // bucket width of the k = 2 SPF (KspArgs::delta)
+  uint32_t chunk = kKspChunk;  // sources per workgroup
   uint64_t epoch = 0;  // graph state the plan was derived from
   std::vector<uint32_t> srcs;
   DevBuf<uint32_t> d_srcs, d_D, d_H, d_all, d_wt_rev;
@@ -478,6 +507,14 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   for (uint32_t i = 0; i < n_src; ++i)
     if (srcs[i] >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
   p->lw = c->max_link / 32 + 1;
+  {  // bucket width: the mean up-link metric (env SPF_KSP2_DELTA overrides;
+     // 4294967295 = no order, the plain hop-synchronous sweep)
+    uint64_t sum = 0;
+    for (uint32_t e = 0; e < c->E; ++e) sum += c->wt[e];
+    p->delta = c->E ? (uint32_t)std::max<uint64_t>(1, sum / c->E) : 1;
+    if (const char* env = std::getenv("SPF_KSP2_DELTA")) p->delta = (uint32_t)std::strtoul(env, nullptr, 10);
+    if (const char* env = std::getenv("SPF_KSP2_CHUNK")) p->chunk = std::max(1ul, std::strtoul(env, nullptr, 10));
+  }
   // graph staged in LDS when its 16-bit copy fits beside >= 2 waves
   if (c->E < 65536 && c->max_metric < 65536 && c->max_link < 65536 && !std::getenv("SPF_KSP2_HBM")) {
     for (uint32_t w = kKspLdsMaxThreads / 64; w >= 2; --w)
@@ -549,9 +586,9 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   GGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p, c->N};
-  // blocks: (destination, chunk of kKspChunk sources)
-  const uint32_t chunks = (p->n_src + kKspChunk - 1) / kKspChunk;
-  KspArgs a{p->d_D.p, p->d_H.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, d_pairs,
+  // blocks: (destination, chunk of p->chunk sources)
+  const uint32_t chunks = (p->n_src + p->chunk - 1) / p->chunk;
+  KspArgs a{p->d_D.p, p->d_H.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, p->chunk, p->delta, d_pairs,
             d_pool, pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p};
   if (p->lds_waves)
     hipLaunchKernelGGL(ksp2_lds_kernel, dim3(c->N * chunks), dim3(64 * p->lds_waves), p->lds, s,
