@@ -92,23 +92,30 @@ struct GGraph {
   __device__ uint32_t col(uint32_t e) const { return col_[e]; }
   __device__ uint32_t w(uint32_t e) const { return wt[e]; }
   __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
-  __device__ uint32_t link(uint32_t e) const { return link_[e]; }
+  __device__ uint32_t link(uint32_t e) const { return link_[e]; }  // bitmap index
+  __device__ uint32_t out_link(uint32_t e) const { return link_[e]; }  // pool record
   __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
 };
 
+// The staged graph indexes its link bitmaps by the edge pair {e, rev(e)}
+// (min of the two ids) instead of the link id: an up link is exactly one
+// such pair (checked when the plan is made), and the 16-bit link array then
+// stays out of LDS -- room for one more wave per workgroup.  Pool records
+// still carry link ids, read from HBM.
 struct LGraph {
   const uint16_t* row_ptr;  // [N+1] (E < 65536)
   const uint16_t* col_;
   const uint16_t* wt;       // metrics < 65536
   const uint16_t* rev_;
-  const uint16_t* link_;    // link ids < 65536
+  const uint32_t* glink;    // link ids (HBM)
   const uint8_t* ovl_;
   uint32_t N;
   __device__ uint32_t rp(uint32_t v) const { return row_ptr[v]; }
   __device__ uint32_t col(uint32_t e) const { return col_[e]; }
   __device__ uint32_t w(uint32_t e) const { return wt[e]; }
   __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
-  __device__ uint32_t link(uint32_t e) const { return link_[e]; }
+  __device__ uint32_t link(uint32_t e) const { return min(e, (uint32_t)rev_[e]); }
+  __device__ uint32_t out_link(uint32_t e) const { return glink[e]; }
   __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
 };
 
@@ -197,9 +204,12 @@ __device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint3
   const uint32_t lane = __lane_id();
   const uint32_t at = pool_alloc(pc, depth + 2, used, cap, overflow);
   for (uint32_t j = lane; j < depth; j += 64) {
-    const uint32_t l = g.link(stack[depth - 1 - j]);  // src -> dst order
-    if (mark) atomicOr(&mark[l >> 5], 1u << (l & 31));
-    if (at != kInf) pool[(size_t)at + 2 + j] = l;
+    const uint32_t e = stack[depth - 1 - j];  // src -> dst order
+    if (mark) {
+      const uint32_t l = g.link(e);
+      atomicOr(&mark[l >> 5], 1u << (l & 31));
+    }
+    if (at != kInf) pool[(size_t)at + 2 + j] = g.out_link(e);
   }
   if (at != kInf && lane == 0) {
     pool[at] = depth;
@@ -436,20 +446,18 @@ __global__ __launch_bounds__(kKspLdsMaxThreads) void ksp2_lds_kernel(GGraph gg, 
   uint16_t* col = rp + 2 * rp_words;
   uint16_t* wt = col + 2 * e_words;
   uint16_t* rev = wt + 2 * e_words;
-  uint16_t* link = rev + 2 * e_words;
-  uint8_t* ovl = reinterpret_cast<uint8_t*>(link + 2 * e_words);
+  uint8_t* ovl = reinterpret_cast<uint8_t*>(rev + 2 * e_words);
   uint32_t* wave_base = reinterpret_cast<uint32_t*>(ovl + ((N + 3) & ~3u));
   for (uint32_t v = threadIdx.x; v <= N; v += blockDim.x) rp[v] = (uint16_t)gg.row_ptr[v];
   for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
     col[e] = (uint16_t)gg.col_[e];
     wt[e] = (uint16_t)gg.wt[e];
     rev[e] = (uint16_t)gg.rev_[e];
-    link[e] = (uint16_t)gg.link_[e];
   }
   for (uint32_t v = threadIdx.x; v < N; v += blockDim.x) ovl[v] = gg.ovl_[v];
   stage_heuristic_row(a, H, ctl);
   __syncthreads();
-  const LGraph g{rp, col, wt, rev, link, ovl, N};
+  const LGraph g{rp, col, wt, rev, gg.link_, ovl, N};
   ksp2_block<LGraph, uint16_t>(g, a, H, ctl, wave_base);
 }
 
@@ -462,7 +470,7 @@ size_t ksp2_lds_bytes(uint32_t N, uint32_t pitch, uint32_t lw) {
 size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw,
                             uint32_t waves) {
   const size_t bm_words = (N + 31) / 32;
-  const size_t graph = 4ull * ((N + 2) / 2 + 4ull * ((E + 1) / 2)) + ((N + 3) & ~3u);
+  const size_t graph = 4ull * ((N + 2) / 2 + 3ull * ((E + 1) / 2)) + ((N + 3) & ~3u);
   return 4ull * (pitch + 4) + graph + 4ull * waves * wave_lds_words<uint16_t>(pitch, bm_words, lw);
 }
 
@@ -515,12 +523,24 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     if (const char* env = std::getenv("SPF_KSP2_DELTA")) p->delta = (uint32_t)std::strtoul(env, nullptr, 10);
     if (const char* env = std::getenv("SPF_KSP2_CHUNK")) p->chunk = std::max(1ul, std::strtoul(env, nullptr, 10));
   }
-  // graph staged in LDS when its 16-bit copy fits beside >= 2 waves
-  if (c->E < 65536 && c->max_metric < 65536 && c->max_link < 65536 && !std::getenv("SPF_KSP2_HBM")) {
+  // graph staged in LDS when its 16-bit copy fits beside >= 2 waves and
+  // every up link is one {e, rev(e)} pair (LGraph's bitmap index)
+  bool pairs_are_links = c->E < 65536;
+  {
+    std::vector<uint8_t> seen(c->max_link + 1, 0);
+    for (uint32_t e = 0; e < c->E && pairs_are_links; ++e) {
+      const uint32_t r = c->rev[e];
+      if (r >= c->E || c->rev[r] != e || c->link[r] != c->link[e]) pairs_are_links = false;
+      else if (e <= r && seen[c->link[e]]++) pairs_are_links = false;  // one pair per link
+    }
+  }
+  if (pairs_are_links && c->max_metric < 65536 && !std::getenv("SPF_KSP2_HBM")) {
+    const uint32_t lw_pairs = c->E / 32 + 1;
     for (uint32_t w = kKspLdsMaxThreads / 64; w >= 2; --w)
-      if (ksp2_lds_graph_bytes(c->N, c->E, c->pitch, p->lw, w) <= kMaxLdsKsp) {
+      if (ksp2_lds_graph_bytes(c->N, c->E, c->pitch, lw_pairs, w) <= kMaxLdsKsp) {
         p->lds_waves = w;
-        p->lds = ksp2_lds_graph_bytes(c->N, c->E, c->pitch, p->lw, w);
+        p->lw = lw_pairs;
+        p->lds = ksp2_lds_graph_bytes(c->N, c->E, c->pitch, lw_pairs, w);
         break;
       }
   }
