@@ -61,16 +61,35 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
   return x;
 }
 
+// Exclusive prefix sum over the wave with DPP moves (no LDS round trips):
+// row_shr 1/2/4/8 inside each 16-lane row (lanes shifted in from outside the
+// row read 0), then row_bcast15 / row_bcast31 carry row totals upwards.
 __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x, uint32_t* total) {
-  const uint32_t lane = __lane_id();
   uint32_t inc = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d, 64);
-    if (lane >= (uint32_t)d) inc += y;
-  }
-  *total = __shfl(inc, 63, 64);
+  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xf, 0xf, true);  // row_shr:1
+  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xf, 0xf, true);  // row_shr:2
+  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xf, 0xf, true);  // row_shr:4
+  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xf, 0xf, true);  // row_shr:8
+  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  inc += __builtin_amdgcn_update_dpp(0u, inc, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  *total = __builtin_amdgcn_readlane(inc, 63);
   return inc - x;
+}
+
+// Minimum of the keys held by lanes 0 .. n-1 (n <= 64, wave-uniform): a
+// handful of lane reads into scalar registers for small n, the shuffle
+// reduction otherwise.
+__device__ __forceinline__ uint64_t lanes_min64(uint64_t x, uint32_t n) {
+  n = __builtin_amdgcn_readfirstlane(n);
+  if (n > 8) return wave_min64(x);
+  uint64_t m = ~0ull;
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t y = ((uint64_t)__builtin_amdgcn_readlane(hi, j) << 32) |
+                       __builtin_amdgcn_readlane(lo, j);
+    m = y < m ? y : m;
+  }
+  return m;
 }
 
 __device__ __forceinline__ bool bit(const uint32_t* bm, uint32_t i) {
@@ -132,7 +151,8 @@ __device__ uint32_t pool_alloc(PoolCursor& pc, uint32_t words, unsigned long lon
     const uint32_t grab = words > kPoolGrab ? words : kPoolGrab;
     uint64_t base = 0;
     if (__lane_id() == 0) base = atomicAdd(used, (unsigned long long)grab);
-    base = __shfl(base, 0, 64);
+    base = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(base >> 32), 0) << 32) |
+           __builtin_amdgcn_readlane((uint32_t)base, 0);
     pc.cur = base;
     pc.end = base + grab;
   }
@@ -161,8 +181,8 @@ __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, ui
     }
     const uint32_t dv = D[v];
     uint64_t best = ~0ull;
-    const uint32_t e_end = g.rp(v + 1);
-    for (uint32_t e = g.rp(v) + lane; e < e_end; e += 64) {
+    const uint32_t e_beg = g.rp(v), e_end = g.rp(v + 1);
+    for (uint32_t e = e_beg + lane; e < e_end; e += 64) {
       // in-edge u -> v is the reverse of the out-edge v -> u
       const uint32_t u = g.col(e);
       const uint32_t r = g.rev(e);
@@ -174,7 +194,7 @@ __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, ui
         if (ok) best = min(best, ((uint64_t)du << 32) | r);
       }
     }
-    best = wave_min64(best);
+    best = lanes_min64(best, min(e_end - e_beg, 64u));
     if (best == ~0ull) {  // every pathLink of v tried: back up one level
       if (k == 0) return false;
       --k;
@@ -254,7 +274,11 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
   while (qlen) {
     uint64_t defer_f = ~0ull;  // smallest f left pending by this lane
     bool expanded = false;
-    for (uint32_t i = lane; i < qlen; i += 64) {
+    // a short frontier gets 2^lg lanes per node, each taking every 2^lg-th
+    // edge: the dependent chain per lane is one or two edges, not deg(u)
+    const uint32_t lg = qlen <= 16 ? 2u : (qlen <= 32 ? 1u : 0u);
+    const uint32_t slot = lane & ((1u << lg) - 1u);
+    for (uint32_t i = lane >> lg; i < qlen; i += 64u >> lg) {
       const uint32_t u = q[i];
       if (g.ovl(u) && u != src) continue;  // drained: recorded, not expanded
       const uint32_t du = D[u];
@@ -262,13 +286,13 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
       const uint64_t f = (uint64_t)du + H[u];
       if (f > bound || u == dst) continue;
       if (f > T) {  // a later bucket: stays pending
-        atomicOr(&bm[u >> 5], 1u << (u & 31));
+        if (slot == 0) atomicOr(&bm[u >> 5], 1u << (u & 31));
         defer_f = min(defer_f, f);
         continue;
       }
       expanded = true;
       const uint32_t e_end = g.rp(u + 1);
-      for (uint32_t e = g.rp(u); e < e_end; ++e) {
+      for (uint32_t e = g.rp(u) + slot; e < e_end; e += 1u << lg) {
         if (bit(ign, g.link(e))) continue;
         const uint32_t nd = du + g.w(e);
         const uint32_t v = g.col(e);
@@ -355,7 +379,7 @@ __device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint
   for (;;) {
     uint32_t i = 0;
     if (lane == 0) i = atomicAdd(&ctl[0], 1u);
-    i = __shfl(i, 0, 64);
+    i = __builtin_amdgcn_readlane(i, 0);
     if (i >= i_end) break;
     const uint32_t s = a.srcs[i];
     const uint32_t* Drow = a.Dsrc + (size_t)i * pitch;
