@@ -77,17 +77,21 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x, uint32_t* total
 }
 
 // Minimum of the keys held by lanes 0 .. n-1 (n <= 64, wave-uniform): a
-// handful of lane reads into scalar registers for small n, the shuffle
-// reduction otherwise.
-__device__ __forceinline__ uint64_t lanes_min64(uint64_t x, uint32_t n) {
+// handful of lane reads into scalar registers for small n (*arg = the lane
+// holding it), the shuffle reduction otherwise (*arg = 64: unknown).
+__device__ __forceinline__ uint64_t lanes_min64(uint64_t x, uint32_t n, uint32_t* arg) {
   n = __builtin_amdgcn_readfirstlane(n);
+  *arg = 64;
   if (n > 8) return wave_min64(x);
   uint64_t m = ~0ull;
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   for (uint32_t j = 0; j < n; ++j) {
     const uint64_t y = ((uint64_t)__builtin_amdgcn_readlane(hi, j) << 32) |
                        __builtin_amdgcn_readlane(lo, j);
-    m = y < m ? y : m;
+    if (y < m) {
+      m = y;
+      *arg = j;
+    }
   }
   return m;
 }
@@ -112,6 +116,7 @@ struct GGraph {
   __device__ uint32_t w(uint32_t e) const { return wt[e]; }
   __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
   __device__ uint32_t link(uint32_t e) const { return link_[e]; }  // bitmap index
+  __device__ uint32_t link_of(uint32_t e, uint32_t) const { return link_[e]; }  // r = rev(e)
   __device__ uint32_t out_link(uint32_t e) const { return link_[e]; }  // pool record
   __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
 };
@@ -134,6 +139,7 @@ struct LGraph {
   __device__ uint32_t w(uint32_t e) const { return wt[e]; }
   __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
   __device__ uint32_t link(uint32_t e) const { return min(e, (uint32_t)rev_[e]); }
+  __device__ uint32_t link_of(uint32_t e, uint32_t r) const { return min(e, r); }  // r = rev(e)
   __device__ uint32_t out_link(uint32_t e) const { return glink[e]; }
   __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
 };
@@ -173,43 +179,60 @@ template <class G, class ST>
 __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, uint32_t* vis,
                           ST* stack, uint32_t src, uint32_t dst, uint32_t* depth) {
   const uint32_t lane = __lane_id();
-  uint32_t k = 0, v = dst;
+  uint32_t k = 0, v = dst, dv = D[dst];
   for (;;) {
     if (v == src) {
       *depth = k;
       return true;
     }
-    const uint32_t dv = D[v];
     uint64_t best = ~0ull;
+    uint32_t tail = 0, tl = 0;  // this lane's best candidate: tail node, link index
     const uint32_t e_beg = g.rp(v), e_end = g.rp(v + 1);
     for (uint32_t e = e_beg + lane; e < e_end; e += 64) {
-      // in-edge u -> v is the reverse of the out-edge v -> u
+      // in-edge u -> v is the reverse of the out-edge v -> u; every test's
+      // load is issued up front (two dependent LDS rounds per step)
       const uint32_t u = g.col(e);
       const uint32_t r = g.rev(e);
-      const uint32_t l = g.link(e);
-      bool ok = !(g.ovl(u) && u != src) && !bit(vis, l) && !(ign && bit(ign, l));
-      if (ok) {
-        const uint32_t du = D[u];
-        ok = du != kInf && du + g.w(r) == dv;
-        if (ok) best = min(best, ((uint64_t)du << 32) | r);
+      const uint32_t l = g.link_of(e, r);
+      const bool drained = g.ovl(u) && u != src;
+      const bool tried = bit(vis, l) || (ign && bit(ign, l));
+      const uint32_t du = D[u];
+      const uint32_t wr = g.w(r);
+      if (!drained && !tried && du != kInf && du + wr == dv) {
+        const uint64_t key = ((uint64_t)du << 32) | r;
+        if (key < best) {
+          best = key;
+          tail = u;
+          tl = l;
+        }
       }
     }
-    best = lanes_min64(best, min(e_end - e_beg, 64u));
+    uint32_t arg;
+    best = lanes_min64(best, min(e_end - e_beg, 64u), &arg);
     if (best == ~0ull) {  // every pathLink of v tried: back up one level
       if (k == 0) return false;
       --k;
       v = k == 0 ? dst : g.col(g.rev(stack[k - 1]));
+      dv = D[v];
       continue;
     }
     const uint32_t r = (uint32_t)best;
-    const uint32_t l = g.link(r);
+    uint32_t l, u;
+    if (arg < 64) {  // the winning lane's tail and link
+      u = __builtin_amdgcn_readlane(tail, arg);
+      l = __builtin_amdgcn_readlane(tl, arg);
+    } else {
+      u = g.col(g.rev(r));
+      l = g.link(r);
+    }
     if (lane == 0) {
       vis[l >> 5] |= 1u << (l & 31);
       stack[k] = (ST)r;
     }
     wave_sync();
     ++k;
-    v = g.col(g.rev(r));  // tail of r
+    v = u;  // tail of r, D[u] = the key's high word
+    dv = (uint32_t)(best >> 32);
   }
 }
 
@@ -293,11 +316,11 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
       expanded = true;
       const uint32_t e_end = g.rp(u + 1);
       for (uint32_t e = g.rp(u) + slot; e < e_end; e += 1u << lg) {
-        if (bit(ign, g.link(e))) continue;
-        const uint32_t nd = du + g.w(e);
         const uint32_t v = g.col(e);
+        const uint32_t nd = du + g.w(e);
+        const bool ignored = bit(ign, g.link(e));
         const uint32_t hv = H[v];
-        if (hv == kInf || (uint64_t)nd + hv > bound) continue;
+        if (ignored || hv == kInf || (uint64_t)nd + hv > bound) continue;
         if (nd < atomicMin(&D[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
       }
     }
