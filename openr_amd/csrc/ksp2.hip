@@ -281,9 +281,10 @@ __device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint3
 template <class G>
 __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, uint32_t bm_words,
                           const uint32_t* ign, uint32_t src, uint32_t dst, uint32_t pitch,
-                          const uint32_t* H, uint32_t delta) {
+                          const uint32_t* H, uint32_t delta, unsigned long long* prof) {
   const uint32_t lane = __lane_id();
-  for (uint32_t v = lane; v < pitch; v += 64) D[v] = kInf;
+  for (uint32_t t = lane; t < pitch / 4; t += 64)
+    reinterpret_cast<uint4*>(D)[t] = make_uint4(kInf, kInf, kInf, kInf);
   for (uint32_t i = lane; i < bm_words; i += 64) bm[i] = 0;
   wave_sync();
   if (lane == 0) {
@@ -294,20 +295,23 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
   uint32_t qlen = 1;
   uint64_t width = delta;
   uint64_t T = (uint64_t)H[src] + width;  // expand pending nodes with f <= T
+  uint32_t sweeps = 0, raises = 0, pending = 0;  // SPF_KSP2_PROF counters
   while (qlen) {
-    uint64_t defer_f = ~0ull;  // smallest f left pending by this lane
-    bool expanded = false;
+    ++sweeps;
+    pending += qlen;
     // a short frontier gets 2^lg lanes per node, each taking every 2^lg-th
     // edge: the dependent chain per lane is one or two edges, not deg(u)
     const uint32_t lg = qlen <= 16 ? 2u : (qlen <= 32 ? 1u : 0u);
     const uint32_t slot = lane & ((1u << lg) - 1u);
+    uint64_t defer_f = ~0ull;  // smallest f left pending by this lane
+    bool expanded = false;
     for (uint32_t i = lane >> lg; i < qlen; i += 64u >> lg) {
       const uint32_t u = q[i];
-      if (g.ovl(u) && u != src) continue;  // drained: recorded, not expanded
+      const bool drained = g.ovl(u) && u != src;  // recorded, not expanded
       const uint32_t du = D[u];
       const uint32_t bound = D[dst];
       const uint64_t f = (uint64_t)du + H[u];
-      if (f > bound || u == dst) continue;
+      if (drained || f > bound || u == dst) continue;
       if (f > T) {  // a later bucket: stays pending
         if (slot == 0) atomicOr(&bm[u >> 5], 1u << (u & 31));
         defer_f = min(defer_f, f);
@@ -327,6 +331,7 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
     if (!__ballot(expanded)) {  // everything pending lies past T: next bucket,
       const uint64_t m = wave_min64(defer_f);  // twice as wide (a long detour or
       if (m != ~0ull) {                        // an unreachable dst: log2 raises)
+        ++raises;
         width = min(2ull * width, 0xFFFFFFFFull);
         T = m + width;
       }
@@ -352,6 +357,11 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
     wave_sync();
     qlen = n;
   }
+  if (prof && __lane_id() == 0) {
+    atomicAdd(&prof[4], (unsigned long long)sweeps);
+    atomicAdd(&prof[5], (unsigned long long)raises);
+    atomicAdd(&prof[6], (unsigned long long)pending);
+  }
 }
 
 struct KspArgs {
@@ -371,7 +381,8 @@ struct KspArgs {
 template <class ST>
 __host__ __device__ constexpr size_t wave_lds_words(uint32_t pitch, uint32_t bm_words,
                                                     uint32_t lw) {
-  return pitch + (pitch * sizeof(ST) + 3) / 4 + bm_words + 2ull * lw;
+  // rounded to 4 words: each wave's D row starts 16-byte aligned (b128 access)
+  return (pitch + (pitch * sizeof(ST) + 3) / 4 + bm_words + 2ull * lw + 3) & ~3ull;
 }
 
 // The pair loop of one workgroup: the block owns one destination d (its
@@ -436,7 +447,7 @@ __device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint
       if (n1) {
         ++k2_runs;
         wave_sync();
-        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch, H, a.delta);
+        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch, H, a.delta, a.prof);
         if (a.prof) t2 = __builtin_amdgcn_s_memtime();
         if (Dw[d] != kInf) {
           for (uint32_t j = lane; j < lw; j += 64) vis[j] = 0;
@@ -618,8 +629,8 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     HIP_TRY(c, p->d_H.alloc((size_t)c->N * c->pitch));
   }
   if (std::getenv("SPF_KSP2_PROF")) {
-    HIP_TRY(c, p->d_prof.alloc(4));
-    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 32, c->stream));
+    HIP_TRY(c, p->d_prof.alloc(8));
+    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 64, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   p->epoch = c->epoch;
@@ -670,10 +681,11 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
 
 static spf_status ksp2_debug_phases(spf_ksp2_plan* p) {
   if (!p || !p->d_prof.p) return SPF_OK;
-  unsigned long long h[4];
+  unsigned long long h[8];
   HIP_TRY(p->ctx, hipMemcpy(h, p->d_prof.p, sizeof h, hipMemcpyDeviceToHost));
   std::fprintf(stderr, "ksp2 phases (clock sums over waves): k1 trace %llu, k2 spf %llu, "
-               "k2 trace %llu, pairs %llu\n", h[0], h[1], h[2], h[3]);
+               "k2 trace %llu, pairs %llu; k2 spf sweeps %llu, bucket raises %llu, "
+               "queued nodes %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
   return SPF_OK;
 }
 
