@@ -226,7 +226,7 @@ __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, ui
       l = g.link(r);
     }
     if (lane == 0) {
-      vis[l >> 5] |= 1u << (l & 31);
+      atomicOr(&vis[l >> 5], 1u << (l & 31));  // ds_or: no read round trip
       stack[k] = (ST)r;
     }
     wave_sync();
