@@ -1124,16 +1124,16 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
 __global__ __launch_bounds__(256) void repair_wave_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ hot, const uint32_t* __restrict__ n_hot,
     uint32_t* cursor, uint2* big, uint32_t* n_big, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
-    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out) {
+    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out, uint32_t cap) {
   __shared__ TeamCtl ctl[4];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t team = (size_t)blockIdx.x * 4 + w;
   mark += team * g.N;
-  dlist += team * kWaveCap;
-  dnew += team * kWaveCap;
-  nhn += team * kWaveCap * g.W;
-  lvl += team * (kWaveCap + 1);
-  ord += team * 2 * kWaveCap;  // level list + its hubs
+  dlist += team * cap;
+  dnew += team * cap;
+  nhn += team * cap * g.W;
+  lvl += team * (cap + 1);
+  ord += team * 2 * cap;  // level list + its hubs
   const uint32_t total = *n_hot;
   for (;;) {
     uint32_t k = 0;
@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
     k = __shfl(k, 0, 64);
     if (k >= total) break;
     const uint2 h = hot[k];
-    if (!repair<64>(g, B, mark, dlist, dnew, nhn, lvl, ord, kWaveCap, &ctl[w], lane, h.y,
+    if (!repair<64>(g, B, mark, dlist, dnew, nhn, lvl, ord, cap, &ctl[w], lane, h.y,
                     out + h.x)) {
       if (lane == 0) big[atomicAdd(n_big, 1u)] = h;
     }
@@ -1286,6 +1286,10 @@ struct spf_whatif_plan {
   uint32_t group = 0, group_teams = 0;  // workgroups per group team (0: one-workgroup teams)
   DevBuf<uint32_t> d_parent, d_sub;
   uint32_t big_teams = 0;
+  // |D| a wave team holds (its scratch) and the parent-subtree size past
+  // which classify sends a failure to the workgroup teams (A/B:
+  // SPF_WHATIF_WAVECAP, SPF_WHATIF_CLASSIFY)
+  uint32_t wave_cap = kWaveCap, classify_cap = kWaveCap;
   DevBuf<unsigned long long> d_prof;  // SPF_WHATIF_PROF diagnostics
   DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
   DevBuf<uint32_t> b_mark, b_dlist, b_dnew, b_nhn, b_lvl, b_ord;  // workgroup-team scratch
@@ -1389,7 +1393,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
      // the scratch budget (SPF_WHATIF_WAVES=<per CU>, a multiple of 4: A/B)
     const char* e = std::getenv("SPF_WHATIF_WAVES");
     const size_t per_cu = e ? std::max(4, atoi(e) & ~3) : 12;
-    const size_t per_team = 4ull * (N + kWaveCap * (4ull + p->W) + kWaveCap + 1);
+    if (const char* ec = std::getenv("SPF_WHATIF_WAVECAP")) p->wave_cap = std::max(64, atoi(ec));
+    p->classify_cap = p->wave_cap;
+    if (const char* ec = std::getenv("SPF_WHATIF_CLASSIFY")) p->classify_cap = std::max(1, atoi(ec));
+    const size_t cap = p->wave_cap;
+    const size_t per_team = 4ull * (N + cap * (4ull + p->W) + cap + 1);
     const size_t fit = std::max<size_t>(4, kWaveScratch / per_team) & ~size_t(3);
     p->wave_teams = (uint32_t)std::min<size_t>(per_cu * c->n_cu, fit);
   }
@@ -1421,11 +1429,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->d_cnt.alloc(8));
   const size_t wt = p->wave_teams;
   HIP_TRY(c, p->w_mark.alloc(wt * N));
-  HIP_TRY(c, p->w_dlist.alloc(wt * kWaveCap));
-  HIP_TRY(c, p->w_dnew.alloc(wt * kWaveCap));
-  HIP_TRY(c, p->w_nhn.alloc(wt * kWaveCap * p->W));
-  HIP_TRY(c, p->w_lvl.alloc(wt * (kWaveCap + 1)));
-  HIP_TRY(c, p->w_ord.alloc(wt * 2 * kWaveCap));
+  HIP_TRY(c, p->w_dlist.alloc(wt * p->wave_cap));
+  HIP_TRY(c, p->w_dnew.alloc(wt * p->wave_cap));
+  HIP_TRY(c, p->w_nhn.alloc(wt * p->wave_cap * p->W));
+  HIP_TRY(c, p->w_lvl.alloc(wt * (p->wave_cap + 1)));
+  HIP_TRY(c, p->w_ord.alloc(wt * 2 * p->wave_cap));
   {  // workgroup teams: one per CU, two sets (b_*, c_*) within the scratch budget
     const size_t per_team = 4ull * ((size_t)N * (6 + p->W) + 1);
     p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / 2 / per_team));
@@ -1517,7 +1525,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   if (p->n_fail) {
     hipLaunchKernelGGL(classify_kernel, dim3((p->n_fail + 255) / 256), dim3(256), 0, s, g,
                        p->d_dist.p, p->d_H.p, p->d_fails.p, p->n_fail, p->d_link_edge.p,
-                       p->d_sub.p, kWaveCap, d_out, p->d_hot.p, p->d_cnt.p, p->d_big0.p,
+                       p->d_sub.p, p->classify_cap, d_out, p->d_hot.p, p->d_cnt.p, p->d_big0.p,
                        p->d_cnt.p + 3);
     HIP_TRY(c, hipGetLastError());
     WiBase B{p->d_dist.p, p->d_nhb.p, p->d_H.p};
@@ -1549,7 +1557,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     hipLaunchKernelGGL(repair_wave_kernel, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                        p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
                        p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p, p->w_ord.p,
-                       d_out);
+                       d_out, p->wave_cap);
     HIP_TRY(c, hipGetLastError());
     hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
