@@ -86,6 +86,7 @@ struct spf_ctx {
   // scratch for spf_preds
   spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
   spfi::DevBuf<uint32_t> d_gq, d_gq2, d_gbm, d_gctr;  // global-memory SSSP scratch
+  spfi::DevBuf<uint32_t> d_gbar;  // its grid-barrier counters (whatif.hip XGrid)
   spfi::DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
 };
 
@@ -111,6 +112,7 @@ struct spf_plan {
   uint32_t max_xcd_units = 0;
   bool big = false;  // spf_big_kernel (whatif.hip): graphs beyond the LDS kernels
   spfi::DevBuf<uint32_t> b_q, b_q2, b_bm, b_ctr, b_nbr_bit, b_nhb, b_lvl, b_order, b_misc, b_parent;
+  spfi::DevBuf<uint32_t> b_bar;  // spf_big_kernel's grid-barrier counters
   spfi::DevBuf<uint64_t> d_nh_off;
   spfi::DevBuf<uint32_t> d_nb_row, d_nb_row_off, d_nb_drained;  // next-hop pass inputs
   uint32_t dead = 0;  // nb_row value of a drained neighbour

@@ -106,9 +106,70 @@ struct WiBase {
 // ---------------------------------------------------------------------------
 //  cooperative (grid-synchronised) single-source SSSP and unfailed result
 // ---------------------------------------------------------------------------
-namespace cg = cooperative_groups;
 constexpr int kCoopThreads = 512;  // one block per CU: always co-resident
 constexpr uint32_t kCoopHubDeg = 32;  // nodes above this degree get a whole wave
+
+// Grid barrier of the cooperative kernels, XCD-hierarchical (MI355X_MICROARCH
+// barrier-xcd: 4.1 us at 256 workgroups against 26.3 us for the software
+// cooperative_groups grid sync, which the what-if base pass crossed ~70
+// times).  Blocks are grouped by blockIdx % 8 (the XCD round-robin of the
+// dispatcher); each arrival bumps its group's counter, the group's last
+// arrival bumps the top counter, waits for every group and publishes the
+// generation its group polls.  Counters only grow within a launch (the k-th
+// barrier completes at k arrivals per block) and are zeroed before each
+// launch (kGridBarWords words, one 128-byte line per counter).
+constexpr uint32_t kBarPad = 32;
+constexpr uint32_t kGridBarWords = 17 * kBarPad;  // cnt[8], top, gen[8]
+constexpr uint32_t kBarSpin = 1u << 26;            // ~seconds: never a silent hang
+
+struct XGrid {
+  uint32_t* bar;
+  __device__ void sync() const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t nb = gridDim.x, x = blockIdx.x & 7u;
+      const uint32_t nx = (nb - x + 7u) / 8u;  // blocks of this group (>= 1)
+      const uint32_t ngroups = nb < 8u ? nb : 8u;
+      uint32_t* top = bar + 8 * kBarPad;
+      uint32_t* gen = bar + (9 + x) * kBarPad;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t =
+          __hip_atomic_fetch_add(bar + x * kBarPad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t g = t / nx + 1;  // the generation this arrival completes
+      if (t % nx == nx - 1) {         // last of its group: the group's leader
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t k = 0; k < kBarSpin &&
+             __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g * ngroups;
+             ++k)
+          __builtin_amdgcn_s_sleep(1);
+        __hip_atomic_store(gen, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (uint32_t k = 0; k < kBarSpin &&
+             __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g;
+             ++k)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+};
+
+// inclusive prefix sum over the wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
 
 struct CoopSssp {
   const uint32_t* row_ptr;
@@ -123,12 +184,13 @@ struct CoopSssp {
   uint32_t* qb;
   uint32_t* bm;   // [ceil(N/32)] next-frontier bitmap
   uint32_t* ctr;  // [4] rotating queue lengths + spare
+  uint32_t* bar = nullptr;  // [kGridBarWords] XGrid counters, zero at launch
 };
 
 // Frontier Bellman-Ford over the whole grid: expansion, grid barrier,
 // bitmap compaction into the other queue, grid barrier.  Data written by
 // other workgroups is read with agent-scope atomics (ld) or atomicExch.
-__device__ void coop_sssp(cg::grid_group& grid, const CoopSssp& a) {
+__device__ void coop_sssp(const XGrid& grid, const CoopSssp& a) {
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
   const uint32_t lane = threadIdx.x & 63;
@@ -180,10 +242,19 @@ __device__ void coop_sssp(cg::grid_group& grid, const CoopSssp& a) {
       }
     }
     grid.sync();
-    for (uint32_t w = gtid; w < bm_words; w += gsz) {
-      uint32_t word = atomicExch(&a.bm[w], 0u);
-      if (!word) continue;
-      uint32_t at = atomicAdd(nctr, (uint32_t)__popc(word));
+    for (uint32_t wb = gtid - lane; wb < bm_words; wb += gsz) {  // wave-uniform
+      const uint32_t w = wb + lane;
+      uint32_t word = w < bm_words ? atomicExch(&a.bm[w], 0u) : 0u;
+      // one queue-counter atomic per wave (a returning atomic per word on one
+      // counter serialises at ~88 per us)
+      const uint32_t cnt = (uint32_t)__popc(word);
+      const uint32_t incl = wave_incl_scan32(cnt);
+      const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+      if (!total) continue;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(nctr, total);
+      base = __builtin_amdgcn_readlane(base, 0);
+      uint32_t at = base + incl - cnt;
       while (word) {
         const uint32_t b = __ffs(word) - 1;
         word &= word - 1;
@@ -195,7 +266,7 @@ __device__ void coop_sssp(cg::grid_group& grid, const CoopSssp& a) {
 }
 
 __global__ __launch_bounds__(kCoopThreads) void gsssp_coop_kernel(CoopSssp a) {
-  cg::grid_group grid = cg::this_grid();
+  const XGrid grid{a.bar};
   coop_sssp(grid, a);
 }
 
@@ -262,19 +333,6 @@ __device__ __forceinline__ uint32_t nh_word(const WiGraph& g, const uint32_t* di
     acc |= x[0] | x[1] | x[2] | x[3];
   }
   return acc;
-}
-
-// the first tight expanded predecessor of v in CSR order (v reachable, != src)
-__device__ __forceinline__ uint32_t first_tight_pred(const WiGraph& g, const uint32_t* dist,
-                                                     uint32_t v) {
-  const uint32_t dv = dist[v];
-  for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-    const uint32_t u = g.col[e];
-    if (g.ovl[u] && u != g.src) continue;
-    const uint32_t du = ld(&dist[u]);
-    if (du != kInf && du + in_w(g, e) == dv) return u;
-  }
-  return kInf;
 }
 
 // nh(v) of a hub by one wave: lanes test v's in-edges 64 at a time, then
@@ -347,6 +405,65 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
   }
 }
 
+// nh(v) and parent[v] of a non-hub node (degree <= kCoopHubDeg) by a
+// segment of S lanes (S = a power of two >= min(W, 64), 64 / S nodes per
+// wave, segment-uniform call): lane l of the segment tests in-edges l, l + S,
+// ... once, then every tight tail's words are ORed in with lane = word.  An
+// item per (v, word) instead rescans v's in-edges W times (what-if base:
+// W = 31, next hops 4.3 ms of the 5.7 ms pass, r02_v61).
+__device__ void seg_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, uint32_t* parent,
+                       uint32_t v, uint32_t S, uint32_t lane) {
+  const uint32_t sl = lane & (S - 1), base = lane - sl;
+  const uint64_t segmask = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << base;
+  const uint32_t dv = ld(&dist[v]), W = g.W;
+  const uint32_t e0 = g.row_ptr[v], e1 = g.row_ptr[v + 1];
+  bool have_parent = false;
+  for (uint32_t j0 = 0; j0 < W; j0 += S) {
+    const uint32_t j = j0 + sl;
+    uint32_t acc = 0;
+    for (uint32_t eb = e0; eb < e1; eb += S) {  // segment-uniform
+      const uint32_t e = eb + sl;
+      uint32_t u = kInf;
+      if (e < e1) {
+        const uint32_t cu = g.col[e];
+        const uint32_t du = ld(&dist[cu]);
+        const uint32_t w = g.hop ? 1u : g.wt[g.rev[e]];
+        if ((!g.ovl[cu] || cu == g.src) && du != kInf && du + w == dv) u = cu;
+      }
+      uint64_t tight = __ballot(u != kInf) & segmask;
+      if (tight && !have_parent) {  // segment-uniform: CSR order, first tight tail
+        have_parent = true;
+        const uint32_t first = __shfl(u, __builtin_ctzll(tight), 64);
+        if (sl == 0) st(&parent[v], first);
+      }
+      while (tight) {  // the tight tails' words, 4 loads in flight
+        uint32_t tu[4], x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          tu[q] = kInf;
+          if (tight) {
+            tu[q] = __shfl(u, __builtin_ctzll(tight), 64);
+            tight &= tight - 1;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          x[q] = tu[q] != kInf && tu[q] != g.src && j < W ? ld(&nhb[(size_t)tu[q] * W + j]) : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc |= x[q];
+          if (tu[q] == g.src) {
+            const uint32_t jb = g.nbr_bit[v];
+            if (j == (jb >> 5)) acc |= 1u << (jb & 31);
+          }
+        }
+      }
+    }
+    if (j < W) st(&nhb[(size_t)v * W + j], acc);
+  }
+  if (!have_parent && sl == 0) st(&parent[v], kInf);
+}
+
 // Next-hop bitsets nhb[v][W] of the SPF in `dist` (every distance final,
 // after coop_sssp): nodes bucketed by distance value and settled level by
 // level (every tight predecessor of a level-d node sits at a lower level)
@@ -354,7 +471,7 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
 // monotone union otherwise.  nhb must be zero and lvl[0..kLevelCap],
 // misc[0..7] zero on entry.  Returns whether the level path ran (then
 // lvl[d] = end of bucket d in `order`).  Starts and ends with a grid barrier.
-__device__ bool level_nh(cg::grid_group& grid, const WiGraph& g, const uint32_t* dist,
+__device__ bool level_nh(const XGrid& grid, const WiGraph& g, const uint32_t* dist,
                          uint32_t* nhb, uint32_t* lvl, uint32_t* order, uint32_t* misc,
                          uint32_t* parent) {
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -418,22 +535,22 @@ __device__ bool level_nh(cg::grid_group& grid, const WiGraph& g, const uint32_t*
     for (uint32_t d = 1; d <= maxd; ++d) {
       const uint32_t end = ld(&lvl[d]);
       if (end == begin) continue;  // empty level: uniform skip
-      const uint64_t items = (uint64_t)(end - begin) * W;
-      for (uint64_t b = gtid - lane; b < items; b += gsz) {  // wave-uniform
-        const uint64_t x = b + lane;
-        uint32_t v = 0, j = 0;
+      const uint32_t n_lvl = end - begin;
+      // 64 / S nodes per wave, a segment of S lanes each (seg_nh)
+      const uint32_t S = W <= 16 ? 16u : (W <= 32 ? 32u : 64u);
+      const uint32_t per_wave = 64 / S, seg = lane / S;
+      const uint32_t waves = gsz / 64, wave = gtid / 64;
+      for (uint32_t wb = wave * per_wave; wb < n_lvl; wb += waves * per_wave) {  // wave-uniform
+        const uint32_t i = wb + seg;
+        uint32_t v = 0;
         bool hub = false;
-        if (x < items) {
-          v = ld(&order[begin + (uint32_t)(x / W)]);
-          j = (uint32_t)(x % W);
+        if (i < n_lvl) {
+          v = ld(&order[begin + i]);
           hub = g.row_ptr[v + 1] - g.row_ptr[v] > kCoopHubDeg;
-          if (!hub) {
-            st(&nhb[(size_t)v * W + j], nh_word(g, dist, nhb, v, j));
-            if (j == 0) st(&parent[v], first_tight_pred(g, dist, v));
-          }
+          if (!hub) seg_nh(g, dist, nhb, parent, v, S, lane);  // segment-uniform
         }
-        // a hub's W words are made once, by the wave, at its j = 0 item
-        for (uint64_t hubs = __ballot(hub && j == 0); hubs; hubs &= hubs - 1)
+        // a hub's W words are made once, by the whole wave
+        for (uint64_t hubs = __ballot(hub && (lane & (S - 1)) == 0); hubs; hubs &= hubs - 1)
           hub_nh(g, dist, nhb, parent, __shfl(v, __builtin_ctzll(hubs), 64), lane);
       }
       begin = end;
@@ -463,7 +580,7 @@ __device__ bool level_nh(cg::grid_group& grid, const WiGraph& g, const uint32_t*
 }
 
 __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
-  cg::grid_group grid = cg::this_grid();
+  const XGrid grid{a.sp.bar};
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
   const WiGraph& g = a.g;
@@ -560,7 +677,7 @@ struct BigArgs {
 };
 
 __global__ __launch_bounds__(kCoopThreads) void spf_big_kernel(BigArgs a) {
-  cg::grid_group grid = cg::this_grid();
+  const XGrid grid{a.sp.bar};
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
   const uint32_t lane = threadIdx.x & 63;
@@ -1276,6 +1393,7 @@ struct spf_whatif_plan {
   uint32_t src = 0, n_fail = 0, W = 0, wave_teams = 0;
   uint64_t epoch = 0;  // graph state the plan was derived from
   DevBuf<uint32_t> d_fails, d_link_edge, d_nbr_bit, d_dist, d_q, d_q2, d_bm, d_nhb, d_ctr;
+  DevBuf<uint32_t> d_bar;  // the base kernel's grid-barrier counters
   DevBuf<uint32_t> d_lvl, d_order, d_misc;
   DevBuf<unsigned long long> d_H;
   DevBuf<uint2> d_hot, d_big, d_big0, d_big1;  // d_big1: d_big0 largest first
@@ -1304,7 +1422,19 @@ struct spf_whatif_plan {
 
 namespace spfi {
 
-uint32_t coop_blocks(spf_ctx* c) { return c->n_cu; }  // one 512-thread block per CU
+// Blocks of a cooperative launch: `per_cu` 512-thread blocks per CU, clamped
+// to what the occupancy calculator says stays co-resident (grid.sync needs
+// every block resident).  SPF_COOP_PER_CU overrides (A/B).
+uint32_t coop_blocks(spf_ctx* c, const void* kernel, uint32_t per_cu) {
+  if (const char* e = std::getenv("SPF_COOP_PER_CU")) per_cu = std::max(1, atoi(e));
+  int fit = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit, kernel, kCoopThreads, 0) != hipSuccess ||
+      fit < 1) {
+    (void)hipGetLastError();
+    fit = 1;
+  }
+  return c->n_cu * std::min<uint32_t>(per_cu, (uint32_t)fit);
+}
 
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
                         hipStream_t s) {
@@ -1313,10 +1443,14 @@ spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
   HIP_TRY(c, c->d_gq2.alloc(N));
   HIP_TRY(c, c->d_gbm.alloc((N + 31) / 32));
   HIP_TRY(c, c->d_gctr.alloc(4));
+  HIP_TRY(c, c->d_gbar.alloc(kGridBarWords));
+  HIP_TRY(c, hipMemsetAsync(c->d_gbar.p, 0, 4 * kGridBarWords, s));
   CoopSssp a{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, ign, N, src,
              hop ? 1u : 0u, dist, c->d_gq.p, c->d_gq2.p, c->d_gbm.p, c->d_gctr.p};
+  a.bar = c->d_gbar.p;
   void* args[] = {&a};
-  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)gsssp_coop_kernel, dim3(coop_blocks(c)),
+  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)gsssp_coop_kernel,
+                                        dim3(coop_blocks(c, (const void*)gsssp_coop_kernel, 1)),
                                         dim3(kCoopThreads), args, 0, s));
   return SPF_OK;
 }
@@ -1328,6 +1462,8 @@ spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh,
   HIP_TRY(c, p->b_q2.alloc(N));
   HIP_TRY(c, p->b_bm.alloc((N + 31) / 32));
   HIP_TRY(c, p->b_ctr.alloc(4));
+  HIP_TRY(c, p->b_bar.alloc(kGridBarWords));
+  HIP_TRY(c, hipMemsetAsync(p->b_bar.p, 0, 4 * kGridBarWords, s));
   if (!p->b_nbr_bit.p) {
     HIP_TRY(c, p->b_nbr_bit.alloc(N));
     HIP_TRY(c, hipMemsetAsync(p->b_nbr_bit.p, 0xFF, 4ull * N, s));
@@ -1344,8 +1480,10 @@ spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh,
             g, p->d_srcs.p, p->n_src, c->d_nb_ptr.p, c->d_nb_id.p, d_dist, c->pitch, d_nh,
             p->d_nh_off.p, p->b_nbr_bit.p, p->b_nhb.p, p->b_lvl.p, p->b_order.p, p->b_misc.p,
             p->b_parent.p};
+  a.sp.bar = p->b_bar.p;
   void* args[] = {&a};
-  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)spf_big_kernel, dim3(coop_blocks(c)),
+  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)spf_big_kernel,
+                                        dim3(coop_blocks(c, (const void*)spf_big_kernel, 1)),
                                         dim3(kCoopThreads), args, 0, s));
   return SPF_OK;
 }
@@ -1411,6 +1549,7 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->d_bm.alloc((N + 31) / 32));
   HIP_TRY(c, p->d_nhb.alloc((size_t)N * p->W));
   HIP_TRY(c, p->d_ctr.alloc(4));
+  HIP_TRY(c, p->d_bar.alloc(kGridBarWords));
   HIP_TRY(c, p->d_lvl.alloc(kLevelCap + 1));
   HIP_TRY(c, p->d_order.alloc(N));
   HIP_TRY(c, p->d_misc.alloc(8));
@@ -1514,8 +1653,11 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
                g, p->d_nhb.p, p->d_lvl.p, p->d_order.p, p->d_misc.p, p->d_H.p,
                p->d_prof.p ? p->d_prof.p + 16ull * p->big_teams : nullptr, p->d_parent.p,
                p->d_sub.p};
+    a.sp.bar = p->d_bar.p;
+    HIP_TRY(c, hipMemsetAsync(p->d_bar.p, 0, 4 * kGridBarWords, s));
     void* args[] = {&a};
-    HIP_TRY(c, hipLaunchCooperativeKernel((const void*)whatif_base_kernel, dim3(coop_blocks(c)),
+    HIP_TRY(c, hipLaunchCooperativeKernel((const void*)whatif_base_kernel,
+                                          dim3(coop_blocks(c, (const void*)whatif_base_kernel, 1)),
                                           dim3(kCoopThreads), args, 0, s));
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
