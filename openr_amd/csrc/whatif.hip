@@ -58,10 +58,17 @@ __device__ __forceinline__ void st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Wave-wide minimum with DPP moves (row shifts, then row broadcasts; lanes
+// with no source keep ~0u) -- __shfl compiles to ds_bpermute, an LDS round
+// trip per step.  Every lane of the wave must be active.
 __device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) x = min(x, (uint32_t)__shfl_xor(x, d, 64));
-  return x;
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return __builtin_amdgcn_readlane(x, 63);
 }
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -237,7 +244,8 @@ __device__ void coop_sssp(const XGrid& grid, const CoopSssp& a) {
         for (uint32_t e = e0; e < e1; ++e) relax(e, du);
       for (uint64_t hubs = __ballot(hub); hubs; hubs &= hubs - 1) {
         const int l = __builtin_ctzll(hubs);
-        const uint32_t hb = __shfl(e0, l, 64), he = __shfl(e1, l, 64), hd = __shfl(du, l, 64);
+        const uint32_t hb = __builtin_amdgcn_readlane(e0, l), he = __builtin_amdgcn_readlane(e1, l),
+                       hd = __builtin_amdgcn_readlane(du, l);
         for (uint32_t e = hb + lane; e < he; e += 64) relax(e, hd);
       }
     }
@@ -373,7 +381,7 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
       const uint64_t tight = __ballot(u != kInf);
       if (tight && !have_parent) {  // wave-uniform
         have_parent = true;
-        const uint32_t first = __shfl(u, __builtin_ctzll(tight), 64);
+        const uint32_t first = __builtin_amdgcn_readlane(u, __builtin_ctzll(tight));
         if (lane == 0) st(&parent[v], first);
       }
       // the tight tails' words 8 at a time, their loads issued together
@@ -383,7 +391,7 @@ __device__ void hub_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
         for (int q = 0; q < 8; ++q) {
           tu[q] = kInf;
           if (t) {  // wave-uniform
-            tu[q] = __shfl(u, __builtin_ctzll(t), 64);
+            tu[q] = __builtin_amdgcn_readlane(u, __builtin_ctzll(t));
             t &= t - 1;
           }
         }
@@ -551,7 +559,7 @@ __device__ bool level_nh(const XGrid& grid, const WiGraph& g, const uint32_t* di
         }
         // a hub's W words are made once, by the whole wave
         for (uint64_t hubs = __ballot(hub && (lane & (S - 1)) == 0); hubs; hubs &= hubs - 1)
-          hub_nh(g, dist, nhb, parent, __shfl(v, __builtin_ctzll(hubs), 64), lane);
+          hub_nh(g, dist, nhb, parent, __builtin_amdgcn_readlane(v, __builtin_ctzll(hubs)), lane);
       }
       begin = end;
       grid.sync();
@@ -1090,7 +1098,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         }
         for (uint64_t mask = __ballot(tight); mask; mask &= mask - 1) {
           const uint32_t b = __ffsll((unsigned long long)mask) - 1;
-          const uint32_t pu = __shfl(u, b, 64), pm = __shfl(mu, b, 64);
+          const uint32_t pu = __builtin_amdgcn_readlane(u, b), pm = __builtin_amdgcn_readlane(mu, b);
           const uint32_t* from = pm != kInf ? nhn + (size_t)pm * W : B.nhb + (size_t)pu * W;
           for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
         }
@@ -1160,13 +1168,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         for (uint32_t base = 0; base < nlev; base += 64) {
           const uint32_t b = base + tt;
           const uint32_t x = b < nlev ? ldw<GROUP>(&lvl[b]) : 0u;
-          uint32_t inc = x;
-          for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(inc, d, 64);
-            if (tt >= (uint32_t)d) inc += y;
-          }
+          const uint32_t inc = wave_incl_scan32(x);
           if (b < nlev) stw<GROUP>(&lvl[b], carry + inc - x);
-          carry += __shfl(inc, 63, 64);
+          carry += __builtin_amdgcn_readlane(inc, 63);
         }
       }
       team_sync<TEAM, GROUP>(ctl);
@@ -1255,7 +1259,7 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
   for (;;) {
     uint32_t k = 0;
     if (lane == 0) k = atomicAdd(cursor, 1u);
-    k = __shfl(k, 0, 64);
+    k = __builtin_amdgcn_readlane(k, 0);
     if (k >= total) break;
     const uint2 h = hot[k];
     if (!repair<64>(g, B, mark, dlist, dnew, nhn, lvl, ord, cap, &ctl[w], lane, h.y,
