@@ -74,16 +74,37 @@ constexpr size_t kMaxLds = 160 * 1024;
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// Wave-wide scans and reductions with DPP moves: row_shr 1/2/4/8 inside each
+// 16-lane row (lanes shifted in from outside the row read 0 -- the identity
+// of +, | and max over unsigned values), then row_bcast15 / row_bcast31 carry
+// the row results upwards; lane 63 ends with the whole wave's.  __shfl
+// compiles to ds_bpermute, one LDS round trip per step (msbfs_kernel<10>'s
+// per-slice record made 18 of them in a dependent chain).  Every lane of
+// the wave must be active.
+#define SPF_DPP_STEPS(OP)                                                        \
+  x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true)); \
+  x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true)); \
+  x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true)); \
+  x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true)); \
+  x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false)); \
+  x = OP(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));
+__device__ __forceinline__ uint32_t dpp_add(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ uint32_t dpp_or(uint32_t a, uint32_t b) { return a | b; }
+__device__ __forceinline__ uint32_t dpp_max(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t* total) {
-  const uint32_t lane = lane_id();
-  uint32_t inc = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d, 64);
-    if (lane >= (uint32_t)d) inc += y;
-  }
-  *total = __shfl(inc, 63, 64);
-  return inc - x;
+  const uint32_t own = x;
+  SPF_DPP_STEPS(dpp_add)
+  *total = __builtin_amdgcn_readlane(x, 63);
+  return x - own;
+}
+__device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
+  SPF_DPP_STEPS(dpp_or)
+  return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
+  SPF_DPP_STEPS(dpp_max)
+  return __builtin_amdgcn_readlane(x, 63);
 }
 
 __device__ __forceinline__ bool link_ignored(const uint32_t* ign, uint32_t l) {
@@ -197,7 +218,7 @@ __global__ __launch_bounds__(THREADS) void sssp_kernel(
       const uint32_t pre = wave_excl_scan(__popc(word), &tot);
       uint32_t at = 0;
       if (lane == 0 && tot) at = atomicAdd(&ctl[C_QLEN], tot);
-      at = __shfl(at, 0, 64) + pre;
+      at = __builtin_amdgcn_readlane(at, 0) + pre;
       while (word) {
         const uint32_t b = __ffs(word) - 1;
         word &= word - 1;
@@ -268,13 +289,7 @@ inline uint32_t ms_own(uint32_t N) {
 // costs the store path measurably).
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    lo |= __shfl_xor(lo, d, 64);
-    hi |= __shfl_xor(hi, d, 64);
-  }
-  return ((uint64_t)hi << 32) | lo;
+  return ((uint64_t)wave_or32((uint32_t)(x >> 32)) << 32) | wave_or32((uint32_t)x);
 }
 
 //   LCOL: the sliced-ELL columns are staged once in LDS as u16 (when they fit
@@ -443,10 +458,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     // discovers a node or two per level -- grids, rings).  Trip counts:
     // #sources vs the largest per-node count.
     const uint32_t nsrc = (uint32_t)__popcll(((uint64_t)mhi << 32) | mlo);
-    uint32_t maxpop = (uint32_t)__popcll(x);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) maxpop = max(maxpop, (uint32_t)__shfl_xor((int)maxpop, d, 64));
-    maxpop = __builtin_amdgcn_readfirstlane(maxpop);
+    const uint32_t maxpop = wave_max32((uint32_t)__popcll(x));
     if (maxpop * kMsLaneStoreRatio < nsrc) {
       uint64_t m = x;
       for (uint32_t it = 0; it < maxpop; ++it) {
