@@ -50,15 +50,25 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Wave-wide minimum of 64-bit keys with DPP moves (row shifts, then row
+// broadcasts; a lane with no source keeps ~0) and a lane read: no
+// ds_bpermute round trips.  Every lane of the wave must be active.
+template <int CTRL, int ROWS, bool BOUND>
+__device__ __forceinline__ uint64_t dpp_min64_step(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_update_dpp(~0u, (uint32_t)x, CTRL, ROWS, 0xf, BOUND);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(~0u, (uint32_t)(x >> 32), CTRL, ROWS, 0xf, BOUND);
+  const uint64_t y = ((uint64_t)hi << 32) | lo;
+  return y < x ? y : x;
+}
 __device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t lo = __shfl_xor((uint32_t)x, d, 64);
-    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), d, 64);
-    const uint64_t y = ((uint64_t)hi << 32) | lo;
-    x = y < x ? y : x;
-  }
-  return x;
+  x = dpp_min64_step<0x111, 0xf, false>(x);  // row_shr:1
+  x = dpp_min64_step<0x112, 0xf, false>(x);  // row_shr:2
+  x = dpp_min64_step<0x114, 0xf, false>(x);  // row_shr:4
+  x = dpp_min64_step<0x118, 0xf, false>(x);  // row_shr:8
+  x = dpp_min64_step<0x142, 0xa, false>(x);  // row_bcast:15
+  x = dpp_min64_step<0x143, 0xc, false>(x);  // row_bcast:31
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), 63) << 32) |
+         __builtin_amdgcn_readlane((uint32_t)x, 63);
 }
 
 // Exclusive prefix sum over the wave with DPP moves (no LDS round trips):
