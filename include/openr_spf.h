@@ -285,7 +285,7 @@ spf_status spf_ksp2_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
  *                   the distinct up neighbours of src in the unfailed graph
  *                   (ascending id), ceil(k/32) words.
  * The unfailed result's digest is {0, 0, hash}.  Global-memory kernels, no
- * LDS size limit: repair scratch is sized from fixed HBM budgets (4 GB of
+ * LDS size limit: repair scratch is sized from fixed HBM budgets (8 GB of
  * wave teams, 8 GB of workgroup teams, fewer teams on bigger graphs) plus
  * O(N) per plan; an allocation failure returns SPF_E_NOMEM.  Weighted
  * metrics must be positive. */

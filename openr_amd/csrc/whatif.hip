@@ -47,7 +47,7 @@ namespace {
 constexpr uint32_t kBusy = 0xFFFFFFFEu;
 constexpr uint32_t kWaveCap = 1024;            // |D| a wave team can hold
 constexpr size_t kBigScratch = 8ull << 30;     // HBM budget of the workgroup teams (both sets)
-constexpr size_t kWaveScratch = 4ull << 30;    // HBM budget of the wave teams
+constexpr size_t kWaveScratch = 8ull << 30;    // HBM budget of the wave teams
 constexpr uint32_t kDialLevels = 1024;         // distinct distances settled bucket by bucket
 constexpr uint32_t kHubDeg = 32;               // nodes above this degree get a whole wave
 
@@ -1530,11 +1530,12 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   const uint32_t k = c->nb_ptr[src + 1] - c->nb_ptr[src];
   for (uint32_t j = 0; j < k; ++j) nbr_bit[c->nb_id[c->nb_ptr[src] + j]] = j;
   p->W = std::max<uint32_t>(1, (k + 31) / 32);
-  {  // wave teams: 12 per CU (3 waves per SIMD beside the group teams' 2;
-     // 8: 23.3 ms, 12: 20.1, 16: 22.7 on the 1M-link graph, r02_v30) within
-     // the scratch budget (SPF_WHATIF_WAVES=<per CU>, a multiple of 4: A/B)
+  {  // wave teams: 16 per CU within the scratch budget (failures on the
+     // 1M-link graph, r02_v75 with 8 GB: 12: 17.9 ms, 16: 16.4, 20: 20.2,
+     // 24: 19.6; r02_v30 before the lane-read / DPP repairs: 12 best)
+     // (SPF_WHATIF_WAVES=<per CU>, a multiple of 4: A/B)
     const char* e = std::getenv("SPF_WHATIF_WAVES");
-    const size_t per_cu = e ? std::max(4, atoi(e) & ~3) : 12;
+    const size_t per_cu = e ? std::max(4, atoi(e) & ~3) : 16;
     if (const char* ec = std::getenv("SPF_WHATIF_WAVECAP")) p->wave_cap = std::max(64, atoi(ec));
     p->classify_cap = p->wave_cap;
     if (const char* ec = std::getenv("SPF_WHATIF_CLASSIFY")) p->classify_cap = std::max(1, atoi(ec));
