@@ -131,40 +131,49 @@ class Dev:
         self.bufs = []
 
 
+def make_topology(name: str):
+    """The all-sources workloads' synthetic topologies: (Topology, description)."""
+    from openr_amd import topology as T
+
+    if name == "fabric_full":
+        return T.fabric(10000, full=True), \
+            "fabric_full numOfSws=10000 (RoutingBenchmarkUtils.cpp:247-400, every pod wired)"
+    if name == "fabric_ref":
+        return T.fabric(10000, full=False), \
+            "fabric_ref numOfSws=10000 (reference generator incl. per-pod emplace quirk)"
+    if name == "fabric_rtt":
+        return T.fabric_rtt(), ("fabric_full wiring, per-direction metrics max(rtt/100,1) from "
+                                "seeded RTTs (LinkMonitor.cpp:44-47), weighted SPF")
+    if name == "grid100":
+        return T.grid(100), "grid 100x100 (RoutingBenchmarkUtils.cpp:161-240)"
+    raise ValueError(name)
+
+
 class AllSources:
     """configs[1]/[2]: one all-sources SPF + ECMP pass per step.
 
-    strong (default): one LSDB, its sources split over the ranks in
-    contiguous id blocks balanced by next-hop work
-    (sharding.AllSourcesLayout), each rank writing its results straight into
-    a send buffer that is gathered to rank 0 over RCCL inside the step -- the
-    whole-graph result (every source's distance row and next-hop bitmaps)
-    ends on rank 0.  Send buffers alternate between two steps, so step t+1's
-    kernels overlap step t's gather; the timed region ends after the last
-    gather.  weak (--scaling weak): rank r solves its own LSDB snapshot
-    (rack switch r drained, BM_DecisionFabric's per-iteration perturbation,
-    RoutingBenchmarkUtils.cpp:406-447), results stay on each GPU."""
+    strong scaling (default), results resident (default): one LSDB, its
+    sources split over the ranks in contiguous id blocks balanced by next-hop
+    work (sharding.AllSourcesLayout); every rank writes its sources' distance
+    rows and next-hop bitmaps into buffers that stay in its HBM -- the
+    sharded result the facade serves getSpfResult(node) from on the owning
+    rank (Decision::getDecisionRouteDb per node, Decision.cpp:1480-1500).  No
+    data-path collective inside the step; after the timed steps every rank
+    digests its rows on the GPU (spf_plan_digest) and rank 0 gathers the
+    digests (RCCL) and checks every source against the oracle's committed
+    digests.  --results gather (labelled extra) instead gathers every rank's
+    rows and bitmaps to rank 0 inside the step.  --scaling weak: rank r
+    solves its own LSDB snapshot (rack switch r drained, BM_DecisionFabric's
+    per-iteration perturbation, RoutingBenchmarkUtils.cpp:406-447)."""
 
     unit = "solves/s"
 
     def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb,
-                 scaling: str = "strong"):
-        from openr_amd import topology as T
+                 scaling: str = "strong", results: str = "resident"):
         from openr_amd.sharding import AllSourcesLayout, snapshot_for_rank
 
-        if name == "fabric_full":
-            topo = T.fabric(10000, full=True)
-            self.desc = "fabric_full numOfSws=10000 (RoutingBenchmarkUtils.cpp:247-400, every pod wired)"
-        elif name == "fabric_ref":
-            topo = T.fabric(10000, full=False)
-            self.desc = "fabric_ref numOfSws=10000 (reference generator incl. per-pod emplace quirk)"
-        elif name == "fabric_rtt":
-            topo = T.fabric_rtt()
-            self.desc = ("fabric_full wiring, per-direction metrics max(rtt/100,1) from seeded RTTs "
-                         "(LinkMonitor.cpp:44-47), weighted SPF")
-        else:
-            topo = T.grid(100)
-            self.desc = "grid 100x100 (RoutingBenchmarkUtils.cpp:161-240)"
+        topo, self.desc = make_topology(name)
+        self.name = name
         self.scaling = scaling
         if scaling == "weak":  # rank r's snapshot: one node drained
             topo.lsdb = snapshot_for_rank(topo.lsdb, rank)
@@ -175,21 +184,25 @@ class AllSources:
         eng.load(rp, col, met, lid, ovl)
         self.eng, self.rank, self.world, self.dev = eng, rank, world, dev
         k = np.array([len(eng.neighbors(s)) for s in range(self.n)], np.int64)
+        self.k = k
         pitch = eng.pitch
-        gather = scaling == "strong" and world > 1
+        split = scaling == "strong"
+        gather = split and world > 1 and results == "gather"
+        self.results = "gather" if gather else ("resident" if split else "per-rank snapshot")
         # the gathered distance rows: the plans' u8 rows when every rank's
         # are lossless (checked once below), a quarter of the u32 bytes
-        layout = AllSourcesLayout(k, pitch, world if gather else 1)
-        srcs = layout.srcs[rank if gather else 0]
+        layout = AllSourcesLayout(k, pitch, world if split else 1)
+        srcs = layout.srcs[rank if split else 0]
+        self.srcs = srcs
         self.plan = eng.plan(srcs)
         self.dist_bytes = 4
         if gather and self.plan.row_mode() != "u32" and self._narrow_lossless(dev, len(srcs), pitch):
             self.dist_bytes = 1
             layout = AllSourcesLayout(k, pitch, world, dist_bytes=1)
         self.layout = layout
-        assert np.array_equal(self.plan.nh_off, self.layout.plan_nh_off(rank if gather else 0))
+        assert np.array_equal(self.plan.nh_off, self.layout.plan_nh_off(rank if split else 0))
         cap = self.layout.cap
-        self.dist_words = self.layout.dist_words[rank if gather else 0]
+        self.dist_words = self.layout.dist_words[rank if split else 0]
         # u8 rows on the wire: the plan's u32 rows go to a scratch buffer
         self.d32 = dev.buf(max(1, len(srcs) * pitch)) if self.dist_bytes == 1 else None
         self.nbuf = 2 if gather else 1
@@ -206,7 +219,8 @@ class AllSources:
                      if self.dist_bytes == 1 else "u32 distance rows + next-hop bitmaps")
         # SURVEY.md §8(d) per-solve figure (one CSR sweep charged per solve)
         n, e = self.n, self.e
-        self.survey_bytes = int(len(srcs) * (4 * (n + 1) + 8 * e + n + 4 * n)
+        self.graph_bytes = 4 * (n + 1) + 8 * e + n  # row_ptr, col + metric, drain bits
+        self.survey_bytes = int(len(srcs) * (self.graph_bytes + 4 * n)
                                 + len(srcs) * int(np.sum((k[srcs] + 7) // 8)))
         # the execute's timed phases: distance kernel, row slicing (sliced
         # next-hop plans), next-hop kernel
@@ -214,14 +228,39 @@ class AllSources:
         self.kernels = tuple(k for k in self.phases if k)
         self.narrow = self.plan.row_mode()
         self._phase_bytes()
+        self._algorithmic_bytes()
         self.parallelism = (
             f"sources in contiguous id blocks over {world} rank(s) (one LSDB), plan closure "
             f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source results "
             f"({self.wire}) gathered to rank 0 over RCCL in the step "
             f"({self.gather_bytes / 1e6:.0f} MB/step, send buffers double-buffered)"
             if gather else
-            "one rank, all sources" if scaling == "strong" else
+            f"sources in contiguous id blocks over {world} rank(s) (one LSDB, graph replicated), "
+            f"plan closure {self.plan.closure_rows} rows for {len(srcs)} sources; results "
+            f"resident in each rank's HBM (no collective in the step); per-source digests "
+            f"gathered to rank 0 after the timed steps"
+            if split else
             f"weak: one LSDB snapshot per rank ({world} ranks), results stay on each GPU")
+
+    def _algorithmic_bytes(self) -> None:
+        """Algorithmic HBM bytes per execute and per phase: the outputs the
+        path must produce (u32 distance rows, next-hop bitmaps) plus one read
+        of the graph (row_ptr, col, metric, drain bits) per kernel."""
+        m, n = len(self.srcs), self.n
+        rows = 4 * m * n
+        bitmaps = 4 * int(self.plan.nh_words)
+        g = self.graph_bytes
+        alg = {}
+        bfs, sl, ecmp = self.phases
+        if ecmp is None:  # exact / big kernels: rows and next hops in one kernel
+            alg[bfs] = rows + bitmaps + g
+        else:
+            alg[bfs] = rows + g
+            if sl:
+                alg[sl] = 0  # an internal transform: no algorithmic output
+            alg[ecmp] = bitmaps + g
+        self.alg_bytes = alg
+        self.alg_execute_bytes = rows + bitmaps + g
 
     def step(self) -> None:
         b = self.i % self.nbuf
@@ -239,6 +278,46 @@ class AllSources:
 
             out = list(self.recv[b].unbind(0)) if self.rank == 0 else None
             self.works[b] = dist.gather(buf.t, out, dst=0, async_op=True)
+
+    def verify(self):
+        """Untimed, after the timed steps: every rank digests the rows and
+        bitmaps its last execute left in its HBM (spf_plan_digest, on the
+        GPU), rank 0 gathers the digests (RCCL) and compares every source with
+        the oracle's committed digests (tests/golden/fullsize_<workload>.npz,
+        oracle/spf_oracle.cpp).  None when there is nothing to compare (weak
+        snapshots, u8 wire rows, no golden file)."""
+        if self.results == "per-rank snapshot" or self.dist_bytes != 4:
+            return None
+        buf = self.send[(self.i - 1) % self.nbuf]
+        m = len(self.srcs)
+        dg = self.dev.buf(max(1, m), np.int64, zero=True)
+        self.plan.digest(buf.ptr, buf.ptr + 4 * self.dist_words, dg.ptr, self.dev.stream())
+        self.dev.sync()
+        self.eng.check()
+        if self.world > 1:
+            from openr_amd.sharding import gather_padded
+
+            got = gather_padded(dg.t, m)
+            parts = [g.cpu().numpy().view(np.uint64) for g in got] if self.rank == 0 else None
+        else:
+            parts = [dg.numpy()[:m].view(np.uint64)]
+        if self.rank != 0:
+            return None
+        digest = np.zeros(self.n, np.uint64)
+        for r, part in enumerate(parts):
+            digest[self.layout.srcs[r]] = part
+        gold = ROOT / "tests" / "golden" / f"fullsize_{self.name}.npz"
+        if not gold.exists():
+            return {"checked_sources": 0, "note": f"no {gold.name}"}
+        z = np.load(gold)  # allow_pickle=False (default): arrays only
+        want = np.zeros(self.n, np.uint64)
+        want[z["srcs"].astype(np.int64)] = z["digest"].astype(np.uint64)
+        bad = np.nonzero(digest != want)[0]
+        return {"checked_sources": int(len(z["srcs"])), "mismatches": int(len(bad)),
+                "first_mismatch": int(bad[0]) if len(bad) else None,
+                "against": f"tests/golden/{gold.name} (oracle/spf_oracle.cpp digests of every "
+                           "source), engine digests from spf_plan_digest on each rank's "
+                           "resident rows, gathered to rank 0"}
 
     def _narrow_lossless(self, dev, m: int, pitch: int) -> bool:
         """One untimed execute: are this rank's u8 rows exact (no distance
@@ -419,6 +498,12 @@ class Ksp2AllPairs:
         self.kernel_bytes = {
             "sssp_kernel": len(self.srcs) * (4 * (n + 1) + 8 * e + n + 4 * self.eng.pitch),
             "ksp2_kernel": blocks * csr + 16 * self.units + 4 * int(cnt_h[0])}
+        # algorithmic: the k = 1 distance rows (u32) + one graph read; the
+        # pair records (16 B) + path pool + one graph read (incl. link ids)
+        g = 4 * (n + 1) + 8 * e + n
+        self.alg_bytes = {"sssp_kernel": 4 * len(self.srcs) * n + g,
+                          "ksp2_kernel": 16 * self.units + 4 * int(cnt_h[0]) + g + 4 * e}
+        self.alg_execute_bytes = sum(self.alg_bytes.values())
         return {"sssp_kernel": a / max(cnt, 1), "ksp2_kernel": b / max(cnt, 1)}
 
     def edges_per_unit(self) -> int:
@@ -488,6 +573,16 @@ class WhatIfAllLinks:
         words = (len(eng.neighbors(self.src)) + 31) // 32
         self.kernel_bytes = {"base": csr + 4 * n + 4 * words * n,
                              "failures": csr + 4 * self.units + 16 * self.units}
+        # algorithmic: the unfailed distances + next-hop words + one graph
+        # read; the failure list, one graph read and a digest per failure
+        g = 4 * (n + 1) + 8 * e + n
+        self.alg_bytes = {"base": g + 4 * n + 4 * words * n,
+                          "failures": g + 4 * self.units + 16 * self.units}
+        self.alg_execute_bytes = sum(self.alg_bytes.values())
+        self.pmc_kernels = {"base": ["whatif_base_kernel"],
+                            "failures": ["classify_kernel", "sort_big_kernel", "repair_wave_kernel",
+                                         "repair_group_kernel", "repair_block_kernel",
+                                         "base_digest_kernel"]}
         self.parallelism = (f"failures dealt round-robin over {world} rank(s), graph replicated, "
                             "unfailed SPF recomputed per rank; digests gathered to rank 0 "
                             "(RCCL gather) in the step")
@@ -608,6 +703,97 @@ WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": All
              "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks, "fabric_lfa": FacadeLfa}
 
 
+def _pmc_kernels(workload: str, kernels):
+    """Per-kernel PMC records of the kernels whose names start with one of
+    `kernels` in the committed profiles/pmc_<workload>.json
+    (tools/pmc_summary.py): ([(name, record)], provenance) or ([], reason)."""
+    pmc = ROOT / "profiles" / f"pmc_{workload}.json"
+    if not pmc.exists():
+        return [], f"{pmc.relative_to(ROOT)} not found"
+    try:
+        pj = json.loads(pmc.read_text())
+    except Exception as e:  # noqa: BLE001
+        return [], f"{pmc.relative_to(ROOT)}: {e!r}"
+    hits = []
+    for kname, kv in pj.get("per_kernel", {}).items():
+        # (the staged-graph KSP2 kernel is ksp2_lds_kernel)
+        if any(kname.startswith(k) or kname.replace("_lds", "").startswith(k) for k in kernels):
+            hits.append((kname, kv))
+    if not hits:
+        return [], f"{pmc.relative_to(ROOT)} has no {'/'.join(kernels)}"
+    return hits, (f"{pmc.relative_to(ROOT)} ({pj.get('source', 'rocprofv3 --pmc')}; kernels "
+                  f"{', '.join(h[0] for h in hits)}; FETCH_SIZE x2 + WRITE_SIZE per dispatch)")
+
+
+def roofline_block(wl, kms, launch_ms: float, workload: str, rank: int):
+    """Roofline of the dominant kernel (largest HIP-event time of one execute).
+
+    frac (= frac_algorithmic): the algorithmic bytes of that kernel -- the
+    outputs the path must write plus one read of the graph
+    (wl.alg_bytes) -- over its time, over 8 TB/s.  frac_measured: the same
+    kernel's HBM bytes from the committed PMC run (FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 corrections) over the same
+    time.  l2_frac: the bytes the kernel's structure moves through L2 (per
+    workgroup graph sweeps, internal u8 / bit-plane rows: wl.kernel_bytes,
+    spf_plan_traffic) over the time -- what round 2 reported as frac.
+    limiter: what the PMC says bounds the kernel."""
+    alg = getattr(wl, "alg_bytes", None)
+    if not alg:
+        return None
+    dominant = max(kms, key=kms.get)
+    t = kms[dominant] * 1e-3
+    achieved = alg[dominant] / t / 1e9
+    hits, src = _pmc_kernels(workload, getattr(wl, "pmc_kernels", {}).get(dominant, [dominant]))
+    traffic = sum(kv["fetch_bytes_x2"] + kv["write_bytes"] for _, kv in hits) if hits else None
+    limiter = None
+    if hits:  # the phase's busiest kernel (most wave cycles) names the limiter
+        kv = max(hits, key=lambda h: h[1].get("counters_per_dispatch", {}).get("SQ_WAVE_CYCLES", 0))[1]
+        cs = kv.get("counters_per_dispatch", {})
+        wc = cs.get("SQ_WAVE_CYCLES") or 0
+        wait = kv.get("sq_wait_any_per_wave_cycle")
+        valu = kv.get("sq_active_inst_valu_per_wave_cycle")
+        anyi = kv.get("sq_active_inst_any_per_wave_cycle")
+        lds = cs.get("SQ_INSTS_LDS", 0) / wc if wc else None
+        hbm_frac = traffic / t / 1e9 / HBM_PEAK_GBS
+        kind = ("hbm" if hbm_frac >= 0.6 else
+                "latency (waves waiting on memory / LDS)" if (wait or 0) >= 0.45 else
+                "issue (instruction-bound)" if (anyi or 0) >= 0.45 else "mixed")
+        limiter = {"kind": kind, "sq_wait_any_per_wave_cycle": wait,
+                   "sq_active_inst_valu_per_wave_cycle": valu,
+                   "sq_active_inst_any_per_wave_cycle": anyi,
+                   "sq_insts_lds_per_wave_cycle": lds,
+                   "l2_hit_rate": kv.get("l2_hit_rate"), "source": src}
+    elif rank == 0:
+        print(f"bench: {src}: roofline.traffic is null", file=sys.stderr)
+    kb = wl.kernel_bytes
+    out = {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "frac_algorithmic": achieved / HBM_PEAK_GBS,
+        "frac_measured": None if traffic is None else traffic / t / 1e9 / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "traffic_source": src if traffic is not None else None,
+        "kernel": dominant,
+        "kernel_ms": kms,
+        "algorithmic_bytes": alg,
+        "algorithmic_bytes_note": getattr(wl, "alg_note", "outputs + one graph read per kernel"),
+        "l2_frac": kb[dominant] / t / 1e9 / HBM_PEAK_GBS,
+        "l2_bytes": kb,
+        "limiter": limiter,
+        # the whole execute: algorithmic bytes over the summed kernel time
+        "execute_frac_algorithmic": getattr(wl, "alg_execute_bytes", sum(alg.values()))
+        / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        # SURVEY.md §8(d)'s per-solve figure (a full CSR sweep charged to every
+        # solve) over the algorithmic bytes: how much sweep work batching shares
+        "survey_bytes_per_launch": wl.survey_bytes,
+        "reuse_factor": wl.survey_bytes / max(1, sum(alg.values())),
+    }
+    return out
+
+
 def _dump_maps_at_exit(path: str) -> None:
     """Diagnostics: copy /proc/self/maps when the interpreter finalises, so
     addresses in a native crash during exit-time teardown can be attributed
@@ -629,9 +815,12 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of CPU-baseline sampling (0 disables)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                    help="all-sources workloads: split one LSDB's sources over ranks and "
-                         "gather the results to rank 0 (strong), or one LSDB snapshot per "
-                         "rank with results left on each GPU (weak)")
+                    help="all-sources workloads: split one LSDB's sources over ranks "
+                         "(strong), or one LSDB snapshot per rank (weak)")
+    ap.add_argument("--results", default="resident", choices=["resident", "gather"],
+                    help="strong all-sources: results stay in each rank's HBM, digests "
+                         "checked after the run (resident), or every rank's rows and "
+                         "bitmaps gathered to rank 0 inside the step (gather)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -649,7 +838,8 @@ def main() -> None:
 
     cls = WORKLOADS[args.workload]
     if cls is AllSources:
-        wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb, scaling=args.scaling)
+        wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb, scaling=args.scaling,
+                 results=args.results)
     else:
         wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb)
     for _ in range(args.warmup):
@@ -675,6 +865,9 @@ def main() -> None:
         elapsed = float(t.item())
     kms = wl.kernel_ms()
     launch_ms = sum(kms.values())
+    parity = wl.verify() if hasattr(wl, "verify") else None
+    if hasattr(wl, "eng"):
+        wl.eng.check()  # a grid-resident kernel's barrier gave up: the run is invalid
 
     # whole-job units: weak = every rank did `units`; strong = ranks split them
     units = wl.units
@@ -685,28 +878,7 @@ def main() -> None:
     value = units * args.steps / elapsed
     gteps = units * wl.edges_per_unit() * args.steps / elapsed / 1e9
 
-    # roofline of the dominant kernel: the bytes it must move (its structure's
-    # compulsory traffic, wl.kernel_bytes) over its HIP-event time
-    dominant = max(kms, key=kms.get)
-    kbytes = wl.kernel_bytes
-    achieved = kbytes[dominant] / (kms[dominant] * 1e-3) / 1e9
-    traffic, traffic_src = None, None
-    pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
-    if pmc.exists():
-        try:
-            pj = json.loads(pmc.read_text())
-            for kname, kv in pj.get("per_kernel", {}).items():
-                # (the staged-graph KSP2 kernel is ksp2_lds_kernel)
-                if kname.startswith(dominant) or kname.replace("_lds", "").startswith(dominant):
-                    traffic = kv["fetch_bytes_x2"] + kv["write_bytes"]
-                    traffic_src = (f"{pmc.relative_to(ROOT)} ({pj.get('source', 'rocprofv3 --pmc')}"
-                                   f"; kernel {kname}; FETCH_SIZE x2 + WRITE_SIZE)")
-        except Exception as e:  # noqa: BLE001
-            print(f"bench: no PMC traffic from {pmc}: {e!r}", file=sys.stderr)
-            traffic = None
-    elif rank == 0:
-        print(f"bench: {pmc} not found: roofline.traffic is null", file=sys.stderr)
-
+    roofline = roofline_block(wl, kms, launch_ms, args.workload, rank)
     out = {
         "metric": METRIC if isinstance(wl, AllSources) else (
             "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN"
@@ -733,28 +905,15 @@ def main() -> None:
             "units_per_step_per_rank": wl.units,
             "parallelism": wl.parallelism,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "kernel": dominant,
-            "kernel_ms": kms,
-            "kernel_bytes": kbytes,
-            # the whole execute: every kernel's compulsory bytes over their summed time
-            "execute_frac": sum(kbytes.values()) / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            # SURVEY.md §8(d)'s per-solve figure (a full CSR sweep charged to every
-            # solve) over the compulsory bytes: how much sweep work batching shares
-            "survey_bytes_per_launch": wl.survey_bytes,
-            "reuse_factor": wl.survey_bytes / sum(kbytes.values()),
-        },
+        "roofline": roofline,
         "cpu_baseline": None,
     }
+    if parity is not None:
+        out["parity"] = parity
     if getattr(wl, "gather", False):
         out["config"]["gather_bytes_per_step"] = wl.gather_bytes
+    if isinstance(wl, AllSources):
+        out["config"]["results"] = wl.results
     if isinstance(wl, AllSources):
         out["config"]["next_hop_rows"] = wl.narrow  # u32 | u8 | sliced (bit planes)
     if isinstance(wl, WhatIfAllLinks):

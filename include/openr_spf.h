@@ -145,7 +145,8 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
  * sweep, per-level stores), 2 msbfs_planes_kernel (32 sources, register bit
  * planes, rows written once), 3 exact_spf_kernel, 4 spf_big_kernel (graphs
  * beyond the LDS-resident kernels: one source at a time on the whole chip,
- * next hops inside); *narrow = 0 when the
+ * next hops inside), 5 mssp_kernel (weighted, positive metrics: 2-16 sources
+ * per workgroup, u16 labels in LDS, min-plus sweeps); *narrow = 0 when the
  * next-hop pass (ecmp_kernel) reads the u32 rows, 1 when it reads u8 rows,
  * 2 when slice_rows_kernel turns the u8 rows into bit planes and
  * ecmp_sliced_kernel matches those.
@@ -167,6 +168,16 @@ spf_status spf_plan_traffic_phases(const spf_plan* plan, uint64_t* bytes);
  * synchronisation, no allocation: capturable into a hipGraph. */
 spf_status spf_plan_execute(spf_plan* plan, uint32_t* d_dist, uint32_t* d_nh,
                             void* stream);
+/* Per-source digests of an execute's output (d_dist / d_nh as passed to
+ * spf_plan_execute), enqueued on `stream`: d_out[i] (u64) = sum mod 2^64 over
+ * reachable v of mix(mix(v + 1) + dist(v)) ^ fnv1a64(nh(v) as u32 words),
+ * mix = splitmix64's finaliser, nh(v) = v's next-hop set as a bitset over the
+ * source's distinct up neighbours (the what-if digest's node term).  What a
+ * rank ships when its rows stay resident on its GPU (multi-GPU all-sources),
+ * and what the parity tests compare with the oracle's digests.  No
+ * reference counterpart. */
+spf_status spf_plan_digest(spf_plan* plan, const void* d_dist, const uint32_t* d_nh,
+                           uint64_t* d_out, void* stream);
 /* The narrow (u8) distance rows of the plan's last execute, for plans whose
  * distance kernel keeps them (spf_plan_kernels: *narrow != 0): row i (source
  * srcs[i]) byte v = d(srcs[i], v) when below 254, 254 when d >= 254, 255
@@ -304,7 +315,7 @@ void spf_whatif_plan_destroy(spf_whatif_plan* plan);
 uint32_t spf_whatif_plan_failures(const spf_whatif_plan* plan);
 spf_status spf_whatif_plan_links(const spf_whatif_plan* plan, uint32_t* links /* [n_fail] */);
 /* d_out = [n_fail] digests, d_base = 1 digest (may be NULL).  Enqueued on
- * `stream` (cooperative launch for the unfailed solve); no host
+ * `stream` (a grid-resident launch for the unfailed solve); no host
  * synchronisation.  Failures with a large affected region are repaired on a
  * side stream owned by the ctx, forked from and joined back into `stream`
  * with events, so all work is ordered after earlier work on `stream` and
@@ -351,6 +362,16 @@ spf_status spf_routes(spf_ctx* ctx, uint32_t me, const uint32_t* set_ptr,
  * distance stores, pull sweep, barrier; end), per wave: out[w*64] = count,
  * out[w*64 + 1 ..] = clocks of wave w (16 waves).  Copies up to cap words. */
 spf_status spf_debug_stamps(spf_ctx* ctx, uint64_t* out, uint32_t cap, uint32_t* n);
+
+/* Waits for every launch on the context's device and reports whether a
+ * grid-resident kernel's barrier (spf_big_kernel, the what-if unfailed pass,
+ * the global-memory SSSP, the what-if group teams) gave up waiting: its spin
+ * is bounded so a block that never arrives cannot hang the GPU, and the
+ * outputs of that launch are then invalid.  SPF_E_HIP (and the flag is
+ * cleared) when one did; SPF_OK otherwise.  The synchronous convenience calls
+ * (spf_solve, spf_whatif_solve, spf_whatif_stats, ...) check it themselves.
+ * No reference counterpart. */
+spf_status spf_device_check(spf_ctx* ctx);
 
 /* ---- counters ----------------------------------------------------------- */
 /* Logical single-source solves executed (the reference's decision.spf_runs,

@@ -165,6 +165,7 @@ PROTOTYPES = {
     "spf_plan_traffic_phases": (C.c_int, [_vp, _u64p]),
     "spf_plan_execute": (C.c_int, [_vp, _vp, _vp, _vp]),
     "spf_plan_copy_narrow_rows": (C.c_int, [_vp, _vp, _vp]),
+    "spf_plan_digest": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "spf_plan_execute_host": (C.c_int, [_vp, _u32p, _u32p]),
     "spf_plan_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_plan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
@@ -177,6 +178,7 @@ PROTOTYPES = {
     "spf_preds": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _u32p, C.c_uint32, _u32p,
                             _u32p, _u32p, C.c_uint32, _u32p]),
     "spf_solves": (C.c_uint64, [_vp]),
+    "spf_device_check": (C.c_int, [_vp]),
     "spf_debug_stamps": (C.c_int, [_vp, _u64p, C.c_uint32, _u32p]),
     "spf_ksp2_plan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.POINTER(_vp)]),
     "spf_ksp2_plan_destroy": (None, [_vp]),

@@ -39,12 +39,31 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every source to an object in parallel (hipcc -c, one process
+    per file, at most 8), then link the shared library."""
+    from concurrent.futures import ThreadPoolExecutor
+
     if not force and not needs_build():
         return OUT
     OUT.parent.mkdir(parents=True, exist_ok=True)
+    obj_dir = OUT.parent / "obj"
+    obj_dir.mkdir(exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             f"-I{ROOT / 'include'}"]
+
+    def compile_one(src: Path) -> Path:
+        obj = obj_dir / (src.name + ".o")
+        cmd = [hipcc(), *flags, "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "8")), 8))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", f"-I{ROOT / 'include'}", *map(str, SOURCES), "-o", str(tmp)]
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -47,6 +47,14 @@ struct DevBuf {
   }
 };
 
+// exact_spf_kernel scratch (exact.hip): per-wave heap, labels, next hops.
+struct ExactScratch {
+  DevBuf<uint8_t> buf;
+  DevBuf<uint32_t> ctr;  // next source
+  uint64_t per_wave = 0;
+  uint32_t waves = 0, wmax = 0;
+};
+
 }  // namespace spfi
 
 struct spf_ctx {
@@ -68,8 +76,7 @@ struct spf_ctx {
   std::vector<uint32_t> row_ptr, col, wt, rev, link;
   std::vector<int32_t> met;  // metrics as advertised (exact kernel)
   spfi::DevBuf<int32_t> d_met;
-  spfi::DevBuf<uint8_t> d_exact;      // exact kernel: per-wave heap/labels/next hops
-  spfi::DevBuf<uint32_t> d_exact_ctr;
+  spfi::ExactScratch exact1;  // spf_solve_exact (synchronous one-shot solves) only
   std::vector<uint8_t> ovl;
   std::vector<uint32_t> nb_ptr, nb_id, nb_w;  // distinct up neighbours
   uint32_t big_nodes = 0;                    // nodes with degree > kBigDeg
@@ -87,6 +94,11 @@ struct spf_ctx {
   spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
   spfi::DevBuf<uint32_t> d_gq, d_gq2, d_gbm, d_gctr;  // global-memory SSSP scratch
   spfi::DevBuf<uint32_t> d_gbar;  // its grid-barrier counters (whatif.hip XGrid)
+  // mssp_kernel tables (mssp.hip), valid for graph epoch mp_epoch
+  spfi::DevBuf<uint32_t> d_mp_ell, d_mp_smap;
+  uint32_t mp_slots = 0, mp_ovf_at = 0;
+  bool mp_redo = true;
+  uint64_t mp_epoch = ~0ull;
   spfi::DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
 };
 
@@ -104,7 +116,10 @@ struct spf_plan {
   bool sliced = false;  // ... and the next-hop pass on its bit-sliced form
   bool expand = false;  // ... the u32 rows expanded from the u8 ones (BFS stores bytes only)
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
+  bool mp = false;      // weighted: mssp_kernel (mssp.hip), S sources per workgroup
+  spfi::DevBuf<uint32_t> d_redo;  // mp: rows whose u16 labels may have overflowed
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
+  spfi::ExactScratch xs;  // exact: the kernel's scratch, reserved by build_plan
   spfi::DevBuf<uint32_t> d_srcs, d_closure, d_row_of, d_req_rows, d_D;
   spfi::DevBuf<uint8_t> d_Dn;
   spfi::DevBuf<uint32_t> d_S, d_maxd;  // sliced rows (+ dead row); deepest BFS level + 8 counters
@@ -114,6 +129,7 @@ struct spf_plan {
   spfi::DevBuf<uint32_t> b_q, b_q2, b_bm, b_ctr, b_nbr_bit, b_nhb, b_lvl, b_order, b_misc, b_parent;
   spfi::DevBuf<uint32_t> b_bar;  // spf_big_kernel's grid-barrier counters
   spfi::DevBuf<uint64_t> d_nh_off;
+  spfi::DevBuf<uint32_t> d_words;  // [n_src] next-hop bitmaps per source (spf_plan_digest)
   spfi::DevBuf<uint32_t> d_nb_row, d_nb_row_off, d_nb_drained;  // next-hop pass inputs
   uint32_t dead = 0;  // nb_row value of a drained neighbour
   spfi::DevBuf<uint32_t> d_slot_src;  // next-hop blocks: source per (slot, XCD)
@@ -155,16 +171,27 @@ spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
                        const uint32_t* ign, uint32_t* D, hipStream_t s,
                        const uint32_t* wt = nullptr, const uint8_t* ovl = nullptr,
-                       uint8_t* Dn = nullptr);
+                       uint8_t* Dn = nullptr, const uint32_t* redo = nullptr);
+// Multi-source weighted distances (mssp.hip): mssp_words() = LDS words per
+// node (0: does not apply), mssp_prepare() builds its tables for the current
+// graph epoch (plan build), launch_mssp() enqueues it (+ the overflow redo
+// pass over `redo` = [1 + rows] words of plan scratch).
+uint32_t mssp_words(const spf_ctx* c);
+spf_status mssp_prepare(spf_ctx* c);
+spf_status mssp_set_lds_limits(spf_ctx* c);
+spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
+                       uint8_t* Dn, uint32_t* redo, hipStream_t s);
 // Single-source SSSP in global memory, one cooperative grid (any graph
 // size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,
                         hipStream_t s);
 // The exact kernel (exact.hip) over n_src sources: dist rows (u32 or u64,
 // pitch entries), planar next-hop bitmaps at nh_off, optional pop ranks.
-spf_status launch_exact(spf_ctx* c, const uint32_t* d_srcs, uint32_t n_src, const uint64_t* d_nh_off,
-                        uint32_t Wmax, bool hop, bool dist64, const uint32_t* ign, void* d_dist,
-                        uint32_t* d_nh, uint32_t* d_pop, hipStream_t s);
+spf_status exact_reserve(spf_ctx* c, ExactScratch* x, uint32_t n_src, uint32_t Wmax);
+spf_status launch_exact(spf_ctx* c, ExactScratch* x, const uint32_t* d_srcs, uint32_t n_src,
+                        const uint64_t* d_nh_off, uint32_t Wmax, bool hop, bool dist64,
+                        const uint32_t* ign, void* d_dist, uint32_t* d_nh, uint32_t* d_pop,
+                        hipStream_t s);
 // spf_big_kernel (whatif.hip): the plan's sources one after another on the
 // whole chip -- frontier SSSP into the dist rows, next hops in distance
 // order, transposed into the plan's bitmaps.  Positive metrics or hop counts.

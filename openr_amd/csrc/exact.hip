@@ -49,6 +49,7 @@ struct ExactArgs {
   uint8_t* scratch;
   uint64_t per_wave;
   uint32_t* ctr;           // [1] next source
+  uint32_t waves;          // waves with scratch; surplus waves of the last block exit
 };
 
 struct Scratch {
@@ -111,6 +112,7 @@ enum { kNone = 0, kReset = 1, kUnion = 2 };
 __global__ __launch_bounds__(kExactThreads) void exact_spf_kernel(ExactArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * (kExactThreads / 64) + (threadIdx.x >> 6);
+  if (wave >= a.waves) return;  // wave-uniform: no scratch for it
   uint8_t* base = a.scratch + wave * a.per_wave;
   const uint32_t N = a.N, W = a.Wmax;
   Scratch s;
@@ -244,26 +246,43 @@ __global__ __launch_bounds__(kExactThreads) void exact_spf_kernel(ExactArgs a) {
 
 namespace spfi {
 
-// Enqueue the exact kernel over the plan's sources (include/openr_spf.h
-// SPF_FLAG_DIST64, and every plan outside the fast kernels' envelope).
-spf_status launch_exact(spf_ctx* c, const uint32_t* d_srcs, uint32_t n_src, const uint64_t* d_nh_off,
-                        uint32_t Wmax, bool hop, bool dist64, const uint32_t* ign, void* d_dist,
-                        uint32_t* d_nh, uint32_t* d_pop, hipStream_t s) {
+// Scratch of the exact kernel for up to `n_src` sources with at most `Wmax`
+// next-hop words per node: waves x (16N + 4NW + N) bytes, at most 4 GB, at
+// most 16 waves per CU.  Allocation happens here (plan build / one-shot
+// solves), never inside spf_plan_execute.
+spf_status exact_reserve(spf_ctx* c, ExactScratch* x, uint32_t n_src, uint32_t Wmax) {
   const uint64_t N = c->N;
   const uint64_t W = std::max<uint32_t>(Wmax, 1);
-  const uint64_t per_wave = ((8 * N + 8 * N + 4 * N * W + N) + 255) & ~uint64_t(255);
+  x->per_wave = ((8 * N + 8 * N + 4 * N * W + N) + 255) & ~uint64_t(255);
+  x->wmax = (uint32_t)W;
   constexpr uint64_t kBudget = 4ull << 30;
-  uint64_t waves = std::min<uint64_t>(n_src, std::max<uint64_t>(1, kBudget / per_wave));
+  uint64_t waves = std::min<uint64_t>(std::max<uint32_t>(n_src, 1), std::max<uint64_t>(1, kBudget / x->per_wave));
   waves = std::min<uint64_t>(waves, 16ull * c->n_cu);
-  const uint64_t blocks = (waves + 3) / 4;
-  HIP_TRY(c, c->d_exact.alloc(blocks * 4 * per_wave));
-  HIP_TRY(c, c->d_exact_ctr.alloc(1));
-  HIP_TRY(c, hipMemsetAsync(c->d_exact_ctr.p, 0, 4, s));
+  x->waves = (uint32_t)waves;
+  HIP_TRY(c, x->buf.alloc(waves * x->per_wave));
+  HIP_TRY(c, x->ctr.alloc(1));
+  return SPF_OK;
+}
+
+// Enqueue the exact kernel over the plan's sources (include/openr_spf.h
+// SPF_FLAG_DIST64, and every plan outside the fast kernels' envelope).  No
+// allocation, no host synchronisation: the scratch `x` (reserved for at
+// least Wmax words) belongs to the caller -- the plan, or the context for
+// the synchronous one-shot solves.
+spf_status launch_exact(spf_ctx* c, ExactScratch* x, const uint32_t* d_srcs, uint32_t n_src,
+                        const uint64_t* d_nh_off, uint32_t Wmax, bool hop, bool dist64,
+                        const uint32_t* ign, void* d_dist, uint32_t* d_nh, uint32_t* d_pop,
+                        hipStream_t s) {
+  if (!x->buf.p || !x->ctr.p || Wmax > x->wmax)
+    return fail(c, SPF_E_STATE, "exact kernel scratch not reserved for %u next-hop words", Wmax);
+  HIP_TRY(c, hipMemsetAsync(x->ctr.p, 0, 4, s));
+  const uint32_t waves = std::min<uint32_t>(x->waves, std::max<uint32_t>(n_src, 1));
+  const uint32_t blocks = (waves + 3) / 4;
   ExactArgs a{c->d_row_ptr.p, c->d_col.p, c->d_met.p, c->d_ovl.p, c->d_link.p, ign,
               c->d_nb_ptr.p, c->d_nb_id.p, d_srcs, n_src, c->N, c->pitch, hop ? 1u : 0u,
-              dist64 ? 1u : 0u, (uint32_t)W, d_dist, d_nh, d_nh_off, d_pop, c->d_exact.p,
-              per_wave, c->d_exact_ctr.p};
-  hipLaunchKernelGGL(exact_spf_kernel, dim3((uint32_t)blocks), dim3(kExactThreads), 0, s, a);
+              dist64 ? 1u : 0u, x->wmax, d_dist, d_nh, d_nh_off, d_pop, x->buf.p,
+              x->per_wave, x->ctr.p, waves};
+  hipLaunchKernelGGL(exact_spf_kernel, dim3(blocks), dim3(kExactThreads), 0, s, a);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }

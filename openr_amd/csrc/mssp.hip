@@ -1,0 +1,350 @@
+// ============================================================================
+//  mssp.hip -- multi-source weighted SPF distances (positive metrics): S
+//  sources per workgroup, their distance rows resident in LDS as packed u16
+//  pairs, relaxed by min-plus pull sweeps over a sliced-ELL copy of the
+//  in-edges until nothing changes.
+//
+//  Reference: LinkState::runSpf (openr/decision/LinkState.cpp:808-882) with
+//  useLinkMetric = true; production metrics are RTT-derived
+//  (openr/link-monitor/LinkMonitor.cpp:44-47), so the weighted path is the
+//  one a deployment runs.  For positive metrics the final distances are the
+//  order-free fixed point
+//      d_s(s) = 0,  d_s(v) = min over up in-edges u -> v with u expanded
+//                            (u == s or u not drained) of d_s(u) + w(u, v)
+//  (DESIGN.md §3), which any sequence of monotone relaxations reaches; the
+//  next-hop pass (ecmp_kernel) then works from the rows as for every other
+//  distance kernel.
+//
+//  Layout: LDS row block dist[v][SD] (u32 words, each two u16 labels: source
+//  2q in the low half, 2q + 1 in the high half), 0xFFFF = not reached, node N
+//  = the all-unreached padding target of the ELL.  One pull sweep: each wave
+//  owns whole 64-node slices (dealt by width, mp_smap), lane = node; for
+//  every ELL column j the lane's in-neighbour u and in-weight w come in one
+//  packed u32 (u | w << 16); a node whose labels did not change since the
+//  last sweep it was read in is skipped (3 rotating change bitmaps; a column
+//  is skipped by the whole wave when no lane's neighbour changed), otherwise
+//  its SD words are read with one LDS load and folded into the lane's
+//  accumulators with v_pk_add_u16 (clamp) + v_pk_min_u16: one instruction
+//  pair per two sources.  Updates are in place (Gauss-Seidel); every value
+//  ever written is the length of a real walk, so the result is exact once a
+//  sweep changes nothing.  Drained nodes take labels but never set their
+//  change bit, so they are never expanded; each source's own out-edges are
+//  applied once at the start (a drained source is expanded, :831-838).
+//
+//  u16 labels: clamped sums are min(true, 0xFFFF) exactly, so a true
+//  distance >= 0xFFFF shows up as some node in [0xFFFF - max metric,
+//  0xFFFF) on its path; such rows are listed in `redo` and recomputed by
+//  sssp_kernel (u32 labels).  The host skips that launch when the graph's
+//  hop diameter bounds every distance below the threshold.
+// ============================================================================
+#include "engine_internal.h"
+
+using namespace spfi;
+
+namespace {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t add_sat2(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, a),
+                                                                    __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t min2(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                __builtin_bit_cast(u16x2, b)));
+}
+
+constexpr int kMpThreads = 1024;
+constexpr uint32_t kMpWaves = kMpThreads / 64;
+constexpr uint32_t kMpNoSlice = 0xFFFFFFFFu;
+constexpr size_t kMpMaxLds = 160 * 1024;
+constexpr size_t kMpStaticLds = 256;  // the kernel's own static LDS (__syncthreads_or)
+
+// LDS minimum of one u16 half of a word (CAS loop: two sources share a word)
+__device__ void lds_min16(uint32_t* p, uint32_t half, uint32_t val) {
+  uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (;;) {
+    const uint32_t cur = half ? old >> 16 : old & 0xFFFFu;
+    if (val >= cur) return;
+    const uint32_t nw = half ? (old & 0xFFFFu) | (val << 16) : (old & 0xFFFF0000u) | val;
+    const uint32_t got = atomicCAS(p, old, nw);
+    if (got == old) return;
+    old = got;
+  }
+}
+
+template <int SD>
+__device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&d)[SD]) {
+  if constexpr (SD == 4) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+  } else if constexpr (SD == 2) {
+    const uint2 x = *reinterpret_cast<const uint2*>(p);
+    d[0] = x.x; d[1] = x.y;
+  } else if constexpr (SD == 8) {
+    const uint4 x = reinterpret_cast<const uint4*>(p)[0], y = reinterpret_cast<const uint4*>(p)[1];
+    d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+    d[4] = y.x; d[5] = y.y; d[6] = y.z; d[7] = y.w;
+  } else {
+    d[0] = p[0];
+  }
+}
+
+template <int SD>
+__global__ __launch_bounds__(kMpThreads) void mssp_kernel(
+    const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ ell,
+    const uint32_t* __restrict__ smap, uint32_t slots, const uint32_t* __restrict__ row_ptr,
+    const uint32_t* __restrict__ col, const uint32_t* __restrict__ wt,
+    const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src, uint32_t n_rows,
+    uint32_t N, uint32_t pitch, uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
+    uint32_t ovf_at, uint32_t* __restrict__ redo) {
+  constexpr uint32_t S = 2 * SD;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t bw = (N + 32) / 32;  // change-bitmap words (nodes 0..N)
+  uint32_t* dist = reinterpret_cast<uint32_t*>(smem);  // [(N + 1) * SD]
+  uint32_t* bits = dist + (size_t)(N + 1) * SD;          // [3][bw]
+  uint32_t* flag = bits + 3 * bw;                        // [3]
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t r0 = blockIdx.x * S;
+  const uint32_t nb = min(S, n_rows - r0);
+
+  for (uint32_t i = tid; i < (N + 1) * SD; i += kMpThreads) dist[i] = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < 3 * bw; i += kMpThreads) bits[i] = 0;
+  if (tid < 3) flag[tid] = 0;
+  __syncthreads();
+  if (tid < nb) lds_min16(&dist[rows_src[r0 + tid] * SD + tid / 2], tid & 1, 0);
+  __syncthreads();
+  // each source's own out-edges, once (a wave per source): the source is
+  // expanded even when drained; its label 0 never changes again
+  for (uint32_t si = wave; si < nb; si += kMpWaves) {
+    const uint32_t s = rows_src[r0 + si];
+    const uint32_t e1 = row_ptr[s + 1];
+    for (uint32_t e = row_ptr[s] + lane; e < e1; e += 64) {
+      const uint32_t v = col[e];
+      lds_min16(&dist[v * SD + si / 2], si & 1, wt[e]);
+      if (!ovl[v]) atomicOr(&bits[v >> 5], 1u << (v & 31));
+    }
+  }
+  __syncthreads();
+
+  for (uint32_t it = 0;; ++it) {
+    const uint32_t* cur = bits + (it % 3) * bw;
+    uint32_t* nxt = bits + ((it + 1) % 3) * bw;
+    uint32_t* old = bits + ((it + 2) % 3) * bw;  // read by nobody this sweep
+    for (uint32_t i = tid; i < bw; i += kMpThreads) old[i] = 0;
+    if (tid == 0) flag[(it + 1) % 3] = 0;
+    bool changed = false;
+    for (uint32_t k = 0; k < slots; ++k) {
+      const uint32_t sl = smap[wave * slots + k];
+      if (sl == kMpNoSlice) break;  // a wave's slots are filled from the front
+      const uint32_t v = sl * 64 + lane;
+      const uint32_t b = sell_ptr[sl], w = (sell_ptr[sl + 1] - b) / 64;
+      uint32_t acc[SD];
+#pragma unroll
+      for (int q = 0; q < SD; ++q) acc[q] = 0xFFFFFFFFu;
+      bool got = false;
+      const uint32_t* ep = ell + b + lane;
+      uint32_t ent = w ? ep[0] : 0u;
+      for (uint32_t j = 0; j < w; ++j) {
+        const uint32_t cent = ent;
+        if (j + 1 < w) ent = ep[(j + 1) * 64];  // next column's entry in flight
+        const uint32_t u = cent & 0xFFFFu;
+        const uint32_t m = 1u << (u & 31);
+        const bool c = ((cur[u >> 5] | nxt[u >> 5]) & m) != 0;
+        if (!__builtin_amdgcn_ballot_w64(c)) continue;  // no lane's neighbour changed
+        if (c) {
+          const uint32_t wp = (cent >> 16) * 0x00010001u;
+          uint32_t d[SD];
+          load_words<SD>(&dist[u * SD], d);
+#pragma unroll
+          for (int q = 0; q < SD; ++q) acc[q] = min2(acc[q], add_sat2(d[q], wp));
+          got = true;
+        }
+      }
+      if (got && v < N) {
+        uint32_t* dv = &dist[v * SD];
+        bool dec = false;
+#pragma unroll
+        for (int q = 0; q < SD; ++q) {
+          const uint32_t o = dv[q], nn = min2(o, acc[q]);
+          if (nn != o) {
+            dv[q] = nn;
+            dec = true;
+          }
+        }
+        if (dec) {
+          changed = true;
+          if (!ovl[v]) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+        }
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(changed) && lane == 0) flag[it % 3] = 1;
+    __syncthreads();
+    if (!flag[it % 3]) break;
+  }
+
+  // ---- rows: u32 (kInf = unreached, and past N as sssp_kernel) and the
+  // u8 copy next-hop pass; overflow-suspect rows go to `redo` ----
+  for (uint32_t si = 0; si < nb; ++si) {
+    const uint32_t row = r0 + si;
+    uint32_t ovf = 0;
+    for (uint32_t q = tid; q < pitch / 4; q += kMpThreads) {
+      uint32_t o[4];
+      uint32_t nb8 = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t v = 4 * q + t;
+        uint32_t d = kInf;
+        if (v < N) {
+          const uint32_t x = dist[v * SD + si / 2];
+          const uint32_t h = (si & 1) ? x >> 16 : x & 0xFFFFu;
+          if (h != 0xFFFFu) {
+            d = h;
+            ovf |= h >= ovf_at;
+          }
+        }
+        o[t] = d;
+        nb8 |= (d == kInf ? 0xFFu : min(d, 254u)) << (8 * t);
+      }
+      reinterpret_cast<uint4*>(D + (size_t)row * pitch)[q] = make_uint4(o[0], o[1], o[2], o[3]);
+      if (Dn) reinterpret_cast<uint32_t*>(Dn + (size_t)row * pitch)[q] = nb8;
+    }
+    if (__syncthreads_or(ovf) && tid == 0 && redo) redo[1 + atomicAdd(redo, 1u)] = row;
+  }
+}
+
+template <int SD>
+size_t mp_lds(uint32_t N) {
+  return 4ull * (N + 1) * SD + 4ull * 3 * ((N + 32) / 32) + 16;
+}
+
+bool mp_fits(uint32_t N, uint32_t sd) {
+  return 4ull * (N + 1) * sd + 4ull * 3 * ((N + 32) / 32) + 16 + kMpStaticLds <= kMpMaxLds;
+}
+
+}  // namespace
+
+namespace spfi {
+
+// Dwords per node of mssp_kernel's LDS rows (sources per workgroup / 2) for
+// this graph, 0 when the multi-source kernel does not apply: positive
+// metrics below 2^16 - 1, node ids below 2^16 (packed ELL entries), rows of
+// at least two sources in LDS.  SPF_MSSP=0 turns it off (A/B, tests).
+uint32_t mssp_words(const spf_ctx* c) {
+  if (const char* e = std::getenv("SPF_MSSP"))
+    if (e[0] == '0') return 0;
+  if (c->nonpos || c->max_metric >= 0xFFFFu || c->N >= 0xFFFFu) return 0;
+  if (const char* e = std::getenv("SPF_MSSP_SD")) {  // A/B: fixed sources per workgroup
+    const uint32_t sd = (uint32_t)atoi(e);
+    return (sd == 1 || sd == 2 || sd == 4 || sd == 8) && mp_fits(c->N, sd) ? sd : 0;
+  }
+  for (uint32_t sd : {8u, 4u, 2u, 1u})
+    if (mp_fits(c->N, sd)) return sd;
+  return 0;
+}
+
+// The packed in-edge ELL (u | w(u -> v) << 16 at the sliced-ELL position of
+// v's j-th CSR edge, padding N | 0) and the per-wave slice map, rebuilt when
+// the graph changed (metrics are patchable in place).  Also the bound that
+// decides whether any row can overflow u16 labels.
+spf_status mssp_prepare(spf_ctx* c) {
+  if (c->mp_epoch == c->epoch && c->d_mp_ell.p) return SPF_OK;
+  const uint32_t N = c->N;
+  const uint32_t n_slices = (N + 63) / 64;
+  std::vector<uint32_t> ell(c->sell_ptr.back(), N);
+  for (uint32_t v = 0; v < N; ++v) {
+    const uint32_t sl = v / 64, ln = v % 64;
+    for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j) {
+      const uint32_t e = c->row_ptr[v] + j;
+      ell[c->sell_ptr[sl] + j * 64 + ln] = c->col[e] | (c->wt[c->rev[e]] << 16);
+    }
+  }
+  // slices dealt widest first to the wave with the least width so far
+  const uint32_t slots = std::max(1u, (n_slices + kMpWaves - 1) / kMpWaves);
+  std::vector<uint32_t> order(n_slices), load(kMpWaves, 0), used(kMpWaves, 0);
+  for (uint32_t i = 0; i < n_slices; ++i) order[i] = i;
+  auto width = [&](uint32_t sl) { return (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / 64; };
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return width(a) > width(b); });
+  std::vector<uint32_t> smap((size_t)kMpWaves * slots, kMpNoSlice);
+  for (uint32_t sl : order) {
+    uint32_t best = kMpWaves;
+    for (uint32_t w = 0; w < kMpWaves; ++w)
+      if (used[w] < slots && (best == kMpWaves || load[w] < load[best])) best = w;
+    smap[(size_t)best * slots + used[best]++] = sl;
+    load[best] += std::max(1u, width(sl));
+  }
+  // overflow bound: with no drained node, d(s, v) <= max metric x hops(s, v)
+  // <= max metric x 2 ecc(r) for any r of the component (BFS from one node
+  // per component); otherwise only the trivial bound (N - 1) x max metric
+  uint64_t bound = (uint64_t)(N ? N - 1 : 0) * c->max_metric;
+  bool drained = false;
+  for (uint32_t v = 0; v < N; ++v) drained |= c->ovl[v] != 0;
+  if (!drained) {
+    std::vector<uint32_t> hop(N, kInf), q;
+    uint32_t ecc = 0;
+    for (uint32_t r = 0; r < N; ++r) {
+      if (hop[r] != kInf) continue;
+      hop[r] = 0;
+      q.assign(1, r);
+      for (size_t h = 0; h < q.size(); ++h) {
+        const uint32_t u = q[h];
+        for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+          if (hop[c->col[e]] == kInf) {
+            hop[c->col[e]] = hop[u] + 1;
+            ecc = std::max(ecc, hop[u] + 1);
+            q.push_back(c->col[e]);
+          }
+      }
+    }
+    bound = std::min<uint64_t>(bound, 2ull * ecc * c->max_metric);
+  }
+  c->mp_ovf_at = 0xFFFFu - c->max_metric;
+  c->mp_redo = bound >= c->mp_ovf_at;
+  c->mp_slots = slots;
+  HIP_TRY(c, c->d_mp_ell.upload(ell.data(), ell.size(), c->stream));
+  HIP_TRY(c, c->d_mp_smap.upload(smap.data(), smap.size(), c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->mp_epoch = c->epoch;
+  return SPF_OK;
+}
+
+spf_status mssp_set_lds_limits(spf_ctx* c) {
+  const int lim = (int)(kMpMaxLds - kMpStaticLds);
+  for (const void* f : {(const void*)mssp_kernel<1>, (const void*)mssp_kernel<2>,
+                        (const void*)mssp_kernel<4>, (const void*)mssp_kernel<8>})
+    HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+  return SPF_OK;
+}
+
+// Distances of `rows` sources (device list rows_src) into D [rows][pitch]
+// (+ the u8 copy Dn): mssp_kernel, then -- when an overflow is possible --
+// sssp_kernel over the rows it listed in `redo` ([1 + rows] words).
+spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
+                       uint8_t* Dn, uint32_t* redo, hipStream_t s) {
+  const uint32_t sd = mssp_words(c);
+  if (!sd) return fail(c, SPF_E_STATE, "mssp kernel does not apply to this graph");
+  if (c->mp_epoch != c->epoch) return fail(c, SPF_E_STATE, "mssp tables stale: rebuild the plan");
+  if (c->mp_redo) HIP_TRY(c, hipMemsetAsync(redo, 0, 4, s));
+  const uint32_t S = 2 * sd;
+  const dim3 g((rows + S - 1) / S), b(kMpThreads);
+  const uint32_t N = c->N;
+  uint32_t* rd = c->mp_redo ? redo : nullptr;
+#define MP_LAUNCH(SDV)                                                                            \
+  hipLaunchKernelGGL(mssp_kernel<SDV>, g, b, mp_lds<SDV>(N), s, c->d_sell_ptr.p, c->d_mp_ell.p,   \
+                     c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
+                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd)
+  switch (sd) {
+    case 8: MP_LAUNCH(8); break;
+    case 4: MP_LAUNCH(4); break;
+    case 2: MP_LAUNCH(2); break;
+    default: MP_LAUNCH(1); break;
+  }
+#undef MP_LAUNCH
+  HIP_TRY(c, hipGetLastError());
+  if (c->mp_redo)
+    return launch_sssp(c, rows_src, rows, false, nullptr, D, s, nullptr, nullptr, Dn, redo);
+  return SPF_OK;
+}
+
+}  // namespace spfi

@@ -128,7 +128,8 @@ __global__ __launch_bounds__(THREADS) void sssp_kernel(
     const uint32_t* __restrict__ link, const uint32_t* __restrict__ ign,
     const uint32_t* __restrict__ rows_src, uint32_t N, uint32_t pitch,
     uint32_t bm_words, uint32_t big_cap, uint32_t* __restrict__ D,
-    uint8_t* __restrict__ Dn /* optional u8 copy (npitch == pitch) */) {
+    uint8_t* __restrict__ Dn /* optional u8 copy (npitch == pitch) */,
+    const uint32_t* __restrict__ redo /* optional [count, rows...]: redo only those rows */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* dist = reinterpret_cast<uint32_t*>(smem);  // [pitch]
   uint32_t* bm = dist + pitch;                         // [bm_words] next frontier
@@ -140,7 +141,11 @@ __global__ __launch_bounds__(THREADS) void sssp_kernel(
   const uint32_t lane = lane_id();
   const uint32_t wave = tid >> 6;
   constexpr uint32_t kWaves = THREADS / 64;
-  const uint32_t row = blockIdx.x;
+  uint32_t row = blockIdx.x;
+  if (redo) {  // mssp_kernel's overflow rows (launched over all rows, mostly empty)
+    if (row >= redo[0]) return;
+    row = redo[1 + row];
+  }
   const uint32_t src = rows_src[row];
 
   for (uint32_t v = tid; v < pitch; v += THREADS) dist[v] = kInf;
@@ -1313,6 +1318,55 @@ __global__ void gather_rows_kernel(const uint32_t* __restrict__ D, uint32_t pitc
 }
 
 // ---------------------------------------------------------------------------
+//  per-source result digests (spf_plan_digest): the checksum a rank ships
+//  instead of its rows when results stay resident on its GPU
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t dg_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// Block (chunk of 256 destinations, source i); thread = destination v.  The
+// next-hop words of v are assembled 32 neighbours at a time from the planar
+// bitmaps (lanes of a wave read the same two words: broadcast loads) and fed
+// to FNV-1a in word order; the per-node terms are summed with a wave
+// reduction and one 64-bit atomic per wave.
+template <bool D64>
+__global__ __launch_bounds__(256) void digest_kernel(const void* __restrict__ dist, uint32_t pitch,
+                                                     uint32_t N, const uint32_t* __restrict__ nh,
+                                                     const uint64_t* __restrict__ nh_off,
+                                                     const uint32_t* __restrict__ words,
+                                                     unsigned long long* __restrict__ out) {
+  const uint32_t i = blockIdx.y;
+  const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+  uint64_t term = 0;
+  if (v < N) {
+    const uint64_t d = D64 ? reinterpret_cast<const uint64_t*>(dist)[(size_t)i * pitch + v]
+                           : reinterpret_cast<const uint32_t*>(dist)[(size_t)i * pitch + v];
+    if (d != (D64 ? ~0ull : (uint64_t)kInf)) {
+      const uint32_t k = words[i], wpm = pitch / 32;
+      const uint32_t* b = nh + nh_off[i] + v / 32;
+      const uint32_t sh = v % 32;
+      uint64_t f = 0xcbf29ce484222325ull;
+      for (uint32_t j0 = 0; j0 < k; j0 += 32) {
+        uint32_t w = 0;
+        const uint32_t jn = min(32u, k - j0);
+        for (uint32_t j = 0; j < jn; ++j) w |= ((b[(size_t)(j0 + j) * wpm] >> sh) & 1u) << j;
+        f ^= w;
+        f *= 0x100000001b3ull;
+      }
+      term = dg_mix64(dg_mix64((uint64_t)v + 1) + d) ^ f;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)term, o, 64), hi = __shfl_xor((uint32_t)(term >> 32), o, 64);
+    term += ((uint64_t)hi << 32) | lo;
+  }
+  if ((threadIdx.x & 63) == 0 && term) atomicAdd(&out[i], (unsigned long long)term);
+}
+
+// ---------------------------------------------------------------------------
 //  3. predecessor lists (pathLinks) of one source
 // ---------------------------------------------------------------------------
 // pass 0: count, pass 1: fill sorted by (dist[u], edge id) -- edge ids of one
@@ -1778,8 +1832,14 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     }
     p->nh_total = off;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (p->exact) {
+      const spf_status st = exact_reserve(c, &p->xs, n_src, p->wmax);
+      if (st != SPF_OK) return st;
+    }
     HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
     HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
+  HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
+    HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     p->epoch = c->epoch;
     return SPF_OK;
@@ -1844,7 +1904,15 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   HIP_TRY(c, p->d_row_of.upload(row_of.data(), N, c->stream));
   HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
+  HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
+  // weighted: S sources per workgroup on mssp_kernel where it applies
+  p->mp = !p->ms && !hop && mssp_words(c) > 0;
+  if (p->mp) {
+    const spf_status st = mssp_prepare(c);
+    if (st != SPF_OK) return st;
+    HIP_TRY(c, p->d_redo.alloc(1 + p->closure.size()));
+  }
   // weighted plans keep a u8 copy too when the pitches agree (the sssp
   // kernel writes it beside the u32 row; the next-hop pass compares bytes and
   // falls back to u32 rows per wave where the source's row saturates)
@@ -2012,7 +2080,7 @@ uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->clos
 
 spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
-  *bfs = p->big ? 4u : p->exact ? 3u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
+  *bfs = p->big ? 4u : p->exact ? 3u : p->mp ? 5u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
   *narrow = p->sliced ? 2u : p->narrow ? 1u : 0u;
   return SPF_OK;
 }
@@ -2073,6 +2141,11 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
     // expand plans: the u32 rows are written by the slicing pass instead
     bfs = groups * (csr + N) + (p->expand ? 0ull : rows * c->pitch * 4ull) +
           (p->narrow ? rows * c->npitch : 0ull);
+  } else if (p->mp) {  // per workgroup: the packed ELL + slice map once; rows written once
+    const uint64_t S = 2ull * mssp_words(c);
+    const uint64_t groups = (rows + S - 1) / S;
+    bfs = groups * (4ull * c->sell_ptr.back() + 4ull * c->sell_ptr.size() + 4ull * (N + 1) + N) +
+          rows * (4ull * c->pitch + (p->narrow ? c->npitch : 0ull));
   } else {
     bfs = rows * (4ull * (N + 1) + 8ull * E + N + 4ull * c->pitch + (p->narrow ? c->npitch : 0ull));
   }
@@ -2118,7 +2191,7 @@ namespace spfi {
 // Launch the SSSP kernel over `rows` closure rows (device list rows_src).
 spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool hop,
                        const uint32_t* ign, uint32_t* D, hipStream_t s, const uint32_t* wt,
-                       const uint8_t* ovl, uint8_t* Dn) {
+                       const uint8_t* ovl, uint8_t* Dn, const uint32_t* redo) {
   if (!wt) wt = c->d_wt.p;
   if (!ovl) ovl = c->d_ovl.p;
   const uint32_t N = c->N, pitch = c->pitch, bm_words = (N + 31) / 32;
@@ -2133,7 +2206,7 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 #define SSSP_LAUNCH(QT, U, TH)                                                            \
   hipLaunchKernelGGL((sssp_kernel<QT, U, TH>), g, dim3(TH), lds, s, c->d_row_ptr.p,       \
                      c->d_col.p, wt, ovl, c->d_link.p, ign, rows_src, N, pitch, bm_words,  \
-                     c->big_nodes, D, Dn)
+                     c->big_nodes, D, Dn, redo)
 #define SSSP_TH(QT, U)                                  \
   do {                                                  \
     if (threads >= 1024) SSSP_LAUNCH(QT, U, 1024);      \
@@ -2322,6 +2395,8 @@ spf_status set_lds_limits(spf_ctx* c) {
 #undef SSK
   for (const void* f : fns)
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+  const spf_status st = mssp_set_lds_limits(c);
+  if (st != SPF_OK) return st;
   done = true;
   return SPF_OK;
 }
@@ -2375,7 +2450,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     }
     const spf_status st =
         p->big ? launch_big(c, p, d_dist, d_nh, hop, s)
-               : launch_exact(c, p->d_srcs.p, p->n_src, p->d_nh_off.p, p->wmax, hop,
+               : launch_exact(c, &p->xs, p->d_srcs.p, p->n_src, p->d_nh_off.p, p->wmax, hop,
                               (p->flags & SPF_FLAG_DIST64) != 0, nullptr, d_dist, d_nh, nullptr, s);
     if (st != SPF_OK) return st;
     if (ev)
@@ -2396,6 +2471,8 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                        sliced ? p->d_maxd.p : nullptr, s,
                                        sliced && p->expand ? kSlSat : 0u)
+                  : p->mp ? launch_mssp(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
+                                        p->d_redo.p, s)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s, nullptr,
                                       nullptr, p->narrow ? p->d_Dn.p : nullptr);
   if (st != SPF_OK) return st;
@@ -2431,6 +2508,29 @@ spf_status spf_plan_copy_narrow_rows(spf_plan* p, uint8_t* d_out, void* stream) 
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   hipLaunchKernelGGL(gather_rows_u8_kernel, dim3(std::min<uint32_t>((c->npitch / 16 + 255) / 256, 64), p->n_src),
                      dim3(256), 0, s, p->d_Dn.p, c->npitch, p->d_req_rows.p, d_out);
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
+spf_status spf_plan_digest(spf_plan* p, const void* d_dist, const uint32_t* d_nh, uint64_t* d_out,
+                           void* stream) {
+  if (!p || !d_dist || !d_out || (p->nh_total && !d_nh))
+    return fail(p ? p->ctx : nullptr, SPF_E_INVALID, "spf_plan_digest: NULL argument");
+  spf_ctx* c = p->ctx;
+  if (p->shape != c->shape)
+    return fail(c, SPF_E_STATE, "graph reloaded since the plan was created: recreate it");
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  HIP_TRY(c, hipMemsetAsync(d_out, 0, 8ull * p->n_src, s));
+  if (!p->n_src) return SPF_OK;
+  const dim3 grid((c->N + 255) / 256, p->n_src);
+  const uint32_t* nh = p->nh_total ? d_nh : p->d_words.p;  // never read when every k = 0
+  auto* o = reinterpret_cast<unsigned long long*>(d_out);
+  if (p->flags & SPF_FLAG_DIST64)
+    hipLaunchKernelGGL(digest_kernel<true>, grid, dim3(256), 0, s, d_dist, c->pitch, c->N, nh,
+                       p->d_nh_off.p, p->d_words.p, o);
+  else
+    hipLaunchKernelGGL(digest_kernel<false>, grid, dim3(256), 0, s, d_dist, c->pitch, c->N, nh,
+                       p->d_nh_off.p, p->d_words.p, o);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2490,7 +2590,7 @@ spf_status spf_plan_execute_host(spf_plan* p, uint32_t* dist_out, uint32_t* nh_o
     HIP_TRY(c, hipMemcpyAsync(nh_out, p->h_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return SPF_OK;
+  return p->big ? spf_device_check(c) : SPF_OK;
 }
 
 spf_status spf_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
@@ -2532,7 +2632,8 @@ spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ig
   if (st != SPF_OK) return st;
   HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
   HIP_TRY(c, c->d_row.alloc(c->pitch));
-  if (sssp_lds_bytes(c->N, c->pitch, c->big_nodes, c->N <= 65535) > kMaxLds) {
+  const bool grid_resident = sssp_lds_bytes(c->N, c->pitch, c->big_nodes, c->N <= 65535) > kMaxLds;
+  if (grid_resident) {
     st = launch_gsssp(c, src, hop, ign, c->d_row.p, c->stream);
   } else {
     st = launch_sssp(c, c->d_one_src.p, 1, hop, ign, c->d_row.p, c->stream);
@@ -2541,7 +2642,7 @@ spf_status spf_sssp(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ig
   HIP_TRY(c, hipMemcpyAsync(dist_out, c->d_row.p, 4ull * c->N, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->solves += 1;
-  return SPF_OK;
+  return grid_resident ? spf_device_check(c) : SPF_OK;
 }
 
 spf_status spf_solve_exact(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* ignore_links,
@@ -2567,8 +2668,11 @@ spf_status spf_solve_exact(spf_ctx* c, uint32_t src, uint32_t flags, const uint3
   HIP_TRY(c, d_dist.alloc((size_t)c->pitch * (d64 ? 2 : 1)));
   HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(nh_words, 1)));
   if (pop_out) HIP_TRY(c, d_pop.alloc(c->pitch));
-  st = launch_exact(c, c->d_one_src.p, 1, d_off.p, std::max<uint32_t>(1, (k + 31) / 32), hop, d64,
-                    ign, d_dist.p, d_nh.p, pop_out ? d_pop.p : nullptr, c->stream);
+  const uint32_t wk = std::max<uint32_t>(1, (k + 31) / 32);
+  st = exact_reserve(c, &c->exact1, 1, wk);
+  if (st != SPF_OK) return st;
+  st = launch_exact(c, &c->exact1, c->d_one_src.p, 1, d_off.p, wk, hop, d64, ign, d_dist.p, d_nh.p,
+                    pop_out ? d_pop.p : nullptr, c->stream);
   if (st != SPF_OK) return st;
   if (d64 && dist64_out)
     HIP_TRY(c, hipMemcpyAsync(dist64_out, d_dist.p, 8ull * c->N, hipMemcpyDeviceToHost, c->stream));

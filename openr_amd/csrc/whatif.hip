@@ -34,8 +34,6 @@
 // ============================================================================
 #include "engine_internal.h"
 
-#include <hip/hip_cooperative_groups.h>
-
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -111,12 +109,12 @@ struct WiBase {
 };
 
 // ---------------------------------------------------------------------------
-//  cooperative (grid-synchronised) single-source SSSP and unfailed result
+//  grid-synchronised (XGrid) single-source SSSP and unfailed result
 // ---------------------------------------------------------------------------
 constexpr int kCoopThreads = 512;  // one block per CU: always co-resident
 constexpr uint32_t kCoopHubDeg = 32;  // nodes above this degree get a whole wave
 
-// Grid barrier of the cooperative kernels, XCD-hierarchical (MI355X_MICROARCH
+// Grid barrier of the grid-resident kernels, XCD-hierarchical (MI355X_MICROARCH
 // barrier-xcd: 4.1 us at 256 workgroups against 26.3 us for the software
 // cooperative_groups grid sync, which the what-if base pass crossed ~70
 // times).  Blocks are grouped by blockIdx % 8 (the XCD round-robin of the
@@ -128,6 +126,15 @@ constexpr uint32_t kCoopHubDeg = 32;  // nodes above this degree get a whole wav
 constexpr uint32_t kBarPad = 32;
 constexpr uint32_t kGridBarWords = 17 * kBarPad;  // cnt[8], top, gen[8]
 constexpr uint32_t kBarSpin = 1u << 26;            // ~seconds: never a silent hang
+
+// A barrier spin that ran out (a member never arrived: not co-resident, or
+// a fault) sets this word and falls through; the host reads and clears it
+// (spf_device_check) and reports SPF_E_HIP instead of the launch's output.
+__device__ uint32_t g_barrier_timeout;
+
+__device__ __forceinline__ void barrier_timed_out() {
+  __hip_atomic_store(&g_barrier_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 struct XGrid {
   uint32_t* bar;
@@ -145,21 +152,23 @@ struct XGrid {
       const uint32_t t =
           __hip_atomic_fetch_add(bar + x * kBarPad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t g = t / nx + 1;  // the generation this arrival completes
+      uint32_t k = 0;
       if (t % nx == nx - 1) {         // last of its group: the group's leader
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t k = 0; k < kBarSpin &&
-             __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g * ngroups;
+        for (; k < kBarSpin &&
+               __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g * ngroups;
              ++k)
           __builtin_amdgcn_s_sleep(1);
         __hip_atomic_store(gen, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        for (uint32_t k = 0; k < kBarSpin &&
-             __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g;
+        for (; k < kBarSpin &&
+               __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g;
              ++k)
           __builtin_amdgcn_s_sleep(1);
       }
+      if (k == kBarSpin) barrier_timed_out();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -278,7 +287,7 @@ __global__ __launch_bounds__(kCoopThreads) void gsssp_coop_kernel(CoopSssp a) {
   coop_sssp(grid, a);
 }
 
-// The unfailed result of a what-if batch in one cooperative launch:
+// The unfailed result of a what-if batch in one grid-resident launch:
 // SPF, next-hop bitsets in distance order (bucketed by distance value when
 // at most kMaxLevels distinct values occur, fixed-point sweeps otherwise),
 // result hash.
@@ -658,7 +667,7 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
 //  batched SPF + next hops beyond the LDS-resident kernels (plans on graphs
 //  too large for them, positive metrics or hop counts)
 // ---------------------------------------------------------------------------
-// One cooperative launch walks the plan's sources one after another, the
+// One grid-resident launch walks the plan's sources one after another, the
 // whole chip on each: frontier SSSP straight into the source's output row
 // (coop_sssp), next hops per node in distance order (level_nh, node-major
 // scratch nhb[v][W]), then a transpose into the plan's bitmap layout (bit v
@@ -778,7 +787,7 @@ struct TeamCtl {
 };
 
 // A team is a wave (64), a workgroup (1024) or a group of TEAM / 1024
-// workgroups of one cooperative launch on one XCD (team_sync = the agent-scope
+// workgroups of one grid-resident launch on one XCD (team_sync = the agent-scope
 // release -> arrival counter -> poll -> acquire hand-off of
 // MI355X_MICROARCH.md §Workgroup dispatch; the counter only grows, so the
 // barrier of the k-th call completes at k * G arrivals)
@@ -794,8 +803,12 @@ __device__ __forceinline__ void team_sync(TeamCtl* ctl) {
       const uint32_t ticket =
           __hip_atomic_fetch_add(&ctl->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t target = (ticket / G + 1) * G;
-      while (__hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+      uint32_t k = 0;
+      for (; k < kBarSpin &&
+             __hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
+           ++k)
         __builtin_amdgcn_s_sleep(1);
+      if (k == kBarSpin) barrier_timed_out();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1317,7 +1330,7 @@ __global__ __launch_bounds__(1024) void sort_big_kernel(const uint2* __restrict_
   }
 }
 
-// Group teams of G workgroups of kGroupWg threads (one cooperative launch, a
+// Group teams of G workgroups of kGroupWg threads (one grid-resident launch, a
 // workgroup per CU): the largest repairs get G CUs each.  Half-size
 // workgroups (8 waves, 2 per SIMD) co-reside with the wave teams' blocks, so
 // both progress from the start.  Members of a team sit on one XCD (blocks x
@@ -1366,16 +1379,32 @@ struct GroupArgs {
   unsigned long long* prof;
 };
 
+// A launch whose blocks meet at barriers (XGrid, the group teams'
+// team_sync): a regular launch of at most `per_cu` blocks per CU, checked
+// against the occupancy calculator so that every block of the grid fits on
+// the chip at once -- the barriers' precondition, which the cooperative
+// launch used to assert.  Blocks of other kernels running beside it (the
+// wave teams) never wait on it, so its blocks all become resident.  (The
+// cooperative launch is not used: under rocprofv3 a process that made one
+// faulted in exit-time runtime teardown)
+hipError_t launch_resident(const void* kernel, uint32_t blocks, uint32_t threads, void** args,
+                           uint32_t n_cu, hipStream_t s) {
+  int fit = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit, kernel, threads, 0);
+  if (e != hipSuccess) return e;
+  if (fit < 1 || (uint64_t)fit * n_cu < blocks) return hipErrorCooperativeLaunchTooLarge;
+  return hipLaunchKernel(kernel, dim3(blocks), dim3(threads), args, 0, s);
+}
+
 template <int G>
 hipError_t launch_group_g(GroupArgs& a, uint32_t n_cu, hipStream_t s) {
   void* args[] = {&a.g, &a.B, &a.big, &a.n_big, &a.cursor, &a.ctls, &a.mark, &a.dlist, &a.dnew,
                   &a.nhn, &a.lvl, &a.ord, &a.out, &a.prof};
-  return hipLaunchCooperativeKernel((const void*)repair_group_kernel<G>, dim3(n_cu),
-                                    dim3(kGroupWg), args, 0, s);
+  return launch_resident((const void*)repair_group_kernel<G>, n_cu, kGroupWg, args, n_cu, s);
 }
 
-// one cooperative launch, a workgroup per CU (every member of every team
-// resident at once: the team barrier's precondition)
+// one launch, a workgroup per CU (every member of every team resident at
+// once: the team barrier's precondition)
 hipError_t launch_group(uint32_t G, GroupArgs& a, uint32_t n_cu, hipStream_t s) {
   switch (G) {
     case 2: return launch_group_g<2>(a, n_cu, s);
@@ -1426,9 +1455,9 @@ struct spf_whatif_plan {
 
 namespace spfi {
 
-// Blocks of a cooperative launch: `per_cu` 512-thread blocks per CU, clamped
-// to what the occupancy calculator says stays co-resident (grid.sync needs
-// every block resident).  SPF_COOP_PER_CU overrides (A/B).
+// Blocks of a grid-barrier launch: `per_cu` 512-thread blocks per CU, clamped
+// to what the occupancy calculator says stays co-resident (XGrid needs every
+// block resident).  SPF_COOP_PER_CU overrides (A/B).
 uint32_t coop_blocks(spf_ctx* c, const void* kernel, uint32_t per_cu) {
   if (const char* e = std::getenv("SPF_COOP_PER_CU")) per_cu = std::max(1, atoi(e));
   int fit = 0;
@@ -1453,9 +1482,9 @@ spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
              hop ? 1u : 0u, dist, c->d_gq.p, c->d_gq2.p, c->d_gbm.p, c->d_gctr.p};
   a.bar = c->d_gbar.p;
   void* args[] = {&a};
-  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)gsssp_coop_kernel,
-                                        dim3(coop_blocks(c, (const void*)gsssp_coop_kernel, 1)),
-                                        dim3(kCoopThreads), args, 0, s));
+  HIP_TRY(c, launch_resident((const void*)gsssp_coop_kernel,
+                             coop_blocks(c, (const void*)gsssp_coop_kernel, 1), kCoopThreads, args,
+                             c->n_cu, s));
   return SPF_OK;
 }
 
@@ -1486,9 +1515,9 @@ spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh,
             p->b_parent.p};
   a.sp.bar = p->b_bar.p;
   void* args[] = {&a};
-  HIP_TRY(c, hipLaunchCooperativeKernel((const void*)spf_big_kernel,
-                                        dim3(coop_blocks(c, (const void*)spf_big_kernel, 1)),
-                                        dim3(kCoopThreads), args, 0, s));
+  HIP_TRY(c, launch_resident((const void*)spf_big_kernel,
+                             coop_blocks(c, (const void*)spf_big_kernel, 1), kCoopThreads, args,
+                             c->n_cu, s));
   return SPF_OK;
 }
 
@@ -1651,7 +1680,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   }
   WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
             p->d_nbr_bit.p, N, p->src, p->W};
-  // 1. unfailed SPF, next hops, hash: one cooperative launch
+  // 1. unfailed SPF, next hops, hash: one grid-resident launch
   {
     BaseArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr,
                         N, p->src, 0u, p->d_dist.p, p->d_q.p, p->d_q2.p, p->d_bm.p, p->d_ctr.p},
@@ -1661,9 +1690,9 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     a.sp.bar = p->d_bar.p;
     HIP_TRY(c, hipMemsetAsync(p->d_bar.p, 0, 4 * kGridBarWords, s));
     void* args[] = {&a};
-    HIP_TRY(c, hipLaunchCooperativeKernel((const void*)whatif_base_kernel,
-                                          dim3(coop_blocks(c, (const void*)whatif_base_kernel, 1)),
-                                          dim3(kCoopThreads), args, 0, s));
+    HIP_TRY(c, launch_resident((const void*)whatif_base_kernel,
+                               coop_blocks(c, (const void*)whatif_base_kernel, 1), kCoopThreads,
+                               args, c->n_cu, s));
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   // 2. failures
@@ -1746,6 +1775,7 @@ spf_status spf_whatif_stats(spf_whatif_plan* p, uint32_t* n_hot, uint32_t* n_big
   // null stream does not order after it): copy on that stream and wait
   HIP_TRY(c, hipMemcpyAsync(cnt, p->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, p->last));
   HIP_TRY(c, hipStreamSynchronize(p->last));
+  if (const spf_status st = spf_device_check(c); st != SPF_OK) return st;
   if (n_hot) *n_hot = cnt[0] + cnt[3];  // wave list + classified big
   if (n_big) *n_big = cnt[2] + cnt[3];  // wave overflow + classified big
   return SPF_OK;
@@ -1800,7 +1830,23 @@ spf_status spf_whatif_solve(spf_ctx* c, uint32_t src, const uint32_t* fail_links
     HIP_TRY(c, hipMemcpyAsync(base, d_base.p, sizeof(spf_whatif_digest), hipMemcpyDeviceToHost,
                               c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return SPF_OK;
+  return spf_device_check(c);
+}
+
+spf_status spf_device_check(spf_ctx* c) {
+  if (!c) return fail(c, SPF_E_INVALID, "spf_device_check: NULL context");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipDeviceSynchronize());
+  uint32_t flag = 0;
+  const uint32_t zero = 0;
+  HIP_TRY(c, hipMemcpyFromSymbol(&flag, HIP_SYMBOL(g_barrier_timeout), sizeof flag, 0,
+                                 hipMemcpyDeviceToHost));
+  if (!flag) return SPF_OK;
+  HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_barrier_timeout), &zero, sizeof zero, 0,
+                               hipMemcpyHostToDevice));
+  return fail(c, SPF_E_HIP,
+              "a grid / team barrier timed out on device %d (blocks not co-resident?): the "
+              "results of the launches since the last check are invalid", c->device);
 }
 
 }  // extern "C"

@@ -82,6 +82,13 @@ class SpfPlan(NativeHandle):
         self._eng._err(N.lib.spf_plan_copy_narrow_rows(self._h, C.c_void_p(d_out),
                                                        C.c_void_p(stream) if stream else None))
 
+    def digest(self, d_dist: int, d_nh: int, d_out: int, stream: int = 0) -> None:
+        """Enqueue per-source u64 digests of an execute's output into d_out
+        (n_src words, spf_plan_digest)."""
+        self._eng._err(N.lib.spf_plan_digest(self._h, C.c_void_p(d_dist), C.c_void_p(d_nh),
+                                             C.c_void_p(d_out),
+                                             C.c_void_p(stream) if stream else None))
+
     def execute_host(self) -> "SolveResult":
         """Execute into host arrays (spf_plan_execute_host)."""
         n = self._eng.n_nodes
@@ -91,7 +98,7 @@ class SpfPlan(NativeHandle):
         return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
 
     BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel",
-                   "spf_big_kernel")
+                   "spf_big_kernel", "mssp_kernel")
     ROW_MODES = ("u32", "u8", "sliced")
 
     def kernels(self) -> Tuple[str, bool]:
@@ -114,7 +121,7 @@ class SpfPlan(NativeHandle):
         row slicing, next-hop pass); None where a phase launches nothing."""
         bfs, narrow = self._kernel_codes()
         name = self.BFS_KERNELS[bfs]
-        if bfs >= 3 or not self.nh_words:  # exact / big kernels: next hops inside
+        if bfs in (3, 4) or not self.nh_words:  # exact / big kernels: next hops inside
             return name, None, None
         if narrow == 2:
             return name, "slice_rows_kernel", "ecmp_sliced_kernel"
@@ -358,6 +365,12 @@ class SpfEngine(NativeHandle):
 
     def solves(self) -> int:
         return int(N.lib.spf_solves(self._h))
+
+    def check(self) -> None:
+        """Wait for the device and raise if a grid-resident kernel's barrier
+        gave up waiting since the last check (spf_device_check): the outputs
+        of those launches are invalid."""
+        self._err(N.lib.spf_device_check(self._h))
 
     # ---- solves -----------------------------------------------------------------
     @property

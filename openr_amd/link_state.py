@@ -33,10 +33,9 @@ class Link:
     """Snapshot of ``openr::Link`` (LinkState.h:82-175) taken at query time."""
 
     __slots__ = ("_n1", "_n2", "_if1", "_if2", "_m1", "_m2", "_l1", "_l2",
-                 "_o1", "_o2", "_up", "hash", "_key", "_area", "_v4", "_v6", "_ident")
+                 "_o1", "_o2", "_up", "hash", "_key", "_area", "_v4", "_v6")
 
     def __init__(self, ls: "LinkState", d: N.LsLinkDesc, link_id: int = -1) -> None:
-        self._ident = (id(ls), link_id)  # pathAInPathB identity (one link of one LinkState)
         name = ls._name
         self._n1, self._n2 = name(d.node1), name(d.node2)
         self._if1, self._if2 = d.if1.decode(), d.if2.decode()
@@ -157,7 +156,11 @@ def _change(c: N.LsChange) -> LinkStateChange:
 
 class _LazySpfResult(Mapping):
     """SpfResult (unordered_map<string, NodeSpfResult>) backed by numpy
-    copies of the C-ABI view; a NodeSpfResult is built when first read."""
+    copies of the C-ABI view; a NodeSpfResult is built when first read.
+    Like the reference's ``SpfResult const&`` into the memo, it is valid until
+    the next topology change: link ids are resolved lazily through the
+    LinkState's link table, so reading an unmaterialised entry after the
+    topology changed raises instead of naming the wrong links."""
 
     def __init__(self, ls: "LinkState", v: "N.LsSpfView") -> None:
         import numpy as np
@@ -167,6 +170,7 @@ class _LazySpfResult(Mapping):
 
         n = int(v.n)
         self._ls = ls
+        self._gen = ls._gen
         self._node = arr(v.node, n, np.uint32)
         self._metric = arr(v.metric, n, np.uint64)
         self._nh_ptr = arr(v.nh_ptr, n + 1, np.uint32)
@@ -187,8 +191,10 @@ class _LazySpfResult(Mapping):
     def __getitem__(self, key: str) -> NodeSpfResult:
         r = self._made.get(key)
         if r is None:
-            i = self._idx()[key]
             ls = self._ls
+            if ls._gen != self._gen:
+                raise RuntimeError("SpfResult read after a topology change: call getSpfResult again")
+            i = self._idx()[key]
             a, b = int(self._nh_ptr[i]), int(self._nh_ptr[i + 1])
             nh = {ls._name(int(x)) for x in self._nh_node[a:b]}
             a, b = int(self._pl_ptr[i]), int(self._pl_ptr[i + 1])
@@ -420,14 +426,16 @@ class LinkState(N.NativeHandle):
     def pathAInPathB(a: Sequence, b: Sequence) -> bool:
         """``LinkState::pathAInPathB`` (LinkState.h:395-410) through the C-ABI
         (``ls_path_a_in_path_b``): a is a contiguous run of b.  Links compare
-        by identity, as the reference's shared_ptr<Link> elements do: the same
-        link of one LinkState, or the same standalone ``OwnedLink``."""
+        by value, as the reference's ``*a.at(i) == *b.at(j)`` does
+        (Link::operator==, LinkState.cpp:356-361: hash and orderedNames), so
+        equal links of different LinkStates, snapshots and ``OwnedLink``s
+        match.  Each distinct value gets one integer code for the C-ABI."""
         import numpy as np
 
         ids: Dict[object, int] = {}
 
         def enc(p):
-            return np.array([ids.setdefault(getattr(l, "_ident", None) or ("obj", id(l)), len(ids))
+            return np.array([ids.setdefault((int(l.hash), l.orderedNames), len(ids))
                              for l in p] or [0], np.uint32)
 
         ea, eb = enc(a), enc(b)
@@ -473,6 +481,12 @@ class OwnedLink(N.NativeHandle):
             int(adj1.isOverloaded), node2.encode(), adj2.ifName.encode(), adj2.metric,
             adj2.adjLabel, int(adj2.isOverloaded), C.byref(h)), "ls_link_create")
         self._adopt(h)
+        # orderedNames_ = minmax((n1, if1), (n2, if2)) (LinkState.cpp:127-137)
+        self._key = tuple(sorted([(node1, adj1.ifName), (node2, adj2.ifName)]))
+
+    @property
+    def orderedNames(self) -> Tuple[Tuple[str, str], Tuple[str, str]]:
+        return self._key  # type: ignore[return-value]
 
     def _side(self, fn, node: str, out):
         if fn(self._h, node.encode(), C.byref(out)) != N.SPF_OK:

@@ -1,0 +1,52 @@
+"""mssp_kernel (csrc/mssp.hip): the weighted all-sources distance kernel, S
+sources per workgroup with u16 labels in LDS and min-plus sweeps, against the
+oracle (LinkState::runSpf, LinkState.cpp:808-882), every source, with every
+LDS row width (SPF_MSSP_SD = 1, 2, 4, 8: 2-16 sources per workgroup), drained
+nodes, non-closed source sets and the u16-overflow redo path (rows whose
+labels may have clamped are recomputed by sssp_kernel).  Full size: every
+source of fabric_rtt and wan2k_spf is in test_gpu_fullsize.py."""
+
+import numpy as np
+import pytest
+
+from openr_amd import topology as T
+from test_gpu_engine import compare, load
+
+pytestmark = pytest.mark.gpu
+
+WEIGHTED = [
+    ("fabric_rtt600", lambda: T.fabric_rtt(num_sws=600)),
+    ("wan300", lambda: T.wan(300, 150, seed=3)),
+    ("dense_drained", lambda: T.random_graph(400, 3200, 5, max_metric=40, overload_frac=0.05)),
+    ("sparse_drained", lambda: T.random_graph(300, 450, 8, max_metric=9, parallel_frac=0.2,
+                                              overload_frac=0.1, link_overload_frac=0.05)),
+    ("disconnected", lambda: T.random_graph(200, 150, 4, max_metric=7, overload_frac=0.2)),
+]
+
+
+@pytest.mark.parametrize("sd", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("name,make", WEIGHTED, ids=[w[0] for w in WEIGHTED])
+def test_mssp_every_width_matches_oracle(name, make, sd, monkeypatch):
+    monkeypatch.setenv("SPF_MSSP_SD", sd)
+    names, eng, orc = load(make())
+    assert eng.plan([0]).kernels()[0] == "mssp_kernel"
+    compare(names, eng, orc, list(range(len(names))))
+
+
+def test_mssp_subsets_duplicates_and_single_sources():
+    names, eng, orc = load(T.random_graph(120, 500, 13, max_metric=30, overload_frac=0.1))
+    rng = np.random.default_rng(2)
+    for srcs in ([7], [3, 3, 9], [int(x) for x in rng.choice(len(names), 21, replace=False)]):
+        compare(names, eng, orc, srcs)
+
+
+@pytest.mark.parametrize("drained", [0.0, 0.1])
+def test_mssp_u16_overflow_rows_are_redone(drained):
+    """Metrics up to 30000 on a sparse graph: distances pass 65535, the u16
+    labels clamp and those rows are recomputed with u32 labels."""
+    topo = T.random_graph(250, 320, 17, max_metric=30000, overload_frac=drained)
+    names, eng, orc = load(topo)
+    assert eng.plan([0]).kernels()[0] == "mssp_kernel"
+    res = compare(names, eng, orc, list(range(len(names))))
+    d = res.dist[res.dist != 0xFFFFFFFF]
+    assert d.max() > 0xFFFF  # the redo path was needed

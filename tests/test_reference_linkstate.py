@@ -198,3 +198,28 @@ def test_path_a_in_path_b_over_link_state_links():
         # a fresh snapshot of the same link is the same link
         l1b = [l for l in ls.linksFromNode("1") if l == l1][0]
         assert f([l1b], [l1])
+
+
+def test_path_a_in_path_b_compares_by_value():
+    """Links compare by value (Link::operator==, LinkState.cpp:356-361):
+    two distinct OwnedLinks with the same endpoints are equal, and a link of
+    a LinkState equals an OwnedLink with the same (hash, orderedNames)."""
+    from helpers import get_link_state_dbs
+
+    a = OwnedLink(K_DEFAULT_AREA, "1", _bare("1/2"), "2", _bare("2/1"))
+    b = OwnedLink(K_DEFAULT_AREA, "2", _bare("2/1"), "1", _bare("1/2"))  # same link, sides swapped
+    c = OwnedLink(K_DEFAULT_AREA, "2", _bare("2/3"), "3", _bare("3/2"))
+    assert a is not b and a == b and a != c
+    f = LinkState.pathAInPathB
+    assert f([a], [c, b]) and f([b, c], [a, c]) and not f([a, c], [c, a])
+    with LinkState(device=-1) as ls1, LinkState(device=-1) as ls2:
+        dbs = get_link_state_dbs({1: [2], 2: [1, 3], 3: [2]})
+        ls1.updateAdjacencyDatabases(dbs)
+        ls2.updateAdjacencyDatabases(dbs)
+        x = {l.getOtherNodeName("2"): l for l in ls1.linksFromNode("2")}
+        y = {l.getOtherNodeName("2"): l for l in ls2.linksFromNode("2")}
+        assert f([x["1"]], [y["3"], y["1"]]) and not f([x["1"], x["3"]], [y["3"], y["1"]])
+        owned = OwnedLink(K_DEFAULT_AREA, "1", _bare(x["1"].getIfaceFromNode("1")),
+                          "2", _bare(x["1"].getIfaceFromNode("2")))
+        assert owned.hash == x["1"].hash
+        assert f([owned], [y["1"]])
