@@ -663,23 +663,38 @@ class FacadeLfa:
         self.kernel_bytes = {"facade": 1}
         self.survey_bytes = 0
         self.parallelism = "one LinkState per process (replicas)"
-        self.lat = []
+        self.lat, self.pub = [], []
+        self.prefetch = os.environ.get("BENCH_LFA_PREFETCH", "1") != "0"
 
     def step(self) -> None:
         # the C-ABI the C++ binding calls: the results are
-        # the LinkState's memo arrays (ls_spf_view); no Python objects built
+        # the LinkState's memo arrays (ls_spf_view); no Python objects built.
+        # me + every neighbour in one batched plan (ls_prefetch_spf_results,
+        # what SpfSolver's LFA does), then the per-node getSpfResult reads
         t0 = time.perf_counter()
         self.victim.isOverloaded = not self.victim.isOverloaded
         self.ls.updateAdjacencyDatabase(self.victim)
+        t1 = time.perf_counter()
+        if self.prefetch:
+            self.ls.prefetchSpfResults([self.me] + self.nbrs)
         for node in [self.me] + self.nbrs:
             v = self.ls._spf_view(node)
             assert v.n > 0
-        self.lat.append(time.perf_counter() - t0)
+        t2 = time.perf_counter()
+        self.lat.append(t2 - t0)
+        self.pub.append(t1 - t0)
 
     def enable_timing(self, k: int) -> None:
-        self.lat = []
+        self.lat, self.pub = [], []
+        self.ph0 = self.ls.debugPhaseNs()
 
     def kernel_ms(self):
+        ph = [(b - a) / 1e6 / max(1, len(self.lat)) for a, b in zip(self.ph0, self.ls.debugPhaseNs())]
+        self.phase_ms = {"publication (updateAdjacencyDatabase + flatten patch)":
+                         1e3 * float(np.mean(self.pub)) if self.pub else 0.0,
+                         "plan build": ph[0], "GPU execute + copy back": ph[1],
+                         "pathLinks (batched preds kernel + copy back)": ph[2],
+                         "host result assembly": ph[3]}
         return {"facade": 1e3 * float(np.mean(self.lat)) if self.lat else 0.0}
 
     def edges_per_unit(self) -> int:
@@ -916,6 +931,9 @@ def main() -> None:
         out["config"]["results"] = wl.results
     if isinstance(wl, AllSources):
         out["config"]["next_hop_rows"] = wl.narrow  # u32 | u8 | sliced (bit planes)
+    if isinstance(wl, FacadeLfa):
+        out["config"]["phase_ms_per_step"] = wl.phase_ms
+        out["config"]["batched_prefetch"] = wl.prefetch
     if isinstance(wl, WhatIfAllLinks):
         out["config"]["hot_failures_per_rank"] = wl.n_hot
         out["config"]["workgroup_team_failures_per_rank"] = wl.n_big

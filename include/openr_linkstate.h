@@ -131,6 +131,21 @@ spf_status ls_get_kth_paths(ls_state* ls, const char* src, const char* dst,
  * own (LinkState.cpp:778-779, 815).  Used by SpfSolver's KSP2_ED_ECMP route
  * build (Decision.cpp:895-1018). */
 spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src);
+/* Batch fill of the getSpfResult memo for `n` nodes (use_link_metric as in
+ * ls_get_spf_result) with one plan: one GPU execute, one copy back, one
+ * batched pathLinks launch -- what SpfSolver's LFA needs before it asks for
+ * getSpfResult(me) and getSpfResult(n) of every neighbour n
+ * (Decision.cpp:1158-1165).  Results equal the one-by-one queries; spf_runs
+ * counts each entry when it is first read (LinkState.cpp:815), so counts match
+ * the reference whether or not a caller prefetches.  Nodes already memoised,
+ * duplicates and off-graph nodes are skipped; graphs needing the exact kernel
+ * (zero / negative metrics, u64) are left to the per-node path. */
+spf_status ls_prefetch_spf_results(ls_state* ls, const char* const* nodes, uint32_t n,
+                                   int use_link_metric);
+/* Cumulative getSpfResult cost by phase in ns since creation: out[0] plan
+ * build, [1] GPU execute + copy back, [2] pathLinks, [3] host result
+ * assembly (diagnostics; no reference counterpart). */
+void ls_debug_phase_ns(const ls_state* ls, uint64_t* out);
 spf_status ls_get_metric_a_to_b(ls_state* ls, const char* a, const char* b,
                                 int use_link_metric, uint64_t* metric,
                                 int* has_value);

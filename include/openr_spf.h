@@ -193,6 +193,16 @@ spf_status spf_plan_copy_narrow_rows(spf_plan* plan, uint8_t* d_out, void* strea
  * NULL.  Device staging is owned by the plan. */
 spf_status spf_plan_execute_host(spf_plan* plan, uint32_t* dist, uint32_t* nh);
 /* (with SPF_FLAG_DIST64, `dist` is read as uint64_t[n_src][n_nodes]) */
+/* pathLinks of every source of the plan's last spf_plan_execute_host, one
+ * batched launch (the batch form of spf_preds): pred_ptr = [n_src][n_nodes+1]
+ * absolute offsets into pred_edge (source i's list for v is
+ * pred_edge[pred_ptr[i*(n+1)+v] .. pred_ptr[i*(n+1)+v+1]), directed CSR edge
+ * ids in the reference's order, LinkState.cpp:857-873); *n_preds = total.
+ * With pred_edge == NULL only the offsets are written; SPF_E_NOMEM when cap <
+ * *n_preds.  SPF_E_UNSUPPORTED for exact / big plans (spf_solve_exact's pop
+ * ranks order those). */
+spf_status spf_plan_preds(spf_plan* plan, uint32_t* pred_ptr, uint32_t* pred_edge, uint64_t cap,
+                          uint64_t* n_preds);
 
 /* Kernel timing with HIP events recorded on the execute stream: after
  * spf_plan_enable_timing(plan, K), each of the next K executes records events

@@ -218,6 +218,9 @@ PROTOTYPES = {
     "ls_link_info": (C.c_int, [_vp, C.c_uint32, C.POINTER(LsLinkDesc)]),
     "ls_get_spf_result": (C.c_int, [_vp, C.c_char_p, C.c_int, C.POINTER(LsSpfView)]),
     "ls_prefetch_kth_paths": (C.c_int, [_vp, C.c_char_p]),
+    "ls_prefetch_spf_results": (C.c_int, [_vp, _vp, C.c_uint32, C.c_int]),
+    "ls_debug_phase_ns": (None, [_vp, _vp]),
+    "spf_plan_preds": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp]),
     "ls_get_kth_paths": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_uint64,
                                    C.POINTER(LsPathsView)]),
     "ls_get_metric_a_to_b": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_int, _u64p,

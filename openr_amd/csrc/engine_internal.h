@@ -134,6 +134,8 @@ struct spf_plan {
   uint32_t dead = 0;  // nb_row value of a drained neighbour
   spfi::DevBuf<uint32_t> d_slot_src;  // next-hop blocks: source per (slot, XCD)
   spfi::DevBuf<uint32_t> h_dist, h_nh;  // spf_plan_execute_host staging
+  uint64_t h_epoch = ~0ull;              // graph epoch of the rows in h_dist
+  spfi::DevBuf<uint32_t> h_pcnt, h_pedge;  // spf_plan_preds scratch
   size_t slots = 0;
   size_t lds_bytes = 0;
   bool q16 = true;

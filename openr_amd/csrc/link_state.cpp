@@ -17,6 +17,7 @@
 //     invalidated on topology changes, as LinkState.h:271-301 does.
 // ============================================================================
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <cstdarg>
 #include <cstdio>
@@ -165,6 +166,9 @@ struct SpfMemo {
   // csr-indexed predecessor lists for path tracing
   std::vector<uint32_t> pred_ptr, pred_edge;
   std::vector<uint32_t> dist;  // csr-indexed (empty for an off-graph source)
+  // filled by ls_prefetch_spf_results: the reference's runSpf (and its
+  // decision.spf_runs count) happens on the first getSpfResult
+  uint8_t pending = 0;
 };
 struct PathMemo {
   std::vector<uint32_t> path_ptr{0}, link;
@@ -211,6 +215,9 @@ struct ls_state {
 
   // memo
   std::map<std::pair<uint32_t, int>, SpfMemo> spf_memo;
+  // getSpfResult cost by phase, ns (ls_debug_phase_ns): plan build, GPU
+  // execute + copy back, pathLinks, host result assembly
+  uint64_t phase_ns[4] = {0, 0, 0, 0};
   std::map<std::tuple<uint32_t, uint32_t, uint64_t>, PathMemo> ksp_memo;
 
   uint32_t intern(const std::string& s) {
@@ -593,11 +600,72 @@ spf_status exact_spf(ls_state* ls, uint32_t s, bool ulm, const std::vector<uint3
   return SPF_OK;
 }
 
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// A source's memo entry from its engine output: csr distance row, its
+// next-hop bitmaps (k of pitch/32 words, bitmap j = destinations routed via
+// neighbour nbr[j]) and its pathLinks (csr-indexed pred_ptr / pred_edge;
+// d64 = u64 distances of exact solves, else empty).
+void fill_memo(const ls_state* ls, const uint32_t* dist, const std::vector<uint64_t>& d64,
+               const uint32_t* nh, uint32_t k, uint32_t wpm, const std::vector<uint32_t>& nbr,
+               const uint32_t* pred_ptr, const uint32_t* pred_edge, SpfMemo& m) {
+  const uint32_t N = (uint32_t)ls->csr_name.size();
+  // next hops per destination from the per-neighbour bitmaps: set bits
+  // counted, then placed in neighbour order -- O(k * N/32 + bits), not O(k * N)
+  const uint32_t nw = (N + 31) / 32, nv = nw * 32;  // bitmap words / nodes they cover
+  std::vector<uint32_t> at(nv + 1, 0);
+  for (uint32_t j = 0; j < k; ++j)
+    for (uint32_t w = 0; w < nw; ++w)
+      for (uint32_t x = nh[(size_t)j * wpm + w]; x; x &= x - 1) ++at[w * 32 + __builtin_ctz(x) + 1];
+  for (uint32_t v = 0; v < nv; ++v) at[v + 1] += at[v];
+  std::vector<uint32_t> nh_of(at[nv]);
+  {
+    std::vector<uint32_t> fill(at.begin(), at.end() - 1);
+    for (uint32_t j = 0; j < k; ++j)
+      for (uint32_t w = 0; w < nw; ++w)
+        for (uint32_t x = nh[(size_t)j * wpm + w]; x; x &= x - 1) nh_of[fill[w * 32 + __builtin_ctz(x)]++] = j;
+  }
+  m.node.reserve(N);
+  m.metric.reserve(N);
+  m.nh_ptr.reserve(N + 1);
+  m.pl_ptr.reserve(N + 1);
+  m.nh_node.reserve(at[nv]);
+  for (uint32_t v = 0; v < N; ++v) {
+    if (dist[v] == SPF_UNREACHABLE) continue;
+    m.node.push_back(ls->csr_name[v]);
+    m.metric.push_back(d64.empty() ? (uint64_t)dist[v] : d64[v]);
+    for (uint32_t t = at[v]; t < at[v + 1]; ++t) m.nh_node.push_back(ls->csr_name[nbr[nh_of[t]]]);
+    m.nh_ptr.push_back((uint32_t)m.nh_node.size());
+    for (uint32_t p = pred_ptr[v]; p < pred_ptr[v + 1]; ++p) {
+      const uint32_t e = pred_edge[p];
+      m.pl_link.push_back(ls->link_id[e]);
+      m.pl_prev.push_back(ls->csr_name[ls->edge_tail[e]]);
+    }
+    m.pl_ptr.push_back((uint32_t)m.pl_link.size());
+  }
+}
+
+std::vector<uint32_t> src_neighbors(const ls_state* ls, uint32_t s) {
+  uint32_t k = 0;
+  spf_src_neighbors(ls->eng, s, nullptr, 0, &k);
+  std::vector<uint32_t> nbr(k);
+  spf_src_neighbors(ls->eng, s, nbr.data(), k, &k);
+  return nbr;
+}
+
 // getSpfResult (LinkState.cpp:793-803) -> memo entry
 spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out) {
   auto key = std::make_pair(node, (int)ulm);
   auto it = ls->spf_memo.find(key);
   if (it != ls->spf_memo.end()) {
+    if (it->second.pending) {  // prefetched: this is the reference's runSpf call
+      it->second.pending = 0;
+      ls->spf_runs++;
+    }
     *out = &it->second;
     return SPF_OK;
   }
@@ -616,63 +684,45 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
   } else {
     const uint32_t N = (uint32_t)ls->csr_name.size();
     const uint32_t flags = ulm ? 0u : SPF_FLAG_HOP_COUNT;
-    uint32_t k = 0;
-    spf_src_neighbors(ls->eng, s, nullptr, 0, &k);
-    std::vector<uint32_t> nbr(k);
-    spf_src_neighbors(ls->eng, s, nbr.data(), k, &k);
+    const std::vector<uint32_t> nbr = src_neighbors(ls, s);
+    const uint32_t k = (uint32_t)nbr.size();
     const uint32_t pitch = spf_row_pitch(ls->eng);
     const uint32_t wpm = pitch / 32;  // u32 words per destination bitmap
     const uint64_t words = (uint64_t)k * wpm;
     m.dist.resize(N);
     std::vector<uint32_t> nh(std::max<uint64_t>(words, 1));
     std::vector<uint64_t> d64;
+    uint64_t t0 = now_ns();
     if (needs_exact(ls, ulm)) {
       st = exact_spf(ls, s, ulm, {}, d64, &nh, m.pred_ptr, m.pred_edge);
       if (st != SPF_OK) return st;
       for (uint32_t v = 0; v < N; ++v)  // csr-indexed reachability for path tracing
         m.dist[v] = d64[v] == SPF_UNREACHABLE64 ? SPF_UNREACHABLE : 0u;
+      ls->phase_ns[1] += now_ns() - t0;
     } else {
-      st = spf_solve(ls->eng, &s, 1, flags, m.dist.data(), nh.data());
+      spf_plan* raw = nullptr;
+      st = spf_plan_create(ls->eng, &s, 1, flags, &raw);
       if (st != SPF_OK) return eng_fail(ls, st);
-      uint32_t npred = 0;
+      std::unique_ptr<spf_plan, void (*)(spf_plan*)> plan(raw, spf_plan_destroy);
+      uint64_t t1 = now_ns();
+      ls->phase_ns[0] += t1 - t0;
+      st = spf_plan_execute_host(plan.get(), m.dist.data(), nh.data());
+      if (st != SPF_OK) return eng_fail(ls, st);
+      t0 = now_ns();
+      ls->phase_ns[1] += t0 - t1;
       m.pred_ptr.resize(N + 1);
-      st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(), nullptr, 0,
-                     &npred);
+      uint64_t npred = 0;
+      st = spf_plan_preds(plan.get(), m.pred_ptr.data(), nullptr, 0, &npred);
       if (st != SPF_OK) return eng_fail(ls, st);
       m.pred_edge.resize(npred);
-      st = spf_preds(ls->eng, s, flags, nullptr, 0, m.dist.data(), m.pred_ptr.data(),
-                     m.pred_edge.data(), npred, &npred);
+      st = spf_plan_preds(plan.get(), m.pred_ptr.data(), m.pred_edge.data(), npred, &npred);
       if (st != SPF_OK) return eng_fail(ls, st);
+      ls->phase_ns[2] += now_ns() - t0;
     }
-    // next hops per destination from the per-neighbour bitmaps (bitmap j:
-    // destinations routed via neighbour j): set bits counted, then placed
-    // in neighbour order -- O(k * N/32 + bits), not O(k * N)
-    const uint32_t nw = (N + 31) / 32, nv = nw * 32;  // bitmap words / nodes they cover
-    std::vector<uint32_t> at(nv + 1, 0);
-    for (uint32_t j = 0; j < k; ++j)
-      for (uint32_t w = 0; w < nw; ++w)
-        for (uint32_t x = nh[(size_t)j * wpm + w]; x; x &= x - 1) ++at[w * 32 + __builtin_ctz(x) + 1];
-    for (uint32_t v = 0; v < nv; ++v) at[v + 1] += at[v];
-    std::vector<uint32_t> nh_of(at[nv]);
-    {
-      std::vector<uint32_t> fill(at.begin(), at.end() - 1);
-      for (uint32_t j = 0; j < k; ++j)
-        for (uint32_t w = 0; w < nw; ++w)
-          for (uint32_t x = nh[(size_t)j * wpm + w]; x; x &= x - 1) nh_of[fill[w * 32 + __builtin_ctz(x)]++] = j;
-    }
-    for (uint32_t v = 0; v < N; ++v) {
-      if (m.dist[v] == SPF_UNREACHABLE) continue;
-      m.node.push_back(ls->csr_name[v]);
-      m.metric.push_back(d64.empty() ? (uint64_t)m.dist[v] : d64[v]);
-      for (uint32_t t = at[v]; t < at[v + 1]; ++t) m.nh_node.push_back(ls->csr_name[nbr[nh_of[t]]]);
-      m.nh_ptr.push_back((uint32_t)m.nh_node.size());
-      for (uint32_t p = m.pred_ptr[v]; p < m.pred_ptr[v + 1]; ++p) {
-        const uint32_t e = m.pred_edge[p];
-        m.pl_link.push_back(ls->link_id[e]);
-        m.pl_prev.push_back(ls->csr_name[ls->edge_tail[e]]);
-      }
-      m.pl_ptr.push_back((uint32_t)m.pl_link.size());
-    }
+    t0 = now_ns();
+    fill_memo(ls, m.dist.data(), d64, nh.data(), k, wpm, nbr, m.pred_ptr.data(),
+              m.pred_edge.data(), m);
+    ls->phase_ns[3] += now_ns() - t0;
   }
   *out = &ls->spf_memo.emplace(key, std::move(m)).first->second;
   return SPF_OK;
@@ -1039,6 +1089,80 @@ spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src_c) {
     }
   }
   return SPF_OK;
+}
+
+// getSpfResult for several nodes in one batched plan (the SPF analogue of
+// ls_prefetch_kth_paths): SpfSolver's LFA asks for getSpfResult(me) and then
+// getSpfResult(n) for every neighbour n (Decision.cpp:1158-1165).  The memo
+// entries are marked pending: decision.spf_runs is counted when each is
+// first read, as if it had been computed then.
+spf_status ls_prefetch_spf_results(ls_state* ls, const char* const* nodes, uint32_t n, int ulm) {
+  if (!ls || (n && !nodes)) return SPF_E_INVALID;
+  spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  if (!ls->eng) return lfail(ls, SPF_E_NO_DEVICE, "LinkState created host-only (device < 0)");
+  if (needs_exact(ls, ulm != 0)) return SPF_OK;  // the exact kernel answers node by node
+  std::vector<uint32_t> srcs, ids;
+  std::unordered_set<uint32_t> seen;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!nodes[i]) return lfail(ls, SPF_E_INVALID, "ls_prefetch_spf_results: NULL node name");
+    const uint32_t id = ls->intern(nodes[i]);
+    const uint32_t s = id < ls->csr_of.size() ? ls->csr_of[id] : kNone;
+    if (s == kNone || ls->spf_memo.count(std::make_pair(id, ulm != 0 ? 1 : 0)) || !seen.insert(s).second)
+      continue;  // off-graph sources are trivial; memoised ones are done
+    srcs.push_back(s);
+    ids.push_back(id);
+  }
+  if (srcs.empty()) return SPF_OK;
+  const uint32_t N = (uint32_t)ls->csr_name.size();
+  const uint32_t flags = ulm ? 0u : SPF_FLAG_HOP_COUNT;
+  uint64_t t0 = now_ns();
+  spf_plan* raw = nullptr;
+  st = spf_plan_create(ls->eng, srcs.data(), (uint32_t)srcs.size(), flags, &raw);
+  if (st != SPF_OK) return eng_fail(ls, st);
+  std::unique_ptr<spf_plan, void (*)(spf_plan*)> plan(raw, spf_plan_destroy);
+  const uint32_t m = (uint32_t)srcs.size();
+  std::vector<uint64_t> nh_off(m);
+  std::vector<uint32_t> kk(m);
+  spf_plan_nh_layout(plan.get(), nh_off.data(), kk.data());
+  std::vector<uint32_t> dist((size_t)m * N);
+  std::vector<uint32_t> nh(std::max<uint64_t>(spf_plan_nh_words(plan.get()), 1));
+  uint64_t t1 = now_ns();
+  ls->phase_ns[0] += t1 - t0;
+  st = spf_plan_execute_host(plan.get(), dist.data(), nh.data());
+  if (st != SPF_OK) return eng_fail(ls, st);
+  t0 = now_ns();
+  ls->phase_ns[1] += t0 - t1;
+  std::vector<uint32_t> pred_ptr((size_t)m * (N + 1));
+  uint64_t npred = 0;
+  std::vector<uint32_t> pred_edge((size_t)m * ls->col.size() + 1);  // every in-edge at most once per source
+  st = spf_plan_preds(plan.get(), pred_ptr.data(), pred_edge.data(), pred_edge.size(), &npred);
+  if (st != SPF_OK) return eng_fail(ls, st);
+  t1 = now_ns();
+  ls->phase_ns[2] += t1 - t0;
+  const uint32_t wpm = spf_row_pitch(ls->eng) / 32;
+  const std::vector<uint64_t> none;
+  for (uint32_t i = 0; i < m; ++i) {
+    SpfMemo e;
+    e.dist.assign(dist.begin() + (size_t)i * N, dist.begin() + (size_t)(i + 1) * N);
+    const uint32_t* pp = pred_ptr.data() + (size_t)i * (N + 1);
+    // csr-indexed predecessor lists of this source, offsets rebased to 0
+    e.pred_ptr.resize(N + 1);
+    for (uint32_t v = 0; v <= N; ++v) e.pred_ptr[v] = pp[v] - pp[0];
+    e.pred_edge.assign(pred_edge.begin() + pp[0], pred_edge.begin() + pp[N]);
+    fill_memo(ls, e.dist.data(), none, nh.data() + nh_off[i], kk[i], wpm, src_neighbors(ls, srcs[i]),
+              e.pred_ptr.data(), e.pred_edge.data(), e);
+    e.pending = 1;
+    ls->spf_memo.emplace(std::make_pair(ids[i], ulm != 0 ? 1 : 0), std::move(e));
+  }
+  ls->phase_ns[3] += now_ns() - t1;
+  return SPF_OK;
+}
+
+// Cumulative getSpfResult cost by phase in ns: [0] plan build, [1] GPU
+// execute + copy back, [2] pathLinks, [3] host result assembly.
+void ls_debug_phase_ns(const ls_state* ls, uint64_t* out) {
+  for (int i = 0; i < 4; ++i) out[i] = ls ? ls->phase_ns[i] : 0;
 }
 
 // getMetricFromAToB (LinkState.cpp:740-751)

@@ -1373,19 +1373,24 @@ __global__ __launch_bounds__(256) void digest_kernel(const void* __restrict__ di
 // tail are contiguous in CSR order and tails appear in id (= name) order, so
 // this is the reference's (pop order, linksFromNode order).
 template <int PASS>
-__global__ void preds_kernel(const uint32_t* __restrict__ dist,  // [N]
+__global__ void preds_kernel(const uint32_t* __restrict__ dist0,  // [n_src][pitch]
+                             uint32_t pitch,
                              const uint32_t* __restrict__ row_ptr,
                              const uint32_t* __restrict__ col,
                              const uint32_t* __restrict__ wt,
                              const uint32_t* __restrict__ rev,
                              const uint8_t* __restrict__ ovl,
                              const uint32_t* __restrict__ link,
-                             const uint32_t* __restrict__ ign, uint32_t src,
+                             const uint32_t* __restrict__ ign,
+                             const uint32_t* __restrict__ srcs,  // [n_src] (blockIdx.y)
                              uint32_t N, uint32_t hop,
-                             uint32_t* __restrict__ cnt_or_ptr,
+                             uint32_t* __restrict__ cnt_or_ptr0,  // [n_src][N + 1]
                              uint32_t* __restrict__ pred_edge) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= N) return;
+  const uint32_t* dist = dist0 + (size_t)blockIdx.y * pitch;
+  uint32_t* cnt_or_ptr = cnt_or_ptr0 + (size_t)blockIdx.y * (N + 1);
+  const uint32_t src = srcs[blockIdx.y];
   const uint32_t dv = dist[v];
   uint32_t n = 0;
   uint32_t base = PASS ? cnt_or_ptr[v] : 0;
@@ -2582,6 +2587,7 @@ spf_status spf_plan_execute_host(spf_plan* p, uint32_t* dist_out, uint32_t* nh_o
   HIP_TRY(c, p->h_nh.alloc(std::max<uint64_t>(p->nh_total, 1)));
   const spf_status st = spf_plan_execute(p, p->h_dist.p, p->h_nh.p, nullptr);
   if (st != SPF_OK) return st;
+  p->h_epoch = c->epoch;
   if (dist_out) {
     HIP_TRY(c, hipMemcpy2DAsync(dist_out, (size_t)c->N * lab, p->h_dist.p, (size_t)c->pitch * lab,
                                 (size_t)c->N * lab, p->n_src, hipMemcpyDeviceToHost, c->stream));
@@ -2701,9 +2707,10 @@ spf_status spf_preds(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* i
   HIP_TRY(c, c->d_row.upload(dist, N, c->stream));
   HIP_TRY(c, c->d_pred_cnt.alloc(N + 1));
   const dim3 g((N + 255) / 256), b(256);
-  hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, c->d_row.p, c->d_row_ptr.p, c->d_col.p,
-                     c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign, src, N, hop ? 1u : 0u,
-                     c->d_pred_cnt.p, (uint32_t*)nullptr);
+  HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
+  hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, c->d_row.p, N, c->d_row_ptr.p,
+                     c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign,
+                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, (uint32_t*)nullptr);
   HIP_TRY(c, hipGetLastError());
   std::vector<uint32_t> cnt(N);
   HIP_TRY(c, hipMemcpyAsync(cnt.data(), c->d_pred_cnt.p, 4ull * N, hipMemcpyDeviceToHost, c->stream));
@@ -2715,13 +2722,63 @@ spf_status spf_preds(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* i
   if (cap < pred_ptr[N]) return fail(c, SPF_E_INVALID, "pred_edge capacity %u < %u", cap, pred_ptr[N]);
   HIP_TRY(c, hipMemcpyAsync(c->d_pred_cnt.p, pred_ptr, 4ull * N, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, c->d_pred_edge.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
-  hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, c->d_row.p, c->d_row_ptr.p, c->d_col.p,
-                     c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign, src, N, hop ? 1u : 0u,
-                     c->d_pred_cnt.p, c->d_pred_edge.p);
+  hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, c->d_row.p, N, c->d_row_ptr.p,
+                     c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign,
+                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, c->d_pred_edge.p);
   HIP_TRY(c, hipGetLastError());
   if (pred_ptr[N])
     HIP_TRY(c, hipMemcpyAsync(pred_edge, c->d_pred_edge.p, 4ull * pred_ptr[N], hipMemcpyDeviceToHost,
                               c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SPF_OK;
+}
+
+spf_status spf_plan_preds(spf_plan* p, uint32_t* pred_ptr, uint32_t* pred_edge, uint64_t cap,
+                          uint64_t* n_preds) {
+  if (!p || !pred_ptr || !n_preds) return fail(p ? p->ctx : nullptr, SPF_E_INVALID, "spf_plan_preds: NULL argument");
+  spf_ctx* c = p->ctx;
+  if (p->exact || p->big)
+    return fail(c, SPF_E_UNSUPPORTED, "spf_plan_preds: exact / big plans order pathLinks by pop rank "
+                                      "(spf_solve_exact)");
+  if (!p->h_dist.p || p->h_epoch != c->epoch)
+    return fail(c, SPF_E_STATE, "spf_plan_preds: no spf_plan_execute_host on the current graph");
+  const uint32_t N = c->N, n = p->n_src;
+  const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t slots = (size_t)n * (N + 1);
+  HIP_TRY(c, p->h_pcnt.alloc(slots));
+  const dim3 g((N + 255) / 256, n), b(256);
+  hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, p->h_dist.p, c->pitch, c->d_row_ptr.p,
+                     c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, nullptr,
+                     p->d_srcs.p, N, hop ? 1u : 0u, p->h_pcnt.p, (uint32_t*)nullptr);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpyAsync(pred_ptr, p->h_pcnt.p, 4ull * slots, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // counts -> absolute offsets: source i's list of v starts at pred_ptr[i*(N+1) + v],
+  // pred_ptr[i*(N+1) + N] = the end of source i's lists
+  uint64_t at = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t* pp = pred_ptr + (size_t)i * (N + 1);
+    for (uint32_t v = 0; v < N; ++v) {
+      const uint32_t cnt = pp[v];
+      if (at + cnt > 0xFFFFFFFFull) return fail(c, SPF_E_UNSUPPORTED, "spf_plan_preds: > 2^32 entries");
+      pp[v] = (uint32_t)at;
+      at += cnt;
+    }
+    pp[N] = (uint32_t)at;
+  }
+  *n_preds = at;
+  if (!pred_edge) return SPF_OK;
+  if (cap < at) return fail(c, SPF_E_NOMEM, "spf_plan_preds: capacity %llu < %llu",
+                            (unsigned long long)cap, (unsigned long long)at);
+  HIP_TRY(c, hipMemcpyAsync(p->h_pcnt.p, pred_ptr, 4ull * slots, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, p->h_pedge.alloc(std::max<uint64_t>(at, 1)));
+  hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, p->h_dist.p, c->pitch, c->d_row_ptr.p,
+                     c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, nullptr,
+                     p->d_srcs.p, N, hop ? 1u : 0u, p->h_pcnt.p, p->h_pedge.p);
+  HIP_TRY(c, hipGetLastError());
+  if (at)
+    HIP_TRY(c, hipMemcpyAsync(pred_edge, p->h_pedge.p, 4ull * at, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return SPF_OK;
 }

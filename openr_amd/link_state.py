@@ -407,6 +407,20 @@ class LinkState(N.NativeHandle):
         batched KSP2 launch (ls_prefetch_kth_paths)."""
         self._err(N.lib.ls_prefetch_kth_paths(self._h, src.encode()))
 
+    def prefetchSpfResults(self, nodes: Sequence[str], useLinkMetric: bool = True) -> None:
+        """Fill the getSpfResult memo for every node of `nodes` with one
+        batched plan (ls_prefetch_spf_results); spfRuns() counts each when it
+        is first read, as the reference's one-by-one calls would."""
+        arr = (C.c_char_p * max(1, len(nodes)))(*[n.encode() for n in nodes])
+        self._err(N.lib.ls_prefetch_spf_results(self._h, arr, len(nodes), int(bool(useLinkMetric))))
+
+    def debugPhaseNs(self) -> Tuple[int, int, int, int]:
+        """Cumulative getSpfResult cost (ns): plan build, GPU execute + copy
+        back, pathLinks, host assembly (ls_debug_phase_ns)."""
+        out = (C.c_uint64 * 4)()
+        N.lib.ls_debug_phase_ns(self._h, out)
+        return tuple(int(x) for x in out)  # type: ignore[return-value]
+
     def getMetricFromAToB(self, a: str, b: str, useLinkMetric: bool = True) -> Optional[int]:
         m = C.c_uint64()
         has = C.c_int()

@@ -272,6 +272,9 @@ class SpfSolver:
             for nh in mine[d].nextHops():
                 nextHopNodes[(nh, d)] = shortest - ls.getMetricFromAToB(me, nh)
         if self.computeLfaPaths and minCost:
+            # me + every neighbour in one batched plan (Decision.cpp:1158-1165)
+            ls.prefetchSpfResults([me] + [l.getOtherNodeName(me) for l in ls.linksFromNode(me)
+                                          if l.isUp()])
             for link in ls.linksFromNode(me):
                 if not link.isUp():
                     continue

@@ -57,3 +57,43 @@ def test_incremental_updates_invalidate_memo():
         c2 = ls.updateAdjacencyDatabases(one)
         assert c1 == [(c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged) for c in c2]
         assert spf_canonical(ls.getSpfResult(src)) == orc.spf(src)
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("ulm", [True, False], ids=["metric", "hops"])
+def test_prefetch_spf_results_equal_single_queries_and_count_runs(seed, ulm):
+    """ls_prefetch_spf_results (one batched plan for me + every LFA
+    neighbour, Decision.cpp:1158-1165): the same SpfResults as the one-by-one
+    queries (metrics, next hops, pathLinks order, against the oracle), and
+    spf_runs counts each node when it is first read, as the reference's
+    getSpfResult calls would (LinkState.cpp:815)."""
+    topo = T.random_graph(60, 150, 300 + seed, max_metric=6, parallel_frac=0.2,
+                          overload_frac=0.1, link_overload_frac=0.05)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    ls = LinkState()
+    ls.updateAdjacencyDatabases(topo.lsdb)
+    me = topo.nodes[seed]
+    nbrs = sorted({l.getOtherNodeName(me) for l in ls.linksFromNode(me)})
+    want = [me] + nbrs + ["not-a-node", me]
+    runs0 = ls.spfRuns()
+    ls.prefetchSpfResults(want, ulm)
+    assert ls.spfRuns() == runs0  # nothing read yet
+    for i, node in enumerate([me] + nbrs):
+        assert spf_canonical(ls.getSpfResult(node, ulm)) == orc.spf(node, ulm), node
+        assert ls.spfRuns() == runs0 + i + 1
+    ls.getSpfResult(me, ulm)
+    assert ls.spfRuns() == runs0 + 1 + len(nbrs)  # memoised
+
+
+def test_prefetch_spf_results_fabric_all_neighbours():
+    topo = T.fabric(1000, full=True)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    ls = LinkState()
+    ls.updateAdjacencyDatabases(topo.lsdb)
+    me = "3-0-0"
+    nbrs = sorted({l.getOtherNodeName(me) for l in ls.linksFromNode(me)})
+    ls.prefetchSpfResults([me] + nbrs)
+    for node in [me] + nbrs:
+        assert spf_canonical(ls.getSpfResult(node)) == orc.spf(node), node
