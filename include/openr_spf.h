@@ -264,7 +264,10 @@ spf_status spf_preds(spf_ctx* ctx, uint32_t src, uint32_t flags,
  *
  * Output: pairs[i * n_nodes + d] (below) and a pool of u32 words holding path
  * records [n_links, next record offset (SPF_KSP2_NONE = last), link ids...];
- * the k = 1 and k = 2 lists of a pair start at first[0] / first[1]. */
+ * the k = 1 and k = 2 lists of a pair start at first[0] / first[1].
+ * Graphs with a metric <= 0, u64 labels, more than 65535 nodes or a
+ * working set past the LDS run on the exact kernel (runSpf replayed in pop
+ * order per pair, HBM scratch): same output, far slower. */
 #define SPF_KSP2_NONE 0xFFFFFFFFu
 typedef struct spf_ksp2_pair {
   uint32_t first[2];   /* pool offset of the first k = 1 / k = 2 record */
@@ -308,8 +311,11 @@ spf_status spf_ksp2_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
  * The unfailed result's digest is {0, 0, hash}.  Global-memory kernels, no
  * LDS size limit: repair scratch is sized from fixed HBM budgets (8 GB of
  * wave teams, 8 GB of workgroup teams, fewer teams on bigger graphs) plus
- * O(N) per plan; an allocation failure returns SPF_E_NOMEM.  Weighted
- * metrics must be positive. */
+ * O(N) per plan; an allocation failure returns SPF_E_NOMEM.  Graphs with a
+ * metric <= 0 or u64 labels run on the exact kernel: the unfailed run
+ * replayed in pop order, and for every failure one of whose directions is a
+ * pathLink of it, runSpf(src, true, {l}) replayed by one wavefront (the
+ * others keep the unfailed digest). */
 typedef struct spf_whatif_digest {
   uint32_t n_dist_changed;
   uint32_t n_nh_changed;

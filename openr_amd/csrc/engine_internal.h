@@ -55,6 +55,26 @@ struct ExactScratch {
   uint32_t waves = 0, wmax = 0;
 };
 
+// What-if batches on the exact kernel (zero / negative metrics, u64): one
+// replayed runSpf per failure that touches a pathLink, digests vs the
+// unfailed run (exact.hip).
+struct ExactWhatIf {
+  ExactScratch xs;
+  DevBuf<uint32_t> fails, link_edge, base_pop, base_nh;
+  DevBuf<uint64_t> base_d;
+  DevBuf<spf_whatif_digest> base_dig;
+  uint32_t src = 0, n_fail = 0, W = 1;
+};
+
+// KSP2 on the exact kernel: the sources' runs (labels, pop ranks), then a
+// wave per pair tracing k = 1 and replaying k = 2 (exact.hip).
+struct ExactKsp2 {
+  ExactScratch xs_a, xs_b;
+  DevBuf<uint32_t> srcs, POP;
+  DevBuf<uint64_t> D;
+  uint32_t n_src = 0, lw = 0;
+};
+
 }  // namespace spfi
 
 struct spf_ctx {
@@ -189,7 +209,17 @@ spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
                         hipStream_t s);
 // The exact kernel (exact.hip) over n_src sources: dist rows (u32 or u64,
 // pitch entries), planar next-hop bitmaps at nh_off, optional pop ranks.
-spf_status exact_reserve(spf_ctx* c, ExactScratch* x, uint32_t n_src, uint32_t Wmax);
+spf_status exact_reserve(spf_ctx* c, ExactScratch* x, uint32_t n_src, uint32_t Wmax,
+                         uint64_t extra = 0);
+spf_status exact_whatif_prepare(spf_ctx* c, ExactWhatIf* x, uint32_t src,
+                                const std::vector<uint32_t>& fails,
+                                const std::vector<uint32_t>& link_edge);
+spf_status exact_whatif_launch(spf_ctx* c, ExactWhatIf* x, spf_whatif_digest* d_out,
+                               spf_whatif_digest* d_base, hipStream_t s, hipEvent_t mid);
+spf_status exact_ksp2_prepare(spf_ctx* c, ExactKsp2* x, const std::vector<uint32_t>& srcs);
+spf_status exact_ksp2_launch(spf_ctx* c, ExactKsp2* x, spf_ksp2_pair* d_pairs, uint32_t* d_pool,
+                             uint64_t pool_words, uint64_t* d_counters, hipStream_t s,
+                             hipEvent_t mid);
 spf_status launch_exact(spf_ctx* c, ExactScratch* x, const uint32_t* d_srcs, uint32_t n_src,
                         const uint64_t* d_nh_off, uint32_t Wmax, bool hop, bool dist64,
                         const uint32_t* ign, void* d_dist, uint32_t* d_nh, uint32_t* d_pop,

@@ -558,6 +558,9 @@ struct spf_ksp2_plan {
   uint32_t lds_waves = 0;  // > 0: the staged-graph kernel with this many waves
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
+  // outside the batched kernel's envelope (metrics <= 0, u64 labels, more
+  // than 65535 nodes or a working set past the LDS): the exact kernel
+  std::unique_ptr<spfi::ExactKsp2> exact;
   ~spf_ksp2_plan() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
@@ -571,17 +574,23 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   *out = nullptr;
   if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
   if (n_src == 0 || !srcs) return fail(c, SPF_E_INVALID, "empty source list");
-  if (c->nonpos || c->needs64)
-    return fail(c, SPF_E_UNSUPPORTED,
-                "graph has up links with metric <= 0 or needs u64 distances (the batched KSP2 "
-                "kernel runs u32 weighted SPF; LinkState.getKthPaths takes the exact path)");
-  if (c->N > 65535) return fail(c, SPF_E_UNSUPPORTED, "KSP2 kernel supports <= 65535 nodes");
   auto p = std::make_unique<spf_ksp2_plan>();
   p->ctx = c;
   p->n_src = n_src;
   p->srcs.assign(srcs, srcs + n_src);
   for (uint32_t i = 0; i < n_src; ++i)
     if (srcs[i] >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", srcs[i]);
+  auto go_exact = [&]() -> spf_status {
+    HIP_TRY(c, hipSetDevice(c->device));
+    p->exact = std::make_unique<spfi::ExactKsp2>();
+    const spf_status st = exact_ksp2_prepare(c, p->exact.get(), p->srcs);
+    if (st != SPF_OK) return st;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    p->epoch = c->epoch;
+    *out = p.release();
+    return SPF_OK;
+  };
+  if (c->nonpos || c->needs64 || c->N > 65535 || std::getenv("SPF_KSP2_EXACT")) return go_exact();
   p->lw = c->max_link / 32 + 1;
   {  // bucket width: the mean up-link metric (env SPF_KSP2_DELTA overrides;
      // 4294967295 = no order, the plain hop-synchronous sweep)
@@ -613,9 +622,7 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
       }
   }
   if (!p->lds_waves) p->lds = ksp2_lds_bytes(c->N, c->pitch, p->lw);
-  if (p->lds > kMaxLdsKsp)
-    return fail(c, SPF_E_UNSUPPORTED, "KSP2 working set of %zu B exceeds the LDS (%u nodes)",
-                p->lds, c->N);
+  if (p->lds > kMaxLdsKsp) return go_exact();  // the per-wave rows do not fit the LDS
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_kernel,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
@@ -667,6 +674,14 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
   HIP_TRY(c, hipMemsetAsync(d_counters, 0, 4 * sizeof(uint64_t), s));
+  if (p->exact) {
+    const spf_status st = exact_ksp2_launch(c, p->exact.get(), d_pairs, d_pool, pool_words,
+                                            d_counters, s, ev ? ev[1] : nullptr);
+    if (st != SPF_OK) return st;
+    if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+    c->solves += p->n_src;
+    return SPF_OK;
+  }
   spf_status st = launch_sssp(c, p->d_srcs.p, p->n_src, false, nullptr, p->d_D.p, s);
   if (st != SPF_OK) return st;
   st = launch_sssp(c, p->d_all.p, c->N, false, nullptr, p->d_H.p, s, p->d_wt_rev.p,

@@ -1059,9 +1059,8 @@ spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src_c) {
   const uint32_t src = ls->intern(src_c);
   const uint32_t s = src < ls->csr_of.size() ? ls->csr_of[src] : kNone;
   if (s == kNone) return SPF_OK;  // not in the graph: every query is empty anyway
-  // outside the batched kernel's envelope (zero / negative metrics, u64):
-  // nothing to prefetch, getKthPaths answers pair by pair on the exact kernel
-  if (needs_exact(ls, true)) return SPF_OK;
+  // (zero / negative metrics, u64 labels, big graphs: the engine's KSP2
+  // plan runs on the exact kernel, same output)
   const uint32_t N = (uint32_t)ls->csr_name.size();
   std::vector<spf_ksp2_pair> pairs(N);
   std::vector<uint32_t> pool;

@@ -1448,6 +1448,8 @@ struct spf_whatif_plan {
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
   hipStream_t last = nullptr;  // stream of the last execute (spf_whatif_stats waits on it)
+  // zero / negative metrics or u64 labels: every failure on the exact kernel
+  std::unique_ptr<spfi::ExactWhatIf> exact;
   ~spf_whatif_plan() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
@@ -1531,10 +1533,6 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   *out = nullptr;
   if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
   if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
-  if (c->nonpos || c->needs64)
-    return fail(c, SPF_E_UNSUPPORTED,
-                "graph has up links with metric <= 0 or needs u64 distances (what-if batches "
-                "run u32 weighted SPF with positive metrics)");
   auto p = std::make_unique<spf_whatif_plan>();
   p->ctx = c;
   p->src = src;
@@ -1554,6 +1552,20 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
       if (link_edge[l] != kInf) fails.push_back(l);
   }
   p->n_fail = (uint32_t)fails.size();
+  if (c->nonpos || c->needs64) {
+    // zero / negative metrics, u64 labels: the exact kernel replays
+    // runSpf(src, true, {l}) for every failure touching a pathLink
+    HIP_TRY(c, hipSetDevice(c->device));
+    p->exact = std::make_unique<spfi::ExactWhatIf>();
+    const spf_status st = exact_whatif_prepare(c, p->exact.get(), src, fails, link_edge);
+    if (st != SPF_OK) return st;
+    if (!fails.empty()) HIP_TRY(c, p->d_fails.upload(fails.data(), fails.size(), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    p->W = p->exact->W;
+    p->epoch = c->epoch;
+    *out = p.release();
+    return SPF_OK;
+  }
   // bit of each distinct up neighbour of src
   std::vector<uint32_t> nbr_bit(N, kInf);
   const uint32_t k = c->nb_ptr[src + 1] - c->nb_ptr[src];
@@ -1678,6 +1690,13 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     ++p->timing_n;
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
+  if (p->exact) {
+    const spf_status st = exact_whatif_launch(c, p->exact.get(), d_out, d_base, s, ev ? ev[1] : nullptr);
+    if (st != SPF_OK) return st;
+    if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+    c->solves += 1ull + p->n_fail;
+    return SPF_OK;
+  }
   WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
             p->d_nbr_bit.p, N, p->src, p->W};
   // 1. unfailed SPF, next hops, hash: one grid-resident launch
@@ -1771,6 +1790,12 @@ spf_status spf_whatif_stats(spf_whatif_plan* p, uint32_t* n_hot, uint32_t* n_big
   spf_ctx* c = p->ctx;
   uint32_t cnt[4] = {0, 0, 0, 0};
   if (!p->last) return fail(c, SPF_E_STATE, "spf_whatif_stats: no execute yet");
+  if (p->exact) {  // every failure is a re-run on the exact kernel (cold ones skipped inside)
+    HIP_TRY(c, hipStreamSynchronize(p->last));
+    if (n_hot) *n_hot = p->n_fail;
+    if (n_big) *n_big = 0;
+    return SPF_OK;
+  }
   // the counters are written on the execute stream (non-blocking, so the
   // null stream does not order after it): copy on that stream and wait
   HIP_TRY(c, hipMemcpyAsync(cnt, p->d_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, p->last));
