@@ -63,7 +63,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-pthread", *map(str, objs), "-o",
+           str(tmp)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

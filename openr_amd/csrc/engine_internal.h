@@ -114,6 +114,9 @@ struct spf_ctx {
   spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
   spfi::DevBuf<uint32_t> d_gq, d_gq2, d_gbm, d_gctr;  // global-memory SSSP scratch
   spfi::DevBuf<uint32_t> d_gbar;  // its grid-barrier counters (whatif.hip XGrid)
+  // per-node eccentricity estimates (planes BFS batch order), for ecc_epoch
+  std::vector<uint32_t> ecc;
+  uint64_t ecc_epoch = ~0ull;
   // mssp_kernel tables (mssp.hip), valid for graph epoch mp_epoch
   spfi::DevBuf<uint32_t> d_mp_ell, d_mp_smap;
   uint32_t mp_slots = 0, mp_ovf_at = 0;
@@ -137,6 +140,8 @@ struct spf_plan {
   bool expand = false;  // ... the u32 rows expanded from the u8 ones (BFS stores bytes only)
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
   bool mp = false;      // weighted: mssp_kernel (mssp.hip), S sources per workgroup
+  bool pl_order = false;  // planes BFS: rows batched deepest-first (d_pl_order)
+  spfi::DevBuf<uint32_t> d_pl_order;
   spfi::DevBuf<uint32_t> d_redo;  // mp: rows whose u16 labels may have overflowed
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
   spfi::ExactScratch xs;  // exact: the kernel's scratch, reserved by build_plan

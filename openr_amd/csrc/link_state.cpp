@@ -26,6 +26,7 @@
 #include <map>
 #include <memory>
 #include <optional>
+#include <thread>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -1141,19 +1142,36 @@ spf_status ls_prefetch_spf_results(ls_state* ls, const char* const* nodes, uint3
   ls->phase_ns[2] += t1 - t0;
   const uint32_t wpm = spf_row_pitch(ls->eng) / 32;
   const std::vector<uint64_t> none;
-  for (uint32_t i = 0; i < m; ++i) {
-    SpfMemo e;
+  std::vector<SpfMemo> memos(m);
+  std::vector<std::vector<uint32_t>> nbrs(m);
+  for (uint32_t i = 0; i < m; ++i) nbrs[i] = src_neighbors(ls, srcs[i]);
+  // the host assembly of each source's result is independent (read-only
+  // LinkState tables): one thread per source, at most 16
+  auto build = [&](uint32_t i) {
+    SpfMemo& e = memos[i];
     e.dist.assign(dist.begin() + (size_t)i * N, dist.begin() + (size_t)(i + 1) * N);
     const uint32_t* pp = pred_ptr.data() + (size_t)i * (N + 1);
     // csr-indexed predecessor lists of this source, offsets rebased to 0
     e.pred_ptr.resize(N + 1);
     for (uint32_t v = 0; v <= N; ++v) e.pred_ptr[v] = pp[v] - pp[0];
     e.pred_edge.assign(pred_edge.begin() + pp[0], pred_edge.begin() + pp[N]);
-    fill_memo(ls, e.dist.data(), none, nh.data() + nh_off[i], kk[i], wpm, src_neighbors(ls, srcs[i]),
+    fill_memo(ls, e.dist.data(), none, nh.data() + nh_off[i], kk[i], wpm, nbrs[i],
               e.pred_ptr.data(), e.pred_edge.data(), e);
     e.pending = 1;
-    ls->spf_memo.emplace(std::make_pair(ids[i], ulm != 0 ? 1 : 0), std::move(e));
+  };
+  const uint32_t nt = std::min<uint32_t>(m, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (nt <= 1) {
+    for (uint32_t i = 0; i < m; ++i) build(i);
+  } else {
+    std::vector<std::thread> pool;
+    for (uint32_t t = 0; t < nt; ++t)
+      pool.emplace_back([&, t]() {
+        for (uint32_t i = t; i < m; i += nt) build(i);
+      });
+    for (auto& th : pool) th.join();
   }
+  for (uint32_t i = 0; i < m; ++i)
+    ls->spf_memo.emplace(std::make_pair(ids[i], ulm != 0 ? 1 : 0), std::move(memos[i]));
   ls->phase_ns[3] += now_ns() - t1;
   return SPF_OK;
 }

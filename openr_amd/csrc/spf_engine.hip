@@ -658,7 +658,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
     const uint32_t* __restrict__ sell4_ptr, const uint2* __restrict__ sell4, uint32_t n4,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src, uint32_t n_rows,
     uint32_t bs, uint32_t N, uint32_t pitch, uint32_t npitch, uint32_t* __restrict__ D,
-    uint8_t* __restrict__ Dn) {
+    uint8_t* __restrict__ Dn, const uint32_t* __restrict__ order /* slot -> row, or null */) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint2* lcol = reinterpret_cast<uint2*>(smem);                   // [n4] (LCOL)
   // F0/F1: one word per owned node slot (OWN * 1024 >= N + 1); slots past
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
   }
   __syncthreads();
   if (tid < nb) {
-    const uint32_t src = rows_src[row0 + tid];
+    const uint32_t src = rows_src[order ? order[row0 + tid] : row0 + tid];
     F0[src] = 1u << tid;  // sources of a batch are distinct
     if (ovl[src]) o_node[atomicAdd(o_cnt, 1u)] = src | (tid << 24);
   }
@@ -773,8 +773,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
       // windows carry the marker value kPlWindow in their planes.
       const bool first = base == 0;
       for (uint32_t s = 0; s < nb; ++s) {
-        uint32_t* drow = D + (size_t)(row0 + s) * pitch;
-        uint8_t* nrow = Dn ? Dn + (size_t)(row0 + s) * npitch : nullptr;
+        const uint32_t row = order ? order[row0 + s] : row0 + s;
+        uint32_t* drow = D + (size_t)row * pitch;
+        uint8_t* nrow = Dn ? Dn + (size_t)row * npitch : nullptr;
 #pragma unroll
         for (int i = 0; i < OWN; ++i) {
           const uint32_t v = tid + i * kMsThreads;
@@ -1780,6 +1781,48 @@ namespace {
 // BFS (one coalesced store per row).  SPF_NARROW=0/1 overrides (experiments).
 bool use_planes(const spf_ctx* c);
 
+// Eccentricity estimate of every node (hop counts, drains ignored): the
+// largest BFS distance from a few landmarks -- the node farthest from node
+// 0, then repeatedly the node farthest from every landmark so far (on a grid:
+// the corners, which makes it exact).  Cached per graph epoch.
+const std::vector<uint32_t>& ecc_estimate(spf_ctx* c) {
+  if (c->ecc_epoch == c->epoch && c->ecc.size() == c->N) return c->ecc;
+  const uint32_t N = c->N;
+  std::vector<uint32_t> d(N), mind(N, kInf), q;
+  c->ecc.assign(N, 0);
+  auto bfs = [&](uint32_t r) {
+    std::fill(d.begin(), d.end(), kInf);
+    d[r] = 0;
+    q.assign(1, r);
+    for (size_t h = 0; h < q.size(); ++h) {
+      const uint32_t u = q[h];
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+        if (d[c->col[e]] == kInf) {
+          d[c->col[e]] = d[u] + 1;
+          q.push_back(c->col[e]);
+        }
+    }
+  };
+  uint32_t land = 0;
+  for (int j = 0; j < 9 && N; ++j) {
+    bfs(land);
+    uint32_t far = land, best = 0;
+    for (uint32_t v = 0; v < N; ++v) {
+      if (d[v] == kInf) continue;
+      if (j > 0) c->ecc[v] = std::max(c->ecc[v], d[v]);  // landmark 0 (node 0's far end) onwards
+      mind[v] = std::min(mind[v], d[v]);
+      if (j == 0 ? d[v] > best : mind[v] > best) {
+        best = j == 0 ? d[v] : mind[v];
+        far = v;
+      }
+    }
+    if (j == 0) std::fill(mind.begin(), mind.end(), kInf);  // node 0 is no landmark
+    land = far;
+  }
+  c->ecc_epoch = c->epoch;
+  return c->ecc;
+}
+
 bool use_narrow(const spf_ctx* c, const spf_plan* p) {
   if (const char* e = std::getenv("SPF_NARROW")) return e[0] != '0';
   // the register-plane BFS writes each row once, coalesced: the u8 copy
@@ -1911,6 +1954,22 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
   HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
+  // register-plane BFS: batches of similar depth, deepest first (more than
+  // one round of batches only; SPF_PL_ORDER=0 keeps the plan order, A/B)
+  p->pl_order = false;
+  if (p->ms && use_planes(c) && p->closure.size() > (size_t)kPlBatch * c->n_cu) {
+    const char* e = std::getenv("SPF_PL_ORDER");
+    if (!(e && e[0] == '0')) {
+      const std::vector<uint32_t>& ecc = ecc_estimate(c);
+      std::vector<uint32_t> order(p->closure.size());
+      std::iota(order.begin(), order.end(), 0u);
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return ecc[p->closure[a]] > ecc[p->closure[b]];
+      });
+      HIP_TRY(c, p->d_pl_order.upload(order.data(), order.size(), c->stream));
+      p->pl_order = true;
+    }
+  }
   // weighted: S sources per workgroup on mssp_kernel where it applies
   p->mp = !p->ms && !hop && mssp_words(c) > 0;
   if (p->mp) {
@@ -2278,23 +2337,30 @@ void msbfs_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t*
 
 size_t planes_lds_bytes(uint32_t own) { return 8ull * own * kMsThreads + 4ull * (kPlBatch + 4); }
 
+//   order (optional): rows sorted by estimated eccentricity, deepest first.
+//   A batch runs until its deepest source's search ends, so batches of
+//   similar depth waste no levels, and the deep ones start first while the
+//   shallow ones fill the CUs that free up (grid 100x100: eccentricities
+//   100..198; 313 full batches are 1.22 rounds of the chip); without it the
+//   batches are spread evenly over rounds.
 template <int OWN>
 void planes_launch(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D, uint8_t* Dn,
-                   hipStream_t s) {
+                   const uint32_t* order, hipStream_t s) {
   const uint32_t n4 = c->sell4_ptr.back();
   const size_t lds = planes_lds_bytes(OWN), lds_col = lds + 8ull * n4;
   const bool lcol = lds_col <= kMaxLds;
   const uint32_t rounds = (rows + kPlBatch * c->n_cu - 1) / (kPlBatch * c->n_cu);
-  const uint32_t bs = std::min<uint32_t>(kPlBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
+  const uint32_t bs = order ? kPlBatch
+                            : std::min<uint32_t>(kPlBatch, (rows + rounds * c->n_cu - 1) / (rounds * c->n_cu));
   const uint2* col4 = reinterpret_cast<const uint2*>(c->d_sell4.p);
   if (lcol)
     hipLaunchKernelGGL((msbfs_planes_kernel<OWN, true>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds_col, s, c->d_sell4_ptr.p, col4, n4, c->d_ovl.p, rows_src, rows, bs, c->N,
-                       c->pitch, c->npitch, D, Dn);
+                       c->pitch, c->npitch, D, Dn, order);
   else
     hipLaunchKernelGGL((msbfs_planes_kernel<OWN, false>), dim3((rows + bs - 1) / bs), dim3(kMsThreads),
                        lds, s, c->d_sell4_ptr.p, col4, n4, c->d_ovl.p, rows_src, rows, bs, c->N,
-                       c->pitch, c->npitch, D, Dn);
+                       c->pitch, c->npitch, D, Dn, order);
 }
 
 // Which BFS variant: the register-plane kernel needs N <= 10240; it wins
@@ -2308,7 +2374,8 @@ bool use_planes(const spf_ctx* c) {
 }
 
 spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
-                        uint8_t* Dn, uint32_t* maxd, hipStream_t s, uint32_t d_from = 0) {
+                        uint8_t* Dn, uint32_t* maxd, hipStream_t s, uint32_t d_from = 0,
+                        const uint32_t* order = nullptr) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
     HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
@@ -2318,11 +2385,11 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
   }
   const uint32_t own = ms_own(c->N);
   if (use_planes(c)) {
-    if (own <= 1) planes_launch<1>(c, rows_src, rows, D, Dn, s);
-    else if (own <= 2) planes_launch<2>(c, rows_src, rows, D, Dn, s);
-    else if (own <= 4) planes_launch<4>(c, rows_src, rows, D, Dn, s);
-    else if (own <= 8) planes_launch<8>(c, rows_src, rows, D, Dn, s);
-    else planes_launch<10>(c, rows_src, rows, D, Dn, s);
+    if (own <= 1) planes_launch<1>(c, rows_src, rows, D, Dn, order, s);
+    else if (own <= 2) planes_launch<2>(c, rows_src, rows, D, Dn, order, s);
+    else if (own <= 4) planes_launch<4>(c, rows_src, rows, D, Dn, order, s);
+    else if (own <= 8) planes_launch<8>(c, rows_src, rows, D, Dn, order, s);
+    else planes_launch<10>(c, rows_src, rows, D, Dn, order, s);
     HIP_TRY(c, hipGetLastError());
     return SPF_OK;
   }
@@ -2475,7 +2542,8 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   }
   spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                        sliced ? p->d_maxd.p : nullptr, s,
-                                       sliced && p->expand ? kSlSat : 0u)
+                                       sliced && p->expand ? kSlSat : 0u,
+                                       p->pl_order ? p->d_pl_order.p : nullptr)
                   : p->mp ? launch_mssp(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                         p->d_redo.p, s)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s, nullptr,

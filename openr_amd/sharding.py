@@ -2,10 +2,13 @@
 
 All-sources SPF + ECMP (the ``bench.py`` default):
 one LSDB replicated on every GPU, its sources split over ranks
-(:class:`AllSourcesLayout`), every rank solving its share and the per-source
-results -- distance rows and next-hop bitmaps in the engine's layout --
-gathered to rank 0 over RCCL (``Decision::getDecisionRouteDb`` for every
-node, Decision.cpp:1480-1500, answered from one place).  Sources go to ranks
+(:class:`AllSourcesLayout`), every rank solving its share.  By default the
+per-source results -- distance rows and next-hop bitmaps in the engine's
+layout -- stay resident in the owning rank's HBM (``Decision::
+getDecisionRouteDb`` for a node is answered by the rank that owns it,
+Decision.cpp:1480-1500); rank 0 gathers only per-source digests
+(:meth:`AllSourcesLayout.assemble_digests`).  The dense mode gathers every
+rank's rows and bitmaps to rank 0 over RCCL instead.  Sources go to ranks
 in contiguous blocks of node-id order balanced by next-hop work: a source's
 next hops need the distance rows of its neighbours, which the rank computes
 too (the plan's closure), and contiguous blocks keep that closure small
@@ -67,7 +70,13 @@ class AllSourcesLayout:
     ``world x cap`` words from which :meth:`dist_row` / :meth:`nh_block`
     read any source's result."""
 
-    def __init__(self, k: np.ndarray, pitch: int, world: int, dist_bytes: int = 4) -> None:
+    # a source's cost in next-hop bitmaps (N/8 bytes each): its k bitmaps plus
+    # its distance rows (u32 + u8 copy = 5N bytes = 40 bitmaps) -- the bytes
+    # every rank's kernels write dominate a pass
+    ROW_COST = 40
+
+    def __init__(self, k: np.ndarray, pitch: int, world: int, dist_bytes: int = 4,
+                 row_cost: float = ROW_COST) -> None:
         k = np.asarray(k, np.int64)
         n = len(k)
         assert dist_bytes in (1, 4) and (pitch * dist_bytes) % 4 == 0
@@ -76,8 +85,8 @@ class AllSourcesLayout:
         row_words = pitch * dist_bytes // 4  # a distance row in u32 words
         self.k = k
         wpm = pitch // 32
-        # contiguous blocks balanced by next-hop work (k + 1 bitmaps-ish per source)
-        cost = np.cumsum(k + 1, dtype=np.float64)
+        # contiguous blocks balanced by the bytes each source's results take
+        cost = np.cumsum(k + row_cost, dtype=np.float64)
         total = cost[-1] if n else 0.0
         bounds = [0] + [int(np.searchsorted(cost, total * r / world, side="right"))
                         for r in range(1, world)] + [n]
@@ -120,6 +129,19 @@ class AllSourcesLayout:
         r = int(self.rank_of[s])
         o = int(self.nh_off[s])
         return recv[r][o: o + int(self.k[s]) * (self.pitch // 32)]
+
+    def owner(self, s: int):
+        """(rank, row index in that rank's plan) holding source s's result."""
+        return int(self.rank_of[s]), int(self.index_of[s])
+
+    def assemble_digests(self, parts: Sequence) -> np.ndarray:
+        """Per-source u64 digests of the whole graph from every rank's list
+        (rank r's plan order = ``srcs[r]``), as rank 0 receives them."""
+        out = np.zeros(self.n, np.uint64)
+        for r, part in enumerate(parts):
+            a = np.asarray(part.cpu() if hasattr(part, "cpu") else part)
+            out[self.srcs[r]] = a.view(np.uint64)[: len(self.srcs[r])]
+        return out
 
     def dense(self, recv: Sequence):
         """Rank 0's gathered buffers as whole-graph arrays (host numpy):

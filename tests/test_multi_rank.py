@@ -1,10 +1,15 @@
-"""The multi-GPU sharding logic on CPU with the gloo backend (world size 2).
+"""The multi-GPU sharding logic on CPU with the gloo backend (world size 2-3).
 
 Each rank builds its own LSDB snapshot (weak scaling) or its interleaved
-source shard (strong scaling), solves it with the CPU oracle standing in for
-the GPU (no device here), and all_gathers 64-bit per-source digests; rank 0
-recomputes every rank's work alone and checks the gathered digests, the
-timing MAX reduction, and that shards partition the sources.
+source shard, solves it with the CPU oracle standing in for the GPU (no
+device here), and all_gathers 64-bit per-source digests; rank 0 recomputes
+every rank's work alone and checks the gathered digests, the timing MAX
+reduction, and that shards partition the sources.  The all-sources layout
+(contiguous blocks balanced by next-hop work, bench.py's default) is
+covered in both result modes: resident rows with per-source digests
+gathered to rank 0, and the dense gather of rows + bitmaps.  The engine's
+own per-rank plans and GPU digests are checked against the oracle's
+full-size digests in tests/test_gpu_sharded.py.
 """
 
 import os
@@ -323,9 +328,70 @@ def test_all_sources_layout_blocks_balance_next_hop_work():
 
     rng = np.random.default_rng(0)
     k = rng.integers(1, 200, 9976)
+    rc = AllSourcesLayout.ROW_COST
     for world in (1, 2, 4, 8):
         lay = AllSourcesLayout(k, 10048, world)
         assert np.array_equal(np.concatenate(lay.srcs), np.arange(9976))
-        work = [int((k[s] + 1).sum()) for s in lay.srcs]
-        assert max(work) - min(work) <= 2 * k.max() + 2
+        work = [int((k[s] + rc).sum()) for s in lay.srcs]
+        assert max(work) - min(work) <= 2 * (k.max() + rc)
         assert lay.cap == max(lay.words)
+
+
+def _resident_worker(rank, world, port, q):
+    """bench.py's resident mode: rank r solves its contiguous block, digests
+    its own rows (the oracle's digest_planar over the engine's output layout
+    standing in for spf_plan_digest), rank 0 gathers the digests
+    (gather_padded) and reassembles them with the layout."""
+    import sys
+    from pathlib import Path
+
+    here = Path(__file__).resolve().parent
+    sys.path.insert(0, str(here))
+    sys.path.insert(0, str(here.parent))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from oracle import NameTable, OracleLinkState, source_digests
+    from openr_amd import topology as T
+    from openr_amd.engine import graph_from_lsdb
+    from openr_amd.sharding import AllSourcesLayout, gather_padded
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        topo = T.fabric_rtt(num_sws=700)
+        names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+        n = len(names)
+        k = np.array([len({int(c) for c in col[rp[v]:rp[v + 1]]}) for v in range(n)], np.int64)
+        layout = AllSourcesLayout(k, 1024, world)
+        orc = OracleLinkState()
+        orc.update_packed(topo.lsdb)
+        table = NameTable(names)
+        mine = source_digests(orc, table, layout.srcs[rank], threads=1)
+        t = torch.from_numpy(mine.view(np.int64).copy())
+        got = gather_padded(t, len(mine))
+        if rank == 0:
+            whole = layout.assemble_digests(got)
+            alone = source_digests(orc, table, np.arange(n, dtype=np.uint32), threads=1)
+            q.put(("ok", bool(np.array_equal(whole, alone)),
+                   sorted(np.concatenate(layout.srcs).tolist()) == list(range(n))))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", repr(e), False))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_resident_mode_digest_gather_reassembles_single_rank_digests(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_resident_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    status, same, partition = q.get(timeout=600)
+    for p in ps:
+        p.join(timeout=120)
+    assert status == "ok", same
+    assert same and partition
