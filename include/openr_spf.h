@@ -146,7 +146,9 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
  * planes, rows written once), 3 exact_spf_kernel, 4 spf_big_kernel (graphs
  * beyond the LDS-resident kernels: one source at a time on the whole chip,
  * next hops inside), 5 mssp_kernel (weighted, positive metrics: 2-16 sources
- * per workgroup, u16 labels in LDS, min-plus sweeps); *narrow = 0 when the
+ * per workgroup, u16 labels in LDS, min-plus sweeps), 6 msbfs_team_kernel (unit
+ * metrics, plans with few sources: each batch's sweep split over a team of
+ * workgroups on one XCD); *narrow = 0 when the
  * next-hop pass (ecmp_kernel) reads the u32 rows, 1 when it reads u8 rows,
  * 2 when slice_rows_kernel turns the u8 rows into bit planes and
  * ecmp_sliced_kernel matches those.

@@ -141,6 +141,10 @@ struct spf_plan {
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
   bool mp = false;      // weighted: mssp_kernel (mssp.hip), S sources per workgroup
   bool pl_order = false;  // planes BFS: rows batched deepest-first (d_pl_order)
+  // msbfs_team_kernel (msbfs_team.hip): G workgroups per batch when the plan
+  // has too few batches to fill the chip (tm_G == 0: msbfs_kernel)
+  uint32_t tm_G = 0, tm_own = 0, tm_teams = 0, tm_bs = 0;
+  spfi::DevBuf<uint32_t> d_tm_map, d_tm_F, d_tm_bar;
   spfi::DevBuf<uint32_t> d_pl_order;
   spfi::DevBuf<uint32_t> d_redo;  // mp: rows whose u16 labels may have overflowed
   uint32_t wmax = 0;    // exact: max next-hop words per node over the plan's sources
@@ -204,6 +208,13 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 // graph epoch (plan build), launch_mssp() enqueues it (+ the overflow redo
 // pass over `redo` = [1 + rows] words of plan scratch).
 uint32_t mssp_words(const spf_ctx* c);
+// Team BFS (msbfs_team.hip): the team size for a unit plan of `rows` rows
+// (0: not used), its tables, its launch, its barrier-timeout flag.
+uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows);
+spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G);
+spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, uint32_t rows,
+                             uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s);
+spf_status msbfs_team_timed_out(spf_ctx* c, bool* out);
 spf_status mssp_prepare(spf_ctx* c);
 spf_status mssp_set_lds_limits(spf_ctx* c);
 spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,

@@ -1970,6 +1970,16 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       p->pl_order = true;
     }
   }
+  // few batches (a rank's share of a multi-GPU pass): teams of workgroups
+  // per batch (msbfs_team.hip) instead of one workgroup sweeping everything
+  p->tm_G = 0;
+  if (p->ms && !use_planes(c) && !p->expand) {
+    const uint32_t G = msbfs_team_size(c, (uint32_t)p->closure.size());
+    if (G) {
+      const spf_status st = msbfs_team_prepare(c, p, G);
+      if (st != SPF_OK) return st;
+    }
+  }
   // weighted: S sources per workgroup on mssp_kernel where it applies
   p->mp = !p->ms && !hop && mssp_words(c) > 0;
   if (p->mp) {
@@ -2144,7 +2154,8 @@ uint32_t spf_plan_closure_rows(const spf_plan* p) { return p ? (uint32_t)p->clos
 
 spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) {
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
-  *bfs = p->big ? 4u : p->exact ? 3u : p->mp ? 5u : !p->ms ? 0u : use_planes(p->ctx) ? 2u : 1u;
+  *bfs = p->big ? 4u : p->exact ? 3u : p->mp ? 5u : !p->ms ? 0u : p->tm_G ? 6u
+                                                          : use_planes(p->ctx) ? 2u : 1u;
   *narrow = p->sliced ? 2u : p->narrow ? 1u : 0u;
   return SPF_OK;
 }
@@ -2540,7 +2551,10 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     ++p->timing_n;
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
-  spf_status st = p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
+  spf_status st =
+      p->tm_G ? launch_msbfs_team(c, p, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
+                                  sliced ? p->d_maxd.p : nullptr, s)
+      : p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                        sliced ? p->d_maxd.p : nullptr, s,
                                        sliced && p->expand ? kSlSat : 0u,
                                        p->pl_order ? p->d_pl_order.p : nullptr)

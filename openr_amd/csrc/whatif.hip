@@ -1866,7 +1866,9 @@ spf_status spf_device_check(spf_ctx* c) {
   const uint32_t zero = 0;
   HIP_TRY(c, hipMemcpyFromSymbol(&flag, HIP_SYMBOL(g_barrier_timeout), sizeof flag, 0,
                                  hipMemcpyDeviceToHost));
-  if (!flag) return SPF_OK;
+  bool team = false;
+  if (const spf_status st = msbfs_team_timed_out(c, &team); st != SPF_OK) return st;
+  if (!flag && !team) return SPF_OK;
   HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_barrier_timeout), &zero, sizeof zero, 0,
                                hipMemcpyHostToDevice));
   return fail(c, SPF_E_HIP,

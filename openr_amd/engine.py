@@ -98,7 +98,7 @@ class SpfPlan(NativeHandle):
         return SolveResult(dist, nh, self.nh_off, self.words, self._eng.pitch)
 
     BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel",
-                   "spf_big_kernel", "mssp_kernel")
+                   "spf_big_kernel", "mssp_kernel", "msbfs_team_kernel")
     ROW_MODES = ("u32", "u8", "sliced")
 
     def kernels(self) -> Tuple[str, bool]:

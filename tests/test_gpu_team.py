@@ -1,0 +1,53 @@
+"""msbfs_team_kernel (csrc/msbfs_team.hip): the unit-metric multi-source BFS
+whose batches are swept by a team of G workgroups on one XCD -- what a rank
+of a multi-GPU all-sources pass runs (few sources per GPU) -- against the
+oracle, every source, for every team size (SPF_MSBFS_TEAM = G), with drained
+nodes, hop counts and every next-hop row form."""
+
+import numpy as np
+import pytest
+
+from openr_amd import topology as T
+from test_gpu_engine import ROW_MODES, compare, load
+
+pytestmark = pytest.mark.gpu
+
+GRAPHS = [
+    ("fabric_full1000", lambda: T.fabric(1000, full=True)),
+    ("fabric_ref1000", lambda: T.fabric(1000, full=False)),
+    ("rand_drained", lambda: T.random_graph(300, 3000, 11, max_metric=1, overload_frac=0.1)),
+    ("sparse_drained", lambda: T.random_graph(400, 600, 3, max_metric=1, overload_frac=0.05)),
+]
+
+
+@pytest.mark.parametrize("G", ["2", "4", "8", "16", "32"])
+@pytest.mark.parametrize("name,make", GRAPHS, ids=[g[0] for g in GRAPHS])
+def test_team_bfs_every_team_size(name, make, G, monkeypatch):
+    monkeypatch.setenv("SPF_MSBFS_TEAM", G)
+    monkeypatch.setenv("SPF_MSBFS", "masks")
+    names, eng, orc = load(make())
+    assert eng.plan([0], hop=True).kernels()[0] == "msbfs_team_kernel"
+    compare(names, eng, orc, list(range(len(names))), hop=True)
+    compare(names, eng, orc, list(range(len(names))))
+    compare(names, eng, orc, [5, 1, 5, 0])  # unsorted, duplicated sources
+
+
+@pytest.mark.parametrize("narrow", ["0", "1", "2"])
+def test_team_bfs_every_row_form(narrow, monkeypatch):
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "8")
+    monkeypatch.setenv("SPF_MSBFS", "masks")
+    monkeypatch.setenv("SPF_NARROW", narrow)
+    names, eng, orc = load(T.fabric(1000, full=True))
+    p = eng.plan([0], hop=True)
+    assert p.kernels()[0] == "msbfs_team_kernel" and p.row_mode() == ROW_MODES[narrow]
+    compare(names, eng, orc, list(range(len(names))))
+
+
+def test_team_bfs_chosen_for_a_rank_share_of_the_fabric():
+    """A world-8 rank's share of fabric_full (~1250 sources) takes the team
+    kernel by default; the full graph keeps msbfs_kernel."""
+    names, eng, orc = load(T.fabric(10000, full=True))
+    assert eng.plan(list(range(1250))).kernels()[0] == "msbfs_team_kernel"
+    assert eng.plan(list(range(len(names)))).kernels()[0] == "msbfs_kernel"
+    rng = np.random.default_rng(3)
+    compare(names, eng, orc, sorted(int(x) for x in rng.choice(len(names), 40, replace=False)))
