@@ -183,7 +183,8 @@ class AllSources:
         eng = eng_cls(dev.index)
         eng.load(rp, col, met, lid, ovl)
         self.eng, self.rank, self.world, self.dev = eng, rank, world, dev
-        k = np.array([len(eng.neighbors(s)) for s in range(self.n)], np.int64)
+        nbrs = [eng.neighbors(s) for s in range(self.n)]
+        k = np.array([len(x) for x in nbrs], np.int64)
         self.k = k
         pitch = eng.pitch
         split = scaling == "strong"
@@ -191,14 +192,14 @@ class AllSources:
         self.results = "gather" if gather else ("resident" if split else "per-rank snapshot")
         # the gathered distance rows: the plans' u8 rows when every rank's
         # are lossless (checked once below), a quarter of the u32 bytes
-        layout = AllSourcesLayout(k, pitch, world if split else 1)
+        layout = AllSourcesLayout(k, pitch, world if split else 1, nbrs=nbrs)
         srcs = layout.srcs[rank if split else 0]
         self.srcs = srcs
         self.plan = eng.plan(srcs)
         self.dist_bytes = 4
         if gather and self.plan.row_mode() != "u32" and self._narrow_lossless(dev, len(srcs), pitch):
             self.dist_bytes = 1
-            layout = AllSourcesLayout(k, pitch, world, dist_bytes=1)
+            layout = AllSourcesLayout(k, pitch, world, dist_bytes=1, nbrs=nbrs)
         self.layout = layout
         assert np.array_equal(self.plan.nh_off, self.layout.plan_nh_off(rank if split else 0))
         cap = self.layout.cap

@@ -117,6 +117,8 @@ struct spf_ctx {
   // per-node eccentricity estimates (planes BFS batch order), for ecc_epoch
   std::vector<uint32_t> ecc;
   uint64_t ecc_epoch = ~0ull;
+  uint32_t dbound = 0;  // hop-distance upper bound (depth_bound), for dbound_epoch
+  uint64_t dbound_epoch = ~0ull;
   // mssp_kernel tables (mssp.hip), valid for graph epoch mp_epoch
   spfi::DevBuf<uint32_t> d_mp_ell, d_mp_smap;
   uint32_t mp_slots = 0, mp_ovf_at = 0;
@@ -134,6 +136,7 @@ struct spf_plan {
   std::vector<uint32_t> words;
   uint64_t nh_total = 0;
   bool direct = false;  // closure == srcs: D is the caller's dist buffer
+  bool prefix = false;  // closure[i] == srcs[i] for i < n_src (distinct sources)
   bool ms = false;      // unit metrics: multi-source BFS
   bool narrow = false;  // ... writing the u8 narrow copy for the next-hop pass
   bool sliced = false;  // ... and the next-hop pass on its bit-sliced form
@@ -143,7 +146,8 @@ struct spf_plan {
   bool pl_order = false;  // planes BFS: rows batched deepest-first (d_pl_order)
   // msbfs_team_kernel (msbfs_team.hip): G workgroups per batch when the plan
   // has too few batches to fill the chip (tm_G == 0: msbfs_kernel)
-  uint32_t tm_G = 0, tm_own = 0, tm_teams = 0, tm_bs = 0;
+  uint32_t tm_G = 0, tm_own = 0, tm_teams = 0, tm_bs = 0, tm_nacc = 0;
+  uint32_t tm_rptr_at = 0, tm_runs_at = 0;  // d_tm_map = finalize slots | stream ranges | streams
   spfi::DevBuf<uint32_t> d_tm_map, d_tm_F, d_tm_bar;
   spfi::DevBuf<uint32_t> d_pl_order;
   spfi::DevBuf<uint32_t> d_redo;  // mp: rows whose u16 labels may have overflowed
@@ -213,7 +217,8 @@ uint32_t mssp_words(const spf_ctx* c);
 uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows);
 spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G);
 spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, uint32_t rows,
-                             uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s);
+                             uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s,
+                             uint32_t d_rows);  // u32 rows written: closure rows < d_rows
 spf_status msbfs_team_timed_out(spf_ctx* c, bool* out);
 spf_status mssp_prepare(spf_ctx* c);
 spf_status mssp_set_lds_limits(spf_ctx* c);

@@ -14,15 +14,32 @@
 //  fine with 10k sources (256 batches fill the chip), but a rank of an 8-GPU
 //  run holds ~1250 sources: 20-32 batches, 88 % of the CUs idle and the
 //  same time per pass as the whole graph.  Here the batch's sweep is split
-//  over G workgroups (G = 256 / next_pow2(batches)); the frontier masks F
-//  live in global memory (the team's 2 x 8(N + 1) bytes stay in its XCD's
-//  L2) and a level ends at a team barrier (agent-scope release -> arrival
-//  counter -> poll -> acquire, MI355X_MICROARCH.md's workgroup hand-off).
-//  Teams are persistent (one workgroup per CU, every member resident at
-//  once; spins are bounded) and walk their batches; level counters run on
-//  across batches, so flags and barriers need no reset between them.
+//  over G workgroups (the largest G whose 256 / G teams still hold every
+//  source in one round of <= 64-source batches).
+//
+//  Per level, each member:
+//    * sweeps its share of the column groups with the whole frontier in LDS
+//      (Fl, 8 B per node): a member's slices' column groups are cut into 16
+//      equal ranges (one per wave), so a fabric's 173-wide spine slices are
+//      spread over several waves instead of setting the level's latency;
+//      runs of one slice ORed into an LDS accumulator per slice;
+//    * finalizes its slices (new = acc & ~visited, stores of the level's
+//      distances), writes their next-frontier masks to the team's buffer in
+//      global memory (stays in the XCD's L2);
+//    * team barrier (agent-scope release -> arrival counter -> poll ->
+//      acquire, MI355X_MICROARCH.md's workgroup hand-off);
+//    * copies the whole next frontier from L2 into its LDS (80 KB at 10k
+//      nodes, uint4 loads).
+//  Level 0 needs no exchange (every member marks the sources itself).  A
+//  slice whose nodes have every source is skipped by later sweeps, and a
+//  level after which every slice is finished ends the batch without the
+//  empty level.  Teams are persistent (one workgroup per CU, every member
+//  resident at once; spins are bounded) and walk their batches; level
+//  counters run on across batches, so flags and barriers need no reset.
 // ============================================================================
 #include "engine_internal.h"
+
+#include <cstdio>
 
 using namespace spfi;
 
@@ -31,75 +48,79 @@ namespace {
 constexpr int kTmThreads = 1024;
 constexpr uint32_t kTmWaves = kTmThreads / 64;
 constexpr uint32_t kTmBatch = 64;
-constexpr uint32_t kTmNoSlice = 0x03FFFFFFu;  // an unused slot: its nodes lie past N
 constexpr uint32_t kTmSpin = 1u << 26;        // ~seconds: never a silent hang
-constexpr int kTmUnroll = 8;
+constexpr size_t kTmMaxLds = 160 * 1024;
+constexpr int kTmPlanes = 3;                              // distance bit planes per owned node
+constexpr uint32_t kTmWindow = (1u << kTmPlanes) - 1;     // levels per window; marker value
+constexpr int kTmCopy = 10;                               // uint4 per thread of the frontier copy
+constexpr uint32_t kTmRows = 16;                          // sources per flush tile (80 B each per node)
 constexpr uint32_t kTmBarPad = 32;            // words per team: counter line + 3 flag lines
 
 // set when a team barrier gave up (spf_device_check reads it via msbfs_team_timed_out)
 __device__ uint32_t g_team_timeout;
 
-__device__ __forceinline__ uint32_t tm_or32(uint32_t x) {
-  x |= __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true);
-  x |= __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);
-  x |= __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true);
-  x |= __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true);
-  x |= __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);
-  x |= __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);
-  return __builtin_amdgcn_readlane(x, 63);
-}
-__device__ __forceinline__ uint32_t tm_max32(uint32_t x) {
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));
-  return __builtin_amdgcn_readlane(x, 63);
-}
-__device__ __forceinline__ uint64_t tm_or64(uint64_t x) {
-  return ((uint64_t)tm_or32((uint32_t)(x >> 32)) << 32) | tm_or32((uint32_t)x);
-}
-
 struct TeamArgs {
-  const uint32_t* sell_ptr;
   const uint32_t* sell_col;
-  const uint32_t* tsmap;  // [G][kTmWaves][own] slice of (member, wave, slot)
+  const uint32_t* fin;    // [G][kTmWaves][OWN] finalized slices: slice | slot << 16 (0xFFFF: none)
+  const uint32_t* mptr;   // [G * kTmWaves + 1] column-stream ranges of (member, wave), multiples of 16
   const uint8_t* ovl;
   const uint32_t* rows_src;
-  uint32_t n_rows, bs, n_batches, N, pitch, npitch, G, teams_per_xcd;
+  uint32_t n_rows, bs, n_batches, N, pitch, npitch, G, teams_per_xcd, n_acc, fwords, front_bytes;
+  uint32_t col_bytes;  // sell_col incl. its trailing padding group
+  uint32_t d_rows;     // closure rows < d_rows have u32 rows in D (the request's prefix)
   uint32_t* D;
   uint8_t* Dn;
   uint32_t* maxd;
-  unsigned long long* F;  // [teams][2][N + 1]
-  uint32_t* bar;          // [teams][kTmBarPad * 4], zero at launch
+  unsigned long long* F;  // [teams][2][fwords]: the levels' frontiers, exchanged through L2
+  uint32_t* bar;          // [teams][kTmBarPad * 4]: arrivals, exits | 3 flag lines; zero at launch
+  unsigned long long* stamps;  // diagnostics (SPF_STAMPS=<block>), usually null
 };
 
-// team barrier: every member's stores drained and released at agent scope,
-// one arrival per member on the team's counter, poll, acquire
-__device__ __forceinline__ void team_barrier(uint32_t* cnt, uint32_t G) {
+// Team hand-off of a level (MI355X_MICROARCH.md, inter-workgroup visibility,
+// hand-off row 1 -- no L2 write-back, no L1 invalidate): every member's
+// frontier words are stored write-through (sc1) and drained by each storing
+// wave (vmcnt(0)), then ONE lane of the member adds its arrival to the
+// level's word -- 1 + 256 * (found new nodes) + 65536 * (has unfinished
+// slices) -- and polls it with sc1 loads until all G arrived; the frontier
+// is read back with sc1 loads only.  Returns the level's word.
+__device__ __forceinline__ uint32_t team_arrive(uint32_t* word, uint32_t G, uint32_t val,
+                                                uint32_t* bcast) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t target = (ticket / G + 1) * G;
-    uint32_t k = 0;
-    for (; k < kTmSpin && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++k)
+    __hip_atomic_fetch_add(word, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t w = 0, k = 0;
+    for (; k < kTmSpin; ++k) {
+      w = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((w & 0xFFu) >= G) break;
       __builtin_amdgcn_s_sleep(1);
+    }
     if (k == kTmSpin) __hip_atomic_store(&g_team_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *bcast = w;
   }
   __syncthreads();
+  return *bcast;
 }
 
+// 16-byte write-through (sc1) load: aux bit 4 = sc1 on gfx940+
+__device__ __forceinline__ uint4 ld_sc1_16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// LDS: Fl[fwords] (the whole frontier of the previous level), Acc[n_acc][64]
+// (column-stream ORs of the member's slices), the batch's sources.
+// Distances stay in registers as kTmPlanes bit planes per owned node (bit s
+// of plane b = bit b of d(s, v) - base) and are written once per window.
 template <int OWN>
-__global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a) {
-  __shared__ uint32_t src_l[kTmBatch];
-  __shared__ uint32_t o_node[kTmBatch];
-  __shared__ uint32_t o_cnt;
-  __shared__ uint32_t any_l;
+__global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
+                                                                const uint32_t* __restrict__ meta) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* Fl = reinterpret_cast<uint64_t*>(smem);  // [fwords]; the flush tiles reuse it
+  uint64_t* Acc = reinterpret_cast<uint64_t*>(smem + a.front_bytes);
+  uint32_t* src_l = reinterpret_cast<uint32_t*>(Acc + (size_t)a.n_acc * 64);
+  uint32_t* any_l = src_l + kTmBatch;  // [0]: this member's level flags, [1]: broadcast word
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // block -> (XCD, team on it, member): blocks are dealt to the XCDs round
@@ -109,168 +130,287 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a) {
   const uint32_t member = j % G;
   const uint32_t team = xcd * a.teams_per_xcd + j / G;
   const uint32_t n_teams = 8 * a.teams_per_xcd;
-  const uint32_t N = a.N;
-  unsigned long long* F0 = a.F + (size_t)team * 2 * (N + 1);
-  uint32_t* cnt = a.bar + (size_t)team * kTmBarPad * 4;
-  uint32_t* flag = cnt + kTmBarPad;  // flag[L % 3] at flag + (L % 3) * kTmBarPad
+  const uint32_t N = a.N, fw = a.fwords;
+  unsigned long long* F0 = a.F + (size_t)team * 2 * fw;
+  const __amdgpu_buffer_rsrc_t frs =
+      __builtin_amdgcn_make_buffer_rsrc(F0, 0, (int)(16u * fw), 0x00020000);
+  uint32_t* cnt = a.bar + (size_t)team * kTmBarPad * 4;  // [0]: unused, [1]: exits
+  uint32_t* lvw = cnt + kTmBarPad;  // level word of level L at lvw + (L % 3) * kTmBarPad
+  const uint32_t mw = __builtin_amdgcn_readfirstlane(member * kTmWaves + wv);
+  const uint32_t m_beg = __builtin_amdgcn_readfirstlane(a.mptr[mw]);
+  const uint32_t n_chunks = __builtin_amdgcn_readfirstlane((a.mptr[mw + 1] - m_beg) / 16u);
+  const uint32_t* ms = meta + m_beg;
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(a.sell_col), 0, (int)(a.col_bytes), 0x00020000);
+  // diagnostics: lane 0 of every wave of block stamps[1024] logs s_memtime at
+  // each phase boundary into stamps[wave * 64 + 1 ..], the count at [wave * 64]
+  const bool stamp = a.stamps && blockIdx.x == (uint32_t)a.stamps[64 * 16] && lane == 0;
+  uint32_t n_stamp = 0;
+#define TM_STAMP()                                                                      \
+  do {                                                                                  \
+    if (stamp && n_stamp < 63) a.stamps[wv * 64 + ++n_stamp] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+  TM_STAMP();
 
-  // owned slices (wave-uniform), their columns
-  uint32_t sv[OWN], sb[OWN], sw[OWN];
+  // finalized slices (wave-uniform): first node, Acc slot
+  uint32_t sv[OWN], slot[OWN];
   uint32_t drained = 0;
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
-    const uint32_t sl = a.tsmap[((size_t)member * kTmWaves + wv) * OWN + i];
-    sv[i] = __builtin_amdgcn_readfirstlane(sl * 64u);
-    const bool live = sv[i] < N;
-    const uint32_t slice = live ? sl : 0u;
-    const uint32_t b = live ? a.sell_ptr[slice] : 0u;
-    const uint32_t e = live ? a.sell_ptr[slice + 1] : 0u;
-    sb[i] = __builtin_amdgcn_readfirstlane(b);
-    sw[i] = __builtin_amdgcn_readfirstlane((e - b) / 64u);
+    const uint32_t f = a.fin[(size_t)mw * OWN + i];
+    const bool live = (f & 0xFFFFu) != 0xFFFFu;
+    sv[i] = __builtin_amdgcn_readfirstlane(live ? (f & 0xFFFFu) * 64u : 0x7FFFFFFFu);
+    slot[i] = __builtin_amdgcn_readfirstlane(f >> 16);
     const uint32_t v = sv[i] + lane;
     if (v < N && a.ovl[v]) drained |= 1u << i;
   }
-  if (tid == 0) any_l = 0;
-  if (member == 0 && tid == 0) {  // the padding target of both buffers stays 0
-    F0[N] = 0ull;
-    F0[2 * (N + 1) - 1] = 0ull;
+  if (member == 0 && tid == 0) {  // the padding entries of both buffers stay 0
+    for (uint32_t t = N; t < fw; ++t) {
+      __hip_atomic_store(&F0[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&F0[fw + t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
+  for (uint32_t t = tid; t < a.n_acc * 64; t += kTmThreads) Acc[t] = 0ull;
+
+  // ---- one pass over this wave's column stream: 16 column loads per chunk,
+  // the next chunk's loads in flight while this chunk's LDS reads run;
+  // consecutive groups of one slice ORed in registers, flushed into the
+  // slice's accumulator when the slot changes (the stream is slot-sorted) ----
+  auto sweep = [&]() {
+    uint64_t acc = 0;
+    uint32_t cur = 0xFFFFFFFFu;
+    uint32_t ca[16], cb[16];
+    auto load = [&](uint32_t k, uint32_t (&c)[16]) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {  // buffer loads: group offset in an SGPR, lane offset in a VGPR
+        const uint32_t g = __builtin_amdgcn_readfirstlane(ms[k * 16 + u]) & 0xFFFFFu;
+        c[u] = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 4u), (int)(g * 256u), 0);
+      }
+    };
+    auto proc = [&](uint32_t k, const uint32_t (&c)[16]) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const uint64_t f = Fl[c[u]];
+        const uint32_t sl = __builtin_amdgcn_readfirstlane(ms[k * 16 + u]) >> 20;
+        if (sl != cur) {
+          if (cur != 0xFFFFFFFFu && acc)
+            atomicOr(reinterpret_cast<unsigned long long*>(&Acc[cur * 64 + lane]), acc);
+          cur = sl;
+          acc = 0;
+        }
+        acc |= f;
+      }
+    };
+    if (n_chunks == 0) return;
+    load(0, ca);
+    for (uint32_t k = 0; k < n_chunks; k += 2) {
+      if (k + 1 < n_chunks) load(k + 1, cb);
+      proc(k, ca);
+      if (k + 1 < n_chunks) {
+        if (k + 2 < n_chunks) load(k + 2, ca);
+        proc(k + 1, cb);
+      }
+    }
+    if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&Acc[cur * 64 + lane]), acc);
+  };
 
   uint32_t L = 0;  // running level counter of the team (flags, buffers)
   for (uint32_t batch = team; batch < a.n_batches; batch += n_teams) {
     const uint32_t row0 = batch * a.bs;
     const uint32_t nb = min(a.bs, a.n_rows - row0);
     const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-    if (tid == 0) o_cnt = 0;
+    for (uint32_t t = tid; t < fw / 2; t += kTmThreads)
+      reinterpret_cast<uint4*>(Fl)[t] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
+    // level 0, computed by every member alone: the sources' own bits (a
+    // drained source expands as itself)
     if (tid < nb) {
       const uint32_t src = a.rows_src[row0 + tid];
       src_l[tid] = src;
-      if (a.ovl[src]) o_node[atomicAdd(&o_cnt, 1u)] = src | (tid << 24);
+      atomicOr(reinterpret_cast<unsigned long long*>(&Fl[src]), 1ull << tid);
     }
     __syncthreads();
-    const uint32_t n_osrc = o_cnt;
-    auto own_bits = [&](uint32_t v, uint64_t x) {
-      uint64_t own = 0;
-      for (uint32_t k = 0; k < n_osrc; ++k)
-        if ((o_node[k] & 0xFFFFFFu) == v) own = 1ull << (o_node[k] >> 24);
-      return x & own;
-    };
-    // level 0: a node's own source bits
-    uint64_t vis[OWN];
-    unsigned long long* Fc = F0 + (size_t)(L & 1u) * (N + 1);
+    uint64_t vis[OWN], P[OWN][kTmPlanes];
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = sv[i] + lane;
-      uint64_t m = 0;
-      if (v < N)
-        for (uint32_t s = 0; s < nb; ++s) m |= (src_l[s] == v ? 1ull : 0ull) << s;
-      vis[i] = m;
-      if (v < N) Fc[v] = m;  // a drained source expands as itself: m is its own bit
+      vis[i] = v < N ? Fl[v] : 0ull;
+#pragma unroll
+      for (int b = 0; b < kTmPlanes; ++b) P[i][b] = 0ull;
     }
-    // ---- record a level: D[s][v] = lvl for every new (s, v) of slice i ----
-    auto record = [&](int i, uint64_t x, uint32_t lvl) {
-      if (__ballot(x != 0ull) == 0ull) return;
-      const uint32_t nl = min(lvl, 254u);
-      const uint64_t wm = tm_or64(x);
-      const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)wm);
-      const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(wm >> 32));
-      const uint32_t v = sv[i] + lane;
-      const uint32_t nsrc = (uint32_t)__popcll(((uint64_t)mhi << 32) | mlo);
-      const uint32_t maxpop = tm_max32((uint32_t)__popcll(x));
-      if (maxpop * 4u < nsrc) {  // few per node: each lane walks its own sources
-        uint64_t m = x;
-        for (uint32_t it = 0; it < maxpop; ++it) {
-          if (m) {
-            const uint32_t s = __ffsll((unsigned long long)m) - 1;
-            if (a.D) a.D[(size_t)(row0 + s) * a.pitch + v] = lvl;
-            if (a.Dn) a.Dn[(size_t)(row0 + s) * a.npitch + v] = (uint8_t)nl;
-            m &= m - 1;
+    // ---- write the window's distances: every (s, v) of the owned slices
+    // in the first window (unreached = kInf), later only those found in it
+    // (entries of earlier windows carry the marker kTmWindow in the planes) ----
+    uint32_t base = 0;
+    // the first window's flush covers every (s, v) and goes through a
+    // per-wave LDS tile (the frontier's space, free by then): d of kTmRows
+    // sources x 64 nodes, read back as 16-byte row pieces -- one dwordx4
+    // store per 4 u32 rows and per 16 u8 rows instead of a dword and a byte
+    // store per row (the store issue rate bounded the per-row form)
+    auto flush = [&]() {
+      if (base == 0) {
+        uint32_t* T32 = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * kTmRows * 80;
+        uint8_t* T8 = reinterpret_cast<uint8_t*>(T32 + kTmRows * 64);
+#pragma unroll
+        for (int i = 0; i < OWN; ++i) {
+          if (sv[i] >= N) continue;  // wave-uniform
+          const uint32_t v = sv[i] + lane;
+          for (uint32_t g0 = 0; g0 < nb; g0 += kTmRows) {
+            const uint32_t gn = min(kTmRows, nb - g0);
+            for (uint32_t r = 0; r < gn; ++r) {
+              const uint32_t s = g0 + r;
+              uint32_t q = 0;
+#pragma unroll
+              for (int b = 0; b < kTmPlanes; ++b) q |= (uint32_t)((P[i][b] >> s) & 1ull) << b;
+              const bool seen = v < N && ((vis[i] >> s) & 1ull);
+              const uint32_t d = seen ? base + q : kInf;
+              T32[r * 64 + lane] = d;
+              T8[r * 64 + lane] = d == kInf ? 0xFFu : (uint8_t)min(d, 254u);
+            }
+            if (a.D)
+              for (uint32_t r4 = 0; r4 < gn; r4 += 4) {
+                const uint32_t r = r4 + (lane >> 4);
+                if (r < gn && row0 + g0 + r < a.d_rows) {
+                  const uint4 x = *reinterpret_cast<const uint4*>(T32 + r * 64 + (lane & 15) * 4);
+                  *reinterpret_cast<uint4*>(a.D + (size_t)(row0 + g0 + r) * a.pitch + sv[i] +
+                                            (lane & 15) * 4) = x;
+                }
+              }
+            if (a.Dn) {
+              const uint32_t r = lane >> 2;
+              if (r < gn) {
+                const uint4 x = *reinterpret_cast<const uint4*>(T8 + r * 64 + (lane & 3) * 16);
+                *reinterpret_cast<uint4*>(a.Dn + (size_t)(row0 + g0 + r) * a.npitch + sv[i] +
+                                          (lane & 3) * 16) = x;
+              }
+            }
           }
         }
         return;
       }
-      for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {  // a store per source
-        const uint32_t s = __ffsll((unsigned long long)m) - 1;
-        if ((x >> s) & 1ull) {
-          if (a.D) a.D[(size_t)(row0 + s) * a.pitch + v] = lvl;
-          if (a.Dn) a.Dn[(size_t)(row0 + s) * a.npitch + v] = (uint8_t)nl;
+      // later windows (searches deeper than the planes): the entries found
+      // in the window, one store per lane
+      for (uint32_t s = 0; s < nb; ++s) {
+        uint32_t* drow = a.D && row0 + s < a.d_rows ? a.D + (size_t)(row0 + s) * a.pitch : nullptr;
+        uint8_t* nrow = a.Dn ? a.Dn + (size_t)(row0 + s) * a.npitch : nullptr;
+#pragma unroll
+        for (int i = 0; i < OWN; ++i) {
+          if (sv[i] >= N) continue;  // wave-uniform
+          const uint32_t v = sv[i] + lane;
+          uint32_t q = 0;
+#pragma unroll
+          for (int b = 0; b < kTmPlanes; ++b) q |= (uint32_t)((P[i][b] >> s) & 1ull) << b;
+          const bool seen = v < N && ((vis[i] >> s) & 1ull);
+          if (seen && q != kTmWindow) {
+            if (drow) drow[v] = base + q;
+            if (nrow) nrow[v] = (uint8_t)min(base + q, 254u);
+          }
         }
       }
     };
-#pragma unroll
-    for (int i = 0; i < OWN; ++i) record(i, vis[i], 0);
-    team_barrier(cnt, G);
     uint32_t depth = 0;
     for (uint32_t lvl = 1;; ++lvl) {
       ++L;
-      const unsigned long long* Fp = F0 + (size_t)((L - 1) & 1u) * (N + 1);  // level lvl - 1
-      unsigned long long* Fn = F0 + (size_t)(L & 1u) * (N + 1);
-      if (member == 0 && tid == 0)
-        __hip_atomic_store(flag + ((L + 1) % 3) * kTmBarPad, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long* Fn = F0 + (size_t)(L & 1u) * fw;
+      if (member == 0 && tid == 0)  // the word of level L + 1 (its last readers passed level L - 1)
+        __hip_atomic_store(lvw + ((L + 1) % 3) * kTmBarPad, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sweep();
+      TM_STAMP();
+      __syncthreads();
+      TM_STAMP();
+      // ---- finalize the owned slices: new bits, planes, next frontier
+      // (write-through: the hand-off's payload) ----
+      const uint32_t rel = lvl - base;  // 1 .. kTmWindow - 1
       uint64_t any = 0;
+      bool open = false;
 #pragma unroll
       for (int i = 0; i < OWN; ++i) {
         const uint32_t v = sv[i] + lane;
-        const bool need = v < N && vis[i] != all;
-        uint64_t nx = 0;
-        if (__ballot(need)) {
-          const uint32_t* cp = a.sell_col + sb[i] + lane;
-          const uint32_t w = sw[i];
-          uint64_t acc = 0;
-          uint32_t jj = 0;
-          for (; jj + kTmUnroll <= w; jj += kTmUnroll) {
-            uint32_t c[kTmUnroll];
+        if (sv[i] >= N) continue;  // wave-uniform
+        const uint64_t x = Acc[slot[i] * 64 + lane];
+        Acc[slot[i] * 64 + lane] = 0ull;
+        const uint64_t nx = v < N ? x & ~vis[i] : 0ull;
+        vis[i] |= nx;
 #pragma unroll
-            for (int u = 0; u < kTmUnroll; ++u) c[u] = cp[(jj + u) * 64];
-#pragma unroll
-            for (int u = 0; u < kTmUnroll; ++u) acc |= Fp[c[u]];
-          }
-          for (; jj < w; ++jj) acc |= Fp[cp[jj * 64]];
-          if (need) {
-            nx = acc & ~vis[i];
-            vis[i] |= nx;
-          }
-        }
-        if (v < N) Fn[v] = ((drained >> i) & 1u) ? own_bits(v, nx) : nx;
+        for (int b = 0; b < kTmPlanes; ++b)
+          if ((rel >> b) & 1u) P[i][b] |= nx;
+        if (v < N)  // drained: expands as its own source only (level 0)
+          __hip_atomic_store(&Fn[v], ((drained >> i) & 1u) ? 0ull : nx, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         any |= nx;
-        record(i, nx, lvl);
+        if (__ballot(v < N && vis[i] != all)) open = true;
       }
-      if (__ballot(any != 0ull) && lane == 0) any_l = 1;
+      if (__ballot(any != 0ull) && lane == 0) atomicOr(any_l, 1u);
+      if (open && lane == 0) atomicOr(any_l, 2u);
       __syncthreads();
-      if (tid == 0) {
-        if (any_l)
-          __hip_atomic_store(flag + (L % 3) * kTmBarPad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        any_l = 0;  // set again only after the barrier below
-      }
-      team_barrier(cnt, G);
-      if (!__hip_atomic_load(flag + (L % 3) * kTmBarPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      const uint32_t mine = *any_l;
+      TM_STAMP();
+      const uint32_t w = team_arrive(lvw + (L % 3) * kTmBarPad, G,
+                                     1u + ((mine & 1u) << 8) + ((mine & 2u) << 15), any_l + 1);
+      if (tid == 0) *any_l = 0;  // read by every thread before team_arrive's second barrier
+      TM_STAMP();
+      if (((w >> 8) & 0xFFu) == 0) {
         depth = lvl - 1;  // level lvl found nothing: the batch's deepest level
         break;
       }
-    }
-    if (a.maxd && member == 0 && tid == 0) atomicMax(a.maxd, depth);
-    // ---- unreachable (s, v) pairs of the owned slices, row padding ----
-    uint64_t miss = 0;
+      if (((w >> 16) & 0xFFu) == 0) {
+        depth = lvl;  // every node has every source: level lvl is the last
+        break;
+      }
+      if (rel == kTmWindow - 1) {  // window full: write it, mark its entries, next window
+        flush();
 #pragma unroll
-    for (int i = 0; i < OWN; ++i)
-      if (sv[i] + lane < N) miss |= ~vis[i] & all;
-    for (uint64_t m = tm_or64(miss); m; m &= m - 1) {
-      const uint32_t s = __ffsll((unsigned long long)m) - 1;
+        for (int i = 0; i < OWN; ++i)
 #pragma unroll
-      for (int i = 0; i < OWN; ++i) {
-        const uint32_t v = sv[i] + lane;
-        if (v < N && !((vis[i] >> s) & 1ull)) {
-          if (a.D) a.D[(size_t)(row0 + s) * a.pitch + v] = kInf;
-          if (a.Dn) a.Dn[(size_t)(row0 + s) * a.npitch + v] = 0xFF;
+          for (int b = 0; b < kTmPlanes; ++b) P[i][b] |= vis[i];
+        base += kTmWindow;
+        __syncthreads();  // the flush's LDS tiles are read before the copy below
+      }
+      // ---- the next level's frontier into LDS: sc1 loads (L2-served, no
+      // invalidate needed), every load issued before the stores ----
+      {
+        const uint32_t fo = (L & 1u) * fw * 8u;
+        uint4* dst4 = reinterpret_cast<uint4*>(Fl);
+#pragma unroll
+        for (int h = 0; h < kTmCopy; h += kTmCopy / 2) {  // two halves: registers
+          uint4 t4[kTmCopy / 2];
+#pragma unroll
+          for (int q = 0; q < kTmCopy / 2; ++q) {
+            const uint32_t t = tid + (h + q) * kTmThreads;
+            if (t < fw / 2) t4[q] = ld_sc1_16(frs, fo + 16u * t);
+          }
+#pragma unroll
+          for (int q = 0; q < kTmCopy / 2; ++q) {
+            const uint32_t t = tid + (h + q) * kTmThreads;
+            if (t < fw / 2) dst4[t] = t4[q];
+          }
         }
       }
+      __syncthreads();
+      TM_STAMP();
     }
+    __syncthreads();  // every wave past its last frontier read: the tiles may overwrite Fl
+    flush();
+    if (a.maxd && member == 0 && tid == 0) atomicMax(a.maxd, depth);
     for (uint32_t s = 0; s < nb; ++s)  // padding past N, split over the members
       for (uint32_t v = N + member * kTmThreads + tid; v < a.npitch; v += G * kTmThreads) {
-        if (a.D && v < a.pitch) a.D[(size_t)(row0 + s) * a.pitch + v] = kInf;
+        if (a.D && v < a.pitch && row0 + s < a.d_rows) a.D[(size_t)(row0 + s) * a.pitch + v] = kInf;
         if (a.Dn) a.Dn[(size_t)(row0 + s) * a.npitch + v] = 0xFF;
       }
+    __syncthreads();  // Fl, src_l are reset by the next batch
+    TM_STAMP();
+  }
+  if (stamp) a.stamps[wv * 64] = n_stamp;
+#undef TM_STAMP
+  // the team's last member out zeroes its barrier words for the next launch
+  // (no memset per execute; every member passes here, timed-out ones too)
+  __syncthreads();
+  if (tid == 0) {
+    if (__hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+      for (uint32_t k = 0; k < 3; ++k)
+        __hip_atomic_store(lvw + k * kTmBarPad, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -280,79 +420,174 @@ namespace spfi {
 
 // Team shape for a plan of `rows` unit-metric rows: G workgroups per batch
 // (0: msbfs_kernel's one workgroup per batch is better -- enough batches to
-// fill the chip), batch size bs, and per-(member, wave) owned slots.
-// SPF_MSBFS_TEAM=0 disables, =G forces a team size (A/B, tests).
+// fill the chip).  SPF_MSBFS_TEAM=0 disables, =G forces a team size (A/B, tests).
+static size_t team_lds(uint32_t fwords, uint32_t n_acc) {
+  const size_t front = std::max<size_t>(8ull * fwords, (size_t)kTmWaves * kTmRows * 80 * 4);
+  return front + 8ull * 64 * n_acc + 4ull * (kTmBatch + 2) + 16;
+}
+
+static const void* team_kernel(uint32_t own) {
+  return own <= 1 ? (const void*)msbfs_team_kernel<1>
+         : own <= 2 ? (const void*)msbfs_team_kernel<2>
+                    : (const void*)msbfs_team_kernel<4>;
+}
+
+static uint32_t team_fwords(uint32_t N) { return (N + 2) & ~1u; }  // >= N + 1, even (uint4 copies)
+
 uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows) {
   if (c->n_cu % 8 || rows == 0) return 0;
   const char* e = std::getenv("SPF_MSBFS_TEAM");
   if (e && e[0] == '0') return 0;
   const uint32_t per_xcd = c->n_cu / 8;
-  uint32_t G = 0;
-  if (e) {
-    G = (uint32_t)atoi(e);
-  } else {
-    const uint32_t batches = (rows + kTmBatch - 1) / kTmBatch;
-    if (batches * 2 > c->n_cu) return 0;  // >= half the CUs busy anyway
-    // the largest G whose teams still cover every batch in one round
-    G = 1;
-    while (G * 2 <= per_xcd && (c->n_cu / (G * 2)) >= batches) G *= 2;
-  }
-  if (G < 2 || G > per_xcd || per_xcd % G) return 0;
   const uint32_t n_slices = (c->N + 63) / 64;
-  if ((n_slices + G * kTmWaves - 1) / (G * kTmWaves) > 16) return 0;  // OWN <= 16
-  return G;
+  if (n_slices >= 0xFFFFu) return 0;
+  auto valid = [&](uint32_t G) {
+    if (G < 2 || G > per_xcd || per_xcd % G) return false;
+    // LDS: the frontier plus the slice accumulators of the largest member;
+    // registers: OWN <= 4 finalized slices per wave
+    const uint32_t per_member = (n_slices + G - 1) / G + 2;
+    return team_lds(team_fwords(c->N), per_member) <= kTmMaxLds &&
+           (per_member + kTmWaves - 1) / kTmWaves <= 4;
+  };
+  if (e) {
+    const uint32_t G = (uint32_t)atoi(e);
+    return valid(G) ? G : 0;
+  }
+  // per-level cost model (us): msbfs_kernel sweeps every column group with
+  // one workgroup (16 waves, ~6.5 groups per us per wave: 8 dependent loads
+  // in flight); a team of G sweeps 1/G of them with 16-load chunks (~32
+  // groups per us per wave) plus a fixed per-level cost (barrier, frontier
+  // copy) and takes ceil(batches / teams) rounds.  SPF_TEAM_LEVEL_US tunes.
+  const double groups = (double)(c->sell_ptr.back() / 64);
+  const char* lu = std::getenv("SPF_TEAM_LEVEL_US");
+  const double level_us = lu ? atof(lu) : 4.0;
+  const double single = groups / kTmWaves / 6.5;
+  const uint64_t batches = (rows + kTmBatch - 1) / kTmBatch;
+  uint32_t best = 0;
+  double best_cost = single;
+  for (uint32_t G = 2; G <= per_xcd; G *= 2) {
+    if (!valid(G)) continue;
+    const uint64_t teams = c->n_cu / G;
+    const double rounds = (double)((batches + teams - 1) / teams);
+    const double cost = rounds * (groups / (kTmWaves * G) / 32.0 + level_us);
+    if (cost < best_cost) best_cost = cost, best = G;
+  }
+  return best;
 }
 
 spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
   const uint32_t n_slices = (c->N + 63) / 64;
-  const uint32_t need = (n_slices + G * kTmWaves - 1) / (G * kTmWaves);
-  const uint32_t own = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : need <= 8 ? 8 : 16;
-  // slices dealt widest first to the (member, wave) with the least width
-  const uint32_t units = G * kTmWaves;
-  std::vector<uint32_t> order(n_slices), load(units, 0), used(units, 0);
-  for (uint32_t i = 0; i < n_slices; ++i) order[i] = i;
   auto width = [&](uint32_t sl) { return (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / 64; };
+  // slices to members, widest first to the least-loaded member (column
+  // groups + a slice's finalize cost)
+  std::vector<uint32_t> order(n_slices);
+  for (uint32_t i = 0; i < n_slices; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return width(x) > width(y); });
-  std::vector<uint32_t> tsmap((size_t)units * own, kTmNoSlice);
+  std::vector<std::vector<uint32_t>> mem(G);
+  std::vector<uint64_t> load(G, 0);
   for (uint32_t sl : order) {
-    uint32_t best = units;
-    for (uint32_t u = 0; u < units; ++u)
-      if (used[u] < own && (best == units || load[u] < load[best])) best = u;
-    tsmap[(size_t)best * own + used[best]++] = sl;
-    load[best] += std::max(1u, width(sl));
+    uint32_t best = 0;
+    for (uint32_t m = 1; m < G; ++m)
+      if (load[m] < load[best] || (load[m] == load[best] && mem[m].size() < mem[best].size())) best = m;
+    mem[best].push_back(sl);
+    load[best] += width(sl) + 2;
   }
+  uint32_t n_acc = 1;
+  for (auto& v : mem) n_acc = std::max<uint32_t>(n_acc, (uint32_t)v.size());
+  const uint32_t need = (n_acc + kTmWaves - 1) / kTmWaves;
+  const uint32_t own = need <= 1 ? 1 : need <= 2 ? 2 : 4;
+  if (need > 4 || team_lds(team_fwords(c->N), n_acc) > kTmMaxLds)
+    return fail(c, SPF_E_INVALID, "msbfs_team: %u slices per member do not fit", n_acc);
+  // per member: finalize slots dealt round robin to the waves; the member's
+  // column groups (its slices' in order) cut into kTmWaves equal ranges, each
+  // range a stream of {group | slot << 20}, padded to whole chunks of 16 with
+  // the all-padding group after the last slice (sell_col's tail)
+  const uint32_t units = G * kTmWaves;
+  const uint32_t dummy = c->sell_ptr.back() / 64;
+  if (dummy >= (1u << 20) || n_acc >= (1u << 12))
+    return fail(c, SPF_E_INVALID, "msbfs_team: column groups exceed the stream encoding");
+  std::vector<uint32_t> fin((size_t)units * own, 0xFFFFu), mptr(units + 1, 0);
+  std::vector<uint32_t> meta;
+  for (uint32_t m = 0; m < G; ++m) {
+    const auto& S = mem[m];
+    for (uint32_t k = 0; k < S.size(); ++k)
+      fin[((size_t)m * kTmWaves + k % kTmWaves) * own + k / kTmWaves] = S[k] | (k << 16);
+    std::vector<uint32_t> all;  // the member's stream
+    for (uint32_t k = 0; k < S.size(); ++k)
+      for (uint32_t g = 0; g < width(S[k]); ++g) all.push_back((c->sell_ptr[S[k]] / 64 + g) | (k << 20));
+    const uint64_t T = all.size();
+    for (uint32_t w = 0; w < kTmWaves; ++w) {
+      mptr[m * kTmWaves + w] = (uint32_t)meta.size();
+      const uint64_t b = T * w / kTmWaves, e = T * (w + 1) / kTmWaves;
+      for (uint64_t t = b; t < e; ++t) meta.push_back(all[t]);
+      if (e > b)
+        while (meta.size() % 16) meta.push_back(dummy | (all[e - 1] & 0xFFF00000u));
+    }
+  }
+  mptr[units] = (uint32_t)meta.size();
   const uint32_t per_xcd = c->n_cu / 8;
   const uint32_t teams = 8 * (per_xcd / G);
   const uint32_t rows = (uint32_t)p->closure.size();
+  const uint32_t fw = team_fwords(c->N);
+  {  // every member must be resident at once (one workgroup per CU): else
+     // the plan keeps msbfs_kernel (tm_G stays 0; spf_plan_kernels tells)
+    const void* k = team_kernel(own);
+    HIP_TRY(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTmMaxLds));
+    int fit = 0;
+    HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit, k, kTmThreads, team_lds(fw, n_acc)));
+    if (fit < 1 || (uint64_t)fit * c->n_cu < (uint64_t)teams * G) {
+      if (std::getenv("SPF_TEAM_DEBUG"))
+        std::fprintf(stderr, "msbfs_team: <%u> not co-resident (%d per CU, %zu B LDS, G %u): msbfs_kernel\n",
+                     own, fit, team_lds(fw, n_acc), G);
+      p->tm_G = 0;
+      return SPF_OK;
+    }
+  }
   p->tm_G = G;
   p->tm_own = own;
   p->tm_teams = teams;
-  p->tm_bs = std::min<uint32_t>(kTmBatch, (rows + teams - 1) / teams);
-  HIP_TRY(c, p->d_tm_map.upload(tsmap.data(), tsmap.size(), c->stream));
-  HIP_TRY(c, p->d_tm_F.alloc((size_t)teams * 2 * (c->N + 1) * 2));  // u64 as 2 words
+  p->tm_nacc = n_acc;
+  {  // equal batches over whole rounds of the teams
+    const uint32_t rounds = (rows + kTmBatch * teams - 1) / (kTmBatch * teams);
+    p->tm_bs = std::min<uint32_t>(kTmBatch, (rows + teams * rounds - 1) / (teams * rounds));
+  }
+  std::vector<uint32_t> tab;  // fin | mptr | (16-entry aligned) meta, one upload
+  tab.insert(tab.end(), fin.begin(), fin.end());
+  p->tm_rptr_at = (uint32_t)tab.size();
+  tab.insert(tab.end(), mptr.begin(), mptr.end());
+  while (tab.size() % 16) tab.push_back(0);
+  p->tm_runs_at = (uint32_t)tab.size();
+  tab.insert(tab.end(), meta.begin(), meta.end());
+  HIP_TRY(c, p->d_tm_map.upload(tab.data(), tab.size(), c->stream));
+  HIP_TRY(c, p->d_tm_F.alloc((size_t)teams * 2 * fw * 2));  // u64 as 2 words
   HIP_TRY(c, p->d_tm_bar.alloc((size_t)teams * kTmBarPad * 4));
+  // zeroed once: every launch leaves them zero (the kernel's exit protocol)
+  HIP_TRY(c, hipMemsetAsync(p->d_tm_bar.p, 0, 4ull * teams * kTmBarPad * 4, c->stream));
   return SPF_OK;
 }
 
 spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, uint32_t rows,
-                             uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s) {
-  HIP_TRY(c, hipMemsetAsync(p->d_tm_bar.p, 0, 4ull * p->tm_teams * kTmBarPad * 4, s));
-  TeamArgs a{c->d_sell_ptr.p, c->d_sell_col.p, p->d_tm_map.p, c->d_ovl.p, rows_src, rows,
-             p->tm_bs, (rows + p->tm_bs - 1) / p->tm_bs, c->N, c->pitch, c->npitch, p->tm_G,
-             (c->n_cu / 8) / p->tm_G, D, Dn, maxd,
-             reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p};
+                             uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s,
+                             uint32_t d_rows) {
+  if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
+    HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
+    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
+    const unsigned long long wg = std::strtoull(std::getenv("SPF_STAMPS"), nullptr, 10);
+    HIP_TRY(c, hipMemcpyAsync(c->d_stamps.p + 64 * 16, &wg, 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  const uint32_t fw = team_fwords(c->N);
+  TeamArgs a{c->d_sell_col.p, p->d_tm_map.p, p->d_tm_map.p + p->tm_rptr_at, c->d_ovl.p, rows_src,
+             rows, p->tm_bs, (rows + p->tm_bs - 1) / p->tm_bs, c->N, c->pitch, c->npitch, p->tm_G,
+             (c->n_cu / 8) / p->tm_G, p->tm_nacc, fw,
+             (uint32_t)std::max<size_t>(8ull * fw, (size_t)kTmWaves * kTmRows * 80 * 4),
+             (uint32_t)(4ull * c->sell_col.size()), d_rows, D, Dn, maxd,
+             reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p};
+  const uint32_t* meta = p->d_tm_map.p + p->tm_runs_at;
   const uint32_t blocks = p->tm_teams * p->tm_G;  // = n_cu: one persistent workgroup per CU
-  void* args[] = {&a};
-  const void* k = p->tm_own <= 1   ? (const void*)msbfs_team_kernel<1>
-                  : p->tm_own <= 2 ? (const void*)msbfs_team_kernel<2>
-                  : p->tm_own <= 4 ? (const void*)msbfs_team_kernel<4>
-                  : p->tm_own <= 8 ? (const void*)msbfs_team_kernel<8>
-                                   : (const void*)msbfs_team_kernel<16>;
-  int fit = 0;
-  HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit, k, kTmThreads, 0));
-  if (fit < 1 || (uint64_t)fit * c->n_cu < blocks)
-    return fail(c, SPF_E_HIP, "msbfs_team_kernel: %u blocks not co-resident", blocks);
-  HIP_TRY(c, hipLaunchKernel(k, dim3(blocks), dim3(kTmThreads), args, 0, s));
+  const size_t lds = team_lds(fw, p->tm_nacc);
+  void* args[] = {&a, &meta};
+  HIP_TRY(c, hipLaunchKernel(team_kernel(p->tm_own), dim3(blocks), dim3(kTmThreads), args, lds, s));
   return SPF_OK;
 }
 

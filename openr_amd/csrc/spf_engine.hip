@@ -1598,7 +1598,8 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
         w = std::max(w, c->row_ptr[v + 1] - c->row_ptr[v]);
       c->sell_ptr[sl + 1] = c->sell_ptr[sl] + w * kSliceW;
     }
-    c->sell_col.assign(c->sell_ptr[n_slices], N);
+    // + one trailing all-padding group (msbfs_team.hip pads its column streams with it)
+    c->sell_col.assign(c->sell_ptr[n_slices] + kSliceW, N);
     for (uint32_t v = 0; v < N; ++v) {
       const uint32_t sl = v / kSliceW, ln = v % kSliceW;
       for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j)
@@ -1823,6 +1824,40 @@ const std::vector<uint32_t>& ecc_estimate(spf_ctx* c) {
   return c->ecc;
 }
 
+// An upper bound on every hop distance of the graph (any source, drained
+// nodes expanded only as the source, LinkState.cpp:831-838): paths run
+// s -> x -> ... -> y -> v with x .. y in H = the non-drained nodes, so
+// d(s, v) <= 2 + d_H(x, y) <= 2 + 2 ecc_H(r) for any r of x's component of
+// H.  One BFS in H per component.  Plans whose rows cannot saturate the u8
+// copy (bound < 254) never need u32 rows of non-source closure rows.
+uint32_t depth_bound(spf_ctx* c) {
+  if (c->dbound_epoch == c->epoch) return c->dbound;
+  const uint32_t N = c->N;
+  std::vector<uint32_t> d(N, kInf), q;
+  uint32_t worst = 0;
+  for (uint32_t r = 0; r < N; ++r) {
+    if (c->ovl[r] || d[r] != kInf) continue;
+    d[r] = 0;
+    q.assign(1, r);
+    uint32_t ecc = 0;
+    for (size_t h = 0; h < q.size(); ++h) {
+      const uint32_t u = q[h];
+      ecc = std::max(ecc, d[u]);
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+        const uint32_t x = c->col[e];
+        if (!c->ovl[x] && d[x] == kInf) {
+          d[x] = d[u] + 1;
+          q.push_back(x);
+        }
+      }
+    }
+    worst = std::max(worst, ecc);
+  }
+  c->dbound = 2 + 2 * worst;
+  c->dbound_epoch = c->epoch;
+  return c->dbound;
+}
+
 bool use_narrow(const spf_ctx* c, const spf_plan* p) {
   if (const char* e = std::getenv("SPF_NARROW")) return e[0] != '0';
   // the register-plane BFS writes each row once, coalesced: the u8 copy
@@ -1924,6 +1959,11 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
         p->closure.push_back(x);
       }
     };
+    // distinct sources first (rows 0 .. n_src - 1 are the request's rows:
+    // kernels that can write a row prefix straight into the caller's buffer
+    // do, msbfs_team_kernel), then the neighbours the next-hop pass reads
+    if (distinct)
+      for (uint32_t i = 0; i < n_src; ++i) add(srcs[i]);
     for (uint32_t i = 0; i < n_src; ++i) {
       const uint32_t s = srcs[i];
       add(s);
@@ -1931,6 +1971,9 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
         if (!c->ovl[c->nb_id[j]]) add(c->nb_id[j]);
     }
   }
+  // closure[i] == srcs[i] for i < n_src, and no row can saturate the u8
+  // copy (whose saturated entries the next-hop pass reads from u32 rows)
+  p->prefix = distinct && depth_bound(c) < kSlSat;
   std::vector<uint32_t> req_rows(n_src);
   for (uint32_t i = 0; i < n_src; ++i) req_rows[i] = row_of[srcs[i]];
   // next-hop layout
@@ -2062,7 +2105,13 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       // offset lists are read 16-byte aligned)
       const uint32_t chunks = (wpm + 63) / 64;
       const char* ue = std::getenv("SPF_SLICED_UNIT");  // A/B knob
-      const uint32_t unit = ue ? (uint32_t)atoi(ue) : kSlUnit;
+      // small plans (a rank's share of a multi-GPU pass) get smaller units so
+      // the waves still cover the chip: about 16 units per CU, 16..kSlUnit
+      uint64_t matches = 0;
+      for (uint32_t i = 0; i < n_src; ++i) matches += (uint64_t)p->words[i] * chunks;
+      const uint32_t fill = (uint32_t)std::min<uint64_t>(
+          kSlUnit, std::max<uint64_t>(16, matches / (16ull * c->n_cu) / 8 * 8));
+      const uint32_t unit = ue ? (uint32_t)atoi(ue) : fill;
       std::vector<uint32_t> units, unit_off(9, 0);
       p->max_xcd_units = 0;
       for (int g = 0; g < 8; ++g) {
@@ -2541,7 +2590,11 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     c->solves += p->n_src;
     return SPF_OK;
   }
-  uint32_t* D = p->direct ? d_dist : p->d_D.p;
+  // team plans whose closure starts with the request's rows write those
+  // rows' u32 distances straight into d_dist (and no others): no scratch
+  // rows, no gather
+  const bool team_direct = p->tm_G && p->prefix && !p->direct;
+  uint32_t* D = (p->direct || team_direct) ? d_dist : p->d_D.p;
   const uint32_t rows = (uint32_t)p->closure.size();
   const bool sliced = p->sliced && p->nh_total;
   if (sliced) HIP_TRY(c, hipMemsetAsync(p->d_maxd.p, 0, 4, s));  // msbfs_kernel's atomicMax target
@@ -2553,7 +2606,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   }
   spf_status st =
       p->tm_G ? launch_msbfs_team(c, p, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
-                                  sliced ? p->d_maxd.p : nullptr, s)
+                                  sliced ? p->d_maxd.p : nullptr, s, team_direct ? p->n_src : rows)
       : p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                        sliced ? p->d_maxd.p : nullptr, s,
                                        sliced && p->expand ? kSlSat : 0u,
@@ -2576,7 +2629,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     if (st != SPF_OK) return st;
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
-  if (!p->direct) {
+  if (!p->direct && !team_direct) {
     hipLaunchKernelGGL(gather_rows_kernel, dim3(std::min<uint32_t>((pitch / 4 + 255) / 256, 64), p->n_src),
                        dim3(256), 0, s, D, pitch, p->d_req_rows.p, d_dist);
     HIP_TRY(c, hipGetLastError());

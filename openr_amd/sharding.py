@@ -9,10 +9,11 @@ getDecisionRouteDb`` for a node is answered by the rank that owns it,
 Decision.cpp:1480-1500); rank 0 gathers only per-source digests
 (:meth:`AllSourcesLayout.assemble_digests`).  The dense mode gathers every
 rank's rows and bitmaps to rank 0 over RCCL instead.  Sources go to ranks
-in contiguous blocks of node-id order balanced by next-hop work: a source's
-next hops need the distance rows of its neighbours, which the rank computes
-too (the plan's closure), and contiguous blocks keep that closure small
-where interleaving would pull in nearly every row of a fabric.
+balanced by next-hop work, grouped so that each rank's closure stays small:
+a source's next hops need the distance rows of its neighbours, which the
+rank computes too (the plan's closure).  Contiguous id blocks keep it small
+on grids; a fabric needs the locality partition (:func:`locality_partition`:
+a pod's switches together), which halves the largest closure of 8 ranks.
 
 Weak scaling over per-rank LSDB snapshots (``snapshot_for_rank``, the
 per-iteration drain of ``BM_DecisionFabric``, RoutingBenchmarkUtils.cpp:
@@ -26,7 +27,7 @@ tensors in the tests).
 
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -52,6 +53,56 @@ def source_shard(n_sources: int, rank: int, world: int) -> np.ndarray:
     return np.arange(rank, n_sources, world, dtype=np.uint32)
 
 
+def closure_sizes(srcs: Sequence[np.ndarray], nbrs: Sequence, n: int) -> List[int]:
+    """Rows each rank's plan solves: its sources and their distinct up
+    neighbours (the next-hop pass of source s reads the rows of s's
+    neighbours, spf_plan_closure_rows)."""
+    out = []
+    for ss in srcs:
+        m = np.zeros(n, bool)
+        m[np.asarray(ss, np.int64)] = True
+        if len(ss):
+            m[np.concatenate([np.asarray(nbrs[int(s)], np.int64) for s in ss])] = True
+        out.append(int(m.sum()))
+    return out
+
+
+def locality_partition(nbrs: Sequence, cost: np.ndarray, world: int,
+                       slack: float = 0.03) -> List[np.ndarray]:
+    """Sources to ranks so that each rank's closure (its sources plus their
+    neighbours, all of which its plan must solve) stays small: a one-pass
+    streaming partition (in the manner of linear deterministic greedy):
+    nodes in ascending degree, each to the rank whose closure it grows least
+    among the ranks whose source cost stays within (1 + slack) of the mean,
+    ties to the least-loaded rank.  Low-degree nodes first: a fabric's rack
+    switches gather by pod (they share their pod's fabric switches), the
+    fabric switches follow their pod and a plane's spines land together --
+    the closure of a rank of 8 is ~1.8k rows instead of up to 4.8k for id
+    blocks (FSW blocks need every rack switch of their pods).  Generic: only
+    the neighbour lists are used."""
+    n = len(nbrs)
+    deg = np.array([len(x) for x in nbrs], np.int64)
+    order = np.lexsort((np.arange(n), deg))
+    cost = np.asarray(cost, np.float64)
+    cap = cost.sum() / world * (1.0 + slack)
+    clo = np.zeros((world, n), bool)
+    load = np.zeros(world)
+    owner = np.empty(n, np.int64)
+    for v in order:
+        nb = np.append(np.asarray(nbrs[v], np.int64), v)
+        new = (~clo[:, nb]).sum(axis=1).astype(np.float64)
+        ok = load + cost[v] <= cap
+        if not ok.any():
+            ok[:] = True
+        new[~ok] = np.inf
+        best = np.flatnonzero(new == new.min())
+        r = int(best[np.argmin(load[best])])
+        owner[v] = r
+        clo[r, nb] = True
+        load[r] += cost[v]
+    return [np.flatnonzero(owner == r).astype(np.uint32) for r in range(world)]
+
+
 class AllSourcesLayout:
     """Where every source's result lives when the all-sources pass is split
     over `world` ranks and gathered to rank 0.
@@ -74,9 +125,10 @@ class AllSourcesLayout:
     # its distance rows (u32 + u8 copy = 5N bytes = 40 bitmaps) -- the bytes
     # every rank's kernels write dominate a pass
     ROW_COST = 40
+    LOCALITY_MAX_NODES = 1 << 16
 
     def __init__(self, k: np.ndarray, pitch: int, world: int, dist_bytes: int = 4,
-                 row_cost: float = ROW_COST) -> None:
+                 row_cost: float = ROW_COST, nbrs: Optional[Sequence] = None) -> None:
         k = np.asarray(k, np.int64)
         n = len(k)
         assert dist_bytes in (1, 4) and (pitch * dist_bytes) % 4 == 0
@@ -91,6 +143,18 @@ class AllSourcesLayout:
         bounds = [0] + [int(np.searchsorted(cost, total * r / world, side="right"))
                         for r in range(1, world)] + [n]
         self.srcs = [np.arange(bounds[r], bounds[r + 1], dtype=np.uint32) for r in range(world)]
+        self.partition = "contiguous"
+        self.closure = None
+        if nbrs is not None and world > 1 and n <= self.LOCALITY_MAX_NODES:
+            # a rank also solves its sources' neighbours (the next-hop pass
+            # reads their rows): take the locality partition when its largest
+            # closure is smaller than the contiguous blocks'
+            cont = closure_sizes(self.srcs, nbrs, n)
+            loc = locality_partition(nbrs, k + row_cost, world)
+            loc_c = closure_sizes(loc, nbrs, n)
+            self.closure = cont
+            if max(loc_c) < max(cont):
+                self.srcs, self.closure, self.partition = loc, loc_c, "locality"
         self.rank_of = np.zeros(n, np.int64)
         self.index_of = np.zeros(n, np.int64)
         self.nh_off = np.zeros(n, np.int64)  # word offset within the rank's send buffer
