@@ -153,8 +153,9 @@ class AllSources:
     """configs[1]/[2]: one all-sources SPF + ECMP pass per step.
 
     strong scaling (default), results resident (default): one LSDB, its
-    sources split over the ranks in contiguous id blocks balanced by next-hop
-    work (sharding.AllSourcesLayout); every rank writes its sources' distance
+    sources split over the ranks balanced by next-hop work, grouped so each
+    rank's closure stays small (sharding.AllSourcesLayout: contiguous id
+    blocks or the locality partition); every rank writes its sources' distance
     rows and next-hop bitmaps into buffers that stay in its HBM -- the
     sharded result the facade serves getSpfResult(node) from on the owning
     rank (Decision::getDecisionRouteDb per node, Decision.cpp:1480-1500).  No
@@ -231,12 +232,13 @@ class AllSources:
         self._phase_bytes()
         self._algorithmic_bytes()
         self.parallelism = (
-            f"sources in contiguous id blocks over {world} rank(s) (one LSDB), plan closure "
+            f"sources split over {world} rank(s) ({self.layout.partition} partition, one LSDB), plan closure "
             f"{self.plan.closure_rows} rows for {len(srcs)} sources; per-source results "
             f"({self.wire}) gathered to rank 0 over RCCL in the step "
             f"({self.gather_bytes / 1e6:.0f} MB/step, send buffers double-buffered)"
             if gather else
-            f"sources in contiguous id blocks over {world} rank(s) (one LSDB, graph replicated), "
+            f"sources split over {world} rank(s) ({self.layout.partition} partition: "
+            f"closure rows per rank {self.layout.closure}; one LSDB, graph replicated), "
             f"plan closure {self.plan.closure_rows} rows for {len(srcs)} sources; results "
             f"resident in each rank's HBM (no collective in the step); per-source digests "
             f"gathered to rank 0 after the timed steps"

@@ -151,7 +151,8 @@ uint32_t spf_plan_closure_rows(const spf_plan* plan); /* sources actually solved
  * workgroups on one XCD); *narrow = 0 when the
  * next-hop pass (ecmp_kernel) reads the u32 rows, 1 when it reads u8 rows,
  * 2 when slice_rows_kernel turns the u8 rows into bit planes and
- * ecmp_sliced_kernel matches those.
+ * ecmp_sliced_kernel matches those, 3 when msbfs_team_kernel writes the bit
+ * planes itself (4 per word; no u8 rows, no slicing pass).
  * No reference counterpart (engine introspection). */
 spf_status spf_plan_kernels(const spf_plan* plan, uint32_t* bfs, uint32_t* narrow);
 /* Bytes the distance kernel and the next-hop kernel of one execute must move

@@ -144,6 +144,7 @@ struct spf_plan {
   bool exact = false;   // exact_spf_kernel (exact.hip): zero/negative metrics, u64, any size
   bool mp = false;      // weighted: mssp_kernel (mssp.hip), S sources per workgroup
   bool pl_order = false;  // planes BFS: rows batched deepest-first (d_pl_order)
+  bool sdirect = false;   // team plan writing the sliced rows itself (kTeamPlanes planes, no u8 rows)
   // msbfs_team_kernel (msbfs_team.hip): G workgroups per batch when the plan
   // has too few batches to fill the chip (tm_G == 0: msbfs_kernel)
   uint32_t tm_G = 0, tm_own = 0, tm_teams = 0, tm_bs = 0, tm_nacc = 0;
@@ -218,7 +219,10 @@ uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows);
 spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G);
 spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, uint32_t rows,
                              uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s,
-                             uint32_t d_rows);  // u32 rows written: closure rows < d_rows
+                             uint32_t d_rows,  // u32 rows written: closure rows < d_rows
+                             uint32_t* S = nullptr, uint32_t s_stride = 0);  // sdirect planes
+// planes per word of the rows msbfs_team_kernel slices itself (sdirect plans)
+constexpr uint32_t kTeamPlanes = 4;
 spf_status msbfs_team_timed_out(spf_ctx* c, bool* out);
 spf_status mssp_prepare(spf_ctx* c);
 spf_status mssp_set_lds_limits(spf_ctx* c);

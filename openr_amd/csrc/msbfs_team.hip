@@ -50,8 +50,9 @@ constexpr uint32_t kTmWaves = kTmThreads / 64;
 constexpr uint32_t kTmBatch = 64;
 constexpr uint32_t kTmSpin = 1u << 26;        // ~seconds: never a silent hang
 constexpr size_t kTmMaxLds = 160 * 1024;
-constexpr int kTmPlanes = 3;                              // distance bit planes per owned node
+constexpr int kTmPlanes = 4;                              // distance bit planes per owned node
 constexpr uint32_t kTmWindow = (1u << kTmPlanes) - 1;     // levels per window; marker value
+static_assert(kTmPlanes == (int)kTeamPlanes, "sdirect rows: the next-hop pass reads kTeamPlanes planes");
 constexpr int kTmCopy = 10;                               // uint4 per thread of the frontier copy
 constexpr uint32_t kTmRows = 16;                          // sources per flush tile (80 B each per node)
 constexpr uint32_t kTmBarPad = 32;            // words per team: counter line + 3 flag lines
@@ -68,6 +69,8 @@ struct TeamArgs {
   uint32_t n_rows, bs, n_batches, N, pitch, npitch, G, teams_per_xcd, n_acc, fwords, front_bytes;
   uint32_t col_bytes;  // sell_col incl. its trailing padding group
   uint32_t d_rows;     // closure rows < d_rows have u32 rows in D (the request's prefix)
+  uint32_t* S;         // sdirect: bit-sliced rows (kTmPlanes planes per 32-node word) instead of Dn
+  uint32_t s_stride;   // words per sliced row
   uint32_t* D;
   uint8_t* Dn;
   uint32_t* maxd;
@@ -257,15 +260,22 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
           const uint32_t v = sv[i] + lane;
           for (uint32_t g0 = 0; g0 < nb; g0 += kTmRows) {
             const uint32_t gn = min(kTmRows, nb - g0);
+            // a group's 16 sources lie in one 32-bit half of the masks: 32-bit
+            // bit-field extracts, ~12 VALU per (source, node) (the 64-bit
+            // shifts made the flush VALU-bound)
+            const bool hi = g0 >= 32;
+            uint32_t pw[kTmPlanes];
+#pragma unroll
+            for (int b = 0; b < kTmPlanes; ++b) pw[b] = hi ? (uint32_t)(P[i][b] >> 32) : (uint32_t)P[i][b];
+            const uint32_t vw = v < N ? (hi ? (uint32_t)(vis[i] >> 32) : (uint32_t)vis[i]) : 0u;
             for (uint32_t r = 0; r < gn; ++r) {
-              const uint32_t s = g0 + r;
+              const uint32_t sh = (g0 + r) & 31u;
               uint32_t q = 0;
 #pragma unroll
-              for (int b = 0; b < kTmPlanes; ++b) q |= (uint32_t)((P[i][b] >> s) & 1ull) << b;
-              const bool seen = v < N && ((vis[i] >> s) & 1ull);
-              const uint32_t d = seen ? base + q : kInf;
-              T32[r * 64 + lane] = d;
-              T8[r * 64 + lane] = d == kInf ? 0xFFu : (uint8_t)min(d, 254u);
+              for (int b = 0; b < kTmPlanes; ++b) q |= ((pw[b] >> sh) & 1u) << b;
+              const bool seen = (vw >> sh) & 1u;
+              T32[r * 64 + lane] = seen ? q : kInf;  // first window: base == 0
+              T8[r * 64 + lane] = seen ? q : 0xFFu;   // q <= kTmWindow - 1 < 254
             }
             if (a.D)
               for (uint32_t r4 = 0; r4 < gn; r4 += 4) {
@@ -276,6 +286,34 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
                                             (lane & 15) * 4) = x;
                 }
               }
+            if (a.S) {
+              // the sliced rows (ecmp_sliced_kernel's layout with P =
+              // kTmPlanes): word w of row r holds plane b at w * P + b, bit t
+              // = node 32w + t; code all-ones = unreachable (byte 0xFF; nodes
+              // past N too).  From the byte tile: lane (row r = lane / 4,
+              // quarter q = lane % 4) turns its 16 bytes into a 16-bit piece
+              // of each plane (slice_rows_kernel's multiply gather), lanes
+              // q and q ^ 1 join their pieces into the word (DPP quad swap),
+              // even quarters store their word's P planes as one dwordx4
+              const uint32_t r = lane >> 2;
+              const uint4 x = *reinterpret_cast<const uint4*>(T8 + (r < gn ? r : 0) * 64 + (lane & 3) * 16);
+              const uint32_t dw[4] = {x.x, x.y, x.z, x.w};
+              uint32_t wd[kTmPlanes];
+#pragma unroll
+              for (int b = 0; b < kTmPlanes; ++b) {
+                uint32_t h = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  h |= ((((dw[q] >> b) & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+                const uint32_t o = (uint32_t)__builtin_amdgcn_mov_dpp((int)h, 0xB1, 0xF, 0xF, false);  // quad_perm(1,0,3,2)
+                wd[b] = h | (o << 16);  // even quarter: its own piece low, the odd neighbour's high
+              }
+              if (r < gn && (lane & 1) == 0) {
+                uint4* o = reinterpret_cast<uint4*>(a.S + (size_t)(row0 + g0 + r) * a.s_stride +
+                                                    (sv[i] / 32u + ((lane >> 1) & 1)) * kTmPlanes);
+                *o = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+              }
+            }
             if (a.Dn) {
               const uint32_t r = lane >> 2;
               if (r < gn) {
@@ -453,15 +491,17 @@ uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows) {
     const uint32_t G = (uint32_t)atoi(e);
     return valid(G) ? G : 0;
   }
-  // per-level cost model (us): msbfs_kernel sweeps every column group with
-  // one workgroup (16 waves, ~6.5 groups per us per wave: 8 dependent loads
-  // in flight); a team of G sweeps 1/G of them with 16-load chunks (~32
-  // groups per us per wave) plus a fixed per-level cost (barrier, frontier
-  // copy) and takes ceil(batches / teams) rounds.  SPF_TEAM_LEVEL_US tunes.
+  // per-level cost model (us), fitted to fabric_full stamps and kernel
+  // times (r03_v11..v14): msbfs_kernel sweeps every column group with one
+  // workgroup (16 waves, ~6.5 groups per us per wave, +20 % for its
+  // per-level stores); a team of G sweeps 1/G of them (~4 groups per us per
+  // wave: column loads, LDS gathers and the accumulator ORs) plus ~5 us per
+  // level (write-through hand-off, arrival word, frontier copy) and takes
+  // ceil(batches / teams) rounds.  SPF_TEAM_LEVEL_US tunes the fixed part.
   const double groups = (double)(c->sell_ptr.back() / 64);
   const char* lu = std::getenv("SPF_TEAM_LEVEL_US");
-  const double level_us = lu ? atof(lu) : 4.0;
-  const double single = groups / kTmWaves / 6.5;
+  const double level_us = lu ? atof(lu) : 5.0;
+  const double single = groups / kTmWaves / 6.5 * 1.2;
   const uint64_t batches = (rows + kTmBatch - 1) / kTmBatch;
   uint32_t best = 0;
   double best_cost = single;
@@ -469,7 +509,7 @@ uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows) {
     if (!valid(G)) continue;
     const uint64_t teams = c->n_cu / G;
     const double rounds = (double)((batches + teams - 1) / teams);
-    const double cost = rounds * (groups / (kTmWaves * G) / 32.0 + level_us);
+    const double cost = rounds * (groups / (kTmWaves * G) / 4.0 + level_us);
     if (cost < best_cost) best_cost = cost, best = G;
   }
   return best;
@@ -533,14 +573,25 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
      // the plan keeps msbfs_kernel (tm_G stays 0; spf_plan_kernels tells)
     const void* k = team_kernel(own);
     HIP_TRY(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTmMaxLds));
-    int fit = 0;
-    HIP_TRY(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit, k, kTmThreads, team_lds(fw, n_acc)));
-    if (fit < 1 || (uint64_t)fit * c->n_cu < (uint64_t)teams * G) {
+    // one block per CU needs: the block's registers (compiled for 1024
+    // threads: maxThreadsPerBlock), its LDS within the CU's 160 KiB, and
+    // one block per CU in the grid (teams * G == n_cu).  (The occupancy API
+    // answered 0 for this kernel on some boxes and 1 on others with the same
+    // image and the same arguments; these static facts decide instead.)
+    hipFuncAttributes fa{};
+    HIP_TRY(c, hipFuncGetAttributes(&fa, k));
+    const size_t lds = team_lds(fw, n_acc) + fa.sharedSizeBytes;
+    if (fa.maxThreadsPerBlock < (int)kTmThreads || lds > kTmMaxLds || (uint64_t)teams * G > c->n_cu) {
       if (std::getenv("SPF_TEAM_DEBUG"))
-        std::fprintf(stderr, "msbfs_team: <%u> not co-resident (%d per CU, %zu B LDS, G %u): msbfs_kernel\n",
-                     own, fit, team_lds(fw, n_acc), G);
+        std::fprintf(stderr, "msbfs_team: <%u> not co-resident (max threads %d, %zu B LDS, G %u): msbfs_kernel\n",
+                     own, fa.maxThreadsPerBlock, lds, G);
       p->tm_G = 0;
       return SPF_OK;
+    }
+    if (std::getenv("SPF_TEAM_DEBUG")) {
+      int fit = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit, k, kTmThreads, team_lds(fw, n_acc));
+      std::fprintf(stderr, "msbfs_team: <%u> G %u, %zu B LDS, occupancy API %d per CU\n", own, G, lds, fit);
     }
   }
   p->tm_G = G;
@@ -568,7 +619,7 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
 
 spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, uint32_t rows,
                              uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s,
-                             uint32_t d_rows) {
+                             uint32_t d_rows, uint32_t* S, uint32_t s_stride) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
     HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
@@ -581,7 +632,7 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
              rows, p->tm_bs, (rows + p->tm_bs - 1) / p->tm_bs, c->N, c->pitch, c->npitch, p->tm_G,
              (c->n_cu / 8) / p->tm_G, p->tm_nacc, fw,
              (uint32_t)std::max<size_t>(8ull * fw, (size_t)kTmWaves * kTmRows * 80 * 4),
-             (uint32_t)(4ull * c->sell_col.size()), d_rows, D, Dn, maxd,
+             (uint32_t)(4ull * c->sell_col.size()), d_rows, S, s_stride, D, Dn, maxd,
              reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p};
   const uint32_t* meta = p->d_tm_map.p + p->tm_runs_at;
   const uint32_t blocks = p->tm_teams * p->tm_G;  // = n_cu: one persistent workgroup per CU

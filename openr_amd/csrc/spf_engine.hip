@@ -1219,12 +1219,13 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     const uint32_t* __restrict__ nb_w, const uint32_t* __restrict__ nb_row,
     const uint32_t* __restrict__ nb_row_off, const uint32_t* __restrict__ nb_drained,
     uint32_t dead, uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
-    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes) {
-  const uint32_t md = *maxd;
+    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes,
+    uint32_t fixed_p /* rows sliced by the BFS itself (sdirect): P planes, maxd unused */) {
+  const uint32_t md = fixed_p ? 0u : *maxd;
   const uint32_t g = blockIdx.x & 7;  // this block's XCD (round-robin placement)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wpm = pitch / 32;
-  const uint32_t P = md < kSlSat ? 32u - __clz(md + 1u) : 0u;  // 0: saturated
+  const uint32_t P = fixed_p ? fixed_p : md < kSlSat ? 32u - __clz(md + 1u) : 0u;  // 0: saturated
   const uint32_t rstride = kSlSlots * wpm;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(S), 0, (int)s_bytes, 0x00020000);
@@ -2048,6 +2049,11 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     // kernel's time (r02_v25/r02_v26)
     const char* x = std::getenv("SPF_EXPAND");
     p->expand = p->sliced && c->pitch <= c->npitch && x && x[0] == '1';
+    // team plans whose depth stays below the planes' all-ones code write the
+    // sliced rows themselves: no u8 rows, no slicing pass (SPF_SDIRECT=0: A/B)
+    const char* sd = std::getenv("SPF_SDIRECT");
+    p->sdirect = p->sliced && p->nh_total && p->tm_G && p->prefix && !p->expand &&
+                 depth_bound(c) < (1u << kTeamPlanes) - 1 && !(sd && sd[0] == '0');
   }
   const uint32_t wpm = c->pitch / 32;
   const uint64_t rstride = (uint64_t)kSlSlots * wpm;  // sliced row: words
@@ -2149,7 +2155,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors end here
   }
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
-  if (p->narrow) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
+  if (p->narrow && !p->sdirect) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
     HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
     HIP_TRY(c, hipMemsetAsync(p->d_Dn.p + p->closure.size() * c->npitch, 0xFF, c->npitch, c->stream));
   }
@@ -2205,7 +2211,7 @@ spf_status spf_plan_kernels(const spf_plan* p, uint32_t* bfs, uint32_t* narrow) 
   if (!p || !bfs || !narrow) return SPF_E_INVALID;
   *bfs = p->big ? 4u : p->exact ? 3u : p->mp ? 5u : !p->ms ? 0u : p->tm_G ? 6u
                                                           : use_planes(p->ctx) ? 2u : 1u;
-  *narrow = p->sliced ? 2u : p->narrow ? 1u : 0u;
+  *narrow = p->sdirect ? 3u : p->sliced ? 2u : p->narrow ? 1u : 0u;
   return SPF_OK;
 }
 
@@ -2502,7 +2508,7 @@ spf_status launch_ecmp_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool h
                      c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p,
                      p->d_nb_drained.p, p->dead, hop ? 1u : 0u, p->d_nh_off.p, d_nh,
                      reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p,
-                     (uint32_t)(p->d_S.n * 4));
+                     (uint32_t)(p->d_S.n * 4), p->sdirect ? kTeamPlanes : 0u);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -2593,7 +2599,9 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   // team plans whose closure starts with the request's rows write those
   // rows' u32 distances straight into d_dist (and no others): no scratch
   // rows, no gather
-  const bool team_direct = p->tm_G && p->prefix && !p->direct;
+  // (u8 or sliced rows only: the u32-row next-hop pass reads the neighbours'
+  // u32 rows, which then exist nowhere)
+  const bool team_direct = p->tm_G && p->prefix && !p->direct && p->narrow;
   uint32_t* D = (p->direct || team_direct) ? d_dist : p->d_D.p;
   const uint32_t rows = (uint32_t)p->closure.size();
   const bool sliced = p->sliced && p->nh_total;
@@ -2605,8 +2613,12 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     HIP_TRY(c, hipEventRecord(ev[0], s));
   }
   spf_status st =
-      p->tm_G ? launch_msbfs_team(c, p, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
-                                  sliced ? p->d_maxd.p : nullptr, s, team_direct ? p->n_src : rows)
+      p->tm_G ? launch_msbfs_team(c, p, p->d_closure.p, rows, D,
+                                  p->narrow && !p->sdirect ? p->d_Dn.p : nullptr,
+                                  sliced && !p->sdirect ? p->d_maxd.p : nullptr, s,
+                                  team_direct ? p->n_src : rows,
+                                  p->sdirect ? p->d_S.p : nullptr,
+                                  kSlSlots * (pitch / 32))
       : p->ms ? launch_msbfs(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
                                        sliced ? p->d_maxd.p : nullptr, s,
                                        sliced && p->expand ? kSlSat : 0u,
@@ -2617,7 +2629,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
                                       nullptr, p->narrow ? p->d_Dn.p : nullptr);
   if (st != SPF_OK) return st;
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
-  if (sliced) {
+  if (sliced && !p->sdirect) {
     st = launch_sliced(c, p, D, hop, d_nh, s);
     if (st != SPF_OK) return st;
   }

@@ -99,7 +99,7 @@ class SpfPlan(NativeHandle):
 
     BFS_KERNELS = ("sssp_kernel", "msbfs_kernel", "msbfs_planes_kernel", "exact_spf_kernel",
                    "spf_big_kernel", "mssp_kernel", "msbfs_team_kernel")
-    ROW_MODES = ("u32", "u8", "sliced")
+    ROW_MODES = ("u32", "u8", "sliced", "sliced_bfs")
 
     def kernels(self) -> Tuple[str, bool]:
         """(distance kernel name, next-hop pass reads u8 narrow rows or their
@@ -113,7 +113,8 @@ class SpfPlan(NativeHandle):
         return bfs.value, narrow.value
 
     def row_mode(self) -> str:
-        """Rows the next-hop pass reads: "u32", "u8" or "sliced" (bit planes)."""
+        """Rows the next-hop pass reads: "u32", "u8", "sliced" (bit planes from
+        the u8 rows) or "sliced_bfs" (bit planes written by the team BFS)."""
         return self.ROW_MODES[self._kernel_codes()[1]]
 
     def phase_kernels(self) -> Tuple[str, Optional[str], Optional[str]]:
@@ -125,6 +126,8 @@ class SpfPlan(NativeHandle):
             return name, None, None
         if narrow == 2:
             return name, "slice_rows_kernel", "ecmp_sliced_kernel"
+        if narrow == 3:
+            return name, None, "ecmp_sliced_kernel"
         return name, None, "ecmp_kernel"
 
     def traffic(self) -> Tuple[int, int]:

@@ -140,6 +140,7 @@ def test_next_hop_pass_every_row_form(name, make, narrow, monkeypatch):
     SPF_NARROW=0/1/2 forces it), unit metrics and hop counts."""
     monkeypatch.setenv("SPF_NARROW", narrow)
     monkeypatch.setenv("SPF_MSBFS", "masks")  # the per-level BFS reports the depth slicing needs
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "0")  # msbfs_kernel's row forms (team: test_gpu_team.py)
     names, eng, orc = load(make())
     assert eng.plan([0], hop=True).row_mode() == ROW_MODES[narrow]
     compare(names, eng, orc, list(range(len(names))), hop=True)
@@ -168,6 +169,7 @@ def test_sliced_plane_counts(depth, monkeypatch):
     saturates)."""
     monkeypatch.setenv("SPF_NARROW", "2")
     monkeypatch.setenv("SPF_MSBFS", "masks")
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "0")  # slice_rows_kernel's plane counts
     names, eng, orc = load(T.clique_with_tail(12, depth))
     p = eng.plan([0], hop=True)
     assert p.row_mode() == "sliced"
@@ -222,6 +224,7 @@ def test_expanded_u32_rows(name, make, expand, monkeypatch):
     monkeypatch.setenv("SPF_EXPAND", expand)
     monkeypatch.setenv("SPF_NARROW", "2")
     monkeypatch.setenv("SPF_MSBFS", "masks")
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "0")
     names, eng, orc = load(make())
     assert eng.plan([0], hop=True).row_mode() == "sliced"
     compare(names, eng, orc, list(range(len(names))), hop=True)

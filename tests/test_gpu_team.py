@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from openr_amd import topology as T
-from test_gpu_engine import ROW_MODES, compare, load
+from test_gpu_engine import compare, load
 
 pytestmark = pytest.mark.gpu
 
@@ -32,14 +32,37 @@ def test_team_bfs_every_team_size(name, make, G, monkeypatch):
     compare(names, eng, orc, [5, 1, 5, 0])  # unsorted, duplicated sources
 
 
-@pytest.mark.parametrize("narrow", ["0", "1", "2"])
-def test_team_bfs_every_row_form(narrow, monkeypatch):
+@pytest.mark.parametrize("narrow,sdirect,mode", [("0", "1", "u32"), ("1", "1", "u8"),
+                                                  ("2", "0", "sliced"), ("2", "1", "sliced_bfs")])
+def test_team_bfs_every_row_form(narrow, sdirect, mode, monkeypatch):
+    """Every row form behind the team BFS: u32 rows, u8 rows, bit planes
+    sliced from the u8 rows, and bit planes the team kernel writes itself
+    (sdirect: no u8 rows, no slicing pass)."""
     monkeypatch.setenv("SPF_MSBFS_TEAM", "8")
     monkeypatch.setenv("SPF_MSBFS", "masks")
     monkeypatch.setenv("SPF_NARROW", narrow)
+    monkeypatch.setenv("SPF_SDIRECT", sdirect)
     names, eng, orc = load(T.fabric(1000, full=True))
     p = eng.plan([0], hop=True)
-    assert p.kernels()[0] == "msbfs_team_kernel" and p.row_mode() == ROW_MODES[narrow]
+    assert p.kernels()[0] == "msbfs_team_kernel" and p.row_mode() == mode
+    compare(names, eng, orc, list(range(len(names))))
+    compare(names, eng, orc, list(range(0, len(names), 7)), hop=True)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 5, 6, 13, 14, 15, 16, 40])
+def test_team_planes_every_depth(depth, monkeypatch):
+    """The team kernel's distances live in 4 register bit planes per node,
+    written in windows of 15 levels: shallow graphs take the sdirect rows
+    (the planes are the next-hop pass's input), deeper ones the u8 rows and
+    window flushes (a dense core with a path tail sets the depth)."""
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "4")
+    monkeypatch.setenv("SPF_MSBFS", "masks")
+    monkeypatch.setenv("SPF_NARROW", "2")
+    names, eng, orc = load(T.clique_with_tail(12, depth))
+    p = eng.plan([0], hop=True)
+    assert p.kernels()[0] == "msbfs_team_kernel"
+    assert p.row_mode() in ("sliced", "sliced_bfs")
+    compare(names, eng, orc, list(range(len(names))), hop=True)
     compare(names, eng, orc, list(range(len(names))))
 
 
