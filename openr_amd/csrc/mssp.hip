@@ -59,6 +59,7 @@ constexpr uint32_t kMpWaves = kMpThreads / 64;
 constexpr uint32_t kMpNoSlice = 0xFFFFFFFFu;
 constexpr size_t kMpMaxLds = 160 * 1024;
 constexpr size_t kMpStaticLds = 256;  // the kernel's own static LDS (__syncthreads_or)
+constexpr uint32_t kMpAhead = 8;      // packed in-edge loads per group (two groups in flight)
 
 // LDS minimum of one u16 half of a word (CAS loop: two sources share a word)
 __device__ void lds_min16(uint32_t* p, uint32_t half, uint32_t val) {
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     const uint32_t* __restrict__ col, const uint32_t* __restrict__ wt,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src, uint32_t n_rows,
     uint32_t N, uint32_t pitch, uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
-    uint32_t ovf_at, uint32_t* __restrict__ redo) {
+    uint32_t ovf_at, uint32_t* __restrict__ redo,
+    unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */) {
   constexpr uint32_t S = 2 * SD;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t bw = (N + 32) / 32;  // change-bitmap words (nodes 0..N)
@@ -128,6 +130,18 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
   }
   __syncthreads();
 
+  // the lane's drained bit of each of its wave's slots (bit k), once: the
+  // sweeps test it without a global load
+  uint32_t dmask = 0;
+  {
+    const uint32_t* wm = smap + __builtin_amdgcn_readfirstlane(wave) * slots;
+    for (uint32_t k = 0; k < slots && k < 32; ++k) {
+      const uint32_t sl = wm[k];
+      if (sl == kMpNoSlice) break;
+      const uint32_t v = sl * 64 + lane;
+      if (v < N && ovl[v]) dmask |= 1u << k;
+    }
+  }
   for (uint32_t it = 0;; ++it) {
     const uint32_t* cur = bits + (it % 3) * bw;
     uint32_t* nxt = bits + ((it + 1) % 3) * bw;
@@ -135,31 +149,70 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     for (uint32_t i = tid; i < bw; i += kMpThreads) old[i] = 0;
     if (tid == 0) flag[(it + 1) % 3] = 0;
     bool changed = false;
+    // the wave's slot table by scalar loads, the next slot's entry fetched
+    // while this slot's columns run (a dependent smap -> sell_ptr chain per
+    // slot was ~2 us of every sweep's critical path)
+    const uint32_t* wmap = smap + __builtin_amdgcn_readfirstlane(wave) * slots;
+    uint32_t nsl = wmap[0];
+    uint32_t nb0 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl], nb1 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl + 1];
     for (uint32_t k = 0; k < slots; ++k) {
-      const uint32_t sl = smap[wave * slots + k];
+      const uint32_t sl = nsl;
       if (sl == kMpNoSlice) break;  // a wave's slots are filled from the front
+      const uint32_t b = nb0, w = (nb1 - nb0) / 64;
+      nsl = k + 1 < slots ? wmap[k + 1] : kMpNoSlice;
+      if (nsl != kMpNoSlice) {
+        nb0 = sell_ptr[nsl];
+        nb1 = sell_ptr[nsl + 1];
+      }
       const uint32_t v = sl * 64 + lane;
-      const uint32_t b = sell_ptr[sl], w = (sell_ptr[sl + 1] - b) / 64;
       uint32_t acc[SD];
 #pragma unroll
       for (int q = 0; q < SD; ++q) acc[q] = 0xFFFFFFFFu;
       bool got = false;
       const uint32_t* ep = ell + b + lane;
-      uint32_t ent = w ? ep[0] : 0u;
-      for (uint32_t j = 0; j < w; ++j) {
-        const uint32_t cent = ent;
-        if (j + 1 < w) ent = ep[(j + 1) * 64];  // next column's entry in flight
-        const uint32_t u = cent & 0xFFFFu;
-        const uint32_t m = 1u << (u & 31);
-        const bool c = ((cur[u >> 5] | nxt[u >> 5]) & m) != 0;
-        if (!__builtin_amdgcn_ballot_w64(c)) continue;  // no lane's neighbour changed
-        if (c) {
-          const uint32_t wp = (cent >> 16) * 0x00010001u;
-          uint32_t d[SD];
-          load_words<SD>(&dist[u * SD], d);
+      // the slice's packed in-edges kMpAhead columns at a time, the next
+      // group's loads in flight while this group's labels are folded (one
+      // entry in flight made every column an L2 round trip)
+      // a group of kMpAhead columns: every change-bit read issued, then
+      // every label read of the lanes whose neighbour changed (exec-masked,
+      // all in flight), then the folds -- the per-column chain of two
+      // dependent LDS round trips bounded the sweep (5.7 sweeps of ~67 us)
+      auto fold = [&](const uint32_t (&e)[kMpAhead], uint32_t n) {
+        uint32_t cw[kMpAhead];
 #pragma unroll
-          for (int q = 0; q < SD; ++q) acc[q] = min2(acc[q], add_sat2(d[q], wp));
-          got = true;
+        for (int t = 0; t < (int)kMpAhead; ++t) {
+          const uint32_t u = e[t] & 0xFFFFu;
+          cw[t] = cur[u >> 5] | nxt[u >> 5];
+        }
+        uint32_t d[kMpAhead][SD];
+        bool c[kMpAhead];
+#pragma unroll
+        for (int t = 0; t < (int)kMpAhead; ++t) {
+          const uint32_t u = e[t] & 0xFFFFu;
+          c[t] = (uint32_t)t < n && ((cw[t] >> (u & 31)) & 1u);
+          if (c[t]) load_words<SD>(&dist[u * SD], d[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < (int)kMpAhead; ++t)
+          if (c[t]) {
+            const uint32_t wp = (e[t] >> 16) * 0x00010001u;
+#pragma unroll
+            for (int q = 0; q < SD; ++q) acc[q] = min2(acc[q], add_sat2(d[t][q], wp));
+            got = true;
+          }
+      };
+      uint32_t ea[kMpAhead], eb[kMpAhead];
+      auto load = [&](uint32_t j0, uint32_t (&e)[kMpAhead]) {
+#pragma unroll
+        for (int t = 0; t < (int)kMpAhead; ++t) e[t] = j0 + t < w ? ep[(j0 + t) * 64] : N;  // N: padding
+      };
+      load(0, ea);
+      for (uint32_t j0 = 0; j0 < w; j0 += 2 * kMpAhead) {
+        if (j0 + kMpAhead < w) load(j0 + kMpAhead, eb);
+        fold(ea, w - j0);
+        if (j0 + kMpAhead < w) {
+          if (j0 + 2 * kMpAhead < w) load(j0 + 2 * kMpAhead, ea);
+          fold(eb, w - j0 - kMpAhead);
         }
       }
       if (got && v < N) {
@@ -175,13 +228,20 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         }
         if (dec) {
           changed = true;
-          if (!ovl[v]) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+          if (k < 32 ? !((dmask >> k) & 1u) : !ovl[v]) atomicOr(&nxt[v >> 5], 1u << (v & 31));
         }
       }
     }
     if (__builtin_amdgcn_ballot_w64(changed) && lane == 0) flag[it % 3] = 1;
     __syncthreads();
-    if (!flag[it % 3]) break;
+    if (!flag[it % 3]) {
+      if (stats && tid == 0) {
+        atomicAdd(&stats[0], (unsigned long long)(it + 1));
+        atomicMax(&stats[1], (unsigned long long)(it + 1));
+        atomicAdd(&stats[2], 1ull);
+      }
+      break;
+    }
   }
 
   // ---- rows: u32 (kInf = unreached, and past N as sssp_kernel) and the
@@ -326,6 +386,10 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   if (!sd) return fail(c, SPF_E_STATE, "mssp kernel does not apply to this graph");
   if (c->mp_epoch != c->epoch) return fail(c, SPF_E_STATE, "mssp tables stale: rebuild the plan");
   if (c->mp_redo) HIP_TRY(c, hipMemsetAsync(redo, 0, 4, s));
+  if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {  // sweep counters (diagnostics)
+    HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
+    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, (64 * 16 + 1) * 8, s));
+  }
   const uint32_t S = 2 * sd;
   const dim3 g((rows + S - 1) / S), b(kMpThreads);
   const uint32_t N = c->N;
@@ -333,7 +397,7 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
 #define MP_LAUNCH(SDV)                                                                            \
   hipLaunchKernelGGL(mssp_kernel<SDV>, g, b, mp_lds<SDV>(N), s, c->d_sell_ptr.p, c->d_mp_ell.p,   \
                      c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
-                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd)
+                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, c->d_stamps.p)
   switch (sd) {
     case 8: MP_LAUNCH(8); break;
     case 4: MP_LAUNCH(4); break;
