@@ -2085,8 +2085,10 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     // 1/(8 * runs) of the work each, every run to the XCD with the least
     // work so far (runs come in request order: the heavy spine and fabric
     // switches first)
+    // (a rank's share of a multi-GPU pass -- ~1.3k sources -- does best with
+    // two long runs per XCD: 0.097 -> 0.095 ms per world-8 rank, r03_v25)
     const char* env = std::getenv("SPF_ECMP_RUNS");
-    const uint32_t runs = env ? (uint32_t)atoi(env) : kEcmpRunsPerXcd;
+    const uint32_t runs = env ? (uint32_t)atoi(env) : n_src >= 4096 ? kEcmpRunsPerXcd : 2u;
     std::vector<uint32_t> lists[8];
     if (runs == 0) {  // plain round-robin
       for (uint32_t i = 0; i < n_src; ++i) lists[i % 8].push_back(i);
