@@ -128,7 +128,8 @@ class AllSourcesLayout:
     LOCALITY_MAX_NODES = 1 << 16
 
     def __init__(self, k: np.ndarray, pitch: int, world: int, dist_bytes: int = 4,
-                 row_cost: float = ROW_COST, nbrs: Optional[Sequence] = None) -> None:
+                 row_cost: float = ROW_COST, nbrs: Optional[Sequence] = None,
+                 partition: str = "auto") -> None:
         k = np.asarray(k, np.int64)
         n = len(k)
         assert dist_bytes in (1, 4) and (pitch * dist_bytes) % 4 == 0
@@ -153,7 +154,7 @@ class AllSourcesLayout:
             loc = locality_partition(nbrs, k + row_cost, world)
             loc_c = closure_sizes(loc, nbrs, n)
             self.closure = cont
-            if max(loc_c) < max(cont):
+            if partition == "locality" or (partition == "auto" and max(loc_c) < max(cont)):
                 self.srcs, self.closure, self.partition = loc, loc_c, "locality"
         self.rank_of = np.zeros(n, np.int64)
         self.index_of = np.zeros(n, np.int64)

@@ -1,7 +1,7 @@
 """Sharded-resident all-sources on the GPU (bench.py's default multi-GPU mode,
 SURVEY.md §8(e) row 1): every rank of a world-size-N run executes one plan
-over its contiguous block of sources (sharding.AllSourcesLayout) and keeps
-the rows in its own HBM; after the run rank 0 gathers per-source digests
+over its share of the sources (sharding.AllSourcesLayout: contiguous id
+blocks or the locality partition) and keeps the rows in its own HBM; after the run rank 0 gathers per-source digests
 computed on the GPU (spf_plan_digest).
 
 On one GPU each rank's plan is run in turn, into its own buffers, exactly as
@@ -42,8 +42,14 @@ def _run_rank(eng, srcs, dist64=False):
 
 
 @pytest.mark.parametrize("name", ["fabric_full", "grid100", "fabric_rtt"])
-@pytest.mark.parametrize("world", [2, 4])
-def test_emulated_ranks_resident_digests_match_oracle(name, world):
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("partition", ["contiguous", "bench"])
+def test_emulated_ranks_resident_digests_match_oracle(name, world, partition):
+    """Every rank's plan of a world-N split -- the contiguous id blocks, and
+    the layout bench.py builds (neighbour lists given: the locality
+    partition where it shrinks the closures; team BFS plans for the rank
+    shares of unit-metric graphs) -- digested on the GPU and reassembled,
+    against the oracle's digest of every source."""
     meta, g = golden(name)
     ls, names, csr, cd = _make(name)
     assert cd == meta["csr_digest"]
@@ -52,12 +58,17 @@ def test_emulated_ranks_resident_digests_match_oracle(name, world):
     eng = SpfEngine(0)
     try:
         eng.load(*csr)
-        k = np.array([len(eng.neighbors(s)) for s in range(len(names))], np.int64)
-        layout = AllSourcesLayout(k, eng.pitch, world)
+        nbrs = [eng.neighbors(s) for s in range(len(names))]
+        k = np.array([len(x) for x in nbrs], np.int64)
+        layout = AllSourcesLayout(k, eng.pitch, world, nbrs=nbrs if partition == "bench" else None)
+        if partition == "bench" and name != "grid100":
+            assert layout.partition == "locality"  # fabrics: pods together
         got = np.zeros(len(names), np.uint64)
         for r in range(world):
             got[layout.srcs[r]] = _run_rank(eng, layout.srcs[r])
         assert sorted(np.concatenate(layout.srcs).tolist()) == list(range(len(names)))
+        if name == "fabric_full" and world == 8 and partition == "bench":
+            assert eng.plan(layout.srcs[0]).kernels()[0] == "msbfs_team_kernel"
     finally:
         eng.close()
     bad = np.nonzero(got != want)[0]

@@ -252,7 +252,7 @@ def test_two_rank_ksp2_and_whatif_exchange_gloo():
 
 
 # ---- all-sources split + gather to rank 0 ------------
-def _all_sources_worker(rank, world, port, q, dist_bytes=4):
+def _all_sources_worker(rank, world, port, q, dist_bytes=4, locality=False):
     import sys
     from pathlib import Path
 
@@ -275,8 +275,11 @@ def _all_sources_worker(rank, world, port, q, dist_bytes=4):
         names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
         n = len(names)
         pitch = (n + 63) // 64 * 64
-        k = np.array([len(set(col[rp[v]:rp[v + 1]].tolist())) for v in range(n)])
-        lay = AllSourcesLayout(k, pitch, world, dist_bytes)
+        nbrs = [np.unique(col[rp[v]:rp[v + 1]]) for v in range(n)]
+        k = np.array([len(x) for x in nbrs])
+        lay = AllSourcesLayout(k, pitch, world, dist_bytes, nbrs=nbrs if locality else None,
+                               partition="locality" if locality else "auto")
+        assert lay.partition == ("locality" if locality else "contiguous")
         orc = OracleLinkState()
         orc.update_packed(topo.lsdb)
         # this rank's share, in the plan layout, written into the send buffer
@@ -303,16 +306,18 @@ def _all_sources_worker(rank, world, port, q, dist_bytes=4):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dist_bytes", [(2, 4), (3, 4), (2, 1), (3, 1)])
-def test_all_sources_split_and_gather_reassembles_single_rank_result(world, dist_bytes):
-    """One LSDB, sources split over ranks, every rank's dist rows (u32, or
-    the engine's u8 rows) + next-hop bitmaps gathered to rank 0 (gloo here,
-    RCCL in bench.py): rank 0's reassembled arrays equal the single-rank
-    all-sources result bit for bit."""
+@pytest.mark.parametrize("world,dist_bytes,locality", [(2, 4, False), (3, 4, False), (2, 1, False),
+                                                       (3, 1, False), (2, 4, True), (3, 1, True)])
+def test_all_sources_split_and_gather_reassembles_single_rank_result(world, dist_bytes, locality):
+    """One LSDB, sources split over ranks (contiguous id blocks, or the
+    locality partition bench.py takes for fabrics), every rank's dist rows
+    (u32, or the engine's u8 rows) + next-hop bitmaps gathered to rank 0
+    (gloo here, RCCL in bench.py): rank 0's reassembled arrays equal the
+    single-rank all-sources result bit for bit."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_all_sources_worker, args=(r, world, port, q, dist_bytes))
+    procs = [ctx.Process(target=_all_sources_worker, args=(r, world, port, q, dist_bytes, locality))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -321,6 +326,41 @@ def test_all_sources_split_and_gather_reassembles_single_rank_result(world, dist
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == (True, True, True)
+
+
+def test_locality_partition_shrinks_fabric_closures():
+    """sharding.locality_partition on fabric_full (the bench's 8-rank split):
+    every source on exactly one rank, each rank's sources ascending, source
+    cost within the slack of the mean (plus one source), and the largest
+    closure -- the rows a rank's plan must solve -- well below the
+    contiguous blocks' (which need every rack switch of a fabric block's
+    pods).  A grid keeps its contiguous blocks."""
+    from openr_amd import topology as T
+    from openr_amd.engine import graph_from_lsdb
+    from openr_amd.sharding import AllSourcesLayout, closure_sizes, locality_partition
+
+    topo = T.fabric(10000, full=True)
+    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+    n = len(names)
+    nbrs = [np.unique(col[rp[v]:rp[v + 1]]) for v in range(n)]
+    k = np.array([len(x) for x in nbrs], np.int64)
+    cost = k + AllSourcesLayout.ROW_COST
+    for world in (2, 4, 8):
+        parts = locality_partition(nbrs, cost, world)
+        allv = np.concatenate(parts)
+        assert sorted(allv.tolist()) == list(range(n))
+        assert all(np.all(np.diff(p.astype(np.int64)) > 0) for p in parts)
+        load = [int(cost[p].sum()) for p in parts]
+        assert max(load) <= cost.sum() / world * 1.03 + cost.max()
+        lay = AllSourcesLayout(k, 10240, world, nbrs=nbrs)
+        cont = closure_sizes(AllSourcesLayout(k, 10240, world).srcs, nbrs, n)
+        assert lay.partition == "locality" and max(lay.closure) < 0.75 * max(cont)
+    gt = T.grid(30)
+    names, rp, col, met, lid, ovl = graph_from_lsdb(gt.lsdb)
+    nb = [np.unique(col[rp[v]:rp[v + 1]]) for v in range(len(names))]
+    lay = AllSourcesLayout(np.array([len(x) for x in nb]), 1024, 4, nbrs=nb)
+    assert lay.partition in ("contiguous", "locality")
+    assert sorted(np.concatenate(lay.srcs).tolist()) == list(range(len(names)))
 
 
 def test_all_sources_layout_blocks_balance_next_hop_work():
@@ -338,7 +378,7 @@ def test_all_sources_layout_blocks_balance_next_hop_work():
 
 
 def _resident_worker(rank, world, port, q):
-    """bench.py's resident mode: rank r solves its contiguous block, digests
+    """bench.py's resident mode: rank r solves its share of the sources, digests
     its own rows (the oracle's digest_planar over the engine's output layout
     standing in for spf_plan_digest), rank 0 gathers the digests
     (gather_padded) and reassembles them with the layout."""
@@ -362,8 +402,9 @@ def _resident_worker(rank, world, port, q):
         topo = T.fabric_rtt(num_sws=700)
         names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
         n = len(names)
-        k = np.array([len({int(c) for c in col[rp[v]:rp[v + 1]]}) for v in range(n)], np.int64)
-        layout = AllSourcesLayout(k, 1024, world)
+        nbrs = [np.unique(col[rp[v]:rp[v + 1]]) for v in range(n)]
+        k = np.array([len(x) for x in nbrs], np.int64)
+        layout = AllSourcesLayout(k, 1024, world, nbrs=nbrs)  # bench.py's layout
         orc = OracleLinkState()
         orc.update_packed(topo.lsdb)
         table = NameTable(names)
