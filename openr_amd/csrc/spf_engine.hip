@@ -841,29 +841,30 @@ __device__ __forceinline__ uint32_t eq_mask16(const uint4& a, const uint4& t) {
   return x ^ d ^ (d << 6);
 }
 
-// Weighted narrow match: byte targets d_s(v) - w of the lane's 16
-// destinations (word q, byte b = destination 4q + b) and the mask of those
-// with a target at all, in eq_mask16's bit order: d_s(v) >= w (v is neither
-// the source nor closer than the link) and d_s(v) < 254 (the wave takes the
-// exact u32 path when any byte of its source slice saturated).  A neighbour
-// byte equals a valid target (< 254) only if it is that exact distance.
-__device__ __forceinline__ uint32_t weighted_targets16(const uint4& raw, uint32_t w, uint4* t) {
-  const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
-  uint32_t tt[4], valid = 0;
+// Weighted narrow match without per-neighbour targets: bit n (eq_mask16's
+// order) set iff a_n + w == s_n for the neighbour's byte a_n and the
+// source's byte s_n, bytes split into 16-bit halves so the add cannot carry
+// (SWAR: ~12 ops per 4 destinations where deriving targets d_s - w per
+// neighbour cost ~100 per 16).  No false matches: a = 255 (unreachable,
+// drained neighbour's dead row) or 254 (saturated) sums past every
+// unsaturated source byte; s = 255 needs a finite a only through a drained
+// x, whose row is the dead row; s = 0 (the source) needs w = 0.  w >= 254
+// matches nothing in the fast path (the source bytes stay below 254).
+__device__ __forceinline__ uint32_t weighted_mask16(const uint4& a4, const uint32_t (&sl)[4],
+                                                    const uint32_t (&sh)[4], uint32_t w) {
+  if (w >= 0xFEu) return 0u;
+  const uint32_t W2 = w * 0x00010001u;
+  const uint32_t a[4] = {a4.x, a4.y, a4.z, a4.w};
+  uint32_t m = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    uint32_t o = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t x = (rw[q] >> (8 * b)) & 0xFFu;
-      const bool ok = x >= w && x < 0xFEu;
-      o |= (ok ? x - w : 0xFEu) << (8 * b);
-      valid |= (uint32_t)ok << (4 * q + b);
-    }
-    tt[q] = o;
+    const uint32_t xl = ((a[q] & 0x00FF00FFu) + W2) ^ sl[q];
+    const uint32_t xh = (((a[q] >> 8) & 0x00FF00FFu) + W2) ^ sh[q];
+    const uint32_t zl = ~(((xl & 0x7FFF7FFFu) + 0x7FFF7FFFu) | xl) & 0x80008000u;  // bytes 0, 2
+    const uint32_t zh = ~(((xh & 0x7FFF7FFFu) + 0x7FFF7FFFu) | xh) & 0x80008000u;  // bytes 1, 3
+    m |= (((zl >> 15) & 1u) | ((zh >> 14) & 2u) | ((zl >> 29) & 4u) | ((zh >> 28) & 8u)) << (4 * q);
   }
-  *t = make_uint4(tt[0], tt[1], tt[2], tt[3]);
-  return valid;
+  return m;
 }
 
 // nb_row[nb_row_off[i] + j]: byte offset in Dn (row * npitch) of the narrow
@@ -939,6 +940,16 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
     const bool st = cbase / 16 + lane < pitch / 16;
     const uint32_t loff = lane * 16;
     const uint8_t* dn_c = Dn + cbase;
+    // weighted: the source's bytes as 16-bit halves (weighted_mask16)
+    uint32_t ssl[4], ssh[4];
+    {
+      const uint32_t rw[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ssl[q] = rw[q] & 0x00FF00FFu;
+        ssh[q] = (rw[q] >> 8) & 0x00FF00FFu;
+      }
+    }
     // unconditional loads (drained neighbours and list padding point at the
     // all-0xFF dead row), so the waits count exactly: group B's loads stay in
     // flight while group A is matched
@@ -953,10 +964,8 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
       for (int u = 0; u < kEcmpUnroll; ++u) {
         if (j0 + u >= k) break;
         uint32_t m;
-        if (weighted) {  // wave-uniform: targets d_s - w(s, x) per neighbour
-          uint4 tw;
-          const uint32_t valid = weighted_targets16(raw, nb_w[nb0 + j0 + u], &tw);
-          m = eq_mask16(r[u], tw) & valid;
+        if (weighted) {  // wave-uniform: d_x + w(s, x) == d_s, byte-wise
+          m = weighted_mask16(r[u], ssl, ssh, nb_w[nb0 + j0 + u]);
         } else {
           m = eq_mask16(r[u], tg);
         }
