@@ -47,6 +47,31 @@ struct DevBuf {
   }
 };
 
+// Pinned host staging (hipHostMalloc): device-to-host copies at PCIe rate
+// instead of the runtime's chunked pageable path.
+template <typename T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  ~PinBuf() { reset(); }
+  void reset() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    reset();
+    const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T),
+                                       hipHostMallocDefault);
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+};
+
 // exact_spf_kernel scratch (exact.hip): per-wave heap, labels, next hops.
 struct ExactScratch {
   DevBuf<uint8_t> buf;
@@ -112,6 +137,7 @@ struct spf_ctx {
   spfi::DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
   spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
+  spfi::DevBuf<unsigned long long> d_pred_key;
   spfi::DevBuf<uint32_t> d_gq, d_gq2, d_gbm, d_gctr;  // global-memory SSSP scratch
   spfi::DevBuf<uint32_t> d_gbar;  // its grid-barrier counters (whatif.hip XGrid)
   // per-node eccentricity estimates (planes BFS batch order), for ecc_epoch
@@ -125,6 +151,9 @@ struct spf_ctx {
   bool mp_redo = true;
   uint64_t mp_epoch = ~0ull;
   spfi::DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
+  // spf_plan_preds' pinned staging: lives with the context (the facade makes
+  // a plan per query; pinning per plan cost more than it saved)
+  spfi::PinBuf<uint32_t> pin_preds;
 };
 
 struct spf_plan {
@@ -158,6 +187,7 @@ struct spf_plan {
   spfi::DevBuf<uint8_t> d_Dn;
   spfi::DevBuf<uint32_t> d_S, d_maxd;  // sliced rows (+ dead row); deepest BFS level + 8 counters
   spfi::DevBuf<uint32_t> d_units, d_unit_off;  // sliced pass: uint4 work units per XCD
+  spfi::DevBuf<uint32_t> d_gtab;  // sliced pass: source groups ([n, sources...] each)
   uint32_t max_xcd_units = 0;
   bool big = false;  // spf_big_kernel (whatif.hip): graphs beyond the LDS kernels
   spfi::DevBuf<uint32_t> b_q, b_q2, b_bm, b_ctr, b_nbr_bit, b_nhb, b_lvl, b_order, b_misc, b_parent;
@@ -170,6 +200,7 @@ struct spf_plan {
   spfi::DevBuf<uint32_t> h_dist, h_nh;  // spf_plan_execute_host staging
   uint64_t h_epoch = ~0ull;              // graph epoch of the rows in h_dist
   spfi::DevBuf<uint32_t> h_pcnt, h_pedge;  // spf_plan_preds scratch
+  spfi::DevBuf<unsigned long long> h_pkey;  // ... its sort keys
   size_t slots = 0;
   size_t lds_bytes = 0;
   bool q16 = true;

@@ -1135,8 +1135,11 @@ spf_status ls_prefetch_spf_results(ls_state* ls, const char* const* nodes, uint3
   ls->phase_ns[1] += t0 - t1;
   std::vector<uint32_t> pred_ptr((size_t)m * (N + 1));
   uint64_t npred = 0;
-  std::vector<uint32_t> pred_edge((size_t)m * ls->col.size() + 1);  // every in-edge at most once per source
-  st = spf_plan_preds(plan.get(), pred_ptr.data(), pred_edge.data(), pred_edge.size(), &npred);
+  // every in-edge at most once per source; left uninitialised (8 MB of
+  // zeroing for a fabric's me + 8 neighbours otherwise)
+  const size_t pred_cap = (size_t)m * ls->col.size() + 1;
+  std::unique_ptr<uint32_t[]> pred_edge(new uint32_t[pred_cap]);
+  st = spf_plan_preds(plan.get(), pred_ptr.data(), pred_edge.get(), pred_cap, &npred);
   if (st != SPF_OK) return eng_fail(ls, st);
   t1 = now_ns();
   ls->phase_ns[2] += t1 - t0;
@@ -1154,7 +1157,7 @@ spf_status ls_prefetch_spf_results(ls_state* ls, const char* const* nodes, uint3
     // csr-indexed predecessor lists of this source, offsets rebased to 0
     e.pred_ptr.resize(N + 1);
     for (uint32_t v = 0; v <= N; ++v) e.pred_ptr[v] = pp[v] - pp[0];
-    e.pred_edge.assign(pred_edge.begin() + pp[0], pred_edge.begin() + pp[N]);
+    e.pred_edge.assign(pred_edge.get() + pp[0], pred_edge.get() + pp[N]);
     fill_memo(ls, e.dist.data(), none, nh.data() + nh_off[i], kk[i], wpm, nbrs[i],
               e.pred_ptr.data(), e.pred_edge.data(), e);
     e.pending = 1;

@@ -35,6 +35,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -1208,6 +1209,82 @@ __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_
   }
 }
 
+// Grouped match (sources with identical neighbour lists: a pod's rack
+// switches, a plane's spines): the group's source planes of one 64-word chunk
+// stay in registers and every neighbour row is loaded once for all of them
+// (the per-source pass loads it once per source -- the next-hop pass is
+// bound by those L2 reads).  gs <= kSlGroup sources; lane = output word w.
+constexpr uint32_t kSlGroup = 8;
+template <int P>
+__device__ __forceinline__ void grouped_pass(__amdgpu_buffer_rsrc_t rs, uint32_t* __restrict__ nh,
+                                             const uint64_t* __restrict__ nh_off,
+                                             const uint32_t* __restrict__ row_of,
+                                             const uint32_t* __restrict__ req_src,
+                                             const uint32_t* __restrict__ gm, uint32_t gs,
+                                             uint32_t wpm, const uint32_t* __restrict__ offs,
+                                             uint32_t j0, uint32_t j1, uint32_t w, bool live) {
+  const uint32_t wpb = w * P * 4;
+  uint32_t t[kSlGroup][P], valid[kSlGroup];
+  uint32_t* out[kSlGroup];
+#pragma unroll
+  for (uint32_t q = 0; q < kSlGroup; ++q) {
+    valid[q] = 0;
+    out[q] = nh;
+#pragma unroll
+    for (int b = 0; b < P; ++b) t[q][b] = 0;
+    if (q < gs) {
+      const uint32_t i = gm[q];
+      out[q] = nh + nh_off[i];
+      Planes<P> sv;
+      bload<P>(sv.v, rs, wpb, row_of[req_src[i]] * kSlSlots * wpm * 4);
+      uint32_t ones = ~0u, zeros = ~0u, borrow = ~0u;
+#pragma unroll
+      for (int b = 0; b < P; ++b) {
+        const uint32_t x = sv.v[b];
+        ones &= x;
+        zeros &= ~x;
+        t[q][b] = x ^ borrow;  // t = d_s - 1
+        borrow &= ~x;
+      }
+      valid[q] = ~(ones | zeros);
+    }
+  }
+  // two groups of 4 neighbour rows in flight (row offset lists are padded:
+  // loads past j1 read the dead row)
+  constexpr int U = 4;
+  offs += j0;
+  const uint32_t k = j1 - j0;
+  auto load_group = [&](uint32_t jj, Planes<P> (&r)[U]) {
+    const uint4 o4 = *reinterpret_cast<const uint4*>(offs + jj);
+    const uint32_t o[U] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+    for (int v = 0; v < U; ++v) bload<P>(r[v].v, rs, wpb, o[v] * 4);
+  };
+  auto match_group = [&](uint32_t jj, const Planes<P> (&r)[U]) {
+#pragma unroll
+    for (int v = 0; v < U; ++v) {
+      if (jj + v >= k) break;
+      const size_t at = (size_t)(j0 + jj + v) * wpm + w;
+#pragma unroll
+      for (uint32_t q = 0; q < kSlGroup; ++q) {
+        if (q >= gs) break;  // wave-uniform
+        uint32_t diff = 0;
+#pragma unroll
+        for (int b = 0; b < P; ++b) diff |= r[v].v[b] ^ t[q][b];
+        if (live) out[q][at] = ~diff & valid[q];
+      }
+    }
+  };
+  Planes<P> ra[U], rb[U];
+  load_group(0, ra);
+  for (uint32_t jj = 0; jj < k; jj += 2 * U) {
+    load_group(jj + U, rb);
+    match_group(jj, ra);
+    load_group(jj + 2 * U, ra);
+    match_group(jj + U, rb);
+  }
+}
+
 // Work units: (source i, chunks [c0, c1) of 64 words, neighbours [j0, j1)),
 // at most about kSlUnit neighbour-chunk matches each (spf_plan_create keeps
 // light sources whole and cuts heavy ones per chunk and neighbour range),
@@ -1228,7 +1305,8 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     const uint32_t* __restrict__ nb_w, const uint32_t* __restrict__ nb_row,
     const uint32_t* __restrict__ nb_row_off, const uint32_t* __restrict__ nb_drained,
     uint32_t dead, uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
-    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off, uint32_t s_bytes,
+    const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off,
+    const uint32_t* __restrict__ gtab /* group units: [n, sources...] */, uint32_t s_bytes,
     uint32_t fixed_p /* rows sliced by the BFS itself (sdirect): P planes, maxd unused */) {
   const uint32_t md = fixed_p ? 0u : *maxd;
   const uint32_t g = blockIdx.x & 7;  // this block's XCD (round-robin placement)
@@ -1243,9 +1321,9 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
   const uint32_t t = (blockIdx.x >> 3) * kEcmpWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t u_begin = unit_off[g];
   if (t >= unit_off[g + 1] - u_begin) return;  // whole wave: no barriers below
-  {
-    const uint4 u = units[u_begin + t];
-    const uint32_t i = u.x, c0 = u.y & 0xFFFFu, c1 = u.y >> 16, j0 = u.z, j1 = u.w;
+  // one source's units: chunks [c0, c1), neighbours [j0, j1)
+  auto single = [&](const uint32_t i, const uint32_t c0, const uint32_t c1, const uint32_t j0,
+                    const uint32_t j1) {
     const uint32_t s = req_src[i];
     const uint32_t nb0 = nb_ptr[s], k = j1 - j0;
     const uint32_t srow = row_of[s];
@@ -1300,7 +1378,25 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
         }
       }
     }
+  };
+  const uint4 u = units[u_begin + t];
+  if (u.y >> 31) {  // a group unit: sources with identical neighbour lists, one chunk
+    const uint32_t* gm = gtab + u.x + 1;
+    const uint32_t gs = __builtin_amdgcn_readfirstlane(gtab[u.x]), c = u.y & 0xFFFFu;
+    const uint32_t* offs = nb_row + nb_row_off[gm[0]];  // the same list for every member
+    const uint32_t w = c * 64 + lane;
+    const bool live = w < wpm;
+    switch (P) {
+      case 1: grouped_pass<1>(rs, nh, nh_off, row_of, req_src, gm, gs, wpm, offs, u.z, u.w, w, live); break;
+      case 2: grouped_pass<2>(rs, nh, nh_off, row_of, req_src, gm, gs, wpm, offs, u.z, u.w, w, live); break;
+      case 3: grouped_pass<3>(rs, nh, nh_off, row_of, req_src, gm, gs, wpm, offs, u.z, u.w, w, live); break;
+      case 4: grouped_pass<4>(rs, nh, nh_off, row_of, req_src, gm, gs, wpm, offs, u.z, u.w, w, live); break;
+      default:  // deeper planes or saturated rows: member by member
+        for (uint32_t q = 0; q < gs; ++q) single(gm[q], c, c + 1, u.z, u.w);
+    }
+    return;
   }
+  single(u.x, u.y & 0xFFFFu, u.y >> 16, u.z, u.w);
 }
 
 // ---------------------------------------------------------------------------
@@ -1396,7 +1492,8 @@ __global__ void preds_kernel(const uint32_t* __restrict__ dist0,  // [n_src][pit
                              const uint32_t* __restrict__ srcs,  // [n_src] (blockIdx.y)
                              uint32_t N, uint32_t hop,
                              uint32_t* __restrict__ cnt_or_ptr0,  // [n_src][N + 1]
-                             uint32_t* __restrict__ pred_edge) {
+                             uint32_t* __restrict__ pred_edge,
+                             unsigned long long* __restrict__ pred_key /* PASS 1: sort keys */) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= N) return;
   const uint32_t* dist = dist0 + (size_t)blockIdx.y * pitch;
@@ -1415,16 +1512,19 @@ __global__ void preds_kernel(const uint32_t* __restrict__ dist0,  // [n_src][pit
       if (du == kInf) continue;
       if (du + (hop ? 1u : wt[r]) != dv) continue;
       if (PASS) {
-        // insertion into the sorted segment [base, base+n)
+        // insertion into the sorted segment [base, base+n) by (dist of the
+        // tail, edge id), the keys kept beside the edges (one load per step
+        // where re-deriving a key was three dependent loads)
+        const unsigned long long key = ((unsigned long long)du << 32) | r;
         uint32_t p = base + n;
         while (p > base) {
-          const uint32_t pe = pred_edge[p - 1];
-          const uint32_t pu = col[rev[pe]];  // tail of edge pe
-          const uint32_t pd = dist[pu];
-          if (pd < du || (pd == du && pe < r)) break;
-          pred_edge[p] = pe;
+          const unsigned long long pk = pred_key[p - 1];
+          if (pk < key) break;
+          pred_key[p] = pk;
+          pred_edge[p] = (uint32_t)pk;
           --p;
         }
+        pred_key[p] = key;
         pred_edge[p] = r;
       }
       ++n;
@@ -2129,13 +2229,48 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       const uint32_t fill = (uint32_t)std::min<uint64_t>(
           kSlUnit, std::max<uint64_t>(16, matches / (16ull * c->n_cu) / 8 * 8));
       const uint32_t unit = ue ? (uint32_t)atoi(ue) : fill;
-      std::vector<uint32_t> units, unit_off(9, 0);
+      std::vector<uint32_t> units, unit_off(9, 0), gtab;
+      // sources of one XCD list with identical neighbour rows and no drained
+      // neighbour (a pod's rack switches, a plane's spines) form groups of up
+      // to kSlGroup: one wave loads each neighbour row once for the group
+      // (SPF_SLICED_GROUP=0: A/B)
+      const char* ge = std::getenv("SPF_SLICED_GROUP");
+      const bool grouping = !(ge && ge[0] == '0');
+      std::vector<int32_t> leader_of(n_src, -1);  // >= 0: gtab offset, -2: member
       p->max_xcd_units = 0;
       for (int g = 0; g < 8; ++g) {
         unit_off[g] = (uint32_t)(units.size() / 4);
+        if (grouping) {
+          std::map<std::vector<uint32_t>, std::vector<uint32_t>> same;
+          for (uint32_t i : lists[g])
+            if (p->words[i] && !nb_drained[i])
+              same[std::vector<uint32_t>(nb_row.begin() + nb_row_off[i],
+                                         nb_row.begin() + nb_row_off[i] + p->words[i])]
+                  .push_back(i);
+          for (auto& kv : same)
+            for (size_t a = 0; a + 1 < kv.second.size(); a += kSlGroup) {
+              const size_t b = std::min(kv.second.size(), a + kSlGroup);
+              leader_of[kv.second[a]] = (int32_t)gtab.size();
+              gtab.push_back((uint32_t)(b - a));
+              for (size_t q = a; q < b; ++q) {
+                gtab.push_back(kv.second[q]);
+                if (q > a) leader_of[kv.second[q]] = -2;
+              }
+            }
+        }
         for (uint32_t i : lists[g]) {
           const uint32_t k = p->words[i];
-          if (k == 0) continue;
+          if (k == 0 || leader_of[i] == -2) continue;
+          if (leader_of[i] >= 0) {  // per chunk, ranges of about `unit` matches
+            const uint32_t gs = gtab[leader_of[i]];
+            const uint32_t parts = (uint32_t)(((uint64_t)k * gs + unit - 1) / unit);
+            const uint32_t jstep = ((k + parts - 1) / parts + 7) / 8 * 8;
+            for (uint32_t ch = 0; ch < chunks; ++ch)
+              for (uint32_t j = 0; j < k; j += jstep)
+                units.insert(units.end(), {(uint32_t)leader_of[i], ch | (1u << 31), j,
+                                           std::min(k, j + jstep)});
+            continue;
+          }
           if ((uint64_t)k * chunks <= unit) {
             units.insert(units.end(), {i, 0u | (chunks << 16), 0u, k});
             continue;
@@ -2154,6 +2289,8 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       if (units.empty()) units.assign(4, 0);
       HIP_TRY(c, p->d_units.upload(units.data(), units.size(), c->stream));
       HIP_TRY(c, p->d_unit_off.upload(unit_off.data(), 9, c->stream));
+      if (gtab.empty()) gtab.push_back(0);
+      HIP_TRY(c, p->d_gtab.upload(gtab.data(), gtab.size(), c->stream));
     }
     size_t most = 0;
     for (auto& l : lists) most = std::max(most, l.size());
@@ -2270,7 +2407,14 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
     *ecmp_bytes = 0;
     return SPF_OK;
   }
-  if (p->ms) {
+  if (p->tm_G) {  // team BFS: each batch sweeps the column stream once (column + meta
+                  // words); rows written: u32 for the prefix when direct, u8 or planes
+    const uint64_t batches = (rows + p->tm_bs - 1) / p->tm_bs;
+    const bool direct = p->prefix && !p->direct && p->narrow;
+    const uint64_t wbytes = 4ull * (c->pitch / 32);
+    bfs = batches * (8ull * c->sell_ptr.back() + N) + (direct ? p->n_src : rows) * c->pitch * 4ull +
+          (p->sdirect ? rows * kTeamPlanes * wbytes : p->narrow ? rows * c->npitch : 0ull);
+  } else if (p->ms) {
     const bool planes = use_planes(c);
     const uint32_t batch = planes ? kPlBatch : kMsBatch;
     const uint64_t rounds = (rows + (uint64_t)batch * c->n_cu - 1) / ((uint64_t)batch * c->n_cu);
@@ -2293,9 +2437,14 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
   *bfs_bytes = bfs;
   if (p->sliced && p->nh_total) {
     // planes in use: from the last execute's deepest level (one 4-byte read)
+    // (sdirect: kTeamPlanes planes written by the BFS itself, no slicing pass)
+    const uint64_t wbytes = 4ull * (c->pitch / 32);
+    if (p->sdirect) {
+      *ecmp_bytes = rows * kTeamPlanes * wbytes + 4ull * p->nh_total;
+      return SPF_OK;
+    }
     uint32_t md = 0;
     HIP_TRY(p->ctx, hipMemcpy(&md, p->d_maxd.p, 4, hipMemcpyDeviceToHost));
-    const uint64_t wbytes = 4ull * (c->pitch / 32);
     const uint64_t expand = p->expand ? rows * 4ull * c->pitch : 0ull;  // u32 rows written
     if (md < kSlSat) {
       const uint64_t P = 32u - __builtin_clz(md + 1u);
@@ -2518,7 +2667,7 @@ spf_status launch_ecmp_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool h
                      p->d_maxd.p, D, c->pitch, p->d_srcs.p, p->d_row_of.p,
                      c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p,
                      p->d_nb_drained.p, p->dead, hop ? 1u : 0u, p->d_nh_off.p, d_nh,
-                     reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p,
+                     reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p, p->d_gtab.p,
                      (uint32_t)(p->d_S.n * 4), p->sdirect ? kTeamPlanes : 0u);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
@@ -2616,7 +2765,8 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
   uint32_t* D = (p->direct || team_direct) ? d_dist : p->d_D.p;
   const uint32_t rows = (uint32_t)p->closure.size();
   const bool sliced = p->sliced && p->nh_total;
-  if (sliced) HIP_TRY(c, hipMemsetAsync(p->d_maxd.p, 0, 4, s));  // msbfs_kernel's atomicMax target
+  if (sliced && !p->sdirect)  // msbfs_kernel's atomicMax target (sdirect plans: planes fixed)
+    HIP_TRY(c, hipMemsetAsync(p->d_maxd.p, 0, 4, s));
   hipEvent_t* ev = nullptr;
   if (p->timing_cap) {
     ev = &p->ev[4 * (p->timing_n % p->timing_cap)];
@@ -2754,7 +2904,9 @@ spf_status spf_plan_execute_host(spf_plan* p, uint32_t* dist_out, uint32_t* nh_o
     HIP_TRY(c, hipMemcpyAsync(nh_out, p->h_nh.p, p->nh_total * 4, hipMemcpyDeviceToHost, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return p->big ? spf_device_check(c) : SPF_OK;
+  // grid-resident kernels (spf_big_kernel, the team BFS) report a barrier
+  // that gave up (blocks not co-resident) here instead of wrong rows
+  return (p->big || p->tm_G) ? spf_device_check(c) : SPF_OK;
 }
 
 spf_status spf_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
@@ -2868,7 +3020,8 @@ spf_status spf_preds(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* i
   HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
   hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, c->d_row.p, N, c->d_row_ptr.p,
                      c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign,
-                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, (uint32_t*)nullptr);
+                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, (uint32_t*)nullptr,
+                     (unsigned long long*)nullptr);
   HIP_TRY(c, hipGetLastError());
   std::vector<uint32_t> cnt(N);
   HIP_TRY(c, hipMemcpyAsync(cnt.data(), c->d_pred_cnt.p, 4ull * N, hipMemcpyDeviceToHost, c->stream));
@@ -2880,9 +3033,11 @@ spf_status spf_preds(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* i
   if (cap < pred_ptr[N]) return fail(c, SPF_E_INVALID, "pred_edge capacity %u < %u", cap, pred_ptr[N]);
   HIP_TRY(c, hipMemcpyAsync(c->d_pred_cnt.p, pred_ptr, 4ull * N, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, c->d_pred_edge.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
+  HIP_TRY(c, c->d_pred_key.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
   hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, c->d_row.p, N, c->d_row_ptr.p,
                      c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign,
-                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, c->d_pred_edge.p);
+                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, c->d_pred_edge.p,
+                     c->d_pred_key.p);
   HIP_TRY(c, hipGetLastError());
   if (pred_ptr[N])
     HIP_TRY(c, hipMemcpyAsync(pred_edge, c->d_pred_edge.p, 4ull * pred_ptr[N], hipMemcpyDeviceToHost,
@@ -2908,10 +3063,13 @@ spf_status spf_plan_preds(spf_plan* p, uint32_t* pred_ptr, uint32_t* pred_edge, 
   const dim3 g((N + 255) / 256, n), b(256);
   hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, p->h_dist.p, c->pitch, c->d_row_ptr.p,
                      c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, nullptr,
-                     p->d_srcs.p, N, hop ? 1u : 0u, p->h_pcnt.p, (uint32_t*)nullptr);
+                     p->d_srcs.p, N, hop ? 1u : 0u, p->h_pcnt.p, (uint32_t*)nullptr,
+                     (unsigned long long*)nullptr);
   HIP_TRY(c, hipGetLastError());
-  HIP_TRY(c, hipMemcpyAsync(pred_ptr, p->h_pcnt.p, 4ull * slots, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, c->pin_preds.alloc(slots));
+  HIP_TRY(c, hipMemcpyAsync(c->pin_preds.p, p->h_pcnt.p, 4ull * slots, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::memcpy(pred_ptr, c->pin_preds.p, 4ull * slots);
   // counts -> absolute offsets: source i's list of v starts at pred_ptr[i*(N+1) + v],
   // pred_ptr[i*(N+1) + N] = the end of source i's lists
   uint64_t at = 0;
@@ -2929,15 +3087,20 @@ spf_status spf_plan_preds(spf_plan* p, uint32_t* pred_ptr, uint32_t* pred_edge, 
   if (!pred_edge) return SPF_OK;
   if (cap < at) return fail(c, SPF_E_NOMEM, "spf_plan_preds: capacity %llu < %llu",
                             (unsigned long long)cap, (unsigned long long)at);
-  HIP_TRY(c, hipMemcpyAsync(p->h_pcnt.p, pred_ptr, 4ull * slots, hipMemcpyHostToDevice, c->stream));
+  // one staging buffer for the upload and the edges (sized before either copy)
+  HIP_TRY(c, c->pin_preds.alloc(std::max<uint64_t>(slots, at)));
+  std::memcpy(c->pin_preds.p, pred_ptr, 4ull * slots);
+  HIP_TRY(c, hipMemcpyAsync(p->h_pcnt.p, c->pin_preds.p, 4ull * slots, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, p->h_pedge.alloc(std::max<uint64_t>(at, 1)));
+  HIP_TRY(c, p->h_pkey.alloc(std::max<uint64_t>(at, 1)));
   hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, p->h_dist.p, c->pitch, c->d_row_ptr.p,
                      c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, nullptr,
-                     p->d_srcs.p, N, hop ? 1u : 0u, p->h_pcnt.p, p->h_pedge.p);
+                     p->d_srcs.p, N, hop ? 1u : 0u, p->h_pcnt.p, p->h_pedge.p, p->h_pkey.p);
   HIP_TRY(c, hipGetLastError());
   if (at)
-    HIP_TRY(c, hipMemcpyAsync(pred_edge, p->h_pedge.p, 4ull * at, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->pin_preds.p, p->h_pedge.p, 4ull * at, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (at) std::memcpy(pred_edge, c->pin_preds.p, 4ull * at);
   return SPF_OK;
 }
 

@@ -62,7 +62,11 @@ class DeviceArray:
         return self.n * self.dtype.itemsize
 
     def zero(self) -> None:
+        """Zero the buffer and wait for it: hipMemset runs on the null stream,
+        which the engine's non-blocking streams do not wait for (an unfinished
+        memset overwrote a plan's first next-hop bitmaps once)."""
         _check(_lib.hipMemset(C.c_void_p(self.ptr), 0, max(1, self.nbytes)), "hipMemset")
+        synchronize()
 
     def numpy(self) -> np.ndarray:
         out = np.empty(self.n, self.dtype)
