@@ -147,6 +147,7 @@ struct spf_ctx {
   uint64_t dbound_epoch = ~0ull;
   // mssp_kernel tables (mssp.hip), valid for graph epoch mp_epoch
   spfi::DevBuf<uint32_t> d_mp_ell, d_mp_smap;
+  spfi::DevBuf<uint32_t> d_mp_dep;  // per slice: the slices its nodes' out-edges reach (CSR)
   uint32_t mp_slots = 0, mp_ovf_at = 0;
   bool mp_redo = true;
   uint64_t mp_epoch = ~0ull;

@@ -98,7 +98,8 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     const uint32_t* __restrict__ col, const uint32_t* __restrict__ wt,
     const uint8_t* __restrict__ ovl, const uint32_t* __restrict__ rows_src, uint32_t n_rows,
     uint32_t N, uint32_t pitch, uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
-    uint32_t ovf_at, uint32_t* __restrict__ redo,
+    uint32_t ovf_at, uint32_t* __restrict__ redo, uint32_t alt,
+    const uint32_t* __restrict__ dep /* [n_slices + 1] offsets, then out-slice lists; null: no skipping */,
     unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */) {
   constexpr uint32_t S = 2 * SD;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -106,6 +107,8 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
   uint32_t* dist = reinterpret_cast<uint32_t*>(smem);  // [(N + 1) * SD]
   uint32_t* bits = dist + (size_t)(N + 1) * SD;          // [3][bw]
   uint32_t* flag = bits + 3 * bw;                        // [3]
+  const uint32_t n_slices = (N + 63) / 64, sw = (n_slices + 31) / 32;
+  uint32_t* sbits = flag + 4;                            // [3][sw]: slices to sweep
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t r0 = blockIdx.x * S;
@@ -113,6 +116,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 
   for (uint32_t i = tid; i < (N + 1) * SD; i += kMpThreads) dist[i] = 0xFFFFFFFFu;
   for (uint32_t i = tid; i < 3 * bw; i += kMpThreads) bits[i] = 0;
+  for (uint32_t i = tid; i < 3 * sw; i += kMpThreads) sbits[i] = 0;
   if (tid < 3) flag[tid] = 0;
   __syncthreads();
   if (tid < nb) lds_min16(&dist[rows_src[r0 + tid] * SD + tid / 2], tid & 1, 0);
@@ -132,38 +136,56 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 
   // the lane's drained bit of each of its wave's slots (bit k), once: the
   // sweeps test it without a global load
-  uint32_t dmask = 0;
+  uint32_t dmask = 0, n_my = 0;  // + the wave's slot count (filled from the front)
   {
     const uint32_t* wm = smap + __builtin_amdgcn_readfirstlane(wave) * slots;
-    for (uint32_t k = 0; k < slots && k < 32; ++k) {
+    for (uint32_t k = 0; k < slots; ++k) {
       const uint32_t sl = wm[k];
       if (sl == kMpNoSlice) break;
+      n_my = k + 1;
       const uint32_t v = sl * 64 + lane;
-      if (v < N && ovl[v]) dmask |= 1u << k;
+      if (k < 32 && v < N && ovl[v]) dmask |= 1u << k;
     }
+    n_my = __builtin_amdgcn_readfirstlane(n_my);
   }
   for (uint32_t it = 0;; ++it) {
     const uint32_t* cur = bits + (it % 3) * bw;
     uint32_t* nxt = bits + ((it + 1) % 3) * bw;
     uint32_t* old = bits + ((it + 2) % 3) * bw;  // read by nobody this sweep
     for (uint32_t i = tid; i < bw; i += kMpThreads) old[i] = 0;
+    // slice-level dirt (dep != null): a slice is swept when one of its
+    // in-neighbours changed in the previous sweep or this one (every slice in
+    // the first sweep); a slice with a decreased non-drained node marks the
+    // slices its out-edges reach
+    const uint32_t* scur = sbits + (it % 3) * sw;
+    uint32_t* snxt = sbits + ((it + 1) % 3) * sw;
+    for (uint32_t i = tid; i < sw; i += kMpThreads) sbits[((it + 2) % 3) * sw + i] = 0;
     if (tid == 0) flag[(it + 1) % 3] = 0;
     bool changed = false;
     // the wave's slot table by scalar loads, the next slot's entry fetched
     // while this slot's columns run (a dependent smap -> sell_ptr chain per
     // slot was ~2 us of every sweep's critical path)
     const uint32_t* wmap = smap + __builtin_amdgcn_readfirstlane(wave) * slots;
-    uint32_t nsl = wmap[0];
+    // odd sweeps walk the wave's slots backwards (narrow slices first): a
+    // forward sweep carries paths whose hops go from wide to narrow nodes
+    // (spine -> fabric -> rack switch), a backward one the opposite turns
+    const bool back = alt && (it & 1u);
+    auto slot_at = [&](uint32_t k) { return back ? n_my - 1u - k : k; };
+    uint32_t nsl = n_my ? wmap[slot_at(0)] : kMpNoSlice;
     uint32_t nb0 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl], nb1 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl + 1];
-    for (uint32_t k = 0; k < slots; ++k) {
+    for (uint32_t kk = 0; kk < n_my; ++kk) {
+      const uint32_t k = slot_at(kk);
       const uint32_t sl = nsl;
-      if (sl == kMpNoSlice) break;  // a wave's slots are filled from the front
       const uint32_t b = nb0, w = (nb1 - nb0) / 64;
-      nsl = k + 1 < slots ? wmap[k + 1] : kMpNoSlice;
+      nsl = kk + 1 < n_my ? wmap[slot_at(kk + 1)] : kMpNoSlice;
       if (nsl != kMpNoSlice) {
         nb0 = sell_ptr[nsl];
         nb1 = sell_ptr[nsl + 1];
       }
+      if (dep && it > 0 &&
+          !(__builtin_amdgcn_readfirstlane(scur[sl >> 5] | snxt[sl >> 5]) >> (sl & 31) & 1u))
+        continue;  // no in-neighbour changed since this slice's last sweep
+      if (stats && lane == 0) atomicAdd(&stats[3], 1ull);  // slices swept (diagnostics)
       const uint32_t v = sl * 64 + lane;
       uint32_t acc[SD];
 #pragma unroll
@@ -215,6 +237,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
           fold(eb, w - j0 - kMpAhead);
         }
       }
+      bool expands = false;
       if (got && v < N) {
         uint32_t* dv = &dist[v * SD];
         bool dec = false;
@@ -228,7 +251,16 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         }
         if (dec) {
           changed = true;
-          if (k < 32 ? !((dmask >> k) & 1u) : !ovl[v]) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+          expands = k < 32 ? !((dmask >> k) & 1u) : !ovl[v];
+          if (expands) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+        }
+      }
+      // (whole wave: every lane takes its share of the list)
+      if (dep && __builtin_amdgcn_ballot_w64(expands)) {
+        const uint32_t d0 = dep[sl], d1 = dep[sl + 1];
+        for (uint32_t t = d0 + lane; t < d1; t += 64) {
+          const uint32_t o = dep[t];
+          atomicOr(&snxt[o >> 5], 1u << (o & 31));
         }
       }
     }
@@ -276,11 +308,13 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 
 template <int SD>
 size_t mp_lds(uint32_t N) {
-  return 4ull * (N + 1) * SD + 4ull * 3 * ((N + 32) / 32) + 16;
+  return 4ull * (N + 1) * SD + 4ull * 3 * ((N + 32) / 32) + 16 + 4ull * 3 * (((N + 63) / 64 + 31) / 32);
 }
 
 bool mp_fits(uint32_t N, uint32_t sd) {
-  return 4ull * (N + 1) * sd + 4ull * 3 * ((N + 32) / 32) + 16 + kMpStaticLds <= kMpMaxLds;
+  return 4ull * (N + 1) * sd + 4ull * 3 * ((N + 32) / 32) + 16 + 4ull * 3 * (((N + 63) / 64 + 31) / 32) +
+             kMpStaticLds <=
+         kMpMaxLds;
 }
 
 }  // namespace
@@ -334,6 +368,25 @@ spf_status mssp_prepare(spf_ctx* c) {
     smap[(size_t)best * slots + used[best]++] = sl;
     load[best] += std::max(1u, width(sl));
   }
+  // per slice: the other slices its nodes' out-edges reach (the mssp
+  // kernel's slice-level dirt)
+  std::vector<uint32_t> dep(n_slices + 1, 0);
+  {
+    std::vector<std::vector<uint32_t>> outs(n_slices);
+    std::vector<uint32_t> mark(n_slices, kInf);
+    for (uint32_t sl = 0; sl < n_slices; ++sl) {
+      for (uint32_t u = sl * 64; u < std::min(N, sl * 64 + 64); ++u)
+        for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+          const uint32_t o = c->col[e] / 64;
+          if (mark[o] != sl) mark[o] = sl, outs[sl].push_back(o);
+        }
+      std::sort(outs[sl].begin(), outs[sl].end());
+    }
+    for (uint32_t sl = 0; sl < n_slices; ++sl) dep[sl + 1] = dep[sl] + (uint32_t)outs[sl].size();
+    for (uint32_t sl = 0; sl < n_slices; ++sl) dep[sl] += n_slices + 1;
+    dep[n_slices] += n_slices + 1;
+    for (auto& o : outs) dep.insert(dep.end(), o.begin(), o.end());
+  }
   // overflow bound: with no drained node, d(s, v) <= max metric x hops(s, v)
   // <= max metric x 2 ecc(r) for any r of the component (BFS from one node
   // per component); otherwise only the trivial bound (N - 1) x max metric
@@ -364,6 +417,7 @@ spf_status mssp_prepare(spf_ctx* c) {
   c->mp_slots = slots;
   HIP_TRY(c, c->d_mp_ell.upload(ell.data(), ell.size(), c->stream));
   HIP_TRY(c, c->d_mp_smap.upload(smap.data(), smap.size(), c->stream));
+  HIP_TRY(c, c->d_mp_dep.upload(dep.data(), dep.size(), c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->mp_epoch = c->epoch;
   return SPF_OK;
@@ -394,10 +448,14 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   const dim3 g((rows + S - 1) / S), b(kMpThreads);
   const uint32_t N = c->N;
   uint32_t* rd = c->mp_redo ? redo : nullptr;
+  const char* ae = std::getenv("SPF_MSSP_ALT");  // A/B: alternating sweep direction
+  const uint32_t alt = ae ? (uint32_t)atoi(ae) : 0u;
+  const char* ke = std::getenv("SPF_MSSP_SKIP");  // A/B: slice-level dirt (default on)
+  const uint32_t* dep = ke && ke[0] == '0' ? nullptr : c->d_mp_dep.p;
 #define MP_LAUNCH(SDV)                                                                            \
   hipLaunchKernelGGL(mssp_kernel<SDV>, g, b, mp_lds<SDV>(N), s, c->d_sell_ptr.p, c->d_mp_ell.p,   \
                      c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
-                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, c->d_stamps.p)
+                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, alt, dep, c->d_stamps.p)
   switch (sd) {
     case 8: MP_LAUNCH(8); break;
     case 4: MP_LAUNCH(4); break;
