@@ -851,21 +851,29 @@ __device__ __forceinline__ uint32_t eq_mask16(const uint4& a, const uint4& t) {
 // unsaturated source byte; s = 255 needs a finite a only through a drained
 // x, whose row is the dead row; s = 0 (the source) needs w = 0.  w >= 254
 // matches nothing in the fast path (the source bytes stay below 254).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t weighted_mask16(const uint4& a4, const uint32_t (&sl)[4],
                                                     const uint32_t (&sh)[4], uint32_t w) {
   if (w >= 0xFEu) return 0u;
-  const uint32_t W2 = w * 0x00010001u;
+  const u16x2 W2 = {(unsigned short)w, (unsigned short)w};
+  const u16x2 one = {1, 1};
   const uint32_t a[4] = {a4.x, a4.y, a4.z, a4.w};
-  uint32_t m = 0;
+  // per word q: bytes 0, 2 and bytes 1, 3 as 16-bit halves (v_perm), a + w
+  // and the xor with the source's halves packed (v_pk_add_u16), zero halves
+  // -> 1 by a saturating 1 - x (v_pk_sub_u16 clamp); the four result bits
+  // land at 4q, 4q + 1 (bytes 0, 1) and 16 + 4q, 17 + 4q (bytes 2, 3)
+  uint32_t T = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t xl = ((a[q] & 0x00FF00FFu) + W2) ^ sl[q];
-    const uint32_t xh = (((a[q] >> 8) & 0x00FF00FFu) + W2) ^ sh[q];
-    const uint32_t zl = ~(((xl & 0x7FFF7FFFu) + 0x7FFF7FFFu) | xl) & 0x80008000u;  // bytes 0, 2
-    const uint32_t zh = ~(((xh & 0x7FFF7FFFu) + 0x7FFF7FFFu) | xh) & 0x80008000u;  // bytes 1, 3
-    m |= (((zl >> 15) & 1u) | ((zh >> 14) & 2u) | ((zl >> 29) & 4u) | ((zh >> 28) & 8u)) << (4 * q);
+    const u16x2 lo = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, a[q], 0x0c020c00u));
+    const u16x2 hi = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, a[q], 0x0c030c01u));
+    const uint32_t xl = __builtin_bit_cast(uint32_t, (u16x2)(lo + W2)) ^ sl[q];
+    const uint32_t xh = __builtin_bit_cast(uint32_t, (u16x2)(hi + W2)) ^ sh[q];
+    const uint32_t zl = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(one, __builtin_bit_cast(u16x2, xl)));
+    const uint32_t zh = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(one, __builtin_bit_cast(u16x2, xh)));
+    T |= (zl | (zh << 1)) << (4 * q);
   }
-  return m;
+  return (T | (T >> 14)) & 0xFFFFu;
 }
 
 // nb_row[nb_row_off[i] + j]: byte offset in Dn (row * npitch) of the narrow
