@@ -149,7 +149,10 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     n_my = __builtin_amdgcn_readfirstlane(n_my);
   }
   for (uint32_t it = 0;; ++it) {
-    const uint32_t* cur = bits + (it % 3) * bw;
+    // bitmap it % 3: nodes changed in sweep it - 1 or it (read by this
+    // sweep; a change sets it and the next sweep's); (it + 2) % 3 is idle
+    uint32_t* cur_w = bits + (it % 3) * bw;
+    const uint32_t* cur = cur_w;
     uint32_t* nxt = bits + ((it + 1) % 3) * bw;
     uint32_t* old = bits + ((it + 2) % 3) * bw;  // read by nobody this sweep
     for (uint32_t i = tid; i < bw; i += kMpThreads) old[i] = 0;
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 #pragma unroll
         for (int t = 0; t < (int)kMpAhead; ++t) {
           const uint32_t u = e[t] & 0xFFFFu;
-          cw[t] = cur[u >> 5] | nxt[u >> 5];
+          cw[t] = cur[u >> 5];  // changed in the previous sweep or this one
         }
         uint32_t d[kMpAhead][SD];
         bool c[kMpAhead];
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 #pragma unroll
         for (int t = 0; t < (int)kMpAhead; ++t)
           if (c[t]) {
-            const uint32_t wp = (e[t] >> 16) * 0x00010001u;
+            const uint32_t wp = __builtin_amdgcn_perm(e[t], e[t], 0x03020302u);  // w | w << 16
 #pragma unroll
             for (int q = 0; q < SD; ++q) acc[q] = min2(acc[q], add_sat2(d[t][q], wp));
             got = true;
@@ -252,7 +255,10 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         if (dec) {
           changed = true;
           expands = k < 32 ? !((dmask >> k) & 1u) : !ovl[v];
-          if (expands) atomicOr(&nxt[v >> 5], 1u << (v & 31));
+          if (expands) {  // seen as changed by this sweep and the next
+            atomicOr(&cur_w[v >> 5], 1u << (v & 31));
+            atomicOr(&nxt[v >> 5], 1u << (v & 31));
+          }
         }
       }
       // (whole wave: every lane takes its share of the list)
