@@ -229,16 +229,23 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
       uint32_t ea[kMpAhead], eb[kMpAhead];
       auto load = [&](uint32_t j0, uint32_t (&e)[kMpAhead]) {
 #pragma unroll
-        for (int t = 0; t < (int)kMpAhead; ++t) e[t] = j0 + t < w ? ep[(j0 + t) * 64] : N;  // N: padding
+        for (int t = 0; t < (int)kMpAhead; ++t) {
+          // unconditional (the ELL is padded past its last slice): a
+          // branch per column made the compiler drain every load in flight
+          // (vmcnt(0)) before each group's folds
+          // (columns past the slice's w read the next slice's entries --
+          // valid node ids -- and fold() never uses them: t < n)
+          e[t] = ep[(j0 + t) * 64];
+        }
       };
+      // every group load unconditional (the ELL is padded): a load under a
+      // branch makes the join's wait count drain the loads in flight
       load(0, ea);
       for (uint32_t j0 = 0; j0 < w; j0 += 2 * kMpAhead) {
-        if (j0 + kMpAhead < w) load(j0 + kMpAhead, eb);
+        load(j0 + kMpAhead, eb);
         fold(ea, w - j0);
-        if (j0 + kMpAhead < w) {
-          if (j0 + 2 * kMpAhead < w) load(j0 + 2 * kMpAhead, ea);
-          fold(eb, w - j0 - kMpAhead);
-        }
+        load(j0 + 2 * kMpAhead, ea);
+        if (j0 + kMpAhead < w) fold(eb, w - j0 - kMpAhead);
       }
       bool expands = false;
       if (got && v < N) {
@@ -352,7 +359,9 @@ spf_status mssp_prepare(spf_ctx* c) {
   if (c->mp_epoch == c->epoch && c->d_mp_ell.p) return SPF_OK;
   const uint32_t N = c->N;
   const uint32_t n_slices = (N + 63) / 64;
-  std::vector<uint32_t> ell(c->sell_ptr.back(), N);
+  // (+ 4 groups of kMpAhead columns of padding: the kernel's column loads
+  // run unconditionally up to two groups past a slice's last column)
+  std::vector<uint32_t> ell(c->sell_ptr.back() + 4ull * kMpAhead * 64, N);
   for (uint32_t v = 0; v < N; ++v) {
     const uint32_t sl = v / 64, ln = v % 64;
     for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j) {
