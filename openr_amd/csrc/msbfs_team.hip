@@ -182,37 +182,51 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
   auto sweep = [&]() {
     uint64_t acc = 0;
     uint32_t cur = 0xFFFFFFFFu;
-    uint32_t ca[16], cb[16];
-    auto load = [&](uint32_t k, uint32_t (&c)[16]) {
+    constexpr int H = 8;  // columns per step: two steps in flight (registers: OWN = 4 planes)
+    uint32_t ca[H], cb[H];
+    // a step's column loads: stream words by scalar loads, group offset in
+    // an SGPR, lane offset in a VGPR
+    auto load = [&](uint32_t k, uint32_t (&c)[H]) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {  // buffer loads: group offset in an SGPR, lane offset in a VGPR
-        const uint32_t g = __builtin_amdgcn_readfirstlane(ms[k * 16 + u]) & 0xFFFFFu;
+      for (int u = 0; u < H; ++u) {
+        const uint32_t g = __builtin_amdgcn_readfirstlane(ms[k * H + u]) & 0xFFFFFu;
         c[u] = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 4u), (int)(g * 256u), 0);
       }
     };
-    auto proc = [&](uint32_t k, const uint32_t (&c)[16]) {
+    // the step's stream words and frontier gathers all issued before the
+    // first is used (a scalar load between them serialized one LDS round
+    // trip per column: both count on lgkmcnt)
+    auto proc = [&](uint32_t k, const uint32_t (&c)[H]) {
+      uint32_t m[H];
+      uint64_t f[H];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const uint64_t f = Fl[c[u]];
-        const uint32_t sl = __builtin_amdgcn_readfirstlane(ms[k * 16 + u]) >> 20;
+      for (int u = 0; u < H; ++u) m[u] = __builtin_amdgcn_readfirstlane(ms[k * H + u]);
+#pragma unroll
+      for (int u = 0; u < H; ++u) f[u] = Fl[c[u]];
+#pragma unroll
+      for (int u = 0; u < H; ++u) {
+        const uint32_t sl = m[u] >> 20;
         if (sl != cur) {
           if (cur != 0xFFFFFFFFu && acc)
             atomicOr(reinterpret_cast<unsigned long long*>(&Acc[cur * 64 + lane]), acc);
           cur = sl;
           acc = 0;
         }
-        acc |= f;
+        acc |= f[u];
       }
     };
-    if (n_chunks == 0) return;
+    const uint32_t n_steps = n_chunks * (16 / H);
+    if (n_steps == 0) return;
+    // loads unconditional (the stream table is padded with two chunks of the
+    // all-padding group; past a wave's range they read the next wave's
+    // groups, never processed): a load under a branch made the join's wait
+    // count drain the next step's loads before every step's gathers
     load(0, ca);
-    for (uint32_t k = 0; k < n_chunks; k += 2) {
-      if (k + 1 < n_chunks) load(k + 1, cb);
+    for (uint32_t k = 0; k < n_steps; k += 2) {
+      load(k + 1, cb);
       proc(k, ca);
-      if (k + 1 < n_chunks) {
-        if (k + 2 < n_chunks) load(k + 2, ca);
-        proc(k + 1, cb);
-      }
+      load(k + 2, ca);
+      if (k + 1 < n_steps) proc(k + 1, cb);
     }
     if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&Acc[cur * 64 + lane]), acc);
   };
@@ -609,6 +623,7 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
   while (tab.size() % 16) tab.push_back(0);
   p->tm_runs_at = (uint32_t)tab.size();
   tab.insert(tab.end(), meta.begin(), meta.end());
+  tab.insert(tab.end(), 32, dummy);  // the sweep's loads run up to two chunks past a range
   HIP_TRY(c, p->d_tm_map.upload(tab.data(), tab.size(), c->stream));
   HIP_TRY(c, p->d_tm_F.alloc((size_t)teams * 2 * fw * 2));  // u64 as 2 words
   HIP_TRY(c, p->d_tm_bar.alloc((size_t)teams * kTmBarPad * 4));
