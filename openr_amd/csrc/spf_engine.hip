@@ -331,6 +331,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t row0 = blockIdx.x * bs;  // bs <= 64 sources per workgroup
+  // sell_col with its padding columns (spf_graph_load: 32 past the last slice)
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(sell_col), 0, (int)((n_col + 32u * kSliceW) * 4u), 0x00020000);
   const uint32_t nb = min(bs, n_rows - row0);
   const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
   // diagnostics: lane 0 of every wave of workgroup 0 logs phase clocks into
@@ -497,8 +500,44 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       const uint32_t w = sw[i];
       uint64_t acc = 0;
       uint32_t j = 0;
-      // kMsUnroll column loads in flight, then the remainder in groups of
-      // 4, 2, 1 (w is wave-uniform: scalar branches, no F reads wasted on
+      if constexpr (!LCOL) {
+        // columns from L2: two groups of kMsUnroll loads in flight, issued
+        // unconditionally (sell_col is padded past its last slice; columns
+        // past w read the next slice's valid ids and are not ORed) -- a load
+        // under a branch makes the join's wait count drain the group in
+        // flight, one L2 round trip per group
+        // buffer loads: the slice's column base in an SGPR, the lane's
+        // offset in a VGPR (a 64-bit address pair per owned slice spilled)
+        uint32_t ca[kMsUnroll], cb[kMsUnroll];
+        auto load = [&](uint32_t j0, uint32_t (&c)[kMsUnroll]) {
+#pragma unroll
+          for (int u = 0; u < kMsUnroll; ++u)
+            c[u] = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 4u),
+                                                        (int)((sb[i] + (j0 + u) * kSliceW) * 4u), 0);
+        };
+        auto fold = [&](const uint32_t (&c)[kMsUnroll], uint32_t n) {
+          uint64_t f[kMsUnroll];
+#pragma unroll
+          for (int u = 0; u < kMsUnroll; ++u) f[u] = Fc[c[u]];
+#pragma unroll
+          for (int u = 0; u < kMsUnroll; ++u)
+            if ((uint32_t)u < n) acc |= f[u];
+        };
+        load(0, ca);
+        for (; j < w; j += 2 * kMsUnroll) {
+          load(j + kMsUnroll, cb);
+          fold(ca, w - j);
+          load(j + 2 * kMsUnroll, ca);
+          if (j + kMsUnroll < w) fold(cb, w - j - kMsUnroll);
+        }
+        if (need) {
+          nx = acc & ~vis[i];
+          vis[i] |= nx;
+        }
+        return nx;
+      }
+      // LDS columns: kMsUnroll loads at a time, then the remainder in groups
+      // of 4, 2, 1 (w is wave-uniform: scalar branches, no F reads wasted on
       // padding -- the LDS port is what bounds the sweep)
       for (; j + kMsUnroll <= w; j += kMsUnroll) {
         uint32_t c[kMsUnroll];
@@ -654,6 +693,7 @@ constexpr uint32_t kPlWindow = (1u << kPlanes) - 1;  // relative levels 0..254, 
 //   whose node is finished read F[N] (a broadcast).
 //   F is double-buffered: one barrier per level.
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <int OWN, bool LCOL>
 __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
     const uint32_t* __restrict__ sell4_ptr, const uint2* __restrict__ sell4, uint32_t n4,
@@ -675,6 +715,14 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
   const uint32_t row0 = blockIdx.x * bs;  // bs <= 32
   const uint32_t nb = min(bs, n_rows - row0);
   const uint32_t all = nb == 32 ? ~0u : ((1u << nb) - 1u);
+  // column entries from L2 by buffer loads: the slice's entry base in an
+  // SGPR, the lane's offset in a VGPR (per-slice 64-bit addresses spilled)
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint2*>(sell4), 0, (int)(n4 * 8u), 0x00020000);
+  auto col4 = [&](uint32_t entry, uint32_t ln) -> uint2 {
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(crs, (int)(ln * 8u), (int)(entry * 8u), 0);
+    return make_uint2(x.x, x.y);
+  };
 
   for (uint32_t v = tid; v < kF; v += kMsThreads) F0[v] = F1[v] = 0;
   if (LCOL)
@@ -694,6 +742,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
 
   uint32_t vis[OWN], P[OWN][kPlanes];
   uint32_t dslices = 0;  // bit i: owned slice i holds a drained node (wave-uniform)
+  uint32_t dlane = 0;    // bit i: this lane's node of slot i is drained (no ovl loads per level)
   uint32_t sb[OWN], sg[OWN];  // owned slice i: first packed entry, groups (wave-uniform)
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
@@ -701,7 +750,9 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
     vis[i] = v < N ? F0[v] : all;
 #pragma unroll
     for (int b = 0; b < kPlanes; ++b) P[i][b] = 0u;
-    if (__ballot(v < N && ovl[v])) dslices |= 1u << i;
+    const bool dr = v < N && ovl[v];
+    dlane |= (uint32_t)dr << i;
+    if (__ballot(dr)) dslices |= 1u << i;
     const uint32_t slice = (tid - lane + i * kMsThreads) / kSliceW;
     const bool live = slice * kSliceW < N;
     const uint32_t b = live ? sell4_ptr[slice] : 0u;
@@ -723,14 +774,14 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
     uint32_t any = 0;
     const unsigned char* Fb = reinterpret_cast<const unsigned char*>(Fc);
 #define PL_F(off) (*reinterpret_cast<const uint32_t*>(Fb + (off)))
-    uint2 qn = LCOL ? lcol[sb[0] + ln] : sell4[sb[0] + ln];
+    uint2 qn = LCOL ? lcol[sb[0] + ln] : col4(sb[0], ln);
 #pragma unroll
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = tid + i * kMsThreads;
       uint32_t nx = 0;
       const uint2 q = qn;
       // group 0 of slice i + 1 is loaded while slice i waits for its F reads
-      if (i + 1 < OWN) qn = LCOL ? lcol[sb[i + 1] + ln] : sell4[sb[i + 1] + ln];
+      if (i + 1 < OWN) qn = LCOL ? lcol[sb[i + 1] + ln] : col4(sb[i + 1], ln);
       // a uniform branch per slice: skips finished slices and keeps the
       // scheduler from hoisting ten slices' loads (register pressure).
       // No per-lane masking: a finished node gets nx = 0 from ~vis, a slot
@@ -739,7 +790,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
         uint32_t acc = PL_F(q.x & 0xFFFFu) | PL_F(q.x >> 16) | PL_F(q.y & 0xFFFFu) | PL_F(q.y >> 16);
 #pragma unroll 1
         for (uint32_t g = 1; g < sg[i]; ++g) {  // wider slices: the remaining groups
-          const uint2 r = LCOL ? lcol[sb[i] + g * kSliceW + ln] : sell4[sb[i] + g * kSliceW + ln];
+          const uint2 r = LCOL ? lcol[sb[i] + g * kSliceW + ln] : col4(sb[i] + g * kSliceW, ln);
           acc |= PL_F(r.x & 0xFFFFu) | PL_F(r.x >> 16) | PL_F(r.y & 0xFFFFu) | PL_F(r.y >> 16);
         }
         nx = acc & ~vis[i];
@@ -751,7 +802,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
       }
       uint32_t f = nx;
       if ((dslices >> i) & 1u) {  // the slice holds a drained node (uniform test)
-        if (v < N && ovl[v]) {    // drained: expands only as its own source
+        if ((dlane >> i) & 1u) {  // drained: expands only as its own source
           uint32_t own = 0;
           for (uint32_t k = 0; k < n_osrc; ++k)
             if ((o_node[k] & 0xFFFFFFu) == v) own = 1u << (o_node[k] >> 24);
@@ -1131,7 +1182,6 @@ struct Planes {
   uint32_t v[P];
 };
 
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -1717,7 +1767,10 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
       c->sell_ptr[sl + 1] = c->sell_ptr[sl] + w * kSliceW;
     }
     // + one trailing all-padding group (msbfs_team.hip pads its column streams with it)
-    c->sell_col.assign(c->sell_ptr[n_slices] + kSliceW, N);
+    // + padding columns (node N): the trailing all-padding group the team
+    // kernel's stream pads with, and the BFS kernels' unconditional loads up
+    // to three groups of 8 columns past a slice's last column
+    c->sell_col.assign(c->sell_ptr[n_slices] + 32 * kSliceW, N);
     for (uint32_t v = 0; v < N; ++v) {
       const uint32_t sl = v / kSliceW, ln = v % kSliceW;
       for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j)
