@@ -295,9 +295,11 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
               for (uint32_t r4 = 0; r4 < gn; r4 += 4) {
                 const uint32_t r = r4 + (lane >> 4);
                 if (r < gn && row0 + g0 + r < a.d_rows) {
-                  const uint4 x = *reinterpret_cast<const uint4*>(T32 + r * 64 + (lane & 15) * 4);
-                  *reinterpret_cast<uint4*>(a.D + (size_t)(row0 + g0 + r) * a.pitch + sv[i] +
-                                            (lane & 15) * 4) = x;
+                  // streaming (nt) store: the u32 rows are outputs, never re-read here
+                  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                  const v4u x = *reinterpret_cast<const v4u*>(T32 + r * 64 + (lane & 15) * 4);
+                  __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(a.D + (size_t)(row0 + g0 + r) * a.pitch +
+                                                                       sv[i] + (lane & 15) * 4));
                 }
               }
             if (a.S) {

@@ -312,7 +312,11 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         o[t] = d;
         nb8 |= (d == kInf ? 0xFFu : min(d, 254u)) << (8 * t);
       }
-      reinterpret_cast<uint4*>(D + (size_t)row * pitch)[q] = make_uint4(o[0], o[1], o[2], o[3]);
+      {  // streaming store: the rows are outputs (the next-hop pass reads the u8 copy)
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u x = {o[0], o[1], o[2], o[3]};
+        __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(D + (size_t)row * pitch) + q);
+      }
       if (Dn) reinterpret_cast<uint32_t*>(Dn + (size_t)row * pitch)[q] = nb8;
     }
     if (__syncthreads_or(ovf) && tid == 0 && redo) redo[1 + atomicAdd(redo, 1u)] = row;

@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       for (uint32_t it = 0; it < maxpop; ++it) {
         if (m) {
           const uint32_t s = __ffsll((unsigned long long)m) - 1;
-          if (DL) DL[(size_t)(row0 + s) * pitch + v] = L;
+          if (DL) __builtin_nontemporal_store(L, &DL[(size_t)(row0 + s) * pitch + v]);
           if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
           m &= m - 1;
         }
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     for (uint64_t m = ((uint64_t)mhi << 32) | mlo; m; m &= m - 1) {
       const uint32_t s = __ffsll((unsigned long long)m) - 1;
       if ((x >> s) & 1ull) {
-        if (DL) DL[(size_t)(row0 + s) * pitch + v] = L;
+        if (DL) __builtin_nontemporal_store(L, &DL[(size_t)(row0 + s) * pitch + v]);
         if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = (uint8_t)nl;
       }
     }
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     for (int i = 0; i < OWN; ++i) {
       const uint32_t v = sv[i] + lane;
       if (v < N && !((vis[i] >> s) & 1ull)) {
-        if (D && d_from == 0) drow[v] = kInf;
+        if (D && d_from == 0) __builtin_nontemporal_store(kInf, &drow[v]);
         if (Dn) nrow[v] = 0xFF;
       }
     }
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     uint32_t* drow = D + (size_t)(row0 + s) * pitch;
     uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
     for (uint32_t v = N + tid; v < npitch; v += kMsThreads) {
-      if (D && d_from == 0 && v < pitch) drow[v] = kInf;
+      if (D && d_from == 0 && v < pitch) __builtin_nontemporal_store(kInf, &drow[v]);
       if (Dn) nrow[v] = 0xFF;
     }
   }
@@ -837,7 +837,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
           const bool seen = v < N && ((vis[i] >> s) & 1u);
           const uint32_t d = seen ? base + r : kInf;
           if (first || (seen && r != kPlWindow)) {
-            if (v < pitch) drow[v] = d;
+            if (v < pitch) __builtin_nontemporal_store(d, &drow[v]);
             if (nrow && v < npitch) nrow[v] = d == kInf ? 0xFFu : (uint8_t)min(d, 254u);
           }
         }
@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
           m = eq_mask16(r[u], tg);
         }
         uint16_t* o = reinterpret_cast<uint16_t*>(out_w + (size_t)(j0 + u) * wpm);
-        if (st) o[lane] = (uint16_t)m;
+        if (st) __builtin_nontemporal_store((uint16_t)m, &o[lane]);
       }
     };
     uint4 ra[kEcmpUnroll], rb[kEcmpUnroll];
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_kernel(
             m |= (uint32_t)(a[e] != kInf && a[e] + wj == b[4 * q + e]) << (4 * q + e);
         }
       }
-      if (st) reinterpret_cast<uint16_t*>(out_w + (size_t)j * wpm)[lane] = (uint16_t)m;
+      if (st) __builtin_nontemporal_store((uint16_t)m, &reinterpret_cast<uint16_t*>(out_w + (size_t)j * wpm)[lane]);
     }
   }
   // drained neighbour x: its bitmap is empty except, possibly, x itself --
@@ -1212,6 +1212,13 @@ __device__ __forceinline__ void bload(uint32_t* d, __amdgpu_buffer_rsrc_t r, uin
 //   rs: the sliced rows (S); ro: the source's bitmaps (nh + nh_off[i]).
 //   offs/k: the unit's neighbour range (its row offsets, its length); jb:
 //   the range's first neighbour index (the bitmap the first result goes to).
+#ifndef SPF_SL_STORE_AUX
+#define SPF_SL_STORE_AUX 2
+#endif
+// bitmap store cache policy: 2 = nt (streaming: the bitmaps are outputs,
+// never re-read by the pass; fabric_full next hops 0.102 -> 0.079 ms,
+// gpurun_out/r03_nt); 0 = default (build-time A/B)
+constexpr int kSlStoreAux = SPF_SL_STORE_AUX;
 template <int P, int U = (P <= 4 ? 4 : 2)>
 __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t ro,
                                             uint32_t wpm, uint32_t srow,
@@ -1254,7 +1261,7 @@ __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_
       for (int b = 0; b < P; ++b) diff |= r[u].v[b] ^ t[b];
       if (live)
         __builtin_amdgcn_raw_buffer_store_b32(~diff & valid, ro, (int)(w * 4),
-                                              (int)((jb + j0 + u) * wpm * 4), 0);
+                                              (int)((jb + j0 + u) * wpm * 4), kSlStoreAux);
     }
   };
   Planes<P> ra[U], rb[U];
@@ -1329,7 +1336,10 @@ __device__ __forceinline__ void grouped_pass(__amdgpu_buffer_rsrc_t rs, uint32_t
         uint32_t diff = 0;
 #pragma unroll
         for (int b = 0; b < P; ++b) diff |= r[v].v[b] ^ t[q][b];
-        if (live) out[q][at] = ~diff & valid[q];
+        if (live) {
+          if constexpr (kSlStoreAux) __builtin_nontemporal_store(~diff & valid[q], &out[q][at]);
+          else out[q][at] = ~diff & valid[q];
+        }
       }
     }
   };
