@@ -2924,7 +2924,9 @@ spf_status spf_plan_enable_timing(spf_plan* p, uint32_t max_executes) {
   spf_ctx* c = p->ctx;
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
   p->ev.assign(4ull * max_executes, nullptr);
-  for (auto& e : p->ev) HIP_TRY(c, hipEventCreate(&e));
+  // timing only: no system-scope fence (its L2 writeback + invalidate cost
+  // ~5 us per event and left the next kernel a cold L2)
+  for (auto& e : p->ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   p->timing_cap = max_executes;
   p->timing_n = 0;
   return SPF_OK;

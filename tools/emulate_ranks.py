@@ -60,7 +60,7 @@ def main() -> None:
     t1 = None
     for world in [int(x) for x in args.worlds.split(",")]:
         layout = AllSourcesLayout(k, eng.pitch, world, nbrs=nbrs)
-        per_rank, phases, digests, wall = [], [], {}, []
+        per_rank, phases, digests, wall, wall_nt = [], [], {}, [], []
         for r in range(world):
             srcs = layout.srcs[r]
             plan = eng.plan(srcs)
@@ -82,6 +82,17 @@ def main() -> None:
                 plan.execute(d.ptr, nh.ptr)
             dev.sync()
             wall.append((time.perf_counter() - t0) * 1e3 / args.steps)
+            # the same without timing events (a fresh plan: no event records)
+            plan_nt = eng.plan(srcs)
+            for _ in range(2):
+                plan_nt.execute(d.ptr, nh.ptr)
+            dev.sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                plan_nt.execute(d.ptr, nh.ptr)
+            dev.sync()
+            wall_nt.append((time.perf_counter() - t0) * 1e3 / args.steps)
+            plan_nt.close()
             plan.digest(d.ptr, nh.ptr, dg.ptr)
             dev.sync()
             got = dg.numpy()[: len(srcs)].view(np.uint64)
@@ -100,7 +111,7 @@ def main() -> None:
             bad = sum(1 for s, v in digests.items() if want.get(s) != v)
         print(json.dumps({
             "workload": args.workload, "world": world, "sources": n,
-            "rank_ms": [round(x, 4) for x in wall], "rank_kernel_ms": [round(x, 4) for x in per_rank],
+            "rank_ms": [round(x, 4) for x in wall], "rank_ms_no_events": [round(x, 4) for x in wall_nt], "rank_kernel_ms": [round(x, 4) for x in per_rank],
             "rank_phase_ms": phases, "partition": layout.partition, "closure": layout.closure,
             "rank_sources": [len(s) for s in layout.srcs],
             "step_ms": round(t, 4),
