@@ -50,3 +50,16 @@ def test_mssp_u16_overflow_rows_are_redone(drained):
     res = compare(names, eng, orc, list(range(len(names))))
     d = res.dist[res.dist != 0xFFFFFFFF]
     assert d.max() > 0xFFFF  # the redo path was needed
+
+
+@pytest.mark.parametrize("skip", ["0", "1"])
+@pytest.mark.parametrize("name,make", WEIGHTED[:3], ids=[w[0] for w in WEIGHTED[:3]])
+def test_mssp_slice_dirt_on_and_off(name, make, skip, monkeypatch):
+    """Slice-level dirt (a slice is swept only when one of its in-neighbour
+    slices changed; SPF_MSSP_SKIP=0 sweeps every slice) and the alternating
+    sweep direction knob (SPF_MSSP_ALT) reach the same fixed point."""
+    monkeypatch.setenv("SPF_MSSP_SKIP", skip)
+    monkeypatch.setenv("SPF_MSSP_ALT", skip)
+    names, eng, orc = load(make())
+    assert eng.plan([0]).kernels()[0] == "mssp_kernel"
+    compare(names, eng, orc, list(range(len(names))))

@@ -73,3 +73,18 @@ def test_team_bfs_chosen_for_a_rank_share_of_the_fabric():
     assert eng.plan(list(range(1250))).kernels()[0] == "msbfs_team_kernel"
     rng = np.random.default_rng(3)
     compare(names, eng, orc, sorted(int(x) for x in rng.choice(len(names), 40, replace=False)))
+
+
+@pytest.mark.parametrize("group", ["0", "1"])
+def test_sliced_next_hops_grouped_and_per_source(group, monkeypatch):
+    """The sliced next-hop pass with grouped units (sources of one XCD list
+    with identical neighbour rows share each row load) and without
+    (SPF_SLICED_GROUP=0), on the BFS-written planes and on sliced u8 rows,
+    with drained nodes (their sources are never grouped)."""
+    monkeypatch.setenv("SPF_SLICED_GROUP", group)
+    monkeypatch.setenv("SPF_NARROW", "2")
+    for topo in (T.fabric(1000, full=True),
+                 T.random_graph(300, 3000, 11, max_metric=1, overload_frac=0.1)):
+        names, eng, orc = load(topo)
+        assert eng.plan([0]).row_mode() in ("sliced", "sliced_bfs")
+        compare(names, eng, orc, list(range(len(names))))
