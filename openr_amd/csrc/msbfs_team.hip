@@ -77,6 +77,8 @@ struct TeamArgs {
   unsigned long long* F;  // [teams][2][fwords]: the levels' frontiers, exchanged through L2
   uint32_t* bar;          // [teams][kTmBarPad * 4]: arrivals, exits | 3 flag lines; zero at launch
   unsigned long long* stamps;  // diagnostics (SPF_STAMPS=<block>), usually null
+  const uint32_t* need;        // [G][need_words]: the 64-node frontier slices a member's stream reads
+  uint32_t need_words;
 };
 
 // Team hand-off of a level (MI355X_MICROARCH.md, inter-workgroup visibility,
@@ -166,6 +168,17 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
     slot[i] = __builtin_amdgcn_readfirstlane(f >> 16);
     const uint32_t v = sv[i] + lane;
     if (v < N && a.ovl[v]) drained |= 1u << i;
+  }
+  // the frontier copy's 16-byte pieces (2 nodes each, piece t = tid + k *
+  // kTmThreads) this member's sweep reads: a member of 8 reads ~1/4 of the
+  // frontier's 64-node slices, the others stay stale in its LDS
+  uint32_t cpm = 0;
+#pragma unroll
+  for (int k = 0; k < kTmCopy; ++k) {
+    const uint32_t t = tid + k * kTmThreads, sl = t >> 5;
+    if (t < fw / 2 && (sl >> 5) < a.need_words &&
+        ((a.need[member * a.need_words + (sl >> 5)] >> (sl & 31)) & 1u))
+      cpm |= 1u << k;
   }
   if (member == 0 && tid == 0) {  // the padding entries of both buffers stay 0
     for (uint32_t t = N; t < fw; ++t) {
@@ -431,12 +444,12 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
 #pragma unroll
           for (int q = 0; q < kTmCopy / 2; ++q) {
             const uint32_t t = tid + (h + q) * kTmThreads;
-            if (t < fw / 2) t4[q] = ld_sc1_16(frs, fo + 16u * t);
+            if ((cpm >> (h + q)) & 1u) t4[q] = ld_sc1_16(frs, fo + 16u * t);
           }
 #pragma unroll
           for (int q = 0; q < kTmCopy / 2; ++q) {
             const uint32_t t = tid + (h + q) * kTmThreads;
-            if (t < fw / 2) dst4[t] = t4[q];
+            if ((cpm >> (h + q)) & 1u) dst4[t] = t4[q];
           }
         }
       }
@@ -626,6 +639,22 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
   p->tm_runs_at = (uint32_t)tab.size();
   tab.insert(tab.end(), meta.begin(), meta.end());
   tab.insert(tab.end(), 32, dummy);  // the sweep's loads run up to two chunks past a range
+  {  // per member: the 64-node slices its stream's columns read (frontier copy)
+    const uint32_t fslices = (team_fwords(c->N) + 63) / 64;
+    const uint32_t nw = (fslices + 31) / 32;
+    p->tm_need_at = (uint32_t)tab.size();
+    p->tm_need_words = nw;
+    tab.resize(tab.size() + (size_t)G * nw, 0u);
+    uint32_t* need = tab.data() + p->tm_need_at;
+    const char* ne = std::getenv("SPF_TEAM_FULLCOPY");  // A/B: copy the whole frontier
+    for (uint32_t m = 0; m < G; ++m)
+      for (uint32_t sl : mem[m])
+        for (uint32_t e = c->sell_ptr[sl]; e < c->sell_ptr[sl + 1]; ++e) {
+          const uint32_t x = c->sell_col[e] / 64;
+          need[(size_t)m * nw + x / 32] |= 1u << (x % 32);
+        }
+    if (ne && ne[0] == '1') std::fill(need, need + (size_t)G * nw, ~0u);
+  }
   HIP_TRY(c, p->d_tm_map.upload(tab.data(), tab.size(), c->stream));
   HIP_TRY(c, p->d_tm_F.alloc((size_t)teams * 2 * fw * 2));  // u64 as 2 words
   HIP_TRY(c, p->d_tm_bar.alloc((size_t)teams * kTmBarPad * 4));
@@ -650,7 +679,8 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
              (c->n_cu / 8) / p->tm_G, p->tm_nacc, fw,
              (uint32_t)std::max<size_t>(8ull * fw, (size_t)kTmWaves * kTmRows * 80 * 4),
              (uint32_t)(4ull * c->sell_col.size()), d_rows, S, s_stride, D, Dn, maxd,
-             reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p};
+             reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p,
+             p->d_tm_map.p + p->tm_need_at, p->tm_need_words};
   const uint32_t* meta = p->d_tm_map.p + p->tm_runs_at;
   const uint32_t blocks = p->tm_teams * p->tm_G;  // = n_cu: one persistent workgroup per CU
   const size_t lds = team_lds(fw, p->tm_nacc);
