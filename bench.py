@@ -6,14 +6,20 @@ fabric (BASELINE.json configs[2]; metric "all-sources SPF solves/sec + GTEPS,
 Default workload (fabric_full): a step = one all-sources pass, every node of
 the fabric solved as a source (distances + ECMP next-hop bitsets, bit-exact
 with the reference's LinkState::runSpf, openr/decision/LinkState.cpp:808-882).
-With --gpus N the sources are split over the N ranks (contiguous id blocks
-balanced by next-hop work, sharding.AllSourcesLayout) and every rank's
-distance rows and next-hop bitmaps are gathered to rank 0 over RCCL inside
-the step, so rank 0 holds the whole-graph result (strong scaling: the work
-per step is fixed).  --scaling weak instead gives rank r its own LSDB
-snapshot (rack switch r drained, BM_DecisionFabric's per-iteration
-perturbation, RoutingBenchmarkUtils.cpp:406-447) and leaves results on each
-GPU.
+With --gpus N under torchrun (one process per GPU, the driver's launch) the
+sources are split over the N ranks (sharding.AllSourcesLayout: the locality
+partition on fabrics, contiguous id blocks on grids; the rule of the engine's
+spf_partition_sources), every rank's distance rows and next-hop bitmaps stay
+RESIDENT in its own HBM (no collective inside the step), and after the timed
+steps rank 0 gathers per-source digests (RCCL) and checks every source
+against the oracle (strong scaling: the work per step is fixed).
+--results gather (labelled extra) gathers the rows and bitmaps to rank 0
+inside the step instead; --scaling weak gives rank r its own LSDB snapshot
+(rack switch r drained, BM_DecisionFabric's per-iteration perturbation,
+RoutingBenchmarkUtils.cpp:406-447).  Without torchrun, --gpus N (or
+--devices 0,1,..., repeats allowed) runs the same split from ONE process
+through the multi-device context spf_mctx (Open/R's Decision is one process,
+Decision.cpp:1484).
 
 Other BASELINE configs (--workload):
   grid100    configs[1]: all-sources SPF + ECMP on grid 100x100 (as above)
@@ -27,6 +33,7 @@ Other BASELINE configs (--workload):
              failures sharded over ranks, digests gathered with RCCL.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fabric_full]
+    python bench.py --devices 0,0,0,0 [--graphs]      (one process, 4 members)
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 
@@ -420,6 +427,84 @@ class AllSources:
                 "sample": f"{done} seeded-random sources of the same topology, full runSpf each, "
                           f"{cores} threads x one LinkState replica ({dt:.1f} s wall on "
                           f"{cpu_model()}; oracle/spf_oracle.cpp)"}
+
+
+class AllSourcesMulti(AllSources):
+    """configs[1]/[2] through the single-process multi-device context
+    (spf_mctx / spf_mplan, include/openr_spf.h): ONE process -- as Open/R's
+    Decision is (Decision.cpp:1484) -- drives every listed GPU; the sources
+    are split over the members (locality partition), every member's rows and
+    bitmaps stay in its HBM, digests are checked after the timed steps.
+    Device ids may repeat (--devices 0,0,0,0 on a one-GPU box): members of one
+    device then run one after another on it, so the per-member times are what
+    each GPU of an N-GPU node would take (the slowest sets an N-GPU step)."""
+
+    def __init__(self, name: str, devices, graphs: bool = False):
+        from openr_amd.engine import SpfMultiEngine, graph_from_lsdb
+
+        topo, self.desc = make_topology(name)
+        self.name, self.topo, self.scaling = name, topo, "strong"
+        names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+        self.n, self.e = len(names), len(col)
+        self.devices = list(devices)
+        self.m = SpfMultiEngine(self.devices)
+        self.m.load(rp, col, met, lid, ovl)
+        self.eng = self.m.member0
+        self.plan = self.m.plan(np.arange(self.n, dtype=np.uint32))
+        self.plan.set_graphs(graphs)
+        self.graphs = graphs
+        self.units = self.n
+        self.results = "resident"
+        self.narrow = self.plan.member_kernels(0)[0]
+        k = np.array([len(self.m.neighbors(s)) for s in range(self.n)], np.int64)
+        wpm = self.m.pitch // 32
+        self.graph_bytes = 4 * (self.n + 1) + 8 * self.e + self.n
+        # per member: its u32 rows + bitmaps + one graph read
+        self.member_bytes = []
+        for i in range(len(self.devices)):
+            mine = [s for s in range(self.n) if self.plan.owner(s)[0] == i]
+            self.member_bytes.append(4 * len(mine) * self.n + 4 * int(k[mine].sum()) * wpm
+                                     + self.graph_bytes)
+        self.survey_bytes = int(self.n * (self.graph_bytes + 4 * self.n) + self.n * int(np.sum((k + 7) // 8)))
+        self.kernels = ("execute",)
+        self.parallelism = (
+            f"one process, {len(self.devices)} member(s) on device(s) {self.devices} "
+            f"(spf_mctx); {self.plan.partition} partition, closure rows per member "
+            f"{self.plan.closure_rows}, sources per member {self.plan.shard_sizes()}; results "
+            f"resident on each member (no copy in the step); hipGraph replays "
+            f"{'on' if graphs else 'off'}")
+
+    def step(self) -> None:
+        self.plan.execute()
+
+    def finish(self) -> None:
+        self.plan.synchronize()
+
+    def verify(self):
+        digest = self.plan.digest()
+        gold = ROOT / "tests" / "golden" / f"fullsize_{self.name}.npz"
+        if not gold.exists():
+            return {"checked_sources": 0, "note": f"no {gold.name}"}
+        z = np.load(gold)
+        want = np.zeros(self.n, np.uint64)
+        want[z["srcs"].astype(np.int64)] = z["digest"].astype(np.uint64)
+        bad = np.nonzero(digest != want)[0]
+        return {"checked_sources": int(len(z["srcs"])), "mismatches": int(len(bad)),
+                "first_mismatch": int(bad[0]) if len(bad) else None,
+                "against": f"tests/golden/{gold.name}, engine digests (spf_mplan_digest) of "
+                           "every member's resident rows"}
+
+    def enable_timing(self, k: int) -> None:
+        self.plan.enable_timing(k)
+
+    def kernel_ms(self):
+        ms, cnt = self.plan.timing()
+        self.member_ms = [t / max(cnt, 1) for t in ms]
+        slow = int(np.argmax(self.member_ms))
+        self.alg_bytes = {"execute": self.member_bytes[slow]}
+        self.alg_execute_bytes = self.member_bytes[slow]
+        self.kernel_bytes = {"execute": self.member_bytes[slow]}
+        return {"execute": self.member_ms[slow]}
 
 
 class Ksp2AllPairs:
@@ -837,9 +922,17 @@ def main() -> None:
                     help="strong all-sources: results stay in each rank's HBM, digests "
                          "checked after the run (resident), or every rank's rows and "
                          "bitmaps gathered to rank 0 inside the step (gather)")
+    ap.add_argument("--devices", default=None,
+                    help="single-process multi-device run (spf_mctx): comma-separated device "
+                         "ids, repeats allowed (0,0,0,0 emulates 4 GPUs on one); default with "
+                         "--gpus N > 1 and no torchrun: 0..N-1")
+    ap.add_argument("--graphs", action="store_true",
+                    help="multi-device run: replay each member's execute as a hipGraph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and (args.devices or args.gpus > 1):
+        return main_multi(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -895,6 +988,9 @@ def main() -> None:
     gteps = units * wl.edges_per_unit() * args.steps / elapsed / 1e9
 
     roofline = roofline_block(wl, kms, launch_ms, args.workload, rank)
+    if parity and parity.get("mismatches"):
+        print(f"bench: PARITY FAILURE: {parity['mismatches']} of {parity['checked_sources']} "
+              f"checked results differ from the oracle", file=sys.stderr)
     out = {
         "metric": METRIC if isinstance(wl, AllSources) else (
             "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN"
@@ -951,6 +1047,70 @@ def main() -> None:
     dev.close()
     if world == 1 and os.environ.get("BENCH_DEVICE_RESET"):
         dev.hip.device_reset()
+    if parity and parity.get("mismatches"):
+        sys.exit(3)  # a result that differs from the oracle is not a measurement
+
+
+def main_multi(args) -> None:
+    """--devices / --gpus N without torchrun: the single-process
+    multi-device context (AllSourcesMulti)."""
+    if WORKLOADS.get(args.workload) is not AllSources:
+        raise SystemExit("the single-process multi-device run covers the all-sources workloads")
+    devices = ([int(x) for x in args.devices.split(",")] if args.devices
+               else list(range(args.gpus)))
+    from openr_amd import hiprt
+
+    hiprt.set_device(devices[0])
+    wl = AllSourcesMulti(args.workload, devices, graphs=args.graphs)
+    for _ in range(args.warmup):
+        wl.step()
+    wl.finish()
+    wl.enable_timing(max(1, args.steps))
+    wl.finish()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    wl.finish()
+    elapsed = time.perf_counter() - t0
+    kms = wl.kernel_ms()
+    parity = wl.verify()
+    distinct = sorted(set(devices))
+    value = wl.units * args.steps / elapsed
+    slow = max(wl.member_ms)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": wl.unit,
+        "n_gpus": len(distinct),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "gteps": wl.units * wl.e * args.steps / elapsed / 1e9,
+        "config": {
+            "workload": wl.desc, "nodes": wl.n, "directed_up_edges": wl.e,
+            "members": len(devices), "devices": devices, "parallelism": wl.parallelism,
+            "member_execute_ms": wl.member_ms,
+            # members sharing a GPU run one after another: the slowest member
+            # is what a step of len(devices) separate GPUs would take
+            "projected_step_ms_one_member_per_gpu": slow,
+            "projected_value_one_member_per_gpu": wl.units / (slow * 1e-3),
+            "hip_graphs": wl.graphs,
+        },
+        "roofline": roofline_block(wl, kms, sum(kms.values()), args.workload, 0),
+        "cpu_baseline": None,
+        "parity": parity,
+    }
+    print(json.dumps(out), flush=True)
+    from openr_amd.engine import close_all
+
+    close_all()
+    if parity and parity.get("mismatches"):
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -90,6 +90,12 @@ typedef struct ls_paths_view {
 /* device < 0 creates a host-only state: LSDB bookkeeping and CSR flatten work,
  * shortest-path queries fail with SPF_E_NO_DEVICE (used by CPU-only tests). */
 spf_status ls_create(const char* area, int device, ls_state** out);
+/* A LinkState served by several GPUs of the node (spf_mctx over gpu_ids; ids
+ * may repeat): the graph is replicated to every one; single-source queries
+ * run on the first; ls_prefetch_all_sources splits an all-sources pass over
+ * all of them.  Open/R's Decision reaches every GPU from its one thread
+ * (Decision.cpp:1484). */
+spf_status ls_create_multi(const char* area, const int* gpu_ids, uint32_t n, ls_state** out);
 void ls_destroy(ls_state* ls);
 const char* ls_last_error(const ls_state* ls);
 /* LinkState::getArea (LinkState.h:356-359) */
@@ -142,6 +148,21 @@ spf_status ls_prefetch_kth_paths(ls_state* ls, const char* src);
  * (zero / negative metrics, u64) are left to the per-node path. */
 spf_status ls_prefetch_spf_results(ls_state* ls, const char* const* nodes, uint32_t n,
                                    int use_link_metric);
+/* getSpfResult for EVERY node of the graph -- what
+ * Decision::getDecisionRouteDb does node by node (Decision.cpp:1480-1500) --
+ * as one all-sources pass split over the GPUs of an ls_create_multi state
+ * (SPF_E_STATE for a single-device state).  Results stay resident on the GPU
+ * that computed them; a later ls_get_spf_result(node) (same use_link_metric)
+ * reads node's row and next-hop bitmaps from its owner and computes its
+ * pathLinks there, and counts decision.spf_runs then (LinkState.cpp:815), as
+ * the reference's lazy getSpfResult would.  Any topology change drops the
+ * pass (the memo invalidation, LinkState.cpp:509-512, 714-717, 730-731).
+ * Graphs needing the exact kernel (zero / negative metrics, u64) are left to
+ * the per-node path. */
+spf_status ls_prefetch_all_sources(ls_state* ls, int use_link_metric);
+/* The resident pass (NULL when none is valid): per-source digests
+ * (spf_mplan_digest), owners, device buffers. */
+spf_mplan* ls_all_sources_plan(ls_state* ls);
 /* Cumulative getSpfResult cost by phase in ns since creation: out[0] plan
  * build, [1] GPU execute + copy back, [2] pathLinks, [3] host result
  * assembly (diagnostics; no reference counterpart). */

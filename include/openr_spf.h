@@ -375,6 +375,90 @@ spf_status spf_routes(spf_ctx* ctx, uint32_t me, const uint32_t* set_ptr,
                       uint64_t* min_metric, uint32_t* nh_count, uint32_t* nh_edge,
                       uint64_t* nh_metric);
 
+/* ---- multi-device context: several GPUs behind one host thread ----------- */
+/* SURVEY.md §8(b)'s spf_ctx_create(gpu_ids, ngpu): Open/R's Decision runs in
+ * one process on one event-base thread (Decision.cpp:1484), so the GPUs of a
+ * node are reached from one context, not a process per GPU.  An spf_mctx
+ * holds one member engine context per listed device id (ids may repeat: the
+ * members of one device share its execute stream and run one after another
+ * there), each with a replica of the graph.  An spf_mplan splits a batch of
+ * sources over the members and keeps each member's distance rows and
+ * next-hop bitmaps resident in that member's HBM; queries are answered by the
+ * owning member.  Results are bit-identical to one spf_plan over the batch.
+ *
+ * Partition of the sources (also usable on its own, host only):
+ *   SPF_PARTITION_CONTIGUOUS  blocks of the request order balanced by the
+ *                             bytes each source's results take (k + 40
+ *                             bitmaps, k = distinct up neighbours)
+ *   SPF_PARTITION_LOCALITY    a streaming partition keeping each member's
+ *                             closure (sources + their neighbours, whose rows
+ *                             the next-hop pass reads) small: a fabric's pods
+ *                             and planes stay together
+ *   SPF_PARTITION_AUTO        locality when its largest closure is smaller
+ *                             (graphs up to 65,536 nodes), else contiguous */
+#define SPF_PARTITION_AUTO 0u
+#define SPF_PARTITION_CONTIGUOUS 1u
+#define SPF_PARTITION_LOCALITY 2u
+/* nb_ptr/nb_id: distinct up neighbours per node (spf_src_neighbors of every
+ * node, CSR form); part_out[i] = part of srcs[i]; *mode_used = the rule taken. */
+spf_status spf_partition_sources(const uint32_t* nb_ptr, const uint32_t* nb_id, uint32_t n_nodes,
+                                 const uint32_t* srcs, uint32_t n_src, uint32_t n_parts,
+                                 uint32_t mode, uint32_t* part_out, uint32_t* mode_used);
+
+typedef struct spf_mctx spf_mctx;
+typedef struct spf_mplan spf_mplan;
+spf_status spf_mctx_create(const int* gpu_ids, uint32_t n, spf_mctx** out);
+void spf_mctx_destroy(spf_mctx* m);
+const char* spf_mctx_last_error(const spf_mctx* m);
+uint32_t spf_mctx_size(const spf_mctx* m);
+/* member i's engine context (owned by the mctx; every single-context call
+ * works on it) and its device id */
+spf_ctx* spf_mctx_member(spf_mctx* m, uint32_t i);
+int spf_mctx_device(const spf_mctx* m, uint32_t i);
+/* graph replicated to every member; patches applied to every replica */
+spf_status spf_mctx_graph_load(spf_mctx* m, const spf_graph* g);
+spf_status spf_mctx_graph_set_overload(spf_mctx* m, const uint32_t* nodes,
+                                       const uint8_t* overloaded, uint32_t n);
+spf_status spf_mctx_graph_set_metric(spf_mctx* m, const uint32_t* edges, const int32_t* metric,
+                                     uint32_t n);
+
+/* A batch of sources split over the members (partition `mode`), result
+ * buffers owned by the plan on each member's device. */
+spf_status spf_mplan_create(spf_mctx* m, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
+                            uint32_t mode, spf_mplan** out);
+void spf_mplan_destroy(spf_mplan* mp);
+uint32_t spf_mplan_partition(const spf_mplan* mp);   /* SPF_PARTITION_* taken */
+/* request index i (srcs[i]) -> owning member, row in that member's plan */
+spf_status spf_mplan_owner(const spf_mplan* mp, uint32_t i, uint32_t* member, uint32_t* row);
+/* member's share: its plan (spf_plan_nh_layout etc.), its resident device
+ * buffers ([n][pitch] rows, next-hop words) -- for device-side consumers */
+spf_status spf_mplan_shard(spf_mplan* mp, uint32_t member, uint32_t* n_src, spf_plan** plan,
+                           void** d_dist, uint32_t** d_nh);
+uint32_t spf_mplan_closure_rows(const spf_mplan* mp, uint32_t member);
+/* enable != 0: each member's execute is captured into a hipGraph after the
+ * first execute of a graph epoch and replayed after that (re-captured after
+ * an in-place patch) */
+spf_status spf_mplan_set_graphs(spf_mplan* mp, int enable);
+/* Enqueue every member's execute on its device's stream; no host wait. */
+spf_status spf_mplan_execute(spf_mplan* mp);
+/* Wait for every member and check its grid / team barriers (spf_device_check). */
+spf_status spf_mplan_synchronize(spf_mplan* mp);
+/* Per-source digests (spf_plan_digest's hash) in request order, computed on
+ * each owning device; waits. */
+spf_status spf_mplan_digest(spf_mplan* mp, uint64_t* out);
+/* Source i's result from its owner: dist = [n_nodes] (u32, u64 with
+ * SPF_FLAG_DIST64), nh = k bitmaps of spf_row_pitch/32 words (k = distinct up
+ * neighbours of srcs[i]); either may be NULL.  Waits for the owner's stream. */
+spf_status spf_mplan_read(spf_mplan* mp, uint32_t i, void* dist, uint32_t* nh);
+/* pathLinks of source i (spf_preds' output) from the resident row on its
+ * owning device; SPF_E_UNSUPPORTED for zero / negative metrics and u64 rows. */
+spf_status spf_mplan_preds(spf_mplan* mp, uint32_t i, uint32_t* pred_ptr, uint32_t* pred_edge,
+                           uint32_t cap, uint32_t* n_preds);
+/* HIP-event time of each member's executes: ms[member] summed over the last
+ * executes since enable / the last call, *n = executes. */
+spf_status spf_mplan_enable_timing(spf_mplan* mp, uint32_t max_executes);
+spf_status spf_mplan_timing(spf_mplan* mp, double* ms, uint32_t* n);
+
 /* ---- diagnostics ---------------------------------------------------------- */
 /* With SPF_STAMPS set in the environment, the multi-source BFS kernel records
  * s_memtime clocks of workgroup 0 at its phase boundaries (init, then per level:

@@ -32,6 +32,10 @@ SPF_FLAG_DIST64 = 0x2
 SPF_UNREACHABLE64 = 0xFFFFFFFFFFFFFFFF
 SPF_KSP2_NONE = 0xFFFFFFFF
 SPF_ROUTE_LFA = 0x1
+SPF_PARTITION_AUTO = 0
+SPF_PARTITION_CONTIGUOUS = 1
+SPF_PARTITION_LOCALITY = 2
+PARTITION_NAMES = {SPF_PARTITION_CONTIGUOUS: "contiguous", SPF_PARTITION_LOCALITY: "locality"}
 
 _STATUS_NAMES = {
     SPF_E_INVALID: "SPF_E_INVALID",
@@ -197,8 +201,39 @@ PROTOTYPES = {
     "spf_whatif_solve": (C.c_int, [_vp, C.c_uint32, _u32p, C.c_uint32, _vp, _vp]),
     "spf_routes": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p, C.c_uint32, C.c_uint32, _u64p,
                              _u32p, _u32p, _u64p]),
+    # multi-device context (openr_spf.h)
+    "spf_partition_sources": (C.c_int, [_u32p, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, _u32p, _u32p]),
+    "spf_mctx_create": (C.c_int, [C.POINTER(C.c_int), C.c_uint32, C.POINTER(_vp)]),
+    "spf_mctx_destroy": (None, [_vp]),
+    "spf_mctx_last_error": (C.c_char_p, [_vp]),
+    "spf_mctx_size": (C.c_uint32, [_vp]),
+    "spf_mctx_member": (_vp, [_vp, C.c_uint32]),
+    "spf_mctx_device": (C.c_int, [_vp, C.c_uint32]),
+    "spf_mctx_graph_load": (C.c_int, [_vp, C.POINTER(SpfGraph)]),
+    "spf_mctx_graph_set_overload": (C.c_int, [_vp, _u32p, _u8p, C.c_uint32]),
+    "spf_mctx_graph_set_metric": (C.c_int, [_vp, _u32p, _i32p, C.c_uint32]),
+    "spf_mplan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.POINTER(_vp)]),
+    "spf_mplan_destroy": (None, [_vp]),
+    "spf_mplan_partition": (C.c_uint32, [_vp]),
+    "spf_mplan_owner": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p]),
+    "spf_mplan_shard": (C.c_int, [_vp, C.c_uint32, _u32p, C.POINTER(_vp), C.POINTER(_vp),
+                                  C.POINTER(_vp)]),
+    "spf_mplan_closure_rows": (C.c_uint32, [_vp, C.c_uint32]),
+    "spf_mplan_set_graphs": (C.c_int, [_vp, C.c_int]),
+    "spf_mplan_execute": (C.c_int, [_vp]),
+    "spf_mplan_synchronize": (C.c_int, [_vp]),
+    "spf_mplan_digest": (C.c_int, [_vp, _u64p]),
+    "spf_mplan_read": (C.c_int, [_vp, C.c_uint32, _vp, _u32p]),
+    "spf_mplan_preds": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p, C.c_uint32, _u32p]),
+    "spf_mplan_enable_timing": (C.c_int, [_vp, C.c_uint32]),
+    "spf_mplan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), _u32p]),
     # LinkState facade (openr_linkstate.h)
     "ls_create": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
+    "ls_create_multi": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.c_uint32, C.POINTER(_vp)]),
+    "ls_prefetch_all_sources": (C.c_int, [_vp, C.c_int]),
+    "ls_all_sources_plan": (_vp, [_vp]),
     "ls_destroy": (None, [_vp]),
     "ls_last_error": (C.c_char_p, [_vp]),
     "ls_get_area": (C.c_char_p, [_vp]),

@@ -108,6 +108,9 @@ struct spf_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;  // what-if workgroup teams (lazily created, lives with the ctx)
   hipEvent_t side_fork = nullptr, side_join = nullptr;
+  // barrier-timeout word of this context's grid-resident / team launches
+  // (spf_device_check reads and clears it)
+  spfi::DevBuf<uint32_t> d_fault;
   std::string err;
   uint64_t solves = 0;
   uint64_t shape = 0;  // bumped by spf_graph_load (CSR structure)
@@ -256,7 +259,6 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
                              uint32_t* S = nullptr, uint32_t s_stride = 0);  // sdirect planes
 // planes per word of the rows msbfs_team_kernel slices itself (sdirect plans)
 constexpr uint32_t kTeamPlanes = 4;
-spf_status msbfs_team_timed_out(spf_ctx* c, bool* out);
 spf_status mssp_prepare(spf_ctx* c);
 spf_status mssp_set_lds_limits(spf_ctx* c);
 spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
@@ -289,5 +291,19 @@ spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh,
                       hipStream_t s);
 // Raise the dynamic-LDS limit of the engine's LDS-resident kernels.
 spf_status set_lds_limits(spf_ctx* c);
+// Order a launch whose workgroups wait on each other (grid barriers, team
+// BFS) on stream s after the previous such launch of this process on the
+// same device, whatever context or stream that was on: two of them running
+// at once could each hold part of the CUs the other's members need (each
+// waits for members that cannot become resident until it exits).  Call
+// before the launch, then resident_done(c, s) after it.
+spf_status resident_order(spf_ctx* c, hipStream_t s);
+spf_status resident_done(spf_ctx* c, hipStream_t s);
+void resident_forget(const spf_ctx* c);
+// pathLinks of `src` from its u32 distance row on the device (spf_preds
+// without the upload; spf_mplan_preds reads a resident row).
+spf_status preds_from_row(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
+                          const uint32_t* d_row, uint32_t* pred_ptr, uint32_t* pred_edge,
+                          uint32_t cap, uint32_t* n_preds, hipStream_t s);
 
 }  // namespace spfi

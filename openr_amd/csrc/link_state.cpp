@@ -25,6 +25,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <numeric>
 #include <optional>
 #include <thread>
 #include <string>
@@ -190,6 +191,12 @@ struct ls_state {
   int device = 0;
   std::string err;
   spf_ctx* eng = nullptr;
+  // several GPUs (ls_create_multi): eng is member 0 of meng (single-source
+  // queries), `all` the resident all-sources pass of ls_prefetch_all_sources
+  spf_mctx* meng = nullptr;
+  spf_mplan* all = nullptr;
+  bool all_valid = false;  // `all` holds results of the current graph
+  int all_ulm = 1;
   uint64_t spf_runs = 0;
 
   // names
@@ -248,13 +255,32 @@ spf_status lfail(ls_state* ls, spf_status st, const char* fmt, ...) {
 }
 
 spf_status eng_fail(ls_state* ls, spf_status st) {
-  ls->err = std::string("engine: ") + spf_last_error(ls->eng);
+  ls->err = std::string("engine: ") + (ls->meng ? spf_mctx_last_error(ls->meng) : "") +
+            (ls->meng ? " / " : "") + spf_last_error(ls->eng);
   return st;
 }
 
 void clear_results(ls_state* ls) {
   ls->spf_memo.clear();
   ls->ksp_memo.clear();
+  ls->all_valid = false;  // the resident pass answered the old graph
+}
+
+// graph to the engine: every member's replica when several GPUs serve it
+spf_status eng_load(ls_state* ls, const spf_graph* g) {
+  if (ls->all) {  // bound to the old CSR structure
+    spf_mplan_destroy(ls->all);
+    ls->all = nullptr;
+  }
+  return ls->meng ? spf_mctx_graph_load(ls->meng, g) : spf_graph_load(ls->eng, g);
+}
+spf_status eng_set_overload(ls_state* ls, const uint32_t* nodes, const uint8_t* v, uint32_t n) {
+  return ls->meng ? spf_mctx_graph_set_overload(ls->meng, nodes, v, n)
+                  : spf_graph_set_overload(ls->eng, nodes, v, n);
+}
+spf_status eng_set_metric(ls_state* ls, const uint32_t* edges, const int32_t* m, uint32_t n) {
+  return ls->meng ? spf_mctx_graph_set_metric(ls->meng, edges, m, n)
+                  : spf_graph_set_metric(ls->eng, edges, m, n);
 }
 
 void clear_memo(ls_state* ls) {
@@ -458,8 +484,7 @@ spf_status flatten(ls_state* ls) {
     }
     ls->pending_ovl.clear();
     if (!nodes.empty() && ls->eng && ls->engine_loaded) {
-      const spf_status st =
-          spf_graph_set_overload(ls->eng, nodes.data(), vals.data(), (uint32_t)nodes.size());
+      const spf_status st = eng_set_overload(ls, nodes.data(), vals.data(), (uint32_t)nodes.size());
       if (st != SPF_OK) return eng_fail(ls, st);
     }
     return SPF_OK;
@@ -519,9 +544,8 @@ spf_status flatten(ls_state* ls) {
         nodes.push_back(u);
         vals.push_back(ls->ovl[u]);
       }
-    spf_status st = spf_graph_set_metric(ls->eng, edges.data(), mets.data(), (uint32_t)edges.size());
-    if (st == SPF_OK)
-      st = spf_graph_set_overload(ls->eng, nodes.data(), vals.data(), (uint32_t)nodes.size());
+    spf_status st = eng_set_metric(ls, edges.data(), mets.data(), (uint32_t)edges.size());
+    if (st == SPF_OK) st = eng_set_overload(ls, nodes.data(), vals.data(), (uint32_t)nodes.size());
     if (st != SPF_OK) {
       ls->engine_loaded = false;
       return eng_fail(ls, st);
@@ -539,7 +563,7 @@ spf_status flatten(ls_state* ls) {
     g.metric = ls->metric.data();
     g.link_id = ls->link_id.data();
     g.overloaded = ls->ovl.data();
-    const spf_status st = spf_graph_load(ls->eng, &g);
+    const spf_status st = eng_load(ls, &g);
     if (st != SPF_OK) return eng_fail(ls, st);
     ls->engine_loaded = true;
   }
@@ -694,7 +718,23 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
     std::vector<uint32_t> nh(std::max<uint64_t>(words, 1));
     std::vector<uint64_t> d64;
     uint64_t t0 = now_ns();
-    if (needs_exact(ls, ulm)) {
+    if (ls->all && ls->all_valid && ls->all_ulm == (ulm ? 1 : 0)) {
+      // answered by the GPU holding the resident all-sources pass (every
+      // csr node is a source of `all`, request index = csr id)
+      st = spf_mplan_read(ls->all, s, m.dist.data(), nh.data());
+      if (st != SPF_OK) return eng_fail(ls, st);
+      uint64_t t1 = now_ns();
+      ls->phase_ns[1] += t1 - t0;
+      m.pred_ptr.resize(N + 1);
+      uint32_t npred = 0;
+      st = spf_mplan_preds(ls->all, s, m.pred_ptr.data(), nullptr, 0, &npred);
+      if (st != SPF_OK) return eng_fail(ls, st);
+      m.pred_edge.resize(npred);
+      st = spf_mplan_preds(ls->all, s, m.pred_ptr.data(), m.pred_edge.data(), npred, &npred);
+      if (st != SPF_OK) return eng_fail(ls, st);
+      t0 = now_ns();
+      ls->phase_ns[2] += t0 - t1;
+    } else if (needs_exact(ls, ulm)) {
       st = exact_spf(ls, s, ulm, {}, d64, &nh, m.pred_ptr, m.pred_edge);
       if (st != SPF_OK) return st;
       for (uint32_t v = 0; v < N; ++v)  // csr-indexed reachability for path tracing
@@ -869,6 +909,53 @@ spf_status read_lsdb(ls_state* ls, const openr_lsdb* in, uint32_t d, uint32_t* n
 
 extern "C" {
 
+spf_status ls_create_multi(const char* area, const int* gpu_ids, uint32_t n, ls_state** out) {
+  if (!out || !gpu_ids || n == 0) return SPF_E_INVALID;
+  *out = nullptr;
+  auto ls = std::make_unique<ls_state>();
+  ls->area = area ? area : "0";
+  ls->device = gpu_ids[0];
+  const spf_status st = spf_mctx_create(gpu_ids, n, &ls->meng);
+  if (st != SPF_OK) return st;  // spf_global_error() has the reason
+  ls->eng = spf_mctx_member(ls->meng, 0);
+  *out = ls.release();
+  return SPF_OK;
+}
+
+// getSpfResult for every node, as Decision::getDecisionRouteDb asks for each
+// node of the area (Decision.cpp:1480-1500): one all-sources pass split over
+// the GPUs, results resident on the owning GPU until the next graph change.
+spf_status ls_prefetch_all_sources(ls_state* ls, int ulm) {
+  if (!ls) return SPF_E_INVALID;
+  spf_status st = flatten(ls);
+  if (st != SPF_OK) return st;
+  if (!ls->eng) return lfail(ls, SPF_E_NO_DEVICE, "LinkState created host-only (device < 0)");
+  if (!ls->meng) return lfail(ls, SPF_E_STATE, "ls_prefetch_all_sources needs ls_create_multi");
+  if (needs_exact(ls, ulm != 0)) return SPF_OK;  // the exact kernel answers node by node
+  const uint32_t N = (uint32_t)ls->csr_name.size();
+  if (N == 0) return SPF_OK;
+  const uint32_t flags = ulm ? 0u : SPF_FLAG_HOP_COUNT;
+  if (ls->all && ls->all_ulm != (ulm != 0 ? 1 : 0)) {
+    spf_mplan_destroy(ls->all);
+    ls->all = nullptr;
+  }
+  if (!ls->all) {
+    std::vector<uint32_t> srcs(N);
+    std::iota(srcs.begin(), srcs.end(), 0u);
+    st = spf_mplan_create(ls->meng, srcs.data(), N, flags, SPF_PARTITION_AUTO, &ls->all);
+    if (st != SPF_OK) return eng_fail(ls, st);
+    ls->all_ulm = ulm != 0 ? 1 : 0;
+  }
+  ls->all_valid = false;
+  st = spf_mplan_execute(ls->all);
+  if (st == SPF_OK) st = spf_mplan_synchronize(ls->all);
+  if (st != SPF_OK) return eng_fail(ls, st);
+  ls->all_valid = true;
+  return SPF_OK;
+}
+
+spf_mplan* ls_all_sources_plan(ls_state* ls) { return ls && ls->all_valid ? ls->all : nullptr; }
+
 spf_status ls_create(const char* area, int device, ls_state** out) {
   if (!out) return SPF_E_INVALID;
   *out = nullptr;
@@ -885,7 +972,11 @@ spf_status ls_create(const char* area, int device, ls_state** out) {
 
 void ls_destroy(ls_state* ls) {
   if (!ls) return;
-  spf_ctx_destroy(ls->eng);
+  spf_mplan_destroy(ls->all);
+  if (ls->meng)
+    spf_mctx_destroy(ls->meng);  // owns eng
+  else
+    spf_ctx_destroy(ls->eng);
   delete ls;
 }
 

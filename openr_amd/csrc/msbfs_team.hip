@@ -57,9 +57,6 @@ constexpr int kTmCopy = 10;                               // uint4 per thread of
 constexpr uint32_t kTmRows = 16;                          // sources per flush tile (80 B each per node)
 constexpr uint32_t kTmBarPad = 32;            // words per team: counter line + 3 flag lines
 
-// set when a team barrier gave up (spf_device_check reads it via msbfs_team_timed_out)
-__device__ uint32_t g_team_timeout;
-
 struct TeamArgs {
   const uint32_t* sell_col;
   const uint32_t* fin;    // [G][kTmWaves][OWN] finalized slices: slice | slot << 16 (0xFFFF: none)
@@ -79,6 +76,7 @@ struct TeamArgs {
   unsigned long long* stamps;  // diagnostics (SPF_STAMPS=<block>), usually null
   const uint32_t* need;        // [G][need_words]: the 64-node frontier slices a member's stream reads
   uint32_t need_words;
+  uint32_t* fault;  // the context's barrier-timeout word (spf_device_check)
 };
 
 // Team hand-off of a level (MI355X_MICROARCH.md, inter-workgroup visibility,
@@ -88,8 +86,18 @@ struct TeamArgs {
 // level's word -- 1 + 256 * (found new nodes) + 65536 * (has unfinished
 // slices) -- and polls it with sc1 loads until all G arrived; the frontier
 // is read back with sc1 loads only.  Returns the level's word.
+// Correctness does not depend on where the members run: this is row 1 of
+// MI355X_MICROARCH.md's sc1 hand-off table (one lane per storing workgroup
+// adds to an agent-scope counter after every wave's vmcnt(0) and a
+// workgroup barrier; the consumer polls with sc1 loads and every load of the
+// handed-off bytes is an sc1 load; the payload is stored sc1), which holds
+// same-XCD and cross-XCD alike.  blockIdx % 8 groups members for L2
+// locality (speed) only.  The launch is ordered after any other
+// grid-resident launch of the process on the device (resident_order), so
+// its one-workgroup-per-CU grid is not starved of CUs by another waiting
+// grid; the spin stays bounded and reports through the context's fault word.
 __device__ __forceinline__ uint32_t team_arrive(uint32_t* word, uint32_t G, uint32_t val,
-                                                uint32_t* bcast) {
+                                                uint32_t* bcast, uint32_t* fault) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -100,7 +108,7 @@ __device__ __forceinline__ uint32_t team_arrive(uint32_t* word, uint32_t G, uint
       if ((w & 0xFFu) >= G) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (k == kTmSpin) __hip_atomic_store(&g_team_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (k == kTmSpin) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     *bcast = w;
   }
   __syncthreads();
@@ -413,7 +421,8 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
       const uint32_t mine = *any_l;
       TM_STAMP();
       const uint32_t w = team_arrive(lvw + (L % 3) * kTmBarPad, G,
-                                     1u + ((mine & 1u) << 8) + ((mine & 2u) << 15), any_l + 1);
+                                     1u + ((mine & 1u) << 8) + ((mine & 2u) << 15), any_l + 1,
+                                     a.fault);
       if (tid == 0) *any_l = 0;  // read by every thread before team_arrive's second barrier
       TM_STAMP();
       if (((w >> 8) & 0xFFu) == 0) {
@@ -680,23 +689,14 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
              (uint32_t)std::max<size_t>(8ull * fw, (size_t)kTmWaves * kTmRows * 80 * 4),
              (uint32_t)(4ull * c->sell_col.size()), d_rows, S, s_stride, D, Dn, maxd,
              reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p,
-             p->d_tm_map.p + p->tm_need_at, p->tm_need_words};
+             p->d_tm_map.p + p->tm_need_at, p->tm_need_words, c->d_fault.p};
   const uint32_t* meta = p->d_tm_map.p + p->tm_runs_at;
   const uint32_t blocks = p->tm_teams * p->tm_G;  // = n_cu: one persistent workgroup per CU
   const size_t lds = team_lds(fw, p->tm_nacc);
   void* args[] = {&a, &meta};
+  if (const spf_status st = resident_order(c, s); st != SPF_OK) return st;
   HIP_TRY(c, hipLaunchKernel(team_kernel(p->tm_own), dim3(blocks), dim3(kTmThreads), args, lds, s));
-  return SPF_OK;
-}
-
-// reads and clears the team barriers' timeout flag (spf_device_check)
-spf_status msbfs_team_timed_out(spf_ctx* c, bool* out) {
-  uint32_t flag = 0;
-  const uint32_t zero = 0;
-  HIP_TRY(c, hipMemcpyFromSymbol(&flag, HIP_SYMBOL(g_team_timeout), sizeof flag, 0, hipMemcpyDeviceToHost));
-  if (flag) HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_team_timeout), &zero, sizeof zero, 0, hipMemcpyHostToDevice));
-  *out = flag != 0;
-  return SPF_OK;
+  return resident_done(c, s);
 }
 
 }  // namespace spfi

@@ -1,0 +1,547 @@
+// ============================================================================
+//  multi.cpp -- several GPUs behind one C-ABI context (include/openr_spf.h,
+//  "multi-device context").
+//
+//  Open/R's Decision is one process on one event-base thread
+//  (openr/decision/Decision.cpp:1484): the LinkState it owns must reach every
+//  GPU of the node from that thread, not through a process per GPU.  An
+//  spf_mctx holds one engine context (spf_ctx) per listed device, each with
+//  its own replica of the graph (the CSR is small and
+//  replicated); an spf_mplan splits a batch of sources over the members --
+//  the locality partition (a source's next hops need its neighbours' rows,
+//  so a member solves its sources' neighbours too: keep that closure small)
+//  or contiguous blocks -- and keeps every member's distance rows and
+//  next-hop bitmaps resident in that member's HBM.  Queries
+//  (spf_mplan_read / spf_mplan_preds / spf_mplan_digest) are answered by the
+//  owning member: the way Decision::getDecisionRouteDb(node) for every node
+//  (Decision.cpp:1480-1500) reads an all-sources pass.
+//
+//  Device ids may repeat (one GPU holding several members, e.g. for tests on
+//  a one-GPU machine): members of one device share that device's execute
+//  stream, so their executes run one after another there, exactly as they
+//  would run side by side on separate GPUs.
+// ============================================================================
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "engine_internal.h"
+
+using namespace spfi;
+
+namespace {
+
+// a source's cost in next-hop bitmaps: its k bitmaps plus its distance rows
+// (u32 + the u8 copy = 5N bytes = 40 bitmaps of N/8 bytes); the same
+// constant as openr_amd/sharding.py AllSourcesLayout.ROW_COST
+constexpr double kRowCost = 40.0;
+constexpr uint32_t kLocalityMaxNodes = 1u << 16;
+
+// closure sizes of a partition: per part, its sources plus their neighbours
+std::vector<uint32_t> closure_sizes(const uint32_t* nb_ptr, const uint32_t* nb_id, uint32_t n_nodes,
+                                    const uint32_t* srcs, uint32_t n_src, const uint32_t* part,
+                                    uint32_t n_parts) {
+  std::vector<uint32_t> out(n_parts, 0);
+  std::vector<uint32_t> mark(n_nodes, 0xFFFFFFFFu);
+  for (uint32_t r = 0; r < n_parts; ++r) {
+    uint32_t cnt = 0;
+    auto add = [&](uint32_t x) {
+      if (mark[x] != r) mark[x] = r, ++cnt;
+    };
+    for (uint32_t i = 0; i < n_src; ++i) {
+      if (part[i] != r) continue;
+      add(srcs[i]);
+      for (uint32_t e = nb_ptr[srcs[i]]; e < nb_ptr[srcs[i] + 1]; ++e) add(nb_id[e]);
+    }
+    out[r] = cnt;
+  }
+  return out;
+}
+
+// contiguous blocks of the request order balanced by cost (k + kRowCost):
+// block r ends at the first prefix cost above total * (r+1) / n_parts
+void contiguous_parts(const uint32_t* nb_ptr, const uint32_t* srcs, uint32_t n_src,
+                      uint32_t n_parts, uint32_t* part) {
+  std::vector<double> cum(n_src);
+  double acc = 0;
+  for (uint32_t i = 0; i < n_src; ++i) {
+    acc += (double)(nb_ptr[srcs[i] + 1] - nb_ptr[srcs[i]]) + kRowCost;
+    cum[i] = acc;
+  }
+  std::vector<uint32_t> bounds(n_parts + 1, 0);
+  bounds[n_parts] = n_src;
+  for (uint32_t r = 1; r < n_parts; ++r)
+    bounds[r] = (uint32_t)(std::upper_bound(cum.begin(), cum.end(), acc * r / n_parts) - cum.begin());
+  for (uint32_t r = 0; r < n_parts; ++r)
+    for (uint32_t i = bounds[r]; i < std::max(bounds[r], bounds[r + 1]); ++i) part[i] = r;
+}
+
+// One-pass streaming partition (linear deterministic greedy): sources in
+// ascending (degree, position), each to the part whose closure it grows
+// least among the parts whose cost stays within 3 % of the mean, ties to
+// the least loaded, then the lowest part.  Low-degree nodes first: a
+// fabric's rack switches gather by pod, the fabric switches follow their
+// pod, a plane's spines land together.  Same rule as sharding.py
+// locality_partition (tests/test_partition.py checks they agree).
+void locality_parts(const uint32_t* nb_ptr, const uint32_t* nb_id, uint32_t n_nodes,
+                    const uint32_t* srcs, uint32_t n_src, uint32_t n_parts, uint32_t* part) {
+  std::vector<uint32_t> order(n_src);
+  std::iota(order.begin(), order.end(), 0u);
+  auto deg = [&](uint32_t i) { return nb_ptr[srcs[i] + 1] - nb_ptr[srcs[i]]; };
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return deg(a) < deg(b); });
+  double total = 0;
+  for (uint32_t i = 0; i < n_src; ++i) total += (double)deg(i) + kRowCost;
+  const double cap = total / n_parts * (1.0 + 0.03);  // sharding.py: sum / world * (1 + slack)
+  std::vector<uint8_t> clo((size_t)n_parts * n_nodes, 0);
+  std::vector<double> load(n_parts, 0.0);
+  std::vector<double> grow(n_parts);
+  for (uint32_t i : order) {
+    const uint32_t v = srcs[i];
+    const double cost = (double)deg(i) + kRowCost;
+    bool any_ok = false;
+    for (uint32_t r = 0; r < n_parts; ++r) any_ok |= load[r] + cost <= cap;
+    for (uint32_t r = 0; r < n_parts; ++r) {
+      if (any_ok && !(load[r] + cost <= cap)) {
+        grow[r] = std::numeric_limits<double>::infinity();
+        continue;
+      }
+      const uint8_t* c = clo.data() + (size_t)r * n_nodes;
+      uint32_t g = c[v] ? 0u : 1u;
+      for (uint32_t e = nb_ptr[v]; e < nb_ptr[v + 1]; ++e) g += c[nb_id[e]] ? 0u : 1u;
+      grow[r] = g;
+    }
+    const double best = *std::min_element(grow.begin(), grow.end());
+    uint32_t pick = n_parts;
+    for (uint32_t r = 0; r < n_parts; ++r)
+      if (grow[r] == best && (pick == n_parts || load[r] < load[pick])) pick = r;
+    part[i] = pick;
+    uint8_t* c = clo.data() + (size_t)pick * n_nodes;
+    c[v] = 1;
+    for (uint32_t e = nb_ptr[v]; e < nb_ptr[v + 1]; ++e) c[nb_id[e]] = 1;
+    load[pick] += cost;
+  }
+}
+
+uint32_t partition(const uint32_t* nb_ptr, const uint32_t* nb_id, uint32_t n_nodes,
+                   const uint32_t* srcs, uint32_t n_src, uint32_t n_parts, uint32_t mode,
+                   uint32_t* part) {
+  contiguous_parts(nb_ptr, srcs, n_src, n_parts, part);
+  if (mode == SPF_PARTITION_CONTIGUOUS || n_parts <= 1) return SPF_PARTITION_CONTIGUOUS;
+  if (mode == SPF_PARTITION_AUTO && n_nodes > kLocalityMaxNodes) return SPF_PARTITION_CONTIGUOUS;
+  std::vector<uint32_t> loc(n_src);
+  locality_parts(nb_ptr, nb_id, n_nodes, srcs, n_src, n_parts, loc.data());
+  if (mode == SPF_PARTITION_AUTO) {
+    const auto a = closure_sizes(nb_ptr, nb_id, n_nodes, srcs, n_src, part, n_parts);
+    const auto b = closure_sizes(nb_ptr, nb_id, n_nodes, srcs, n_src, loc.data(), n_parts);
+    if (*std::max_element(b.begin(), b.end()) >= *std::max_element(a.begin(), a.end()))
+      return SPF_PARTITION_CONTIGUOUS;
+  }
+  std::copy(loc.begin(), loc.end(), part);
+  return SPF_PARTITION_LOCALITY;
+}
+
+}  // namespace
+
+struct spf_mctx {
+  std::vector<spf_ctx*> members;
+  std::vector<hipStream_t> exec;  // per member: its device's execute stream (shared by repeats)
+  std::string err;
+  ~spf_mctx() {
+    for (spf_ctx* c : members) spf_ctx_destroy(c);
+  }
+};
+
+struct spf_mplan {
+  spf_mctx* m = nullptr;
+  uint32_t n_src = 0, flags = 0, mode = 0;
+  std::vector<uint32_t> srcs, owner, row;  // per request index: member, row in its plan
+  struct Part {
+    spf_plan* plan = nullptr;
+    std::vector<uint32_t> req;  // request indices in plan order
+    std::vector<uint64_t> nh_off;
+    std::vector<uint32_t> words;
+    DevBuf<uint32_t> dist, nh;
+    DevBuf<unsigned long long> dig;
+    hipGraphExec_t gexec = nullptr;
+    hipGraph_t graph = nullptr;
+    uint64_t g_epoch = ~0ull;  // graph epoch the captured executes belong to
+    std::vector<hipEvent_t> ev;  // timing: [2 * cap] start / end per execute
+  };
+  std::unique_ptr<Part[]> parts;  // [n_parts]
+  uint32_t n_parts = 0;
+  bool graphs = false;
+  uint32_t timing_cap = 0, timing_n = 0;
+  ~spf_mplan() {
+    for (size_t i = 0; i < n_parts; ++i) {
+      Part& p = parts[i];
+      if (!p.plan) continue;
+      (void)hipSetDevice(m->members[i]->device);
+      (void)hipStreamSynchronize(m->exec[i]);
+      if (p.gexec) (void)hipGraphExecDestroy(p.gexec);
+      if (p.graph) (void)hipGraphDestroy(p.graph);
+      for (hipEvent_t e : p.ev) (void)hipEventDestroy(e);
+      spf_plan_destroy(p.plan);
+      p.dist.reset();
+      p.nh.reset();
+      p.dig.reset();
+    }
+  }
+};
+
+namespace {
+
+spf_status mfail(spf_mctx* m, spf_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (m) m->err = buf;
+  g_err = buf;
+  return st;
+}
+
+spf_status member_fail(spf_mctx* m, uint32_t i, spf_status st) {
+  return mfail(m, st, "member %u (device %d): %s", i, m->members[i]->device,
+               spf_last_error(m->members[i]));
+}
+
+#define M_HIP(m, expr)                                                                   \
+  do {                                                                                   \
+    const hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess)                                                                \
+      return mfail(m, e_ == hipErrorOutOfMemory ? SPF_E_NOMEM : SPF_E_HIP, "%s: %s (%s:%d)", \
+                   #expr, hipGetErrorString(e_), __FILE__, __LINE__);                     \
+  } while (0)
+
+// One member's execute on its device's stream: a replay of the captured
+// graph when one matches the member's graph epoch, else the plan's execute
+// (which re-derives the plan after an in-place patch) -- captured then for
+// the next call when graphs are on.
+spf_status run_part(spf_mplan* mp, uint32_t i) {
+  spf_mctx* m = mp->m;
+  spf_ctx* c = m->members[i];
+  spf_mplan::Part& p = mp->parts[i];
+  const hipStream_t s = m->exec[i];
+  M_HIP(m, hipSetDevice(c->device));
+  hipEvent_t* ev = nullptr;
+  if (mp->timing_cap) {
+    ev = &p.ev[2 * (mp->timing_n % mp->timing_cap)];
+    M_HIP(m, hipEventRecord(ev[0], s));
+  }
+  if (p.gexec && p.g_epoch == spf_graph_epoch(c)) {
+    M_HIP(m, hipGraphLaunch(p.gexec, s));
+  } else {
+    if (p.gexec) {
+      (void)hipGraphExecDestroy(p.gexec);
+      (void)hipGraphDestroy(p.graph);
+      p.gexec = nullptr;
+      p.graph = nullptr;
+    }
+    spf_status st = spf_plan_execute(p.plan, p.dist.p, p.nh.p, s);
+    if (st != SPF_OK) return member_fail(m, i, st);
+    if (mp->graphs) {  // the plan is derived for this epoch now: capture its launches
+      M_HIP(m, hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+      st = spf_plan_execute(p.plan, p.dist.p, p.nh.p, s);
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(s, &g);
+      if (st != SPF_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return member_fail(m, i, st);
+      }
+      M_HIP(m, e);
+      M_HIP(m, hipGraphInstantiate(&p.gexec, g, nullptr, nullptr, 0));
+      p.graph = g;
+      p.g_epoch = spf_graph_epoch(c);
+    }
+  }
+  if (ev) M_HIP(m, hipEventRecord(ev[1], s));
+  return SPF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+spf_status spf_partition_sources(const uint32_t* nb_ptr, const uint32_t* nb_id, uint32_t n_nodes,
+                                 const uint32_t* srcs, uint32_t n_src, uint32_t n_parts,
+                                 uint32_t mode, uint32_t* part_out, uint32_t* mode_used) {
+  if (!nb_ptr || (n_src && (!srcs || !part_out)) || n_parts == 0 || mode > SPF_PARTITION_LOCALITY)
+    return mfail(nullptr, SPF_E_INVALID, "spf_partition_sources: bad argument");
+  if (nb_ptr[n_nodes] && !nb_id) return mfail(nullptr, SPF_E_INVALID, "spf_partition_sources: nb_id NULL");
+  for (uint32_t i = 0; i < n_src; ++i)
+    if (srcs[i] >= n_nodes) return mfail(nullptr, SPF_E_INVALID, "source %u out of range", srcs[i]);
+  const uint32_t used = partition(nb_ptr, nb_id, n_nodes, srcs, n_src, n_parts, mode, part_out);
+  if (mode_used) *mode_used = used;
+  return SPF_OK;
+}
+
+spf_status spf_mctx_create(const int* gpu_ids, uint32_t n, spf_mctx** out) {
+  if (!out || !gpu_ids || n == 0) return mfail(nullptr, SPF_E_INVALID, "spf_mctx_create: bad argument");
+  *out = nullptr;
+  auto m = std::make_unique<spf_mctx>();
+  std::map<int, hipStream_t> dev_stream;
+  for (uint32_t i = 0; i < n; ++i) {
+    spf_ctx* c = nullptr;
+    const spf_status st = spf_ctx_create(gpu_ids[i], &c);
+    if (st != SPF_OK) return mfail(nullptr, st, "member %u: %s", i, spf_global_error());
+    m->members.push_back(c);
+    auto it = dev_stream.find(gpu_ids[i]);
+    if (it == dev_stream.end()) it = dev_stream.emplace(gpu_ids[i], c->stream).first;
+    m->exec.push_back(it->second);
+  }
+  *out = m.release();
+  return SPF_OK;
+}
+
+void spf_mctx_destroy(spf_mctx* m) { delete m; }
+const char* spf_mctx_last_error(const spf_mctx* m) { return m ? m->err.c_str() : g_err.c_str(); }
+uint32_t spf_mctx_size(const spf_mctx* m) { return m ? (uint32_t)m->members.size() : 0; }
+spf_ctx* spf_mctx_member(spf_mctx* m, uint32_t i) {
+  return m && i < m->members.size() ? m->members[i] : nullptr;
+}
+int spf_mctx_device(const spf_mctx* m, uint32_t i) {
+  return m && i < m->members.size() ? m->members[i]->device : -1;
+}
+
+spf_status spf_mctx_graph_load(spf_mctx* m, const spf_graph* g) {
+  if (!m || !g) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_load: NULL argument");
+  for (uint32_t i = 0; i < m->members.size(); ++i) {
+    const spf_status st = spf_graph_load(m->members[i], g);
+    if (st != SPF_OK) return member_fail(m, i, st);
+  }
+  return SPF_OK;
+}
+
+spf_status spf_mctx_graph_set_overload(spf_mctx* m, const uint32_t* nodes, const uint8_t* overloaded,
+                                       uint32_t n) {
+  if (!m) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_set_overload: NULL context");
+  for (uint32_t i = 0; i < m->members.size(); ++i) {
+    const spf_status st = spf_graph_set_overload(m->members[i], nodes, overloaded, n);
+    if (st != SPF_OK) return member_fail(m, i, st);
+  }
+  return SPF_OK;
+}
+
+spf_status spf_mctx_graph_set_metric(spf_mctx* m, const uint32_t* edges, const int32_t* metric,
+                                     uint32_t n) {
+  if (!m) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_set_metric: NULL context");
+  for (uint32_t i = 0; i < m->members.size(); ++i) {
+    const spf_status st = spf_graph_set_metric(m->members[i], edges, metric, n);
+    if (st != SPF_OK) return member_fail(m, i, st);
+  }
+  return SPF_OK;
+}
+
+spf_status spf_mplan_create(spf_mctx* m, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
+                            uint32_t mode, spf_mplan** out) {
+  if (!m || !out || !srcs || n_src == 0 || mode > SPF_PARTITION_LOCALITY)
+    return mfail(m, SPF_E_INVALID, "spf_mplan_create: bad argument");
+  *out = nullptr;
+  spf_ctx* c0 = m->members[0];
+  for (spf_ctx* c : m->members)
+    if (!c->loaded || c->shape == 0 || c->N != c0->N)
+      return mfail(m, SPF_E_STATE, "spf_mplan_create: load the graph with spf_mctx_graph_load first");
+  for (uint32_t i = 0; i < n_src; ++i)
+    if (srcs[i] >= c0->N) return mfail(m, SPF_E_INVALID, "source %u out of range", srcs[i]);
+  const uint32_t P = (uint32_t)m->members.size();
+  auto mp = std::make_unique<spf_mplan>();
+  mp->m = m;
+  mp->n_src = n_src;
+  mp->flags = flags;
+  mp->srcs.assign(srcs, srcs + n_src);
+  mp->owner.resize(n_src);
+  mp->row.resize(n_src);
+  mp->mode = partition(c0->nb_ptr.data(), c0->nb_id.data(), c0->N, srcs, n_src, P, mode,
+                       mp->owner.data());
+  mp->parts.reset(new spf_mplan::Part[P]);
+  mp->n_parts = P;
+  for (uint32_t i = 0; i < n_src; ++i) {
+    spf_mplan::Part& p = mp->parts[mp->owner[i]];
+    mp->row[i] = (uint32_t)p.req.size();
+    p.req.push_back(i);
+  }
+  const uint32_t pitch = c0->pitch;
+  const size_t lab = (flags & SPF_FLAG_DIST64) ? 2 : 1;
+  for (uint32_t r = 0; r < P; ++r) {
+    spf_mplan::Part& p = mp->parts[r];
+    if (p.req.empty()) continue;
+    spf_ctx* c = m->members[r];
+    std::vector<uint32_t> ps(p.req.size());
+    for (size_t t = 0; t < ps.size(); ++t) ps[t] = srcs[p.req[t]];
+    spf_status st = spf_plan_create(c, ps.data(), (uint32_t)ps.size(), flags, &p.plan);
+    if (st != SPF_OK) return member_fail(m, r, st);
+    p.nh_off.resize(ps.size());
+    p.words.resize(ps.size());
+    spf_plan_nh_layout(p.plan, p.nh_off.data(), p.words.data());
+    M_HIP(m, hipSetDevice(c->device));
+    M_HIP(m, p.dist.alloc(ps.size() * pitch * lab));
+    M_HIP(m, p.nh.alloc(std::max<uint64_t>(spf_plan_nh_words(p.plan), 1)));
+    M_HIP(m, p.dig.alloc(ps.size()));
+  }
+  *out = mp.release();
+  return SPF_OK;
+}
+
+void spf_mplan_destroy(spf_mplan* mp) { delete mp; }
+
+uint32_t spf_mplan_partition(const spf_mplan* mp) { return mp ? mp->mode : 0; }
+
+spf_status spf_mplan_owner(const spf_mplan* mp, uint32_t i, uint32_t* member, uint32_t* row) {
+  if (!mp || i >= mp->n_src) return SPF_E_INVALID;
+  if (member) *member = mp->owner[i];
+  if (row) *row = mp->row[i];
+  return SPF_OK;
+}
+
+spf_status spf_mplan_shard(spf_mplan* mp, uint32_t member, uint32_t* n_src, spf_plan** plan,
+                           void** d_dist, uint32_t** d_nh) {
+  if (!mp || member >= mp->n_parts) return SPF_E_INVALID;
+  spf_mplan::Part& p = mp->parts[member];
+  if (n_src) *n_src = (uint32_t)p.req.size();
+  if (plan) *plan = p.plan;
+  if (d_dist) *d_dist = p.dist.p;
+  if (d_nh) *d_nh = p.nh.p;
+  return SPF_OK;
+}
+
+spf_status spf_mplan_set_graphs(spf_mplan* mp, int enable) {
+  if (!mp) return SPF_E_INVALID;
+  mp->graphs = enable != 0;
+  return SPF_OK;
+}
+
+spf_status spf_mplan_execute(spf_mplan* mp) {
+  if (!mp) return mfail(nullptr, SPF_E_INVALID, "spf_mplan_execute: NULL plan");
+  for (uint32_t i = 0; i < mp->n_parts; ++i) {
+    if (!mp->parts[i].plan) continue;
+    const spf_status st = run_part(mp, i);
+    if (st != SPF_OK) return st;
+  }
+  if (mp->timing_cap) ++mp->timing_n;
+  return SPF_OK;
+}
+
+spf_status spf_mplan_synchronize(spf_mplan* mp) {
+  if (!mp) return mfail(nullptr, SPF_E_INVALID, "spf_mplan_synchronize: NULL plan");
+  spf_mctx* m = mp->m;
+  for (uint32_t i = 0; i < mp->n_parts; ++i) {
+    if (!mp->parts[i].plan) continue;
+    M_HIP(m, hipSetDevice(m->members[i]->device));
+    M_HIP(m, hipStreamSynchronize(m->exec[i]));
+    const spf_status st = spf_device_check(m->members[i]);
+    if (st != SPF_OK) return member_fail(m, i, st);
+  }
+  return SPF_OK;
+}
+
+spf_status spf_mplan_digest(spf_mplan* mp, uint64_t* out) {
+  if (!mp || !out) return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_digest: NULL argument");
+  spf_mctx* m = mp->m;
+  std::vector<std::vector<uint64_t>> h(mp->n_parts);
+  for (uint32_t i = 0; i < mp->n_parts; ++i) {
+    spf_mplan::Part& p = mp->parts[i];
+    if (!p.plan) continue;
+    M_HIP(m, hipSetDevice(m->members[i]->device));
+    spf_status st = spf_plan_digest(p.plan, p.dist.p, p.nh.p, reinterpret_cast<uint64_t*>(p.dig.p),
+                                    m->exec[i]);
+    if (st != SPF_OK) return member_fail(m, i, st);
+    h[i].resize(p.req.size());
+    M_HIP(m, hipMemcpyAsync(h[i].data(), p.dig.p, 8 * p.req.size(), hipMemcpyDeviceToHost, m->exec[i]));
+  }
+  const spf_status st = spf_mplan_synchronize(mp);
+  if (st != SPF_OK) return st;
+  for (uint32_t i = 0; i < mp->n_parts; ++i)
+    for (size_t t = 0; t < mp->parts[i].req.size(); ++t) out[mp->parts[i].req[t]] = h[i][t];
+  return SPF_OK;
+}
+
+spf_status spf_mplan_read(spf_mplan* mp, uint32_t i, void* dist, uint32_t* nh) {
+  if (!mp || i >= mp->n_src) return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_read: bad argument");
+  spf_mctx* m = mp->m;
+  const uint32_t r = mp->owner[i], row = mp->row[i];
+  spf_mplan::Part& p = mp->parts[r];
+  spf_ctx* c = m->members[r];
+  const size_t lab = (mp->flags & SPF_FLAG_DIST64) ? 8 : 4;
+  M_HIP(m, hipSetDevice(c->device));
+  if (dist)
+    M_HIP(m, hipMemcpyAsync(dist, reinterpret_cast<const uint8_t*>(p.dist.p) + (size_t)row * c->pitch * lab,
+                            (size_t)c->N * lab, hipMemcpyDeviceToHost, m->exec[r]));
+  const uint64_t words = (uint64_t)p.words[row] * (c->pitch / 32);
+  if (nh && words)
+    M_HIP(m, hipMemcpyAsync(nh, p.nh.p + p.nh_off[row], 4 * words, hipMemcpyDeviceToHost, m->exec[r]));
+  M_HIP(m, hipStreamSynchronize(m->exec[r]));
+  return SPF_OK;
+}
+
+spf_status spf_mplan_preds(spf_mplan* mp, uint32_t i, uint32_t* pred_ptr, uint32_t* pred_edge,
+                           uint32_t cap, uint32_t* n_preds) {
+  if (!mp || i >= mp->n_src || !pred_ptr || !n_preds)
+    return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_preds: bad argument");
+  spf_mctx* m = mp->m;
+  const uint32_t r = mp->owner[i];
+  spf_ctx* c = m->members[r];
+  const bool hop = (mp->flags & SPF_FLAG_HOP_COUNT) != 0;
+  if ((mp->flags & SPF_FLAG_DIST64) || (!hop && c->nonpos))
+    return mfail(m, SPF_E_UNSUPPORTED, "spf_mplan_preds: zero / negative metrics and u64 rows "
+                                       "order pathLinks by pop rank (spf_solve_exact)");
+  const uint32_t* d_row = mp->parts[r].dist.p + (size_t)mp->row[i] * c->pitch;
+  const spf_status st = preds_from_row(c, mp->srcs[i], hop, nullptr, d_row, pred_ptr, pred_edge,
+                                       cap, n_preds, m->exec[r]);
+  return st == SPF_OK ? SPF_OK : member_fail(m, r, st);
+}
+
+uint32_t spf_mplan_closure_rows(const spf_mplan* mp, uint32_t member) {
+  if (!mp || member >= mp->n_parts || !mp->parts[member].plan) return 0;
+  return spf_plan_closure_rows(mp->parts[member].plan);
+}
+
+spf_status spf_mplan_enable_timing(spf_mplan* mp, uint32_t max_executes) {
+  if (!mp) return SPF_E_INVALID;
+  spf_mctx* m = mp->m;
+  for (uint32_t i = 0; i < mp->n_parts; ++i) {
+    spf_mplan::Part& p = mp->parts[i];
+    if (!p.plan) continue;
+    M_HIP(m, hipSetDevice(m->members[i]->device));
+    for (hipEvent_t e : p.ev) (void)hipEventDestroy(e);
+    p.ev.assign(2ull * max_executes, nullptr);
+    for (auto& e : p.ev) M_HIP(m, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  }
+  mp->timing_cap = max_executes;
+  mp->timing_n = 0;
+  return SPF_OK;
+}
+
+// per member: summed milliseconds of its executes (start to end on its
+// stream), and the number of executes
+spf_status spf_mplan_timing(spf_mplan* mp, double* ms, uint32_t* n) {
+  if (!mp || !mp->timing_cap || !ms) return SPF_E_STATE;
+  spf_mctx* m = mp->m;
+  const uint32_t cnt = std::min(mp->timing_n, mp->timing_cap);
+  for (uint32_t i = 0; i < mp->n_parts; ++i) {
+    ms[i] = 0;
+    spf_mplan::Part& p = mp->parts[i];
+    if (!p.plan) continue;
+    M_HIP(m, hipSetDevice(m->members[i]->device));
+    for (uint32_t k = 0; k < cnt; ++k) {
+      float t = 0;
+      M_HIP(m, hipEventSynchronize(p.ev[2 * k + 1]));
+      M_HIP(m, hipEventElapsedTime(&t, p.ev[2 * k], p.ev[2 * k + 1]));
+      ms[i] += t;
+    }
+  }
+  if (n) *n = cnt;
+  mp->timing_n = 0;
+  return SPF_OK;
+}
+
+}  // extern "C"

@@ -37,6 +37,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <type_traits>
@@ -1645,8 +1646,15 @@ spf_status spf_ctx_create(int device, spf_ctx** out) {
   c->n_cu = (uint32_t)std::max(1, prop.multiProcessorCount);
   if (hipSetDevice(device) != hipSuccess)
     return fail(nullptr, SPF_E_HIP, "hipSetDevice(%d) failed", device);
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+  // a BLOCKING stream: work enqueued with stream = NULL ("the context's
+  // stream") is ordered after earlier work on the legacy null stream, so a
+  // caller's hipMemset / hipMemcpy on the null stream before an execute is
+  // seen by it (round 3 lost a plan's first bitmaps to exactly that race
+  // with a non-blocking stream)
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess)
     return fail(nullptr, SPF_E_HIP, "hipStreamCreate failed");
+  if (c->d_fault.alloc(1) != hipSuccess || hipMemset(c->d_fault.p, 0, 4) != hipSuccess)
+    return fail(nullptr, SPF_E_HIP, "fault word allocation failed");
   *out = c.release();
   return SPF_OK;
 }
@@ -1654,6 +1662,7 @@ spf_status spf_ctx_create(int device, spf_ctx** out) {
 void spf_ctx_destroy(spf_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  spfi::resident_forget(c);
   if (c->stream) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
@@ -2102,7 +2111,6 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     }
     HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
     HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
-  HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
     HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     p->epoch = c->epoch;
@@ -2778,6 +2786,94 @@ namespace {
 
 namespace spfi {
 
+// Process-wide order of the launches whose workgroups wait on each other
+// (engine_internal.h resident_order): per device, the stream of the last
+// such launch and an event recorded after it.  A launch on another stream
+// waits for that event first.
+namespace {
+struct ResidentSlot {
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  const spf_ctx* owner = nullptr;  // context whose launch recorded ev
+};
+std::mutex g_resident_mu;
+std::map<int, ResidentSlot> g_resident;
+}  // namespace
+
+// (a stream being captured into a hipGraph is skipped: a capture may not
+// wait on an event recorded outside it, and the graph's replays are ordered
+// by the stream they are launched on)
+static bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+spf_status resident_order(spf_ctx* c, hipStream_t s) {
+  if (capturing(s)) return SPF_OK;
+  std::lock_guard<std::mutex> lk(g_resident_mu);
+  ResidentSlot& r = g_resident[c->device];
+  if (r.ev && r.last != s) HIP_TRY(c, hipStreamWaitEvent(s, r.ev, 0));
+  return SPF_OK;
+}
+
+spf_status resident_done(spf_ctx* c, hipStream_t s) {
+  if (capturing(s)) return SPF_OK;
+  std::lock_guard<std::mutex> lk(g_resident_mu);
+  ResidentSlot& r = g_resident[c->device];
+  if (!r.ev)
+    HIP_TRY(c, hipEventCreateWithFlags(&r.ev, hipEventDisableTiming | hipEventDisableSystemFence));
+  HIP_TRY(c, hipEventRecord(r.ev, s));
+  r.last = s;
+  r.owner = c;
+  return SPF_OK;
+}
+
+// a context going away: its streams may be reused by the runtime, so the
+// next launch on any stream waits for the recorded event instead of
+// trusting a stale stream handle
+void resident_forget(const spf_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_resident_mu);
+  for (auto& kv : g_resident)
+    if (kv.second.owner == c) kv.second.last = nullptr, kv.second.owner = nullptr;
+}
+
+// pathLinks of one source from its distance row already on the device
+// (d_row = [N] u32, positive metrics or hop counts): counts, host prefix
+// sum, then the ordered lists (the batch form is spf_plan_preds).
+spf_status preds_from_row(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
+                          const uint32_t* d_row, uint32_t* pred_ptr, uint32_t* pred_edge,
+                          uint32_t cap, uint32_t* n_preds, hipStream_t s) {
+  const uint32_t N = c->N;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, c->d_pred_cnt.alloc(N + 1));
+  const dim3 g((N + 255) / 256), b(256);
+  HIP_TRY(c, c->d_one_src.upload(&src, 1, s));
+  hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, s, d_row, N, c->d_row_ptr.p, c->d_col.p,
+                     c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign, c->d_one_src.p, N,
+                     hop ? 1u : 0u, c->d_pred_cnt.p, (uint32_t*)nullptr,
+                     (unsigned long long*)nullptr);
+  HIP_TRY(c, hipGetLastError());
+  std::vector<uint32_t> cnt(N);
+  HIP_TRY(c, hipMemcpyAsync(cnt.data(), c->d_pred_cnt.p, 4ull * N, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  pred_ptr[0] = 0;
+  for (uint32_t v = 0; v < N; ++v) pred_ptr[v + 1] = pred_ptr[v] + cnt[v];
+  *n_preds = pred_ptr[N];
+  if (!pred_edge) return SPF_OK;
+  if (cap < pred_ptr[N]) return fail(c, SPF_E_INVALID, "pred_edge capacity %u < %u", cap, pred_ptr[N]);
+  HIP_TRY(c, hipMemcpyAsync(c->d_pred_cnt.p, pred_ptr, 4ull * N, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, c->d_pred_edge.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
+  HIP_TRY(c, c->d_pred_key.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
+  hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, s, d_row, N, c->d_row_ptr.p, c->d_col.p,
+                     c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign, c->d_one_src.p, N,
+                     hop ? 1u : 0u, c->d_pred_cnt.p, c->d_pred_edge.p, c->d_pred_key.p);
+  HIP_TRY(c, hipGetLastError());
+  if (pred_ptr[N])
+    HIP_TRY(c, hipMemcpyAsync(pred_edge, c->d_pred_edge.p, 4ull * pred_ptr[N], hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return SPF_OK;
+}
+
 // Upload an ignore set (undirected link ids) as a device bitmap; NULL if empty.
 spf_status upload_ignore(spf_ctx* c, const uint32_t* ignore, uint32_t n_ignore,
                          const uint32_t** dev) {
@@ -3082,50 +3178,26 @@ spf_status spf_preds(spf_ctx* c, uint32_t src, uint32_t flags, const uint32_t* i
   if (!c || !dist || !pred_ptr || !n_preds) return fail(c, SPF_E_INVALID, "spf_preds: NULL argument");
   if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
   if (src >= c->N) return fail(c, SPF_E_INVALID, "source %u out of range", src);
-  const uint32_t N = c->N;
-  const bool hop = (flags & SPF_FLAG_HOP_COUNT) != 0;
   const uint32_t* ign = nullptr;
   spf_status st = upload_ignore(c, ignore_links, n_ignore, &ign);
   if (st != SPF_OK) return st;
-  HIP_TRY(c, c->d_row.upload(dist, N, c->stream));
-  HIP_TRY(c, c->d_pred_cnt.alloc(N + 1));
-  const dim3 g((N + 255) / 256), b(256);
-  HIP_TRY(c, c->d_one_src.upload(&src, 1, c->stream));
-  hipLaunchKernelGGL((preds_kernel<0>), g, b, 0, c->stream, c->d_row.p, N, c->d_row_ptr.p,
-                     c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign,
-                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, (uint32_t*)nullptr,
-                     (unsigned long long*)nullptr);
-  HIP_TRY(c, hipGetLastError());
-  std::vector<uint32_t> cnt(N);
-  HIP_TRY(c, hipMemcpyAsync(cnt.data(), c->d_pred_cnt.p, 4ull * N, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  pred_ptr[0] = 0;
-  for (uint32_t v = 0; v < N; ++v) pred_ptr[v + 1] = pred_ptr[v] + cnt[v];
-  *n_preds = pred_ptr[N];
-  if (!pred_edge) return SPF_OK;
-  if (cap < pred_ptr[N]) return fail(c, SPF_E_INVALID, "pred_edge capacity %u < %u", cap, pred_ptr[N]);
-  HIP_TRY(c, hipMemcpyAsync(c->d_pred_cnt.p, pred_ptr, 4ull * N, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, c->d_pred_edge.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
-  HIP_TRY(c, c->d_pred_key.alloc(std::max<uint32_t>(pred_ptr[N], 1)));
-  hipLaunchKernelGGL((preds_kernel<1>), g, b, 0, c->stream, c->d_row.p, N, c->d_row_ptr.p,
-                     c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_ovl.p, c->d_link.p, ign,
-                     c->d_one_src.p, N, hop ? 1u : 0u, c->d_pred_cnt.p, c->d_pred_edge.p,
-                     c->d_pred_key.p);
-  HIP_TRY(c, hipGetLastError());
-  if (pred_ptr[N])
-    HIP_TRY(c, hipMemcpyAsync(pred_edge, c->d_pred_edge.p, 4ull * pred_ptr[N], hipMemcpyDeviceToHost,
-                              c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return SPF_OK;
+  HIP_TRY(c, c->d_row.upload(dist, c->N, c->stream));
+  return preds_from_row(c, src, (flags & SPF_FLAG_HOP_COUNT) != 0, ign, c->d_row.p, pred_ptr,
+                        pred_edge, cap, n_preds, c->stream);
 }
 
 spf_status spf_plan_preds(spf_plan* p, uint32_t* pred_ptr, uint32_t* pred_edge, uint64_t cap,
                           uint64_t* n_preds) {
   if (!p || !pred_ptr || !n_preds) return fail(p ? p->ctx : nullptr, SPF_E_INVALID, "spf_plan_preds: NULL argument");
   spf_ctx* c = p->ctx;
-  if (p->exact || p->big)
-    return fail(c, SPF_E_UNSUPPORTED, "spf_plan_preds: exact / big plans order pathLinks by pop rank "
-                                      "(spf_solve_exact)");
+  // positive metrics (or hop counts) with u32 rows: pathLinks follow from the
+  // distance row alone, whichever kernel wrote it -- big plans
+  // and exact plans of large positive-metric graphs included.  Zero /
+  // negative metrics and u64 rows need the pop order (spf_solve_exact).
+  const bool hop_only = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
+  if ((p->flags & SPF_FLAG_DIST64) || (!hop_only && c->nonpos))
+    return fail(c, SPF_E_UNSUPPORTED, "spf_plan_preds: zero / negative metrics and u64 rows order "
+                                      "pathLinks by pop rank (spf_solve_exact)");
   if (!p->h_dist.p || p->h_epoch != c->epoch)
     return fail(c, SPF_E_STATE, "spf_plan_preds: no spf_plan_execute_host on the current graph");
   const uint32_t N = c->N, n = p->n_src;

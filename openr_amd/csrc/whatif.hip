@@ -95,6 +95,7 @@ struct WiGraph {
   const uint32_t* nbr_bit;  // [N] j if v is the src's j-th distinct neighbour, else kInf
   uint32_t N, src, W;
   uint32_t hop = 0;  // hop counts: every up link weighs 1 (useLinkMetric = false)
+  uint32_t* fault = nullptr;  // the context's barrier-timeout word (spf_device_check)
 };
 
 // directed weight of the edge reverse to e (tail -> head of the in-edge)
@@ -128,16 +129,17 @@ constexpr uint32_t kGridBarWords = 17 * kBarPad;  // cnt[8], top, gen[8]
 constexpr uint32_t kBarSpin = 1u << 26;            // ~seconds: never a silent hang
 
 // A barrier spin that ran out (a member never arrived: not co-resident, or
-// a fault) sets this word and falls through; the host reads and clears it
-// (spf_device_check) and reports SPF_E_HIP instead of the launch's output.
-__device__ uint32_t g_barrier_timeout;
-
-__device__ __forceinline__ void barrier_timed_out() {
-  __hip_atomic_store(&g_barrier_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// a fault) sets the launching context's fault word and falls through; the
+// host reads and clears it (spf_device_check) and reports SPF_E_HIP instead
+// of the launch's output.  One word per context (spf_ctx::d_fault), so a
+// check on one context neither reports nor clears another's timeout.
+__device__ __forceinline__ void barrier_timed_out(uint32_t* fault) {
+  if (fault) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct XGrid {
   uint32_t* bar;
+  uint32_t* fault;
   __device__ void sync() const {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
     __syncthreads();
@@ -168,7 +170,7 @@ struct XGrid {
              ++k)
           __builtin_amdgcn_s_sleep(1);
       }
-      if (k == kBarSpin) barrier_timed_out();
+      if (k == kBarSpin) barrier_timed_out(fault);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -201,6 +203,7 @@ struct CoopSssp {
   uint32_t* bm;   // [ceil(N/32)] next-frontier bitmap
   uint32_t* ctr;  // [4] rotating queue lengths + spare
   uint32_t* bar = nullptr;  // [kGridBarWords] XGrid counters, zero at launch
+  uint32_t* fault = nullptr;  // the context's barrier-timeout word
 };
 
 // Frontier Bellman-Ford over the whole grid: expansion, grid barrier,
@@ -283,7 +286,7 @@ __device__ void coop_sssp(const XGrid& grid, const CoopSssp& a) {
 }
 
 __global__ __launch_bounds__(kCoopThreads) void gsssp_coop_kernel(CoopSssp a) {
-  const XGrid grid{a.bar};
+  const XGrid grid{a.bar, a.fault};
   coop_sssp(grid, a);
 }
 
@@ -597,7 +600,7 @@ __device__ bool level_nh(const XGrid& grid, const WiGraph& g, const uint32_t* di
 }
 
 __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
-  const XGrid grid{a.sp.bar};
+  const XGrid grid{a.sp.bar, a.sp.fault};
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
   const WiGraph& g = a.g;
@@ -694,7 +697,7 @@ struct BigArgs {
 };
 
 __global__ __launch_bounds__(kCoopThreads) void spf_big_kernel(BigArgs a) {
-  const XGrid grid{a.sp.bar};
+  const XGrid grid{a.sp.bar, a.sp.fault};
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
   const uint32_t lane = threadIdx.x & 63;
@@ -792,7 +795,7 @@ struct TeamCtl {
 // MI355X_MICROARCH.md §Workgroup dispatch; the counter only grows, so the
 // barrier of the k-th call completes at k * G arrivals)
 template <int TEAM, bool GROUP = false>
-__device__ __forceinline__ void team_sync(TeamCtl* ctl) {
+__device__ __forceinline__ void team_sync(TeamCtl* ctl, uint32_t* fault) {
   if constexpr (GROUP) {
     const uint32_t G = TEAM / blockDim.x;  // workgroups per team
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
@@ -808,7 +811,7 @@ __device__ __forceinline__ void team_sync(TeamCtl* ctl) {
              __hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
            ++k)
         __builtin_amdgcn_s_sleep(1);
-      if (k == kBarSpin) barrier_timed_out();
+      if (k == kBarSpin) barrier_timed_out(fault);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -862,12 +865,12 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     dlist[0] = b;
     stw<GROUP>(&mark[b], 0);
   }
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   // ---- D = descendants of b in the unfailed DAG (level by level) ----
   uint32_t lo = 0;
   for (;;) {
     const uint32_t n = ctl->n;
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     if (lo >= n || ctl->ovf) break;
     // a thread per frontier node; hubs (thousands of edges) are queued in
     // ord and expanded by a whole wave each
@@ -895,7 +898,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       const uint32_t dv = B.dist[v];
       for (uint32_t e = b0; e < b1; ++e) child(dv, e);
     }
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     {
       const uint32_t nh_ = ctl->hub;
       for (uint32_t k = wv; k < nh_; k += kWaves) {
@@ -904,19 +907,19 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) child(dv, e);
       }
     }
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     if (tt == 0) ctl->hub = 0;
     lo = n;
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
   }
   const uint32_t n = min(ctl->n, cap);
   const bool ovf = ctl->ovf != 0;
   WI_STAMP(1);
   if (prof && tt == 0) prof[8] = n;
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   if (ovf) {
     for (uint32_t i = tt; i < n; i += TEAM) stw<GROUP>(&mark[dlist[i]], kInf);
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     return false;
   }
   // ---- seeds: best in-edge from outside D (unchanged distances) ----
@@ -939,7 +942,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     for (uint32_t e = b0; e < b1; ++e) best = min(best, seed_edge(e));
     stw<GROUP>(&dnew[i], best);
   }
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   {
     const uint32_t nh_ = ctl->hub;
     for (uint32_t k = wv; k < nh_; k += kWaves) {
@@ -952,7 +955,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (lane == 0) stw<GROUP>(&dnew[i], best);
     }
   }
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   if (tt == 0) ctl->hub = 0;
   // nh word j of a D node from its tight expanded predecessors (D or not);
   // used by the fixed-point fallback
@@ -1028,13 +1031,13 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     ctl->nxt[0] = kInf;
     ctl->lc[0] = 0;
   }
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   {
     uint32_t m = kInf;
     for (uint32_t i = tt; i < n; i += TEAM) m = min(m, ldw<GROUP>(&dnew[i]));
     if (m != kInf) atomicMin(&ctl->dmin, m);
   }
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   WI_STAMP(2);
   // ---- Dial: settle D one distance value at a time (metrics are positive:
   // a node holding the smallest pending value is final), next hops inline ----
@@ -1059,7 +1062,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (d == t) stw<GROUP>(&ord[atomicAdd(cnt, 1u)], i);
       else if (d != kInf && d > t) m = min(m, d);
     }
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     // (b) level nodes: next hops from their tight predecessors, then relax
     // their edges.  A thread per node; hubs (queued after the level list)
     // by a whole wave: ballot over the in-edges, coalesced row ORs.
@@ -1085,7 +1088,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (!g.ovl[v])
         for (uint32_t e = b0; e < b1; ++e) relax(v, e);
     }
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     const uint32_t H_ = *hub_cnt;
     for (uint32_t k = wv; k < H_; k += kWaves) {
       const uint32_t i = ldw<GROUP>(&hubs[k]);
@@ -1121,7 +1124,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) relax(v, e);
     }
     if (m != kInf) atomicMin(next, m);
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     t = *next;
     if (prof && tt == 0) prof[9] = it + 1;
   }
@@ -1144,7 +1147,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       }
       if (any) ctl->flag[it % 3] = 1;
       if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
-      team_sync<TEAM, GROUP>(ctl);
+      team_sync<TEAM, GROUP>(ctl, g.fault);
       if (!ctl->flag[it % 3]) break;
     }
 
@@ -1155,7 +1158,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       ctl->dmin = kInf;
       ctl->dmax = 0;
     }
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     for (uint32_t i = tt; i < n; i += TEAM) {
       const uint32_t d = ldw<GROUP>(&dnew[i]);
       if (d != kInf) {
@@ -1163,19 +1166,19 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         atomicMax(&ctl->dmax, d);
       }
     }
-    team_sync<TEAM, GROUP>(ctl);
+    team_sync<TEAM, GROUP>(ctl, g.fault);
     const uint32_t dmin = ctl->dmin;
     const uint32_t nlev = dmin == kInf ? 0u : ctl->dmax - dmin + 1;
     if (nlev <= cap) {
       // counting sort of D by new distance; a predecessor always sits in a
       // lower level (positive metrics), so one pass per level is exact
       for (uint32_t b = tt; b < nlev; b += TEAM) stw<GROUP>(&lvl[b], 0u);
-      team_sync<TEAM, GROUP>(ctl);
+      team_sync<TEAM, GROUP>(ctl, g.fault);
       for (uint32_t i = tt; i < n; i += TEAM) {
         const uint32_t d = ldw<GROUP>(&dnew[i]);
         if (d != kInf) atomicAdd(&lvl[d - dmin], 1u);
       }
-      team_sync<TEAM, GROUP>(ctl);
+      team_sync<TEAM, GROUP>(ctl, g.fault);
       if (tt < 64) {  // exclusive scan by the team's first wave
         uint32_t carry = 0;
         for (uint32_t base = 0; base < nlev; base += 64) {
@@ -1186,12 +1189,12 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
           carry += __builtin_amdgcn_readlane(inc, 63);
         }
       }
-      team_sync<TEAM, GROUP>(ctl);
+      team_sync<TEAM, GROUP>(ctl, g.fault);
       for (uint32_t i = tt; i < n; i += TEAM) {
         const uint32_t d = ldw<GROUP>(&dnew[i]);
         if (d != kInf) stw<GROUP>(&ord[atomicAdd(&lvl[d - dmin], 1u)], i);
       }
-      team_sync<TEAM, GROUP>(ctl);
+      team_sync<TEAM, GROUP>(ctl, g.fault);
       uint32_t begin = 0;
       for (uint32_t b = 0; b < nlev; ++b) {
         const uint32_t end = ldw<GROUP>(&lvl[b]);
@@ -1202,7 +1205,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
           nhn[(size_t)i * W + j] = nh_of(i, j);
         }
         begin = end;
-        team_sync<TEAM, GROUP>(ctl);
+        team_sync<TEAM, GROUP>(ctl, g.fault);
       }
     } else {
       // fixed-point sweeps (monotone union over the DAG)
@@ -1219,7 +1222,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         }
         if (any) ctl->flag[it % 3] = 1;
         if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
-        team_sync<TEAM, GROUP>(ctl);
+        team_sync<TEAM, GROUP>(ctl, g.fault);
         if (!ctl->flag[it % 3]) break;
       }
     }
@@ -1243,11 +1246,11 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   if (nd_) atomicAdd(&ctl->ndist, (unsigned long long)nd_);
   if (nn_) atomicAdd(&ctl->nnh, (unsigned long long)nn_);
   if (dh) atomicAdd(&ctl->dh, (unsigned long long)dh);
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   if (tt == 0)
     *out = spf_whatif_digest{(uint32_t)ctl->ndist, (uint32_t)ctl->nnh,
                              (uint64_t)(*B.H + ctl->dh)};
-  team_sync<TEAM, GROUP>(ctl);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
   WI_STAMP(5);
 #undef WI_STAMP
   return true;
@@ -1358,7 +1361,7 @@ __global__ __launch_bounds__(kGroupWg) void repair_group_kernel(
   const uint32_t total = *n_big;
   for (;;) {
     if (tt == 0) ctl->next = atomicAdd(cursor, 1u);
-    team_sync<TEAM, true>(ctl);
+    team_sync<TEAM, true>(ctl, g.fault);
     const uint32_t k = ldw<true>(&ctl->next);
     if (k >= total) break;  // team-uniform
     const uint2 h = big[k];
@@ -1483,11 +1486,13 @@ spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,
   CoopSssp a{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, ign, N, src,
              hop ? 1u : 0u, dist, c->d_gq.p, c->d_gq2.p, c->d_gbm.p, c->d_gctr.p};
   a.bar = c->d_gbar.p;
+  a.fault = c->d_fault.p;
   void* args[] = {&a};
+  if (const spf_status st = resident_order(c, s); st != SPF_OK) return st;
   HIP_TRY(c, launch_resident((const void*)gsssp_coop_kernel,
                              coop_blocks(c, (const void*)gsssp_coop_kernel, 1), kCoopThreads, args,
                              c->n_cu, s));
-  return SPF_OK;
+  return resident_done(c, s);
 }
 
 spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, bool hop,
@@ -1509,18 +1514,20 @@ spf_status launch_big(spf_ctx* c, spf_plan* p, uint32_t* d_dist, uint32_t* d_nh,
   HIP_TRY(c, p->b_misc.alloc(8));
   HIP_TRY(c, p->b_parent.alloc(N));
   WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
-            p->b_nbr_bit.p, N, 0u, 1u, hop ? 1u : 0u};
+            p->b_nbr_bit.p, N, 0u, 1u, hop ? 1u : 0u, c->d_fault.p};
   BigArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr, N,
                      0u, hop ? 1u : 0u, d_dist, p->b_q.p, p->b_q2.p, p->b_bm.p, p->b_ctr.p},
             g, p->d_srcs.p, p->n_src, c->d_nb_ptr.p, c->d_nb_id.p, d_dist, c->pitch, d_nh,
             p->d_nh_off.p, p->b_nbr_bit.p, p->b_nhb.p, p->b_lvl.p, p->b_order.p, p->b_misc.p,
             p->b_parent.p};
   a.sp.bar = p->b_bar.p;
+  a.sp.fault = c->d_fault.p;
   void* args[] = {&a};
+  if (const spf_status st = resident_order(c, s); st != SPF_OK) return st;
   HIP_TRY(c, launch_resident((const void*)spf_big_kernel,
                              coop_blocks(c, (const void*)spf_big_kernel, 1), kCoopThreads, args,
                              c->n_cu, s));
-  return SPF_OK;
+  return resident_done(c, s);
 }
 
 }  // namespace spfi
@@ -1699,6 +1706,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   }
   WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
             p->d_nbr_bit.p, N, p->src, p->W};
+  g.fault = c->d_fault.p;
   // 1. unfailed SPF, next hops, hash: one grid-resident launch
   {
     BaseArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr,
@@ -1707,11 +1715,14 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
                p->d_prof.p ? p->d_prof.p + 16ull * p->big_teams : nullptr, p->d_parent.p,
                p->d_sub.p};
     a.sp.bar = p->d_bar.p;
+    a.sp.fault = c->d_fault.p;
     HIP_TRY(c, hipMemsetAsync(p->d_bar.p, 0, 4 * kGridBarWords, s));
     void* args[] = {&a};
+    if (const spf_status st = resident_order(c, s); st != SPF_OK) return st;
     HIP_TRY(c, launch_resident((const void*)whatif_base_kernel,
                                coop_blocks(c, (const void*)whatif_base_kernel, 1), kCoopThreads,
                                args, c->n_cu, s));
+    if (const spf_status st = resident_done(c, s); st != SPF_OK) return st;
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
   // 2. failures
@@ -1740,8 +1751,10 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
       GroupArgs ga{g, B, p->d_big1.p, p->d_cnt.p + 3, p->d_cnt.p + 4,
                    reinterpret_cast<TeamCtl*>(p->d_ctl.p), p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
                    p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p};
+      if (const spf_status st = resident_order(c, side); st != SPF_OK) return st;
       grouped = launch_group(p->group, ga, c->n_cu, side) == hipSuccess;
       if (!grouped) (void)hipGetLastError();  // fall back to one-workgroup teams
+      else if (const spf_status st = resident_done(c, side); st != SPF_OK) return st;
     }
     if (!grouped)
     hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, side, g, B,
@@ -1863,19 +1876,18 @@ spf_status spf_whatif_solve(spf_ctx* c, uint32_t src, const uint32_t* fail_links
 spf_status spf_device_check(spf_ctx* c) {
   if (!c) return fail(c, SPF_E_INVALID, "spf_device_check: NULL context");
   HIP_TRY(c, hipSetDevice(c->device));
+  // every launch of this context may be on a caller's stream: wait for the
+  // device, then read and clear THIS context's fault word only (another
+  // context's timeout stays for its own check)
   HIP_TRY(c, hipDeviceSynchronize());
+  if (!c->d_fault.p) return SPF_OK;
   uint32_t flag = 0;
-  const uint32_t zero = 0;
-  HIP_TRY(c, hipMemcpyFromSymbol(&flag, HIP_SYMBOL(g_barrier_timeout), sizeof flag, 0,
-                                 hipMemcpyDeviceToHost));
-  bool team = false;
-  if (const spf_status st = msbfs_team_timed_out(c, &team); st != SPF_OK) return st;
-  if (!flag && !team) return SPF_OK;
-  HIP_TRY(c, hipMemcpyToSymbol(HIP_SYMBOL(g_barrier_timeout), &zero, sizeof zero, 0,
-                               hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(&flag, c->d_fault.p, sizeof flag, hipMemcpyDeviceToHost));
+  if (!flag) return SPF_OK;
+  HIP_TRY(c, hipMemset(c->d_fault.p, 0, sizeof flag));
   return fail(c, SPF_E_HIP,
               "a grid / team barrier timed out on device %d (blocks not co-resident?): the "
-              "results of the launches since the last check are invalid", c->device);
+              "results of this context's launches since the last check are invalid", c->device);
 }
 
 }  // extern "C"

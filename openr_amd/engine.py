@@ -464,6 +464,182 @@ class SpfEngine(NativeHandle):
         return ptr_, edges[: cnt.value]
 
 
+def partition_sources(nb_ptr, nb_id, srcs, n_parts: int, mode: str = "auto"):
+    """Sources to parts (spf_partition_sources, host only): (part of each
+    source [n_src] u32, the rule taken: "contiguous" | "locality").
+    nb_ptr / nb_id: distinct up neighbours of every node in CSR form."""
+    nb_ptr = np.ascontiguousarray(nb_ptr, np.uint32)
+    nb_id = np.ascontiguousarray(nb_id if len(nb_id) else [0], np.uint32)
+    srcs = np.ascontiguousarray(srcs, np.uint32)
+    code = {"auto": N.SPF_PARTITION_AUTO, "contiguous": N.SPF_PARTITION_CONTIGUOUS,
+            "locality": N.SPF_PARTITION_LOCALITY}[mode]
+    part = np.zeros(max(1, len(srcs)), np.uint32)
+    used = C.c_uint32()
+    st = N.lib.spf_partition_sources(N.ptr(nb_ptr), N.ptr(nb_id), len(nb_ptr) - 1, N.ptr(srcs),
+                                     len(srcs), n_parts, code, N.ptr(part), C.byref(used))
+    N.raise_for(st, N.global_error())
+    return part[: len(srcs)], N.PARTITION_NAMES[used.value]
+
+
+class SpfMultiPlan(NativeHandle):
+    """A source batch split over the members of an ``SpfMultiEngine``
+    (``spf_mplan``): every member's rows and bitmaps stay on its device."""
+
+    _destroy = "spf_mplan_destroy"
+
+    def __init__(self, eng: "SpfMultiEngine", srcs: Sequence[int], flags: int,
+                 mode: str = "auto") -> None:
+        self._eng = eng
+        self.srcs = np.ascontiguousarray(srcs, np.uint32)
+        self.flags = flags
+        code = {"auto": N.SPF_PARTITION_AUTO, "contiguous": N.SPF_PARTITION_CONTIGUOUS,
+                "locality": N.SPF_PARTITION_LOCALITY}[mode]
+        h = C.c_void_p()
+        eng._err(N.lib.spf_mplan_create(eng._h, N.ptr(self.srcs), len(self.srcs), flags, code,
+                                        C.byref(h)))
+        self._adopt(h)
+        self.partition = N.PARTITION_NAMES[int(N.lib.spf_mplan_partition(h))]
+        self.members = eng.size
+        self.closure_rows = [int(N.lib.spf_mplan_closure_rows(h, i)) for i in range(self.members)]
+
+    def owner(self, i: int) -> Tuple[int, int]:
+        """(member, row) holding request index i."""
+        m, r = C.c_uint32(), C.c_uint32()
+        self._eng._err(N.lib.spf_mplan_owner(self._h, i, C.byref(m), C.byref(r)))
+        return m.value, r.value
+
+    def shard_sizes(self) -> List[int]:
+        out = []
+        for i in range(self.members):
+            n = C.c_uint32()
+            self._eng._err(N.lib.spf_mplan_shard(self._h, i, C.byref(n), None, None, None))
+            out.append(n.value)
+        return out
+
+    def member_kernels(self, i: int) -> Optional[Tuple[str, bool]]:
+        """The member's plan kernels (SpfPlan.kernels), None for an idle member."""
+        n, plan = C.c_uint32(), C.c_void_p()
+        self._eng._err(N.lib.spf_mplan_shard(self._h, i, C.byref(n), C.byref(plan), None, None))
+        if not plan.value:
+            return None
+        bfs, narrow = C.c_uint32(), C.c_uint32()
+        N.raise_for(N.lib.spf_plan_kernels(plan, C.byref(bfs), C.byref(narrow)), "spf_plan_kernels")
+        return SpfPlan.BFS_KERNELS[bfs.value], bool(narrow.value)
+
+    def set_graphs(self, enable: bool) -> None:
+        self._eng._err(N.lib.spf_mplan_set_graphs(self._h, int(bool(enable))))
+
+    def execute(self) -> None:
+        self._eng._err(N.lib.spf_mplan_execute(self._h))
+
+    def synchronize(self) -> None:
+        self._eng._err(N.lib.spf_mplan_synchronize(self._h))
+
+    def digest(self) -> np.ndarray:
+        out = np.zeros(max(1, len(self.srcs)), np.uint64)
+        self._eng._err(N.lib.spf_mplan_digest(self._h, N.ptr(out, C.c_uint64)))
+        return out[: len(self.srcs)]
+
+    def read(self, i: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Request i's (dist [n_nodes], next-hop bitmaps bool [k, n_nodes]) from its owner."""
+        n = self._eng.n_nodes
+        k = len(self._eng.neighbors(int(self.srcs[i])))
+        dist = np.zeros(n, np.uint64 if self.flags & DIST64 else np.uint32)
+        nh = np.zeros(max(1, k * self._eng.pitch // 32), np.uint32)
+        self._eng._err(N.lib.spf_mplan_read(self._h, i, dist.ctypes.data, N.ptr(nh)))
+        return dist, nh_matrix(nh, 0, k, self._eng.pitch, n)
+
+    def preds(self, i: int) -> Tuple[np.ndarray, np.ndarray]:
+        n = self._eng.n_nodes
+        ptr_ = np.zeros(n + 1, np.uint32)
+        cnt = C.c_uint32()
+        self._eng._err(N.lib.spf_mplan_preds(self._h, i, N.ptr(ptr_), None, 0, C.byref(cnt)))
+        edges = np.zeros(max(1, cnt.value), np.uint32)
+        self._eng._err(N.lib.spf_mplan_preds(self._h, i, N.ptr(ptr_), N.ptr(edges), cnt.value,
+                                             C.byref(cnt)))
+        return ptr_, edges[: cnt.value]
+
+    def enable_timing(self, max_executes: int) -> None:
+        self._eng._err(N.lib.spf_mplan_enable_timing(self._h, max_executes))
+
+    def timing(self) -> Tuple[List[float], int]:
+        """(per-member summed execute ms, executes) since enable / the last call."""
+        ms = (C.c_double * self.members)()
+        n = C.c_uint32()
+        self._eng._err(N.lib.spf_mplan_timing(self._h, ms, C.byref(n)))
+        return [ms[i] for i in range(self.members)], n.value
+
+
+class SpfMultiEngine(NativeHandle):
+    """Several GPUs behind one context (``spf_mctx``): one member engine per
+    device id (ids may repeat), the graph replicated to each."""
+
+    _LEVEL = 1
+    _destroy = "spf_mctx_destroy"
+
+    def __init__(self, devices: Sequence[int]) -> None:
+        ids = (C.c_int * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        st = N.lib.spf_mctx_create(ids, len(devices), C.byref(h))
+        N.raise_for(st, N.global_error())
+        self._adopt(h)
+        self._plans: "weakref.WeakSet[NativeHandle]" = weakref.WeakSet()
+        self.devices = list(devices)
+        # member 0 answers the graph queries (neighbours, pitch)
+        self.member0 = SpfEngine(handle=C.c_void_p(N.lib.spf_mctx_member(h, 0)))
+
+    @property
+    def size(self) -> int:
+        return int(N.lib.spf_mctx_size(self._h))
+
+    def close(self) -> None:
+        for p in list(getattr(self, "_plans", ())):
+            p.close()
+        super().close()
+
+    def _err(self, st: int) -> None:
+        N.raise_for(st, (N.lib.spf_mctx_last_error(self._h) or b"").decode())
+
+    def load(self, row_ptr, col, metric, link_id, overloaded) -> None:
+        arrs = (np.ascontiguousarray(row_ptr, np.uint32), np.ascontiguousarray(col, np.uint32),
+                np.ascontiguousarray(metric, np.int32), np.ascontiguousarray(link_id, np.uint32),
+                np.ascontiguousarray(overloaded, np.uint8))
+        g = N.SpfGraph()
+        g.n_nodes = len(arrs[0]) - 1
+        g.n_edges = len(arrs[1])
+        g.row_ptr = N.ptr(arrs[0])
+        g.col = N.ptr(arrs[1])
+        g.metric = N.ptr(arrs[2], C.c_int32)
+        g.link_id = N.ptr(arrs[3])
+        g.overloaded = N.ptr(arrs[4], C.c_uint8)
+        self._err(N.lib.spf_mctx_graph_load(self._h, C.byref(g)))
+        self.member0._graph = arrs
+
+    def set_overload(self, nodes, overloaded) -> None:
+        nodes = np.ascontiguousarray(nodes, np.uint32)
+        vals = np.ascontiguousarray(overloaded, np.uint8)
+        self._err(N.lib.spf_mctx_graph_set_overload(self._h, N.ptr(nodes), N.ptr(vals, C.c_uint8),
+                                                    len(nodes)))
+        self.member0._graph[4][nodes] = vals
+
+    @property
+    def pitch(self) -> int:
+        return self.member0.pitch
+
+    @property
+    def n_nodes(self) -> int:
+        return self.member0.n_nodes
+
+    def neighbors(self, src: int) -> np.ndarray:
+        return self.member0.neighbors(src)
+
+    def plan(self, srcs: Sequence[int], hop: bool = False, dist64: bool = False,
+             mode: str = "auto") -> SpfMultiPlan:
+        p = SpfMultiPlan(self, srcs, (HOP_COUNT if hop else 0) | (DIST64 if dist64 else 0), mode)
+        self._plans.add(p)
+        return p
+
+
 def graph_from_lsdb(lsdb, area: str = "0"):
     """Flatten a packed LSDB with the LinkState facade (host side only).
     Returns (node_names, row_ptr, col, metric, link_id, overloaded)."""

@@ -224,9 +224,14 @@ class LinkState(N.NativeHandle):
     _LEVEL = 1
     _destroy = "ls_destroy"
 
-    def __init__(self, area: str = K_DEFAULT_AREA, device: int = 0) -> None:
+    def __init__(self, area: str = K_DEFAULT_AREA, device: int = 0,
+                 devices: Optional[Sequence[int]] = None) -> None:
         h = C.c_void_p()
-        st = N.lib.ls_create(area.encode(), device, C.byref(h))
+        if devices:  # several GPUs behind one state (ls_create_multi)
+            ids = (C.c_int * len(devices))(*[int(d) for d in devices])
+            st = N.lib.ls_create_multi(area.encode(), ids, len(devices), C.byref(h))
+        else:
+            st = N.lib.ls_create(area.encode(), device, C.byref(h))
         N.raise_for(st, N.global_error())
         self._adopt(h)
         self._area = area
@@ -413,6 +418,30 @@ class LinkState(N.NativeHandle):
         is first read, as the reference's one-by-one calls would."""
         arr = (C.c_char_p * max(1, len(nodes)))(*[n.encode() for n in nodes])
         self._err(N.lib.ls_prefetch_spf_results(self._h, arr, len(nodes), int(bool(useLinkMetric))))
+
+    def prefetchAllSources(self, useLinkMetric: bool = True) -> None:
+        """getSpfResult for every node as one all-sources pass split over the
+        state's GPUs (ls_prefetch_all_sources; needs ``devices=[...]``):
+        results stay on their GPU and later getSpfResult(node) calls read
+        node's share from it -- Decision::getDecisionRouteDb for every node
+        (Decision.cpp:1480-1500)."""
+        self._err(N.lib.ls_prefetch_all_sources(self._h, int(bool(useLinkMetric))))
+
+    def allSourcesDigests(self):
+        """Per-node digests (csr order) of the resident all-sources pass, on
+        the owning GPUs (spf_mplan_digest); None when no pass is valid."""
+        import numpy as np
+
+        mp = N.lib.ls_all_sources_plan(self._h)
+        if not mp:
+            return None
+        n = C.c_uint32()
+        e = C.c_uint32()
+        self._err(N.lib.ls_flatten(self._h, C.byref(n), C.byref(e)))
+        out = np.zeros(max(1, n.value), np.uint64)
+        st = N.lib.spf_mplan_digest(C.c_void_p(mp), N.ptr(out, C.c_uint64))
+        N.raise_for(st, N.global_error())
+        return out[: n.value]
 
     def debugPhaseNs(self) -> Tuple[int, int, int, int]:
         """Cumulative getSpfResult cost (ns): plan build, GPU execute + copy

@@ -149,13 +149,27 @@ class AllSourcesLayout:
         if nbrs is not None and world > 1 and n <= self.LOCALITY_MAX_NODES:
             # a rank also solves its sources' neighbours (the next-hop pass
             # reads their rows): take the locality partition when its largest
-            # closure is smaller than the contiguous blocks'
+            # closure is smaller than the contiguous blocks'.  The engine's
+            # spf_partition_sources decides (the rule spf_mplan uses too; the
+            # numpy restatement locality_partition is its test oracle)
+            from .engine import partition_sources
+
             cont = closure_sizes(self.srcs, nbrs, n)
-            loc = locality_partition(nbrs, k + row_cost, world)
-            loc_c = closure_sizes(loc, nbrs, n)
             self.closure = cont
-            if partition == "locality" or (partition == "auto" and max(loc_c) < max(cont)):
-                self.srcs, self.closure, self.partition = loc, loc_c, "locality"
+            if partition in ("auto", "locality") and row_cost == self.ROW_COST:
+                nb_ptr = np.concatenate([[0], np.cumsum([len(x) for x in nbrs])]).astype(np.uint32)
+                nb_id = (np.concatenate([np.asarray(x, np.uint32) for x in nbrs])
+                         if n else np.zeros(0, np.uint32))
+                part, used = partition_sources(nb_ptr, nb_id, np.arange(n, dtype=np.uint32), world,
+                                               partition)
+                if used == "locality":
+                    loc = [np.flatnonzero(part == r).astype(np.uint32) for r in range(world)]
+                    self.srcs, self.closure, self.partition = loc, closure_sizes(loc, nbrs, n), "locality"
+            elif partition in ("auto", "locality"):
+                loc = locality_partition(nbrs, k + row_cost, world)
+                loc_c = closure_sizes(loc, nbrs, n)
+                if partition == "locality" or max(loc_c) < max(cont):
+                    self.srcs, self.closure, self.partition = loc, loc_c, "locality"
         self.rank_of = np.zeros(n, np.int64)
         self.index_of = np.zeros(n, np.int64)
         self.nh_off = np.zeros(n, np.int64)  # word offset within the rank's send buffer

@@ -97,3 +97,26 @@ def test_prefetch_spf_results_fabric_all_neighbours():
     ls.prefetchSpfResults([me] + nbrs)
     for node in [me] + nbrs:
         assert spf_canonical(ls.getSpfResult(node)) == orc.spf(node), node
+
+
+@pytest.mark.parametrize("ulm", [True, False], ids=["metric", "hops"])
+def test_get_spf_result_on_big_plans(ulm, monkeypatch):
+    """graphs beyond the LDS-resident kernels take
+    spf_big_kernel plans; getSpfResult and the batched LFA prefetch must still
+    give the reference's results (pathLinks from the big plan's rows).
+    SPF_BIG=1 sends a small graph there."""
+    monkeypatch.setenv("SPF_BIG", "1")
+    topo = T.random_graph(60, 150, 900, max_metric=6, parallel_frac=0.2,
+                          overload_frac=0.1, link_overload_frac=0.05)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    ls = LinkState()
+    ls.updateAdjacencyDatabases(topo.lsdb)
+    for node in topo.nodes[:10]:
+        assert spf_canonical(ls.getSpfResult(node, ulm)) == orc.spf(node, ulm), node
+    me = topo.nodes[11]
+    nbrs = sorted({l.getOtherNodeName(me) for l in ls.linksFromNode(me)})
+    ls.prefetchSpfResults([me] + nbrs, ulm)
+    for node in [me] + nbrs:
+        assert spf_canonical(ls.getSpfResult(node, ulm)) == orc.spf(node, ulm), node
+    ls.close()
