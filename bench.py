@@ -138,6 +138,25 @@ class Dev:
         self.bufs = []
 
 
+_FNV_P = 0x100000001b3
+_M64 = (1 << 64) - 1
+
+
+def link_value_hash(a: str, b: str, c: str, d: str) -> int:
+    """A link's value identity for digests: FNV-1a over its ordered key
+    (node, ifname, node, ifname), each part closed by a 0x01 byte, then
+    splitmix64's finaliser -- the hash the committed KSP2 fixtures use, so
+    engine digests (spf_ksp2_digest) compare with them."""
+    f = 0xcbf29ce484222325
+    for part in (a, b, c, d):
+        for ch in part.encode():
+            f = ((f ^ ch) * _FNV_P) & _M64
+        f = ((f ^ 0x01) * _FNV_P) & _M64
+    f = ((f ^ (f >> 30)) * 0xbf58476d1ce4e5b9) & _M64
+    f = ((f ^ (f >> 27)) * 0x94d049bb133111eb) & _M64
+    return f ^ (f >> 31)
+
+
 def make_topology(name: str):
     """The all-sources workloads' synthetic topologies: (Topology, description)."""
     from openr_amd import topology as T
@@ -565,6 +584,59 @@ class Ksp2AllPairs:
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
 
+    def verify(self):
+        """Untimed, after the timed steps: every rank digests the pairs and
+        path pool its last execute left (spf_ksp2_digest, on the GPU), rank 0
+        gathers the per-source digests and compares EVERY source with the
+        oracle's (tests/golden/fullsize_wan2k_ksp2_all.npz: getKthPaths k = 1,
+        2 for all 4M pairs, oracle/spf_oracle.cpp)."""
+        from openr_amd.link_state import LinkState
+
+        gold = ROOT / "tests" / "golden" / "fullsize_wan2k_ksp2_all.npz"
+        ls = LinkState(device=-1)
+        ls.updateAdjacencyDatabases(self.topo.lsdb)
+        lid = ls.flatten()[4]
+        lh = np.zeros(int(lid.max()) + 1, np.uint64)
+        for l in np.unique(lid):
+            (a, b), (c, d) = ls._link(int(l)).orderedNames
+            lh[int(l)] = link_value_hash(a, b, c, d)
+        ls.close()
+        d_lh = self.dev.buf(len(lh), np.int64)
+        if d_lh.t is not None:
+            import torch
+
+            d_lh.t.copy_(torch.from_numpy(lh.view(np.int64)))
+        else:
+            d_lh.h.upload(lh.view(np.int64))
+        m = len(self.srcs)
+        dg = self.dev.buf(max(1, m), np.int64, zero=True)
+        self.plan.digest(self.d_pairs.ptr, self.d_pool.ptr, d_lh.ptr, dg.ptr, self.dev.stream())
+        self.dev.sync()
+        self.eng.check()
+        if self.world > 1:
+            from openr_amd.sharding import gather_padded
+
+            got = gather_padded(dg.t, m)
+            parts = [g.cpu().numpy().view(np.uint64) for g in got] if self.rank == 0 else None
+        else:
+            parts = [dg.numpy()[:m].view(np.uint64)]
+        if self.rank != 0:
+            return None
+        digest = np.zeros(self.n, np.uint64)
+        for r, part in enumerate(parts):
+            digest[np.arange(r, self.n, self.world)] = part[: len(range(r, self.n, self.world))]
+        if not gold.exists():
+            return {"checked_sources": 0, "note": f"no {gold.name}"}
+        z = np.load(gold)
+        want = np.zeros(self.n, np.uint64)
+        want[z["srcs"].astype(np.int64)] = z["digest"].astype(np.uint64)
+        bad = np.nonzero(digest[z["srcs"]] != want[z["srcs"]])[0]
+        return {"checked_sources": int(len(z["srcs"])),
+                "checked_pairs": int(len(z["srcs"])) * self.n, "mismatches": int(len(bad)),
+                "first_mismatch": int(z["srcs"][bad[0]]) if len(bad) else None,
+                "against": f"tests/golden/{gold.name} (oracle getKthPaths k=1,2 of every pair), "
+                           "engine digests from spf_ksp2_digest on each rank's last execute"}
+
     def kernel_ms(self):
         a, b, cnt = self.plan.timing()
         cnt_h = self.d_cnt.numpy()
@@ -682,6 +754,48 @@ class WhatIfAllLinks:
 
     def enable_timing(self, k: int) -> None:
         self.plan.enable_timing(k)
+
+    def verify(self):
+        """Untimed, after the timed steps: the digests of the failures the
+        committed fixture holds (tests/golden/fullsize_ba250k_whatif.npz:
+        16.5k of the step's ~1M failures -- uniform and tight links and the
+        3000 shortest-path-tree links with the largest subtrees, oracle
+        runSpf(src, true, {l})), read from the last execute's output on the
+        rank that computed them, compared at rank 0; plus the unfailed
+        digest."""
+        from openr_amd.engine import DIGEST_DTYPE
+
+        gold = ROOT / "tests" / "golden" / "fullsize_ba250k_whatif.npz"
+        if not gold.exists():
+            return {"checked_failures": 0, "note": f"no {gold.name}"}
+        z = np.load(gold)
+        self.dev.sync()
+        self.eng.check()
+        mine = self.d_out.numpy().view(DIGEST_DTYPE)[: self.units]
+        base = self.d_base.numpy().view(DIGEST_DTYPE)[0]
+        pos = np.searchsorted(self.links, z["links"])
+        ok = (pos < len(self.links)) & (self.links[np.minimum(pos, len(self.links) - 1)] == z["links"])
+        sel = np.nonzero(ok)[0]
+        bad_local = sum(int(np.count_nonzero(mine[f][pos[sel]] != z[f][sel]))
+                        for f in ("n_dist_changed", "n_nh_changed", "hash"))
+        base_ok = (int(base["n_dist_changed"]), int(base["n_nh_changed"]), int(base["hash"])) == \
+            tuple(int(x) for x in z["base"])
+        checked = len(sel)
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            t = torch.tensor([checked, bad_local, 0 if base_ok else 1], dtype=torch.int64,
+                             device=self.dev.device)
+            dist.all_reduce(t)
+            checked, bad_local, base_bad = (int(x) for x in t.tolist())
+            base_ok = base_bad == 0
+        if self.rank != 0:
+            return None
+        return {"checked_failures": int(checked), "mismatches": int(bad_local) + (0 if base_ok else 1),
+                "unfailed_digest_ok": bool(base_ok),
+                "against": f"tests/golden/{gold.name} (oracle runSpf(\"0\", true, {{l}}) digests "
+                           "of 16.5k failures incl. the largest repairs), the step's own output"}
 
     def kernel_ms(self):
         a, b, cnt = self.plan.timing()
@@ -989,8 +1103,8 @@ def main() -> None:
 
     roofline = roofline_block(wl, kms, launch_ms, args.workload, rank)
     if parity and parity.get("mismatches"):
-        print(f"bench: PARITY FAILURE: {parity['mismatches']} of {parity['checked_sources']} "
-              f"checked results differ from the oracle", file=sys.stderr)
+        print(f"bench: PARITY FAILURE: {parity['mismatches']} checked results differ from "
+              f"the oracle ({parity})", file=sys.stderr)
     out = {
         "metric": METRIC if isinstance(wl, AllSources) else (
             "all-pairs KSP2 (k=1,2 edge-disjoint paths) pairs/sec, 2k-node WAN"

@@ -167,8 +167,19 @@ spf_status spf_plan_traffic(const spf_plan* plan, uint64_t* bfs_bytes, uint64_t*
 spf_status spf_plan_traffic_phases(const spf_plan* plan, uint64_t* bytes);
 
 /* Execute on device buffers: d_dist = [n_src][pitch] u32, d_nh = nh words.
- * Enqueued on `stream` (a hipStream_t, NULL = the context's stream); no host
- * synchronisation, no allocation: capturable into a hipGraph. */
+ * Enqueued on `stream` (a hipStream_t); NULL = the context's stream, a
+ * BLOCKING stream, so work the caller put on the legacy null stream before
+ * (a hipMemset / hipMemcpy of the outputs) is ordered before the execute.  A
+ * caller's own non-blocking stream gets no such ordering: order it yourself.
+ * Steady state (same graph epoch as the previous execute of the plan): no
+ * host synchronisation, no allocation -- capturable into a hipGraph
+ * (spf_mplan_set_graphs does).  The FIRST execute after an in-place patch
+ * (spf_graph_set_overload / _metric) re-derives the plan on the host and
+ * uploads its tables with a stream synchronisation, and a big plan's first
+ * execute allocates its scratch: run one execute on a new epoch before
+ * capturing.  Launches whose workgroups wait on each other (team BFS, grid
+ * barriers) are ordered after any other such launch of the process on the
+ * same device (see spf_device_check). */
 spf_status spf_plan_execute(spf_plan* plan, uint32_t* d_dist, uint32_t* d_nh,
                             void* stream);
 /* Per-source digests of an execute's output (d_dist / d_nh as passed to
@@ -288,6 +299,16 @@ void spf_ksp2_plan_destroy(spf_ksp2_plan* plan);
  *   [2] bit 0 = overflow.  No host synchronisation, no allocation. */
 spf_status spf_ksp2_execute(spf_ksp2_plan* plan, spf_ksp2_pair* d_pairs, uint32_t* d_pool,
                             uint64_t pool_words, uint64_t* d_counters, void* stream);
+/* Per-source digests of an execute's output, on the GPU (enqueued on
+ * `stream`): d_out[i] = sum mod 2^64 over destinations d of
+ * h(i, d) + mix(d + 1), h = FNV-1a over (0x1000 + n_paths[k], then per path
+ * 0x2000 + length and link_hash[link] of each link) for k = 1, 2 and mix =
+ * splitmix64's finaliser.  link_hash[id] identifies link `id` by value (the
+ * caller hashes its ordered (node, ifname) key), so digests compare across
+ * engines and the oracle.  What the parity checks of all-pairs KSP2 compare;
+ * no reference counterpart. */
+spf_status spf_ksp2_digest(spf_ksp2_plan* plan, const spf_ksp2_pair* d_pairs, const uint32_t* d_pool,
+                           const uint64_t* d_link_hash, uint64_t* d_out, void* stream);
 /* HIP-event kernel timing of the next `max_executes` executes: summed ms of
  * the k = 1 SPF kernel and of the KSP2 kernel. */
 spf_status spf_ksp2_enable_timing(spf_ksp2_plan* plan, uint32_t max_executes);
@@ -467,13 +488,17 @@ spf_status spf_mplan_timing(spf_mplan* mp, double* ms, uint32_t* n);
 spf_status spf_debug_stamps(spf_ctx* ctx, uint64_t* out, uint32_t cap, uint32_t* n);
 
 /* Waits for every launch on the context's device and reports whether a
- * grid-resident kernel's barrier (spf_big_kernel, the what-if unfailed pass,
- * the global-memory SSSP, the what-if group teams) gave up waiting: its spin
- * is bounded so a block that never arrives cannot hang the GPU, and the
- * outputs of that launch are then invalid.  SPF_E_HIP (and the flag is
- * cleared) when one did; SPF_OK otherwise.  The synchronous convenience calls
- * (spf_solve, spf_whatif_solve, spf_whatif_stats, ...) check it themselves.
- * No reference counterpart. */
+ * grid-resident kernel's barrier of THIS context (spf_big_kernel, the
+ * what-if unfailed pass, the global-memory SSSP, the what-if group teams,
+ * the team BFS) gave up waiting: its spin is bounded so a block that never
+ * arrives cannot hang the GPU, and the outputs of that launch are then
+ * invalid.  Each context has its own fault word, so another context's
+ * timeout is neither reported nor cleared here.  SPF_E_HIP (and the word is
+ * cleared) when one did; SPF_OK otherwise.  Such launches of one process
+ * are serialised per device (one cannot starve another of CUs), so a timeout
+ * means a fault or a foreign process holding the CUs.  The synchronous
+ * convenience calls (spf_solve, spf_whatif_solve, spf_whatif_stats, ...)
+ * check it themselves.  No reference counterpart. */
 spf_status spf_device_check(spf_ctx* ctx);
 
 /* ---- counters ----------------------------------------------------------- */

@@ -187,6 +187,7 @@ PROTOTYPES = {
     "spf_ksp2_plan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.POINTER(_vp)]),
     "spf_ksp2_plan_destroy": (None, [_vp]),
     "spf_ksp2_execute": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "spf_ksp2_digest": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "spf_ksp2_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_ksp2_timing": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_double), _u32p]),
     "spf_ksp2_solve": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _u32p, C.c_uint64, _u64p]),

@@ -544,6 +544,41 @@ size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw,
 
 }  // namespace
 
+namespace {
+__device__ __forceinline__ uint64_t dg_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t dg_fnv(uint64_t h, uint64_t x) { return (h ^ x) * 0x100000001b3ULL; }
+
+// spf_ksp2_digest: one thread per (source, destination) walks the pair's two
+// path lists; the per-source sum is commutative (atomic order-free)
+__global__ __launch_bounds__(256) void ksp2_digest_kernel(const spf_ksp2_pair* __restrict__ pairs,
+                                                          const uint32_t* __restrict__ pool,
+                                                          const uint64_t* __restrict__ link_hash,
+                                                          uint32_t n_src, uint32_t n,
+                                                          unsigned long long* __restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = blockIdx.y;
+  if (i >= n_src || t >= n) return;
+  const uint32_t d = (uint32_t)t;
+  const spf_ksp2_pair r = pairs[(size_t)i * n + d];
+  uint64_t h = 0xcbf29ce484222325ULL;
+  for (int k = 0; k < 2; ++k) {
+    h = dg_fnv(h, 0x1000u + r.n_paths[k]);
+    uint32_t at = r.first[k];
+    for (uint32_t q = 0; q < r.n_paths[k]; ++q) {
+      const uint32_t len = pool[at];
+      h = dg_fnv(h, 0x2000u + len);
+      for (uint32_t x = 0; x < len; ++x) h = dg_fnv(h, link_hash[pool[at + 2 + x]]);
+      at = pool[at + 1];
+    }
+  }
+  atomicAdd(&out[i], (unsigned long long)(h + dg_mix64((uint64_t)d + 1)));
+}
+}  // namespace
+
 struct spf_ksp2_plan {
   spf_ctx* ctx = nullptr;
   uint32_t n_src = 0, lw = 0;
@@ -656,6 +691,20 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
 }
 
 void spf_ksp2_plan_destroy(spf_ksp2_plan* p) { delete p; }
+
+spf_status spf_ksp2_digest(spf_ksp2_plan* p, const spf_ksp2_pair* d_pairs, const uint32_t* d_pool,
+                           const uint64_t* d_link_hash, uint64_t* d_out, void* stream) {
+  if (!p || !d_pairs || !d_pool || !d_link_hash || !d_out)
+    return fail(p ? p->ctx : nullptr, SPF_E_INVALID, "spf_ksp2_digest: NULL argument");
+  spf_ctx* c = p->ctx;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  HIP_TRY(c, hipMemsetAsync(d_out, 0, 8ull * p->n_src, s));
+  if (!p->n_src || !c->N) return SPF_OK;
+  hipLaunchKernelGGL(ksp2_digest_kernel, dim3((c->N + 255) / 256, p->n_src), dim3(256), 0, s, d_pairs,
+                     d_pool, d_link_hash, p->n_src, c->N, reinterpret_cast<unsigned long long*>(d_out));
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
 
 spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* d_pool,
                             uint64_t pool_words, uint64_t* d_counters, void* stream) {

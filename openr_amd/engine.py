@@ -213,6 +213,14 @@ class Ksp2Plan(NativeHandle):
                                               pool_words, C.c_void_p(d_counters),
                                               C.c_void_p(stream) if stream else None))
 
+    def digest(self, d_pairs: int, d_pool: int, d_link_hash: int, d_out: int,
+               stream: int = 0) -> None:
+        """Enqueue per-source u64 digests of an execute's pairs and pool into
+        d_out (spf_ksp2_digest; d_link_hash: u64 value hash per link id)."""
+        self._eng._err(N.lib.spf_ksp2_digest(self._h, C.c_void_p(d_pairs), C.c_void_p(d_pool),
+                                             C.c_void_p(d_link_hash), C.c_void_p(d_out),
+                                             C.c_void_p(stream) if stream else None))
+
     def enable_timing(self, max_executes: int) -> None:
         self._eng._err(N.lib.spf_ksp2_enable_timing(self._h, max_executes))
 

@@ -17,6 +17,8 @@ Each fixture is ``tests/golden/fullsize_<name>.npz`` holding the oracle's
 * ``wan2k_ksp2`` -- config 4: getKthPaths(s, d, 1) and (s, d, 2)
   (LinkState.cpp:762-791) for 256 sources x every destination, per-source
   digests plus per-pair digests of 8 of them.
+* ``wan2k_ksp2_all`` -- the same for EVERY source (4M pairs, per-source
+  digests): bench.py's wan_ksp2 line checks its whole output against it.
 * ``ba250k_whatif`` -- config 5: runSpf("0", true, {l}) digests for ~16k
   single-link failures: uniform random links, random tight links and the
   3000 shortest-path-tree links with the largest subtrees (every failure
@@ -61,6 +63,7 @@ WORKLOADS = {
     "fabric_rtt": fabric_rtt,
     "wan2k_spf": lambda: T.wan(2000, 1000, seed=1),
     "wan2k_ksp2": lambda: T.wan(2000, 1000, seed=1),
+    "wan2k_ksp2_all": lambda: T.wan(2000, 1000, seed=1),
     "ba250k_whatif": lambda: T.barabasi_albert(250_000, 4, seed=1),
     "ba250k_spf": lambda: T.barabasi_albert(250_000, 4, seed=1),
 }
@@ -155,6 +158,13 @@ def make(name: str, threads: int) -> None:
         out["digest"] = np.concatenate([d, rest])
         out["pair_digest"] = pairs  # [8, n]
         meta["oracle"] = "getKthPaths k=1,2 (trace + runSpf with ignore set)"
+    elif name == "wan2k_ksp2_all":
+        # every source (config 4's whole workload, 4M pairs): what bench.py's
+        # wan_ksp2 line checks in-bench
+        srcs = np.arange(n, dtype=np.uint32)
+        out["srcs"] = srcs
+        out["digest"] = ksp2_digests(orc, table, srcs, threads=threads)
+        meta["oracle"] = "getKthPaths k=1,2 (trace + runSpf with ignore set), every source"
     elif name == "ba250k_whatif":
         links, big = ba_failures(ls, names, csr, rng)
         fails = [(ls._link(int(l))._n1, ls._link(int(l))._if1) for l in links]

@@ -131,3 +131,60 @@ def test_large_graph_spf_ecmp_ba250k_matches_oracle(big, monkeypatch):
         res = eng.solve(srcs)
         got = digest_planar(res.dist, res.nh, res.nh_off, res.words, res.pitch)
     _report(got, g["digest"][:n], "ba250k per-source digests", [names[int(s)] for s in srcs])
+
+
+def test_ksp2_wan2k_every_source_engine_digest_matches_oracle():
+    """Config 4's whole output -- getKthPaths(s, d, 1|2) for all 4M pairs --
+    reduced on the GPU (spf_ksp2_digest, the reduction bench.py's wan_ksp2
+    line checks) against the oracle's digests of every source
+    (fullsize_wan2k_ksp2_all.npz), and the GPU reduction equals the oracle's
+    reduction (digest_ksp2) of the same output on the 256-source fixture."""
+    import sys
+
+    from openr_amd.hiprt import DeviceArray
+
+    sys.path.insert(0, str(GOLDEN.parent.parent))
+    from bench import link_value_hash
+
+    meta, g = golden("wan2k_ksp2_all")
+    ls, names, csr, cd = _make("wan2k_ksp2_all")
+    assert cd == meta["csr_digest"]
+    lid = csr[3]
+    lh = np.zeros(int(lid.max()) + 1, np.uint64)
+    for l in np.unique(lid):
+        (a, b), (c, d) = ls._link(int(l)).orderedNames
+        lh[int(l)] = link_value_hash(a, b, c, d)
+        assert int(lh[int(l)]) == link_keyhash(link_key(ls._link(int(l))))
+    srcs = g["srcs"]
+    n = len(names)
+    with _engine(csr) as eng:
+        p = eng.ksp2_plan(srcs)
+        pairs = DeviceArray(len(srcs) * n * 4, np.uint32)
+        cnt = DeviceArray(4, np.uint64, zero=True)
+        words = 1 << 20
+        pool = DeviceArray(words, np.uint32)
+        p.execute(pairs.ptr, pool.ptr, words, cnt.ptr)
+        eng.check()
+        used = int(cnt.numpy()[0])
+        if used > words:  # size the pool and run again
+            pool.free()
+            words = used + 1024
+            pool = DeviceArray(words, np.uint32)
+            p.execute(pairs.ptr, pool.ptr, words, cnt.ptr)
+            eng.check()
+        assert not (int(cnt.numpy()[2]) & 1)
+        d_lh = DeviceArray(len(lh), np.uint64)
+        d_lh.upload(lh)
+        dg = DeviceArray(len(srcs), np.uint64, zero=True)
+        p.digest(pairs.ptr, pool.ptr, d_lh.ptr, dg.ptr)
+        eng.check()
+        got = dg.numpy()
+        # the GPU reduction equals the oracle's reduction of the same output
+        sub = np.arange(0, len(srcs), 97)
+        host = digest_ksp2(pairs.numpy().view(np.uint32).reshape(-1, 4)[
+            (sub[:, None] * n + np.arange(n)[None, :]).ravel()], pool.numpy()[:used], len(sub), n, lh)
+        assert np.array_equal(host, got[sub])
+        p.close()
+        for b in (pairs, cnt, pool, d_lh, dg):
+            b.free()
+    _report(got, g["digest"], "KSP2 per-source digests (every source)", [names[int(s)] for s in srcs])
