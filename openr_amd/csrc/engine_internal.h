@@ -153,6 +153,7 @@ struct spf_ctx {
   spfi::DevBuf<uint32_t> d_mp_dep;  // per slice: the slices its nodes' out-edges reach (CSR)
   uint32_t mp_slots = 0, mp_ovf_at = 0;
   bool mp_redo = true;
+  bool mp_u8 = false;  // u8 labels (four sources per LDS word)
   uint64_t mp_epoch = ~0ull;
   spfi::DevBuf<unsigned long long> d_stamps;  // BFS kernel phase stamps (SPF_STAMPS=1)
   // spf_plan_preds' pinned staging: lives with the context (the facade makes
@@ -249,6 +250,7 @@ spf_status launch_sssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, bool
 // graph epoch (plan build), launch_mssp() enqueues it (+ the overflow redo
 // pass over `redo` = [1 + rows] words of plan scratch).
 uint32_t mssp_words(const spf_ctx* c);
+uint32_t mssp_sources(const spf_ctx* c);
 // Team BFS (msbfs_team.hip): the team size for a unit plan of `rows` rows
 // (0: not used), its tables, its launch, its barrier-timeout flag.
 uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows);

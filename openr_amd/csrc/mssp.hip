@@ -31,6 +31,14 @@
 //  change bit, so they are never expanded; each source's own out-edges are
 //  applied once at the start (a drained source is expanded, :831-838).
 //
+//  u8 labels (graphs whose metrics and hop diameter keep distances small:
+//  RTT-derived fabric metrics, max(rtt/100, 1) <= 30 over <= 4 hops): four
+//  sources per word, twice the sources per LDS byte -- a workgroup takes 4 SD
+//  sources instead of 2 SD, so the pass needs half the workgroup rounds.  A
+//  word is split into two u16x2 halves by v_perm (sources 0, 2 and 1, 3),
+//  folded with the same v_pk_add_u16 clamp / v_pk_min_u16 pair into u16
+//  accumulators, and packed back (clamped to 0xFF) when the node updates.
+//
 //  u16 labels: clamped sums are min(true, 0xFFFF) exactly, so a true
 //  distance >= 0xFFFF shows up as some node in [0xFFFF - max metric,
 //  0xFFFF) on its path; such rows are listed in `redo` and recomputed by
@@ -61,18 +69,27 @@ constexpr size_t kMpMaxLds = 160 * 1024;
 constexpr size_t kMpStaticLds = 256;  // the kernel's own static LDS (__syncthreads_or)
 constexpr uint32_t kMpAhead = 8;      // packed in-edge loads per group (two groups in flight)
 
-// LDS minimum of one u16 half of a word (CAS loop: two sources share a word)
-__device__ void lds_min16(uint32_t* p, uint32_t half, uint32_t val) {
+// LDS minimum of one label of a word (CAS loop: several sources share a
+// word): label `slot` of width B bits (16: two per word, 8: four per word)
+template <int B>
+__device__ void lds_min_label(uint32_t* p, uint32_t slot, uint32_t val) {
+  constexpr uint32_t M = (1u << B) - 1u;
+  const uint32_t sh = slot * B;
+  val = min(val, M);
   uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   for (;;) {
-    const uint32_t cur = half ? old >> 16 : old & 0xFFFFu;
+    const uint32_t cur = (old >> sh) & M;
     if (val >= cur) return;
-    const uint32_t nw = half ? (old & 0xFFFFu) | (val << 16) : (old & 0xFFFF0000u) | val;
+    const uint32_t nw = (old & ~(M << sh)) | (val << sh);
     const uint32_t got = atomicCAS(p, old, nw);
     if (got == old) return;
     old = got;
   }
 }
+
+// u8 labels: the two u16x2 halves of a word (bytes 0, 2 and bytes 1, 3)
+__device__ __forceinline__ uint32_t u8_lo(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c020c00u); }
+__device__ __forceinline__ uint32_t u8_hi(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); }
 
 template <int SD>
 __device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&d)[SD]) {
@@ -91,7 +108,7 @@ __device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&d)[SD])
   }
 }
 
-template <int SD>
+template <int SD, bool U8>
 __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     const uint32_t* __restrict__ sell_ptr, const uint32_t* __restrict__ ell,
     const uint32_t* __restrict__ smap, uint32_t slots, const uint32_t* __restrict__ row_ptr,
@@ -101,7 +118,10 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     uint32_t ovf_at, uint32_t* __restrict__ redo, uint32_t alt,
     const uint32_t* __restrict__ dep /* [n_slices + 1] offsets, then out-slice lists; null: no skipping */,
     unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */) {
-  constexpr uint32_t S = 2 * SD;
+  constexpr uint32_t S = (U8 ? 4 : 2) * SD;  // sources per workgroup
+  constexpr uint32_t LPW = U8 ? 4 : 2;       // labels per word
+  constexpr uint32_t LB = U8 ? 8 : 16;       // label bits
+  constexpr uint32_t LM = (1u << LB) - 1u;   // not reached / saturated
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t bw = (N + 32) / 32;  // change-bitmap words (nodes 0..N)
   uint32_t* dist = reinterpret_cast<uint32_t*>(smem);  // [(N + 1) * SD]
@@ -119,7 +139,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
   for (uint32_t i = tid; i < 3 * sw; i += kMpThreads) sbits[i] = 0;
   if (tid < 3) flag[tid] = 0;
   __syncthreads();
-  if (tid < nb) lds_min16(&dist[rows_src[r0 + tid] * SD + tid / 2], tid & 1, 0);
+  if (tid < nb) lds_min_label<LB>(&dist[rows_src[r0 + tid] * SD + tid / LPW], tid % LPW, 0);
   __syncthreads();
   // each source's own out-edges, once (a wave per source): the source is
   // expanded even when drained; its label 0 never changes again
@@ -128,7 +148,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     const uint32_t e1 = row_ptr[s + 1];
     for (uint32_t e = row_ptr[s] + lane; e < e1; e += 64) {
       const uint32_t v = col[e];
-      lds_min16(&dist[v * SD + si / 2], si & 1, wt[e]);
+      lds_min_label<LB>(&dist[v * SD + si / LPW], si % LPW, wt[e]);
       if (!ovl[v]) atomicOr(&bits[v >> 5], 1u << (v & 31));
     }
   }
@@ -190,9 +210,12 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         continue;  // no in-neighbour changed since this slice's last sweep
       if (stats && lane == 0) atomicAdd(&stats[3], 1ull);  // slices swept (diagnostics)
       const uint32_t v = sl * 64 + lane;
-      uint32_t acc[SD];
+      // u16x2 accumulators: SD of them (u16 labels), 2 SD (u8 labels: the
+      // lo / hi halves of each word)
+      constexpr int NA = U8 ? 2 * SD : SD;
+      uint32_t acc[NA];
 #pragma unroll
-      for (int q = 0; q < SD; ++q) acc[q] = 0xFFFFFFFFu;
+      for (int q = 0; q < NA; ++q) acc[q] = 0xFFFFFFFFu;
       bool got = false;
       const uint32_t* ep = ell + b + lane;
       // the slice's packed in-edges kMpAhead columns at a time, the next
@@ -221,8 +244,16 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         for (int t = 0; t < (int)kMpAhead; ++t)
           if (c[t]) {
             const uint32_t wp = __builtin_amdgcn_perm(e[t], e[t], 0x03020302u);  // w | w << 16
+            if constexpr (U8) {
 #pragma unroll
-            for (int q = 0; q < SD; ++q) acc[q] = min2(acc[q], add_sat2(d[t][q], wp));
+              for (int q = 0; q < SD; ++q) {
+                acc[2 * q] = min2(acc[2 * q], add_sat2(u8_lo(d[t][q]), wp));
+                acc[2 * q + 1] = min2(acc[2 * q + 1], add_sat2(u8_hi(d[t][q]), wp));
+              }
+            } else {
+#pragma unroll
+              for (int q = 0; q < SD; ++q) acc[q] = min2(acc[q], add_sat2(d[t][q], wp));
+            }
             got = true;
           }
       };
@@ -253,7 +284,14 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         bool dec = false;
 #pragma unroll
         for (int q = 0; q < SD; ++q) {
-          const uint32_t o = dv[q], nn = min2(o, acc[q]);
+          const uint32_t o = dv[q];
+          uint32_t nn;
+          if constexpr (U8) {  // per byte min(old, clamp(acc, 0xFF)), packed back
+            const uint32_t lo = min2(u8_lo(o), acc[2 * q]), hi = min2(u8_hi(o), acc[2 * q + 1]);
+            nn = lo | (hi << 8);
+          } else {
+            nn = min2(o, acc[q]);
+          }
           if (nn != o) {
             dv[q] = nn;
             dec = true;
@@ -302,9 +340,9 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         const uint32_t v = 4 * q + t;
         uint32_t d = kInf;
         if (v < N) {
-          const uint32_t x = dist[v * SD + si / 2];
-          const uint32_t h = (si & 1) ? x >> 16 : x & 0xFFFFu;
-          if (h != 0xFFFFu) {
+          const uint32_t x = dist[v * SD + si / LPW];
+          const uint32_t h = (x >> ((si % LPW) * LB)) & LM;
+          if (h != LM) {
             d = h;
             ovf |= h >= ovf_at;
           }
@@ -323,8 +361,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
   }
 }
 
-template <int SD>
-size_t mp_lds(uint32_t N) {
+size_t mp_lds(uint32_t N, uint32_t SD) {
   return 4ull * (N + 1) * SD + 4ull * 3 * ((N + 32) / 32) + 16 + 4ull * 3 * (((N + 63) / 64 + 31) / 32);
 }
 
@@ -431,7 +468,17 @@ spf_status mssp_prepare(spf_ctx* c) {
     }
     bound = std::min<uint64_t>(bound, 2ull * ecc * c->max_metric);
   }
-  c->mp_ovf_at = 0xFFFFu - c->max_metric;
+  // u8 labels when distances stay far below 255 on this graph: metrics below
+  // 128 and the hop bound under 2 x 255 (rows that still reach the
+  // saturation band are redone on u32 labels, as for u16).  SPF_MSSP_U8=0/1
+  // forces (A/B, tests).
+  {
+    uint64_t hop_bound = bound;
+    if (drained) hop_bound = ~0ull;
+    c->mp_u8 = c->max_metric < 128 && hop_bound < 510;
+    if (const char* e = std::getenv("SPF_MSSP_U8")) c->mp_u8 = e[0] == '1' && c->max_metric < 255;
+  }
+  c->mp_ovf_at = (c->mp_u8 ? 0xFFu : 0xFFFFu) - c->max_metric;
   c->mp_redo = bound >= c->mp_ovf_at;
   c->mp_slots = slots;
   HIP_TRY(c, c->d_mp_ell.upload(ell.data(), ell.size(), c->stream));
@@ -442,10 +489,16 @@ spf_status mssp_prepare(spf_ctx* c) {
   return SPF_OK;
 }
 
+// sources per workgroup: two labels per LDS word (u16) or four (u8); valid
+// once mssp_prepare ran for the current graph epoch
+uint32_t mssp_sources(const spf_ctx* c) { return (c->mp_u8 ? 4u : 2u) * mssp_words(c); }
+
 spf_status mssp_set_lds_limits(spf_ctx* c) {
   const int lim = (int)(kMpMaxLds - kMpStaticLds);
-  for (const void* f : {(const void*)mssp_kernel<1>, (const void*)mssp_kernel<2>,
-                        (const void*)mssp_kernel<4>, (const void*)mssp_kernel<8>})
+  for (const void* f : {(const void*)mssp_kernel<1, false>, (const void*)mssp_kernel<2, false>,
+                        (const void*)mssp_kernel<4, false>, (const void*)mssp_kernel<8, false>,
+                        (const void*)mssp_kernel<1, true>, (const void*)mssp_kernel<2, true>,
+                        (const void*)mssp_kernel<4, true>, (const void*)mssp_kernel<8, true>})
     HIP_TRY(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
   return SPF_OK;
 }
@@ -463,7 +516,7 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
     HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, (64 * 16 + 1) * 8, s));
   }
-  const uint32_t S = 2 * sd;
+  const uint32_t S = mssp_sources(c);
   const dim3 g((rows + S - 1) / S), b(kMpThreads);
   const uint32_t N = c->N;
   uint32_t* rd = c->mp_redo ? redo : nullptr;
@@ -472,7 +525,13 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   const char* ke = std::getenv("SPF_MSSP_SKIP");  // A/B: slice-level dirt (default on)
   const uint32_t* dep = ke && ke[0] == '0' ? nullptr : c->d_mp_dep.p;
 #define MP_LAUNCH(SDV)                                                                            \
-  hipLaunchKernelGGL(mssp_kernel<SDV>, g, b, mp_lds<SDV>(N), s, c->d_sell_ptr.p, c->d_mp_ell.p,   \
+  if (c->mp_u8) {                                                                                 \
+    MP_LAUNCH2(SDV, true);                                                                        \
+  } else {                                                                                        \
+    MP_LAUNCH2(SDV, false);                                                                       \
+  }
+#define MP_LAUNCH2(SDV, U8V)                                                                      \
+  hipLaunchKernelGGL((mssp_kernel<SDV, U8V>), g, b, mp_lds(N, SDV), s, c->d_sell_ptr.p, c->d_mp_ell.p, \
                      c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
                      c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, alt, dep, c->d_stamps.p)
   switch (sd) {
@@ -482,6 +541,7 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
     default: MP_LAUNCH(1); break;
   }
 #undef MP_LAUNCH
+#undef MP_LAUNCH2
   HIP_TRY(c, hipGetLastError());
   if (c->mp_redo)
     return launch_sssp(c, rows_src, rows, false, nullptr, D, s, nullptr, nullptr, Dn, redo);

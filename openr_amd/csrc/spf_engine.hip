@@ -2506,7 +2506,7 @@ spf_status spf_plan_traffic_phases(const spf_plan* p, uint64_t* bytes) {
     bfs = groups * (csr + N) + (p->expand ? 0ull : rows * c->pitch * 4ull) +
           (p->narrow ? rows * c->npitch : 0ull);
   } else if (p->mp) {  // per workgroup: the packed ELL + slice map once; rows written once
-    const uint64_t S = 2ull * mssp_words(c);
+    const uint64_t S = mssp_sources(c);
     const uint64_t groups = (rows + S - 1) / S;
     bfs = groups * (4ull * c->sell_ptr.back() + 4ull * c->sell_ptr.size() + 4ull * (N + 1) + N) +
           rows * (4ull * c->pitch + (p->narrow ? c->npitch : 0ull));

@@ -24,10 +24,15 @@ WEIGHTED = [
 ]
 
 
+@pytest.mark.parametrize("u8", ["0", "1"], ids=["u16", "u8"])
 @pytest.mark.parametrize("sd", ["1", "2", "4", "8"])
 @pytest.mark.parametrize("name,make", WEIGHTED, ids=[w[0] for w in WEIGHTED])
-def test_mssp_every_width_matches_oracle(name, make, sd, monkeypatch):
+def test_mssp_every_width_matches_oracle(name, make, sd, u8, monkeypatch):
+    """Every LDS row width, with u16 labels (2 sources per word) and u8
+    labels (4 per word; forced here even where distances pass 255 -- those
+    rows take the redo path)."""
     monkeypatch.setenv("SPF_MSSP_SD", sd)
+    monkeypatch.setenv("SPF_MSSP_U8", u8)
     names, eng, orc = load(make())
     assert eng.plan([0]).kernels()[0] == "mssp_kernel"
     compare(names, eng, orc, list(range(len(names))))
@@ -50,6 +55,23 @@ def test_mssp_u16_overflow_rows_are_redone(drained):
     res = compare(names, eng, orc, list(range(len(names))))
     d = res.dist[res.dist != 0xFFFFFFFF]
     assert d.max() > 0xFFFF  # the redo path was needed
+
+
+def test_mssp_u8_is_the_default_on_rtt_fabrics_and_overflow_rows_are_redone(monkeypatch):
+    """RTT-derived fabric metrics (<= 30 over <= 4 hops) take u8 labels by
+    default; a long weighted line forced onto u8 labels (distances up to
+    ~2000) gets its saturated rows recomputed on u32 labels."""
+    from openr_amd import _native as N
+
+    names, eng, orc = load(T.fabric_rtt(num_sws=600))
+    assert eng.plan([0]).kernels()[0] == "mssp_kernel"
+    compare(names, eng, orc, list(range(len(names))))
+    monkeypatch.setenv("SPF_MSSP_U8", "1")
+    topo = T.random_graph(200, 230, 23, max_metric=20, overload_frac=0.05)
+    names, eng, orc = load(topo)
+    res = compare(names, eng, orc, list(range(len(names))))
+    d = res.dist[res.dist != N.SPF_UNREACHABLE]
+    assert d.max() > 0xFF  # the u8 redo path was needed
 
 
 @pytest.mark.parametrize("skip", ["0", "1"])
