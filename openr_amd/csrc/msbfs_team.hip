@@ -77,6 +77,8 @@ struct TeamArgs {
   const uint32_t* need;        // [G][need_words]: the 64-node frontier slices a member's stream reads
   uint32_t need_words;
   uint32_t* fault;  // the context's barrier-timeout word (spf_device_check)
+  uint32_t dbg;     // diagnostics (SPF_TEAM_FLUSH_DBG): bit 0 no u32 row stores, bit 1 no plane
+                    // stores, bit 2 no flush at all (the rows are then invalid)
 };
 
 // Team hand-off of a level (MI355X_MICROARCH.md, inter-workgroup visibility,
@@ -286,6 +288,7 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
     // store per 4 u32 rows and per 16 u8 rows instead of a dword and a byte
     // store per row (the store issue rate bounded the per-row form)
     auto flush = [&]() {
+      if (a.dbg & 4u) return;
       if (base == 0) {
         uint32_t* T32 = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * kTmRows * 80;
         uint8_t* T8 = reinterpret_cast<uint8_t*>(T32 + kTmRows * 64);
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
               T32[r * 64 + lane] = seen ? q : kInf;  // first window: base == 0
               T8[r * 64 + lane] = seen ? q : 0xFFu;   // q <= kTmWindow - 1 < 254
             }
-            if (a.D)
+            if (a.D && !(a.dbg & 1u))
               for (uint32_t r4 = 0; r4 < gn; r4 += 4) {
                 const uint32_t r = r4 + (lane >> 4);
                 if (r < gn && row0 + g0 + r < a.d_rows) {
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
                                                                        sv[i] + (lane & 15) * 4));
                 }
               }
-            if (a.S) {
+            if (a.S && !(a.dbg & 2u)) {
               // the sliced rows (ecmp_sliced_kernel's layout with P =
               // kTmPlanes): word w of row r holds plane b at w * P + b, bit t
               // = node 32w + t; code all-ones = unreachable (byte 0xFF; nodes
@@ -689,7 +692,8 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
              (uint32_t)std::max<size_t>(8ull * fw, (size_t)kTmWaves * kTmRows * 80 * 4),
              (uint32_t)(4ull * c->sell_col.size()), d_rows, S, s_stride, D, Dn, maxd,
              reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p,
-             p->d_tm_map.p + p->tm_need_at, p->tm_need_words, c->d_fault.p};
+             p->d_tm_map.p + p->tm_need_at, p->tm_need_words, c->d_fault.p, 0u};
+  if (const char* e = std::getenv("SPF_TEAM_FLUSH_DBG")) a.dbg = (uint32_t)atoi(e);
   const uint32_t* meta = p->d_tm_map.p + p->tm_runs_at;
   const uint32_t blocks = p->tm_teams * p->tm_G;  // = n_cu: one persistent workgroup per CU
   const size_t lds = team_lds(fw, p->tm_nacc);

@@ -67,7 +67,7 @@ def test_mssp_u8_is_the_default_on_rtt_fabrics_and_overflow_rows_are_redone(monk
     assert eng.plan([0]).kernels()[0] == "mssp_kernel"
     compare(names, eng, orc, list(range(len(names))))
     monkeypatch.setenv("SPF_MSSP_U8", "1")
-    topo = T.random_graph(200, 230, 23, max_metric=20, overload_frac=0.05)
+    topo = T.wan(300, 12, seed=9, max_metric=20)  # a ring with few chords: long paths
     names, eng, orc = load(topo)
     res = compare(names, eng, orc, list(range(len(names))))
     d = res.dist[res.dist != N.SPF_UNREACHABLE]

@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 for s in ${STEPS:-tests emulate bench trace}; do
   case $s in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -v --timeout 300 --timeout-method thread \
         ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -5 "$OUT/pytest_gpu.log"; echo "tests rc=$rc"
       [ $rc -ne 0 ] && exit $rc ;;
