@@ -981,10 +981,21 @@ def roofline_block(wl, kms, launch_ms: float, workload: str, rank: int):
     elif rank == 0:
         print(f"bench: {src}: roofline.traffic is null", file=sys.stderr)
     kb = wl.kernel_bytes
+    practical = None
+    eng = getattr(wl, "eng", None)
+    if eng is not None and os.environ.get("BENCH_NO_COPY_BW") is None:
+        try:  # the measured copy ceiling beside the spec peak
+            practical = eng.copy_bandwidth(1 << 30, 10)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: copy bandwidth: {e!r}", file=sys.stderr)
     out = {
         "bound": "hbm",
         "achieved": achieved,
         "peak": HBM_PEAK_GBS,
+        "practical_peak": practical,
+        "practical_peak_source": "spf_debug_copy_bandwidth: 1 GiB 16-byte copy kernel on this GPU, "
+                                 "read + written bytes / time (HIP events)" if practical else None,
+        "frac_of_practical": achieved / practical if practical else None,
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "frac_algorithmic": achieved / HBM_PEAK_GBS,

@@ -486,6 +486,11 @@ spf_status spf_mplan_timing(spf_mplan* mp, double* ms, uint32_t* n);
  * distance stores, pull sweep, barrier; end), per wave: out[w*64] = count,
  * out[w*64 + 1 ..] = clocks of wave w (16 waves).  Copies up to cap words. */
 spf_status spf_debug_stamps(spf_ctx* ctx, uint64_t* out, uint32_t cap, uint32_t* n);
+/* The device's practical HBM ceiling: a 16-byte grid-stride copy of `bytes`
+ * (read + written per rep, `reps` reps timed with HIP events) -> *gbs in
+ * GB/s of bytes moved.  What bench.py reports beside the 8 TB/s peak
+ * (BASELINE.md §4).  No reference counterpart. */
+spf_status spf_debug_copy_bandwidth(spf_ctx* ctx, uint64_t bytes, uint32_t reps, double* gbs);
 
 /* Waits for every launch on the context's device and reports whether a
  * grid-resident kernel's barrier of THIS context (spf_big_kernel, the

@@ -184,6 +184,7 @@ PROTOTYPES = {
     "spf_solves": (C.c_uint64, [_vp]),
     "spf_device_check": (C.c_int, [_vp]),
     "spf_debug_stamps": (C.c_int, [_vp, _u64p, C.c_uint32, _u32p]),
+    "spf_debug_copy_bandwidth": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "spf_ksp2_plan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.POINTER(_vp)]),
     "spf_ksp2_plan_destroy": (None, [_vp]),
     "spf_ksp2_execute": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),

@@ -78,7 +78,8 @@ struct TeamArgs {
   uint32_t need_words;
   uint32_t* fault;  // the context's barrier-timeout word (spf_device_check)
   uint32_t dbg;     // diagnostics (SPF_TEAM_FLUSH_DBG): bit 0 no u32 row stores, bit 1 no plane
-                    // stores, bit 2 no flush at all (the rows are then invalid)
+                    // stores, bit 2 no flush at all, bit 3 no row padding, bit 4 no maxd
+                    // atomic (the rows are then invalid)
 };
 
 // Team hand-off of a level (MI355X_MICROARCH.md, inter-workgroup visibility,
@@ -470,7 +471,8 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
     }
     __syncthreads();  // every wave past its last frontier read: the tiles may overwrite Fl
     flush();
-    if (a.maxd && member == 0 && tid == 0) atomicMax(a.maxd, depth);
+    if (a.maxd && member == 0 && tid == 0 && !(a.dbg & 16u)) atomicMax(a.maxd, depth);
+    if (!(a.dbg & 8u))
     for (uint32_t s = 0; s < nb; ++s)  // padding past N, split over the members
       for (uint32_t v = N + member * kTmThreads + tid; v < a.npitch; v += G * kTmThreads) {
         if (a.D && v < a.pitch && row0 + s < a.d_rows) a.D[(size_t)(row0 + s) * a.pitch + v] = kInf;

@@ -1482,6 +1482,14 @@ __global__ void gather_rows_u8_kernel(const uint8_t* __restrict__ Dn, uint32_t n
     o[t] = in[t];
 }
 
+// practical HBM ceiling (spf_debug_copy_bandwidth): a grid-stride 16-byte
+// copy, the float4-copy shape of MI355X_MICROARCH.md's measured 6.29 TB/s
+__global__ __launch_bounds__(256) void copy_bw_kernel(const uint4* __restrict__ src,
+                                                      uint4* __restrict__ dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
 __global__ void gather_rows_kernel(const uint32_t* __restrict__ D, uint32_t pitch,
                                    const uint32_t* __restrict__ rows,
                                    uint32_t* __restrict__ out) {
@@ -3085,6 +3093,33 @@ spf_status spf_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src, uint32_t 
   if (st != SPF_OK) return st;
   std::unique_ptr<spf_plan> p(raw);
   return spf_plan_execute_host(p.get(), dist_out, nh_out);
+}
+
+spf_status spf_debug_copy_bandwidth(spf_ctx* c, uint64_t bytes, uint32_t reps, double* gbs) {
+  if (!c || !gbs || bytes < 16 || reps == 0) return fail(c, SPF_E_INVALID, "spf_debug_copy_bandwidth: bad argument");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t n = bytes / 16;
+  DevBuf<uint4> a, b;
+  HIP_TRY(c, a.alloc(n));
+  HIP_TRY(c, b.alloc(n));
+  HIP_TRY(c, hipMemsetAsync(a.p, 1, n * 16, c->stream));
+  const dim3 g(c->n_cu * 8), blk(256);
+  hipLaunchKernelGGL(copy_bw_kernel, g, blk, 0, c->stream, a.p, b.p, n);  // warm
+  HIP_TRY(c, hipGetLastError());
+  hipEvent_t e0, e1;
+  HIP_TRY(c, hipEventCreate(&e0));
+  HIP_TRY(c, hipEventCreate(&e1));
+  HIP_TRY(c, hipEventRecord(e0, c->stream));
+  for (uint32_t r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(copy_bw_kernel, g, blk, 0, c->stream, (r & 1) ? b.p : a.p, (r & 1) ? a.p : b.p, n);
+  HIP_TRY(c, hipEventRecord(e1, c->stream));
+  HIP_TRY(c, hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *gbs = 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;  // bytes read + written
+  return SPF_OK;
 }
 
 spf_status spf_debug_stamps(spf_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n) {

@@ -377,6 +377,12 @@ class SpfEngine(NativeHandle):
     def solves(self) -> int:
         return int(N.lib.spf_solves(self._h))
 
+    def copy_bandwidth(self, nbytes: int = 1 << 30, reps: int = 10) -> float:
+        """Measured practical HBM ceiling in GB/s (spf_debug_copy_bandwidth)."""
+        g = C.c_double()
+        self._err(N.lib.spf_debug_copy_bandwidth(self._h, nbytes, reps, C.byref(g)))
+        return g.value
+
     def check(self) -> None:
         """Wait for the device and raise if a grid-resident kernel's barrier
         gave up waiting since the last check (spf_device_check): the outputs
