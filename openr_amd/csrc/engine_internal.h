@@ -17,6 +17,10 @@
 namespace spfi {
 
 constexpr uint32_t kInf = SPF_UNREACHABLE;
+// diagnostics buffer (SPF_STAMPS): 16 waves x 64 phase stamps of one block,
+// the block selector, then a start / end s_memrealtime pair per block
+constexpr uint32_t kStampBlocks = 1024;
+constexpr uint32_t kStampWords = 64 * 16 + 1 + 2 * kStampBlocks;
 
 extern thread_local std::string g_err;
 

@@ -56,6 +56,7 @@ static_assert(kTmPlanes == (int)kTeamPlanes, "sdirect rows: the next-hop pass re
 constexpr int kTmCopy = 10;                               // uint4 per thread of the frontier copy
 constexpr uint32_t kTmRows = 16;                          // sources per flush tile (80 B each per node)
 constexpr uint32_t kTmBarPad = 32;            // words per team: counter line + 3 flag lines
+constexpr uint32_t kSliceNodes = 64;          // nodes per sliced-ELL slice (= wave width)
 
 struct TeamArgs {
   const uint32_t* sell_col;
@@ -161,6 +162,10 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
   // diagnostics: lane 0 of every wave of block stamps[1024] logs s_memtime at
   // each phase boundary into stamps[wave * 64 + 1 ..], the count at [wave * 64]
   const bool stamp = a.stamps && blockIdx.x == (uint32_t)a.stamps[64 * 16] && lane == 0;
+  // block timeline (with stamps on): s_memrealtime (100 MHz, chip-wide) at
+  // the start and the end of every block, stamps[1025 + 2 b], [1026 + 2 b]
+  if (a.stamps && tid == 0 && blockIdx.x < kStampBlocks)
+    a.stamps[64 * 16 + 1 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   uint32_t n_stamp = 0;
 #define TM_STAMP()                                                                      \
   do {                                                                                  \
@@ -472,16 +477,26 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
     __syncthreads();  // every wave past its last frontier read: the tiles may overwrite Fl
     flush();
     if (a.maxd && member == 0 && tid == 0 && !(a.dbg & 16u)) atomicMax(a.maxd, depth);
-    if (!(a.dbg & 8u))
-    for (uint32_t s = 0; s < nb; ++s)  // padding past N, split over the members
-      for (uint32_t v = N + member * kTmThreads + tid; v < a.npitch; v += G * kTmThreads) {
-        if (a.D && v < a.pitch && row0 + s < a.d_rows) a.D[(size_t)(row0 + s) * a.pitch + v] = kInf;
+    // row padding: the entries past the slices' end (the flush covered every
+    // slice, nodes past N included) -- one flat (row, entry) index dealt to
+    // every thread of every member.  A loop per row, as before, cost ~9 us per
+    // batch in loop overhead at 57 rows (r04_g5 stamps, SPF_TEAM_FLUSH_DBG=8).
+    if (!(a.dbg & 8u)) {
+      const uint32_t v0 = (N + kSliceNodes - 1u) / kSliceNodes * kSliceNodes;
+      const uint32_t pw = a.npitch - v0, tot = nb * pw;
+      for (uint32_t t = member * kTmThreads + tid; t < tot; t += G * kTmThreads) {
+        const uint32_t s = t / pw, v = v0 + t % pw;
+        if (a.D && v < a.pitch && row0 + s < a.d_rows)
+          __builtin_nontemporal_store(kInf, &a.D[(size_t)(row0 + s) * a.pitch + v]);
         if (a.Dn) a.Dn[(size_t)(row0 + s) * a.npitch + v] = 0xFF;
       }
+    }
     __syncthreads();  // Fl, src_l are reset by the next batch
     TM_STAMP();
   }
   if (stamp) a.stamps[wv * 64] = n_stamp;
+  if (a.stamps && tid == 0 && blockIdx.x < kStampBlocks)
+    a.stamps[64 * 16 + 2 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #undef TM_STAMP
   // the team's last member out zeroes its barrier words for the next launch
   // (no memset per execute; every member passes here, timed-out ones too)
@@ -681,8 +696,8 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
                              uint32_t* D, uint8_t* Dn, uint32_t* maxd, hipStream_t s,
                              uint32_t d_rows, uint32_t* S, uint32_t s_stride) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
-    HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
-    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
+    HIP_TRY(c, c->d_stamps.alloc(kStampWords));
+    HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, kStampWords * 8, s));
     const unsigned long long wg = std::strtoull(std::getenv("SPF_STAMPS"), nullptr, 10);
     HIP_TRY(c, hipMemcpyAsync(c->d_stamps.p + 64 * 16, &wg, 8, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipStreamSynchronize(s));

@@ -513,7 +513,7 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   if (c->mp_epoch != c->epoch) return fail(c, SPF_E_STATE, "mssp tables stale: rebuild the plan");
   if (c->mp_redo) HIP_TRY(c, hipMemsetAsync(redo, 0, 4, s));
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {  // sweep counters (diagnostics)
-    HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
+    HIP_TRY(c, c->d_stamps.alloc(kStampWords));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, (64 * 16 + 1) * 8, s));
   }
   const uint32_t S = mssp_sources(c);

@@ -652,12 +652,12 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
       }
     }
   }
-  for (uint32_t s = 0; s < nb; ++s) {
-    uint32_t* drow = D + (size_t)(row0 + s) * pitch;
-    uint8_t* nrow = Dn + (size_t)(row0 + s) * npitch;
-    for (uint32_t v = N + tid; v < npitch; v += kMsThreads) {
-      if (D && d_from == 0 && v < pitch) __builtin_nontemporal_store(kInf, &drow[v]);
-      if (Dn) nrow[v] = 0xFF;
+  {  // row padding past N: one flat (row, entry) index over the workgroup
+    const uint32_t pw = npitch - N, tot = nb * pw;
+    for (uint32_t t = tid; t < tot; t += kMsThreads) {
+      const uint32_t s = t / pw, v = N + t % pw;
+      if (D && d_from == 0 && v < pitch) __builtin_nontemporal_store(kInf, &D[(size_t)(row0 + s) * pitch + v]);
+      if (Dn) Dn[(size_t)(row0 + s) * npitch + v] = 0xFF;
     }
   }
   MS_STAMP();
@@ -1281,6 +1281,7 @@ __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_
 // (the per-source pass loads it once per source -- the next-hop pass is
 // bound by those L2 reads).  gs <= kSlGroup sources; lane = output word w.
 constexpr uint32_t kSlGroup = 8;
+constexpr uint32_t kSlSeg = 4;  // neighbour positions per grouping segment (one uint4 of row offsets)
 template <int P>
 __device__ __forceinline__ void grouped_pass(__amdgpu_buffer_rsrc_t rs, uint32_t* __restrict__ nh,
                                              const uint64_t* __restrict__ nh_off,
@@ -2317,58 +2318,118 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
           kSlUnit, std::max<uint64_t>(16, matches / (16ull * c->n_cu) / 8 * 8));
       const uint32_t unit = ue ? (uint32_t)atoi(ue) : fill;
       std::vector<uint32_t> units, unit_off(9, 0), gtab;
-      // sources of one XCD list with identical neighbour rows and no drained
-      // neighbour (a pod's rack switches, a plane's spines) form groups of up
-      // to kSlGroup: one wave loads each neighbour row once for the group
-      // (SPF_SLICED_GROUP=0: A/B)
+      // Grouped units: neighbour positions are cut into segments of kSlSeg;
+      // sources of one XCD list whose segment q holds the same rows (none
+      // drained) share it -- one wave loads each of those rows once for up
+      // to kSlGroup sources.  Whole lists match for a pod's rack switches and
+      // a plane's spines; a fabric switch's list is [its plane's spines][its
+      // pod's rack switches], so the fabric switches of one plane share the
+      // first part and those of one pod the second.  Consecutive segments of
+      // one member set merge into one range; what no group takes stays with
+      // per-source units.  (SPF_SLICED_GROUP=0: no groups, =1: whole
+      // identical lists only -- round 3's rule; A/B.)
       const char* ge = std::getenv("SPF_SLICED_GROUP");
-      const bool grouping = !(ge && ge[0] == '0');
-      std::vector<int32_t> leader_of(n_src, -1);  // >= 0: gtab offset, -2: member
+      const int gmode = ge ? atoi(ge) : 2;
       p->max_xcd_units = 0;
       for (int g = 0; g < 8; ++g) {
         unit_off[g] = (uint32_t)(units.size() / 4);
-        if (grouping) {
-          std::map<std::vector<uint32_t>, std::vector<uint32_t>> same;
-          for (uint32_t i : lists[g])
-            if (p->words[i] && !nb_drained[i])
-              same[std::vector<uint32_t>(nb_row.begin() + nb_row_off[i],
-                                         nb_row.begin() + nb_row_off[i] + p->words[i])]
-                  .push_back(i);
-          for (auto& kv : same)
-            for (size_t a = 0; a + 1 < kv.second.size(); a += kSlGroup) {
-              const size_t b = std::min(kv.second.size(), a + kSlGroup);
-              leader_of[kv.second[a]] = (int32_t)gtab.size();
-              gtab.push_back((uint32_t)(b - a));
-              for (size_t q = a; q < b; ++q) {
-                gtab.push_back(kv.second[q]);
-                if (q > a) leader_of[kv.second[q]] = -2;
+        // per source of the list: which segments a group took
+        std::map<uint32_t, std::vector<uint8_t>> taken;
+        // member set -> segments (q, end position) it shares
+        std::map<std::vector<uint32_t>, std::vector<std::pair<uint32_t, uint32_t>>> shared;
+        if (gmode) {
+          std::map<std::vector<uint32_t>, std::vector<uint32_t>> seg;
+          for (uint32_t i : lists[g]) {
+            const uint32_t k = p->words[i];
+            if (!k) continue;
+            const uint32_t* r = nb_row.data() + nb_row_off[i];
+            if (gmode == 1) {  // the whole list as one key
+              if (nb_drained[i]) continue;
+              std::vector<uint32_t> key{0u, k};
+              key.insert(key.end(), r, r + k);
+              seg[key].push_back(i);
+              continue;
+            }
+            for (uint32_t q = 0; q * kSlSeg < k; ++q) {
+              const uint32_t j = q * kSlSeg, e = std::min(k, j + kSlSeg);
+              bool dead_in = false;
+              for (uint32_t jj = j; jj < e; ++jj) dead_in |= r[jj] == dead;
+              if (dead_in) continue;
+              std::vector<uint32_t> key{q, e};
+              key.insert(key.end(), r + j, r + e);
+              seg[key].push_back(i);
+            }
+          }
+          for (auto& kv : seg) {
+            const auto& src = kv.second;
+            for (size_t a = 0; a + 1 < src.size(); a += kSlGroup) {
+              const size_t b = std::min(src.size(), a + kSlGroup);
+              if (b - a < 2) break;
+              std::vector<uint32_t> m(src.begin() + a, src.begin() + b);
+              const uint32_t q = kv.first[0], e = kv.first[1];
+              if (gmode == 1) {  // whole list: every segment of it
+                for (uint32_t qq = 0; qq * kSlSeg < e; ++qq)
+                  shared[m].emplace_back(qq, std::min(e, (qq + 1) * kSlSeg));
+              } else {
+                shared[m].emplace_back(q, e);
+              }
+              for (uint32_t i : m) {
+                auto& t = taken[i];
+                if (t.empty()) t.assign((p->words[i] + kSlSeg - 1) / kSlSeg, 0);
+                if (gmode == 1)
+                  std::fill(t.begin(), t.end(), 1);
+                else
+                  t[q] = 1;
               }
             }
+          }
         }
+        // group units: per member set, runs of consecutive segments, per
+        // chunk, ranges of about `unit` matches (multiples of kSlSeg)
+        for (auto& kv : shared) {
+          auto& segs = kv.second;
+          std::sort(segs.begin(), segs.end());
+          const uint32_t gs = (uint32_t)kv.first.size();
+          const uint32_t goff = (uint32_t)gtab.size();
+          gtab.push_back(gs);
+          gtab.insert(gtab.end(), kv.first.begin(), kv.first.end());
+          for (size_t a = 0; a < segs.size();) {
+            size_t b = a + 1;
+            while (b < segs.size() && segs[b].first == segs[b - 1].first + 1) ++b;
+            const uint32_t j0 = segs[a].first * kSlSeg, j1 = segs[b - 1].second;
+            const uint32_t parts = (uint32_t)(((uint64_t)(j1 - j0) * gs + unit - 1) / unit);
+            const uint32_t jstep = ((j1 - j0 + parts - 1) / parts + kSlSeg - 1) / kSlSeg * kSlSeg;
+            for (uint32_t ch = 0; ch < chunks; ++ch)
+              for (uint32_t j = j0; j < j1; j += jstep)
+                units.insert(units.end(), {goff, ch | (1u << 31), j, std::min(j1, j + jstep)});
+            a = b;
+          }
+        }
+        // per-source units over what no group took
         for (uint32_t i : lists[g]) {
           const uint32_t k = p->words[i];
-          if (k == 0 || leader_of[i] == -2) continue;
-          if (leader_of[i] >= 0) {  // per chunk, ranges of about `unit` matches
-            const uint32_t gs = gtab[leader_of[i]];
-            const uint32_t parts = (uint32_t)(((uint64_t)k * gs + unit - 1) / unit);
-            const uint32_t jstep = ((k + parts - 1) / parts + 7) / 8 * 8;
-            for (uint32_t ch = 0; ch < chunks; ++ch)
-              for (uint32_t j = 0; j < k; j += jstep)
-                units.insert(units.end(), {(uint32_t)leader_of[i], ch | (1u << 31), j,
-                                           std::min(k, j + jstep)});
-            continue;
+          if (k == 0) continue;
+          const auto it = taken.find(i);
+          const std::vector<uint8_t>* t = it == taken.end() ? nullptr : &it->second;
+          for (uint32_t q = 0; q * kSlSeg < k;) {
+            if (t && (*t)[q]) {
+              ++q;
+              continue;
+            }
+            uint32_t q1 = q + 1;
+            while (q1 * kSlSeg < k && !(t && (*t)[q1])) ++q1;
+            const uint32_t j0 = q * kSlSeg, j1 = std::min(k, q1 * kSlSeg), kr = j1 - j0;
+            if ((uint64_t)kr * chunks <= unit) {
+              units.insert(units.end(), {i, 0u | (chunks << 16), j0, j1});
+            } else {  // per chunk, equal ranges of <= unit neighbours (multiples of kSlSeg)
+              const uint32_t parts = (kr + unit - 1) / unit;
+              const uint32_t jstep = ((kr + parts - 1) / parts + kSlSeg - 1) / kSlSeg * kSlSeg;
+              for (uint32_t ch = 0; ch < chunks; ++ch)
+                for (uint32_t j = j0; j < j1; j += jstep)
+                  units.insert(units.end(), {i, ch | ((ch + 1) << 16), j, std::min(j1, j + jstep)});
+            }
+            q = q1;
           }
-          if ((uint64_t)k * chunks <= unit) {
-            units.insert(units.end(), {i, 0u | (chunks << 16), 0u, k});
-            continue;
-          }
-          // per chunk, k split into equal ranges of <= unit neighbours
-          // (multiples of 8)
-          const uint32_t parts = (k + unit - 1) / unit;
-          const uint32_t jstep = ((k + parts - 1) / parts + 7) / 8 * 8;
-          for (uint32_t ch = 0; ch < chunks; ++ch)
-            for (uint32_t j = 0; j < k; j += jstep)
-              units.insert(units.end(), {i, ch | ((ch + 1) << 16), j, std::min(k, j + jstep)});
         }
         p->max_xcd_units = std::max(p->max_xcd_units, (uint32_t)(units.size() / 4) - unit_off[g]);
       }
@@ -2690,7 +2751,7 @@ spf_status launch_msbfs(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uin
                         uint8_t* Dn, uint32_t* maxd, hipStream_t s, uint32_t d_from = 0,
                         const uint32_t* order = nullptr) {
   if (!c->d_stamps.p && std::getenv("SPF_STAMPS")) {
-    HIP_TRY(c, c->d_stamps.alloc(64 * 16 + 1));
+    HIP_TRY(c, c->d_stamps.alloc(kStampWords));
     HIP_TRY(c, hipMemsetAsync(c->d_stamps.p, 0, 64 * 16 * 8, s));
     const unsigned long long wg = std::strtoull(std::getenv("SPF_STAMPS"), nullptr, 10);
     HIP_TRY(c, hipMemcpyAsync(c->d_stamps.p + 64 * 16, &wg, 8, hipMemcpyHostToDevice, s));
@@ -3126,7 +3187,7 @@ spf_status spf_debug_stamps(spf_ctx* c, uint64_t* out, uint32_t cap, uint32_t* n
   if (!c || !n) return SPF_E_INVALID;
   *n = 0;
   if (!c->d_stamps.p) return SPF_OK;
-  std::vector<uint64_t> buf(64 * 16);
+  std::vector<uint64_t> buf(kStampWords);
   HIP_TRY(c, hipMemcpy(buf.data(), c->d_stamps.p, buf.size() * 8, hipMemcpyDeviceToHost));
   *n = (uint32_t)std::min<size_t>(cap, buf.size());
   std::copy(buf.begin(), buf.begin() + *n, out);

@@ -369,10 +369,18 @@ class SpfEngine(NativeHandle):
     def debug_stamps(self) -> np.ndarray:
         """BFS phase clocks of workgroup 0 (needs SPF_STAMPS=1 at first execute):
         [16 waves, 64] -- column 0 is the count, columns 1.. the clocks."""
-        out = np.zeros(64 * 16, np.uint64)
+        return self._stamp_words()[: 64 * 16].reshape(16, 64)
+
+    def _stamp_words(self) -> np.ndarray:
+        out = np.zeros(64 * 16 + 1 + 2 * 1024, np.uint64)
         n = C.c_uint32()
         self._err(N.lib.spf_debug_stamps(self._h, N.ptr(out, C.c_uint64), out.size, C.byref(n)))
-        return out.reshape(16, 64)
+        return out
+
+    def debug_timeline(self) -> np.ndarray:
+        """Team BFS block timeline (SPF_STAMPS set): [block, (start, end)]
+        s_memrealtime ticks (100 MHz), zeros for blocks that did not run."""
+        return self._stamp_words()[64 * 16 + 1:].reshape(1024, 2)
 
     def solves(self) -> int:
         return int(N.lib.spf_solves(self._h))

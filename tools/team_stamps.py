@@ -54,6 +54,15 @@ def main():
     for i in range(1, m):
         dd = st[:, i] - st[:, i - 1]
         print(f"interval {i:3d}: {int(dd.min()):8d}..{int(dd.max()):8d} (w{int(dd.argmax()):2d})")
+    tl = eng.debug_timeline().astype(np.int64)
+    live = tl[:, 1] > 0
+    if live.any():
+        t0 = tl[live, 0].min()
+        st, en = (tl[live, 0] - t0) * 10, (tl[live, 1] - t0) * 10  # ns
+        print(f"timeline: {int(live.sum())} blocks, start {st.min()}..{st.max()} ns, "
+              f"end min {en.min()} p50 {int(np.median(en))} p90 {int(np.percentile(en, 90))} max {en.max()} ns")
+        order = np.argsort(en)[::-1][:8]
+        print("latest blocks:", [(int(np.flatnonzero(live)[i]), int(en[i])) for i in order])
     plan.close()
     close_all()
 
