@@ -301,7 +301,7 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* plan, spf_ksp2_pair* d_pairs, uint32_
                             uint64_t pool_words, uint64_t* d_counters, void* stream);
 /* Per-source digests of an execute's output, on the GPU (enqueued on
  * `stream`): d_out[i] = sum mod 2^64 over destinations d of
- * h(i, d) + mix(d + 1), h = FNV-1a over (0x1000 + n_paths[k], then per path
+ * mix(h(i, d) + mix(d + 1)), h = FNV-1a over (0x1000 + n_paths[k], then per path
  * 0x2000 + length and link_hash[link] of each link) for k = 1, 2 and mix =
  * splitmix64's finaliser.  link_hash[id] identifies link `id` by value (the
  * caller hashes its ordered (node, ifname) key), so digests compare across

@@ -575,7 +575,7 @@ __global__ __launch_bounds__(256) void ksp2_digest_kernel(const spf_ksp2_pair* _
       at = pool[at + 1];
     }
   }
-  atomicAdd(&out[i], (unsigned long long)(h + dg_mix64((uint64_t)d + 1)));
+  atomicAdd(&out[i], (unsigned long long)dg_mix64(h + dg_mix64((uint64_t)d + 1)));
 }
 }  // namespace
 
