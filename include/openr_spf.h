@@ -296,7 +296,11 @@ void spf_ksp2_plan_destroy(spf_ksp2_plan* plan);
  * d_pool = pool_words u32, d_counters = 4 u64 zeroed by the call:
  *   [0] pool words claimed (> pool_words means the pool overflowed),
  *   [1] k = 2 SPF runs (the reference's un-memoised runSpf calls, :778-779),
- *   [2] bit 0 = overflow.  No host synchronisation, no allocation. */
+ *   [2] bit 0 = overflow (bit 1: redo list full, never on plans made by
+ *       spf_ksp2_plan_create, which size it for every pair),
+ *   [3] pairs the u16-label waves of a compact plan handed to the u32 redo
+ *       pass (labels past 65534 or paths deeper than 512 links; 0 otherwise).
+ * No host synchronisation, no allocation. */
 spf_status spf_ksp2_execute(spf_ksp2_plan* plan, spf_ksp2_pair* d_pairs, uint32_t* d_pool,
                             uint64_t pool_words, uint64_t* d_counters, void* stream);
 /* Per-source digests of an execute's output, on the GPU (enqueued on

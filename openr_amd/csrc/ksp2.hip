@@ -42,8 +42,10 @@ constexpr int kKspThreads = 256;             // 4 waves, one pair each
 constexpr int kKspWaves = kKspThreads / 64;
 constexpr int kKspLdsMaxThreads = 1024;      // staged-graph kernel: up to 16 waves
 constexpr uint32_t kKspChunk = 64;          // sources per workgroup (default; SPF_KSP2_CHUNK)
-constexpr uint32_t kPoolGrab = 2048;        // words a wave reserves at a time
+constexpr uint32_t kPoolGrab = 256;         // words a wave reserves at a time (~ its pairs' paths)
 constexpr size_t kMaxLdsKsp = 160 * 1024;
+constexpr uint32_t kCompactCap = 512;       // u16-label waves: DFS stack / SPF queue entries
+constexpr uint32_t kRedoBlocks = 256;       // workgroups of the u32 redo pass
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -108,6 +110,54 @@ __device__ __forceinline__ uint64_t lanes_min64(uint64_t x, uint32_t n, uint32_t
 
 __device__ __forceinline__ bool bit(const uint32_t* bm, uint32_t i) {
   return (bm[i >> 5] >> (i & 31)) & 1u;
+}
+
+// A wave's distance row: u32 labels, or u16 labels on compact plans (0xFFFF
+// = unreached or >= 65535; a pair whose labels leave that range is redone
+// with u32 labels, see ksp2_pair).
+__device__ __forceinline__ uint32_t dget(const uint32_t* D, uint32_t v) { return D[v]; }
+__device__ __forceinline__ uint32_t dget(const uint16_t* D, uint32_t v) {
+  const uint32_t x = D[v];
+  return x == 0xFFFFu ? kInf : x;
+}
+__device__ __forceinline__ void dput(uint32_t* D, uint32_t v, uint32_t x) { D[v] = x; }
+__device__ __forceinline__ void dput(uint16_t* D, uint32_t v, uint32_t x) { D[v] = (uint16_t)x; }
+// D[v] = min(D[v], nd); true when the label went down
+__device__ __forceinline__ bool dmin(uint32_t* D, uint32_t v, uint32_t nd) {
+  return nd < atomicMin(&D[v], nd);
+}
+__device__ __forceinline__ bool dmin(uint16_t* D, uint32_t v, uint32_t nd) {
+  // LDS has no 16-bit min: compare-and-swap on the word holding the label
+  uint32_t* w = reinterpret_cast<uint32_t*>(D) + (v >> 1);
+  const uint32_t sh = (v & 1u) * 16u;
+  uint32_t old = *w;
+  for (;;) {
+    if (nd >= ((old >> sh) & 0xFFFFu)) return false;
+    const uint32_t seen = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | (nd << sh));
+    if (seen == old) return true;
+    old = seen;
+  }
+}
+template <class DT>
+__device__ __forceinline__ void fill_unreached(DT* D, uint32_t pitch) {
+  uint4* o = reinterpret_cast<uint4*>(D);
+  for (uint32_t t = __lane_id(); t < pitch * (uint32_t)sizeof(DT) / 16; t += 64)
+    o[t] = make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+// the source's k = 1 row into the wave's labels (u16: saturated at 0xFFFF)
+__device__ __forceinline__ void load_row(uint32_t* D, const uint32_t* Drow, uint32_t pitch) {
+  const uint4* in = reinterpret_cast<const uint4*>(Drow);
+  uint4* o = reinterpret_cast<uint4*>(D);
+  for (uint32_t t = __lane_id(); t < pitch / 4; t += 64) o[t] = in[t];
+}
+__device__ __forceinline__ void load_row(uint16_t* D, const uint32_t* Drow, uint32_t pitch) {
+  const uint4* in = reinterpret_cast<const uint4*>(Drow);
+  uint2* o = reinterpret_cast<uint2*>(D);
+  for (uint32_t t = __lane_id(); t < pitch / 4; t += 64) {
+    const uint4 x = in[t];
+    o[t] = make_uint2(min(x.x, 0xFFFFu) | (min(x.y, 0xFFFFu) << 16),
+                      min(x.z, 0xFFFFu) | (min(x.w, 0xFFFFu) << 16));
+  }
 }
 
 // Graph accessors: the CSR in HBM (any size), or a 16-bit copy staged in
@@ -185,11 +235,14 @@ __device__ uint32_t pool_alloc(PoolCursor& pc, uint32_t words, unsigned long lon
 // in-edges of D (tails expanded, links not in `ign` when given, links not in
 // `vis`).  On success the stack holds the edges dst-first and *depth their
 // count; every link tried is left in `vis`.
-template <class G, class ST>
-__device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, uint32_t* vis,
-                          ST* stack, uint32_t src, uint32_t dst, uint32_t* depth) {
+// A path deeper than `cap` links sets *ovf (u16-label waves: the pair is
+// redone with a full-size stack).
+template <class G, class DT, class ST>
+__device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t* vis,
+                          ST* stack, uint32_t cap, uint32_t src, uint32_t dst, uint32_t* depth,
+                          bool* ovf) {
   const uint32_t lane = __lane_id();
-  uint32_t k = 0, v = dst, dv = D[dst];
+  uint32_t k = 0, v = dst, dv = dget(D, dst);
   for (;;) {
     if (v == src) {
       *depth = k;
@@ -206,7 +259,7 @@ __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, ui
       const uint32_t l = g.link_of(e, r);
       const bool drained = g.ovl(u) && u != src;
       const bool tried = bit(vis, l) || (ign && bit(ign, l));
-      const uint32_t du = D[u];
+      const uint32_t du = dget(D, u);
       const uint32_t wr = g.w(r);
       if (!drained && !tried && du != kInf && du + wr == dv) {
         const uint64_t key = ((uint64_t)du << 32) | r;
@@ -223,7 +276,7 @@ __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, ui
       if (k == 0) return false;
       --k;
       v = k == 0 ? dst : g.col(g.rev(stack[k - 1]));
-      dv = D[v];
+      dv = dget(D, v);
       continue;
     }
     const uint32_t r = (uint32_t)best;
@@ -234,6 +287,10 @@ __device__ bool trace_one(const G& g, const uint32_t* D, const uint32_t* ign, ui
     } else {
       u = g.col(g.rev(r));
       l = g.link(r);
+    }
+    if (k >= cap) {
+      *ovf = true;
+      return false;
     }
     if (lane == 0) {
       atomicOr(&vis[l >> 5], 1u << (l & 31));  // ds_or: no read round trip
@@ -288,23 +345,33 @@ __device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint3
 // after expanding every node within dst's hop count (bound D[dst] = inf
 // until then); with it, only nodes with f < d2(dst) + delta are expanded.
 // The fixpoint -- and so every distance the trace reads -- is the same.
-template <class G>
-__device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, uint32_t bm_words,
-                          const uint32_t* ign, uint32_t src, uint32_t dst, uint32_t pitch,
-                          const uint32_t* H, uint32_t delta, unsigned long long* prof) {
+template <class G, class DT>
+__device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_t* bm,
+                          uint32_t bm_words, const uint32_t* ign, uint32_t src, uint32_t dst,
+                          uint32_t pitch, const uint32_t* H, uint32_t delta,
+                          unsigned long long* prof) {
+  // Returns whether a relaxation was dropped because its label did not fit
+  // u16 (then an unreached dst proves nothing: the caller redoes the pair).
+  // The queue holds at most `qcap` nodes: pending nodes are taken in bitmap
+  // order from a cursor that wraps, so a long frontier is worked in chunks
+  // (label-correcting: the order changes nothing of the fixpoint); the
+  // bucket moves only after a whole round of chunks expanded nothing.
   const uint32_t lane = __lane_id();
-  for (uint32_t t = lane; t < pitch / 4; t += 64)
-    reinterpret_cast<uint4*>(D)[t] = make_uint4(kInf, kInf, kInf, kInf);
+  fill_unreached(D, pitch);
   for (uint32_t i = lane; i < bm_words; i += 64) bm[i] = 0;
   wave_sync();
   if (lane == 0) {
-    D[src] = 0;
+    dput(D, src, 0);
     q[0] = (uint16_t)src;
   }
   wave_sync();
   uint32_t qlen = 1;
+  uint32_t span = bm_words, cur = 0;  // the chunk's bitmap words; next chunk's first word
+  uint32_t idle = 0;                  // bitmap words worked since the last expansion
+  uint64_t idle_f = ~0ull;            // smallest f deferred since then
   uint64_t width = delta;
   uint64_t T = (uint64_t)H[src] + width;  // expand pending nodes with f <= T
+  bool sat = false;
   uint32_t sweeps = 0, raises = 0, pending = 0;  // SPF_KSP2_PROF counters
   while (qlen) {
     ++sweeps;
@@ -318,8 +385,8 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
     for (uint32_t i = lane >> lg; i < qlen; i += 64u >> lg) {
       const uint32_t u = q[i];
       const bool drained = g.ovl(u) && u != src;  // recorded, not expanded
-      const uint32_t du = D[u];
-      const uint32_t bound = D[dst];
+      const uint32_t du = dget(D, u);
+      const uint32_t bound = dget(D, dst);
       const uint64_t f = (uint64_t)du + H[u];
       if (drained || f > bound || u == dst) continue;
       if (f > T) {  // a later bucket: stays pending
@@ -335,32 +402,57 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
         const bool ignored = bit(ign, g.link(e));
         const uint32_t hv = H[v];
         if (ignored || hv == kInf || (uint64_t)nd + hv > bound) continue;
-        if (nd < atomicMin(&D[v], nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+        if (sizeof(DT) == 2 && nd >= 0xFFFFu) {
+          sat = true;
+          continue;
+        }
+        if (dmin(D, v, nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
       }
     }
-    if (!__ballot(expanded)) {  // everything pending lies past T: next bucket,
-      const uint64_t m = wave_min64(defer_f);  // twice as wide (a long detour or
-      if (m != ~0ull) {                        // an unreachable dst: log2 raises)
-        ++raises;
-        width = min(2ull * width, 0xFFFFFFFFull);
-        T = m + width;
+    if (!__ballot(expanded)) {  // everything pending seen lies past T: after a
+      idle += span;             // whole round of such chunks the next bucket,
+      idle_f = min(idle_f, wave_min64(defer_f));  // twice as wide (a long
+      if (idle >= bm_words) {                     // detour or an unreachable
+        if (idle_f != ~0ull) {                    // dst: log2 raises)
+          ++raises;
+          width = min(2ull * width, 0xFFFFFFFFull);
+          T = idle_f + width;
+        }
+        idle = 0;
+        idle_f = ~0ull;
       }
+    } else {
+      idle = 0;
+      idle_f = ~0ull;
     }
     wave_sync();
+    // next chunk: up to qcap pending nodes, bitmap words from `cur` on
     uint32_t n = 0;
+    span = bm_words;
     for (uint32_t base = 0; base < bm_words; base += 64) {
-      const uint32_t i = base + lane;
-      uint32_t word = 0;
-      if (i < bm_words) {
-        word = bm[i];
-        bm[i] = 0;
-      }
+      const uint32_t off = base + lane;
+      uint32_t i = cur + off;
+      if (i >= bm_words) i -= bm_words;
+      uint32_t word = off < bm_words ? bm[i] : 0u;
+      const uint32_t pc = __popc(word);
       uint32_t tot;
-      uint32_t at = n + wave_excl_scan32(__popc(word), &tot);
-      while (word) {
-        const uint32_t b = __ffs(word) - 1;
-        word &= word - 1;
-        q[at++] = (uint16_t)(i * 32 + b);
+      uint32_t at = n + wave_excl_scan32(pc, &tot);
+      const uint64_t cut = __ballot(at + pc > qcap);
+      if (word && at < qcap) {
+        for (uint32_t take = min(pc, qcap - at); take; --take) {
+          const uint32_t b = __ffs(word) - 1;
+          word &= word - 1;
+          q[at++] = (uint16_t)(i * 32 + b);
+        }
+        bm[i] = word;  // bits not taken stay pending
+      }
+      if (cut) {  // the queue is full: the next chunk starts at the first word not taken whole
+        const uint32_t first = base + (uint32_t)__ffsll((unsigned long long)cut) - 1;
+        span = first;
+        cur += first;
+        if (cur >= bm_words) cur -= bm_words;
+        n = qcap;
+        break;
       }
       n += tot;
     }
@@ -372,6 +464,7 @@ __device__ void wave_sssp(const G& g, uint32_t* D, uint16_t* q, uint32_t* bm, ui
     atomicAdd(&prof[5], (unsigned long long)raises);
     atomicAdd(&prof[6], (unsigned long long)pending);
   }
+  return __ballot(sat) != 0;
 }
 
 struct KspArgs {
@@ -383,103 +476,147 @@ struct KspArgs {
   spf_ksp2_pair* pairs;
   uint32_t* pool;
   uint64_t cap;
-  unsigned long long* counters;
+  unsigned long long* counters;  // [3] = pairs queued for the u32 redo pass
   unsigned long long* prof;
+  unsigned long long* redo;  // [redo_cap] (i << 32 | d) of u16-label pairs to redo
+  uint64_t redo_cap;
+  uint32_t lw_redo;  // link bitmap words of the redo pass (link ids)
 };
 
-// Per-wave LDS: Dw [pitch] u32, stack/queue [pitch] ST, bitmap, ign, vis.
-template <class ST>
-__host__ __device__ constexpr size_t wave_lds_words(uint32_t pitch, uint32_t bm_words,
+// One wave's LDS: labels D [pitch] DT, DFS stack / SPF queue [cap] ST,
+// pending bitmap, ign [lw] (the k = 1 links), vis [lw] (links tried).
+template <class DT, class ST>
+struct WaveLds {
+  DT* D;
+  ST* stack;
+  uint16_t* q;
+  uint32_t *bm, *ign, *vis;
+  uint32_t cap, lw;
+};
+
+template <class DT, class ST>
+__host__ __device__ constexpr size_t wave_lds_words(uint32_t pitch, uint32_t cap, uint32_t bm_words,
                                                     uint32_t lw) {
   // rounded to 4 words: each wave's D row starts 16-byte aligned (b128 access)
-  return (pitch + (pitch * sizeof(ST) + 3) / 4 + bm_words + 2ull * lw + 3) & ~3ull;
+  return ((pitch * sizeof(DT) + 3) / 4 + (cap * sizeof(ST) + 3) / 4 + bm_words + 2ull * lw + 3) &
+         ~3ull;
+}
+
+template <class DT, class ST>
+__device__ WaveLds<DT, ST> wave_lds(uint32_t* base, uint32_t pitch, uint32_t cap,
+                                    uint32_t bm_words, uint32_t lw) {
+  WaveLds<DT, ST> m;
+  const uint32_t w = threadIdx.x >> 6;
+  uint32_t* p = base + (size_t)w * wave_lds_words<DT, ST>(pitch, cap, bm_words, lw);
+  m.D = reinterpret_cast<DT*>(p);
+  p += (pitch * sizeof(DT) + 3) / 4;
+  m.stack = reinterpret_cast<ST*>(p);  // DFS stack ...
+  m.q = reinterpret_cast<uint16_t*>(p);  // ... or SPF queue
+  p += (cap * sizeof(ST) + 3) / 4;
+  m.bm = p;
+  m.ign = p + bm_words;
+  m.vis = m.ign + lw;
+  m.cap = cap;
+  m.lw = lw;
+  return m;
+}
+
+// One (source i, destination d) pair: k = 1 (trace on the source's SPF row
+// copied into the wave's D), the k = 2 SPF (into the same D) and k = 2.
+// Returns false -- nothing of the pair written, no k = 2 run counted --
+// when a u16-label wave meets a label past 65534 that matters or a path
+// deeper than its stack: the pair goes to the u32 redo pass.
+template <class G, class DT, class ST>
+__device__ bool ksp2_pair(const G& g, const KspArgs& a, const uint32_t* H,
+                          const WaveLds<DT, ST>& m, uint32_t i, uint32_t d, PoolCursor& pc,
+                          uint32_t* k2_runs) {
+  const uint32_t lane = __lane_id(), N = g.N, bm_words = (N + 31) / 32;
+  unsigned long long* used = a.counters;
+  uint32_t* overflow = reinterpret_cast<uint32_t*>(a.counters + 2);
+  const uint32_t s = a.srcs[i];
+  const uint32_t* Drow = a.Dsrc + (size_t)i * a.pitch;
+  spf_ksp2_pair hdr;
+  hdr.first[0] = hdr.first[1] = kInf;
+  hdr.n_paths[0] = hdr.n_paths[1] = 0;
+  const uint32_t d1 = Drow[d];
+  if (d != s && d1 != kInf) {
+    if (sizeof(DT) == 2 && d1 >= 0xFFFFu) return false;
+    // ---- k = 1: trace in getSpfResult(src) (its row copied to LDS) ----
+    load_row(m.D, Drow, a.pitch);
+    for (uint32_t j = lane; j < m.lw; j += 64) {
+      m.vis[j] = 0;
+      m.ign[j] = 0;
+    }
+    wave_sync();
+    uint32_t prev = kInf;
+    uint32_t depth = 0;
+    uint32_t n1 = 0;
+    bool ovf = false;
+    unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+    while (trace_one(g, m.D, nullptr, m.vis, m.stack, m.cap, s, d, &depth, &ovf) && depth) {
+      prev = emit_path(g, m.stack, depth, a.pool, pc, used, a.cap, overflow, prev, m.ign);
+      if (n1++ == 0) hdr.first[0] = prev;
+    }
+    if (ovf) return false;
+    hdr.n_paths[0] = n1;
+    unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long t2 = t1;
+    // ---- k = 2: runSpf(src, true, links of the k = 1 paths), trace ----
+    if (n1) {
+      wave_sync();
+      const bool sat = wave_sssp(g, m.D, m.q, m.cap, m.bm, bm_words, m.ign, s, d, a.pitch, H,
+                                 a.delta, a.prof);
+      if (a.prof) t2 = __builtin_amdgcn_s_memtime();
+      const uint32_t d2 = dget(m.D, d);
+      if (d2 == kInf && sat) return false;
+      if (d2 != kInf) {
+        for (uint32_t j = lane; j < m.lw; j += 64) m.vis[j] = 0;
+        wave_sync();
+        prev = kInf;
+        uint32_t n2 = 0;
+        while (trace_one(g, m.D, m.ign, m.vis, m.stack, m.cap, s, d, &depth, &ovf) && depth) {
+          prev = emit_path(g, m.stack, depth, a.pool, pc, used, a.cap, overflow, prev, nullptr);
+          if (n2++ == 0) hdr.first[1] = prev;
+        }
+        if (ovf) return false;
+        hdr.n_paths[1] = n2;
+      }
+      ++*k2_runs;
+    }
+    if (a.prof && lane == 0) {
+      const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+      atomicAdd(&a.prof[0], t1 - t0);
+      atomicAdd(&a.prof[1], t2 - t1);
+      atomicAdd(&a.prof[2], t3 - t2);
+      atomicAdd(&a.prof[3], 1ull);
+    }
+  }
+  if (lane == 0) a.pairs[(size_t)i * N + d] = hdr;
+  return true;
 }
 
 // The pair loop of one workgroup: the block owns one destination d (its
 // distances-to-d row H, the A* heuristic, staged in LDS) and a chunk of the
-// sources; waves pull sources from a shared counter and run, per pair,
-// k = 1 (trace on the source's SPF row copied into the wave's D), the k = 2
-// SPF (into the same D) and k = 2.
-template <class G, class ST>
+// sources; waves pull sources from a shared counter.
+template <class G, class DT, class ST>
 __device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint32_t* ctl,
-                           uint32_t* wave_base) {
-  const uint32_t N = g.N, bm_words = (N + 31) / 32, pitch = a.pitch, lw = a.lw;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t* Dw = wave_base + (size_t)w * wave_lds_words<ST>(pitch, bm_words, lw);
-  ST* stack = reinterpret_cast<ST*>(Dw + pitch);           // DFS stack ...
-  uint16_t* q = reinterpret_cast<uint16_t*>(stack);         // ... or SPF queue
-  uint32_t* bm = Dw + pitch + (pitch * sizeof(ST) + 3) / 4;
-  uint32_t* ign = bm + bm_words;                            // [lw] k = 1 links
-  uint32_t* vis = ign + lw;                                 // [lw] visited links
-
+                           const WaveLds<DT, ST>& m) {
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t d = blockIdx.x / a.chunks;
   const uint32_t c = blockIdx.x % a.chunks;
   const uint32_t i_end = min(a.n_src, (c + 1) * a.chunk);
-  unsigned long long* used = a.counters;
-  uint32_t* overflow = reinterpret_cast<uint32_t*>(a.counters + 2);
   PoolCursor pc;
   uint32_t k2_runs = 0;
-
   for (;;) {
     uint32_t i = 0;
     if (lane == 0) i = atomicAdd(&ctl[0], 1u);
     i = __builtin_amdgcn_readlane(i, 0);
     if (i >= i_end) break;
-    const uint32_t s = a.srcs[i];
-    const uint32_t* Drow = a.Dsrc + (size_t)i * pitch;
-    spf_ksp2_pair hdr;
-    hdr.first[0] = hdr.first[1] = kInf;
-    hdr.n_paths[0] = hdr.n_paths[1] = 0;
-    if (d != s && Drow[d] != kInf) {
-      // ---- k = 1: trace in getSpfResult(src) (its row copied to LDS) ----
-      {
-        const uint4* in = reinterpret_cast<const uint4*>(Drow);
-        uint4* o = reinterpret_cast<uint4*>(Dw);
-        for (uint32_t t = lane; t < pitch / 4; t += 64) o[t] = in[t];
-      }
-      for (uint32_t j = lane; j < lw; j += 64) {
-        vis[j] = 0;
-        ign[j] = 0;
-      }
-      wave_sync();
-      uint32_t prev = kInf;
-      uint32_t depth = 0;
-      uint32_t n1 = 0;
-      unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
-      while (trace_one(g, Dw, nullptr, vis, stack, s, d, &depth) && depth) {
-        prev = emit_path(g, stack, depth, a.pool, pc, used, a.cap, overflow, prev, ign);
-        if (n1++ == 0) hdr.first[0] = prev;
-      }
-      hdr.n_paths[0] = n1;
-      unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
-      unsigned long long t2 = t1;
-      // ---- k = 2: runSpf(src, true, links of the k = 1 paths), trace ----
-      if (n1) {
-        ++k2_runs;
-        wave_sync();
-        wave_sssp(g, Dw, q, bm, bm_words, ign, s, d, pitch, H, a.delta, a.prof);
-        if (a.prof) t2 = __builtin_amdgcn_s_memtime();
-        if (Dw[d] != kInf) {
-          for (uint32_t j = lane; j < lw; j += 64) vis[j] = 0;
-          wave_sync();
-          prev = kInf;
-          uint32_t n2 = 0;
-          while (trace_one(g, Dw, ign, vis, stack, s, d, &depth) && depth) {
-            prev = emit_path(g, stack, depth, a.pool, pc, used, a.cap, overflow, prev, nullptr);
-            if (n2++ == 0) hdr.first[1] = prev;
-          }
-          hdr.n_paths[1] = n2;
-        }
-      }
-      if (a.prof && lane == 0) {
-        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-        atomicAdd(&a.prof[0], t1 - t0);
-        atomicAdd(&a.prof[1], t2 - t1);
-        atomicAdd(&a.prof[2], t3 - t2);
-        atomicAdd(&a.prof[3], 1ull);
-      }
+    if (!ksp2_pair(g, a, H, m, i, d, pc, &k2_runs) && lane == 0) {
+      const unsigned long long at = atomicAdd(&a.counters[3], 1ull);
+      if (at < a.redo_cap) a.redo[at] = ((unsigned long long)i << 32) | d;
+      else atomicOr(reinterpret_cast<uint32_t*>(a.counters + 2), 2u);
     }
-    if (lane == 0) a.pairs[(size_t)i * N + d] = hdr;
   }
   if (lane == 0 && k2_runs) atomicAdd(&a.counters[1], (unsigned long long)k2_runs);
 }
@@ -499,10 +636,13 @@ __global__ __launch_bounds__(kKspThreads) void ksp2_kernel(GGraph g, KspArgs a) 
   uint32_t* ctl = H + a.pitch;                      // [4] next source
   stage_heuristic_row(a, H, ctl);
   __syncthreads();
-  ksp2_block<GGraph, uint32_t>(g, a, H, ctl, ctl + 4);
+  const auto m = wave_lds<uint32_t, uint32_t>(ctl + 4, a.pitch, a.pitch, (g.N + 31) / 32, a.lw);
+  ksp2_block(g, a, H, ctl, m);
 }
 
 // Graph staged in LDS as 16-bit arrays; waves per workgroup = blockDim / 64.
+// DT = uint16_t: compact labels and a kCompactCap stack / queue per wave.
+template <class DT>
 __global__ __launch_bounds__(kKspLdsMaxThreads) void ksp2_lds_kernel(GGraph gg, KspArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t N = gg.N;
@@ -515,7 +655,8 @@ __global__ __launch_bounds__(kKspLdsMaxThreads) void ksp2_lds_kernel(GGraph gg, 
   uint16_t* wt = col + 2 * e_words;
   uint16_t* rev = wt + 2 * e_words;
   uint8_t* ovl = reinterpret_cast<uint8_t*>(rev + 2 * e_words);
-  uint32_t* wave_base = reinterpret_cast<uint32_t*>(ovl + ((N + 3) & ~3u));
+  const size_t graph_end = (size_t)(ovl + ((N + 3) & ~3u) - smem);
+  uint32_t* wave_base = reinterpret_cast<uint32_t*>(smem + ((graph_end + 15) & ~(size_t)15));
   for (uint32_t v = threadIdx.x; v <= N; v += blockDim.x) rp[v] = (uint16_t)gg.row_ptr[v];
   for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
     col[e] = (uint16_t)gg.col_[e];
@@ -526,20 +667,52 @@ __global__ __launch_bounds__(kKspLdsMaxThreads) void ksp2_lds_kernel(GGraph gg, 
   stage_heuristic_row(a, H, ctl);
   __syncthreads();
   const LGraph g{rp, col, wt, rev, gg.link_, ovl, N};
-  ksp2_block<LGraph, uint16_t>(g, a, H, ctl, wave_base);
+  const uint32_t cap = sizeof(DT) == 2 ? kCompactCap : a.pitch;
+  const auto m = wave_lds<DT, uint16_t>(wave_base, a.pitch, cap, (N + 31) / 32, a.lw);
+  ksp2_block(g, a, H, ctl, m);
+}
+
+// The u32 redo pass of a compact plan: the pairs its u16-label waves handed
+// back (counters[3] of them), graph and heuristic rows read from HBM, full
+// size stacks.  Exits at once when there are none.
+__global__ __launch_bounds__(kKspThreads) void ksp2_redo_kernel(GGraph g, KspArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned long long n = min((unsigned long long)a.redo_cap, a.counters[3]);
+  if (n == 0) return;
+  const uint32_t waves = blockDim.x >> 6, w = threadIdx.x >> 6;
+  const auto m = wave_lds<uint32_t, uint32_t>(reinterpret_cast<uint32_t*>(smem), a.pitch, a.pitch,
+                                              (g.N + 31) / 32, a.lw_redo);
+  PoolCursor pc;
+  uint32_t k2_runs = 0;
+  for (unsigned long long j = (unsigned long long)blockIdx.x * waves + w; j < n;
+       j += (unsigned long long)gridDim.x * waves) {
+    const unsigned long long r = a.redo[j];
+    const uint32_t i = (uint32_t)(r >> 32), d = (uint32_t)r;
+    (void)ksp2_pair(g, a, a.Hrows + (size_t)d * a.pitch, m, i, d, pc, &k2_runs);
+  }
+  if ((threadIdx.x & 63) == 0 && k2_runs)
+    atomicAdd(&a.counters[1], (unsigned long long)k2_runs);
 }
 
 size_t ksp2_lds_bytes(uint32_t N, uint32_t pitch, uint32_t lw) {
   const size_t bm_words = (N + 31) / 32;
-  return 4ull * (pitch + 4 + kKspWaves * wave_lds_words<uint32_t>(pitch, bm_words, lw));
+  return 4ull * (pitch + 4 + kKspWaves * wave_lds_words<uint32_t, uint32_t>(pitch, pitch, bm_words, lw));
 }
 
 // LDS bytes of the staged-graph kernel with `waves` waves per workgroup
-size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw,
-                            uint32_t waves) {
+// (compact: u16 labels)
+size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw, uint32_t waves,
+                            bool compact) {
   const size_t bm_words = (N + 31) / 32;
   const size_t graph = 4ull * ((N + 2) / 2 + 3ull * ((E + 1) / 2)) + ((N + 3) & ~3u);
-  return 4ull * (pitch + 4) + graph + 4ull * waves * wave_lds_words<uint16_t>(pitch, bm_words, lw);
+  const size_t fixed = (4ull * (pitch + 4) + graph + 15) & ~(size_t)15;
+  const size_t wave = compact ? wave_lds_words<uint16_t, uint16_t>(pitch, kCompactCap, bm_words, lw)
+                              : wave_lds_words<uint32_t, uint16_t>(pitch, pitch, bm_words, lw);
+  return fixed + 4ull * waves * wave;
+}
+
+size_t ksp2_redo_wave_bytes(uint32_t N, uint32_t pitch, uint32_t lw) {
+  return 4ull * wave_lds_words<uint32_t, uint32_t>(pitch, pitch, (N + 31) / 32, lw);
 }
 
 }  // namespace
@@ -591,6 +764,10 @@ struct spf_ksp2_plan {
   DevBuf<unsigned long long> d_prof;  // SPF_KSP2_PROF diagnostics
   size_t lds = 0;
   uint32_t lds_waves = 0;  // > 0: the staged-graph kernel with this many waves
+  bool compact = false;     // ... with u16 labels, and the u32 redo pass behind it
+  uint32_t lw_links = 0, redo_waves = 0;
+  size_t redo_lds = 0;
+  DevBuf<unsigned long long> d_redo;  // [n_src * N] pairs handed to the redo pass
   std::vector<hipEvent_t> ev;
   uint32_t timing_cap = 0, timing_n = 0;
   // outside the batched kernel's envelope (metrics <= 0, u64 labels, more
@@ -626,7 +803,7 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     return SPF_OK;
   };
   if (c->nonpos || c->needs64 || c->N > 65535 || std::getenv("SPF_KSP2_EXACT")) return go_exact();
-  p->lw = c->max_link / 32 + 1;
+  p->lw = p->lw_links = c->max_link / 32 + 1;
   {  // bucket width: the mean up-link metric (env SPF_KSP2_DELTA overrides;
      // 4294967295 = no order, the plain hop-synchronous sweep)
     uint64_t sum = 0;
@@ -648,20 +825,42 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   }
   if (pairs_are_links && c->max_metric < 65536 && !std::getenv("SPF_KSP2_HBM")) {
     const uint32_t lw_pairs = c->E / 32 + 1;
-    for (uint32_t w = kKspLdsMaxThreads / 64; w >= 2; --w)
-      if (ksp2_lds_graph_bytes(c->N, c->E, c->pitch, lw_pairs, w) <= kMaxLdsKsp) {
-        p->lds_waves = w;
-        p->lw = lw_pairs;
-        p->lds = ksp2_lds_graph_bytes(c->N, c->E, c->pitch, lw_pairs, w);
-        break;
+    auto fit = [&](bool compact) -> uint32_t {
+      for (uint32_t w = kKspLdsMaxThreads / 64; w >= 2; --w)
+        if (ksp2_lds_graph_bytes(c->N, c->E, c->pitch, lw_pairs, w, compact) <= kMaxLdsKsp) return w;
+      return 0;
+    };
+    const uint32_t w32 = fit(false);
+    // u16 labels (SPF_KSP2_U16=0: never, =1: whenever they fit): more waves
+    // per CU to hide LDS latency; pairs whose labels pass 65534 or whose
+    // paths outgrow the short stack are redone with u32 labels
+    const char* u16env = std::getenv("SPF_KSP2_U16");
+    const uint32_t redo_wave = (uint32_t)ksp2_redo_wave_bytes(c->N, c->pitch, p->lw_links);
+    const uint32_t redo_waves = std::min<uint32_t>(kKspWaves, (uint32_t)(kMaxLdsKsp / redo_wave));
+    const uint32_t w16 = (u16env && u16env[0] == '0') || !redo_waves ? 0 : fit(true);
+    const bool compact = w16 && (w16 > w32 || (u16env && u16env[0] == '1'));
+    const uint32_t w = compact ? w16 : w32;
+    if (w) {
+      p->lds_waves = w;
+      p->compact = compact;
+      p->lw = lw_pairs;
+      p->lds = ksp2_lds_graph_bytes(c->N, c->E, c->pitch, lw_pairs, w, compact);
+      if (compact) {
+        p->redo_waves = redo_waves;
+        p->redo_lds = (size_t)redo_wave * redo_waves;
       }
+    }
   }
   if (!p->lds_waves) p->lds = ksp2_lds_bytes(c->N, c->pitch, p->lw);
   if (p->lds > kMaxLdsKsp) return go_exact();  // the per-wave rows do not fit the LDS
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_kernel,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
-  HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_lds_kernel,
+  HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_lds_kernel<uint32_t>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
+  HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_lds_kernel<uint16_t>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
+  HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_redo_kernel,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsKsp));
   {
     const spf_status st = set_lds_limits(c);
@@ -669,6 +868,7 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   }
   HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
   HIP_TRY(c, p->d_D.alloc((size_t)n_src * c->pitch));
+  if (p->compact) HIP_TRY(c, p->d_redo.alloc((size_t)n_src * c->N));
   {  // distances TO every node: SPF over transposed metrics, no drains (a
      // lower bound of every drained / link-ignored distance)
     std::vector<uint32_t> all(c->N), wr(c->E);
@@ -741,13 +941,22 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
   // blocks: (destination, chunk of p->chunk sources)
   const uint32_t chunks = (p->n_src + p->chunk - 1) / p->chunk;
   KspArgs a{p->d_D.p, p->d_H.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, p->chunk, p->delta, d_pairs,
-            d_pool, pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p};
-  if (p->lds_waves)
-    hipLaunchKernelGGL(ksp2_lds_kernel, dim3(c->N * chunks), dim3(64 * p->lds_waves), p->lds, s,
-                       g, a);
+            d_pool, pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p,
+            p->d_redo.p, (uint64_t)p->d_redo.n, p->lw_links};
+  if (p->compact)
+    hipLaunchKernelGGL(ksp2_lds_kernel<uint16_t>, dim3(c->N * chunks), dim3(64 * p->lds_waves),
+                       p->lds, s, g, a);
+  else if (p->lds_waves)
+    hipLaunchKernelGGL(ksp2_lds_kernel<uint32_t>, dim3(c->N * chunks), dim3(64 * p->lds_waves),
+                       p->lds, s, g, a);
   else
     hipLaunchKernelGGL(ksp2_kernel, dim3(c->N * chunks), dim3(kKspThreads), p->lds, s, g, a);
   HIP_TRY(c, hipGetLastError());
+  if (p->compact) {  // pairs the u16 waves handed back (usually none: the kernel exits)
+    hipLaunchKernelGGL(ksp2_redo_kernel, dim3(kRedoBlocks), dim3(64 * p->redo_waves), p->redo_lds,
+                       s, g, a);
+    HIP_TRY(c, hipGetLastError());
+  }
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
   c->solves += p->n_src;  // k = 2 runs are added by spf_ksp2_solve / the caller
   return SPF_OK;
