@@ -318,9 +318,11 @@ spf_status spf_ksp2_digest(spf_ksp2_plan* plan, const spf_ksp2_pair* d_pairs, co
 spf_status spf_ksp2_enable_timing(spf_ksp2_plan* plan, uint32_t max_executes);
 spf_status spf_ksp2_timing(spf_ksp2_plan* plan, double* spf_ms, double* ksp_ms, uint32_t* n);
 /* Convenience: plan + execute (growing the device pool on overflow) + copy
- * back.  pairs_out = [n_src * n_nodes]; *pool_used = words written.  With
- * pool_out == NULL or pool_cap < *pool_used only the pairs are copied (the
- * latter returns SPF_E_NOMEM): call again with a pool of *pool_used words. */
+ * back.  pairs_out = [n_src * n_nodes]; the records are repacked densely in
+ * pair order (k = 1 then k = 2, list order), so *pool_used -- the packed
+ * size -- is the same on every call.  With pool_out == NULL or pool_cap <
+ * *pool_used only the pairs are copied (the latter returns SPF_E_NOMEM): call
+ * again with a pool of *pool_used words. */
 spf_status spf_ksp2_solve(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
                           spf_ksp2_pair* pairs_out, uint32_t* pool_out, uint64_t pool_cap,
                           uint64_t* pool_used);

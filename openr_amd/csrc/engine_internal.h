@@ -115,6 +115,7 @@ struct spf_ctx {
   // barrier-timeout word of this context's grid-resident / team launches
   // (spf_device_check reads and clears it)
   spfi::DevBuf<uint32_t> d_fault;
+  bool team_off = false;  // a team barrier timed out: plans keep msbfs_kernel
   std::string err;
   uint64_t solves = 0;
   uint64_t shape = 0;  // bumped by spf_graph_load (CSR structure)

@@ -32,6 +32,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 
 using namespace spfi;
@@ -46,6 +47,7 @@ constexpr uint32_t kPoolGrab = 256;         // words a wave reserves at a time (
 constexpr size_t kMaxLdsKsp = 160 * 1024;
 constexpr uint32_t kCompactCap = 512;       // u16-label waves: DFS stack / SPF queue entries
 constexpr uint32_t kRedoBlocks = 256;       // workgroups of the u32 redo pass
+constexpr uint32_t kProfSlots = 1024;       // SPF_KSP2_PROF: 16-counter slots (by block)
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -112,6 +114,14 @@ __device__ __forceinline__ bool bit(const uint32_t* bm, uint32_t i) {
   return (bm[i >> 5] >> (i & 31)) & 1u;
 }
 
+// The A* heuristic row: u32, or u16 in the staged-graph kernel (0xFFFF =
+// dst unreachable; finite distances saturate at 0xFFFE -- still a lower bound)
+__device__ __forceinline__ uint32_t hget(const uint32_t* H, uint32_t v) { return H[v]; }
+__device__ __forceinline__ uint32_t hget(const uint16_t* H, uint32_t v) {
+  const uint32_t x = H[v];
+  return x == 0xFFFFu ? kInf : x;
+}
+
 // A wave's distance row: u32 labels, or u16 labels on compact plans (0xFFFF
 // = unreached or >= 65535; a pair whose labels leave that range is redone
 // with u32 labels, see ksp2_pair).
@@ -163,6 +173,11 @@ __device__ __forceinline__ void load_row(uint16_t* D, const uint32_t* Drow, uint
 // Graph accessors: the CSR in HBM (any size), or a 16-bit copy staged in
 // LDS by each workgroup (small graphs: every DFS step and relaxation then
 // costs LDS latency instead of L2 latency).
+struct NodeInfo {
+  uint32_t beg, end;  // out-edges [beg, end)
+  bool ovl;           // drained (overloaded)
+};
+
 struct GGraph {
   const uint32_t* row_ptr;
   const uint32_t* col_;
@@ -171,7 +186,7 @@ struct GGraph {
   const uint32_t* link_;
   const uint8_t* ovl_;
   uint32_t N;
-  __device__ uint32_t rp(uint32_t v) const { return row_ptr[v]; }
+  __device__ NodeInfo node(uint32_t v) const { return {row_ptr[v], row_ptr[v + 1], ovl_[v] != 0}; }
   __device__ uint32_t col(uint32_t e) const { return col_[e]; }
   __device__ uint32_t w(uint32_t e) const { return wt[e]; }
   __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
@@ -179,29 +194,45 @@ struct GGraph {
   __device__ uint32_t link_of(uint32_t e, uint32_t) const { return link_[e]; }  // r = rev(e)
   __device__ uint32_t out_link(uint32_t e) const { return link_[e]; }  // pool record
   __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
+  // the ignored-link bitmap: by link id
+  __device__ uint32_t ign_at(uint32_t e) const { return link_[e]; }
+  __device__ void mark_ign(uint32_t* bm, uint32_t e) const {
+    const uint32_t l = link_[e];
+    atomicOr(&bm[l >> 5], 1u << (l & 31));
+  }
 };
 
-// The staged graph indexes its link bitmaps by the edge pair {e, rev(e)}
-// (min of the two ids) instead of the link id: an up link is exactly one
-// such pair (checked when the plan is made), and the 16-bit link array then
-// stays out of LDS -- room for one more wave per workgroup.  Pool records
-// still carry link ids, read from HBM.
+// The staged graph indexes its visited-link bitmap by the edge pair
+// {e, rev(e)} (min of the two ids) instead of the link id: an up link is
+// exactly one such pair (checked when the plan is made), and the 16-bit link
+// array then stays out of LDS -- room for one more wave per workgroup.  The
+// ignored-link bitmap is indexed by edge id, both directions of a link
+// marked, so a relaxation tests it without loading rev(e).  Head and metric
+// share one 32-bit word per edge, first edge, degree and the drained flag one
+// per node (one LDS read each).
 struct LGraph {
-  const uint16_t* row_ptr;  // [N+1] (E < 65536)
-  const uint16_t* col_;
-  const uint16_t* wt;       // metrics < 65536
+  const uint32_t* nd_;      // [N] first edge | degree << 16 | drained << 31 (E < 65536, deg < 32768)
+  const uint32_t* cw_;      // head | metric << 16 (metrics < 65536)
   const uint16_t* rev_;
-  const uint32_t* glink;    // link ids (HBM)
-  const uint8_t* ovl_;
+  const uint32_t* glink;    // link ids (HBM): pool records only
   uint32_t N;
-  __device__ uint32_t rp(uint32_t v) const { return row_ptr[v]; }
-  __device__ uint32_t col(uint32_t e) const { return col_[e]; }
-  __device__ uint32_t w(uint32_t e) const { return wt[e]; }
+  __device__ NodeInfo node(uint32_t v) const {
+    const uint32_t x = nd_[v];
+    return {x & 0xFFFFu, (x & 0xFFFFu) + ((x >> 16) & 0x7FFFu), (x >> 31) != 0};
+  }
+  __device__ uint32_t col(uint32_t e) const { return cw_[e] & 0xFFFFu; }
+  __device__ uint32_t w(uint32_t e) const { return cw_[e] >> 16; }
   __device__ uint32_t rev(uint32_t e) const { return rev_[e]; }
   __device__ uint32_t link(uint32_t e) const { return min(e, (uint32_t)rev_[e]); }
   __device__ uint32_t link_of(uint32_t e, uint32_t r) const { return min(e, r); }  // r = rev(e)
+  __device__ bool ovl(uint32_t v) const { return (nd_[v] >> 31) != 0; }
+  __device__ uint32_t ign_at(uint32_t e) const { return e; }
   __device__ uint32_t out_link(uint32_t e) const { return glink[e]; }
-  __device__ bool ovl(uint32_t v) const { return ovl_[v] != 0; }
+  __device__ void mark_ign(uint32_t* bm, uint32_t e) const {
+    const uint32_t r = rev_[e];
+    atomicOr(&bm[e >> 5], 1u << (e & 31));
+    atomicOr(&bm[r >> 5], 1u << (r & 31));
+  }
 };
 
 // Per-wave bump allocation in the path pool.  Returns the word offset, or
@@ -209,16 +240,21 @@ struct LGraph {
 // learns the size it needs).
 struct PoolCursor {
   uint64_t cur = 0, end = 0;
+  uint32_t grab = kPoolGrab;   // words per reservation (SPF_KSP2_GRAB)
+  bool prof = false;
+  unsigned long long clk = 0;  // SPF_KSP2_PROF: clocks spent reserving
 };
 
 __device__ uint32_t pool_alloc(PoolCursor& pc, uint32_t words, unsigned long long* used,
                                uint64_t cap, uint32_t* overflow) {
   if (pc.cur + words > pc.end) {
-    const uint32_t grab = words > kPoolGrab ? words : kPoolGrab;
+    const uint32_t grab = words > pc.grab ? words : pc.grab;
+    const unsigned long long t0 = pc.prof ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t base = 0;
     if (__lane_id() == 0) base = atomicAdd(used, (unsigned long long)grab);
     base = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(base >> 32), 0) << 32) |
            __builtin_amdgcn_readlane((uint32_t)base, 0);
+    if (pc.prof) pc.clk += __builtin_amdgcn_s_memtime() - t0;
     pc.cur = base;
     pc.end = base + grab;
   }
@@ -240,17 +276,19 @@ __device__ uint32_t pool_alloc(PoolCursor& pc, uint32_t words, unsigned long lon
 template <class G, class DT, class ST>
 __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t* vis,
                           ST* stack, uint32_t cap, uint32_t src, uint32_t dst, uint32_t* depth,
-                          bool* ovf) {
+                          bool* ovf, uint32_t* steps) {
   const uint32_t lane = __lane_id();
   uint32_t k = 0, v = dst, dv = dget(D, dst);
   for (;;) {
+    ++*steps;
     if (v == src) {
       *depth = k;
       return true;
     }
     uint64_t best = ~0ull;
     uint32_t tail = 0, tl = 0;  // this lane's best candidate: tail node, link index
-    const uint32_t e_beg = g.rp(v), e_end = g.rp(v + 1);
+    const NodeInfo nv = g.node(v);
+    const uint32_t e_beg = nv.beg, e_end = nv.end;
     for (uint32_t e = e_beg + lane; e < e_end; e += 64) {
       // in-edge u -> v is the reverse of the out-edge v -> u; every test's
       // load is issued up front (two dependent LDS rounds per step)
@@ -258,7 +296,7 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       const uint32_t r = g.rev(e);
       const uint32_t l = g.link_of(e, r);
       const bool drained = g.ovl(u) && u != src;
-      const bool tried = bit(vis, l) || (ign && bit(ign, l));
+      const bool tried = bit(vis, l) || (ign && bit(ign, g.ign_at(e)));
       const uint32_t du = dget(D, u);
       const uint32_t wr = g.w(r);
       if (!drained && !tried && du != kInf && du + wr == dv) {
@@ -315,10 +353,7 @@ __device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint3
   const uint32_t at = pool_alloc(pc, depth + 2, used, cap, overflow);
   for (uint32_t j = lane; j < depth; j += 64) {
     const uint32_t e = stack[depth - 1 - j];  // src -> dst order
-    if (mark) {
-      const uint32_t l = g.link(e);
-      atomicOr(&mark[l >> 5], 1u << (l & 31));
-    }
+    if (mark) g.mark_ign(mark, e);
     if (at != kInf) pool[(size_t)at + 2 + j] = g.out_link(e);
   }
   if (at != kInf && lane == 0) {
@@ -345,10 +380,10 @@ __device__ uint32_t emit_path(const G& g, const ST* stack, uint32_t depth, uint3
 // after expanding every node within dst's hop count (bound D[dst] = inf
 // until then); with it, only nodes with f < d2(dst) + delta are expanded.
 // The fixpoint -- and so every distance the trace reads -- is the same.
-template <class G, class DT>
+template <class G, class DT, class HT>
 __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_t* bm,
                           uint32_t bm_words, const uint32_t* ign, uint32_t src, uint32_t dst,
-                          uint32_t pitch, const uint32_t* H, uint32_t delta,
+                          uint32_t pitch, const HT* H, uint32_t delta,
                           unsigned long long* prof) {
   // Returns whether a relaxation was dropped because its label did not fit
   // u16 (then an unreached dst proves nothing: the caller redoes the pair).
@@ -370,7 +405,7 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
   uint32_t idle = 0;                  // bitmap words worked since the last expansion
   uint64_t idle_f = ~0ull;            // smallest f deferred since then
   uint64_t width = delta;
-  uint64_t T = (uint64_t)H[src] + width;  // expand pending nodes with f <= T
+  uint64_t T = (uint64_t)hget(H, src) + width;  // expand pending nodes with f <= T
   bool sat = false;
   uint32_t sweeps = 0, raises = 0, pending = 0;  // SPF_KSP2_PROF counters
   while (qlen) {
@@ -384,10 +419,12 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
     bool expanded = false;
     for (uint32_t i = lane >> lg; i < qlen; i += 64u >> lg) {
       const uint32_t u = q[i];
-      const bool drained = g.ovl(u) && u != src;  // recorded, not expanded
+      const NodeInfo nu = g.node(u);
+      const bool drained = nu.ovl && u != src;  // recorded, not expanded
       const uint32_t du = dget(D, u);
+      // dst's label now (read per node: a sweep-start copy expanded 6 % more)
       const uint32_t bound = dget(D, dst);
-      const uint64_t f = (uint64_t)du + H[u];
+      const uint64_t f = (uint64_t)du + hget(H, u);
       if (drained || f > bound || u == dst) continue;
       if (f > T) {  // a later bucket: stays pending
         if (slot == 0) atomicOr(&bm[u >> 5], 1u << (u & 31));
@@ -395,12 +432,11 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
         continue;
       }
       expanded = true;
-      const uint32_t e_end = g.rp(u + 1);
-      for (uint32_t e = g.rp(u) + slot; e < e_end; e += 1u << lg) {
+      for (uint32_t e = nu.beg + slot; e < nu.end; e += 1u << lg) {
         const uint32_t v = g.col(e);
         const uint32_t nd = du + g.w(e);
-        const bool ignored = bit(ign, g.link(e));
-        const uint32_t hv = H[v];
+        const bool ignored = bit(ign, g.ign_at(e));
+        const uint32_t hv = hget(H, v);
         if (ignored || hv == kInf || (uint64_t)nd + hv > bound) continue;
         if (sizeof(DT) == 2 && nd >= 0xFFFFu) {
           sat = true;
@@ -460,6 +496,7 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
     qlen = n;
   }
   if (prof && __lane_id() == 0) {
+    prof += (blockIdx.x & (kProfSlots - 1)) * 16;  // spread: no same-address atomics
     atomicAdd(&prof[4], (unsigned long long)sweeps);
     atomicAdd(&prof[5], (unsigned long long)raises);
     atomicAdd(&prof[6], (unsigned long long)pending);
@@ -481,6 +518,7 @@ struct KspArgs {
   unsigned long long* redo;  // [redo_cap] (i << 32 | d) of u16-label pairs to redo
   uint64_t redo_cap;
   uint32_t lw_redo;  // link bitmap words of the redo pass (link ids)
+  uint32_t grab;     // pool words a wave reserves at a time
 };
 
 // One wave's LDS: labels D [pitch] DT, DFS stack / SPF queue [cap] ST,
@@ -526,8 +564,8 @@ __device__ WaveLds<DT, ST> wave_lds(uint32_t* base, uint32_t pitch, uint32_t cap
 // Returns false -- nothing of the pair written, no k = 2 run counted --
 // when a u16-label wave meets a label past 65534 that matters or a path
 // deeper than its stack: the pair goes to the u32 redo pass.
-template <class G, class DT, class ST>
-__device__ bool ksp2_pair(const G& g, const KspArgs& a, const uint32_t* H,
+template <class G, class DT, class ST, class HT>
+__device__ bool ksp2_pair(const G& g, const KspArgs& a, const HT* H,
                           const WaveLds<DT, ST>& m, uint32_t i, uint32_t d, PoolCursor& pc,
                           uint32_t* k2_runs) {
   const uint32_t lane = __lane_id(), N = g.N, bm_words = (N + 31) / 32;
@@ -552,9 +590,13 @@ __device__ bool ksp2_pair(const G& g, const KspArgs& a, const uint32_t* H,
     uint32_t depth = 0;
     uint32_t n1 = 0;
     bool ovf = false;
+    uint32_t st1 = 0, st2 = 0;  // SPF_KSP2_PROF: trace steps, emit clocks
+    unsigned long long te = 0;
     unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
-    while (trace_one(g, m.D, nullptr, m.vis, m.stack, m.cap, s, d, &depth, &ovf) && depth) {
+    while (trace_one(g, m.D, nullptr, m.vis, m.stack, m.cap, s, d, &depth, &ovf, &st1) && depth) {
+      const unsigned long long e0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
       prev = emit_path(g, m.stack, depth, a.pool, pc, used, a.cap, overflow, prev, m.ign);
+      if (a.prof) te += __builtin_amdgcn_s_memtime() - e0;
       if (n1++ == 0) hdr.first[0] = prev;
     }
     if (ovf) return false;
@@ -574,8 +616,10 @@ __device__ bool ksp2_pair(const G& g, const KspArgs& a, const uint32_t* H,
         wave_sync();
         prev = kInf;
         uint32_t n2 = 0;
-        while (trace_one(g, m.D, m.ign, m.vis, m.stack, m.cap, s, d, &depth, &ovf) && depth) {
+        while (trace_one(g, m.D, m.ign, m.vis, m.stack, m.cap, s, d, &depth, &ovf, &st2) && depth) {
+          const unsigned long long e0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
           prev = emit_path(g, m.stack, depth, a.pool, pc, used, a.cap, overflow, prev, nullptr);
+          if (a.prof) te += __builtin_amdgcn_s_memtime() - e0;
           if (n2++ == 0) hdr.first[1] = prev;
         }
         if (ovf) return false;
@@ -585,10 +629,14 @@ __device__ bool ksp2_pair(const G& g, const KspArgs& a, const uint32_t* H,
     }
     if (a.prof && lane == 0) {
       const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-      atomicAdd(&a.prof[0], t1 - t0);
-      atomicAdd(&a.prof[1], t2 - t1);
-      atomicAdd(&a.prof[2], t3 - t2);
-      atomicAdd(&a.prof[3], 1ull);
+      unsigned long long* P = a.prof + (blockIdx.x & (kProfSlots - 1)) * 16;
+      atomicAdd(&P[0], t1 - t0);
+      atomicAdd(&P[1], t2 - t1);
+      atomicAdd(&P[2], t3 - t2);
+      atomicAdd(&P[3], 1ull);
+      atomicAdd(&P[7], (unsigned long long)st1);
+      atomicAdd(&P[8], (unsigned long long)st2);
+      atomicAdd(&P[9], te);
     }
   }
   if (lane == 0) a.pairs[(size_t)i * N + d] = hdr;
@@ -598,14 +646,16 @@ __device__ bool ksp2_pair(const G& g, const KspArgs& a, const uint32_t* H,
 // The pair loop of one workgroup: the block owns one destination d (its
 // distances-to-d row H, the A* heuristic, staged in LDS) and a chunk of the
 // sources; waves pull sources from a shared counter.
-template <class G, class DT, class ST>
-__device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint32_t* ctl,
+template <class G, class DT, class ST, class HT>
+__device__ void ksp2_block(const G& g, const KspArgs& a, const HT* H, uint32_t* ctl,
                            const WaveLds<DT, ST>& m) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t d = blockIdx.x / a.chunks;
   const uint32_t c = blockIdx.x % a.chunks;
   const uint32_t i_end = min(a.n_src, (c + 1) * a.chunk);
   PoolCursor pc;
+  pc.grab = a.grab;
+  pc.prof = a.prof != nullptr;
   uint32_t k2_runs = 0;
   for (;;) {
     uint32_t i = 0;
@@ -619,6 +669,7 @@ __device__ void ksp2_block(const G& g, const KspArgs& a, const uint32_t* H, uint
     }
   }
   if (lane == 0 && k2_runs) atomicAdd(&a.counters[1], (unsigned long long)k2_runs);
+  if (a.prof && lane == 0) atomicAdd(&a.prof[(blockIdx.x & (kProfSlots - 1)) * 16 + 10], pc.clk);
 }
 
 __device__ void stage_heuristic_row(const KspArgs& a, uint32_t* H, uint32_t* ctl) {
@@ -626,6 +677,17 @@ __device__ void stage_heuristic_row(const KspArgs& a, uint32_t* H, uint32_t* ctl
   const uint4* in = reinterpret_cast<const uint4*>(a.Hrows + (size_t)d * a.pitch);
   uint4* o = reinterpret_cast<uint4*>(H);
   for (uint32_t t = threadIdx.x; t < a.pitch / 4; t += blockDim.x) o[t] = in[t];
+  if (threadIdx.x == 0) ctl[0] = c * a.chunk;
+}
+__device__ __forceinline__ uint32_t h16(uint32_t x) { return x == kInf ? 0xFFFFu : min(x, 0xFFFEu); }
+__device__ void stage_heuristic_row(const KspArgs& a, uint16_t* H, uint32_t* ctl) {
+  const uint32_t d = blockIdx.x / a.chunks, c = blockIdx.x % a.chunks;
+  const uint4* in = reinterpret_cast<const uint4*>(a.Hrows + (size_t)d * a.pitch);
+  uint2* o = reinterpret_cast<uint2*>(H);
+  for (uint32_t t = threadIdx.x; t < a.pitch / 4; t += blockDim.x) {
+    const uint4 x = in[t];
+    o[t] = make_uint2(h16(x.x) | (h16(x.y) << 16), h16(x.z) | (h16(x.w) << 16));
+  }
   if (threadIdx.x == 0) ctl[0] = c * a.chunk;
 }
 
@@ -646,27 +708,26 @@ template <class DT>
 __global__ __launch_bounds__(kKspLdsMaxThreads) void ksp2_lds_kernel(GGraph gg, KspArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t N = gg.N;
-  uint32_t* H = reinterpret_cast<uint32_t*>(smem);  // [pitch] distances to d
-  uint32_t* ctl = H + a.pitch;                      // [4] next source
+  uint16_t* H = reinterpret_cast<uint16_t*>(smem);  // [pitch] distances to d (u16)
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(H + a.pitch);  // [4] next source
   const uint32_t E = gg.row_ptr[N];
-  const uint32_t rp_words = (N + 2) / 2, e_words = (E + 1) / 2;
-  uint16_t* rp = reinterpret_cast<uint16_t*>(ctl + 4);
-  uint16_t* col = rp + 2 * rp_words;
-  uint16_t* wt = col + 2 * e_words;
-  uint16_t* rev = wt + 2 * e_words;
-  uint8_t* ovl = reinterpret_cast<uint8_t*>(rev + 2 * e_words);
-  const size_t graph_end = (size_t)(ovl + ((N + 3) & ~3u) - smem);
+  const uint32_t e_words = (E + 1) / 2;
+  uint32_t* cw = ctl + 4;
+  uint32_t* nd = cw + E;
+  uint16_t* rev = reinterpret_cast<uint16_t*>(nd + N);
+  const size_t graph_end = (size_t)(reinterpret_cast<unsigned char*>(rev + 2 * e_words) - smem);
   uint32_t* wave_base = reinterpret_cast<uint32_t*>(smem + ((graph_end + 15) & ~(size_t)15));
-  for (uint32_t v = threadIdx.x; v <= N; v += blockDim.x) rp[v] = (uint16_t)gg.row_ptr[v];
+  for (uint32_t v = threadIdx.x; v < N; v += blockDim.x) {
+    const uint32_t b = gg.row_ptr[v];
+    nd[v] = b | ((gg.row_ptr[v + 1] - b) << 16) | ((gg.ovl_[v] ? 1u : 0u) << 31);
+  }
   for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
-    col[e] = (uint16_t)gg.col_[e];
-    wt[e] = (uint16_t)gg.wt[e];
+    cw[e] = gg.col_[e] | (gg.wt[e] << 16);
     rev[e] = (uint16_t)gg.rev_[e];
   }
-  for (uint32_t v = threadIdx.x; v < N; v += blockDim.x) ovl[v] = gg.ovl_[v];
   stage_heuristic_row(a, H, ctl);
   __syncthreads();
-  const LGraph g{rp, col, wt, rev, gg.link_, ovl, N};
+  const LGraph g{nd, cw, rev, gg.link_, N};
   const uint32_t cap = sizeof(DT) == 2 ? kCompactCap : a.pitch;
   const auto m = wave_lds<DT, uint16_t>(wave_base, a.pitch, cap, (N + 31) / 32, a.lw);
   ksp2_block(g, a, H, ctl, m);
@@ -683,6 +744,7 @@ __global__ __launch_bounds__(kKspThreads) void ksp2_redo_kernel(GGraph g, KspArg
   const auto m = wave_lds<uint32_t, uint32_t>(reinterpret_cast<uint32_t*>(smem), a.pitch, a.pitch,
                                               (g.N + 31) / 32, a.lw_redo);
   PoolCursor pc;
+  pc.grab = a.grab;
   uint32_t k2_runs = 0;
   for (unsigned long long j = (unsigned long long)blockIdx.x * waves + w; j < n;
        j += (unsigned long long)gridDim.x * waves) {
@@ -704,8 +766,8 @@ size_t ksp2_lds_bytes(uint32_t N, uint32_t pitch, uint32_t lw) {
 size_t ksp2_lds_graph_bytes(uint32_t N, uint32_t E, uint32_t pitch, uint32_t lw, uint32_t waves,
                             bool compact) {
   const size_t bm_words = (N + 31) / 32;
-  const size_t graph = 4ull * ((N + 2) / 2 + 3ull * ((E + 1) / 2)) + ((N + 3) & ~3u);
-  const size_t fixed = (4ull * (pitch + 4) + graph + 15) & ~(size_t)15;
+  const size_t graph = 4ull * (E + N + (E + 1) / 2);  // cw, nd, rev
+  const size_t fixed = (2ull * pitch + 16 + graph + 15) & ~(size_t)15;  // H u16, ctl
   const size_t wave = compact ? wave_lds_words<uint16_t, uint16_t>(pitch, kCompactCap, bm_words, lw)
                               : wave_lds_words<uint32_t, uint16_t>(pitch, pitch, bm_words, lw);
   return fixed + 4ull * waves * wave;
@@ -736,12 +798,14 @@ __global__ __launch_bounds__(256) void ksp2_digest_kernel(const spf_ksp2_pair* _
   const uint32_t i = blockIdx.y;
   if (i >= n_src || t >= n) return;
   const uint32_t d = (uint32_t)t;
-  const spf_ksp2_pair r = pairs[(size_t)i * n + d];
+  const uint4 r = reinterpret_cast<const uint4*>(pairs)[(size_t)i * n + d];  // first[2], n_paths[2]
   uint64_t h = 0xcbf29ce484222325ULL;
+#pragma unroll
   for (int k = 0; k < 2; ++k) {
-    h = dg_fnv(h, 0x1000u + r.n_paths[k]);
-    uint32_t at = r.first[k];
-    for (uint32_t q = 0; q < r.n_paths[k]; ++q) {
+    const uint32_t np = k ? r.w : r.z;
+    h = dg_fnv(h, 0x1000u + np);
+    uint32_t at = k ? r.y : r.x;
+    for (uint32_t q = 0; q < np; ++q) {
       const uint32_t len = pool[at];
       h = dg_fnv(h, 0x2000u + len);
       for (uint32_t x = 0; x < len; ++x) h = dg_fnv(h, link_hash[pool[at + 2 + x]]);
@@ -757,6 +821,7 @@ struct spf_ksp2_plan {
   uint32_t n_src = 0, lw = 0;
   uint32_t delta = 0;  // bucket width of the k = 2 SPF (KspArgs::delta)
   uint32_t chunk = kKspChunk;  // sources per workgroup
+  uint32_t grab = kPoolGrab;   // pool words per wave reservation
   uint64_t epoch = 0;  // graph state the plan was derived from
   std::vector<uint32_t> srcs;
   DevBuf<uint32_t> d_srcs, d_D, d_H, d_all, d_wt_rev;
@@ -811,6 +876,7 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     p->delta = c->E ? (uint32_t)std::max<uint64_t>(1, sum / c->E) : 1;
     if (const char* env = std::getenv("SPF_KSP2_DELTA")) p->delta = (uint32_t)std::strtoul(env, nullptr, 10);
     if (const char* env = std::getenv("SPF_KSP2_CHUNK")) p->chunk = std::max(1ul, std::strtoul(env, nullptr, 10));
+    if (const char* env = std::getenv("SPF_KSP2_GRAB")) p->grab = std::max(64ul, std::strtoul(env, nullptr, 10));
   }
   // graph staged in LDS when its 16-bit copy fits beside >= 2 waves and
   // every up link is one {e, rev(e)} pair (LGraph's bitmap index)
@@ -823,7 +889,9 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
       else if (e <= r && seen[c->link[e]]++) pairs_are_links = false;  // one pair per link
     }
   }
-  if (pairs_are_links && c->max_metric < 65536 && !std::getenv("SPF_KSP2_HBM")) {
+  uint32_t max_deg = 0;  // the staged node word holds degrees < 32768
+  for (uint32_t v = 0; v < c->N; ++v) max_deg = std::max(max_deg, c->row_ptr[v + 1] - c->row_ptr[v]);
+  if (pairs_are_links && c->max_metric < 65536 && max_deg < 32768 && !std::getenv("SPF_KSP2_HBM")) {
     const uint32_t lw_pairs = c->E / 32 + 1;
     auto fit = [&](bool compact) -> uint32_t {
       for (uint32_t w = kKspLdsMaxThreads / 64; w >= 2; --w)
@@ -852,6 +920,10 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     }
   }
   if (!p->lds_waves) p->lds = ksp2_lds_bytes(c->N, c->pitch, p->lw);
+  // ~16 pairs per wave and workgroup: the per-workgroup staging and the
+  // waves' uneven ends amortised (64 -> 256 sources at 16 waves: 89 -> 84 ms)
+  if (!std::getenv("SPF_KSP2_CHUNK"))
+    p->chunk = std::max<uint32_t>(kKspChunk, 16 * (p->lds_waves ? p->lds_waves : kKspWaves));
   if (p->lds > kMaxLdsKsp) return go_exact();  // the per-wave rows do not fit the LDS
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipFuncSetAttribute((const void*)ksp2_kernel,
@@ -881,8 +953,8 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
     HIP_TRY(c, p->d_H.alloc((size_t)c->N * c->pitch));
   }
   if (std::getenv("SPF_KSP2_PROF")) {
-    HIP_TRY(c, p->d_prof.alloc(8));
-    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 64, c->stream));
+    HIP_TRY(c, p->d_prof.alloc(16 * kProfSlots));
+    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 128 * kProfSlots, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   p->epoch = c->epoch;
@@ -942,7 +1014,7 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
   const uint32_t chunks = (p->n_src + p->chunk - 1) / p->chunk;
   KspArgs a{p->d_D.p, p->d_H.p, p->d_srcs.p, p->n_src, c->pitch, p->lw, chunks, p->chunk, p->delta, d_pairs,
             d_pool, pool_words, reinterpret_cast<unsigned long long*>(d_counters), p->d_prof.p,
-            p->d_redo.p, (uint64_t)p->d_redo.n, p->lw_links};
+            p->d_redo.p, (uint64_t)p->d_redo.n, p->lw_links, p->grab};
   if (p->compact)
     hipLaunchKernelGGL(ksp2_lds_kernel<uint16_t>, dim3(c->N * chunks), dim3(64 * p->lds_waves),
                        p->lds, s, g, a);
@@ -964,11 +1036,18 @@ spf_status spf_ksp2_execute(spf_ksp2_plan* p, spf_ksp2_pair* d_pairs, uint32_t* 
 
 static spf_status ksp2_debug_phases(spf_ksp2_plan* p) {
   if (!p || !p->d_prof.p) return SPF_OK;
-  unsigned long long h[8];
-  HIP_TRY(p->ctx, hipMemcpy(h, p->d_prof.p, sizeof h, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> all(16 * kProfSlots);
+  HIP_TRY(p->ctx, hipMemcpy(all.data(), p->d_prof.p, 8 * all.size(), hipMemcpyDeviceToHost));
+  unsigned long long h[16] = {};
+  for (size_t j = 0; j < all.size(); ++j) h[j % 16] += all[j];
   std::fprintf(stderr, "ksp2 phases (clock sums over waves): k1 trace %llu, k2 spf %llu, "
                "k2 trace %llu, pairs %llu; k2 spf sweeps %llu, bucket raises %llu, "
-               "queued nodes %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+               "queued nodes %llu; trace steps k1 %llu k2 %llu; emit clocks %llu (reserving %llu)\n", h[0], h[1],
+               h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10]);
+  const double n = h[3] ? (double)h[3] : 1.0;
+  std::fprintf(stderr, "ksp2 per pair: k1 trace %.0f clk (%.1f steps), k2 spf %.0f clk (%.1f sweeps, "
+               "%.1f queued), k2 trace %.0f clk (%.1f steps), emit %.0f clk\n", h[0] / n, h[7] / n,
+               h[1] / n, h[4] / n, h[6] / n, h[2] / n, h[8] / n, h[9] / n);
   return SPF_OK;
 }
 
@@ -1033,14 +1112,41 @@ spf_status spf_ksp2_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   }
   if (cnt[2] & 1) return fail(c, SPF_E_NOMEM, "KSP2 path pool overflow");
   c->solves += cnt[1];
-  *pool_used = cnt[0];
-  HIP_TRY(c, hipMemcpy(pairs_out, d_pairs.p, n_pairs * sizeof(spf_ksp2_pair),
-                       hipMemcpyDeviceToHost));
-  if (!pool_out) return SPF_OK;
-  if (pool_cap < cnt[0])
+  // The device pool holds the waves' reservations in completion order, with
+  // slack at each one's end: repack the records per pair (pair order, k = 1
+  // then k = 2, list order) so the layout -- and *pool_used -- is the same on
+  // every call (the sizing call's answer fits the second call exactly).
+  std::vector<spf_ksp2_pair> hp(n_pairs);
+  std::vector<uint32_t> pool_h(cnt[0]);
+  HIP_TRY(c, hipMemcpy(hp.data(), d_pairs.p, n_pairs * sizeof(spf_ksp2_pair), hipMemcpyDeviceToHost));
+  if (cnt[0]) HIP_TRY(c, hipMemcpy(pool_h.data(), d_pool.p, cnt[0] * 4, hipMemcpyDeviceToHost));
+  uint64_t dense = 0;
+  for (const spf_ksp2_pair& r : hp)
+    for (int k = 0; k < 2; ++k)
+      for (uint32_t q = 0, at = r.first[k]; q < r.n_paths[k]; ++q, at = pool_h[at + 1]) dense += pool_h[at] + 2ull;
+  if (dense > 0xFFFFFFF0ull) return fail(c, SPF_E_NOMEM, "KSP2 paths exceed 32-bit pool offsets");
+  *pool_used = dense;
+  const bool write = pool_out && pool_cap >= dense;
+  uint64_t cur = 0;
+  for (spf_ksp2_pair& r : hp)
+    for (int k = 0; k < 2; ++k) {
+      uint32_t at = r.first[k];
+      r.first[k] = r.n_paths[k] ? (uint32_t)cur : kInf;
+      for (uint32_t q = 0; q < r.n_paths[k]; ++q) {
+        const uint32_t len = pool_h[at];
+        if (write) {
+          pool_out[cur] = len;
+          pool_out[cur + 1] = q + 1 < r.n_paths[k] ? (uint32_t)(cur + len + 2) : kInf;
+          std::memcpy(pool_out + cur + 2, pool_h.data() + at + 2, 4ull * len);
+        }
+        cur += len + 2ull;
+        at = pool_h[at + 1];
+      }
+    }
+  std::memcpy(pairs_out, hp.data(), n_pairs * sizeof(spf_ksp2_pair));
+  if (pool_out && !write)
     return fail(c, SPF_E_NOMEM, "pool_out holds %llu words, %llu needed",
-                (unsigned long long)pool_cap, (unsigned long long)cnt[0]);
-  if (cnt[0]) HIP_TRY(c, hipMemcpy(pool_out, d_pool.p, cnt[0] * 4, hipMemcpyDeviceToHost));
+                (unsigned long long)pool_cap, (unsigned long long)dense);
   return SPF_OK;
 }
 

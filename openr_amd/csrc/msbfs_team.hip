@@ -112,7 +112,8 @@ __device__ __forceinline__ uint32_t team_arrive(uint32_t* word, uint32_t G, uint
       if ((w & 0xFFu) >= G) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (k == kTmSpin) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // 2 = a team barrier: spf_device_check turns team plans off on the context
+    if (k == kTmSpin) __hip_atomic_fetch_or(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     *bcast = w;
   }
   __syncthreads();
@@ -140,6 +141,9 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
   uint32_t* any_l = src_l + kTmBatch;  // [0]: this member's level flags, [1]: broadcast word
 
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // test hook (SPF_TEAM_FLUSH_DBG bit 32): report a team-barrier timeout
+  if ((a.dbg & 32u) && blockIdx.x == 0 && tid == 0)
+    __hip_atomic_fetch_or(a.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // block -> (XCD, team on it, member): blocks are dealt to the XCDs round
   // robin, so blockIdx % 8 is the XCD; members of a team share its L2
   const uint32_t xcd = blockIdx.x & 7u, j = blockIdx.x >> 3;

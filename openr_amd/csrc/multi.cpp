@@ -174,6 +174,7 @@ struct spf_mplan {
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     uint64_t g_epoch = ~0ull;  // graph epoch the captured executes belong to
+    bool g_team_off = false;   // ... and the context's team switch
     std::vector<hipEvent_t> ev;  // timing: [2 * cap] start / end per execute
   };
   std::unique_ptr<Part[]> parts;  // [n_parts]
@@ -238,7 +239,8 @@ spf_status run_part(spf_mplan* mp, uint32_t i) {
     ev = &p.ev[2 * (mp->timing_n % mp->timing_cap)];
     M_HIP(m, hipEventRecord(ev[0], s));
   }
-  if (p.gexec && p.g_epoch == spf_graph_epoch(c)) {
+  // (a capture made before a team timeout turned teams off is stale too)
+  if (p.gexec && p.g_epoch == spf_graph_epoch(c) && p.g_team_off == c->team_off) {
     M_HIP(m, hipGraphLaunch(p.gexec, s));
   } else {
     if (p.gexec) {
@@ -262,6 +264,7 @@ spf_status run_part(spf_mplan* mp, uint32_t i) {
       M_HIP(m, hipGraphInstantiate(&p.gexec, g, nullptr, nullptr, 0));
       p.graph = g;
       p.g_epoch = spf_graph_epoch(c);
+      p.g_team_off = c->team_off;
     }
   }
   if (ev) M_HIP(m, hipEventRecord(ev[1], s));

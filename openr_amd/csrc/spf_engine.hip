@@ -2214,7 +2214,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   // few batches (a rank's share of a multi-GPU pass): teams of workgroups
   // per batch (msbfs_team.hip) instead of one workgroup sweeping everything
   p->tm_G = 0;
-  if (p->ms && !use_planes(c) && !p->expand) {
+  if (p->ms && !use_planes(c) && !p->expand && !c->team_off) {
     const uint32_t G = msbfs_team_size(c, (uint32_t)p->closure.size());
     if (G) {
       const spf_status st = msbfs_team_prepare(c, p, G);
@@ -2968,7 +2968,9 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     return fail(c, SPF_E_INVALID, "spf_plan_execute: NULL output buffer");
   if (p->shape != c->shape)
     return fail(c, SPF_E_STATE, "graph reloaded since the plan was created: recreate it");
-  if (p->epoch != c->epoch) {  // patched in place: re-derive, same output layout
+  if (p->epoch != c->epoch || (p->tm_G && c->team_off)) {
+    // patched in place, or teams turned off by a timeout: re-derive, same
+    // output layout
     const spf_status st = build_plan(c, p);
     if (st != SPF_OK) return st;
   }

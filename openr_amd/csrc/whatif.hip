@@ -1885,8 +1885,18 @@ spf_status spf_device_check(spf_ctx* c) {
   HIP_TRY(c, hipMemcpy(&flag, c->d_fault.p, sizeof flag, hipMemcpyDeviceToHost));
   if (!flag) return SPF_OK;
   HIP_TRY(c, hipMemset(c->d_fault.p, 0, sizeof flag));
+  if (flag & 2u) {
+    // a team BFS gave up waiting for its members (another process's grid
+    // held CUs): this context's plans stop using teams -- each re-derives
+    // onto msbfs_kernel at its next execute -- instead of polling again
+    c->team_off = true;
+    return fail(c, SPF_E_HIP,
+                "a team BFS barrier timed out on device %d (workgroups not co-resident): the "
+                "results of this context's launches since the last check are invalid; its plans "
+                "run msbfs_kernel from their next execute", c->device);
+  }
   return fail(c, SPF_E_HIP,
-              "a grid / team barrier timed out on device %d (blocks not co-resident?): the "
+              "a grid barrier timed out on device %d (blocks not co-resident?): the "
               "results of this context's launches since the last check are invalid", c->device);
 }
 

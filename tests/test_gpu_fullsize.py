@@ -168,10 +168,11 @@ def test_ksp2_wan2k_every_source_engine_digest_matches_oracle():
         used = int(cnt.numpy()[0])
         if used > words:  # size the pool and run again
             pool.free()
-            words = used + 1024
+            words = used + used // 4 + (1 << 20)  # grab slack varies run to run
             pool = DeviceArray(words, np.uint32)
             p.execute(pairs.ptr, pool.ptr, words, cnt.ptr)
             eng.check()
+            used = int(cnt.numpy()[0])
         assert not (int(cnt.numpy()[2]) & 1)
         d_lh = DeviceArray(len(lh), np.uint64)
         d_lh.upload(lh)

@@ -88,3 +88,31 @@ def test_sliced_next_hops_grouped_and_per_source(group, monkeypatch):
         names, eng, orc = load(topo)
         assert eng.plan([0]).row_mode() in ("sliced", "sliced_bfs")
         compare(names, eng, orc, list(range(len(names))))
+
+
+def test_team_timeout_turns_teams_off_and_the_plan_reruns_on_msbfs_kernel(monkeypatch):
+    """A team barrier that times out (another process's grid holding CUs;
+    here the kernel's test hook SPF_TEAM_FLUSH_DBG=32 reports one) fails the
+    check loudly, and the same plan's next execute re-derives onto
+    msbfs_kernel -- no second poll until timeout -- with oracle-exact rows."""
+    from openr_amd._native import SpfError
+
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "8")
+    monkeypatch.setenv("SPF_MSBFS", "masks")
+    names, eng, orc = load(T.fabric(1000, full=True))
+    srcs = list(range(0, len(names), 3))
+    p = eng.plan(srcs)
+    assert p.kernels()[0] == "msbfs_team_kernel"
+    monkeypatch.setenv("SPF_TEAM_FLUSH_DBG", "32")
+    with pytest.raises(SpfError, match="team BFS barrier timed out"):
+        p.execute_host()
+    monkeypatch.delenv("SPF_TEAM_FLUSH_DBG")
+    res = p.execute_host()
+    assert p.kernels()[0] == "msbfs_kernel"
+    dist, mats = orc.dense(names, srcs, ulm=True)
+    exp = np.where(dist == np.iinfo(np.uint64).max, 0xFFFFFFFF, dist).astype(np.uint32)
+    assert np.array_equal(res.dist, exp)
+    for i, s in enumerate(srcs):
+        k = len(eng.neighbors(s))
+        assert np.array_equal(res.nh_matrix(i), mats[i][:k])
+    assert eng.plan(srcs).kernels()[0] == "msbfs_kernel"  # new plans too
