@@ -279,6 +279,7 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
                           bool* ovf, uint32_t* steps) {
   const uint32_t lane = __lane_id();
   uint32_t k = 0, v = dst, dv = dget(D, dst);
+  NodeInfo nv = g.node(dst);
   for (;;) {
     ++*steps;
     if (v == src) {
@@ -287,7 +288,7 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
     }
     uint64_t best = ~0ull;
     uint32_t tail = 0, tl = 0;  // this lane's best candidate: tail node, link index
-    const NodeInfo nv = g.node(v);
+    uint32_t tb = 0, te = 0;    // ... and its in-edge range (the next step's, if it wins)
     const uint32_t e_beg = nv.beg, e_end = nv.end;
     for (uint32_t e = e_beg + lane; e < e_end; e += 64) {
       // in-edge u -> v is the reverse of the out-edge v -> u; every test's
@@ -295,7 +296,8 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       const uint32_t u = g.col(e);
       const uint32_t r = g.rev(e);
       const uint32_t l = g.link_of(e, r);
-      const bool drained = g.ovl(u) && u != src;
+      const NodeInfo nu = g.node(u);
+      const bool drained = nu.ovl && u != src;
       const bool tried = bit(vis, l) || (ign && bit(ign, g.ign_at(e)));
       const uint32_t du = dget(D, u);
       const uint32_t wr = g.w(r);
@@ -305,6 +307,8 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
           best = key;
           tail = u;
           tl = l;
+          tb = nu.beg;
+          te = nu.end;
         }
       }
     }
@@ -315,16 +319,20 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       --k;
       v = k == 0 ? dst : g.col(g.rev(stack[k - 1]));
       dv = dget(D, v);
+      nv = g.node(v);
       continue;
     }
     const uint32_t r = (uint32_t)best;
     uint32_t l, u;
-    if (arg < 64) {  // the winning lane's tail and link
+    if (arg < 64) {  // the winning lane's tail, link and the tail's in-edges
       u = __builtin_amdgcn_readlane(tail, arg);
       l = __builtin_amdgcn_readlane(tl, arg);
+      nv.beg = __builtin_amdgcn_readlane(tb, arg);
+      nv.end = __builtin_amdgcn_readlane(te, arg);
     } else {
       u = g.col(g.rev(r));
       l = g.link(r);
+      nv = g.node(u);
     }
     if (k >= cap) {
       *ovf = true;
@@ -432,17 +440,33 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
         continue;
       }
       expanded = true;
-      for (uint32_t e = nu.beg + slot; e < nu.end; e += 1u << lg) {
-        const uint32_t v = g.col(e);
-        const uint32_t nd = du + g.w(e);
-        const bool ignored = bit(ign, g.ign_at(e));
-        const uint32_t hv = hget(H, v);
-        if (ignored || hv == kInf || (uint64_t)nd + hv > bound) continue;
+      auto relax = [&](uint32_t v, uint32_t nd, bool ignored, uint32_t hv) {
+        if (ignored || hv == kInf || (uint64_t)nd + hv > bound) return;
         if (sizeof(DT) == 2 && nd >= 0xFFFFu) {
           sat = true;
-          continue;
+          return;
         }
         if (dmin(D, v, nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
+      };
+      // two edges per lane and step, the second's loads under its own mask:
+      // head, metric, ignored bit and heuristic of both in one LDS round each
+      const uint32_t st = 1u << lg;
+      for (uint32_t e = nu.beg + slot; e < nu.end; e += 2u * st) {
+        const uint32_t e1 = e + st;
+        const bool two = e1 < nu.end;
+        const uint32_t v0 = g.col(e), nd0 = du + g.w(e);
+        const bool ig0 = bit(ign, g.ign_at(e));
+        uint32_t v1 = 0, nd1 = 0;
+        bool ig1 = true;
+        if (two) {
+          v1 = g.col(e1);
+          nd1 = du + g.w(e1);
+          ig1 = bit(ign, g.ign_at(e1));
+        }
+        const uint32_t hv0 = hget(H, v0);
+        const uint32_t hv1 = two ? hget(H, v1) : kInf;
+        relax(v0, nd0, ig0, hv0);
+        if (two) relax(v1, nd1, ig1, hv1);
       }
     }
     if (!__ballot(expanded)) {  // everything pending seen lies past T: after a
