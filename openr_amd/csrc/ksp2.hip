@@ -47,7 +47,11 @@ constexpr uint32_t kPoolGrab = 256;         // words a wave reserves at a time (
 constexpr size_t kMaxLdsKsp = 160 * 1024;
 constexpr uint32_t kCompactCap = 512;       // u16-label waves: DFS stack / SPF queue entries
 constexpr uint32_t kRedoBlocks = 256;       // workgroups of the u32 redo pass
-constexpr uint32_t kProfSlots = 1024;       // SPF_KSP2_PROF: 16-counter slots (by block)
+constexpr uint32_t kProfSlots = 1024;
+#ifndef KSP2_EDGES
+#define KSP2_EDGES 2
+#endif
+constexpr uint32_t kKspEdges = KSP2_EDGES;  // edges per lane per relaxation step       // SPF_KSP2_PROF: 16-counter slots (by block)
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -448,25 +452,31 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
         }
         if (dmin(D, v, nd)) atomicOr(&bm[v >> 5], 1u << (v & 31));
       };
-      // two edges per lane and step, the second's loads under its own mask:
-      // head, metric, ignored bit and heuristic of both in one LDS round each
+      // kKspEdges edges per lane and step, each one's loads under its own
+      // mask: head, metric, ignored bit and heuristic of all of them in one
+      // LDS round each (one edge per step: 117k -> 98k clocks per SPF at two;
+      // four: wan_ksp2 76 -> 83 ms, the extra masks and registers)
       const uint32_t st = 1u << lg;
-      for (uint32_t e = nu.beg + slot; e < nu.end; e += 2u * st) {
-        const uint32_t e1 = e + st;
-        const bool two = e1 < nu.end;
-        const uint32_t v0 = g.col(e), nd0 = du + g.w(e);
-        const bool ig0 = bit(ign, g.ign_at(e));
-        uint32_t v1 = 0, nd1 = 0;
-        bool ig1 = true;
-        if (two) {
-          v1 = g.col(e1);
-          nd1 = du + g.w(e1);
-          ig1 = bit(ign, g.ign_at(e1));
+      for (uint32_t e = nu.beg + slot; e < nu.end; e += kKspEdges * st) {
+        uint32_t v[kKspEdges], nd[kKspEdges], hv[kKspEdges];
+        bool ig[kKspEdges];
+#pragma unroll
+        for (uint32_t k = 0; k < kKspEdges; ++k) {
+          const uint32_t ek = e + k * st;
+          v[k] = 0;
+          nd[k] = 0;
+          ig[k] = true;
+          if (k == 0 || ek < nu.end) {
+            v[k] = g.col(ek);
+            nd[k] = du + g.w(ek);
+            ig[k] = bit(ign, g.ign_at(ek));
+          }
         }
-        const uint32_t hv0 = hget(H, v0);
-        const uint32_t hv1 = two ? hget(H, v1) : kInf;
-        relax(v0, nd0, ig0, hv0);
-        if (two) relax(v1, nd1, ig1, hv1);
+#pragma unroll
+        for (uint32_t k = 0; k < kKspEdges; ++k) hv[k] = (k == 0 || e + k * st < nu.end) ? hget(H, v[k]) : kInf;
+#pragma unroll
+        for (uint32_t k = 0; k < kKspEdges; ++k)
+          if (k == 0 || e + k * st < nu.end) relax(v[k], nd[k], ig[k], hv[k]);
       }
     }
     if (!__ballot(expanded)) {  // everything pending seen lies past T: after a
