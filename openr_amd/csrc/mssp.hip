@@ -194,52 +194,20 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     // (spine -> fabric -> rack switch), a backward one the opposite turns
     const bool back = alt && (it & 1u);
     auto slot_at = [&](uint32_t k) { return back ? n_my - 1u - k : k; };
-    // slices whose in-neighbours changed since their last sweep (every
-    // slice in the first sweep).  The next live slice is chosen when the
-    // current one starts -- a stale answer only defers a slice to the next
-    // sweep, which then happens (a change was made) -- so its first column
-    // group can be loaded while the current slice runs
-    auto live = [&](uint32_t s_) -> bool {
-      return !(dep && it > 0) ||
-             ((__builtin_amdgcn_readfirstlane(scur[s_ >> 5] | snxt[s_ >> 5]) >> (s_ & 31)) & 1u);
-    };
-    uint32_t kk = 0, sl = kMpNoSlice;
-    for (; kk < n_my; ++kk) {
-      sl = wmap[slot_at(kk)];
-      if (live(sl)) break;
-    }
-    uint32_t b = 0, w = 0;
-    if (kk < n_my) {
-      b = sell_ptr[sl];
-      w = (sell_ptr[sl + 1] - b) / 64;
-    }
-    const uint32_t* ep = ell + b + lane;
-    uint32_t ea[kMpAhead], eb[kMpAhead];
-    auto load = [&](const uint32_t* p, uint32_t j0, uint32_t (&e)[kMpAhead]) {
-#pragma unroll
-      for (int t = 0; t < (int)kMpAhead; ++t) {
-        // unconditional (the ELL is padded past its last slice): a
-        // branch per column made the compiler drain every load in flight
-        // (vmcnt(0)) before each group's folds
-        // (columns past the slice's w read the next slice's entries --
-        // valid node ids -- and fold() never uses them: t < n)
-        e[t] = p[(j0 + t) * 64];
-      }
-    };
-    load(ep, 0, ea);
-    while (kk < n_my) {
+    uint32_t nsl = n_my ? wmap[slot_at(0)] : kMpNoSlice;
+    uint32_t nb0 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl], nb1 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl + 1];
+    for (uint32_t kk = 0; kk < n_my; ++kk) {
       const uint32_t k = slot_at(kk);
-      uint32_t kn = kk + 1, nsl = kMpNoSlice;
-      for (; kn < n_my; ++kn) {
-        nsl = wmap[slot_at(kn)];
-        if (live(nsl)) break;
+      const uint32_t sl = nsl;
+      const uint32_t b = nb0, w = (nb1 - nb0) / 64;
+      nsl = kk + 1 < n_my ? wmap[slot_at(kk + 1)] : kMpNoSlice;
+      if (nsl != kMpNoSlice) {
+        nb0 = sell_ptr[nsl];
+        nb1 = sell_ptr[nsl + 1];
       }
-      uint32_t nb = b, nw = 0;  // no next slice: the last load re-reads this one's
-      if (kn < n_my) {
-        nb = sell_ptr[nsl];
-        nw = (sell_ptr[nsl + 1] - nb) / 64;
-      }
-      const uint32_t* ep_next = ell + nb + lane;
+      if (dep && it > 0 &&
+          !(__builtin_amdgcn_readfirstlane(scur[sl >> 5] | snxt[sl >> 5]) >> (sl & 31) & 1u))
+        continue;  // no in-neighbour changed since this slice's last sweep
       if (stats && lane == 0) atomicAdd(&stats[3], 1ull);  // slices swept (diagnostics)
       const uint32_t v = sl * 64 + lane;
       // u16x2 accumulators: SD of them (u16 labels), 2 SD (u8 labels: the
@@ -249,6 +217,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 #pragma unroll
       for (int q = 0; q < NA; ++q) acc[q] = 0xFFFFFFFFu;
       bool got = false;
+      const uint32_t* ep = ell + b + lane;
       // the slice's packed in-edges kMpAhead columns at a time, the next
       // group's loads in flight while this group's labels are folded (one
       // entry in flight made every column an L2 round trip)
@@ -288,17 +257,27 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
             got = true;
           }
       };
-      // groups of kMpAhead columns, two in flight; the last load of the
-      // slice is the next live slice's first group (its columns while this
-      // slice's last folds and its update run)
-      uint32_t j0 = 0;
-      do {
-        load(ep, j0 + kMpAhead, eb);
+      uint32_t ea[kMpAhead], eb[kMpAhead];
+      auto load = [&](uint32_t j0, uint32_t (&e)[kMpAhead]) {
+#pragma unroll
+        for (int t = 0; t < (int)kMpAhead; ++t) {
+          // unconditional (the ELL is padded past its last slice): a
+          // branch per column made the compiler drain every load in flight
+          // (vmcnt(0)) before each group's folds
+          // (columns past the slice's w read the next slice's entries --
+          // valid node ids -- and fold() never uses them: t < n)
+          e[t] = ep[(j0 + t) * 64];
+        }
+      };
+      // every group load unconditional (the ELL is padded): a load under a
+      // branch makes the join's wait count drain the loads in flight
+      load(0, ea);
+      for (uint32_t j0 = 0; j0 < w; j0 += 2 * kMpAhead) {
+        load(j0 + kMpAhead, eb);
         fold(ea, w - j0);
-        load(j0 + 2 * kMpAhead < w ? ep : ep_next, j0 + 2 * kMpAhead < w ? j0 + 2 * kMpAhead : 0, ea);
+        load(j0 + 2 * kMpAhead, ea);
         if (j0 + kMpAhead < w) fold(eb, w - j0 - kMpAhead);
-        j0 += 2 * kMpAhead;
-      } while (j0 < w);
+      }
       bool expands = false;
       if (got && v < N) {
         uint32_t* dv = &dist[v * SD];
@@ -335,11 +314,6 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
           atomicOr(&snxt[o >> 5], 1u << (o & 31));
         }
       }
-      kk = kn;
-      sl = nsl;
-      b = nb;
-      w = nw;
-      ep = ep_next;
     }
     if (__builtin_amdgcn_ballot_w64(changed) && lane == 0) flag[it % 3] = 1;
     __syncthreads();
