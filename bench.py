@@ -1071,11 +1071,16 @@ def main() -> None:
     from openr_amd.engine import SpfEngine, graph_from_lsdb
 
     cls = WORKLOADS[args.workload]
+    if rank == 0:  # progress on stderr: building a 250k-node graph takes a while
+        print(f"bench: building {args.workload} (world {world})", file=sys.stderr, flush=True)
     if cls is AllSources:
         wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb, scaling=args.scaling,
                  results=args.results)
     else:
         wl = cls(args.workload, rank, world, dev, SpfEngine, graph_from_lsdb)
+    if rank == 0:
+        print(f"bench: {args.workload} built; {args.warmup} warmup + {args.steps} timed steps",
+              file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         wl.step()
     getattr(wl, "finish", lambda: None)()
