@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 
 using namespace spfi;
 
@@ -79,6 +80,18 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
          __builtin_amdgcn_readlane((uint32_t)x, 63);
 }
 
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(~0u, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ uint64_t wave_min(uint64_t x) { return wave_min64(x); }
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) { return wave_min32(x); }
+
 // Exclusive prefix sum over the wave with DPP moves (no LDS round trips):
 // row_shr 1/2/4/8 inside each 16-lane row (lanes shifted in from outside the
 // row read 0), then row_bcast15 / row_bcast31 carry row totals upwards.
@@ -97,7 +110,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x, uint32_t* total
 // Minimum of the keys held by lanes 0 .. n-1 (n <= 64, wave-uniform): a
 // handful of lane reads into scalar registers for small n (*arg = the lane
 // holding it), the shuffle reduction otherwise (*arg = 64: unknown).
-__device__ __forceinline__ uint64_t lanes_min64(uint64_t x, uint32_t n, uint32_t* arg) {
+__device__ __forceinline__ uint64_t lanes_min(uint64_t x, uint32_t n, uint32_t* arg) {
   n = __builtin_amdgcn_readfirstlane(n);
   *arg = 64;
   if (n > 8) return wave_min64(x);
@@ -106,6 +119,22 @@ __device__ __forceinline__ uint64_t lanes_min64(uint64_t x, uint32_t n, uint32_t
   for (uint32_t j = 0; j < n; ++j) {
     const uint64_t y = ((uint64_t)__builtin_amdgcn_readlane(hi, j) << 32) |
                        __builtin_amdgcn_readlane(lo, j);
+    if (y < m) {
+      m = y;
+      *arg = j;
+    }
+  }
+  return m;
+}
+// 32-bit keys (compact waves: label and edge id both below 2^16): one lane
+// read per candidate
+__device__ __forceinline__ uint32_t lanes_min(uint32_t x, uint32_t n, uint32_t* arg) {
+  n = __builtin_amdgcn_readfirstlane(n);
+  *arg = 64;
+  if (n > 8) return wave_min32(x);
+  uint32_t m = ~0u;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t y = __builtin_amdgcn_readlane(x, j);
     if (y < m) {
       m = y;
       *arg = j;
@@ -282,6 +311,10 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
                           ST* stack, uint32_t cap, uint32_t src, uint32_t dst, uint32_t* depth,
                           bool* ovf, uint32_t* steps) {
   const uint32_t lane = __lane_id();
+  // candidate key (D[tail], edge id): 32 bits in compact waves (both < 2^16)
+  using K = typename std::conditional<sizeof(DT) == 2, uint32_t, uint64_t>::type;
+  constexpr uint32_t KS = sizeof(K) * 4;  // edge-id bits of a key
+  constexpr K KNONE = ~K(0);
   uint32_t k = 0, v = dst, dv = dget(D, dst);
   NodeInfo nv = g.node(dst);
   for (;;) {
@@ -290,7 +323,7 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       *depth = k;
       return true;
     }
-    uint64_t best = ~0ull;
+    K best = KNONE;
     uint32_t tail = 0, tl = 0;  // this lane's best candidate: tail node, link index
     uint32_t tb = 0, te = 0;    // ... and its in-edge range (the next step's, if it wins)
     const uint32_t e_beg = nv.beg, e_end = nv.end;
@@ -306,7 +339,7 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       const uint32_t du = dget(D, u);
       const uint32_t wr = g.w(r);
       if (!drained && !tried && du != kInf && du + wr == dv) {
-        const uint64_t key = ((uint64_t)du << 32) | r;
+        const K key = ((K)du << KS) | r;
         if (key < best) {
           best = key;
           tail = u;
@@ -317,8 +350,8 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       }
     }
     uint32_t arg;
-    best = lanes_min64(best, min(e_end - e_beg, 64u), &arg);
-    if (best == ~0ull) {  // every pathLink of v tried: back up one level
+    best = lanes_min(best, min(e_end - e_beg, 64u), &arg);
+    if (best == KNONE) {  // every pathLink of v tried: back up one level
       if (k == 0) return false;
       --k;
       v = k == 0 ? dst : g.col(g.rev(stack[k - 1]));
@@ -326,7 +359,7 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
       nv = g.node(v);
       continue;
     }
-    const uint32_t r = (uint32_t)best;
+    const uint32_t r = (uint32_t)(best & ((K(1) << KS) - 1));
     uint32_t l, u;
     if (arg < 64) {  // the winning lane's tail, link and the tail's in-edges
       u = __builtin_amdgcn_readlane(tail, arg);
@@ -348,8 +381,8 @@ __device__ bool trace_one(const G& g, const DT* D, const uint32_t* ign, uint32_t
     }
     wave_sync();
     ++k;
-    v = u;  // tail of r, D[u] = the key's high word
-    dv = (uint32_t)(best >> 32);
+    v = u;  // tail of r, D[u] = the key's high part
+    dv = (uint32_t)(best >> KS);
   }
 }
 
@@ -415,9 +448,14 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
   uint32_t qlen = 1;
   uint32_t span = bm_words, cur = 0;  // the chunk's bitmap words; next chunk's first word
   uint32_t idle = 0;                  // bitmap words worked since the last expansion
-  uint64_t idle_f = ~0ull;            // smallest f deferred since then
-  uint64_t width = delta;
-  uint64_t T = (uint64_t)hget(H, src) + width;  // expand pending nodes with f <= T
+  // f = D + H in 32 bits in compact waves (labels and heuristic < 2^16; the
+  // width stops doubling at 2^24, past every finite f), else in 64
+  using F = typename std::conditional<sizeof(DT) == 2, uint32_t, uint64_t>::type;
+  constexpr F FNONE = ~F(0);
+  constexpr F WMAX = sizeof(DT) == 2 ? F(1u << 24) : F(0xFFFFFFFFull);
+  F idle_f = FNONE;  // smallest f deferred since then
+  F width = delta;
+  F T = (F)hget(H, src) + width;  // expand pending nodes with f <= T
   bool sat = false;
   uint32_t sweeps = 0, raises = 0, pending = 0;  // SPF_KSP2_PROF counters
   while (qlen) {
@@ -427,7 +465,7 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
     // edge: the dependent chain per lane is one or two edges, not deg(u)
     const uint32_t lg = qlen <= 16 ? 2u : (qlen <= 32 ? 1u : 0u);
     const uint32_t slot = lane & ((1u << lg) - 1u);
-    uint64_t defer_f = ~0ull;  // smallest f left pending by this lane
+    F defer_f = FNONE;  // smallest f left pending by this lane
     bool expanded = false;
     for (uint32_t i = lane >> lg; i < qlen; i += 64u >> lg) {
       const uint32_t u = q[i];
@@ -436,8 +474,10 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
       const uint32_t du = dget(D, u);
       // dst's label now (read per node: a sweep-start copy expanded 6 % more)
       const uint32_t bound = dget(D, dst);
-      const uint64_t f = (uint64_t)du + hget(H, u);
-      if (drained || f > bound || u == dst) continue;
+      const uint32_t hu = hget(H, u);
+      if (drained || hu == kInf || u == dst) continue;  // (hu unreachable: f past every bound)
+      const F f = (F)du + hu;
+      if (f > bound) continue;
       if (f > T) {  // a later bucket: stays pending
         if (slot == 0) atomicOr(&bm[u >> 5], 1u << (u & 31));
         defer_f = min(defer_f, f);
@@ -481,19 +521,19 @@ __device__ bool wave_sssp(const G& g, DT* D, uint16_t* q, uint32_t qcap, uint32_
     }
     if (!__ballot(expanded)) {  // everything pending seen lies past T: after a
       idle += span;             // whole round of such chunks the next bucket,
-      idle_f = min(idle_f, wave_min64(defer_f));  // twice as wide (a long
+      idle_f = min(idle_f, wave_min(defer_f));  // twice as wide (a long
       if (idle >= bm_words) {                     // detour or an unreachable
-        if (idle_f != ~0ull) {                    // dst: log2 raises)
+        if (idle_f != FNONE) {                    // dst: log2 raises)
           ++raises;
-          width = min(2ull * width, 0xFFFFFFFFull);
+          width = min((F)(2 * width), WMAX);
           T = idle_f + width;
         }
         idle = 0;
-        idle_f = ~0ull;
+        idle_f = FNONE;
       }
     } else {
       idle = 0;
-      idle_f = ~0ull;
+      idle_f = FNONE;
     }
     wave_sync();
     // next chunk: up to qcap pending nodes, bitmap words from `cur` on
