@@ -943,11 +943,12 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
   };
   if (c->nonpos || c->needs64 || c->N > 65535 || std::getenv("SPF_KSP2_EXACT")) return go_exact();
   p->lw = p->lw_links = c->max_link / 32 + 1;
-  {  // bucket width: the mean up-link metric (env SPF_KSP2_DELTA overrides;
+  {  // bucket width: half the mean up-link metric (env SPF_KSP2_DELTA overrides;
      // 4294967295 = no order, the plain hop-synchronous sweep)
     uint64_t sum = 0;
     for (uint32_t e = 0; e < c->E; ++e) sum += c->wt[e];
-    p->delta = c->E ? (uint32_t)std::max<uint64_t>(1, sum / c->E) : 1;
+    // half the mean (wan_ksp2: 74.0 ms at the mean, 73.0 at 200-300, 74.5 at 600)
+    p->delta = c->E ? (uint32_t)std::max<uint64_t>(1, sum / c->E / 2) : 1;
     if (const char* env = std::getenv("SPF_KSP2_DELTA")) p->delta = (uint32_t)std::strtoul(env, nullptr, 10);
     if (const char* env = std::getenv("SPF_KSP2_CHUNK")) p->chunk = std::max(1ul, std::strtoul(env, nullptr, 10));
     if (const char* env = std::getenv("SPF_KSP2_GRAB")) p->grab = std::max(64ul, std::strtoul(env, nullptr, 10));
