@@ -1365,7 +1365,9 @@ __device__ __forceinline__ void grouped_pass(__amdgpu_buffer_rsrc_t rs, uint32_t
 // persistent waves pulling units through per-XCD atomic counters serialised
 // on the counters (r02_v20: 2.4x slower); sc1 bitmap stores (lines leave L2)
 // changed nothing (r02_v22).
-constexpr uint32_t kSlUnit = 128;  // neighbour-chunk matches per unit (at most, about)
+// neighbour-chunk matches per unit (at most, about): fabric_full's pass 68.5
+// us at 128, 66 at 512, 72 at 1024, 92 at 2048 (gpurun_out/r04_s1, r04_s2)
+constexpr uint32_t kSlUnit = 512;
 
 __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     const uint32_t* __restrict__ S, const uint32_t* __restrict__ maxd,
