@@ -269,7 +269,7 @@ constexpr uint32_t kTeamPlanes = 4;
 spf_status mssp_prepare(spf_ctx* c);
 spf_status mssp_set_lds_limits(spf_ctx* c);
 spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
-                       uint8_t* Dn, uint32_t* redo, hipStream_t s);
+                       uint8_t* Dn, uint32_t* redo, hipStream_t s, uint32_t* maxd = nullptr);
 // Single-source SSSP in global memory, one cooperative grid (any graph
 // size); scratch lives in the context.  dist = [N].
 spf_status launch_gsssp(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign, uint32_t* dist,

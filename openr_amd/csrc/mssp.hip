@@ -117,7 +117,8 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     uint32_t N, uint32_t pitch, uint32_t* __restrict__ D, uint8_t* __restrict__ Dn,
     uint32_t ovf_at, uint32_t* __restrict__ redo, uint32_t alt,
     const uint32_t* __restrict__ dep /* [n_slices + 1] offsets, then out-slice lists; null: no skipping */,
-    unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */) {
+    unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */,
+    uint32_t* __restrict__ maxd /* sliced next-hop plans: largest finite distance (254: saturated) */) {
   constexpr uint32_t S = (U8 ? 4 : 2) * SD;  // sources per workgroup
   constexpr uint32_t LPW = U8 ? 4 : 2;       // labels per word
   constexpr uint32_t LB = U8 ? 8 : 16;       // label bits
@@ -329,6 +330,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
 
   // ---- rows: u32 (kInf = unreached, and past N as sssp_kernel) and the
   // u8 copy next-hop pass; overflow-suspect rows go to `redo` ----
+  uint32_t dmax = 0;  // largest finite distance this thread wrote
   for (uint32_t si = 0; si < nb; ++si) {
     const uint32_t row = r0 + si;
     uint32_t ovf = 0;
@@ -345,6 +347,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
           if (h != LM) {
             d = h;
             ovf |= h >= ovf_at;
+            dmax = max(dmax, h);
           }
         }
         o[t] = d;
@@ -357,7 +360,14 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
       }
       if (Dn) reinterpret_cast<uint32_t*>(Dn + (size_t)row * pitch)[q] = nb8;
     }
-    if (__syncthreads_or(ovf) && tid == 0 && redo) redo[1 + atomicAdd(redo, 1u)] = row;
+    if (__syncthreads_or(ovf) && tid == 0) {
+      if (redo) redo[1 + atomicAdd(redo, 1u)] = row;
+      if (maxd) atomicMax(maxd, 254u);  // a redone row may be deep: the bit planes do not apply
+    }
+  }
+  if (maxd) {  // one atomic per wave
+    for (int o = 32; o >= 1; o >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, o));
+    if ((tid & 63) == 0 && dmax) atomicMax(maxd, dmax);
   }
 }
 
@@ -507,7 +517,7 @@ spf_status mssp_set_lds_limits(spf_ctx* c) {
 // (+ the u8 copy Dn): mssp_kernel, then -- when an overflow is possible --
 // sssp_kernel over the rows it listed in `redo` ([1 + rows] words).
 spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint32_t* D,
-                       uint8_t* Dn, uint32_t* redo, hipStream_t s) {
+                       uint8_t* Dn, uint32_t* redo, hipStream_t s, uint32_t* maxd) {
   const uint32_t sd = mssp_words(c);
   if (!sd) return fail(c, SPF_E_STATE, "mssp kernel does not apply to this graph");
   if (c->mp_epoch != c->epoch) return fail(c, SPF_E_STATE, "mssp tables stale: rebuild the plan");
@@ -533,7 +543,8 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
 #define MP_LAUNCH2(SDV, U8V)                                                                      \
   hipLaunchKernelGGL((mssp_kernel<SDV, U8V>), g, b, mp_lds(N, SDV), s, c->d_sell_ptr.p, c->d_mp_ell.p, \
                      c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
-                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, alt, dep, c->d_stamps.p)
+                     c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, alt, dep, c->d_stamps.p, \
+                     maxd)
   switch (sd) {
     case 8: MP_LAUNCH(8); break;
     case 4: MP_LAUNCH(4); break;

@@ -1220,11 +1220,20 @@ __device__ __forceinline__ void bload(uint32_t* d, __amdgpu_buffer_rsrc_t r, uin
 // never re-read by the pass; fabric_full next hops 0.102 -> 0.079 ms,
 // gpurun_out/r03_nt); 0 = default (build-time A/B)
 constexpr int kSlStoreAux = SPF_SL_STORE_AUX;
-template <int P, int U = (P <= 4 ? 4 : 2)>
+//   WEIGHTED (weighted plans, wts = the unit's neighbour metrics): the
+//   test is d_x + w(s, x) == d_s, the sum formed bit-sliced with w a
+//   wave-uniform constant (sum_b = a_b ^ c ^ w_b, carry = a_b c | (a_b ^ c)
+//   w_b) -- ~6 bit operations per plane and 32 destinations where the byte
+//   rows spend ~65 per 16.  A carry out of the top plane (the sum passes the
+//   all-ones code: a drained neighbour's dead row, an unreachable node, or a
+//   metric past the planes) matches nothing; an unreachable d_s (all ones)
+//   cannot equal a finite d_x + w (d_x finite makes d_s finite).
+template <int P, bool WEIGHTED = false, int U = (P <= 4 ? 4 : 2)>
 __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t ro,
                                             uint32_t wpm, uint32_t srow,
                                             const uint32_t* __restrict__ offs, uint32_t k,
-                                            uint32_t jb, uint32_t w, bool live) {
+                                            uint32_t jb, uint32_t w, bool live,
+                                            const uint32_t* __restrict__ wts = nullptr) {
   const uint32_t wpb = w * P * 4;  // the lane's plane bytes inside any row
   Planes<P> sv;
   bload<P>(sv.v, rs, wpb, srow * kSlSlots * wpm * 4);
@@ -1235,7 +1244,7 @@ __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_
     const uint32_t x = sv.v[b];
     ones &= x;
     zeros &= ~x;
-    t[b] = x ^ borrow;  // t = d_s - 1
+    t[b] = WEIGHTED ? x : x ^ borrow;  // unit metrics: t = d_s - 1
     borrow &= ~x;
   }
   // the source itself (d = 0) and unreachable destinations take no next hop;
@@ -1258,8 +1267,24 @@ __device__ __forceinline__ void sliced_pass(__amdgpu_buffer_rsrc_t rs, __amdgpu_
     for (int u = 0; u < U; ++u) {
       if (j0 + u >= k) break;
       uint32_t diff = 0;
+      if constexpr (WEIGHTED) {
+        const uint32_t wj = wts[j0 + u];  // wave-uniform: a scalar load
+        if (wj >> P) {
+          diff = ~0u;  // d_x + w past the planes: no finite d_s there
+        } else {
+          uint32_t c = 0;
 #pragma unroll
-      for (int b = 0; b < P; ++b) diff |= r[u].v[b] ^ t[b];
+          for (int b = 0; b < P; ++b) {
+            const uint32_t a = r[u].v[b], wb = 0u - ((wj >> b) & 1u), ac = a ^ c;
+            diff |= ac ^ wb ^ t[b];
+            c = (a & c) | (ac & wb);
+          }
+          diff |= c;
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < P; ++b) diff |= r[u].v[b] ^ t[b];
+      }
       if (live)
         __builtin_amdgcn_raw_buffer_store_b32(~diff & valid, ro, (int)(w * 4),
                                               (int)((jb + j0 + u) * wpm * 4), kSlStoreAux);
@@ -1379,7 +1404,8 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     uint32_t dead, uint32_t hop, const uint64_t* __restrict__ nh_off, uint32_t* __restrict__ nh,
     const uint4* __restrict__ units, const uint32_t* __restrict__ unit_off,
     const uint32_t* __restrict__ gtab /* group units: [n, sources...] */, uint32_t s_bytes,
-    uint32_t fixed_p /* rows sliced by the BFS itself (sdirect): P planes, maxd unused */) {
+    uint32_t fixed_p /* rows sliced by the BFS itself (sdirect): P planes, maxd unused */,
+    uint32_t weighted /* d_x + w(s, x) == d_s (weighted plans) instead of d_x == d_s - 1 */) {
   const uint32_t md = fixed_p ? 0u : *maxd;
   const uint32_t g = blockIdx.x & 7;  // this block's XCD (round-robin placement)
   const uint32_t lane = threadIdx.x & 63;
@@ -1405,15 +1431,23 @@ __global__ __launch_bounds__(kEcmpThreads) void ecmp_sliced_kernel(
     for (uint32_t c = c0; c < c1; ++c) {
       const uint32_t w0 = c * 64, w = w0 + lane;
       const bool live = w < wpm;
+#define SL_CASE(PV)                                                                          \
+  case PV:                                                                                   \
+    if (weighted)                                                                            \
+      sliced_pass<PV, true>(rs, ro, wpm, srow, offs + j0, k, j0, w, live, nb_w + nb0 + j0);  \
+    else                                                                                     \
+      sliced_pass<PV>(rs, ro, wpm, srow, offs + j0, k, j0, w, live);                         \
+    break;
       switch (P) {
-        case 1: sliced_pass<1>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 2: sliced_pass<2>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 3: sliced_pass<3>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 4: sliced_pass<4>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 5: sliced_pass<5>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 6: sliced_pass<6>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 7: sliced_pass<7>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
-        case 8: sliced_pass<8>(rs, ro, wpm, srow, offs + j0, k, j0, w, live); break;
+        SL_CASE(1)
+        SL_CASE(2)
+        SL_CASE(3)
+        SL_CASE(4)
+        SL_CASE(5)
+        SL_CASE(6)
+        SL_CASE(7)
+        SL_CASE(8)
+#undef SL_CASE
         default: {
           uint32_t* out = nh + nh_off[i] + w;
           // saturated: exact u32 rows, 32 destinations per lane (offsets are
@@ -2240,6 +2274,10 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   {
     const char* e = std::getenv("SPF_NARROW");
     p->sliced = p->ms && p->narrow && !use_planes(c) && !(e && e[0] == '1');
+    // weighted plans on mssp_kernel: its u8 rows sliced too, next hops by
+    // bit-sliced sums d_x + w (sliced_pass<P, true>); SPF_WSLICED=0: byte rows
+    const char* ws = std::getenv("SPF_WSLICED");
+    if (p->mp && p->narrow && !(e && e[0] == '1') && !(ws && ws[0] == '0')) p->sliced = true;
     // SPF_EXPAND=1 (A/B; measured slower): the BFS stores the u8
     // rows only and the slicing pass expands them into the u32 rows.  By
     // default the BFS stores both: its u32 stores drain behind its
@@ -2331,7 +2369,8 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       // per-source units.  (SPF_SLICED_GROUP=0: no groups, =1: whole
       // identical lists only -- round 3's rule; A/B.)
       const char* ge = std::getenv("SPF_SLICED_GROUP");
-      const int gmode = ge ? atoi(ge) : 2;
+      // (weighted plans: no groups -- members share neighbour rows, not metrics)
+      const int gmode = p->mp ? 0 : ge ? atoi(ge) : 2;
       p->max_xcd_units = 0;
       for (int g = 0; g < 8; ++g) {
         unit_off[g] = (uint32_t)(units.size() / 4);
@@ -2818,7 +2857,7 @@ spf_status launch_ecmp_sliced(spf_ctx* c, spf_plan* p, const uint32_t* D, bool h
                      c->d_nb_ptr.p, c->d_nb_id.p, c->d_nb_w.p, p->d_nb_row.p, p->d_nb_row_off.p,
                      p->d_nb_drained.p, p->dead, hop ? 1u : 0u, p->d_nh_off.p, d_nh,
                      reinterpret_cast<const uint4*>(p->d_units.p), p->d_unit_off.p, p->d_gtab.p,
-                     (uint32_t)(p->d_S.n * 4), p->sdirect ? kTeamPlanes : 0u);
+                     (uint32_t)(p->d_S.n * 4), p->sdirect ? kTeamPlanes : 0u, p->mp ? 1u : 0u);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }
@@ -3025,7 +3064,7 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
                                        sliced && p->expand ? kSlSat : 0u,
                                        p->pl_order ? p->d_pl_order.p : nullptr)
                   : p->mp ? launch_mssp(c, p->d_closure.p, rows, D, p->narrow ? p->d_Dn.p : nullptr,
-                                        p->d_redo.p, s)
+                                        p->d_redo.p, s, sliced ? p->d_maxd.p : nullptr)
                         : launch_sssp(c, p->d_closure.p, rows, hop, nullptr, D, s, nullptr,
                                       nullptr, p->narrow ? p->d_Dn.p : nullptr);
   if (st != SPF_OK) return st;

@@ -283,3 +283,24 @@ def test_weighted_narrow_rows(name, make, narrow, monkeypatch):
     plan = eng.plan([0])
     assert plan.row_mode() == ("u8" if narrow == "1" else "u32")
     compare(names, eng, orc, list(range(len(names))))
+
+
+@pytest.mark.parametrize("name,make", [
+    ("fabric_rtt600", lambda: T.fabric_rtt(num_sws=600)),
+    ("wan_dense", lambda: T.random_graph(400, 3200, 5, max_metric=40, overload_frac=0.05)),
+    ("wan_small_metrics", lambda: T.wan(300, 150, seed=4, max_metric=3)),
+    ("wan_deep", lambda: T.random_graph(500, 2600, 9, max_metric=600)),  # saturates: u32 fallback
+    ("rand_parallel", lambda: T.random_graph(120, 400, 7, max_metric=9, parallel_frac=0.2,
+                                             overload_frac=0.1, link_overload_frac=0.05)),
+], ids=["fabric_rtt", "dense_drained", "small_metrics", "deep", "parallel_drained"])
+def test_weighted_sliced_next_hops(name, make, monkeypatch):
+    """Weighted plans on mssp_kernel with bit-sliced rows (the default): next
+    hops from d_x + w(s, x) == d_s formed bit-sliced per 32 destinations,
+    drained neighbours, parallel links, metrics past the planes and rows
+    deep enough to fall back to u32 rows -- every source against the oracle."""
+    monkeypatch.setenv("SPF_NARROW", "2")  # u8 rows (then sliced) at any degree
+    monkeypatch.delenv("SPF_WSLICED", raising=False)
+    names, eng, orc = load(make())
+    plan = eng.plan(list(range(len(names))))
+    assert plan.kernels()[0] == "mssp_kernel" and plan.row_mode() == "sliced"
+    compare(names, eng, orc, list(range(len(names))))
