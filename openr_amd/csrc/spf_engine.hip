@@ -788,7 +788,11 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_planes_kernel(
       // No per-lane masking: a finished node gets nx = 0 from ~vis, a slot
       // past N has only padding columns (F[N] == 0).
       if (__ballot(vis[i] != all)) {
-        uint32_t acc = PL_F(q.x & 0xFFFFu) | PL_F(q.x >> 16) | PL_F(q.y & 0xFFFFu) | PL_F(q.y >> 16);
+        // all four reads in flight before the first use (one LDS round trip)
+        uint32_t f0 = PL_F(q.x & 0xFFFFu), f1 = PL_F(q.x >> 16), f2 = PL_F(q.y & 0xFFFFu),
+                 f3 = PL_F(q.y >> 16);
+        asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+        uint32_t acc = f0 | f1 | f2 | f3;
 #pragma unroll 1
         for (uint32_t g = 1; g < sg[i]; ++g) {  // wider slices: the remaining groups
           const uint2 r = LCOL ? lcol[sb[i] + g * kSliceW + ln] : col4(sb[i] + g * kSliceW, ln);
