@@ -396,19 +396,12 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
   uint32_t sv[OWN];  // first node of owned slice i (wave-uniform)
   uint64_t vis[OWN], nv[OWN];
   uint32_t drained = 0;  // bit i: owned node i is drained
-  uint32_t sb[OWN], sw[OWN];  // owned slice i: column base, width (wave-uniform)
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     sv[i] = __builtin_amdgcn_readfirstlane(smap[wv * OWN + i]) * kSliceW;
     const uint32_t v = sv[i] + lane;
     vis[i] = v < N ? F[v] : 0ull;  // the node's own source bit, if it is a source
     if (v < N && ovl[v]) drained |= 1u << i;
-    const bool live = sv[i] < N;
-    const uint32_t slice = live ? sv[i] / kSliceW : 0u;
-    const uint32_t b = live ? sell_ptr[slice] : 0u;
-    const uint32_t e = live ? sell_ptr[slice + 1] : 0u;
-    sb[i] = __builtin_amdgcn_readfirstlane(b);
-    sw[i] = __builtin_amdgcn_readfirstlane((e - b) / kSliceW);
   }
   __syncthreads();  // the self marks are read
   if (tid < nb) F[src_l[tid]] = 0;
@@ -496,9 +489,15 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
     const bool need = v < N && vis[i] != all;
     uint64_t nx = 0;
     if (__ballot(need)) {  // wave-uniform: the slice has unfinished nodes
-      const uint32_t* cp = sell_col + sb[i] + lane;
-      const uint16_t* lp = lcol + sb[i] + lane;
-      const uint32_t w = sw[i];
+      // the slice's column base and width: scalar loads per call (ten
+      // slices' pairs held across the level loop spilled SGPRs to VGPR
+      // lanes: 110 spills -> 5, fabric_full BFS 0.161 -> 0.157 ms)
+      uint32_t sl = sv[i] / kSliceW;
+      asm volatile("" : "+s"(sl));
+      const uint32_t sbi = sell_ptr[sl];
+      const uint32_t w = (sell_ptr[sl + 1] - sbi) / kSliceW;
+      const uint32_t* cp = sell_col + sbi + lane;
+      const uint16_t* lp = lcol + sbi + lane;
       uint64_t acc = 0;
       uint32_t j = 0;
       if constexpr (!LCOL) {
@@ -514,7 +513,7 @@ __global__ __launch_bounds__(kMsThreads) void msbfs_kernel(
 #pragma unroll
           for (int u = 0; u < kMsUnroll; ++u)
             c[u] = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 4u),
-                                                        (int)((sb[i] + (j0 + u) * kSliceW) * 4u), 0);
+                                                        (int)((sbi + (j0 + u) * kSliceW) * 4u), 0);
         };
         auto fold = [&](const uint32_t (&c)[kMsUnroll], uint32_t n) {
           uint64_t f[kMsUnroll];
