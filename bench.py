@@ -577,7 +577,7 @@ class Ksp2AllPairs:
             # one exchange: every rank's pair headers and path pool to rank 0
             from openr_amd.sharding import gather_padded
 
-            used = int(self.d_cnt.t[0].item())
+            used = min(int(self.d_cnt.t[0].item()), self.d_pool.t.numel())
             gather_padded(self.d_pairs.t, self.d_pairs.t.numel())
             gather_padded(self.d_pool.t, used)
 
@@ -648,11 +648,12 @@ class Ksp2AllPairs:
         self.k2_runs = int(cnt_h[1])
         # compulsory bytes: the k = 1 SPF reads the CSR once per source and
         # writes a distance row; the KSP2 kernel stages the graph once per
-        # block (destination x 64-source chunk) and writes the pair records
-        # and path pool once
+        # block (destination x the plan's source chunk) and writes the pair
+        # records and path pool once
         n, e = self.n, self.e
         csr = 4 * (n + 1) + 12 * e
-        blocks = n * ((len(self.srcs) + 63) // 64)
+        chunk = self.plan.chunk()
+        blocks = n * ((len(self.srcs) + chunk - 1) // chunk)
         self.kernel_bytes = {
             "sssp_kernel": len(self.srcs) * (4 * (n + 1) + 8 * e + n + 4 * self.eng.pitch),
             "ksp2_kernel": blocks * csr + 16 * self.units + 4 * int(cnt_h[0])}

@@ -292,9 +292,14 @@ typedef struct spf_ksp2_plan spf_ksp2_plan;
 spf_status spf_ksp2_plan_create(spf_ctx* ctx, const uint32_t* srcs, uint32_t n_src,
                                 spf_ksp2_plan** out);
 void spf_ksp2_plan_destroy(spf_ksp2_plan* plan);
+/* Sources per KSP2 workgroup (a block is one destination x this many
+ * sources; the graph is staged once per block): for traffic accounting. */
+uint32_t spf_ksp2_plan_chunk(const spf_ksp2_plan* plan);
 /* Enqueue on `stream` (NULL = context stream).  d_pairs = [n_src * n_nodes],
  * d_pool = pool_words u32, d_counters = 4 u64 zeroed by the call:
- *   [0] pool words claimed (> pool_words means the pool overflowed),
+ *   [0] pool words claimed, reservations' unused tails included (may
+ *       exceed pool_words without an overflow: bit 0 of [2] is the only
+ *       overflow signal; the written words are at most min([0], pool_words)),
  *   [1] k = 2 SPF runs (the reference's un-memoised runSpf calls, :778-779),
  *   [2] bit 0 = overflow (bit 1: redo list full, never on plans made by
  *       spf_ksp2_plan_create, which size it for every pair),

@@ -187,6 +187,7 @@ PROTOTYPES = {
     "spf_debug_copy_bandwidth": (C.c_int, [_vp, C.c_uint64, C.c_uint32, C.POINTER(C.c_double)]),
     "spf_ksp2_plan_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.POINTER(_vp)]),
     "spf_ksp2_plan_destroy": (None, [_vp]),
+    "spf_ksp2_plan_chunk": (C.c_uint32, [_vp]),
     "spf_ksp2_execute": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "spf_ksp2_digest": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "spf_ksp2_enable_timing": (C.c_int, [_vp, C.c_uint32]),

@@ -48,11 +48,11 @@ constexpr uint32_t kPoolGrab = 256;         // words a wave reserves at a time (
 constexpr size_t kMaxLdsKsp = 160 * 1024;
 constexpr uint32_t kCompactCap = 512;       // u16-label waves: DFS stack / SPF queue entries
 constexpr uint32_t kRedoBlocks = 256;       // workgroups of the u32 redo pass
-constexpr uint32_t kProfSlots = 1024;
+constexpr uint32_t kProfSlots = 1024;  // SPF_KSP2_PROF: 16-counter slots (by block)
 #ifndef KSP2_EDGES
 #define KSP2_EDGES 2
 #endif
-constexpr uint32_t kKspEdges = KSP2_EDGES;  // edges per lane per relaxation step       // SPF_KSP2_PROF: 16-counter slots (by block)
+constexpr uint32_t kKspEdges = KSP2_EDGES;  // edges per lane per relaxation step
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1038,6 +1038,7 @@ spf_status spf_ksp2_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src
 }
 
 void spf_ksp2_plan_destroy(spf_ksp2_plan* p) { delete p; }
+uint32_t spf_ksp2_plan_chunk(const spf_ksp2_plan* p) { return p ? p->chunk : 0u; }
 
 spf_status spf_ksp2_digest(spf_ksp2_plan* p, const spf_ksp2_pair* d_pairs, const uint32_t* d_pool,
                            const uint64_t* d_link_hash, uint64_t* d_out, void* stream) {
@@ -1192,9 +1193,12 @@ spf_status spf_ksp2_solve(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   // then k = 2, list order) so the layout -- and *pool_used -- is the same on
   // every call (the sizing call's answer fits the second call exactly).
   std::vector<spf_ksp2_pair> hp(n_pairs);
-  std::vector<uint32_t> pool_h(cnt[0]);
+  // cnt[0] counts claimed reservations, a last grab's unused tail included:
+  // it can pass the pool's size with no overflow, so copy what the pool holds
+  const uint64_t held = std::min<uint64_t>(cnt[0], cap);
+  std::vector<uint32_t> pool_h(held);
   HIP_TRY(c, hipMemcpy(hp.data(), d_pairs.p, n_pairs * sizeof(spf_ksp2_pair), hipMemcpyDeviceToHost));
-  if (cnt[0]) HIP_TRY(c, hipMemcpy(pool_h.data(), d_pool.p, cnt[0] * 4, hipMemcpyDeviceToHost));
+  if (held) HIP_TRY(c, hipMemcpy(pool_h.data(), d_pool.p, held * 4, hipMemcpyDeviceToHost));
   uint64_t dense = 0;
   for (const spf_ksp2_pair& r : hp)
     for (int k = 0; k < 2; ++k)

@@ -241,7 +241,20 @@ spf_status run_part(spf_mplan* mp, uint32_t i) {
   }
   // (a capture made before a team timeout turned teams off is stale too)
   if (p.gexec && p.g_epoch == spf_graph_epoch(c) && p.g_team_off == c->team_off) {
+    // A replay bypasses the plan's own resident_order / resident_done (they
+    // skip a capturing stream): a plan with grid-resident launches (team BFS,
+    // big-graph kernel) orders the replay itself, so it never splits the CUs
+    // with another context's resident launch on this device.
+    const bool resident = p.plan->tm_G || p.plan->big;
+    if (resident) {
+      const spf_status st = resident_order(c, s);
+      if (st != SPF_OK) return member_fail(m, i, st);
+    }
     M_HIP(m, hipGraphLaunch(p.gexec, s));
+    if (resident) {
+      const spf_status st = resident_done(c, s);
+      if (st != SPF_OK) return member_fail(m, i, st);
+    }
   } else {
     if (p.gexec) {
       (void)hipGraphExecDestroy(p.gexec);
@@ -249,6 +262,12 @@ spf_status run_part(spf_mplan* mp, uint32_t i) {
       p.gexec = nullptr;
       p.graph = nullptr;
     }
+    // A re-derive (graph patched, teams turned off) rebuilds the plan's
+    // tables on the member's own stream; a member whose execute runs on a
+    // shared stream (repeated device id) waits for what is in flight there
+    // first, so the rebuild never overwrites tables a queued kernel reads.
+    if (s != c->stream && (p.plan->epoch != c->epoch || (p.plan->tm_G && c->team_off)))
+      M_HIP(m, hipStreamSynchronize(s));
     spf_status st = spf_plan_execute(p.plan, p.dist.p, p.nh.p, s);
     if (st != SPF_OK) return member_fail(m, i, st);
     if (mp->graphs) {  // the plan is derived for this epoch now: capture its launches
@@ -316,8 +335,21 @@ int spf_mctx_device(const spf_mctx* m, uint32_t i) {
   return m && i < m->members.size() ? m->members[i]->device : -1;
 }
 
+// Patches upload on each member's own stream, while a member of a repeated
+// device id executes on that device's shared stream: wait for every execute
+// stream first, so a patch never rewrites the drain bytes / metrics a queued
+// execute still reads (spf_mplan_execute returns before its kernels run).
+static spf_status drain_exec(spf_mctx* m) {
+  for (uint32_t i = 0; i < m->members.size(); ++i) {
+    M_HIP(m, hipSetDevice(m->members[i]->device));
+    M_HIP(m, hipStreamSynchronize(m->exec[i]));
+  }
+  return SPF_OK;
+}
+
 spf_status spf_mctx_graph_load(spf_mctx* m, const spf_graph* g) {
   if (!m || !g) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_load: NULL argument");
+  if (const spf_status st = drain_exec(m); st != SPF_OK) return st;
   for (uint32_t i = 0; i < m->members.size(); ++i) {
     const spf_status st = spf_graph_load(m->members[i], g);
     if (st != SPF_OK) return member_fail(m, i, st);
@@ -328,6 +360,7 @@ spf_status spf_mctx_graph_load(spf_mctx* m, const spf_graph* g) {
 spf_status spf_mctx_graph_set_overload(spf_mctx* m, const uint32_t* nodes, const uint8_t* overloaded,
                                        uint32_t n) {
   if (!m) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_set_overload: NULL context");
+  if (const spf_status st = drain_exec(m); st != SPF_OK) return st;
   for (uint32_t i = 0; i < m->members.size(); ++i) {
     const spf_status st = spf_graph_set_overload(m->members[i], nodes, overloaded, n);
     if (st != SPF_OK) return member_fail(m, i, st);
@@ -338,6 +371,7 @@ spf_status spf_mctx_graph_set_overload(spf_mctx* m, const uint32_t* nodes, const
 spf_status spf_mctx_graph_set_metric(spf_mctx* m, const uint32_t* edges, const int32_t* metric,
                                      uint32_t n) {
   if (!m) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_set_metric: NULL context");
+  if (const spf_status st = drain_exec(m); st != SPF_OK) return st;
   for (uint32_t i = 0; i < m->members.size(); ++i) {
     const spf_status st = spf_graph_set_metric(m->members[i], edges, metric, n);
     if (st != SPF_OK) return member_fail(m, i, st);

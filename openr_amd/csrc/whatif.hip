@@ -134,7 +134,25 @@ constexpr uint32_t kBarSpin = 1u << 26;            // ~seconds: never a silent h
 // of the launch's output.  One word per context (spf_ctx::d_fault), so a
 // check on one context neither reports nor clears another's timeout.
 __device__ __forceinline__ void barrier_timed_out(uint32_t* fault) {
-  if (fault) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (fault) __hip_atomic_fetch_or(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A repair loop that reached its iteration bound (it cannot, for a correct
+// kernel: every bound is the loop's worst case + 2) reports where instead of
+// spinning on: bit 3 of the fault word, the phase in bits 8-15
+// (spf_device_check names it).  1 D discovery, 2 label-correcting sweeps,
+// 3 next-hop fixed point.
+__device__ __forceinline__ void loop_bound_hit(uint32_t* fault, uint32_t phase) {
+  if (fault)
+    __hip_atomic_fetch_or(fault, 8u | (phase << 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// After one barrier timed out the launch's results are void; later barriers
+// must not each wait out their own spin (a desynchronised team would cross
+// thousands of them): a spin polls the fault word every 1024 polls and gives
+// up once it is set.
+__device__ __forceinline__ bool fault_set(const uint32_t* fault) {
+  return fault && __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
 }
 
 struct XGrid {
@@ -161,14 +179,18 @@ struct XGrid {
         __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (; k < kBarSpin &&
                __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g * ngroups;
-             ++k)
+             ++k) {
+          if ((k & 1023u) == 1023u && fault_set(fault)) break;
           __builtin_amdgcn_s_sleep(1);
+        }
         __hip_atomic_store(gen, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         for (; k < kBarSpin &&
                __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g;
-             ++k)
+             ++k) {
+          if ((k & 1023u) == 1023u && fault_set(fault)) break;
           __builtin_amdgcn_s_sleep(1);
+        }
       }
       if (k == kBarSpin) barrier_timed_out(fault);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -809,8 +831,10 @@ __device__ __forceinline__ void team_sync(TeamCtl* ctl, uint32_t* fault) {
       uint32_t k = 0;
       for (; k < kBarSpin &&
              __hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
-           ++k)
+           ++k) {
+        if ((k & 1023u) == 1023u && fault_set(fault)) break;
         __builtin_amdgcn_s_sleep(1);
+      }
       if (k == kBarSpin) barrier_timed_out(fault);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -839,39 +863,87 @@ __device__ __forceinline__ void stw(uint32_t* p, uint32_t v) {
   if constexpr (GROUP) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+template <bool GROUP>
+__device__ __forceinline__ unsigned long long ldq(const unsigned long long* p) {
+  if constexpr (GROUP) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <bool GROUP>
+__device__ __forceinline__ void stq(unsigned long long* p, unsigned long long v) {
+  if constexpr (GROUP) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
-template <int TEAM, bool GROUP = false>
+// CHK (the profiled wave instance, SPF_WHATIF_PROF): every scratch-derived
+// index is range-checked before use; an out-of-range one sets bit 4 of the
+// fault word with the site in bits 16-23 and is replaced by a safe value
+// (results then invalid, reported by spf_device_check).
+template <int TEAM, bool GROUP = false, bool CHK = false>
 __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
                        uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, uint32_t cap,
                        TeamCtl* ctl, uint32_t tt, uint32_t e_fail, spf_whatif_digest* out,
-                       unsigned long long* prof = nullptr) {
-  // diagnostics (SPF_WHATIF_PROF): phase clocks of this team's last failure
-#define WI_STAMP(k)                                                      \
-  do {                                                                   \
-    if (prof && tt == 0) prof[k] = __builtin_amdgcn_s_memtime();        \
+                       uint64_t* ph = nullptr) {
+  // diagnostics (SPF_WHATIF_PROF): ph is the caller's register array of 12
+  // counters, accumulated over the team's failures and stored once when the
+  // team exits (no memory traffic inside a repair) -- [0] repairs, [1..5]
+  // 100 MHz ticks in D discovery, seeds, Dial, fallback sweeps, digest;
+  // [8] sum |D|, [9] sum Dial levels, [10] max |D|, [11] repairs given up
+  uint64_t tprev = ph ? wall_clock64() : 0ull;
+#define WI_STAMP(k)                              \
+  do {                                           \
+    if (ph) {                                    \
+      const uint64_t now_ = wall_clock64();      \
+      ph[k] += now_ - tprev;                     \
+      tprev = now_;                              \
+    }                                            \
   } while (0)
-  WI_STAMP(0);
   const uint32_t W = g.W;
   constexpr uint32_t kWaves = TEAM / 64;
+  // range check (CHK): x < lim, or x == kInf when `inf_ok`
+  auto chk = [&](uint32_t x, uint32_t lim, bool inf_ok, uint32_t site, uint32_t safe) -> uint32_t {
+    if constexpr (CHK) {
+      if (!(x < lim || (inf_ok && x == kInf))) {
+        if (g.fault)
+          __hip_atomic_fetch_or(g.fault, 16u | (site << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return safe;
+      }
+    }
+    return x;
+  };
   const uint32_t lane = tt & 63, wv = tt >> 6;
   const uint32_t l = g.link[e_fail];
   const uint32_t b = g.col[e_fail];
   if (tt == 0) {
-    ctl->n = 1;
-    ctl->ovf = 0;
-    ctl->hub = 0;
-    ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
-    ctl->ndist = ctl->nnh = ctl->dh = 0;
+    stw<GROUP>(&ctl->n, 1u);
+    stw<GROUP>(&ctl->ovf, 0u);
+    stw<GROUP>(&ctl->hub, 0u);
+    for (int q = 0; q < 3; ++q) stw<GROUP>(&ctl->flag[q], 0u);
+    stq<GROUP>(&ctl->ndist, 0ull);
+    stq<GROUP>(&ctl->nnh, 0ull);
+    stq<GROUP>(&ctl->dh, 0ull);
     dlist[0] = b;
     stw<GROUP>(&mark[b], 0);
   }
   team_sync<TEAM, GROUP>(ctl, g.fault);
   // ---- D = descendants of b in the unfailed DAG (level by level) ----
+  // Control words (ctl->n / ovf / hub / flag / nxt / lc) are written by
+  // atomics and plain stores of other lanes, waves or CUs: every read of one
+  // is an atomic load at the team's scope (ldw), so the compiler can neither
+  // keep a stale copy in a register nor move the read across the team
+  // barrier.  Every loop is bounded by its worst case + 2 (an iteration adds
+  // a node, or settles one more level); a bound hit reports its phase in the
+  // fault word and leaves the repair (loop_bound_hit).
   uint32_t lo = 0;
-  for (;;) {
-    const uint32_t n = ctl->n;
+  bool bound_hit = false;
+  for (uint32_t iter = 0;; ++iter) {
+    const uint32_t n = ldw<GROUP>(&ctl->n);
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    if (lo >= n || ctl->ovf) break;
+    if (lo >= n || ldw<GROUP>(&ctl->ovf)) break;
+    if (iter > cap + 2) {  // team-uniform
+      bound_hit = true;
+      if (tt == 0) loop_bound_hit(g.fault, 1);
+      break;
+    }
     // a thread per frontier node; hubs (thousands of edges) are queued in
     // ord and expanded by a whole wave each
     auto child = [&](uint32_t dv, uint32_t e) {
@@ -884,11 +956,11 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         stw<GROUP>(&mark[c], idx);
       } else {
         stw<GROUP>(&mark[c], kInf);
-        ctl->ovf = 1;
+        stw<GROUP>(&ctl->ovf, 1u);
       }
     };
     for (uint32_t i = lo + tt; i < n; i += TEAM) {
-      const uint32_t v = dlist[i];
+      const uint32_t v = chk(dlist[i], g.N, false, 1, b);
       if (g.ovl[v]) continue;  // drained (v != src): no DAG children
       const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
       if (b1 - b0 > kHubDeg) {
@@ -900,22 +972,27 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
     {
-      const uint32_t nh_ = ctl->hub;
+      const uint32_t nh_ = ldw<GROUP>(&ctl->hub);
       for (uint32_t k = wv; k < nh_; k += kWaves) {
-        const uint32_t v = dlist[ldw<GROUP>(&ord[k])];
+        const uint32_t v = chk(dlist[chk(ldw<GROUP>(&ord[k]), n, false, 2, 0)], g.N, false, 3, b);
         const uint32_t dv = B.dist[v];
         for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) child(dv, e);
       }
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    if (tt == 0) ctl->hub = 0;
+    if (tt == 0) stw<GROUP>(&ctl->hub, 0u);
     lo = n;
     team_sync<TEAM, GROUP>(ctl, g.fault);
   }
-  const uint32_t n = min(ctl->n, cap);
-  const bool ovf = ctl->ovf != 0;
+  const uint32_t n = min(ldw<GROUP>(&ctl->n), cap);
+  const bool ovf = ldw<GROUP>(&ctl->ovf) != 0 || bound_hit;
   WI_STAMP(1);
-  if (prof && tt == 0) prof[8] = n;
+  if (ph) {
+    ph[0] += 1;
+    ph[8] += n;
+    ph[10] = ph[10] > n ? ph[10] : (uint64_t)n;
+    ph[11] += ovf;
+  }
   team_sync<TEAM, GROUP>(ctl, g.fault);
   if (ovf) {
     for (uint32_t i = tt; i < n; i += TEAM) stw<GROUP>(&mark[dlist[i]], kInf);
@@ -944,9 +1021,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   }
   team_sync<TEAM, GROUP>(ctl, g.fault);
   {
-    const uint32_t nh_ = ctl->hub;
+    const uint32_t nh_ = ldw<GROUP>(&ctl->hub);
     for (uint32_t k = wv; k < nh_; k += kWaves) {
-      const uint32_t i = ldw<GROUP>(&ord[k]);
+      const uint32_t i = chk(ldw<GROUP>(&ord[k]), n, false, 4, 0);
       const uint32_t v = dlist[i];
       uint32_t best = kInf;
       for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64)
@@ -956,7 +1033,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }
   }
   team_sync<TEAM, GROUP>(ctl, g.fault);
-  if (tt == 0) ctl->hub = 0;
+  if (tt == 0) stw<GROUP>(&ctl->hub, 0u);
   // nh word j of a D node from its tight expanded predecessors (D or not);
   // used by the fixed-point fallback
   auto nh_of = [&](uint32_t i, uint32_t j) -> uint32_t {
@@ -967,7 +1044,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.link[e] == l) continue;
       const uint32_t u = g.col[e];
       if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = ldw<GROUP>(&mark[u]);
+      const uint32_t mu = chk(ldw<GROUP>(&mark[u]), n, true, 5, kInf);
       const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
       if (du == kInf || du + in_w(g, e) != dv) continue;
       if (u == g.src) {
@@ -987,11 +1064,11 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (g.link[e] == l) continue;
       const uint32_t u = g.col[e];
       if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = ldw<GROUP>(&mark[u]);
+      const uint32_t mu = chk(ldw<GROUP>(&mark[u]), n, true, 6, kInf);
       const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
       if (du == kInf || du + in_w(g, e) != dv) continue;
       if (u == g.src) {
-        const uint32_t jb = g.nbr_bit[v];
+        const uint32_t jb = chk(g.nbr_bit[v], 32 * W, false, 7, 0);
         row[jb >> 5] |= 1u << (jb & 31);
       } else {
         const uint32_t* from = mu != kInf ? nhn + (size_t)mu * W : B.nhb + (size_t)u * W;
@@ -1027,9 +1104,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   const size_t nw = (size_t)n * W;
   for (size_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
   if (tt == 0) {
-    ctl->dmin = kInf;
-    ctl->nxt[0] = kInf;
-    ctl->lc[0] = 0;
+    stw<GROUP>(&ctl->dmin, kInf);
+    stw<GROUP>(&ctl->nxt[0], kInf);
+    stw<GROUP>(&ctl->lc[0], 0u);
   }
   team_sync<TEAM, GROUP>(ctl, g.fault);
   {
@@ -1042,7 +1119,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   // ---- Dial: settle D one distance value at a time (metrics are positive:
   // a node holding the smallest pending value is final), next hops inline ----
   bool settled = true;
-  uint32_t t = ctl->dmin;
+  uint32_t t = ldw<GROUP>(&ctl->dmin);
   for (uint32_t it = 0; t != kInf; ++it) {
     if (it >= kDialLevels) {  // too many distinct values: sweep instead
       settled = false;
@@ -1051,9 +1128,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     uint32_t* next = &ctl->nxt[it % 3];
     uint32_t* cnt = &ctl->lc[it % 3];
     if (tt == 0) {  // the next level's slots, last read two levels ago
-      ctl->nxt[(it + 1) % 3] = kInf;
-      ctl->lc[(it + 1) % 3] = 0;
-      ctl->lc[(it + 2) % 3] = 0;  // this level's hub counter
+      stw<GROUP>(&ctl->nxt[(it + 1) % 3], kInf);
+      stw<GROUP>(&ctl->lc[(it + 1) % 3], 0u);
+      stw<GROUP>(&ctl->lc[(it + 2) % 3], 0u);  // this level's hub counter
     }
     // (a) the level's nodes (their distance is final) into ord
     uint32_t m = kInf;
@@ -1066,19 +1143,19 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     // (b) level nodes: next hops from their tight predecessors, then relax
     // their edges.  A thread per node; hubs (queued after the level list)
     // by a whole wave: ballot over the in-edges, coalesced row ORs.
-    const uint32_t K = *cnt;
+    const uint32_t K = ldw<GROUP>(cnt);
     uint32_t* hubs = ord + K;
     uint32_t* hub_cnt = &ctl->lc[(it + 2) % 3];  // free this level
     auto relax = [&](uint32_t v, uint32_t e) {
       if (g.link[e] == l) return;
-      const uint32_t ic = ldw<GROUP>(&mark[g.col[e]]);
+      const uint32_t ic = chk(ldw<GROUP>(&mark[g.col[e]]), n, true, 8, kInf);
       if (ic == kInf) return;
       const uint32_t nd = t + g.wt[e];
       if (nd < atomicMin(&dnew[ic], nd)) m = min(m, nd);
     };
     for (uint32_t k = tt; k < K; k += TEAM) {
-      const uint32_t i = ldw<GROUP>(&ord[k]);
-      const uint32_t v = dlist[i];
+      const uint32_t i = chk(ldw<GROUP>(&ord[k]), n, false, 9, 0);
+      const uint32_t v = chk(dlist[i], g.N, false, 10, b);
       const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
       if (b1 - b0 > kHubDeg) {
         stw<GROUP>(&hubs[atomicAdd(hub_cnt, 1u)], i);
@@ -1089,10 +1166,10 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         for (uint32_t e = b0; e < b1; ++e) relax(v, e);
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    const uint32_t H_ = *hub_cnt;
+    const uint32_t H_ = ldw<GROUP>(hub_cnt);
     for (uint32_t k = wv; k < H_; k += kWaves) {
-      const uint32_t i = ldw<GROUP>(&hubs[k]);
-      const uint32_t v = dlist[i];
+      const uint32_t i = chk(ldw<GROUP>(&hubs[k]), n, false, 11, 0);
+      const uint32_t v = chk(dlist[i], g.N, false, 12, b);
       uint32_t* row = nhn + (size_t)i * W;
       const uint32_t jb = g.nbr_bit[v];
       bool from_src = false;
@@ -1103,7 +1180,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         if (e < g.row_ptr[v + 1] && g.link[e] != l) {
           u = g.col[e];
           if (!(g.ovl[u] && u != g.src)) {
-            mu = ldw<GROUP>(&mark[u]);
+            mu = chk(ldw<GROUP>(&mark[u]), n, true, 13, kInf);
             const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
             tight = du != kInf && du + g.wt[g.rev[e]] == t;
           }
@@ -1125,13 +1202,17 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }
     if (m != kInf) atomicMin(next, m);
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    t = *next;
-    if (prof && tt == 0) prof[9] = it + 1;
+    t = ldw<GROUP>(next);
+    if (ph) ph[9] += 1;
   }
   WI_STAMP(3);
   if (!settled) {
-    // ---- label-correcting sweeps inside D ----
+    // ---- label-correcting sweeps inside D (Bellman-Ford: at most n + 1) ----
     for (uint32_t it = 0;; ++it) {
+      if (it > n + 2) {  // team-uniform
+        if (tt == 0) loop_bound_hit(g.fault, 2);
+        break;
+      }
       bool any = false;
       for (uint32_t i = tt; i < n; i += TEAM) {
         const uint32_t v = dlist[i];
@@ -1139,24 +1220,24 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         if (dv == kInf || g.ovl[v]) continue;
         for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
           if (g.link[e] == l) continue;
-          const uint32_t ic = ldw<GROUP>(&mark[g.col[e]]);
+          const uint32_t ic = chk(ldw<GROUP>(&mark[g.col[e]]), n, true, 14, kInf);
           if (ic == kInf) continue;
           const uint32_t nd = dv + g.wt[e];
           if (nd < atomicMin(&dnew[ic], nd)) any = true;
         }
       }
-      if (any) ctl->flag[it % 3] = 1;
-      if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
+      if (any) stw<GROUP>(&ctl->flag[it % 3], 1u);
+      if (tt == 0) stw<GROUP>(&ctl->flag[(it + 1) % 3], 0u);
       team_sync<TEAM, GROUP>(ctl, g.fault);
-      if (!ctl->flag[it % 3]) break;
+      if (!ldw<GROUP>(&ctl->flag[it % 3])) break;
     }
 
     const size_t nw = (size_t)n * W;
     for (size_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
     if (tt == 0) {
-      ctl->flag[0] = ctl->flag[1] = ctl->flag[2] = 0;
-      ctl->dmin = kInf;
-      ctl->dmax = 0;
+      for (int q = 0; q < 3; ++q) stw<GROUP>(&ctl->flag[q], 0u);
+      stw<GROUP>(&ctl->dmin, kInf);
+      stw<GROUP>(&ctl->dmax, 0u);
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
     for (uint32_t i = tt; i < n; i += TEAM) {
@@ -1167,8 +1248,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       }
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    const uint32_t dmin = ctl->dmin;
-    const uint32_t nlev = dmin == kInf ? 0u : ctl->dmax - dmin + 1;
+    const uint32_t dmin = ldw<GROUP>(&ctl->dmin);
+    const uint32_t nlev = dmin == kInf ? 0u : ldw<GROUP>(&ctl->dmax) - dmin + 1;
     if (nlev <= cap) {
       // counting sort of D by new distance; a predecessor always sits in a
       // lower level (positive metrics), so one pass per level is exact
@@ -1201,15 +1282,19 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         if (end == begin) continue;
         const size_t items = (size_t)(end - begin) * W;
         for (size_t x = tt; x < items; x += TEAM) {
-          const uint32_t i = ldw<GROUP>(&ord[begin + x / W]), j = (uint32_t)(x % W);
+          const uint32_t i = chk(ldw<GROUP>(&ord[begin + x / W]), n, false, 15, 0), j = (uint32_t)(x % W);
           nhn[(size_t)i * W + j] = nh_of(i, j);
         }
         begin = end;
         team_sync<TEAM, GROUP>(ctl, g.fault);
       }
     } else {
-      // fixed-point sweeps (monotone union over the DAG)
+      // fixed-point sweeps (monotone union over the DAG: at most depth + 1)
       for (uint32_t it = 0;; ++it) {
+        if (it > n + 2) {  // team-uniform
+          if (tt == 0) loop_bound_hit(g.fault, 3);
+          break;
+        }
         bool any = false;
         for (uint32_t x = tt; x < nw; x += TEAM) {
           const uint32_t i = x / W, j = x % W;
@@ -1220,10 +1305,10 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
             any = true;
           }
         }
-        if (any) ctl->flag[it % 3] = 1;
-        if (tt == 0) ctl->flag[(it + 1) % 3] = 0;
+        if (any) stw<GROUP>(&ctl->flag[it % 3], 1u);
+        if (tt == 0) stw<GROUP>(&ctl->flag[(it + 1) % 3], 0u);
         team_sync<TEAM, GROUP>(ctl, g.fault);
-        if (!ctl->flag[it % 3]) break;
+        if (!ldw<GROUP>(&ctl->flag[it % 3])) break;
       }
     }
   }
@@ -1248,8 +1333,8 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   if (dh) atomicAdd(&ctl->dh, (unsigned long long)dh);
   team_sync<TEAM, GROUP>(ctl, g.fault);
   if (tt == 0)
-    *out = spf_whatif_digest{(uint32_t)ctl->ndist, (uint32_t)ctl->nnh,
-                             (uint64_t)(*B.H + ctl->dh)};
+    *out = spf_whatif_digest{(uint32_t)ldq<GROUP>(&ctl->ndist), (uint32_t)ldq<GROUP>(&ctl->nnh),
+                             (uint64_t)(*B.H + ldq<GROUP>(&ctl->dh))};
   team_sync<TEAM, GROUP>(ctl, g.fault);
   WI_STAMP(5);
 #undef WI_STAMP
@@ -1257,11 +1342,16 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
 }
 
 // wave teams over the hot list; failures whose D overflows kWaveCap are
-// queued for the workgroup teams
+// queued for the workgroup teams.  PROF (SPF_WHATIF_PROF): a separate
+// instance with the per-team phase counters (prof + team * 16), so the
+// production instance's registers -- which set its co-residency with the
+// group teams, spf_whatif_plan_create -- do not change with diagnostics.
+template <bool PROF>
 __global__ __launch_bounds__(256) void repair_wave_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ hot, const uint32_t* __restrict__ n_hot,
     uint32_t* cursor, uint2* big, uint32_t* n_big, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
-    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out, uint32_t cap) {
+    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out, uint32_t cap,
+    unsigned long long* prof) {
   __shared__ TeamCtl ctl[4];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t team = (size_t)blockIdx.x * 4 + w;
@@ -1272,19 +1362,23 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
   lvl += team * (cap + 1);
   ord += team * 2 * cap;  // level list + its hubs
   const uint32_t total = *n_hot;
+  uint64_t ph[12] = {};
   for (;;) {
     uint32_t k = 0;
     if (lane == 0) k = atomicAdd(cursor, 1u);
     k = __builtin_amdgcn_readlane(k, 0);
     if (k >= total) break;
     const uint2 h = hot[k];
-    if (!repair<64>(g, B, mark, dlist, dnew, nhn, lvl, ord, cap, &ctl[w], lane, h.y,
-                    out + h.x)) {
+    if (!repair<64, false, PROF>(g, B, mark, dlist, dnew, nhn, lvl, ord, cap, &ctl[w], lane, h.y,
+                                 out + h.x, PROF ? ph : nullptr)) {
       if (lane == 0) big[atomicAdd(n_big, 1u)] = h;
     }
   }
+  if (PROF && lane == 0)
+    for (int q = 0; q < 12; ++q) prof[team * 16 + q] = ph[q];
 }
 
+template <bool PROF>
 __global__ __launch_bounds__(1024) void repair_block_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
     uint32_t* mark, uint32_t* dlist, uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord,
@@ -1301,11 +1395,14 @@ __global__ __launch_bounds__(1024) void repair_block_kernel(
   lvl += team * ((size_t)g.N + 1);
   ord += team * 2 * (size_t)g.N;  // level list + its hubs
   const uint32_t total = *n_big;
+  uint64_t ph[12] = {};
   for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
     const uint2 h = big[k];
     repair<1024>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, &ctl, threadIdx.x, h.y, out + h.x,
-                 prof ? prof + team * 16 : nullptr);
+                 PROF ? ph : nullptr);
   }
+  if (PROF && threadIdx.x == 0)
+    for (int q = 0; q < 12; ++q) prof[team * 16 + q] = ph[q];
 }
 
 // The classified big failures, largest subtree first (the order the group
@@ -1339,7 +1436,7 @@ __global__ __launch_bounds__(1024) void sort_big_kernel(const uint2* __restrict_
 // both progress from the start.  Members of a team sit on one XCD (blocks x
 // and x + 8 share one); teams pull failures, largest first.
 constexpr int kGroupWg = 512;
-template <int G>
+template <int G, bool PROF>
 __global__ __launch_bounds__(kGroupWg) void repair_group_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
     uint32_t* cursor, TeamCtl* ctls, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
@@ -1359,15 +1456,18 @@ __global__ __launch_bounds__(kGroupWg) void repair_group_kernel(
   lvl += team * ((size_t)g.N + 1);
   ord += team * 2 * (size_t)g.N;
   const uint32_t total = *n_big;
+  uint64_t ph[12] = {};
   for (;;) {
-    if (tt == 0) ctl->next = atomicAdd(cursor, 1u);
+    if (tt == 0) stw<true>(&ctl->next, atomicAdd(cursor, 1u));
     team_sync<TEAM, true>(ctl, g.fault);
     const uint32_t k = ldw<true>(&ctl->next);
     if (k >= total) break;  // team-uniform
     const uint2 h = big[k];
     repair<TEAM, true>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, ctl, tt, h.y, out + h.x,
-                       prof ? prof + team * 16 : nullptr);
+                       PROF ? ph : nullptr);
   }
+  if (PROF && tt == 0)
+    for (int q = 0; q < 12; ++q) prof[team * 16 + q] = ph[q];
 }
 
 struct GroupArgs {
@@ -1403,7 +1503,18 @@ template <int G>
 hipError_t launch_group_g(GroupArgs& a, uint32_t n_cu, hipStream_t s) {
   void* args[] = {&a.g, &a.B, &a.big, &a.n_big, &a.cursor, &a.ctls, &a.mark, &a.dlist, &a.dnew,
                   &a.nhn, &a.lvl, &a.ord, &a.out, &a.prof};
-  return launch_resident((const void*)repair_group_kernel<G>, n_cu, kGroupWg, args, n_cu, s);
+  const void* k = a.prof ? (const void*)repair_group_kernel<G, true> : (const void*)repair_group_kernel<G, false>;
+  return launch_resident(k, n_cu, kGroupWg, args, n_cu, s);
+}
+
+const void* group_kernel(uint32_t G, bool prof) {
+  switch (G) {
+    case 2: return prof ? (const void*)repair_group_kernel<2, true> : (const void*)repair_group_kernel<2, false>;
+    case 4: return prof ? (const void*)repair_group_kernel<4, true> : (const void*)repair_group_kernel<4, false>;
+    case 8: return prof ? (const void*)repair_group_kernel<8, true> : (const void*)repair_group_kernel<8, false>;
+    case 16: return prof ? (const void*)repair_group_kernel<16, true> : (const void*)repair_group_kernel<16, false>;
+    default: return nullptr;
+  }
 }
 
 // one launch, a workgroup per CU (every member of every team resident at
@@ -1619,13 +1730,6 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
     HIP_TRY(c, hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming));
   }
   HIP_TRY(c, p->d_cnt.alloc(8));
-  const size_t wt = p->wave_teams;
-  HIP_TRY(c, p->w_mark.alloc(wt * N));
-  HIP_TRY(c, p->w_dlist.alloc(wt * p->wave_cap));
-  HIP_TRY(c, p->w_dnew.alloc(wt * p->wave_cap));
-  HIP_TRY(c, p->w_nhn.alloc(wt * p->wave_cap * p->W));
-  HIP_TRY(c, p->w_lvl.alloc(wt * (p->wave_cap + 1)));
-  HIP_TRY(c, p->w_ord.alloc(wt * 2 * p->wave_cap));
   {  // workgroup teams: one per CU, two sets (b_*, c_*) within the scratch budget
     const size_t per_team = 4ull * ((size_t)N * (6 + p->W) + 1);
     p->big_teams = (uint32_t)std::max<size_t>(4, std::min<size_t>(c->n_cu, kBigScratch / 2 / per_team));
@@ -1645,6 +1749,36 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
       }
     }
   }
+  if (p->group) {
+    // The group teams' members must all be resident while the wave teams'
+    // blocks hold their CUs (launched beside them on the side stream; a
+    // member that cannot be placed stalls its team at every barrier).  Per
+    // SIMD: the wave teams' waves (one per 256-thread block) and the group
+    // workgroup's 2 waves share 512 VGPRs (granule 8).  Fewer wave teams per
+    // CU until both fit.  (Round 4's stamp pointer in the wave kernel --
+    // 75 -> 80+ VGPRs at 4 waves per SIMD beside 2 x 88 -- broke this sum.)
+    hipFuncAttributes fw{}, fg{};
+    const void* wk = std::getenv("SPF_WHATIF_PROF") ? (const void*)repair_wave_kernel<true>
+                                                    : (const void*)repair_wave_kernel<false>;
+    HIP_TRY(c, hipFuncGetAttributes(&fw, wk));
+    HIP_TRY(c, hipFuncGetAttributes(&fg, group_kernel(p->group, std::getenv("SPF_WHATIF_PROF") != nullptr)));
+    const auto gran = [](int r) { return (uint32_t)((std::max(r, 1) + 7) & ~7); };
+    const uint32_t per_simd_group = kGroupWg / 64 / 4;
+    const uint32_t vw = gran(fw.numRegs), vg = gran(fg.numRegs);
+    uint32_t per_simd_wave = (p->wave_teams + 4 * c->n_cu - 1) / (4 * c->n_cu);
+    while (per_simd_wave > 1 && per_simd_wave * vw + per_simd_group * vg > 512) --per_simd_wave;
+    p->wave_teams = std::min(p->wave_teams, per_simd_wave * 4 * c->n_cu);
+    if (std::getenv("SPF_WHATIF_DEBUG"))
+      std::fprintf(stderr, "whatif: wave kernel %d VGPRs, group<%u> %d VGPRs: %u wave teams (%u per SIMD)\n",
+                   fw.numRegs, p->group, fg.numRegs, p->wave_teams, per_simd_wave);
+  }
+  const size_t wt = p->wave_teams;
+  HIP_TRY(c, p->w_mark.alloc(wt * N));
+  HIP_TRY(c, p->w_dlist.alloc(wt * p->wave_cap));
+  HIP_TRY(c, p->w_dnew.alloc(wt * p->wave_cap));
+  HIP_TRY(c, p->w_nhn.alloc(wt * p->wave_cap * p->W));
+  HIP_TRY(c, p->w_lvl.alloc(wt * (p->wave_cap + 1)));
+  HIP_TRY(c, p->w_ord.alloc(wt * 2 * p->wave_cap));
   HIP_TRY(c, p->b_mark.alloc(bt * N));
   HIP_TRY(c, p->b_dlist.alloc(bt * N));
   HIP_TRY(c, p->b_dnew.alloc(bt * N));
@@ -1661,9 +1795,10 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   // marks start (and are always left) at kInf
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
-  if (std::getenv("SPF_WHATIF_PROF")) {
-    HIP_TRY(c, p->d_prof.alloc(16 * (bt + 1)));
-    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, 16 * (bt + 1) * 8, c->stream));
+  if (std::getenv("SPF_WHATIF_PROF")) {  // [bt teams][base][wave teams] x 16
+    const size_t slots = 16 * (bt + 1 + p->wave_teams);
+    HIP_TRY(c, p->d_prof.alloc(slots));
+    HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, slots * 8, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   p->epoch = c->epoch;
@@ -1756,35 +1891,63 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
       if (!grouped) (void)hipGetLastError();  // fall back to one-workgroup teams
       else if (const spf_status st = resident_done(c, side); st != SPF_OK) return st;
     }
-    if (!grouped)
-    hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, side, g, B,
-                       p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
-                       p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p);
+    if (!grouped) {
+      if (p->d_prof.p)
+        hipLaunchKernelGGL(repair_block_kernel<true>, dim3(p->big_teams), dim3(1024), 0, side, g, B,
+                           p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
+                           p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p);
+      else
+        hipLaunchKernelGGL(repair_block_kernel<false>, dim3(p->big_teams), dim3(1024), 0, side, g, B,
+                           p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
+                           p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, nullptr);
+    }
     HIP_TRY(c, hipGetLastError());
     if (c->side) HIP_TRY(c, hipEventRecord(c->side_join, c->side));
-    hipLaunchKernelGGL(repair_wave_kernel, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
-                       p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                       p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p, p->w_ord.p,
-                       d_out, p->wave_cap);
+    if (p->d_prof.p)
+      hipLaunchKernelGGL(repair_wave_kernel<true>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
+                         p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
+                         p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                         p->w_ord.p, d_out, p->wave_cap,
+                         p->d_prof.p + 16ull * (p->big_teams + 1));
+    else
+      hipLaunchKernelGGL(repair_wave_kernel<false>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
+                         p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
+                         p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                         p->w_ord.p, d_out, p->wave_cap, nullptr);
     HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(repair_block_kernel, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
+    hipLaunchKernelGGL(repair_block_kernel<false>, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
                        p->b_lvl.p, p->b_ord.p, d_out, nullptr);
     HIP_TRY(c, hipGetLastError());
     if (c->side) HIP_TRY(c, hipStreamWaitEvent(s, c->side_join, 0));
   }
-  if (p->d_prof.p) {  // diagnostics: phase times of the workgroup teams
-    std::vector<unsigned long long> h(16ull * (p->big_teams + 1));
+  if (p->d_prof.p) {  // diagnostics: phase ticks (100 MHz) per team, accumulated over repairs
+    const size_t bt = p->big_teams, wt = p->wave_teams;
+    std::vector<unsigned long long> h(16ull * (bt + 1 + wt));
     HIP_TRY(c, hipMemcpyAsync(h.data(), p->d_prof.p, h.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    for (uint32_t t = 0; t < p->big_teams; ++t) {
-      const unsigned long long* r = &h[16ull * t];
-      if (!r[8]) continue;
-      std::fprintf(stderr, "whatif team %u |D|=%llu levels=%llu bfs=%llu seeds=%llu dial=%llu "
-                   "fallback=%llu digest=%llu (x10ns)\n", t, r[8], r[9], (r[1] - r[0]) / 1,
-                   r[2] - r[1], r[3] - r[2], r[4] - r[3], r[5] - r[4]);
+    auto line = [&](const char* who, const unsigned long long* r) {
+      std::fprintf(stderr, "whatif %s repairs=%llu sum|D|=%llu max|D|=%llu dial_levels=%llu gave_up=%llu "
+                   "bfs=%llu seeds=%llu dial=%llu fallback=%llu digest=%llu (x10ns)\n", who, r[0], r[8],
+                   r[10], r[9], r[11], r[1], r[2], r[3], r[4], r[5]);
+    };
+    for (size_t t = 0; t < bt; ++t) {
+      const unsigned long long* r = &h[16 * t];
+      if (!r[0]) continue;
+      char who[32];
+      std::snprintf(who, sizeof who, "team %zu", t);
+      line(who, r);
     }
-    const unsigned long long* r = &h[16ull * p->big_teams];
+    std::vector<unsigned long long> sum(16, 0);  // the wave teams, summed
+    unsigned long long busiest = 0;
+    for (size_t t = 0; t < wt; ++t) {
+      const unsigned long long* r = &h[16 * (bt + 1 + t)];
+      for (int k = 0; k < 16; ++k) sum[k] = k == 10 ? std::max(sum[k], r[k]) : sum[k] + r[k];
+      busiest = std::max(busiest, r[1] + r[2] + r[3] + r[4] + r[5]);
+    }
+    line("wave-teams(sum)", sum.data());
+    std::fprintf(stderr, "whatif wave teams %zu, busiest team %llu ticks (x10ns)\n", wt, busiest);
+    const unsigned long long* r = &h[16 * bt];
     std::fprintf(stderr, "whatif base sssp=%llu nh=%llu hash=%llu (x10ns) maxd=%llu levels=%llu W=%u\n",
                  r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4], r[5], p->W);
   }
@@ -1885,6 +2048,16 @@ spf_status spf_device_check(spf_ctx* c) {
   HIP_TRY(c, hipMemcpy(&flag, c->d_fault.p, sizeof flag, hipMemcpyDeviceToHost));
   if (!flag) return SPF_OK;
   HIP_TRY(c, hipMemset(c->d_fault.p, 0, sizeof flag));
+  if (flag & 24u) {
+    // what-if repair diagnostics: a loop bound (bit 3, phase in bits 8-15) or
+    // a range check of the profiled instance (bit 4, site in bits 16-23)
+    return fail(c, SPF_E_HIP,
+                "what-if repair on device %d: %s%s (fault word 0x%08x: loop phase %u, check site %u); "
+                "the results of this context's launches since the last check are invalid",
+                c->device, (flag & 8u) ? "a repair loop reached its iteration bound " : "",
+                (flag & 16u) ? "a scratch index failed its range check" : "", flag, (flag >> 8) & 0xFFu,
+                (flag >> 16) & 0xFFu);
+  }
   if (flag & 2u) {
     // a team BFS gave up waiting for its members (another process's grid
     // held CUs): this context's plans stop using teams -- each re-derives

@@ -221,6 +221,10 @@ class Ksp2Plan(NativeHandle):
                                              C.c_void_p(d_link_hash), C.c_void_p(d_out),
                                              C.c_void_p(stream) if stream else None))
 
+    def chunk(self) -> int:
+        """Sources per KSP2 workgroup (spf_ksp2_plan_chunk)."""
+        return int(N.lib.spf_ksp2_plan_chunk(self._h))
+
     def enable_timing(self, max_executes: int) -> None:
         self._eng._err(N.lib.spf_ksp2_enable_timing(self._h, max_executes))
 
