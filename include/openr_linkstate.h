@@ -216,6 +216,16 @@ spf_status ls_link_set_overload(ls_link* link, const char* node, int overload,
  * run of b. */
 int ls_path_a_in_path_b(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb);
 
+/* Iteration order of a std::unordered_map<std::string, V> after emplacing
+ * keys[0..n) in that order (duplicates ignored, as emplace does):
+ * order[i] = the index in keys of the i-th key visited; *n_out = distinct
+ * keys.  SpfSolver walks its areaLinkStates map this way
+ * (Decision.cpp:411-412, 574-576, 1124, 1212), and with several areas that
+ * order decides ties (getNextHopsWithMetric's running shortest metric, the
+ * node-label entry of a node present in two areas). */
+spf_status ls_string_map_order(const char* const* keys, uint32_t n, uint32_t* order,
+                               uint32_t* n_out);
+
 /* HoldableValue<bool> / HoldableValue<LinkStateMetric> (LinkState.h:36-58,
  * LinkState.cpp:54-125). */
 typedef struct ls_holdable ls_holdable;

@@ -300,6 +300,7 @@ PROTOTYPES = {
     "ls_link_set_overload": (C.c_int, [_vp, C.c_char_p, C.c_int, C.c_uint64, C.c_uint64,
                                        C.POINTER(C.c_int)]),
     "ls_path_a_in_path_b": (C.c_int, [_u32p, C.c_uint32, _u32p, C.c_uint32]),
+    "ls_string_map_order": (C.c_int, [C.POINTER(C.c_char_p), C.c_uint32, _u32p, _u32p]),
     "ls_holdable_create": (_vp, [C.c_int, C.c_uint64]),
     "ls_holdable_destroy": (None, [_vp]),
     "ls_holdable_value": (C.c_uint64, [_vp]),

@@ -189,6 +189,8 @@ struct spf_plan {
   uint32_t tm_G = 0, tm_own = 0, tm_teams = 0, tm_bs = 0, tm_nacc = 0;
   uint32_t tm_rptr_at = 0, tm_runs_at = 0;  // d_tm_map = finalize slots | stream ranges | streams
   uint32_t tm_need_at = 0, tm_need_words = 0;  // ... | per-member frontier slice masks
+  uint32_t tm_drained_at = 0, tm_n_drained = 0;  // ... | the drained nodes
+  uint32_t tm_push_at = 0, tm_push_n = 0;  // ... | batch push offsets [tm_push_n] | push lists
   spfi::DevBuf<uint32_t> d_tm_map, d_tm_F, d_tm_bar;
   spfi::DevBuf<uint32_t> d_pl_order;
   spfi::DevBuf<uint32_t> d_redo;  // mp: rows whose u16 labels may have overflowed

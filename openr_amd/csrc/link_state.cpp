@@ -1451,6 +1451,20 @@ spf_status ls_link_set_overload(ls_link* l, const char* node, int overload, uint
 // LinkState::pathAInPathB (LinkState.h:395-410): a occurs in b as a contiguous
 // run of equal links (Link::operator==; link ids of one LinkState identify
 // links).
+spf_status ls_string_map_order(const char* const* keys, uint32_t n, uint32_t* order,
+                               uint32_t* n_out) {
+  if ((n && (!keys || !order)) || !n_out) return SPF_E_INVALID;
+  std::unordered_map<std::string, uint32_t> m;  // the same container as the reference's
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!keys[i]) return SPF_E_INVALID;
+    m.emplace(keys[i], i);
+  }
+  uint32_t k = 0;
+  for (const auto& kv : m) order[k++] = kv.second;
+  *n_out = k;
+  return SPF_OK;
+}
+
 int ls_path_a_in_path_b(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb) {
   if (na > nb) return 0;
   for (uint32_t i = 0; i < nb - na + 1; ++i) {

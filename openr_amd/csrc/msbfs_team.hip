@@ -38,6 +38,7 @@
 //  counters run on across batches, so flags and barriers need no reset.
 // ============================================================================
 #include "engine_internal.h"
+#include "wave_ops.h"
 
 #include <cstdio>
 
@@ -78,6 +79,10 @@ struct TeamArgs {
   const uint32_t* need;        // [G][need_words]: the 64-node frontier slices a member's stream reads
   uint32_t need_words;
   uint32_t* fault;  // the context's barrier-timeout word (spf_device_check)
+  const uint32_t* push_off;   // [n_batches + 1]: each batch's level-1 push list
+  const uint32_t* push;       // target | source bit << 24 over the batch's sources' CSR rows
+  const uint32_t* drained;  // the drained nodes (they keep no level-1 frontier bits)
+  uint32_t n_drained;
   uint32_t dbg;     // diagnostics (SPF_TEAM_FLUSH_DBG): bit 0 no u32 row stores, bit 1 no plane
                     // stores, bit 2 no flush at all, bit 3 no row padding, bit 4 no maxd
                     // atomic (the rows are then invalid)
@@ -265,6 +270,7 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
   };
 
   uint32_t L = 0;  // running level counter of the team (flags, buffers)
+  TM_STAMP();  // prologue done
   for (uint32_t batch = team; batch < a.n_batches; batch += n_teams) {
     const uint32_t row0 = batch * a.bs;
     const uint32_t nb = min(a.bs, a.n_rows - row0);
@@ -288,6 +294,47 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
 #pragma unroll
       for (int b = 0; b < kTmPlanes; ++b) P[i][b] = 0ull;
     }
+    __syncthreads();  // the self marks are read
+    if (tid < nb) Fl[src_l[tid]] = 0ull;
+    __syncthreads();
+    // ---- level 1 by push, by every member for the whole graph (no
+    // exchange): each source's bit ORed into its neighbours' entries, the
+    // batch's edges dealt over the workgroup, their loads independent.
+    // Links are up in both directions or neither, so the CSR out-neighbours
+    // are the in-neighbours a pull would read.  The first pull sweep, its
+    // hand-off and frontier copy are gone (msbfs_kernel pushes level 1 too) ----
+    // The batch's push list (target | source bit << 24, built at plan time
+    // from the closure's CSR rows) dealt over the workgroup, four entries
+    // per thread in flight before their LDS ORs.  (A thread per flat edge
+    // finding its source by binary search cost ~10 us on spine batches,
+    // a wave per source ~6, r05_t3 / r05_t4 stamps.)
+    TM_STAMP();  // level 0 done
+    const uint32_t p0 = a.push_off[batch], p1 = a.push_off[batch + 1];
+    const uint32_t n_e = p1 - p0;
+    for (uint32_t t = p0 + tid; t < p1; t += 4 * kTmThreads) {
+      uint32_t x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = t + q * kTmThreads < p1 ? a.push[t + q * kTmThreads] : ~0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (x[q] != ~0u)
+          atomicOr(reinterpret_cast<unsigned long long*>(&Fl[x[q] & 0xFFFFFFu]), 1ull << (x[q] >> 24));
+    }
+    __syncthreads();
+    // level 1 of the owned slices (drained nodes included: recorded, not expanded)
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const uint32_t v = sv[i] + lane;
+      const uint64_t nx = v < N && sv[i] < N ? Fl[v] & ~vis[i] : 0ull;
+      vis[i] |= nx;
+      P[i][0] |= nx;  // relative level 1: plane 0
+    }
+    TM_STAMP();  // push + level-1 finalize done
+    if (a.n_drained) {  // a drained node keeps no level-1 frontier bits
+      __syncthreads();  // every owned read of the pushed entries is done
+      for (uint32_t t = tid; t < a.n_drained; t += kTmThreads) Fl[a.drained[t]] = 0ull;
+    }
+    __syncthreads();
     // ---- write the window's distances: every (s, v) of the owned slices
     // in the first window (unreached = kInf), later only those found in it
     // (entries of earlier windows carry the marker kTmWindow in the planes) ----
@@ -396,8 +443,8 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
         }
       }
     };
-    uint32_t depth = 0;
-    for (uint32_t lvl = 1;; ++lvl) {
+    uint32_t depth = n_e ? 1u : 0u;
+    for (uint32_t lvl = 2; n_e; ++lvl) {
       ++L;
       unsigned long long* Fn = F0 + (size_t)(L & 1u) * fw;
       if (member == 0 && tid == 0)  // the word of level L + 1 (its last readers passed level L - 1)
@@ -688,6 +735,31 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
         }
     if (ne && ne[0] == '1') std::fill(need, need + (size_t)G * nw, ~0u);
   }
+  // the drained nodes (level 1 is pushed into every node's entry; these
+  // keep none of it as frontier)
+  p->tm_drained_at = (uint32_t)tab.size();
+  for (uint32_t v = 0; v < c->N; ++v)
+    if (c->ovl[v]) tab.push_back(v);
+  p->tm_n_drained = (uint32_t)tab.size() - p->tm_drained_at;
+  tab.push_back(0);  // never empty past the offset
+  {  // per batch: its sources' CSR rows as (target | bit << 24), the level-1 push
+    const uint32_t nbat = (rows + p->tm_bs - 1) / p->tm_bs;
+    p->tm_push_n = nbat + 1;
+    p->tm_push_at = (uint32_t)tab.size();
+    tab.resize(tab.size() + nbat + 1, 0u);
+    std::vector<uint32_t> lst;
+    for (uint32_t k = 0; k < nbat; ++k) {
+      tab[p->tm_push_at + k] = (uint32_t)lst.size();
+      for (uint32_t b = 0; b < p->tm_bs && k * p->tm_bs + b < rows; ++b) {
+        const uint32_t src = p->closure[k * p->tm_bs + b];
+        for (uint32_t e = c->row_ptr[src]; e < c->row_ptr[src + 1]; ++e) lst.push_back(c->col[e] | (b << 24));
+      }
+    }
+    tab[p->tm_push_at + nbat] = (uint32_t)lst.size();
+    if (c->N >= (1u << 24) || tab.size() + lst.size() >= (1ull << 32))
+      return fail(c, SPF_E_INVALID, "msbfs_team: push list exceeds its encoding");
+    tab.insert(tab.end(), lst.begin(), lst.end());
+  }
   HIP_TRY(c, p->d_tm_map.upload(tab.data(), tab.size(), c->stream));
   HIP_TRY(c, p->d_tm_F.alloc((size_t)teams * 2 * fw * 2));  // u64 as 2 words
   HIP_TRY(c, p->d_tm_bar.alloc((size_t)teams * kTmBarPad * 4));
@@ -713,7 +785,9 @@ spf_status launch_msbfs_team(spf_ctx* c, spf_plan* p, const uint32_t* rows_src, 
              (uint32_t)std::max<size_t>(8ull * fw, (size_t)kTmWaves * kTmRows * 80 * 4),
              (uint32_t)(4ull * c->sell_col.size()), d_rows, S, s_stride, D, Dn, maxd,
              reinterpret_cast<unsigned long long*>(p->d_tm_F.p), p->d_tm_bar.p, c->d_stamps.p,
-             p->d_tm_map.p + p->tm_need_at, p->tm_need_words, c->d_fault.p, 0u};
+             p->d_tm_map.p + p->tm_need_at, p->tm_need_words, c->d_fault.p,
+             p->d_tm_map.p + p->tm_push_at, p->d_tm_map.p + p->tm_push_at + p->tm_push_n,
+             p->d_tm_map.p + p->tm_drained_at, p->tm_n_drained, 0u};
   if (const char* e = std::getenv("SPF_TEAM_FLUSH_DBG")) a.dbg = (uint32_t)atoi(e);
   const uint32_t* meta = p->d_tm_map.p + p->tm_runs_at;
   const uint32_t blocks = p->tm_teams * p->tm_G;  // = n_cu: one persistent workgroup per CU

@@ -27,8 +27,22 @@ Covered, single area, over the MI355X engine:
   * addBestPaths (:1020-1080): min-nexthop threshold, static next hops of a
     self-advertised prefix with a prepend label.
 
-Not covered yet (raise NotImplementedError): multiple areas, BGP / best-route
-selection by PrefixMetrics.
+  * several areas (Decision.cpp:411-412, 556-722, 1107-1305): the areas
+    walked in the order of the reference's std::unordered_map<std::string,
+    LinkState> (ls_string_map_order), getMinCostNodes per area, ECMP across
+    areas at equal metric, LFA per area, next hops from every area's links;
+    node labels collected over every area;
+  * best-route selection (selectBestRoutes :728-748): openr routes (every
+    advertiser), enable_best_route_selection (selectBestPrefixMetrics /
+    selectBestNodeArea, openr/common/Util.h:486-571, Util.cpp:1028-1040) and
+    BGP metric vectors (runBestPathSelectionBgp :791-832 over
+    MetricVectorUtils::compareMetricVectors, Util.cpp:1101-1217), drained
+    advertisers filtered (maybeFilterDrainedNodes :766-789), the best-routes
+    cache, doNotInstall = BGP && bgpDryRun.
+
+One area takes the batched kernel path for SP_ECMP/IP prefixes and node
+labels; several areas take the reference's per-prefix walk over the memoised
+(GPU) SPF results of every area.
 """
 
 from __future__ import annotations
@@ -82,6 +96,34 @@ def createNextHop(addr: bytes, ifName: Optional[str], metric: int,
                          area, neighborNodeName)
 
 
+@dataclass(frozen=True)
+class PrefixMetrics:
+    """thrift::PrefixMetrics (Lsdb.thrift:228-268)."""
+
+    path_preference: int = 0    # prefer higher
+    source_preference: int = 0  # prefer higher
+    distance: int = 0           # prefer lower
+
+
+@dataclass
+class MetricEntity:
+    """thrift::MetricEntity (Lsdb.thrift:182-204); op is a CompareType name."""
+
+    type: int
+    priority: int
+    op: str = "WIN_IF_PRESENT"  # | "WIN_IF_NOT_PRESENT" | "IGNORE_IF_NOT_PRESENT"
+    isBestPathTieBreaker: bool = False
+    metric: Tuple[int, ...] = ()
+
+
+@dataclass
+class MetricVector:
+    """thrift::MetricVector (Lsdb.thrift:206-212)."""
+
+    version: int = 0
+    metrics: List[MetricEntity] = field(default_factory=list)
+
+
 @dataclass
 class PrefixEntry:
     """The fields of thrift::PrefixEntry (Lsdb.thrift) route building reads."""
@@ -92,6 +134,9 @@ class PrefixEntry:
     forwardingAlgorithm: str = "SP_ECMP"
     prependLabel: Optional[int] = None
     minNexthop: Optional[int] = None
+    metrics: PrefixMetrics = field(default_factory=PrefixMetrics)
+    mv: Optional[MetricVector] = None
+    data: Optional[bytes] = None
 
     @property
     def isV4(self) -> bool:
@@ -126,6 +171,14 @@ class RibUnicastEntry:
     bestArea: str
     doNotInstall: bool = False
 
+    @property
+    def prefixType(self) -> str:
+        return self.bestPrefixEntry.type
+
+    @property
+    def data(self) -> Optional[bytes]:
+        return self.bestPrefixEntry.data
+
 
 @dataclass
 class RibMplsEntry:
@@ -152,7 +205,7 @@ _FWD_ALGO = {"SP_ECMP": 0, "KSP2_ED_ECMP": 1}
 
 
 def getPrefixForwardingTypeAndAlgorithm(entries: Dict[Tuple[str, str], "PrefixEntry"],
-                                        best: Set[Tuple[str, str]]) -> Tuple[str, str]:
+                                        best) -> Tuple[str, str]:
     """openr/common/Util.cpp:617-643."""
     if not entries:
         return "IP", "SP_ECMP"
@@ -165,6 +218,159 @@ def getPrefixForwardingTypeAndAlgorithm(entries: Dict[Tuple[str, str], "PrefixEn
         if t == 0 and a == 0:
             break
     return ("IP", "SR_MPLS")[t], ("SP_ECMP", "KSP2_ED_ECMP")[a]
+
+
+# -- best-route selection helpers (openr/common/Util.h, Util.cpp) ------------------
+NodeAndArea = Tuple[str, str]
+WINNER, TIE_WINNER, TIE, TIE_LOOSER, LOOSER, ERROR = range(6)  # MetricVectorUtils::CompareResult
+
+
+def _not(r: int) -> int:
+    """MetricVectorUtils::operator! (Util.cpp:1074-1096)."""
+    return {WINNER: LOOSER, TIE_WINNER: TIE_LOOSER, TIE: TIE, TIE_LOOSER: TIE_WINNER,
+            LOOSER: WINNER, ERROR: ERROR}[r]
+
+
+def _isDecisive(r: int) -> bool:
+    return r in (WINNER, LOOSER, ERROR)
+
+
+def _compareMetrics(l: Sequence[int], r: Sequence[int], tieBreaker: bool) -> int:
+    """MetricVectorUtils::compareMetrics (Util.cpp:1135-1151)."""
+    if len(l) != len(r):
+        return ERROR
+    for a, b in zip(l, r):
+        if a > b:
+            return TIE_WINNER if tieBreaker else WINNER
+        if a < b:
+            return TIE_LOOSER if tieBreaker else LOOSER
+    return TIE
+
+
+def _resultForLoner(e: MetricEntity) -> int:
+    """MetricVectorUtils::resultForLoner (Util.cpp:1153-1164)."""
+    if e.op == "WIN_IF_PRESENT":
+        return TIE_WINNER if e.isBestPathTieBreaker else WINNER
+    if e.op == "WIN_IF_NOT_PRESENT":
+        return TIE_LOOSER if e.isBestPathTieBreaker else LOOSER
+    return TIE  # IGNORE_IF_NOT_PRESENT
+
+
+def maybeUpdate(target: int, update: int) -> int:
+    """MetricVectorUtils::maybeUpdate (Util.cpp:1166-1171), returning the new target."""
+    return update if (_isDecisive(update) or target == TIE) else target
+
+
+compareMetrics = _compareMetrics
+resultForLoner = _resultForLoner
+isDecisive = _isDecisive
+inverse = _not
+
+
+def compareMetricVectors(l: MetricVector, r: MetricVector) -> int:
+    """MetricVectorUtils::compareMetricVectors (Util.cpp:1173-1216).  Like
+    sortMetricVector (:1120-1133, a const_cast sort) it puts an unsorted
+    vector's entities in decreasing priority IN PLACE -- callers see their
+    vectors reordered, as the reference's do.  (std::sort is not stable; a
+    stable sort here, so equal priorities keep their order.)"""
+    result = TIE
+
+    def upd(u: int) -> None:
+        nonlocal result
+        if _isDecisive(u) or result == TIE:
+            result = u
+
+    if l.version != r.version:
+        return ERROR
+
+    def srt(mv: MetricVector) -> List[MetricEntity]:
+        pr = [e.priority for e in mv.metrics]
+        if any(pr[i] < pr[i + 1] for i in range(len(pr) - 1)):
+            mv.metrics.sort(key=lambda e: -e.priority)
+        return mv.metrics
+
+    L, R = srt(l), srt(r)
+    i = j = 0
+    while not _isDecisive(result) and i < len(L) and j < len(R):
+        a, b = L[i], R[j]
+        if a.type == b.type:
+            if a.isBestPathTieBreaker != b.isBestPathTieBreaker:
+                upd(ERROR)
+            else:
+                upd(_compareMetrics(a.metric, b.metric, a.isBestPathTieBreaker))
+            i += 1
+            j += 1
+        elif a.priority > b.priority:
+            upd(_resultForLoner(a))
+            i += 1
+        elif a.priority < b.priority:
+            upd(_not(_resultForLoner(b)))
+            j += 1
+        else:
+            upd(ERROR)  # same priority, different types
+    while not _isDecisive(result) and i < len(L):
+        upd(_resultForLoner(L[i]))
+        i += 1
+    while not _isDecisive(result) and j < len(R):
+        upd(_not(_resultForLoner(R[j])))
+        j += 1
+    return result
+
+
+def selectBestPrefixMetrics(entries: Dict[NodeAndArea, PrefixEntry]) -> List[NodeAndArea]:
+    """openr/common/Util.h:540-571: the keys with the best (path_preference,
+    source_preference, -distance) tuple, starting from (0, 0, 0) -- so entries
+    below it never enter (a positive distance with zero preferences); a
+    std::set, here a sorted list."""
+    best_t = (0, 0, 0)
+    best: List[NodeAndArea] = []
+    for key, e in entries.items():
+        m = e.metrics
+        t = (m.path_preference, m.source_preference, -m.distance)
+        if t < best_t:
+            continue
+        if t > best_t:
+            best_t, best = t, []
+        best.append(key)
+    return sorted(best)
+
+
+def selectBestNodeArea(allNodeAreas: Sequence[NodeAndArea], myNodeName: str) -> NodeAndArea:
+    """openr/common/Util.cpp:1028-1040: our own entry if we are among them,
+    else the smallest."""
+    for na in allNodeAreas:
+        if na[0] == myNodeName:
+            return na
+    return allNodeAreas[0]
+
+
+@dataclass
+class BestRouteSelectionResult:
+    """openr/decision/RibEntry.h BestRouteSelectionResult; allNodeAreas is a
+    std::set (sorted list here)."""
+
+    success: bool = False
+    allNodeAreas: List[NodeAndArea] = field(default_factory=list)
+    bestNodeArea: Optional[NodeAndArea] = None
+
+    def hasNode(self, node: str) -> bool:
+        return any(na[0] == node for na in self.allNodeAreas)
+
+
+def areaOrder(areaLinkStates: Dict[str, LinkState]) -> List[Tuple[str, LinkState]]:
+    """The areas in the iteration order of the reference's
+    std::unordered_map<std::string, LinkState> when the dict's keys were
+    emplaced in insertion order (ls_string_map_order)."""
+    keys = list(areaLinkStates)
+    if len(keys) <= 1:
+        return list(areaLinkStates.items())
+    arr = (C.c_char_p * len(keys))(*[k.encode() for k in keys])
+    order = (C.c_uint32 * len(keys))()
+    n = C.c_uint32()
+    st = N.lib.ls_string_map_order(arr, len(keys), order, C.byref(n))
+    if st != N.SPF_OK:
+        N.raise_for(st, "ls_string_map_order")
+    return [(keys[order[i]], areaLinkStates[keys[order[i]]]) for i in range(n.value)]
 
 
 @dataclass
@@ -184,8 +390,16 @@ class SpfSolver:
         self.computeLfaPaths = computeLfaPaths
         self.bgpDryRun = bgpDryRun
         self.staticMplsRoutes: Dict[int, List[NextHopThrift]] = {}
-        if enableBestRouteSelection:
-            raise NotImplementedError("best route selection by PrefixMetrics")
+        self.enableBestRouteSelection = enableBestRouteSelection
+        self._bestRoutesCache: Dict[str, BestRouteSelectionResult] = {}
+        self.counters: Dict[str, int] = {}  # the fb303 stats SpfSolver bumps (subset)
+
+    def getBestRoutesCache(self) -> Dict[str, BestRouteSelectionResult]:
+        """SpfSolver::getBestRoutesCache: the last route build's selections."""
+        return dict(self._bestRoutesCache)
+
+    def _bump(self, key: str) -> None:
+        self.counters[key] = self.counters.get(key, 0) + 1
 
     def updateStaticMplsRoutes(self, routesToUpdate: Dict[int, List[NextHopThrift]],
                                routesToDelete: Sequence[int] = ()) -> None:
@@ -357,9 +571,9 @@ class SpfSolver:
         return out
 
     # -- addBestPaths (Decision.cpp:1020-1080) ---------------------------------------
-    def _addBestPaths(self, me: str, prefix: str, best: List[Tuple[str, str]],
+    def _addBestPaths(self, me: str, prefix: str, best: Sequence[Tuple[str, str]],
                       bestNA: Tuple[str, str], ents: Dict[Tuple[str, str], PrefixEntry],
-                      nhs: Set[NextHopThrift]) -> Optional[RibUnicastEntry]:
+                      nhs: Set[NextHopThrift], isBgp: bool = False) -> Optional[RibUnicastEntry]:
         need = None
         for na in best:  # getMinNextHopThreshold: the largest minNexthop
             m = ents[na].minNexthop
@@ -368,57 +582,329 @@ class SpfSolver:
         if need is not None and need > len(nhs):
             return None  # min-nexthop requirement not met
         if any(na[0] == me for na in best):
-            prepend = next((e.prependLabel for na, e in ents.items()
+            prepend = next((e.prependLabel for na, e in sorted(ents.items())
                             if na[0] == me and e.prependLabel is not None), None)
             assert prepend is not None, "self route must carry a prepend label"
             nhs = set(nhs)
             for nh in self.staticMplsRoutes.get(prepend, []):
                 nhs.add(createNextHop(nh.address, None, 0, None))
-        return RibUnicastEntry(prefix, nhs, ents[bestNA], bestNA[1])
+        return RibUnicastEntry(prefix, nhs, ents[bestNA], bestNA[1], isBgp and self.bgpDryRun)
+
+    # -- best-route selection (Decision.cpp:728-832) ---------------------------------
+    def _maybeFilterDrainedNodes(self, res: BestRouteSelectionResult,
+                                 areaLinkStates: Dict[str, LinkState]) -> BestRouteSelectionResult:
+        """:766-789 -- the filtered copy keeps the unfiltered bestNodeArea (its
+        `filtered.bestNodeArea != result.bestNodeArea` test compares a copy
+        with its source)."""
+        kept = [na for na in res.allNodeAreas
+                if not areaLinkStates[na[1]].isNodeOverloaded(na[0])]
+        if not kept:
+            return res
+        return BestRouteSelectionResult(res.success, kept, res.bestNodeArea)
+
+    def _runBestPathSelectionBgp(self, ents: Dict[Tuple[str, str], PrefixEntry],
+                                 areaLinkStates: Dict[str, LinkState]) -> BestRouteSelectionResult:
+        """:791-832.  The reference walks its std::unordered_map of entries;
+        here ascending (node, area) -- the outcome differs only where a tie
+        chain's result depends on the visit order."""
+        ret = BestRouteSelectionResult()
+        bestVector: Optional[MetricVector] = None
+        chosen: List[Tuple[str, str]] = []
+        for na in sorted(ents):
+            mv = ents[na].mv
+            r = WINNER if bestVector is None else compareMetricVectors(mv, bestVector)
+            if r == WINNER:
+                chosen = []
+            if r in (WINNER, TIE_WINNER):
+                bestVector = mv
+                ret.bestNodeArea = na
+            if r in (WINNER, TIE_WINNER, TIE_LOOSER):
+                chosen.append(na)
+            elif r in (TIE, ERROR):
+                ret.allNodeAreas = sorted(chosen)
+                return ret  # tie / error ordering the entries: no route
+        ret.allNodeAreas = sorted(chosen)
+        ret.success = True
+        return self._maybeFilterDrainedNodes(ret, areaLinkStates)
+
+    def _selectBestRoutes(self, me: str, ents: Dict[Tuple[str, str], PrefixEntry], isBgp: bool,
+                          areaLinkStates: Dict[str, LinkState]) -> BestRouteSelectionResult:
+        if self.enableBestRouteSelection:
+            best = selectBestPrefixMetrics(ents)
+            ret = BestRouteSelectionResult(True, best, selectBestNodeArea(best, me) if best else None)
+        elif isBgp:
+            ret = self._runBestPathSelectionBgp(ents, areaLinkStates)
+        else:  # openr routes: every advertiser is best
+            best = sorted(ents)
+            ret = BestRouteSelectionResult(True, best, best[0])
+        return self._maybeFilterDrainedNodes(ret, areaLinkStates)
+
+    # -- several areas: the reference's per-prefix walk (Decision.cpp:1082-1305) ------
+    _INF = (1 << 64) - 1
+
+    @staticmethod
+    def _getMinCostNodes(spf, dstNodeAreas) -> Tuple[int, Set[str]]:
+        """:1082-1105 (the destination's area is not checked: a node of the
+        set reached in any area counts)."""
+        shortest, nodes = SpfSolver._INF, set()
+        for d, _ in sorted(dstNodeAreas):
+            if d not in spf:
+                continue
+            m = spf[d].metric()
+            if shortest >= m:
+                if shortest > m:
+                    shortest, nodes = m, set()
+                nodes.add(d)
+        return shortest, nodes
+
+    def _getNextHopsWithMetric(self, me: str, dstNodeAreas, perDestination: bool,
+                               areas: List[Tuple[str, LinkState]]):
+        """:1107-1196 over the areas in the reference's map order."""
+        M = self._INF
+        nh: Dict[Tuple[str, str], int] = {}
+        shortest = M
+        for area, ls in areas:
+            here = ls.getSpfResult(me)
+            mcm, mc = self._getMinCostNodes(here, dstNodeAreas)
+            if shortest < mcm:
+                continue
+            if shortest > mcm:
+                shortest = mcm
+                nh.clear()
+            if not mc:
+                continue
+            for d in mc:
+                ref = d if perDestination else ""
+                for hop in here[d].nextHops():
+                    nh[(hop, ref)] = (shortest - ls.getMetricFromAToB(me, hop)) & M
+            if self.computeLfaPaths:
+                for link in ls.linksFromNode(me):
+                    if not link.isUp():
+                        continue
+                    nb = link.getOtherNodeName(me)
+                    fromNb = ls.getSpfResult(nb)
+                    nbToHere = fromNb[me].metric()
+                    for d, dArea in sorted(dstNodeAreas):
+                        if area != dArea or d not in fromNb:
+                            continue
+                        dn = fromNb[d].metric()
+                        if dn < ((shortest + nbToHere) & M):  # RFC 5286 (:1180)
+                            key = (nb, d if perDestination else "")
+                            if key not in nh or nh[key] > dn:
+                                nh[key] = dn
+        return shortest, nh
+
+    def _getNextHopsThrift(self, me: str, dstNodeAreas, isV4: bool, perDestination: bool,
+                           minMetric: int, nextHopNodes: Dict[Tuple[str, str], int],
+                           swapLabel: Optional[int], areas: List[Tuple[str, LinkState]],
+                           ents: Dict[Tuple[str, str], PrefixEntry]) -> Set[NextHopThrift]:
+        """:1198-1305 over every area's links."""
+        M = self._INF
+        dsts = sorted(dstNodeAreas) if perDestination else [("", "")]
+        dstSet = set(dstNodeAreas)
+        out: Set[NextHopThrift] = set()
+        for area, ls in areas:
+            labels = ls.getAdjacencyDatabaseLabels() if perDestination else {}
+            for link in ls.linksFromNode(me):
+                nb = link.getOtherNodeName(me)
+                for d, dArea in dsts:
+                    if dArea and area != dArea:
+                        continue
+                    via = nextHopNodes.get((nb, d))
+                    if via is None or not link.isUp():
+                        continue
+                    if d and (nb, area) in dstSet and nb != d:
+                        continue
+                    over = (link.getMetricFromNode(me) + via) & M
+                    if not self.computeLfaPaths and over != minMetric:
+                        continue
+                    action = None
+                    if swapLabel is not None:
+                        action = (MplsAction("PHP") if (nb, area) in dstSet
+                                  else MplsAction("SWAP", swapLabel))
+                    if d:
+                        push: List[int] = []
+                        pe = ents[(d, area)]
+                        if pe.prependLabel is not None:
+                            push.append(pe.prependLabel)
+                            if not isMplsLabelValid(push[-1]):
+                                continue
+                        if d != nb:
+                            push.append(labels[d])  # getAdjacencyDatabases().at(dstNode)
+                            if not isMplsLabelValid(push[-1]):
+                                continue
+                        if push:
+                            action = MplsAction("PUSH", None, tuple(push))
+                    addr = link.getNhV4FromNode(me) if isV4 else link.getNhV6FromNode(me)
+                    out.add(createNextHop(addr, link.getIfaceFromNode(me), over, action,
+                                          link.getArea(), nb))
+        return out
+
+    def _selectBestPathsSpf(self, me: str, prefix: str, res: BestRouteSelectionResult,
+                            ents: Dict[Tuple[str, str], PrefixEntry], isBgp: bool, ftype: str,
+                            areas: List[Tuple[str, LinkState]]) -> Optional[RibUnicastEntry]:
+        """:834-893."""
+        isV4 = next(iter(ents.values())).isV4
+        perDest = ftype == "SR_MPLS"
+        filtered = list(res.allNodeAreas)
+        if res.hasNode(me) and perDest:
+            for na, e in sorted(ents.items()):
+                if na[0] == me and e.prependLabel is not None:
+                    if na in filtered:
+                        filtered.remove(na)
+                    break
+        mn, nhn = self._getNextHopsWithMetric(me, filtered, perDest, areas)
+        if not nhn:
+            self._bump("decision.no_route_to_prefix")
+            return None
+        nhs = self._getNextHopsThrift(me, res.allNodeAreas, isV4, perDest, mn, nhn, None, areas, ents)
+        return self._addBestPaths(me, prefix, res.allNodeAreas, res.bestNodeArea, ents, nhs, isBgp)
+
+    def _selectBestPathsKsp2(self, me: str, prefix: str, res: BestRouteSelectionResult,
+                             ents: Dict[Tuple[str, str], PrefixEntry], isBgp: bool, ftype: str,
+                             areas: List[Tuple[str, LinkState]]) -> Optional[RibUnicastEntry]:
+        """:895-1018, every area's k = 1 / k = 2 paths (a path's label stack
+        and next hop are made once per area, as the reference does)."""
+        if ftype != "SR_MPLS":
+            self._bump("decision.incompatible_forwarding_type")
+            return None
+        paths = []
+        for area, ls in areas:
+            for node, bestArea in res.allNodeAreas:
+                if node == me and bestArea == area:
+                    continue
+                paths.extend(ls.getKthPaths(me, node, 1))
+            first = len(paths)
+            for node, bestArea in res.allNodeAreas:
+                if area != bestArea:
+                    continue
+                for sec in ls.getKthPaths(me, node, 2):
+                    if not any(LinkState.pathAInPathB(paths[i], sec) for i in range(first)):
+                        paths.append(sec)
+        if not paths:
+            return None
+        isV4 = next(iter(ents.values())).isV4
+        out: Set[NextHopThrift] = set()
+        for path in paths:
+            for area, ls in areas:
+                labels = ls.getAdjacencyDatabaseLabels()
+                cost, stack, nxt = 0, deque(), me
+                for link in path:
+                    cost += link.getMetricFromNode(nxt)
+                    nxt = link.getOtherNodeName(nxt)
+                    stack.appendleft(labels[nxt])
+                stack.pop()  # the first hop's label: PHP
+                pe = ents[(nxt, area)]
+                if pe.prependLabel is not None:
+                    stack.appendleft(pe.prependLabel)
+                head = path[0]
+                action = MplsAction("PUSH", None, tuple(stack)) if stack else None
+                addr = head.getNhV4FromNode(me) if isV4 else head.getNhV6FromNode(me)
+                out.add(createNextHop(addr, head.getIfaceFromNode(me), cost, action,
+                                      head.getArea(), head.getOtherNodeName(me)))
+        return self._addBestPaths(me, prefix, res.allNodeAreas, res.bestNodeArea, ents, out, isBgp)
 
     # -- buildRouteDb (Decision.cpp:557-722) ----------------------------------------
     def buildRouteDb(self, myNodeName: str, areaLinkStates: Dict[str, LinkState],
-                     prefixState: PrefixState) -> Optional[DecisionRouteDb]:
-        if len(areaLinkStates) != 1:
-            raise NotImplementedError("multi-area route computation")
-        (area, ls), = areaLinkStates.items()
-        if not ls.hasNode(myNodeName):
+                     prefixState: PrefixState, _generic: bool = False) -> Optional[DecisionRouteDb]:
+        """``_generic`` (tests): take the several-area walk with one area too."""
+        areas = areaOrder(areaLinkStates)
+        if not any(ls.hasNode(myNodeName) for _, ls in areas):
             return None
         me = myNodeName
         db = DecisionRouteDb()
-        mine = ls.getSpfResult(me)  # memoised: reachability for prefix filtering
+        self._bestRoutesCache = {}
+        single = len(areas) == 1 and not _generic
+        mine = {area: ls.getSpfResult(me) for area, ls in areas}  # memoised
 
-        # ---- unicast: destination set per prefix (createRouteForPrefix) ----
-        labels = ls.getAdjacencyDatabaseLabels()
-        uni: List[Tuple[str, Dict[Tuple[str, str], PrefixEntry], List[str], Tuple[str, str]]] = []
-        sr: List[Tuple[str, Dict[Tuple[str, str], PrefixEntry], List[Tuple[str, str]],
-                       Tuple[str, str], str]] = []
+        # ---- unicast: createRouteForPrefix (:390-555) ----
+        uni: List[tuple] = []
+        sr: List[tuple] = []
         for prefix, entries in prefixState.prefixes().items():
-            ents = {na: e for na, e in entries.items() if na[1] == area and na[0] in mine}
+            # entries of nodes unreachable in their own area are dropped
+            ents = {na: e for na, e in entries.items()
+                    if na[1] not in mine or na[0] in mine[na[1]]}
             if not ents:
-                continue  # no reachable advertiser
+                self._bump("decision.no_route_to_prefix")
+                continue
             isV4 = next(iter(ents.values())).isV4
             if isV4 and not self.enableV4:
+                self._bump("decision.skipped_unicast_route")
                 continue
-            if any(e.type == "BGP" for e in ents.values()):
-                raise NotImplementedError("BGP prefixes / metric-vector selection")
-            # openr routes: every advertiser is best (selectBestRoutes), the
-            # best node-area the first of them; drop drained ones unless all
-            # are (maybeFilterDrainedNodes :766-789 -- which keeps the
-            # unfiltered bestNodeArea)
-            allNA = sorted(ents)
-            bestNA = allNA[0]
-            best = [na for na in allNA if not ls.isNodeOverloaded(na[0])] or allNA
+            hasBGP = any(e.type == "BGP" for e in ents.values())
+            hasNonBGP = any(e.type != "BGP" for e in ents.values())
+            missingMv = any(e.type == "BGP" and e.mv is None for e in ents.values())
             hasSelfPrepend = all(e.prependLabel is not None
                                  for na, e in ents.items() if na[0] == me)
-            if any(na[0] == me for na in best) and not hasSelfPrepend:
+            if hasBGP and ((hasNonBGP and not self.enableBestRouteSelection) or missingMv):
+                self._bump("decision.skipped_unicast_route")
+                continue
+            res = self._selectBestRoutes(me, ents, hasBGP, areaLinkStates)
+            if not res.success:
+                continue
+            if not res.allNodeAreas:
+                self._bump("decision.no_route_to_prefix")
+                continue
+            self._bestRoutesCache[prefix] = res
+            if res.hasNode(me) and not hasSelfPrepend:
                 continue  # self-advertised
-            ftype, falgo = getPrefixForwardingTypeAndAlgorithm(ents, set(best))
-            if falgo == "SP_ECMP" and ftype == "IP":
-                uni.append((prefix, ents, [na[0] for na in best], bestNA))
+            ftype, falgo = getPrefixForwardingTypeAndAlgorithm(ents, set(res.allNodeAreas))
+            if not single:
+                r = (self._selectBestPathsSpf if falgo == "SP_ECMP" else self._selectBestPathsKsp2)(
+                    me, prefix, res, ents, hasBGP, ftype, areas)
+                if r is not None:
+                    db.addUnicastRoute(r)
+            elif falgo == "SP_ECMP" and ftype == "IP":
+                uni.append((prefix, ents, [na[0] for na in res.allNodeAreas], res, hasBGP))
             else:
-                sr.append((prefix, ents, best, bestNA, falgo))
+                sr.append((prefix, ents, res, falgo, hasBGP))
 
+        if single:
+            self._buildSingleArea(me, areas[0][0], areas[0][1], db, uni, sr)
+        else:
+            # ---- node labels over every area (:583-664) ----
+            labelToNode: Dict[int, Tuple[str, RibMplsEntry]] = {}
+            for area, ls in areas:
+                for node, top in ls.getAdjacencyDatabaseLabels().items():
+                    if top == 0 or not isMplsLabelValid(top):
+                        continue
+                    cur = labelToNode.get(top)
+                    if cur is not None and cur[0] < node:
+                        continue
+                    if node == me:
+                        labelToNode[top] = (node, RibMplsEntry(top, {NextHopThrift(
+                            bytes(16), None, 0, MplsAction("POP_AND_LOOKUP"), area, None)}))
+                        continue
+                    mn, nhn = self._getNextHopsWithMetric(me, [(node, area)], False, areas)
+                    if not nhn:
+                        self._bump("decision.no_route_to_label")
+                        continue
+                    labelToNode[top] = (node, RibMplsEntry(top, self._getNextHopsThrift(
+                        me, [(node, area)], False, False, mn, nhn, top, areas, {})))
+            for _, entry in labelToNode.values():
+                db.addMplsRoute(entry)
+
+        # ---- adjacency labels of every area (:667-698) ----
+        for _, ls in areas:
+            for link in ls.linksFromNode(me):
+                top = link.getAdjLabelFromNode(me)
+                if top == 0 or not isMplsLabelValid(top):
+                    continue
+                db.addMplsRoute(RibMplsEntry(top, {createNextHop(
+                    link.getNhV6FromNode(me), link.getIfaceFromNode(me),
+                    link.getMetricFromNode(me), MplsAction("PHP"), link.getArea(),
+                    link.getOtherNodeName(me))}))
+        # ---- static MPLS routes (:700-707) ----
+        for top, nhs in self.staticMplsRoutes.items():
+            db.addMplsRoute(RibMplsEntry(top, set(nhs)))
+        return db
+
+    def _buildSingleArea(self, me: str, area: str, ls: LinkState, db: DecisionRouteDb,
+                         uni: List[tuple], sr: List[tuple]) -> None:
+        """One area: every SP_ECMP/IP prefix and node label in ONE batched
+        kernel call (spf_routes), SR_MPLS prefixes over the memoised SPF /
+        one batched KSP2 launch."""
+        labels = ls.getAdjacencyDatabaseLabels()
         # ---- node labels (collisions: Decision.cpp:605-617) ----
         label_to_node: Dict[int, str] = {}
         for node, label in labels.items():
@@ -429,55 +915,49 @@ class SpfSolver:
                 continue
             label_to_node[label] = node
 
-        sets = [dsts for _, _, dsts, _ in uni] + [[n] for n in label_to_node.values()]
+        sets = [dsts for _, _, dsts, _, _ in uni] + [[n] for n in label_to_node.values()]
         sel = self._select(ls, me, sets)
 
-        for (prefix, ents, dsts, bestNA), res in zip(uni, sel[: len(uni)]):
-            if not res.hops:
-                continue  # no route to prefix
+        for (prefix, ents, dsts, res, isBgp), r_ in zip(uni, sel[: len(uni)]):
+            if not r_.hops:
+                self._bump("decision.no_route_to_prefix")
+                continue
             isV4 = next(iter(ents.values())).isV4
-            nhs = self._next_hops(ls, me, area, res, isV4, set(dsts), None)
-            r = self._addBestPaths(me, prefix, [(d, area) for d in dsts], bestNA, ents, nhs)
+            nhs = self._next_hops(ls, me, area, r_, isV4, set(dsts), None)
+            r = self._addBestPaths(me, prefix, res.allNodeAreas, res.bestNodeArea, ents, nhs, isBgp)
             if r is not None:
                 db.addUnicastRoute(r)
 
         # ---- SR_MPLS prefixes: per-destination SP_ECMP or KSP2_ED_ECMP ----
-        if any(falgo == "KSP2_ED_ECMP" for *_, falgo in sr):
+        if any(falgo == "KSP2_ED_ECMP" for *_, falgo, _ in sr):
             ls.prefetchKthPaths(me)  # one batched KSP2 launch for every advertiser
-        for prefix, ents, best, bestNA, falgo in sr:
+        for prefix, ents, res, falgo, isBgp in sr:
+            best = list(res.allNodeAreas)
             isV4 = next(iter(ents.values())).isV4
             if falgo == "KSP2_ED_ECMP":
                 if any(ents[na].forwardingType != "SR_MPLS" for na in best):
+                    self._bump("decision.incompatible_forwarding_type")
                     continue  # incompatible forwarding type (Decision.cpp:905-913)
                 nhs = self._ksp2NextHops(ls, me, area, best, ents, isV4, labels)
             else:
                 nhs = self._srSpfNextHops(ls, me, area, best, ents, isV4, labels)
             if not nhs:
-                continue  # no route to prefix
-            r = self._addBestPaths(me, prefix, best, bestNA, ents, nhs)
+                self._bump("decision.no_route_to_prefix")
+                continue
+            r = self._addBestPaths(me, prefix, best, res.bestNodeArea, ents, nhs, isBgp)
             if r is not None:
                 db.addUnicastRoute(r)
 
-        for (label, node), res in zip(label_to_node.items(), sel[len(uni):]):
+        for (label, node), r_ in zip(label_to_node.items(), sel[len(uni):]):
             if node == me:
                 db.addMplsRoute(RibMplsEntry(label, {NextHopThrift(
                     bytes(16), None, 0, MplsAction("POP_AND_LOOKUP"), area, None)}))
                 continue
-            if not res.hops:
-                continue  # no route to node label
-            db.addMplsRoute(RibMplsEntry(label, self._next_hops(
-                ls, me, area, res, False, {node}, label)))
-
-        # ---- adjacency labels (Decision.cpp:682-707) ----
-        for link in ls.linksFromNode(me):
-            top = link.getAdjLabelFromNode(me)
-            if top == 0 or not isMplsLabelValid(top):
+            if not r_.hops:
+                self._bump("decision.no_route_to_label")
                 continue
-            db.addMplsRoute(RibMplsEntry(top, {createNextHop(
-                link.getNhV6FromNode(me), link.getIfaceFromNode(me),
-                link.getMetricFromNode(me), MplsAction("PHP"), link.getArea(),
-                link.getOtherNodeName(me))}))
-        return db
+            db.addMplsRoute(RibMplsEntry(label, self._next_hops(
+                ls, me, area, r_, False, {node}, label)))
 
     def getNextHops(self, ls: LinkState, me: str, dsts: Sequence[str], isV4: bool = False,
                     swapLabel: Optional[int] = None) -> Tuple[Optional[int], Set[NextHopThrift]]:
