@@ -914,9 +914,190 @@ class FacadeLfa:
                           f"({dt:.1f} s on 1 core of {cpu_model()}; oracle/spf_oracle.cpp)"}
 
 
+class RoutesAllNodes:
+    """CS-2 (SURVEY.md): Decision::getDecisionRouteDb(node) for EVERY node
+    (Decision.cpp:1480-1500, `breeze decision routes --nodes all`) on the
+    10k fabric, every node advertising a loopback: per step one all-sources
+    pass on the GPU (LinkState.prefetchAllSources, rows and bitmaps resident)
+    and every node's route selection towards every loopback with LFA
+    (getNextHopsWithMetric + getNextHopsThrift, Decision.cpp:1082-1305) from
+    the resident rows (spf_mplan_route_digests), reduced to a digest per
+    node on the GPU -- no per-node SPF, no host round trip per node.  Thrift
+    formatting of the 100M routes is not in the step.  value = route
+    databases (nodes) per second."""
+
+    scaling = "replicas"
+    unit = "route_dbs/s"
+    kernels = ("allsources", "routes")
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        from openr_amd import topology as T
+        from openr_amd.link_state import LinkState
+
+        self.topo = T.fabric(10000, full=True)
+        self.lfa = os.environ.get("BENCH_ROUTES_LFA", "1") != "0"
+        self.desc = ("fabric_full numOfSws=10000, a loopback per node; per step: all-sources SPF "
+                     "(resident) + every node's route selection towards every loopback"
+                     + (" with LFA" if self.lfa else "") + " (Decision.cpp:1082-1305)")
+        self.ls = LinkState(devices=[dev.index])
+        self.ls.updateAdjacencyDatabases(self.topo.lsdb)
+        names = self.ls.flatten()[0]
+        self.names = list(names)
+        self.n, self.e = len(names), len(self.ls.flatten()[2])
+        self.set_ptr = np.arange(self.n + 1, dtype=np.uint32)
+        self.set_nodes = np.arange(self.n, dtype=np.uint32)
+        self.ls.prefetchAllSources()
+        self.ls.linkValueHashes()  # cached: the digests' link identities
+        self.units = self.n
+        self.world = world
+        self.kernel_bytes = {"allsources": 1, "routes": 1}
+        self.survey_bytes = 0
+        self.parallelism = "one LinkState per process (replicas); all sources resident on its GPU"
+        self.t_pass, self.t_routes = [], []
+        self.digests = None
+
+    def step(self) -> None:
+        t0 = time.perf_counter()
+        self.ls.prefetchAllSources()  # execute + synchronize
+        t1 = time.perf_counter()
+        self.digests, kms = self.ls.allSourcesRouteDigests(self.set_ptr, self.set_nodes, self.lfa)
+        self.t_pass.append(t1 - t0)
+        self.t_routes.append(kms)
+
+    def enable_timing(self, k: int) -> None:
+        self.t_pass, self.t_routes = [], []
+
+    def kernel_ms(self):
+        self.phase_ms = {"all-sources pass (execute + sync, host clock)": 1e3 * float(np.mean(self.t_pass)),
+                         "route selection kernel (HIP events)": float(np.mean(self.t_routes))}
+        return {"allsources": 1e3 * float(np.mean(self.t_pass)), "routes": float(np.mean(self.t_routes))}
+
+    def edges_per_unit(self) -> int:
+        return self.e
+
+    def _oracle_digests(self, mes, orc=None):
+        sys.path.insert(0, str(ROOT / "tests"))
+        from oracle import NameTable, route_digests  # checker / CPU baseline only
+
+        if orc is None:
+            orc = oracle()()
+            orc.update_packed(self.topo.lsdb)
+        return route_digests(orc, NameTable(self.names), mes, self.set_ptr, self.set_nodes, self.lfa)
+
+    def verify(self):
+        """The last step's digests of 48 nodes (the 16 highest-degree ones
+        and 32 random) against the oracle's restatement."""
+        deg = np.diff(self.ls.flatten()[1].astype(np.int64))
+        rng = np.random.default_rng(11)
+        mes = np.unique(np.concatenate([np.argsort(-deg)[:16], rng.choice(self.n, 32, replace=False)]))
+        want = self._oracle_digests(mes)
+        bad = np.nonzero(self.digests[mes] != want)[0]
+        return {"checked_nodes": int(len(mes)), "sets_per_node": int(len(self.set_ptr) - 1),
+                "mismatches": int(len(bad)),
+                "first_mismatch": self.names[int(mes[bad[0]])] if len(bad) else None,
+                "against": "oracle/spf_oracle.cpp orc_ls_route_digests (getMinCostNodes + "
+                           "getNextHopsWithMetric + getNextHopsThrift restated), same digest"}
+
+    def cpu_baseline(self, budget_s: float):
+        orc = oracle()()
+        orc.update_packed(self.topo.lsdb)
+        rng = np.random.default_rng(5)
+        done, t0, mes_all = 0, time.perf_counter(), rng.permutation(self.n)
+        while time.perf_counter() - t0 < budget_s and done < self.n:
+            self._oracle_digests(mes_all[done:done + 4], orc)
+            done += 4
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "route_dbs/s", "cores": host_cores(), "kind": "port",
+                "sample": f"{done} nodes' route selections towards all {self.n} loopbacks"
+                          f"{' with LFA' if self.lfa else ''}, their SPFs (+ neighbours') included, "
+                          f"{dt:.1f} s on {host_cores()} cores of {cpu_model()} (oracle/spf_oracle.cpp)"}
+
+
+class FacadeRouteBuild:
+    """CS-1 / CS-4 (RoutingBenchmarkUtils.cpp:406-511): after a
+    publication toggling one rack switch's overload bit, SpfSolver.buildRouteDb
+    (me) with LFA over the facade -- every node's loopback prefix and node
+    label, adjacency labels -- as BM_DecisionFabric times it (all of
+    buildRouteDb, processTimes[2]).  value = route builds per second."""
+
+    scaling = "replicas"
+    unit = "route_builds/s"
+    kernels = ("route_build",)
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        from openr_amd import topology as T
+        from openr_amd.link_state import LinkState
+        from openr_amd.lsdb import PackedLsdb
+        from openr_amd.spf_solver import PrefixEntry, PrefixState
+        from openr_amd.wire import unpack
+
+        topo = T.fabric(10000, full=True)
+        dbs = topo.lsdb.dbs.copy()
+        dbs["node_label"] = 1 + np.arange(len(dbs), dtype=np.int32)
+        self.lsdb = PackedLsdb(topo.lsdb.blob, dbs, topo.lsdb.adjs)
+        self.desc = ("fabric_full numOfSws=10000; me = rack switch 3-0-0, LFA on; a v6 loopback "
+                     "and a node label per node; per step one publication toggling rack switch "
+                     "3-1-0's overload bit, then SpfSolver.buildRouteDb(me)")
+        self.ls = LinkState(device=dev.index)
+        self.ls.updateAdjacencyDatabases(self.lsdb)
+        self.me = "3-0-0"
+        names = self.ls.flatten()[0]
+        self.n, self.e = len(names), len(self.ls.flatten()[2])
+        self.ps = PrefixState()
+        for i, nm in enumerate(names):
+            self.ps.updatePrefix(nm, self.ls.getArea(), PrefixEntry(f"fd00:{i // 65536:x}:{i % 65536:x}::/64"))
+        dbs = {d.thisNodeName: d for d in unpack(self.lsdb)}
+        self.victim = dbs["3-1-0"]
+        self.units = 1
+        self.world = world
+        self.kernel_bytes = {"route_build": 1}
+        self.survey_bytes = 0
+        self.parallelism = "one LinkState per process (replicas)"
+        self.pub, self.build, self.routes = [], [], 0
+
+    def step(self) -> None:
+        from openr_amd.spf_solver import SpfSolver
+
+        t0 = time.perf_counter()
+        self.victim.isOverloaded = not self.victim.isOverloaded
+        self.ls.updateAdjacencyDatabase(self.victim)
+        t1 = time.perf_counter()
+        db = SpfSolver(self.me, True, True).buildRouteDb(self.me, {self.ls.getArea(): self.ls}, self.ps)
+        t2 = time.perf_counter()
+        self.routes = len(db.unicastRoutes) + len(db.mplsRoutes)
+        self.pub.append(t1 - t0)
+        self.build.append(t2 - t1)
+
+    def enable_timing(self, k: int) -> None:
+        self.pub, self.build = [], []
+        self.ph0 = self.ls.debugPhaseNs()
+
+    def kernel_ms(self):
+        ph = [(b - a) / 1e6 / max(1, len(self.build)) for a, b in zip(self.ph0, self.ls.debugPhaseNs())]
+        self.phase_ms = {"publication (updateAdjacencyDatabase + flatten patch)": 1e3 * float(np.mean(self.pub)),
+                         "buildRouteDb (selection kernel + host route assembly)": 1e3 * float(np.mean(self.build)),
+                         "of which getSpfResult(me) facade phases (plan, execute+copy, pathLinks, "
+                         "host)": ph, "routes_per_build": self.routes}
+        return {"route_build": 1e3 * (float(np.mean(self.pub)) + float(np.mean(self.build)))}
+
+    def edges_per_unit(self) -> int:
+        return self.e
+
+    def cpu_baseline(self, budget_s: float):
+        return None
+
+
+def host_cores() -> int:
+    sys.path.insert(0, str(ROOT / "tests"))
+    from oracle import host_threads
+
+    return host_threads()
+
+
 WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
              "fabric_rtt": AllSources,
-             "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks, "fabric_lfa": FacadeLfa}
+             "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks, "fabric_lfa": FacadeLfa,
+             "fabric_routes": RoutesAllNodes, "fabric_lfa_routes": FacadeRouteBuild}
 
 
 def _pmc_kernels(workload: str, kernels):
@@ -1141,6 +1322,10 @@ def main() -> None:
             if isinstance(wl, Ksp2AllPairs) else
             "LinkState facade: publication + getSpfResult(me and every LFA neighbour) per sec"
             if isinstance(wl, FacadeLfa) else
+            "getDecisionRouteDb for every node (all-sources SPF + route selection) per sec, 10k fabric"
+            if isinstance(wl, RoutesAllNodes) else
+            "publication + SpfSolver.buildRouteDb(me) with LFA per sec, 10k fabric"
+            if isinstance(wl, FacadeRouteBuild) else
             "what-if single-link-failure SPF reruns/sec, 1M-link scale-free graph"),
         "value": value,
         "unit": wl.unit,
@@ -1172,6 +1357,8 @@ def main() -> None:
         out["config"]["results"] = wl.results
     if isinstance(wl, AllSources):
         out["config"]["next_hop_rows"] = wl.narrow  # u32 | u8 | sliced (bit planes)
+    if isinstance(wl, (RoutesAllNodes, FacadeRouteBuild)):
+        out["config"]["phase_ms_per_step"] = wl.phase_ms
     if isinstance(wl, FacadeLfa):
         out["config"]["phase_ms_per_step"] = wl.phase_ms
         out["config"]["batched_prefetch"] = wl.prefetch

@@ -486,6 +486,29 @@ spf_status spf_mplan_read(spf_mplan* mp, uint32_t i, void* dist, uint32_t* nh);
  * owning device; SPF_E_UNSUPPORTED for zero / negative metrics and u64 rows. */
 spf_status spf_mplan_preds(spf_mplan* mp, uint32_t i, uint32_t* pred_ptr, uint32_t* pred_edge,
                            uint32_t cap, uint32_t* n_preds);
+/* Route selection of many nodes from the resident pass (no new SPF): the
+ * reference's getNextHopsWithMetric + getNextHopsThrift (Decision.cpp:
+ * 1082-1305, perDestination = false, one area) of every me = srcs[me_req[t]]
+ * towards every destination set p (set_ptr / set_nodes as spf_routes),
+ * evaluated on me's owning device from its resident row and bitmaps (LFA:
+ * every neighbour's resident row, read over peer access when it lives on
+ * another device).  What Decision::getDecisionRouteDb(node) for every node
+ * (Decision.cpp:1480-1500) computes, minus the thrift formatting.
+ * spf_mplan_route_digests: per me, digests[t] = sum over sets p with a kept
+ * next hop of mix(mix(0x9e3779b97f4a7c15 (p+1) + shortest) + sum over kept
+ * links of mix(link_hash[link id] + (u32) metric) + p) (mix = splitmix64's
+ * finaliser; link_hash[id] identifies link `id` by value, as for
+ * spf_ksp2_digest); *kernel_ms (optional) = the slowest member's kernel time.
+ * spf_mplan_routes: one me's records in spf_routes' layout.  Rows must be u32
+ * link-metric rows (not SPF_FLAG_HOP_COUNT / SPF_FLAG_DIST64). */
+spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32_t n_me,
+                                   const uint32_t* set_ptr, const uint32_t* set_nodes,
+                                   uint32_t n_sets, uint32_t flags, const uint64_t* link_hash,
+                                   uint32_t n_links, uint64_t* digests, double* kernel_ms);
+spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_ptr,
+                            const uint32_t* set_nodes, uint32_t n_sets, uint32_t flags,
+                            uint64_t* min_metric, uint32_t* nh_count, uint32_t* nh_edge,
+                            uint64_t* nh_metric);
 /* HIP-event time of each member's executes: ms[member] summed over the last
  * executes since enable / the last call, *n = executes. */
 spf_status spf_mplan_enable_timing(spf_mplan* mp, uint32_t max_executes);

@@ -229,6 +229,10 @@ PROTOTYPES = {
     "spf_mplan_synchronize": (C.c_int, [_vp]),
     "spf_mplan_digest": (C.c_int, [_vp, _u64p]),
     "spf_mplan_read": (C.c_int, [_vp, C.c_uint32, _vp, _u32p]),
+    "spf_mplan_route_digests": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _u32p, C.c_uint32, C.c_uint32,
+                                          _u64p, C.c_uint32, _u64p, C.POINTER(C.c_double)]),
+    "spf_mplan_routes": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p, C.c_uint32, C.c_uint32, _u64p, _u32p,
+                                   _u32p, _u64p]),
     "spf_mplan_preds": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p, C.c_uint32, _u32p]),
     "spf_mplan_enable_timing": (C.c_int, [_vp, C.c_uint32]),
     "spf_mplan_timing": (C.c_int, [_vp, C.POINTER(C.c_double), _u32p]),

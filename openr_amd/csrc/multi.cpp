@@ -176,11 +176,19 @@ struct spf_mplan {
     uint64_t g_epoch = ~0ull;  // graph epoch the captured executes belong to
     bool g_team_off = false;   // ... and the context's team switch
     std::vector<hipEvent_t> ev;  // timing: [2 * cap] start / end per execute
+    // route selection over the resident pass (spf_mplan_route_digests /
+    // spf_mplan_routes): every resident row's device address, the request's
+    // sets, its me list and outputs on this member's device
+    DevBuf<unsigned long long> rowp, nhp, lh, rdig, rmin, rmetric;
+    DevBuf<uint32_t> rsp, rsn, rme, rcnt, redge;
+    uint64_t r_epoch = ~0ull;  // execute count the address tables belong to
   };
   std::unique_ptr<Part[]> parts;  // [n_parts]
   uint32_t n_parts = 0;
   bool graphs = false;
   uint32_t timing_cap = 0, timing_n = 0;
+  uint64_t executes = 0;   // bumps on every spf_mplan_execute (route tables follow it)
+  int peer = -1;           // 1: every member can read every other member's HBM
   ~spf_mplan() {
     for (size_t i = 0; i < n_parts; ++i) {
       Part& p = parts[i];
@@ -465,6 +473,7 @@ spf_status spf_mplan_execute(spf_mplan* mp) {
     if (st != SPF_OK) return st;
   }
   if (mp->timing_cap) ++mp->timing_n;
+  ++mp->executes;
   return SPF_OK;
 }
 
@@ -535,6 +544,188 @@ spf_status spf_mplan_preds(spf_mplan* mp, uint32_t i, uint32_t* pred_ptr, uint32
   const spf_status st = preds_from_row(c, mp->srcs[i], hop, nullptr, d_row, pred_ptr, pred_edge,
                                        cap, n_preds, m->exec[r]);
   return st == SPF_OK ? SPF_OK : member_fail(m, r, st);
+}
+
+// ---- route selection over the resident pass ------------------------------
+namespace {
+
+// Every member's table of each resident row's (and bitmap set's) device
+// address, plus the sets, on that member's device.  Rows of another device
+// are read through peer access (xGMI): enabled here once, required for LFA
+// (neighbours' rows) when the members span devices.
+spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t* set_nodes,
+                         uint32_t n_sets, bool lfa, const uint64_t* link_hash, uint32_t n_links) {
+  spf_mctx* m = mp->m;
+  spf_ctx* c0 = m->members[0];
+  const uint32_t N = c0->N;
+  if (mp->flags & SPF_FLAG_DIST64)
+    return mfail(m, SPF_E_UNSUPPORTED, "route selection reads u32 rows (SPF_FLAG_DIST64 plan)");
+  if (mp->flags & SPF_FLAG_HOP_COUNT)
+    return mfail(m, SPF_E_UNSUPPORTED, "route selection needs link-metric rows (useLinkMetric)");
+  for (uint32_t i = 0; i < set_ptr[n_sets]; ++i)
+    if (set_nodes[i] >= N) return mfail(m, SPF_E_INVALID, "set member %u out of range", set_nodes[i]);
+  if (mp->peer < 0) {
+    mp->peer = 1;
+    for (uint32_t a = 0; a < mp->n_parts; ++a)
+      for (uint32_t b = 0; b < mp->n_parts; ++b) {
+        const int da = m->members[a]->device, db = m->members[b]->device;
+        if (da == db) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, da, db) != hipSuccess || !can) {
+          mp->peer = 0;
+          continue;
+        }
+        M_HIP(m, hipSetDevice(da));
+        const hipError_t e = hipDeviceEnablePeerAccess(db, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) mp->peer = 0;
+        (void)hipGetLastError();
+      }
+  }
+  std::vector<unsigned long long> rowp(N, 0), nhp(N, 0);
+  std::vector<int> dev_of(N, -1);
+  for (uint32_t i = 0; i < mp->n_src; ++i) {
+    const uint32_t v = mp->srcs[i], r = mp->owner[i], row = mp->row[i];
+    const spf_mplan::Part& p = mp->parts[r];
+    rowp[v] = (unsigned long long)(uintptr_t)(p.dist.p + (size_t)row * c0->pitch);
+    nhp[v] = (unsigned long long)(uintptr_t)(p.nh.p + p.nh_off[row]);
+    dev_of[v] = m->members[r]->device;
+  }
+  if (lfa && !mp->peer) {
+    // members on distinct devices without peer access: every neighbour of a
+    // member's me must then live on that member's device
+    for (uint32_t i = 0; i < mp->n_src; ++i) {
+      const uint32_t v = mp->srcs[i];
+      for (uint32_t e = c0->nb_ptr[v]; e < c0->nb_ptr[v + 1]; ++e)
+        if (dev_of[c0->nb_id[e]] != dev_of[v])
+          return mfail(m, SPF_E_UNSUPPORTED, "LFA route selection across devices needs peer access");
+    }
+  }
+  for (uint32_t r = 0; r < mp->n_parts; ++r) {
+    spf_mplan::Part& p = mp->parts[r];
+    if (!p.plan) continue;
+    spf_ctx* c = m->members[r];
+    M_HIP(m, hipSetDevice(c->device));
+    const hipStream_t s = m->exec[r];
+    if (p.r_epoch != mp->executes) {
+      M_HIP(m, p.rowp.upload(rowp.data(), N, s));
+      M_HIP(m, p.nhp.upload(nhp.data(), N, s));
+      p.r_epoch = mp->executes;
+    }
+    M_HIP(m, p.rsp.upload(set_ptr, n_sets + 1, s));
+    M_HIP(m, p.rsn.upload(set_nodes, std::max<uint32_t>(1, set_ptr[n_sets]), s));
+    if (link_hash) M_HIP(m, p.lh.upload(reinterpret_cast<const unsigned long long*>(link_hash),
+                                        std::max<uint32_t>(1, n_links), s));
+    // the tables' uploads are pageable copies: done before the caller's
+    // vectors go away (the set arrays are the caller's)
+    M_HIP(m, hipStreamSynchronize(s));
+  }
+  return SPF_OK;
+}
+
+}  // namespace
+
+spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32_t n_me,
+                                   const uint32_t* set_ptr, const uint32_t* set_nodes, uint32_t n_sets,
+                                   uint32_t flags, const uint64_t* link_hash, uint32_t n_links,
+                                   uint64_t* digests, double* kernel_ms) {
+  if (!mp || (n_me && (!me_req || !digests)) || !set_ptr || !link_hash)
+    return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_route_digests: NULL argument");
+  spf_mctx* m = mp->m;
+  spf_ctx* c0 = m->members[0];
+  for (uint32_t t = 0; t < n_me; ++t)
+    if (me_req[t] >= mp->n_src) return mfail(m, SPF_E_INVALID, "me %u is not a request index", me_req[t]);
+  for (uint32_t e = 0; e < c0->E; ++e)
+    if (c0->link[e] >= n_links) return mfail(m, SPF_E_INVALID, "link_hash shorter than the link ids");
+  const bool lfa = (flags & SPF_ROUTE_LFA) != 0;
+  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, link_hash, n_links);
+      st != SPF_OK)
+    return st;
+  std::vector<std::vector<uint32_t>> mine(mp->n_parts), slot(mp->n_parts);
+  for (uint32_t t = 0; t < n_me; ++t) {
+    const uint32_t r = mp->owner[me_req[t]];
+    mine[r].push_back(mp->srcs[me_req[t]]);
+    slot[r].push_back(t);
+  }
+  std::vector<hipEvent_t> ev(2 * mp->n_parts, nullptr);
+  std::vector<std::vector<uint64_t>> got(mp->n_parts);
+  for (uint32_t r = 0; r < mp->n_parts; ++r) {
+    spf_mplan::Part& p = mp->parts[r];
+    if (mine[r].empty()) continue;
+    spf_ctx* c = m->members[r];
+    M_HIP(m, hipSetDevice(c->device));
+    const hipStream_t s = m->exec[r];
+    const uint32_t n = (uint32_t)mine[r].size();
+    M_HIP(m, p.rme.upload(mine[r].data(), n, s));
+    M_HIP(m, p.rdig.alloc(n));
+    M_HIP(m, hipMemsetAsync(p.rdig.p, 0, 8ull * n, s));
+    if (kernel_ms) {
+      M_HIP(m, hipEventCreate(&ev[2 * r]));
+      M_HIP(m, hipEventCreate(&ev[2 * r + 1]));
+      M_HIP(m, hipEventRecord(ev[2 * r], s));
+    }
+    const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, n, p.rsp.p, p.rsn.p, n_sets,
+                                            lfa, p.lh.p, p.rdig.p, nullptr, nullptr, nullptr, nullptr, s);
+    if (st != SPF_OK) return member_fail(m, r, st);
+    if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r + 1], s));
+    got[r].resize(n);
+    M_HIP(m, hipMemcpyAsync(got[r].data(), p.rdig.p, 8ull * n, hipMemcpyDeviceToHost, s));
+  }
+  double worst = 0;
+  for (uint32_t r = 0; r < mp->n_parts; ++r) {
+    if (mine[r].empty()) continue;
+    M_HIP(m, hipSetDevice(m->members[r]->device));
+    M_HIP(m, hipStreamSynchronize(m->exec[r]));
+    if (kernel_ms) {
+      float t = 0;
+      M_HIP(m, hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]));
+      worst = std::max(worst, (double)t);
+      (void)hipEventDestroy(ev[2 * r]);
+      (void)hipEventDestroy(ev[2 * r + 1]);
+    }
+    for (size_t q = 0; q < got[r].size(); ++q) digests[slot[r][q]] = got[r][q];
+  }
+  if (kernel_ms) *kernel_ms = worst;
+  return SPF_OK;
+}
+
+spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_ptr,
+                            const uint32_t* set_nodes, uint32_t n_sets, uint32_t flags,
+                            uint64_t* min_metric, uint32_t* nh_count, uint32_t* nh_edge,
+                            uint64_t* nh_metric) {
+  if (!mp || !set_ptr || !min_metric || !nh_count || !nh_edge || !nh_metric)
+    return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_routes: NULL argument");
+  spf_mctx* m = mp->m;
+  if (me_req >= mp->n_src) return mfail(m, SPF_E_INVALID, "me %u is not a request index", me_req);
+  const bool lfa = (flags & SPF_ROUTE_LFA) != 0;
+  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, nullptr, 0); st != SPF_OK)
+    return st;
+  const uint32_t r = mp->owner[me_req];
+  spf_mplan::Part& p = mp->parts[r];
+  spf_ctx* c = m->members[r];
+  const uint32_t me = mp->srcs[me_req];
+  const uint32_t deg = c->row_ptr[me + 1] - c->row_ptr[me];
+  const size_t cap = (size_t)n_sets * std::max<uint32_t>(1, deg);
+  M_HIP(m, hipSetDevice(c->device));
+  const hipStream_t s = m->exec[r];
+  M_HIP(m, p.rme.upload(&me, 1, s));
+  M_HIP(m, p.rmin.alloc(std::max<uint32_t>(1, n_sets)));
+  M_HIP(m, p.rcnt.alloc(std::max<uint32_t>(1, n_sets)));
+  M_HIP(m, p.redge.alloc(cap));
+  M_HIP(m, p.rmetric.alloc(cap));
+  const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, 1, p.rsp.p, p.rsn.p, n_sets, lfa,
+                                          nullptr, nullptr, reinterpret_cast<uint64_t*>(p.rmin.p),
+                                          p.rcnt.p, p.redge.p, reinterpret_cast<uint64_t*>(p.rmetric.p), s);
+  if (st != SPF_OK) return member_fail(m, r, st);
+  if (n_sets) {
+    M_HIP(m, hipMemcpyAsync(min_metric, p.rmin.p, 8ull * n_sets, hipMemcpyDeviceToHost, s));
+    M_HIP(m, hipMemcpyAsync(nh_count, p.rcnt.p, 4ull * n_sets, hipMemcpyDeviceToHost, s));
+    if (deg) {
+      M_HIP(m, hipMemcpyAsync(nh_edge, p.redge.p, 4ull * cap, hipMemcpyDeviceToHost, s));
+      M_HIP(m, hipMemcpyAsync(nh_metric, p.rmetric.p, 8ull * cap, hipMemcpyDeviceToHost, s));
+    }
+  }
+  M_HIP(m, hipStreamSynchronize(s));
+  return SPF_OK;
 }
 
 uint32_t spf_mplan_closure_rows(const spf_mplan* mp, uint32_t member) {

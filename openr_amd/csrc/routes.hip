@@ -90,7 +90,141 @@ __global__ __launch_bounds__(64) void routes_kernel(
   }
 }
 
+__device__ __forceinline__ uint64_t rmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// Route selection for many `me` nodes over RESIDENT rows (an all-sources
+// pass, spf_mplan): a thread per destination set, a block row per me (every
+// me value wave-uniform: its CSR row, its distinct neighbours, their rows
+// arrive by scalar loads).  Sets of single advertisers sorted by node id make
+// consecutive lanes read consecutive entries of me's row and bitmaps.
+//   rowp[v] / nhp[v]: device addresses of v's u32 distance row and of its
+//   first next-hop bitmap (bitmap j = neighbour j, ascending id, wpm words);
+//   0 where v is not resident (a set member never needs it; LFA needs every
+//   neighbour of me).
+// Per (me, set p) the reference's getMinCostNodes + getNextHopsWithMetric +
+// getNextHopsThrift (Decision.cpp:1082-1305, perDestination = false): per up
+// link e of me towards x, over = w(e) + via(x) with via(x) = shortest -
+// d_me(x) when x is a next hop of a min-cost member, lowered (LFA) to any
+// member's d_x(dst) < shortest + d_x(me); kept when LFA or over == shortest.
+//   DIGEST: digest[slot] += mix(rec + p) over routes with a kept link, rec =
+//   mix(K (p + 1) + shortest) + sum over kept links of mix(link_hash[l] +
+//   (u32) over).  Otherwise (one me) the records of spf_routes.
+constexpr uint32_t kRsThreads = 256;
+template <bool DIGEST>
+__global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
+    const unsigned long long* __restrict__ rowp, const unsigned long long* __restrict__ nhp,
+    uint32_t wpm, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+    const uint32_t* __restrict__ wt, const uint32_t* __restrict__ link,
+    const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
+    const uint32_t* __restrict__ me_ids, const uint32_t* __restrict__ set_ptr,
+    const uint32_t* __restrict__ set_nodes, uint32_t n_sets, uint32_t lfa,
+    const unsigned long long* __restrict__ link_hash, unsigned long long* __restrict__ digest,
+    uint64_t* __restrict__ out_min, uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_edge,
+    uint64_t* __restrict__ out_metric) {
+  const uint32_t me = me_ids[blockIdx.y];
+  const uint32_t p = blockIdx.x * kRsThreads + threadIdx.x;
+  const uint32_t* Dme = reinterpret_cast<const uint32_t*>(rowp[me]);
+  const uint32_t* NHme = reinterpret_cast<const uint32_t*>(nhp[me]);
+  const uint32_t e0 = row_ptr[me], e1 = row_ptr[me + 1];
+  const uint32_t nb0 = nb_ptr[me], k = nb_ptr[me + 1] - nb0;
+  const bool live = p < n_sets;
+  const uint32_t b = live ? set_ptr[p] : 0u, e = live ? set_ptr[p + 1] : 0u;
+  uint64_t shortest = kInf64;
+  for (uint32_t i = b; i < e; ++i) {
+    const uint32_t d = Dme[set_nodes[i]];
+    if (d != kInf && d < shortest) shortest = d;
+  }
+  uint64_t rec = 0;
+  uint32_t cnt = 0;
+  const uint32_t deg = e1 - e0;
+  if (shortest != kInf64 || !DIGEST) {
+    for (uint32_t q = e0; q < e1; ++q) {  // me's up links (wave-uniform)
+      const uint32_t x = col[q];
+      // j: x's index among me's distinct neighbours (binary search, scalar)
+      uint32_t lo = 0, hi = k;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (nb_id[nb0 + mid] <= x) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t j = lo;
+      if (shortest == kInf64) continue;
+      uint64_t via = kInf64;
+      const uint32_t* bm = NHme + (size_t)j * wpm;
+      for (uint32_t i = b; i < e; ++i) {
+        const uint32_t d = set_nodes[i];
+        if (Dme[d] != shortest) continue;
+        if ((bm[d >> 5] >> (d & 31)) & 1u) {
+          via = shortest - Dme[x];
+          break;
+        }
+      }
+      if (lfa) {
+        const uint32_t* Dx = reinterpret_cast<const uint32_t*>(rowp[x]);
+        const uint64_t back = Dx[me];
+        for (uint32_t i = b; i < e; ++i) {
+          const uint32_t dxd = Dx[set_nodes[i]];
+          if (dxd == kInf || back == kInf) continue;
+          if ((uint64_t)dxd < shortest + back && (via == kInf64 || via > dxd)) via = dxd;
+        }
+      }
+      if (via == kInf64) continue;
+      const uint64_t over = (uint64_t)wt[q] + via;
+      if (!lfa && over != shortest) continue;
+      if constexpr (DIGEST) {
+        rec += rmix64(link_hash[link[q]] + (uint32_t)over);
+      } else {
+        out_edge[(size_t)p * deg + cnt] = q;
+        out_metric[(size_t)p * deg + cnt] = over;
+      }
+      ++cnt;
+    }
+  }
+  if constexpr (DIGEST) {
+    uint64_t h = (live && cnt) ? rmix64(rmix64(0x9e3779b97f4a7c15ull * (p + 1) + shortest) + rec + p) : 0ull;
+    // wave sum, one atomic per wave
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint32_t lo2 = __shfl_down((uint32_t)h, d, 64), hi2 = __shfl_down((uint32_t)(h >> 32), d, 64);
+      h += ((uint64_t)hi2 << 32) | lo2;
+    }
+    if ((threadIdx.x & 63) == 0 && h) atomicAdd(&digest[blockIdx.y], (unsigned long long)h);
+  } else if (live) {
+    out_min[p] = shortest;
+    out_cnt[p] = cnt;
+  }
+}
+
 }  // namespace
+
+namespace spfi {
+
+spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
+                             const unsigned long long* d_nhp, const uint32_t* d_me, uint32_t n_me,
+                             const uint32_t* d_set_ptr, const uint32_t* d_set_nodes, uint32_t n_sets,
+                             bool lfa, const unsigned long long* d_link_hash,
+                             unsigned long long* d_digest, uint64_t* d_min, uint32_t* d_cnt,
+                             uint32_t* d_edge, uint64_t* d_metric, hipStream_t s) {
+  if (!n_me || !n_sets) return SPF_OK;
+  const dim3 grid((n_sets + kRsThreads - 1) / kRsThreads, n_me);
+  if (d_digest)
+    hipLaunchKernelGGL(route_sets_kernel<true>, grid, dim3(kRsThreads), 0, s, d_rowp, d_nhp,
+                       c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_nb_ptr.p,
+                       c->d_nb_id.p, d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, d_link_hash,
+                       d_digest, nullptr, nullptr, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL(route_sets_kernel<false>, grid, dim3(kRsThreads), 0, s, d_rowp, d_nhp,
+                       c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_nb_ptr.p,
+                       c->d_nb_id.p, d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, nullptr,
+                       nullptr, d_min, d_cnt, d_edge, d_metric);
+  HIP_TRY(c, hipGetLastError());
+  return SPF_OK;
+}
+
+}  // namespace spfi
 
 extern "C" {
 

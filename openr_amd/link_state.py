@@ -443,6 +443,55 @@ class LinkState(N.NativeHandle):
         N.raise_for(st, N.global_error())
         return out[: n.value]
 
+    def linkValueHashes(self):
+        """u64 value identity of every link id of the flattened graph (FNV-1a
+        over its ordered key, bench.link_value_hash's definition), for the
+        engine's route / KSP2 digests; cached until the topology changes."""
+        import numpy as np
+
+        lid = self.flatten()[4]
+        key = (len(lid), int(lid.max()) if len(lid) else -1, N.lib.ls_num_links(self._h))
+        if getattr(self, "_lh_key", None) == key and self._lh is not None:
+            return self._lh
+        lh = np.zeros(max(1, int(lid.max()) + 1 if len(lid) else 1), np.uint64)
+        M, P = (1 << 64) - 1, 0x100000001b3
+        for l in np.unique(lid):
+            (a, b), (c, d) = self._link(int(l)).orderedNames
+            f = 0xcbf29ce484222325
+            for part in (a, b, c, d):
+                for ch in part.encode():
+                    f = ((f ^ ch) * P) & M
+                f = ((f ^ 0x01) * P) & M
+            f = ((f ^ (f >> 30)) * 0xbf58476d1ce4e5b9) & M
+            f = ((f ^ (f >> 27)) * 0x94d049bb133111eb) & M
+            lh[int(l)] = f ^ (f >> 31)
+        self._lh, self._lh_key = lh, key
+        return lh
+
+    def allSourcesRouteDigests(self, set_ptr, set_nodes, lfa: bool, mes=None):
+        """Route selections of every node (or the csr ids in `mes`) towards
+        every destination set from the resident all-sources pass
+        (spf_mplan_route_digests, needs prefetchAllSources()): per node one
+        u64 digest, and the slowest member's kernel ms."""
+        import numpy as np
+
+        mp = N.lib.ls_all_sources_plan(self._h)
+        if not mp:
+            raise RuntimeError("allSourcesRouteDigests: no resident all-sources pass")
+        n = len(self.flatten()[0])
+        mes = np.arange(n, dtype=np.uint32) if mes is None else np.ascontiguousarray(mes, np.uint32)
+        sp = np.ascontiguousarray(set_ptr, np.uint32)
+        sn = np.ascontiguousarray(set_nodes if len(set_nodes) else [0], np.uint32)
+        lh = self.linkValueHashes()
+        out = np.zeros(max(1, len(mes)), np.uint64)
+        ms = C.c_double()
+        st = N.lib.spf_mplan_route_digests(C.c_void_p(mp), N.ptr(mes), len(mes), N.ptr(sp), N.ptr(sn),
+                                           len(sp) - 1, N.SPF_ROUTE_LFA if lfa else 0,
+                                           N.ptr(lh, C.c_uint64), len(lh), N.ptr(out, C.c_uint64),
+                                           C.byref(ms))
+        N.raise_for(st, N.global_error())
+        return out[: len(mes)], ms.value
+
     def debugPhaseNs(self) -> Tuple[int, int, int, int]:
         """Cumulative getSpfResult cost (ns): plan build, GPU execute + copy
         back, pathLinks, host assembly (ls_debug_phase_ns)."""

@@ -50,7 +50,7 @@ from __future__ import annotations
 import ctypes as C
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Dict, FrozenSet, List, Optional, Sequence, Set, Tuple
+from typing import Dict, FrozenSet, List, NamedTuple, Optional, Sequence, Set, Tuple
 
 import numpy as np
 
@@ -66,19 +66,19 @@ def isMplsLabelValid(label: int) -> bool:
     return MPLS_LABEL_MIN <= label <= MPLS_LABEL_MAX
 
 
-@dataclass(frozen=True)
-class MplsAction:
-    """thrift::MplsAction (openr/if/Network.thrift)."""
+class MplsAction(NamedTuple):
+    """thrift::MplsAction (openr/if/Network.thrift); an immutable value (a
+    named tuple: a route build makes ~10^5 of these objects)."""
 
     action: str  # "PUSH" | "SWAP" | "PHP" | "POP_AND_LOOKUP"
     swapLabel: Optional[int] = None
     pushLabels: Optional[Tuple[int, ...]] = None
 
 
-@dataclass(frozen=True)
-class NextHopThrift:
+class NextHopThrift(NamedTuple):
     """thrift::NextHopThrift (Network.thrift:65-86) as built by createNextHop
-    (openr/common/Util.cpp:907-922): metric is an i32."""
+    (openr/common/Util.cpp:907-922): metric is an i32.  An immutable value
+    (a named tuple, hashable, cheap to build)."""
 
     address: bytes
     ifName: Optional[str]
@@ -373,6 +373,28 @@ def areaOrder(areaLinkStates: Dict[str, LinkState]) -> List[Tuple[str, LinkState
     return [(keys[order[i]], areaLinkStates[keys[order[i]]]) for i in range(n.value)]
 
 
+class _LazySetResults:
+    """spf_routes' outputs as a sequence of _SetResult, built on access."""
+
+    def __init__(self, mins, cnt, edge, metric, deg) -> None:
+        self.mins, self.cnt, self.edge, self.metric, self.deg = mins, cnt, edge, metric, deg
+
+    def __len__(self) -> int:
+        return len(self.cnt)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        mm = int(self.mins[i])
+        b = i * self.deg
+        c = int(self.cnt[i])
+        hops = list(zip(self.edge[b:b + c].tolist(), self.metric[b:b + c].tolist()))
+        return _SetResult(None if mm == (1 << 64) - 1 else mm, hops)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
 @dataclass
 class _SetResult:
     min_metric: Optional[int]
@@ -427,35 +449,51 @@ class SpfSolver:
         cnt = np.zeros(len(sets), np.uint32)
         edge = np.zeros(len(sets) * deg, np.uint32)
         metric = np.zeros(len(sets) * deg, np.uint64)
-        st = N.lib.spf_routes(ls.engine_handle(), m, N.ptr(ptr), N.ptr(nodes), len(sets),
-                              N.SPF_ROUTE_LFA if self.computeLfaPaths else 0,
-                              N.ptr(mins, C.c_uint64), N.ptr(cnt), N.ptr(edge),
-                              N.ptr(metric, C.c_uint64))
+        flags = N.SPF_ROUTE_LFA if self.computeLfaPaths else 0
+        # A resident all-sources pass (LinkState.prefetchAllSources: every
+        # node's row and bitmaps on the GPUs) answers from me's owner with
+        # no new SPF plan; otherwise one batched plan for me (+ neighbours)
+        mp = N.lib.ls_all_sources_plan(ls._h)
+        st = N.SPF_E_UNSUPPORTED
+        if mp:
+            st = N.lib.spf_mplan_routes(C.c_void_p(mp), m, N.ptr(ptr), N.ptr(nodes), len(sets), flags,
+                                        N.ptr(mins, C.c_uint64), N.ptr(cnt), N.ptr(edge),
+                                        N.ptr(metric, C.c_uint64))
+            if st not in (N.SPF_OK, N.SPF_E_UNSUPPORTED):
+                N.raise_for(st, N.global_error())
+        if st != N.SPF_OK:
+            st = N.lib.spf_routes(ls.engine_handle(), m, N.ptr(ptr), N.ptr(nodes), len(sets), flags,
+                                  N.ptr(mins, C.c_uint64), N.ptr(cnt), N.ptr(edge),
+                                  N.ptr(metric, C.c_uint64))
         if st != N.SPF_OK:
             N.raise_for(st, (N.lib.spf_last_error(ls.engine_handle()) or b"").decode())
-        out = []
-        for i in range(len(sets)):
-            mm = int(mins[i])
-            hops = [(int(edge[i * deg + t]), int(metric[i * deg + t])) for t in range(int(cnt[i]))]
-            out.append(_SetResult(None if mm == (1 << 64) - 1 else mm, hops))
         self._lid = lid
-        return out
+        self._raw = (mins, cnt, edge, metric, deg)
+        return _LazySetResults(mins, cnt, edge, metric, deg)
 
     def _next_hops(self, ls: LinkState, me: str, area: str, res: _SetResult, isV4: bool,
                    dsts: Set[str], swapLabel: Optional[int]) -> Set[NextHopThrift]:
         """getNextHopsThrift (Decision.cpp:1198-1305) from the kernel's
         (link, metric) selection."""
         out: Set[NextHopThrift] = set()
+        info = getattr(self, "_edge_info", None)
+        if info is None or info[0] is not ls or info[1] != me or info[2] is not self._lid:
+            info = self._edge_info = (ls, me, self._lid, {})
+        cache = info[3]
         for e, metric in res.hops:
-            link = ls._link(int(self._lid[e]))
-            nb = link.getOtherNodeName(me)
+            li = cache.get(e)
+            if li is None:
+                link = ls._link(int(self._lid[e]))
+                li = cache[e] = (link.getOtherNodeName(me), link.getIfaceFromNode(me),
+                                 bytes(link.getNhV4FromNode(me)), bytes(link.getNhV6FromNode(me)),
+                                 link.getArea())
+            nb, iface, v4, v6, larea = li
             action = None
             if swapLabel is not None:
-                also_dst = nb in dsts
-                action = MplsAction("PHP") if also_dst else MplsAction("SWAP", swapLabel)
-            addr = link.getNhV4FromNode(me) if isV4 else link.getNhV6FromNode(me)
-            out.add(createNextHop(addr, link.getIfaceFromNode(me), metric, action,
-                                  link.getArea(), nb))
+                action = MplsAction("PHP") if nb in dsts else MplsAction("SWAP", swapLabel)
+            m = metric & 0xFFFFFFFF
+            out.add(NextHopThrift(v4 if isV4 else v6, iface, m - (1 << 32) if m >= 1 << 31 else m,
+                                  action, larea, nb))
         return out
 
     # -- SR_MPLS SP_ECMP: getNextHopsWithMetric / getNextHopsThrift with
@@ -918,12 +956,21 @@ class SpfSolver:
         sets = [dsts for _, _, dsts, _, _ in uni] + [[n] for n in label_to_node.values()]
         sel = self._select(ls, me, sets)
 
-        for (prefix, ents, dsts, res, isBgp), r_ in zip(uni, sel[: len(uni)]):
-            if not r_.hops:
+        # IP routes with the same (link, metric) selection share one frozen
+        # next-hop set (a fabric's destinations of one pod select alike)
+        mins, cnt, edge, metric, deg = self._raw
+        shared: Dict[tuple, FrozenSet[NextHopThrift]] = {}
+        for i, (prefix, ents, dsts, res, isBgp) in enumerate(uni):
+            c = int(cnt[i])
+            if not c:
                 self._bump("decision.no_route_to_prefix")
                 continue
             isV4 = next(iter(ents.values())).isV4
-            nhs = self._next_hops(ls, me, area, r_, isV4, set(dsts), None)
+            key = (edge[i * deg:i * deg + c].tobytes(), metric[i * deg:i * deg + c].tobytes(), isV4)
+            nhs = shared.get(key)
+            if nhs is None:
+                nhs = frozenset(self._next_hops(ls, me, area, sel[i], isV4, set(dsts), None))
+                shared[key] = nhs
             r = self._addBestPaths(me, prefix, res.allNodeAreas, res.bestNodeArea, ents, nhs, isBgp)
             if r is not None:
                 db.addUnicastRoute(r)

@@ -1675,6 +1675,100 @@ int orc_ls_ksp2_digests(orc_ls* p, const char* blob, const uint32_t* off, const 
   return 0;
 }
 
+// ---- route selections of many nodes (spf_mplan_route_digests' contract) ----
+// Per me = names[mes[t]]: for every destination set p (set_ptr / set_nodes:
+// node ids of the caller's names table), getMinCostNodes +
+// getNextHopsWithMetric + getNextHopsThrift (Decision.cpp:1082-1305,
+// perDestination = false, one area), exactly as orc_ls_nexthops_json, reduced
+// to sum over sets with a kept link of mix(mix(0x9e3779b97f4a7c15 (p+1) +
+// shortest) + sum over kept links of mix(keyHash(link) + (u32) metric) + p).
+int orc_ls_route_digests(orc_ls* p, const char* blob, const uint32_t* off, const uint32_t* len,
+                         uint32_t n, const uint32_t* mes, uint32_t n_me, const uint32_t* set_ptr,
+                         const uint32_t* set_nodes, uint32_t n_sets, int lfa, int threads,
+                         uint64_t* out) {
+  const orc::NameIds t(blob, off, len, n);
+  const orc::LinkState& ls = p->ls;
+  // the SPF results every me needs (its own, with LFA its neighbours'):
+  // runSpf on `threads` host threads (the memo of getSpfResult is not
+  // thread-safe), then the selections in parallel
+  std::map<std::string, uint32_t> need;
+  for (uint32_t i = 0; i < n_me; ++i) {
+    const std::string& me = t.names[mes[i]];
+    need.emplace(me, 0u);
+    if (lfa)
+      for (const auto& l : ls.linksFrom(me))
+        if (l->isUp()) need.emplace(l->other(me), 0u);
+  }
+  std::vector<std::string> order;
+  for (auto& kv : need) {
+    kv.second = (uint32_t)order.size();
+    order.push_back(kv.first);
+  }
+  std::vector<orc::SpfResult> res(order.size());
+  orc::parallelFor((uint32_t)order.size(), threads,
+                   [&](uint32_t i, int) { res[i] = ls.runSpf(order[i], true); });
+  auto spf = [&](const std::string& v) -> const orc::SpfResult& { return res[need.at(v)]; };
+  orc::parallelFor(n_me, threads, [&](uint32_t i, int) {
+    const std::string& me = t.names[mes[i]];
+    const auto& mine = spf(me);
+    uint64_t acc = 0;
+    for (uint32_t q = 0; q < n_sets; ++q) {
+      std::set<std::string> dstSet;
+      for (uint32_t x = set_ptr[q]; x < set_ptr[q + 1]; ++x) dstSet.insert(t.names[set_nodes[x]]);
+      orc::Metric shortest = std::numeric_limits<orc::Metric>::max();
+      std::set<std::string> minCost;
+      for (const auto& d : dstSet) {
+        auto it = mine.find(d);
+        if (it == mine.end()) continue;
+        if (shortest >= it->second.metric) {
+          if (shortest > it->second.metric) {
+            shortest = it->second.metric;
+            minCost.clear();
+          }
+          minCost.insert(d);
+        }
+      }
+      std::map<std::string, orc::Metric> nextHopNodes;
+      if (!minCost.empty()) {
+        for (const auto& d : minCost)
+          for (const auto& nh : mine.at(d).nextHops) nextHopNodes[nh] = shortest - mine.at(nh).metric;
+        if (lfa) {
+          for (const auto& l : ls.linksFrom(me)) {
+            if (!l->isUp()) continue;
+            const std::string& nb = l->other(me);
+            const auto& fromNb = spf(nb);
+            const orc::Metric nbToHere = fromNb.at(me).metric;
+            for (const auto& d : dstSet) {
+              auto it = fromNb.find(d);
+              if (it == fromNb.end()) continue;
+              const orc::Metric dn = it->second.metric;
+              if (dn < shortest + nbToHere) {
+                auto f = nextHopNodes.find(nb);
+                if (f == nextHopNodes.end()) nextHopNodes.emplace(nb, dn);
+                else if (f->second > dn) f->second = dn;
+              }
+            }
+          }
+        }
+      }
+      uint64_t rec = 0;
+      uint32_t kept = 0;
+      for (const auto& l : ls.linksFrom(me)) {
+        auto f = nextHopNodes.find(l->other(me));
+        if (f == nextHopNodes.end() || !l->isUp()) continue;
+        const orc::Metric over = l->metricFrom(me) + f->second;
+        if (!lfa && over != shortest) continue;
+        rec += mix64(orc::linkKeyHash(*l) + (uint32_t)over);
+        ++kept;
+      }
+      if (kept)
+        acc += mix64(mix64(0x9e3779b97f4a7c15ULL * (q + 1) + shortest) + rec + q);
+    }
+    out[i] = acc;
+  });
+  return 0;
+}
+
 // The same reduction over GPU KSP2 output (spf_ksp2_pair records + path pool
 // of link ids; link_hash[id] = orc_link_keyhash of that link's ordered key).
 int orc_digest_ksp2(uint32_t n_src, uint32_t n, const uint32_t* pairs /* [n_src*n][4] */,

@@ -256,6 +256,9 @@ def sr_nexthops(orc: "OracleLinkState", me: str, dsts: Dict[str, Optional[int]],
 
 # ---- full-size parity digests (oracle/spf_oracle.cpp, "Full-size parity digests") ----
 _u32p, _u64p = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+lib.orc_ls_route_digests.restype = C.c_int
+lib.orc_ls_route_digests.argtypes = [C.c_void_p, C.c_char_p, _u32p, _u32p, C.c_uint32, _u32p,
+                                     C.c_uint32, _u32p, _u32p, C.c_uint32, C.c_int, C.c_int, _u64p]
 lib.orc_link_keyhash.restype = C.c_uint64
 lib.orc_link_keyhash.argtypes = [C.c_char_p] * 4
 lib.orc_ls_source_digests.restype = C.c_int
@@ -369,3 +372,19 @@ def keyvals_order(keys: Sequence[str]) -> List[int]:
     out = np.zeros(max(1, len(keys)), np.uint32)
     k = lib.orc_keyvals_order(arr, len(keys), _p(out))
     return [int(x) for x in out[:k]]
+
+
+def route_digests(orc: "OracleLinkState", table: NameTable, mes: Sequence[int],
+                  set_ptr: np.ndarray, set_nodes: np.ndarray, lfa: bool,
+                  threads: int = 0) -> np.ndarray:
+    """spf_mplan_route_digests' reduction of the reference's route selection
+    (orc_ls_route_digests): one u64 per me (ids into `table`)."""
+    mes = np.ascontiguousarray(mes, np.uint32)
+    sp = np.ascontiguousarray(set_ptr, np.uint32)
+    sn = np.ascontiguousarray(set_nodes if len(set_nodes) else [0], np.uint32)
+    out = np.zeros(max(1, len(mes)), np.uint64)
+    rc = lib.orc_ls_route_digests(orc._h, table.blob, _p(table.offs), _p(table.lens), table.n,
+                                  _p(mes), len(mes), _p(sp), _p(sn), len(sp) - 1, int(lfa),
+                                  threads or host_threads(), _p(out, C.c_uint64))
+    assert rc == 0
+    return out[: len(mes)]

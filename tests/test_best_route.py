@@ -176,3 +176,61 @@ def test_area_order_is_libstdcxx_unordered_map_order():
         out = subprocess.run([str(Path(d, "o")), *keys], check=True, capture_output=True,
                              text=True).stdout.split()
     assert got == out
+
+
+def test_oracle_route_digests_equal_pinned_nexthops():
+    """orc_ls_route_digests (the checker of spf_mplan_route_digests) reduces
+    exactly what orc_ls_nexthops_json returns (the restatement pinned by
+    tests/test_oracle_reference.py to DecisionTest's route expectations):
+    both on random multigraphs with drained nodes and links, SP and LFA."""
+    import numpy as np
+
+    from oracle import NameTable, OracleLinkState, nexthops, route_digests
+    from openr_amd import topology as T
+    from openr_amd.wire import unpack
+
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & M
+        z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & M
+        return z ^ (z >> 31)
+
+    def keyhash(a, b, c, d):
+        f = 0xcbf29ce484222325
+        for part in (a, b, c, d):
+            for ch in part.encode():
+                f = ((f ^ ch) * 0x100000001b3) & M
+            f = ((f ^ 0x01) * 0x100000001b3) & M
+        return mix(f)
+
+    for seed in (3, 4):
+        topo = T.random_graph(25, 60, seed, max_metric=4, parallel_frac=0.3, overload_frac=0.15,
+                              link_overload_frac=0.1)
+        dbs = {d.thisNodeName: d for d in unpack(topo.lsdb)}
+        names = sorted(topo.nodes)
+        orc = OracleLinkState()
+        orc.update_packed(topo.lsdb)
+        rng = np.random.default_rng(seed)
+        sets = [[v] for v in range(len(names))] + [
+            sorted(int(x) for x in rng.choice(len(names), 3, replace=False)) for _ in range(8)]
+        ptr = np.concatenate([[0], np.cumsum([len(s) for s in sets])]).astype(np.uint32)
+        flat = np.concatenate([np.asarray(s, np.uint32) for s in sets])
+        mes = rng.choice(len(names), 6, replace=False)
+        for lfa in (False, True):
+            got = route_digests(orc, NameTable(names), mes, ptr, flat, lfa)
+            for t, me_i in enumerate(mes):
+                me = names[me_i]
+                acc = 0
+                for p, s in enumerate(sets):
+                    r = nexthops(orc, me, [names[v] for v in s], lfa)
+                    if not r["nh"]:
+                        continue
+                    rec = 0
+                    for ifn, metric, nb, *_ in r["nh"]:
+                        oif = next(a.otherIfName for a in dbs[me].adjacencies
+                                   if a.ifName == ifn and a.otherNodeName == nb)
+                        (a, b), (c, d) = sorted([(me, ifn), (nb, oif)])
+                        rec = (rec + mix((keyhash(a, b, c, d) + (metric & 0xFFFFFFFF)) & M)) & M
+                    acc = (acc + mix((mix((0x9e3779b97f4a7c15 * (p + 1) + r["min"]) & M) + rec + p) & M)) & M
+                assert int(got[t]) == acc, (seed, lfa, me)

@@ -1,0 +1,102 @@
+"""Route selection for every node from a resident all-sources pass
+(spf_mplan_route_digests / spf_mplan_routes, include/openr_spf.h): what
+Decision::getDecisionRouteDb(node) for every node (Decision.cpp:1480-1500,
+CS-2) computes, with no SPF per node.
+
+* every node's digest over every destination set (single advertisers and
+  anycast sets, SP and LFA) against the oracle's restatement of
+  getMinCostNodes / getNextHopsWithMetric / getNextHopsThrift
+  (oracle/spf_oracle.cpp orc_ls_route_digests), on random multigraphs with
+  drained nodes and links, a WAN and a fabric, members of 1, 2 and 3 on one
+  GPU;
+* SpfSolver.buildRouteDb answered from the resident pass (spf_mplan_routes)
+  equals the one-node plan path (spf_routes), before and after a
+  publication drops the pass.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import NameTable, OracleLinkState, route_digests
+from openr_amd import topology as T
+from openr_amd.link_state import LinkState
+from openr_amd.spf_solver import PrefixEntry, PrefixState, SpfSolver
+
+pytestmark = pytest.mark.gpu
+
+GRAPHS = [
+    ("rand0", lambda: T.random_graph(60, 170, 12, max_metric=6, parallel_frac=0.25,
+                                     overload_frac=0.1, link_overload_frac=0.05)),
+    ("rand1", lambda: T.random_graph(45, 90, 7, max_metric=3, parallel_frac=0.1,
+                                     overload_frac=0.2)),
+    ("wan120", lambda: T.wan(120, 60, seed=8)),
+    ("fabric1000", lambda: T.fabric(1000, full=True)),
+]
+
+
+def sets_for(n, rng):
+    """Every node alone (loopbacks, node labels), then anycast sets."""
+    sets = [[v] for v in range(n)]
+    for _ in range(40):
+        sets.append(sorted(int(x) for x in rng.choice(n, int(rng.integers(2, 5)), replace=False)))
+    ptr = np.zeros(len(sets) + 1, np.uint32)
+    ptr[1:] = np.cumsum([len(s) for s in sets])
+    return ptr, np.concatenate([np.asarray(s, np.uint32) for s in sets])
+
+
+@pytest.mark.parametrize("name,make", GRAPHS, ids=[g[0] for g in GRAPHS])
+@pytest.mark.parametrize("members", [1, 2, 3])
+@pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
+def test_every_node_route_digests_match_oracle(name, make, members, lfa):
+    topo = make()
+    with LinkState(devices=[0] * members) as ls:
+        ls.updateAdjacencyDatabases(topo.lsdb)
+        ls.prefetchAllSources()
+        names = list(ls.flatten()[0])
+        ptr, nodes = sets_for(len(names), np.random.default_rng(len(names)))
+        got, ms = ls.allSourcesRouteDigests(ptr, nodes, lfa)
+        assert ms >= 0
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    want = route_digests(orc, NameTable(names), np.arange(len(names)), ptr, nodes, lfa)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} nodes differ, first {[names[i] for i in bad[:5]]}"
+    assert np.count_nonzero(want) > len(names) // 2  # routes exist
+
+
+@pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
+def test_route_db_from_resident_pass_equals_plan_path(lfa):
+    topo = T.random_graph(50, 140, 77, max_metric=4, parallel_frac=0.2, overload_frac=0.05)
+    ps = PrefixState()
+    rng = np.random.default_rng(2)
+    names = topo.nodes
+    for i, node in enumerate(names):
+        ps.updatePrefix(node, "0", PrefixEntry(f"fd00:{i:x}::/64"))
+    for i in range(10):  # anycast
+        for a in rng.choice(len(names), 3, replace=False):
+            ps.updatePrefix(names[int(a)], "0", PrefixEntry(f"fd01:{i:x}::/64"))
+
+    def rows(db):
+        return {p: sorted((n.ifName, n.metric, n.neighborNodeName) for n in r.nexthops)
+                for p, r in db.unicastRoutes.items()}
+
+    with LinkState(devices=[0, 0]) as res, LinkState() as one:
+        for ls in (res, one):
+            ls.updateAdjacencyDatabases(topo.lsdb)
+        res.prefetchAllSources()
+        for me in [names[int(i)] for i in rng.choice(len(names), 5, replace=False)]:
+            a = SpfSolver(me, True, lfa).buildRouteDb(me, {"0": res}, ps)
+            b = SpfSolver(me, True, lfa).buildRouteDb(me, {"0": one}, ps)
+            assert rows(a) == rows(b), me
+            assert {l: sorted((n.ifName, n.metric) for n in r.nexthops) for l, r in a.mplsRoutes.items()} \
+                == {l: sorted((n.ifName, n.metric) for n in r.nexthops) for l, r in b.mplsRoutes.items()}
+        # a publication drops the pass: the plan path answers, same routes
+        from openr_amd.wire import unpack
+
+        db0 = unpack(topo.lsdb)[0]
+        db0.isOverloaded = not db0.isOverloaded
+        res.updateAdjacencyDatabase(db0)
+        one.updateAdjacencyDatabase(db0)
+        me = names[3]
+        assert rows(SpfSolver(me, True, lfa).buildRouteDb(me, {"0": res}, ps)) == \
+            rows(SpfSolver(me, True, lfa).buildRouteDb(me, {"0": one}, ps))
