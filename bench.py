@@ -1084,7 +1084,29 @@ class FacadeRouteBuild:
         return self.e
 
     def cpu_baseline(self, budget_s: float):
-        return None
+        """The oracle's route selection for me towards every loopback with LFA
+        (its SPFs from me and each neighbour included), after the same
+        publication; the host route assembly (labels, MPLS routes) is not in
+        it, so this favours the CPU."""
+        sys.path.insert(0, str(ROOT / "tests"))
+        from oracle import NameTable, route_digests  # CPU baseline only
+
+        names = self.ls.flatten()[0]
+        set_ptr = np.arange(self.n + 1, dtype=np.uint32)
+        set_nodes = np.arange(self.n, dtype=np.uint32)
+        me = np.array([list(names).index(self.me)], dtype=np.int64)
+        orc = oracle()()
+        orc.update_packed(self.lsdb)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s or done == 0:
+            route_digests(orc, NameTable(names), me, set_ptr, set_nodes, True)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "route_builds/s", "cores": host_cores(), "kind": "port",
+                "sample": f"{done} route selections of {self.me} towards all {self.n} loopbacks with "
+                          f"LFA (SPF from {self.me} and its neighbours included; no host route "
+                          f"assembly), {dt:.1f} s on {host_cores()} cores of {cpu_model()} "
+                          f"(oracle/spf_oracle.cpp)"}
 
 
 def host_cores() -> int:

@@ -47,7 +47,6 @@ constexpr uint32_t kWaveCap = 1024;            // |D| a wave team can hold
 constexpr size_t kBigScratch = 8ull << 30;     // HBM budget of the workgroup teams (both sets)
 constexpr size_t kWaveScratch = 8ull << 30;    // HBM budget of the wave teams
 constexpr uint32_t kDialLevels = 1024;         // distinct distances settled bucket by bucket
-constexpr uint32_t kHubDeg = 32;               // nodes above this degree get a whole wave
 
 __device__ __forceinline__ uint32_t ld(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -73,16 +72,6 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ uint64_t node_hash(uint32_t v, uint32_t d, const uint32_t* nh,
-                                              uint32_t W) {
-  uint64_t f = 0xcbf29ce484222325ull;
-  for (uint32_t w = 0; w < W; ++w) {
-    f ^= nh[w];
-    f *= 0x100000001b3ull;
-  }
-  return mix64(mix64((uint64_t)v + 1) + d) ^ f;
 }
 
 struct WiGraph {
@@ -874,6 +863,71 @@ __device__ __forceinline__ void stq(unsigned long long* p, unsigned long long v)
   else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ---------------------------------------------------------------------------
+//  wave helpers of the repairs: lanes over flattened edges
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_pull(uint32_t x, uint32_t k) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)x);
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The edges of up to 64 nodes (lane k holds node v, `valid`), flattened:
+// chunks of 64 (node slot, edge) pairs.  f(k, e, act) runs on every lane of
+// the wave (so it may ballot / pull); `act` marks the lanes holding an edge,
+// k is the node slot (lane) that edge belongs to.  All 64 lanes must be
+// active.
+template <class F>
+__device__ __forceinline__ void wave_edges(const uint32_t* __restrict__ row_ptr, uint32_t v,
+                                           bool valid, F&& f) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t b0 = 0, deg = 0;
+  if (valid) {
+    b0 = row_ptr[v];
+    deg = row_ptr[v + 1] - b0;
+  }
+  const uint32_t incl = wave_incl_scan32(deg);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  const uint32_t excl = incl - deg;
+  for (uint32_t base = 0; base < total; base += 64) {
+    const uint32_t s = base + lane;
+    // owner: the last slot whose first edge is <= s (slots with no edges
+    // share their successor's offset and lose to it)
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+      if (lane_pull(excl, k + step) <= s) k += step;
+    const uint32_t e = lane_pull(b0, k) + s - lane_pull(excl, k);
+    f(k, e, s < total);
+  }
+}
+
+// FNV-1a of both next-hop rows of a D node and whether they differ: the
+// words in batches of 8, loads of a batch in flight together.  A node's hash
+// is mix64(mix64(v + 1) + d) ^ FNV-1a(row), as in the base pass's result hash.
+template <bool GROUP>
+__device__ __forceinline__ void row_pair_hash(const uint32_t* h0, const uint32_t* h1, uint32_t W,
+                                              uint64_t& f0, uint64_t& f1, bool& diff) {
+  f0 = f1 = 0xcbf29ce484222325ull;
+  for (uint32_t w = 0; w < W; w += 8) {
+    uint32_t a[8], c[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      a[q] = w + q < W ? h0[w + q] : 0u;
+      c[q] = w + q < W ? ldw<GROUP>(&h1[w + q]) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (w + q < W) {
+        f0 = (f0 ^ a[q]) * 0x100000001b3ull;
+        f1 = (f1 ^ c[q]) * 0x100000001b3ull;
+        diff |= a[q] != c[q];
+      }
+    }
+  }
+}
+
 // CHK (the profiled wave instance, SPF_WHATIF_PROF): every scratch-derived
 // index is range-checked before use; an out-of-range one sets bit 4 of the
 // fault word with the site in bits 16-23 and is replaced by a safe value
@@ -898,7 +952,6 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }                                            \
   } while (0)
   const uint32_t W = g.W;
-  constexpr uint32_t kWaves = TEAM / 64;
   // range check (CHK): x < lim, or x == kInf when `inf_ok`
   auto chk = [&](uint32_t x, uint32_t lim, bool inf_ok, uint32_t site, uint32_t safe) -> uint32_t {
     if constexpr (CHK) {
@@ -944,43 +997,40 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (tt == 0) loop_bound_hit(g.fault, 1);
       break;
     }
-    // a thread per frontier node; hubs (thousands of edges) are queued in
-    // ord and expanded by a whole wave each
-    auto child = [&](uint32_t dv, uint32_t e) {
-      const uint32_t c = g.col[e];
-      if (dv + g.wt[e] != B.dist[c]) return;
-      if (atomicCAS(&mark[c], kInf, kBusy) != kInf) return;
-      const uint32_t idx = atomicAdd(&ctl->n, 1u);
-      if (idx < cap) {
-        dlist[idx] = c;
-        stw<GROUP>(&mark[c], idx);
-      } else {
-        stw<GROUP>(&mark[c], kInf);
-        stw<GROUP>(&ctl->ovf, 1u);
-      }
-    };
-    for (uint32_t i = lo + tt; i < n; i += TEAM) {
-      const uint32_t v = chk(dlist[i], g.N, false, 1, b);
-      if (g.ovl[v]) continue;  // drained (v != src): no DAG children
-      const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
-      if (b1 - b0 > kHubDeg) {
-        stw<GROUP>(&ord[atomicAdd(&ctl->hub, 1u)], i);
-        continue;
-      }
-      const uint32_t dv = B.dist[v];
-      for (uint32_t e = b0; e < b1; ++e) child(dv, e);
+    // each wave takes 64 frontier nodes at a time, lanes over their
+    // flattened edges (wave_edges); new nodes are appended by one counter
+    // atomic per wave
+    for (uint32_t c0 = lo + wv * 64; c0 < n; c0 += TEAM) {
+      const uint32_t i = c0 + lane;
+      const uint32_t v = i < n ? chk(dlist[i], g.N, false, 1, b) : 0u;
+      const bool x = i < n && !g.ovl[v];  // drained (v != src): no DAG children
+      const uint32_t dv = x ? B.dist[v] : 0u;
+      wave_edges(g.row_ptr, v, x, [&](uint32_t k, uint32_t e, bool act) {
+        const uint32_t dk = lane_pull(dv, k);
+        uint32_t c = 0;
+        bool won = false;
+        if (act) {
+          c = g.col[e];
+          if (dk + g.wt[e] == B.dist[c]) won = atomicCAS(&mark[c], kInf, kBusy) == kInf;
+        }
+        const uint64_t wm = __ballot(won);
+        if (wm) {
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(&ctl->n, (uint32_t)__popcll(wm));
+          base = __builtin_amdgcn_readlane(base, 0);
+          if (won) {
+            const uint32_t idx = base + lanes_below(wm);
+            if (idx < cap) {
+              dlist[idx] = c;
+              stw<GROUP>(&mark[c], idx);
+            } else {
+              stw<GROUP>(&mark[c], kInf);
+              stw<GROUP>(&ctl->ovf, 1u);
+            }
+          }
+        }
+      });
     }
-    team_sync<TEAM, GROUP>(ctl, g.fault);
-    {
-      const uint32_t nh_ = ldw<GROUP>(&ctl->hub);
-      for (uint32_t k = wv; k < nh_; k += kWaves) {
-        const uint32_t v = chk(dlist[chk(ldw<GROUP>(&ord[k]), n, false, 2, 0)], g.N, false, 3, b);
-        const uint32_t dv = B.dist[v];
-        for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) child(dv, e);
-      }
-    }
-    team_sync<TEAM, GROUP>(ctl, g.fault);
-    if (tt == 0) stw<GROUP>(&ctl->hub, 0u);
     lo = n;
     team_sync<TEAM, GROUP>(ctl, g.fault);
   }
@@ -1000,40 +1050,31 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     return false;
   }
   // ---- seeds: best in-edge from outside D (unchanged distances) ----
-  auto seed_edge = [&](uint32_t e) -> uint32_t {
-    if (g.link[e] == l) return kInf;
-    const uint32_t u = g.col[e];
-    if (ldw<GROUP>(&mark[u]) != kInf) return kInf;
-    if (g.ovl[u] && u != g.src) return kInf;
-    const uint32_t du = B.dist[u];
-    return du == kInf ? kInf : du + g.wt[g.rev[e]];
-  };
-  for (uint32_t i = tt; i < n; i += TEAM) {
-    const uint32_t v = dlist[i];
-    const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
-    if (b1 - b0 > kHubDeg) {
-      stw<GROUP>(&ord[atomicAdd(&ctl->hub, 1u)], i);
-      continue;
-    }
-    uint32_t best = kInf;
-    for (uint32_t e = b0; e < b1; ++e) best = min(best, seed_edge(e));
-    stw<GROUP>(&dnew[i], best);
+  // waves over 64 D nodes at a time, lanes over their flattened in-edges,
+  // the per-node minimum by atomics on dnew
+  for (uint32_t i = tt; i < n; i += TEAM) stw<GROUP>(&dnew[i], kInf);
+  team_sync<TEAM, GROUP>(ctl, g.fault);
+  for (uint32_t c0 = wv * 64; c0 < n; c0 += TEAM) {
+    const uint32_t i = c0 + lane;
+    const uint32_t v = i < n ? dlist[i] : 0u;
+    wave_edges(g.row_ptr, v, i < n, [&](uint32_t k, uint32_t e, bool act) {
+      uint32_t s = kInf;
+      if (act && g.link[e] != l) {
+        const uint32_t u = g.col[e];
+        if (ldw<GROUP>(&mark[u]) == kInf && !(g.ovl[u] && u != g.src)) {
+          const uint32_t du = B.dist[u];
+          if (du != kInf) s = du + g.wt[g.rev[e]];
+        }
+      }
+      if (s != kInf) {
+        if constexpr (GROUP)
+          __hip_atomic_fetch_min(&dnew[c0 + k], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_fetch_min(&dnew[c0 + k], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    });
   }
   team_sync<TEAM, GROUP>(ctl, g.fault);
-  {
-    const uint32_t nh_ = ldw<GROUP>(&ctl->hub);
-    for (uint32_t k = wv; k < nh_; k += kWaves) {
-      const uint32_t i = chk(ldw<GROUP>(&ord[k]), n, false, 4, 0);
-      const uint32_t v = dlist[i];
-      uint32_t best = kInf;
-      for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64)
-        best = min(best, seed_edge(e));
-      best = wave_min32(best);
-      if (lane == 0) stw<GROUP>(&dnew[i], best);
-    }
-  }
-  team_sync<TEAM, GROUP>(ctl, g.fault);
-  if (tt == 0) stw<GROUP>(&ctl->hub, 0u);
   // nh word j of a D node from its tight expanded predecessors (D or not);
   // used by the fixed-point fallback
   auto nh_of = [&](uint32_t i, uint32_t j) -> uint32_t {
@@ -1055,51 +1096,6 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       }
     }
     return acc;
-  };
-  // nh row of a D node whose distance is final, every tight predecessor's
-  // row final too: one thread per node, the W words in a loop
-  auto nh_row = [&](uint32_t i, uint32_t v, uint32_t dv) {
-    uint32_t* row = nhn + (size_t)i * W;
-    for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e) {
-      if (g.link[e] == l) continue;
-      const uint32_t u = g.col[e];
-      if (g.ovl[u] && u != g.src) continue;
-      const uint32_t mu = chk(ldw<GROUP>(&mark[u]), n, true, 6, kInf);
-      const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
-      if (du == kInf || du + in_w(g, e) != dv) continue;
-      if (u == g.src) {
-        const uint32_t jb = chk(g.nbr_bit[v], 32 * W, false, 7, 0);
-        row[jb >> 5] |= 1u << (jb & 31);
-      } else {
-        const uint32_t* from = mu != kInf ? nhn + (size_t)mu * W : B.nhb + (size_t)u * W;
-        // row and from may alias as far as the compiler knows: batches of 8
-        // loads ahead of their stores keep the loads in flight together
-        // instead of one load-OR-store round trip per word
-        // (wave teams: batches of 4, the registers they can spare beside the
-        // group teams sharing their SIMDs)
-        uint32_t j = 0;
-        if (TEAM >= 512)
-          for (; j + 8 <= W; j += 8) {
-            uint32_t f[8], r[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) f[q] = from[j + q];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) r[q] = row[j + q];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) row[j + q] = r[q] | f[q];
-          }
-        for (; j + 4 <= W; j += 4) {
-          uint32_t f[4], r[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) f[q] = from[j + q];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) r[q] = row[j + q];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) row[j + q] = r[q] | f[q];
-        }
-        for (; j < W; ++j) row[j] |= from[j];
-      }
-    }
   };
   const size_t nw = (size_t)n * W;
   for (size_t x = tt; x < nw; x += TEAM) nhn[x] = 0;
@@ -1130,75 +1126,70 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     if (tt == 0) {  // the next level's slots, last read two levels ago
       stw<GROUP>(&ctl->nxt[(it + 1) % 3], kInf);
       stw<GROUP>(&ctl->lc[(it + 1) % 3], 0u);
-      stw<GROUP>(&ctl->lc[(it + 2) % 3], 0u);  // this level's hub counter
     }
-    // (a) the level's nodes (their distance is final) into ord
+    // (a) the level's nodes (their distance is final) into ord, one counter
+    // atomic per wave
     uint32_t m = kInf;
-    for (uint32_t i = tt; i < n; i += TEAM) {
-      const uint32_t d = ldw<GROUP>(&dnew[i]);
-      if (d == t) stw<GROUP>(&ord[atomicAdd(cnt, 1u)], i);
-      else if (d != kInf && d > t) m = min(m, d);
-    }
-    team_sync<TEAM, GROUP>(ctl, g.fault);
-    // (b) level nodes: next hops from their tight predecessors, then relax
-    // their edges.  A thread per node; hubs (queued after the level list)
-    // by a whole wave: ballot over the in-edges, coalesced row ORs.
-    const uint32_t K = ldw<GROUP>(cnt);
-    uint32_t* hubs = ord + K;
-    uint32_t* hub_cnt = &ctl->lc[(it + 2) % 3];  // free this level
-    auto relax = [&](uint32_t v, uint32_t e) {
-      if (g.link[e] == l) return;
-      const uint32_t ic = chk(ldw<GROUP>(&mark[g.col[e]]), n, true, 8, kInf);
-      if (ic == kInf) return;
-      const uint32_t nd = t + g.wt[e];
-      if (nd < atomicMin(&dnew[ic], nd)) m = min(m, nd);
-    };
-    for (uint32_t k = tt; k < K; k += TEAM) {
-      const uint32_t i = chk(ldw<GROUP>(&ord[k]), n, false, 9, 0);
-      const uint32_t v = chk(dlist[i], g.N, false, 10, b);
-      const uint32_t b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
-      if (b1 - b0 > kHubDeg) {
-        stw<GROUP>(&hubs[atomicAdd(hub_cnt, 1u)], i);
-        continue;
+    for (uint32_t c0 = wv * 64; c0 < n; c0 += TEAM) {
+      const uint32_t i = c0 + lane;
+      const uint32_t d = i < n ? ldw<GROUP>(&dnew[i]) : kInf;
+      const bool sel = d == t;
+      if (d != kInf && d > t) m = min(m, d);
+      const uint64_t sm = __ballot(sel);
+      if (sm) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(sm));
+        base = __builtin_amdgcn_readlane(base, 0);
+        if (sel) stw<GROUP>(&ord[base + lanes_below(sm)], i);
       }
-      nh_row(i, v, t);
-      if (!g.ovl[v])
-        for (uint32_t e = b0; e < b1; ++e) relax(v, e);
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    const uint32_t H_ = ldw<GROUP>(hub_cnt);
-    for (uint32_t k = wv; k < H_; k += kWaves) {
-      const uint32_t i = chk(ldw<GROUP>(&hubs[k]), n, false, 11, 0);
-      const uint32_t v = chk(dlist[i], g.N, false, 12, b);
-      uint32_t* row = nhn + (size_t)i * W;
-      const uint32_t jb = g.nbr_bit[v];
-      bool from_src = false;
-      for (uint32_t base = g.row_ptr[v]; base < g.row_ptr[v + 1]; base += 64) {
-        const uint32_t e = base + lane;
+    // (b) level nodes, 64 per wave at a time, lanes over their flattened
+    // edges: tight predecessors give the next-hop rows (one pair at a time,
+    // coalesced row ORs), out-edges relax the pending nodes
+    const uint32_t K = ldw<GROUP>(cnt);
+    for (uint32_t q0 = wv * 64; q0 < K; q0 += TEAM) {
+      const uint32_t q = q0 + lane;
+      const bool valid = q < K;
+      const uint32_t i = valid ? chk(ldw<GROUP>(&ord[q]), n, false, 9, 0) : 0u;
+      const uint32_t v = valid ? chk(dlist[i], g.N, false, 10, b) : 0u;
+      const uint32_t transit = valid && !g.ovl[v];  // drained: no transit
+      const uint32_t jb = valid ? g.nbr_bit[v] : 0u;
+      wave_edges(g.row_ptr, v, valid, [&](uint32_t k, uint32_t e, bool act) {
+        const uint32_t ik = lane_pull(i, k), tk = lane_pull(transit, k), jk = lane_pull(jb, k);
         uint32_t u = 0, mu = kInf;
-        bool tight = false;
-        if (e < g.row_ptr[v + 1] && g.link[e] != l) {
+        bool tight = false, from_src = false;
+        if (act && g.link[e] != l) {
           u = g.col[e];
+          mu = chk(ldw<GROUP>(&mark[u]), n, true, 13, kInf);
           if (!(g.ovl[u] && u != g.src)) {
-            mu = chk(ldw<GROUP>(&mark[u]), n, true, 13, kInf);
             const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
-            tight = du != kInf && du + g.wt[g.rev[e]] == t;
+            tight = du != kInf && du + in_w(g, e) == t;
+          }
+          if (tk && mu != kInf) {  // relax v -> u (u pending: its value only drops)
+            const uint32_t nd = t + g.wt[e];
+            if (nd < atomicMin(&dnew[mu], nd)) m = min(m, nd);
+          }
+          if (tight && u == g.src) {
+            from_src = true;
+            tight = false;
           }
         }
-        if (tight && u == g.src) {
-          from_src = true;
-          tight = false;
+        for (uint64_t pm = __ballot(tight) | __ballot(from_src); pm; pm &= pm - 1) {
+          const uint32_t bl = __ffsll((unsigned long long)pm) - 1;
+          const uint32_t pi = __builtin_amdgcn_readlane(ik, bl);
+          uint32_t* row = nhn + (size_t)pi * W;
+          if (__builtin_amdgcn_readlane((uint32_t)from_src, bl)) {
+            const uint32_t pj = __builtin_amdgcn_readlane(jk, bl);
+            const uint32_t wj = chk(pj >> 5, W, false, 7, 0);
+            if (lane == (wj & 63)) row[wj] |= 1u << (pj & 31);
+          } else {
+            const uint32_t pu = __builtin_amdgcn_readlane(u, bl), pmu = __builtin_amdgcn_readlane(mu, bl);
+            const uint32_t* from = pmu != kInf ? nhn + (size_t)pmu * W : B.nhb + (size_t)pu * W;
+            for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
+          }
         }
-        for (uint64_t mask = __ballot(tight); mask; mask &= mask - 1) {
-          const uint32_t b = __ffsll((unsigned long long)mask) - 1;
-          const uint32_t pu = __builtin_amdgcn_readlane(u, b), pm = __builtin_amdgcn_readlane(mu, b);
-          const uint32_t* from = pm != kInf ? nhn + (size_t)pm * W : B.nhb + (size_t)pu * W;
-          for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
-        }
-      }
-      if (__ballot(from_src) && lane == ((jb >> 5) & 63)) row[jb >> 5] |= 1u << (jb & 31);
-      if (g.ovl[v]) continue;  // drained: no transit
-      for (uint32_t e = g.row_ptr[v] + lane; e < g.row_ptr[v + 1]; e += 64) relax(v, e);
+      });
     }
     if (m != kInf) atomicMin(next, m);
     team_sync<TEAM, GROUP>(ctl, g.fault);
@@ -1319,13 +1310,13 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   for (uint32_t i = tt; i < n; i += TEAM) {
     const uint32_t v = dlist[i];
     const uint32_t d1 = ldw<GROUP>(&dnew[i]), d0 = B.dist[v];
-    const uint32_t* h0 = B.nhb + (size_t)v * W;
-    const uint32_t* h1 = nhn + (size_t)i * W;
-    nd_ += d1 != d0;
+    uint64_t f0, f1;
     bool diff = d1 == kInf;
-    for (uint32_t w = 0; w < W && !diff; ++w) diff = h0[w] != h1[w];
+    row_pair_hash<GROUP>(B.nhb + (size_t)v * W, nhn + (size_t)i * W, W, f0, f1, diff);
+    const uint64_t base = mix64((uint64_t)v + 1);
+    nd_ += d1 != d0;
     nn_ += diff;
-    dh += (d1 == kInf ? 0ull : node_hash(v, d1, h1, W)) - node_hash(v, d0, h0, W);
+    dh += (d1 == kInf ? 0ull : mix64(base + d1) ^ f1) - (mix64(base + d0) ^ f0);
     stw<GROUP>(&mark[v], kInf);
   }
   if (nd_) atomicAdd(&ctl->ndist, (unsigned long long)nd_);
@@ -1336,6 +1327,251 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     *out = spf_whatif_digest{(uint32_t)ldq<GROUP>(&ctl->ndist), (uint32_t)ldq<GROUP>(&ctl->nnh),
                              (uint64_t)(*B.H + ldq<GROUP>(&ctl->dh))};
   team_sync<TEAM, GROUP>(ctl, g.fault);
+  WI_STAMP(5);
+#undef WI_STAMP
+  return true;
+}
+
+// A wave team's repair (|D| <= cap): repair()'s three phases -- D discovery,
+// seeds, Dial with next hops inline -- and its digest delta, bit for bit, but
+// with the wave's lanes over the flattened edges of up to 64 nodes at a time
+// (wave_edges) instead of a lane per node walking its edges one by one: a
+// node's dependent chain (row_ptr -> col -> mark -> dnew / base row) is paid
+// once per 64 edges instead of once per edge.  The team is one wave, so |D|,
+// the level list length and the next Dial value live in registers
+// (ballot + mbcnt compaction instead of counter atomics); the level list of
+// a D of <= 64 nodes never leaves the registers (ds_permute).  |D| <= cap <=
+// kDialLevels distinct values, so Dial always settles (no fallback sweeps).
+template <bool CHK>
+__device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
+                            uint32_t* dnew, uint32_t* nhn, uint32_t* ord, uint32_t cap,
+                            TeamCtl* ctl, uint32_t lane, uint32_t e_fail, spf_whatif_digest* out,
+                            uint64_t* ph) {
+  uint64_t tprev = ph ? wall_clock64() : 0ull;
+#define WI_STAMP(k)                              \
+  do {                                           \
+    if (ph) {                                    \
+      const uint64_t now_ = wall_clock64();      \
+      ph[k] += now_ - tprev;                     \
+      tprev = now_;                              \
+    }                                            \
+  } while (0)
+  auto chk = [&](uint32_t x, uint32_t lim, bool inf_ok, uint32_t site, uint32_t safe) -> uint32_t {
+    if constexpr (CHK) {
+      if (!(x < lim || (inf_ok && x == kInf))) {
+        if (g.fault)
+          __hip_atomic_fetch_or(g.fault, 16u | (site << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return safe;
+      }
+    }
+    return x;
+  };
+  auto sync = [&]() { team_sync<64>(ctl, g.fault); };
+  const uint32_t W = g.W;
+  const uint32_t l = g.link[e_fail];
+  const uint32_t b = g.col[e_fail];
+  if (lane == 0) {
+    dlist[0] = b;
+    stw<false>(&mark[b], 0u);
+    stq<false>(&ctl->ndist, 0ull);
+    stq<false>(&ctl->nnh, 0ull);
+    stq<false>(&ctl->dh, 0ull);
+  }
+  sync();
+  // ---- D = descendants of b in the unfailed DAG, frontier by frontier ----
+  uint32_t n = 1, lo = 0;
+  bool bad = false;
+  for (uint32_t iter = 0; lo < n && n <= cap; ++iter) {
+    if (iter > cap + 2) {  // wave-uniform
+      bad = true;
+      if (lane == 0) loop_bound_hit(g.fault, 1);
+      break;
+    }
+    const uint32_t hi = n;
+    for (uint32_t c0 = lo; c0 < hi && n <= cap; c0 += 64) {
+      const uint32_t i = c0 + lane;
+      const uint32_t v = i < hi ? chk(ldw<false>(&dlist[i]), g.N, false, 1, b) : 0u;
+      const bool x = i < hi && !g.ovl[v];  // drained (v != src): no DAG children
+      const uint32_t dv = x ? B.dist[v] : 0u;
+      wave_edges(g.row_ptr, v, x, [&](uint32_t k, uint32_t e, bool act) {
+        const uint32_t dk = lane_pull(dv, k);
+        uint32_t c = 0;
+        bool won = false;
+        if (act) {
+          c = g.col[e];
+          if (dk + g.wt[e] == B.dist[c]) won = atomicCAS(&mark[c], kInf, kBusy) == kInf;
+        }
+        const uint64_t wm = __ballot(won);
+        if (won) {
+          const uint32_t idx = n + lanes_below(wm);
+          if (idx < cap) {
+            dlist[idx] = c;
+            stw<false>(&mark[c], idx);
+          } else {
+            stw<false>(&mark[c], kInf);
+          }
+        }
+        n += (uint32_t)__popcll(wm);
+      });
+    }
+    lo = hi;
+    sync();
+  }
+  const bool ovf = n > cap || bad;
+  n = min(n, cap);
+  WI_STAMP(1);
+  if (ph) {
+    ph[0] += 1;
+    ph[8] += n;
+    ph[10] = ph[10] > n ? ph[10] : (uint64_t)n;
+    ph[11] += ovf;
+  }
+  if (ovf) {
+    for (uint32_t i = lane; i < n; i += 64) stw<false>(&mark[ldw<false>(&dlist[i])], kInf);
+    sync();
+    return false;
+  }
+  // ---- seeds: best in-edge from outside D (unchanged distances) ----
+  for (uint32_t i = lane; i < n; i += 64) stw<false>(&dnew[i], kInf);
+  for (size_t x = lane; x < (size_t)n * W; x += 64) nhn[x] = 0;
+  sync();
+  for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const uint32_t v = i < n ? ldw<false>(&dlist[i]) : 0u;
+    wave_edges(g.row_ptr, v, i < n, [&](uint32_t k, uint32_t e, bool act) {
+      uint32_t s = kInf;
+      if (act && g.link[e] != l) {
+        const uint32_t u = g.col[e];
+        if (ldw<false>(&mark[u]) == kInf && !(g.ovl[u] && u != g.src)) {
+          const uint32_t du = B.dist[u];
+          if (du != kInf) s = du + g.wt[g.rev[e]];
+        }
+      }
+      if (s != kInf)
+        __hip_atomic_fetch_min(&dnew[c0 + k], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    });
+  }
+  sync();
+  // the D of <= 64 nodes stays in registers through Dial: lane i holds D
+  // node i (index, node, the source-neighbour bit)
+  const bool small = n <= 64;
+  const uint32_t sv = small && lane < n ? ldw<false>(&dlist[lane]) : 0u;
+  uint32_t t = kInf;
+  for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    t = min(t, i < n ? ldw<false>(&dnew[i]) : kInf);
+  }
+  t = wave_min32(t);
+  WI_STAMP(2);
+  // ---- Dial: settle D one distance value at a time (metrics are positive:
+  // a node holding the smallest pending value is final), next hops inline ----
+  for (uint32_t it = 0; t != kInf; ++it) {
+    if (it > n + 2) {  // every level settles a node: cannot happen
+      if (lane == 0) loop_bound_hit(g.fault, 4);
+      break;
+    }
+    // (a) the level's nodes (their distance is final) and the next value
+    uint32_t m = kInf, K = 0, li = 0, lv = 0;
+    if (small) {
+      const uint32_t d = lane < n ? ldw<false>(&dnew[lane]) : kInf;
+      const bool sel = d == t;
+      if (d != kInf && d > t) m = d;
+      const uint64_t sm = __ballot(sel);
+      K = (uint32_t)__popcll(sm);
+      // compact: the r-th level node to lane r, the rest after them
+      const uint32_t r = lanes_below(sm);
+      const uint32_t dst = sel ? r : K + lane - r;
+      li = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)lane);
+      lv = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)sv);
+    } else {
+      for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t i = c0 + lane;
+        const uint32_t d = i < n ? ldw<false>(&dnew[i]) : kInf;
+        const bool sel = d == t;
+        if (d != kInf && d > t) m = min(m, d);
+        const uint64_t sm = __ballot(sel);
+        if (sel) stw<false>(&ord[K + lanes_below(sm)], i);
+        K += (uint32_t)__popcll(sm);
+      }
+      sync();
+    }
+    // (b) level nodes, 64 at a time: tight predecessors give the next-hop
+    // rows, out-edges relax the pending nodes
+    for (uint32_t q0 = 0; q0 < K; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      const bool valid = q < K;
+      uint32_t i = li, v = lv;
+      if (!small) {
+        i = valid ? chk(ldw<false>(&ord[q]), n, false, 9, 0) : 0u;
+        v = valid ? chk(ldw<false>(&dlist[i]), g.N, false, 10, b) : 0u;
+      }
+      const uint32_t transit = valid && !g.ovl[v];  // drained: no transit
+      const uint32_t jb = valid ? g.nbr_bit[v] : 0u;
+      wave_edges(g.row_ptr, v, valid, [&](uint32_t k, uint32_t e, bool act) {
+        const uint32_t ik = lane_pull(i, k), tk = lane_pull(transit, k), jk = lane_pull(jb, k);
+        uint32_t u = 0, mu = kInf;
+        bool tight = false, from_src = false;
+        if (act && g.link[e] != l) {
+          u = g.col[e];
+          mu = chk(ldw<false>(&mark[u]), n, true, 13, kInf);
+          if (!(g.ovl[u] && u != g.src)) {
+            const uint32_t du = mu != kInf ? ldw<false>(&dnew[mu]) : B.dist[u];
+            tight = du != kInf && du + in_w(g, e) == t;
+          }
+          if (tk && mu != kInf) {  // relax v -> u (u pending: its value only drops)
+            const uint32_t nd = t + g.wt[e];
+            if (nd < atomicMin(&dnew[mu], nd)) m = min(m, nd);
+          }
+          if (tight && u == g.src) {
+            from_src = true;
+            tight = false;
+          }
+        }
+        // the row ORs, one tight pair at a time in lane order
+        for (uint64_t pm = __ballot(tight) | __ballot(from_src); pm; pm &= pm - 1) {
+          const uint32_t bl = __ffsll((unsigned long long)pm) - 1;
+          const uint32_t pi = __builtin_amdgcn_readlane(ik, bl);
+          uint32_t* row = nhn + (size_t)pi * W;
+          if (__builtin_amdgcn_readlane((uint32_t)from_src, bl)) {
+            const uint32_t pj = __builtin_amdgcn_readlane(jk, bl);
+            const uint32_t wj = chk(pj >> 5, W, false, 7, 0);
+            if (lane == (wj & 63)) row[wj] |= 1u << (pj & 31);
+          } else {
+            const uint32_t pu = __builtin_amdgcn_readlane(u, bl), pmu = __builtin_amdgcn_readlane(mu, bl);
+            const uint32_t* from = pmu != kInf ? nhn + (size_t)pmu * W : B.nhb + (size_t)pu * W;
+            for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
+          }
+        }
+      });
+    }
+    sync();
+    t = wave_min32(m);
+    if (ph) ph[9] += 1;
+  }
+  WI_STAMP(3);
+  // ---- digest delta over D, scratch reset ----
+  uint32_t nd_ = 0, nn_ = 0;
+  uint64_t dh = 0;
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t v = ldw<false>(&dlist[i]);
+    const uint32_t d1 = ldw<false>(&dnew[i]), d0 = B.dist[v];
+    uint64_t f0, f1;
+    bool diff = d1 == kInf;
+    row_pair_hash<false>(B.nhb + (size_t)v * W, nhn + (size_t)i * W, W, f0, f1, diff);
+    const uint64_t base = mix64((uint64_t)v + 1);
+    nd_ += d1 != d0;
+    nn_ += diff;
+    dh += (d1 == kInf ? 0ull : mix64(base + d1) ^ f1) - (mix64(base + d0) ^ f0);
+    stw<false>(&mark[v], kInf);
+  }
+  if (nd_) atomicAdd(&ctl->ndist, (unsigned long long)nd_);
+  if (nn_) atomicAdd(&ctl->nnh, (unsigned long long)nn_);
+  if (dh) atomicAdd(&ctl->dh, (unsigned long long)dh);
+  sync();
+  if (lane == 0)
+    *out = spf_whatif_digest{(uint32_t)ldq<false>(&ctl->ndist), (uint32_t)ldq<false>(&ctl->nnh),
+                             (uint64_t)(*B.H + ldq<false>(&ctl->dh))};
+  sync();
   WI_STAMP(5);
 #undef WI_STAMP
   return true;
@@ -1369,8 +1605,8 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
     k = __builtin_amdgcn_readlane(k, 0);
     if (k >= total) break;
     const uint2 h = hot[k];
-    if (!repair<64, false, PROF>(g, B, mark, dlist, dnew, nhn, lvl, ord, cap, &ctl[w], lane, h.y,
-                                 out + h.x, PROF ? ph : nullptr)) {
+    if (!repair_wave<PROF>(g, B, mark, dlist, dnew, nhn, ord, cap, &ctl[w], lane, h.y, out + h.x,
+                           PROF ? ph : nullptr)) {
       if (lane == 0) big[atomicAdd(n_big, 1u)] = h;
     }
   }
