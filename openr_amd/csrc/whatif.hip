@@ -928,6 +928,70 @@ __device__ __forceinline__ void row_pair_hash(const uint32_t* h0, const uint32_t
   }
 }
 
+// The next-hop row ORs of one flattened edge chunk's tight pairs (lanes in
+// pm: a tight predecessor u / its D index mu; lanes in sm: the source itself,
+// jk = the node's source-neighbour bit), in lane order.  A pair belongs to D
+// node ik.  W <= 64: lane j keeps word j of the current node's row in `acc`
+// (`cur` = that node's D index, kInf for none), the loads of 8 pairs in
+// flight together, and the row is stored once, when the node changes (a
+// node's pairs are contiguous in flattened order, its row is zero before its
+// level, and one wave builds it): the caller flushes the last one.  W > 64:
+// a read-modify-write of the row per pair.
+__device__ __forceinline__ void row_pairs(uint64_t pm, uint64_t sm, uint32_t ik, uint32_t jk,
+                                          uint32_t u, uint32_t mu, uint32_t W, uint32_t* nhn,
+                                          const uint32_t* nhb, uint32_t lane, uint32_t& cur,
+                                          uint32_t& acc) {
+  pm |= sm;
+  if (W <= 64) {
+    while (pm) {  // wave-uniform
+      uint32_t pi[8], pj[8], x[8];
+      bool pv[8], ps[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        pv[q] = pm != 0;
+        ps[q] = false;
+        pi[q] = pj[q] = x[q] = 0;
+        if (pv[q]) {
+          const uint32_t bl = __ffsll((unsigned long long)pm) - 1;
+          pm &= pm - 1;
+          pi[q] = __builtin_amdgcn_readlane(ik, bl);
+          ps[q] = (sm >> bl) & 1;
+          if (ps[q]) {
+            pj[q] = __builtin_amdgcn_readlane(jk, bl);
+          } else {
+            const uint32_t pu = __builtin_amdgcn_readlane(u, bl), pmu = __builtin_amdgcn_readlane(mu, bl);
+            const uint32_t* from = pmu != kInf ? nhn + (size_t)pmu * W : nhb + (size_t)pu * W;
+            if (lane < W) x[q] = from[lane];
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (!pv[q]) continue;
+        if (pi[q] != cur) {
+          if (cur != kInf && lane < W) nhn[(size_t)cur * W + lane] = acc;
+          cur = pi[q];
+          acc = 0;
+        }
+        acc |= ps[q] ? (lane == (pj[q] >> 5) ? 1u << (pj[q] & 31) : 0u) : x[q];
+      }
+    }
+  } else {
+    for (; pm; pm &= pm - 1) {
+      const uint32_t bl = __ffsll((unsigned long long)pm) - 1;
+      uint32_t* row = nhn + (size_t)__builtin_amdgcn_readlane(ik, bl) * W;
+      if ((sm >> bl) & 1) {
+        const uint32_t pj = __builtin_amdgcn_readlane(jk, bl);
+        if (lane == ((pj >> 5) & 63) && (pj >> 5) < W) row[pj >> 5] |= 1u << (pj & 31);
+      } else {
+        const uint32_t pu = __builtin_amdgcn_readlane(u, bl), pmu = __builtin_amdgcn_readlane(mu, bl);
+        const uint32_t* from = pmu != kInf ? nhn + (size_t)pmu * W : nhb + (size_t)pu * W;
+        for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
+      }
+    }
+  }
+}
+
 // CHK (the profiled wave instance, SPF_WHATIF_PROF): every scratch-derived
 // index is range-checked before use; an out-of-range one sets bit 4 of the
 // fault word with the site in bits 16-23 and is replaced by a safe value
@@ -1129,18 +1193,32 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     }
     // (a) the level's nodes (their distance is final) into ord, one counter
     // atomic per wave
+    // (4 chunks per pass: their loads in flight together, one atomic)
     uint32_t m = kInf;
-    for (uint32_t c0 = wv * 64; c0 < n; c0 += TEAM) {
-      const uint32_t i = c0 + lane;
-      const uint32_t d = i < n ? ldw<GROUP>(&dnew[i]) : kInf;
-      const bool sel = d == t;
-      if (d != kInf && d > t) m = min(m, d);
-      const uint64_t sm = __ballot(sel);
-      if (sm) {
+    for (uint32_t c0 = wv * 64; c0 < n; c0 += 4 * TEAM) {
+      uint32_t d[4];
+      uint64_t sm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t i = c0 + q * TEAM + lane;
+        d[q] = i < n ? ldw<GROUP>(&dnew[i]) : kInf;
+      }
+      uint32_t tot = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (d[q] != kInf && d[q] > t) m = min(m, d[q]);
+        sm[q] = __ballot(d[q] == t);
+        tot += (uint32_t)__popcll(sm[q]);
+      }
+      if (tot) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(sm));
+        if (lane == 0) base = atomicAdd(cnt, tot);
         base = __builtin_amdgcn_readlane(base, 0);
-        if (sel) stw<GROUP>(&ord[base + lanes_below(sm)], i);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (d[q] == t) stw<GROUP>(&ord[base + lanes_below(sm[q])], c0 + q * TEAM + lane);
+          base += (uint32_t)__popcll(sm[q]);
+        }
       }
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
@@ -1155,6 +1233,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       const uint32_t v = valid ? chk(dlist[i], g.N, false, 10, b) : 0u;
       const uint32_t transit = valid && !g.ovl[v];  // drained: no transit
       const uint32_t jb = valid ? g.nbr_bit[v] : 0u;
+      uint32_t cur = kInf, acc = 0;  // row_pairs' open row
       wave_edges(g.row_ptr, v, valid, [&](uint32_t k, uint32_t e, bool act) {
         const uint32_t ik = lane_pull(i, k), tk = lane_pull(transit, k), jk = lane_pull(jb, k);
         uint32_t u = 0, mu = kInf;
@@ -1175,21 +1254,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
             tight = false;
           }
         }
-        for (uint64_t pm = __ballot(tight) | __ballot(from_src); pm; pm &= pm - 1) {
-          const uint32_t bl = __ffsll((unsigned long long)pm) - 1;
-          const uint32_t pi = __builtin_amdgcn_readlane(ik, bl);
-          uint32_t* row = nhn + (size_t)pi * W;
-          if (__builtin_amdgcn_readlane((uint32_t)from_src, bl)) {
-            const uint32_t pj = __builtin_amdgcn_readlane(jk, bl);
-            const uint32_t wj = chk(pj >> 5, W, false, 7, 0);
-            if (lane == (wj & 63)) row[wj] |= 1u << (pj & 31);
-          } else {
-            const uint32_t pu = __builtin_amdgcn_readlane(u, bl), pmu = __builtin_amdgcn_readlane(mu, bl);
-            const uint32_t* from = pmu != kInf ? nhn + (size_t)pmu * W : B.nhb + (size_t)pu * W;
-            for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
-          }
-        }
+        row_pairs(__ballot(tight), __ballot(from_src), ik, jk, u, mu, W, nhn, B.nhb, lane, cur, acc);
       });
+      if (cur != kInf && lane < W) nhn[(size_t)cur * W + lane] = acc;
     }
     if (m != kInf) atomicMin(next, m);
     team_sync<TEAM, GROUP>(ctl, g.fault);
@@ -1507,6 +1574,7 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
       }
       const uint32_t transit = valid && !g.ovl[v];  // drained: no transit
       const uint32_t jb = valid ? g.nbr_bit[v] : 0u;
+      uint32_t cur = kInf, acc = 0;  // row_pairs' open row
       wave_edges(g.row_ptr, v, valid, [&](uint32_t k, uint32_t e, bool act) {
         const uint32_t ik = lane_pull(i, k), tk = lane_pull(transit, k), jk = lane_pull(jb, k);
         uint32_t u = 0, mu = kInf;
@@ -1528,21 +1596,9 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
           }
         }
         // the row ORs, one tight pair at a time in lane order
-        for (uint64_t pm = __ballot(tight) | __ballot(from_src); pm; pm &= pm - 1) {
-          const uint32_t bl = __ffsll((unsigned long long)pm) - 1;
-          const uint32_t pi = __builtin_amdgcn_readlane(ik, bl);
-          uint32_t* row = nhn + (size_t)pi * W;
-          if (__builtin_amdgcn_readlane((uint32_t)from_src, bl)) {
-            const uint32_t pj = __builtin_amdgcn_readlane(jk, bl);
-            const uint32_t wj = chk(pj >> 5, W, false, 7, 0);
-            if (lane == (wj & 63)) row[wj] |= 1u << (pj & 31);
-          } else {
-            const uint32_t pu = __builtin_amdgcn_readlane(u, bl), pmu = __builtin_amdgcn_readlane(mu, bl);
-            const uint32_t* from = pmu != kInf ? nhn + (size_t)pmu * W : B.nhb + (size_t)pu * W;
-            for (uint32_t j = lane; j < W; j += 64) row[j] |= from[j];
-          }
-        }
+        row_pairs(__ballot(tight), __ballot(from_src), ik, jk, u, mu, W, nhn, B.nhb, lane, cur, acc);
       });
+      if (cur != kInf && lane < W) nhn[(size_t)cur * W + lane] = acc;
     }
     sync();
     t = wave_min32(m);
@@ -1973,9 +2029,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   const size_t bt = p->big_teams;
   {  // group teams over the concurrent (c_*) scratch sets: G workgroups each,
      // n_cu / G teams (a multiple of 8: members share an XCD), no more teams
-     // than scratch sets (SPF_WHATIF_GROUP=1: one-workgroup teams, A/B)
+     // than scratch sets (SPF_WHATIF_GROUP=1: one-workgroup teams, A/B).
+     // G = 8 by default: ba_whatif's failures took 9.3 ms at G = 8 against
+     // 10.2 at 4 and 14.8 at 16 (profiles/r05_whatif/flat)
     const char* e = std::getenv("SPF_WHATIF_GROUP");
-    uint32_t G = e ? (uint32_t)atoi(e) : 4u;
+    uint32_t G = e ? (uint32_t)atoi(e) : 8u;
     if (G > 1) {
       while (G <= 16 && (c->n_cu / G > bt || (c->n_cu / G) % 8)) G *= 2;
       if (G <= 16 && c->n_cu % (8 * G) == 0 && c->n_cu / G >= 8) {
