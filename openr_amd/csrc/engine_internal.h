@@ -142,6 +142,7 @@ struct spf_ctx {
   std::vector<uint32_t> sell4_ptr, sell4;  // packed u16x4 columns (uint2 entries), planes BFS
   spfi::DevBuf<uint32_t> d_sell4_ptr, d_sell4;
   spfi::DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
+  spfi::DevBuf<uint32_t> d_edge_nb;  // per CSR edge: its head's index among the tail's distinct neighbours
   spfi::DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
   spfi::DevBuf<uint32_t> d_pred_cnt, d_pred_edge, d_link, d_ign, d_one_src, d_row;
@@ -156,6 +157,8 @@ struct spf_ctx {
   // mssp_kernel tables (mssp.hip), valid for graph epoch mp_epoch
   spfi::DevBuf<uint32_t> d_mp_ell, d_mp_smap;
   spfi::DevBuf<uint32_t> d_mp_dep;  // per slice: the slices its nodes' out-edges reach (CSR)
+  spfi::DevBuf<uint32_t> d_mp_cls;  // per wave: first slot of each width class (phased first sweep)
+  uint32_t mp_ncls = 0;
   uint32_t mp_slots = 0, mp_ovf_at = 0;
   bool mp_redo = true;
   bool mp_u8 = false;  // u8 labels (four sources per LDS word)

@@ -118,7 +118,9 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     uint32_t ovf_at, uint32_t* __restrict__ redo, uint32_t alt,
     const uint32_t* __restrict__ dep /* [n_slices + 1] offsets, then out-slice lists; null: no skipping */,
     unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */,
-    uint32_t* __restrict__ maxd /* sliced next-hop plans: largest finite distance (254: saturated) */) {
+    uint32_t* __restrict__ maxd /* sliced next-hop plans: largest finite distance (254: saturated) */,
+    const uint32_t* __restrict__ cls /* [kMpWaves][n_cls]: first slot of each width class */,
+    uint32_t n_cls /* > 1: the first sweep goes class by class, a barrier between */) {
   constexpr uint32_t S = (U8 ? 4 : 2) * SD;  // sources per workgroup
   constexpr uint32_t LPW = U8 ? 4 : 2;       // labels per word
   constexpr uint32_t LB = U8 ? 8 : 16;       // label bits
@@ -197,7 +199,19 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     auto slot_at = [&](uint32_t k) { return back ? n_my - 1u - k : k; };
     uint32_t nsl = n_my ? wmap[slot_at(0)] : kMpNoSlice;
     uint32_t nb0 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl], nb1 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl + 1];
+    // phased first sweep: every wave finishes its slices of width class c
+    // (widest first) before any wave starts class c + 1, so the labels flow
+    // hub -> mid -> leaf within the sweep (a hop chain in class order lands
+    // in one sweep instead of one per order inversion between waves)
+    const bool phased = it == 0 && n_cls > 1;
+    uint32_t pc = 1;  // next class boundary of this wave
+    const uint32_t* wcls = cls ? cls + __builtin_amdgcn_readfirstlane(wave) * n_cls : nullptr;
     for (uint32_t kk = 0; kk < n_my; ++kk) {
+      if (phased)
+        while (pc < n_cls && kk == wcls[pc]) {
+          __syncthreads();
+          ++pc;
+        }
       const uint32_t k = slot_at(kk);
       const uint32_t sl = nsl;
       const uint32_t b = nb0, w = (nb1 - nb0) / 64;
@@ -209,7 +223,10 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
       if (dep && it > 0 &&
           !(__builtin_amdgcn_readfirstlane(scur[sl >> 5] | snxt[sl >> 5]) >> (sl & 31) & 1u))
         continue;  // no in-neighbour changed since this slice's last sweep
-      if (stats && lane == 0) atomicAdd(&stats[3], 1ull);  // slices swept (diagnostics)
+      if (stats && lane == 0) {  // slices swept (diagnostics): total, per sweep
+        atomicAdd(&stats[3], 1ull);
+        atomicAdd(&stats[4 + min(it, 11u)], 1ull);
+      }
       const uint32_t v = sl * 64 + lane;
       // u16x2 accumulators: SD of them (u16 labels), 2 SD (u8 labels: the
       // lo / hi halves of each word)
@@ -300,6 +317,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         }
         if (dec) {
           changed = true;
+          if (stats) atomicAdd(&stats[16 + min(it, 11u)], 1ull);  // nodes decreased per sweep
           expands = k < 32 ? !((dmask >> k) & 1u) : !ovl[v];
           if (expands) {  // seen as changed by this sweep and the next
             atomicOr(&cur_w[v >> 5], 1u << (v & 31));
@@ -316,6 +334,8 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
         }
       }
     }
+    if (phased)  // the class barriers this wave has no slices for
+      for (; pc < n_cls; ++pc) __syncthreads();
     if (__builtin_amdgcn_ballot_w64(changed) && lane == 0) flag[it % 3] = 1;
     __syncthreads();
     if (!flag[it % 3]) {
@@ -434,6 +454,39 @@ spf_status mssp_prepare(spf_ctx* c) {
     smap[(size_t)best * slots + used[best]++] = sl;
     load[best] += std::max(1u, width(sl));
   }
+  // width classes (distinct slice widths, widest first; by log2 width when
+  // there are more than kMpMaxCls) and, per wave, the first slot of each:
+  // the phased first sweep's barriers
+  {
+    constexpr uint32_t kMpMaxCls = 8;
+    std::vector<uint32_t> ws;
+    for (uint32_t sl = 0; sl < n_slices; ++sl) ws.push_back(width(sl));
+    std::sort(ws.begin(), ws.end(), std::greater<uint32_t>());
+    ws.erase(std::unique(ws.begin(), ws.end()), ws.end());
+    const bool log_cls = ws.size() > kMpMaxCls;
+    auto key = [&](uint32_t w) { return log_cls ? 32u - (uint32_t)__builtin_clz(std::max(w, 1u)) : w; };
+    std::vector<uint32_t> keys;
+    for (uint32_t w : ws) keys.push_back(key(w));
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());  // descending
+    if (keys.size() > kMpMaxCls) keys.resize(kMpMaxCls);  // the narrowest classes merge into the last
+    const uint32_t n_cls = (uint32_t)keys.size();
+    auto cls_of = [&](uint32_t sl) {
+      const uint32_t k = key(width(sl));
+      uint32_t c = 0;
+      while (c + 1 < n_cls && keys[c] > k) ++c;
+      return c;
+    };
+    std::vector<uint32_t> cl((size_t)kMpWaves * std::max(n_cls, 1u), 0);
+    for (uint32_t w = 0; w < kMpWaves; ++w) {
+      uint32_t k = 0;
+      for (uint32_t c = 0; c < n_cls; ++c) {
+        while (k < slots && smap[(size_t)w * slots + k] != kMpNoSlice && cls_of(smap[(size_t)w * slots + k]) < c) ++k;
+        cl[(size_t)w * n_cls + c] = k;
+      }
+    }
+    c->mp_ncls = n_cls;
+    HIP_TRY(c, c->d_mp_cls.upload(cl.data(), cl.size(), c->stream));
+  }
   // per slice: the other slices its nodes' out-edges reach (the mssp
   // kernel's slice-level dirt)
   std::vector<uint32_t> dep(n_slices + 1, 0);
@@ -534,6 +587,10 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   const uint32_t alt = ae ? (uint32_t)atoi(ae) : 0u;
   const char* ke = std::getenv("SPF_MSSP_SKIP");  // A/B: slice-level dirt (default on)
   const uint32_t* dep = ke && ke[0] == '0' ? nullptr : c->d_mp_dep.p;
+  // class-phased first sweep (default; SPF_MSSP_PHASED=0: A/B): fabric_rtt
+  // 5.24 -> 4.58 sweeps per workgroup, mssp 1.245 -> 1.131 ms (r05_ms2)
+  const char* pe = std::getenv("SPF_MSSP_PHASED");
+  const bool phased = !(pe && pe[0] == '0');
 #define MP_LAUNCH(SDV)                                                                            \
   if (c->mp_u8) {                                                                                 \
     MP_LAUNCH2(SDV, true);                                                                        \
@@ -544,7 +601,7 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   hipLaunchKernelGGL((mssp_kernel<SDV, U8V>), g, b, mp_lds(N, SDV), s, c->d_sell_ptr.p, c->d_mp_ell.p, \
                      c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
                      c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, alt, dep, c->d_stamps.p, \
-                     maxd)
+                     maxd, c->d_mp_cls.p, phased ? c->mp_ncls : 0u)
   switch (sd) {
     case 8: MP_LAUNCH(8); break;
     case 4: MP_LAUNCH(4); break;

@@ -97,7 +97,7 @@ __device__ __forceinline__ uint64_t rmix64(uint64_t z) {
 }
 
 // Route selection for many `me` nodes over RESIDENT rows (an all-sources
-// pass, spf_mplan): a thread per destination set, a block row per me (every
+// pass, spf_mplan): a thread per destination set, a run of blocks per me (every
 // me value wave-uniform: its CSR row, its distinct neighbours, their rows
 // arrive by scalar loads).  Sets of single advertisers sorted by node id make
 // consecutive lanes read consecutive entries of me's row and bitmaps.
@@ -114,71 +114,107 @@ __device__ __forceinline__ uint64_t rmix64(uint64_t z) {
 //   mix(K (p + 1) + shortest) + sum over kept links of mix(link_hash[l] +
 //   (u32) over).  Otherwise (one me) the records of spf_routes.
 constexpr uint32_t kRsThreads = 256;
+constexpr uint32_t kRsGroup = 4;  // consecutive me slots per XCD turn
+constexpr uint32_t kRsLinks = 256;  // me's links staged in LDS per pass
 template <bool DIGEST>
 __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
     const unsigned long long* __restrict__ rowp, const unsigned long long* __restrict__ nhp,
     uint32_t wpm, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
     const uint32_t* __restrict__ wt, const uint32_t* __restrict__ link,
-    const uint32_t* __restrict__ nb_ptr, const uint32_t* __restrict__ nb_id,
+    const uint32_t* __restrict__ edge_nb,
     const uint32_t* __restrict__ me_ids, const uint32_t* __restrict__ set_ptr,
     const uint32_t* __restrict__ set_nodes, uint32_t n_sets, uint32_t lfa,
     const unsigned long long* __restrict__ link_hash, unsigned long long* __restrict__ digest,
     uint64_t* __restrict__ out_min, uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_edge,
-    uint64_t* __restrict__ out_metric) {
-  const uint32_t me = me_ids[blockIdx.y];
-  const uint32_t p = blockIdx.x * kRsThreads + threadIdx.x;
+    uint64_t* __restrict__ out_metric, uint32_t n_me, uint32_t n_chunks) {
+  // XCD-aware block order: blocks are dealt to the 8 XCDs round robin
+  // (blockIdx % 8); me slots go in groups of kRsGroup consecutive slots, group
+  // q to XCD q % 8 (heavy and light nodes of a locality-ordered list spread
+  // over the XCDs), every set chunk of one me back to back on its XCD, so
+  // me's row and bitmaps and its neighbours' rows (shared by the group's other
+  // me) come from that XCD's L2 instead of once per XCD from the MALL
+  const uint32_t g = blockIdx.x & 7u, i = blockIdx.x >> 3;
+  const uint32_t L = i / n_chunks;  // this XCD's L-th me
+  const uint32_t slot = ((L / kRsGroup) * 8 + g) * kRsGroup + L % kRsGroup;
+  if (slot >= n_me) return;  // whole block
+  const uint32_t me = me_ids[slot];
+  const uint32_t p = (i % n_chunks) * kRsThreads + threadIdx.x;
   const uint32_t* Dme = reinterpret_cast<const uint32_t*>(rowp[me]);
   const uint32_t* NHme = reinterpret_cast<const uint32_t*>(nhp[me]);
   const uint32_t e0 = row_ptr[me], e1 = row_ptr[me + 1];
-  const uint32_t nb0 = nb_ptr[me], k = nb_ptr[me + 1] - nb0;
   const bool live = p < n_sets;
   const uint32_t b = live ? set_ptr[p] : 0u, e = live ? set_ptr[p + 1] : 0u;
   uint64_t shortest = kInf64;
-  for (uint32_t i = b; i < e; ++i) {
-    const uint32_t d = Dme[set_nodes[i]];
+  for (uint32_t k = b; k < e; ++k) {
+    const uint32_t d = Dme[set_nodes[k]];
     if (d != kInf && d < shortest) shortest = d;
   }
+  // a one-member set (a loopback, a node label): its node
+  const bool one = e == b + 1;
+  const uint32_t d0 = one ? set_nodes[b] : 0u;
+  // me's up links, kRsLinks at a time, staged in LDS by the whole block: the
+  // neighbour's bitmap index, its row's address, d_me(x), d_x(me), the link's
+  // metric and hash -- formerly a dependent scalar chain per link and thread
+  // (a binary search over me's neighbours, then rowp[x], then d_x(me)); a
+  // spine's 173 links made its blocks the pass's tail
+  __shared__ uint32_t s_j[kRsLinks], s_dmx[kRsLinks], s_back[kRsLinks], s_w[kRsLinks];
+  __shared__ unsigned long long s_row[kRsLinks], s_lh[kRsLinks];
   uint64_t rec = 0;
   uint32_t cnt = 0;
-  const uint32_t deg = e1 - e0;
-  if (shortest != kInf64 || !DIGEST) {
-    for (uint32_t q = e0; q < e1; ++q) {  // me's up links (wave-uniform)
-      const uint32_t x = col[q];
-      // j: x's index among me's distinct neighbours (binary search, scalar)
-      uint32_t lo = 0, hi = k;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (nb_id[nb0 + mid] <= x) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t j = lo;
-      if (shortest == kInf64) continue;
+  for (uint32_t c0 = e0; c0 < e1; c0 += kRsLinks) {  // block-uniform
+    const uint32_t nl = min(kRsLinks, e1 - c0);
+    __syncthreads();  // the previous chunk's reads are done
+    for (uint32_t t = threadIdx.x; t < nl; t += kRsThreads) {
+      const uint32_t q = c0 + t, x = col[q];
+      const unsigned long long rx = lfa ? rowp[x] : 0ull;
+      s_j[t] = edge_nb[q];
+      s_dmx[t] = Dme[x];
+      s_w[t] = wt[q];
+      s_row[t] = rx;
+      s_back[t] = rx ? reinterpret_cast<const uint32_t*>(rx)[me] : kInf;
+      if constexpr (DIGEST) s_lh[t] = link_hash[link[q]];
+    }
+    __syncthreads();
+    if (shortest == kInf64) continue;  // (every thread still meets the barriers)
+    for (uint32_t t = 0; t < nl; ++t) {
+      // getNextHopsWithMetric: x is a shortest-path next hop of a min-cost
+      // member (via = shortest - d_me(x)), lowered with LFA to a member's
+      // d_x(dst) < shortest + d_x(me)
       uint64_t via = kInf64;
-      const uint32_t* bm = NHme + (size_t)j * wpm;
-      for (uint32_t i = b; i < e; ++i) {
-        const uint32_t d = set_nodes[i];
-        if (Dme[d] != shortest) continue;
-        if ((bm[d >> 5] >> (d & 31)) & 1u) {
-          via = shortest - Dme[x];
-          break;
+      const uint32_t* bm = NHme + (size_t)s_j[t] * wpm;
+      const uint32_t* Dx = reinterpret_cast<const uint32_t*>(s_row[t]);
+      const uint64_t back = s_back[t];
+      if (one) {  // Dme[d0] == shortest
+        const uint32_t bw = bm[d0 >> 5];
+        const uint32_t dxd = Dx ? Dx[d0] : kInf;  // (Dx is null without LFA)
+        if ((bw >> (d0 & 31)) & 1u) via = shortest - s_dmx[t];
+        if (lfa && dxd != kInf && back != kInf && (uint64_t)dxd < shortest + back &&
+            (via == kInf64 || via > dxd))
+          via = dxd;
+      } else {
+        for (uint32_t k = b; k < e; ++k) {
+          const uint32_t d = set_nodes[k];
+          if (Dme[d] != shortest) continue;
+          if ((bm[d >> 5] >> (d & 31)) & 1u) {
+            via = shortest - s_dmx[t];
+            break;
+          }
         }
-      }
-      if (lfa) {
-        const uint32_t* Dx = reinterpret_cast<const uint32_t*>(rowp[x]);
-        const uint64_t back = Dx[me];
-        for (uint32_t i = b; i < e; ++i) {
-          const uint32_t dxd = Dx[set_nodes[i]];
-          if (dxd == kInf || back == kInf) continue;
-          if ((uint64_t)dxd < shortest + back && (via == kInf64 || via > dxd)) via = dxd;
-        }
+        if (Dx)
+          for (uint32_t k = b; k < e; ++k) {
+            const uint32_t dxd = Dx[set_nodes[k]];
+            if (dxd == kInf || back == kInf) continue;
+            if ((uint64_t)dxd < shortest + back && (via == kInf64 || via > dxd)) via = dxd;
+          }
       }
       if (via == kInf64) continue;
-      const uint64_t over = (uint64_t)wt[q] + via;
+      const uint64_t over = (uint64_t)s_w[t] + via;
       if (!lfa && over != shortest) continue;
       if constexpr (DIGEST) {
-        rec += rmix64(link_hash[link[q]] + (uint32_t)over);
+        rec += rmix64(s_lh[t] + (uint32_t)over);
       } else {
-        out_edge[(size_t)p * deg + cnt] = q;
+        const uint32_t deg = e1 - e0;
+        out_edge[(size_t)p * deg + cnt] = c0 + t;
         out_metric[(size_t)p * deg + cnt] = over;
       }
       ++cnt;
@@ -191,7 +227,7 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
       const uint32_t lo2 = __shfl_down((uint32_t)h, d, 64), hi2 = __shfl_down((uint32_t)(h >> 32), d, 64);
       h += ((uint64_t)hi2 << 32) | lo2;
     }
-    if ((threadIdx.x & 63) == 0 && h) atomicAdd(&digest[blockIdx.y], (unsigned long long)h);
+    if ((threadIdx.x & 63) == 0 && h) atomicAdd(&digest[slot], (unsigned long long)h);
   } else if (live) {
     out_min[p] = shortest;
     out_cnt[p] = cnt;
@@ -209,17 +245,22 @@ spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
                              unsigned long long* d_digest, uint64_t* d_min, uint32_t* d_cnt,
                              uint32_t* d_edge, uint64_t* d_metric, hipStream_t s) {
   if (!n_me || !n_sets) return SPF_OK;
-  const dim3 grid((n_sets + kRsThreads - 1) / kRsThreads, n_me);
+  const uint32_t n_chunks = (n_sets + kRsThreads - 1) / kRsThreads;
+  const uint32_t groups = (n_me + kRsGroup - 1) / kRsGroup;
+  const uint32_t per_xcd = (groups + 7) / 8 * kRsGroup;  // the most me slots any XCD takes
+  const uint64_t blocks = 8ull * per_xcd * n_chunks;
+  if (blocks >= (1ull << 31)) return fail(c, SPF_E_INVALID, "route sets: grid too large");
+  const dim3 grid((uint32_t)blocks);
   if (d_digest)
     hipLaunchKernelGGL(route_sets_kernel<true>, grid, dim3(kRsThreads), 0, s, d_rowp, d_nhp,
-                       c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_nb_ptr.p,
-                       c->d_nb_id.p, d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, d_link_hash,
-                       d_digest, nullptr, nullptr, nullptr, nullptr);
+                       c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p,
+                       d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, d_link_hash,
+                       d_digest, nullptr, nullptr, nullptr, nullptr, n_me, n_chunks);
   else
     hipLaunchKernelGGL(route_sets_kernel<false>, grid, dim3(kRsThreads), 0, s, d_rowp, d_nhp,
-                       c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_nb_ptr.p,
-                       c->d_nb_id.p, d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, nullptr,
-                       nullptr, d_min, d_cnt, d_edge, d_metric);
+                       c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p,
+                       d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, nullptr,
+                       nullptr, d_min, d_cnt, d_edge, d_metric, n_me, n_chunks);
   HIP_TRY(c, hipGetLastError());
   return SPF_OK;
 }

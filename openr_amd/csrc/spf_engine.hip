@@ -1788,6 +1788,16 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   HIP_TRY(c, c->d_nb_ptr.upload(c->nb_ptr.data(), N + 1, c->stream));
   HIP_TRY(c, c->d_nb_id.upload(c->nb_id.data(), c->nb_id.size(), c->stream));
   HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  {  // per edge: the head's index among the tail's distinct neighbours (the
+     // route selection's next-hop bitmap of that neighbour)
+    std::vector<uint32_t> enb(std::max<uint32_t>(E, 1));
+    for (uint32_t u = 0; u < N; ++u) {
+      const auto b = c->nb_id.begin() + c->nb_ptr[u], e = c->nb_id.begin() + c->nb_ptr[u + 1];
+      for (uint32_t q = c->row_ptr[u]; q < c->row_ptr[u + 1]; ++q)
+        enb[q] = (uint32_t)(std::lower_bound(b, e, c->col[q]) - b);
+    }
+    HIP_TRY(c, c->d_edge_nb.upload(enb.data(), enb.size(), c->stream));
+  }
   // sliced ELL (SELL-64): slice = 64 consecutive nodes, width = max degree in
   // the slice, entry (slice, j, lane) = j-th neighbour of node slice*64+lane,
   // padded with N (F[N] == 0 in the BFS kernel)

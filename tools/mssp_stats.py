@@ -26,6 +26,8 @@ st = eng.debug_stamps().astype(np.int64).ravel()
 print("sweeps total", st[0], "max", st[1], "workgroups", st[2], "mean", st[0] / max(st[2], 1))
 n_sl = (n + 63) // 64
 print("slices swept", st[3], "of", st[0] * n_sl, "slice visits:", round(st[3] / max(1, st[0] * n_sl), 3))
+print("slices swept per sweep", st[4:16].tolist())
+print("nodes decreased per sweep", st[16:28].tolist())
 print("metric range", met.min(), met.max(), "mean", met.mean())
 plan.close()
 close_all()
