@@ -120,7 +120,8 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     unsigned long long* __restrict__ stats /* diagnostics (SPF_STAMPS): [0] sweeps, [1] max, [2] WGs */,
     uint32_t* __restrict__ maxd /* sliced next-hop plans: largest finite distance (254: saturated) */,
     const uint32_t* __restrict__ cls /* [kMpWaves][n_cls]: first slot of each width class */,
-    uint32_t n_cls /* > 1: the first sweep goes class by class, a barrier between */) {
+    uint32_t n_cls /* > 1: phased sweeps go class by class, a barrier between */,
+    uint32_t phase /* bits 0-7: leading sweeps phased; bit 8: odd phased sweeps narrow class first */) {
   constexpr uint32_t S = (U8 ? 4 : 2) * SD;  // sources per workgroup
   constexpr uint32_t LPW = U8 ? 4 : 2;       // labels per word
   constexpr uint32_t LB = U8 ? 8 : 16;       // label bits
@@ -195,24 +196,37 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
     // odd sweeps walk the wave's slots backwards (narrow slices first): a
     // forward sweep carries paths whose hops go from wide to narrow nodes
     // (spine -> fabric -> rack switch), a backward one the opposite turns
-    const bool back = alt && (it & 1u);
+    // phased sweeps (the first `phase & 0xFF`): every wave finishes its
+    // slices of width class c before any wave starts the next class -- widest
+    // first, or (bit 8, odd sweeps) narrowest first -- so labels flow hub ->
+    // mid -> leaf (or back) within the sweep: a hop chain in class order
+    // lands in one sweep instead of one per order inversion between waves
+    const bool phased = n_cls > 1 && it < (phase & 0xFFu);
+    const bool rev = phased && (phase & 0x100u) && (it & 1u);
+    const bool back = phased ? rev : alt && (it & 1u);
     auto slot_at = [&](uint32_t k) { return back ? n_my - 1u - k : k; };
     uint32_t nsl = n_my ? wmap[slot_at(0)] : kMpNoSlice;
     uint32_t nb0 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl], nb1 = nsl == kMpNoSlice ? 0u : sell_ptr[nsl + 1];
-    // phased first sweep: every wave finishes its slices of width class c
-    // (widest first) before any wave starts class c + 1, so the labels flow
-    // hub -> mid -> leaf within the sweep (a hop chain in class order lands
-    // in one sweep instead of one per order inversion between waves)
-    const bool phased = it == 0 && n_cls > 1;
-    uint32_t pc = 1;  // next class boundary of this wave
+    // class barriers: forward, before the first slot of class pc (pc = 1 ..
+    // n_cls - 1); backward, before the first slot below class pc's start
+    // (pc = n_cls - 1 .. 1); a wave with no slot of a class meets its
+    // barrier at the next class, or at the end
+    uint32_t pc = back ? n_cls - 1u : 1u, n_bar = 0;
     const uint32_t* wcls = cls ? cls + __builtin_amdgcn_readfirstlane(wave) * n_cls : nullptr;
     for (uint32_t kk = 0; kk < n_my; ++kk) {
-      if (phased)
-        while (pc < n_cls && kk == wcls[pc]) {
-          __syncthreads();
-          ++pc;
-        }
       const uint32_t k = slot_at(kk);
+      if (phased) {
+        if (!back)
+          while (pc < n_cls && k == wcls[pc]) {
+            __syncthreads();
+            ++pc, ++n_bar;
+          }
+        else
+          while (pc >= 1 && k < wcls[pc]) {
+            __syncthreads();
+            --pc, ++n_bar;
+          }
+      }
       const uint32_t sl = nsl;
       const uint32_t b = nb0, w = (nb1 - nb0) / 64;
       nsl = kk + 1 < n_my ? wmap[slot_at(kk + 1)] : kMpNoSlice;
@@ -335,7 +349,7 @@ __global__ __launch_bounds__(kMpThreads) void mssp_kernel(
       }
     }
     if (phased)  // the class barriers this wave has no slices for
-      for (; pc < n_cls; ++pc) __syncthreads();
+      for (; n_bar + 1 < n_cls; ++n_bar) __syncthreads();
     if (__builtin_amdgcn_ballot_w64(changed) && lane == 0) flag[it % 3] = 1;
     __syncthreads();
     if (!flag[it % 3]) {
@@ -587,10 +601,11 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   const uint32_t alt = ae ? (uint32_t)atoi(ae) : 0u;
   const char* ke = std::getenv("SPF_MSSP_SKIP");  // A/B: slice-level dirt (default on)
   const uint32_t* dep = ke && ke[0] == '0' ? nullptr : c->d_mp_dep.p;
-  // class-phased first sweep (default; SPF_MSSP_PHASED=0: A/B): fabric_rtt
-  // 5.24 -> 4.58 sweeps per workgroup, mssp 1.245 -> 1.131 ms (r05_ms2)
+  // class-phased first sweep (default; SPF_MSSP_PHASED=<phase word>: A/B, 0
+  // off): fabric_rtt 5.24 -> 4.58 sweeps per workgroup, mssp 1.245 -> 1.131
+  // ms (r05_ms2)
   const char* pe = std::getenv("SPF_MSSP_PHASED");
-  const bool phased = !(pe && pe[0] == '0');
+  const uint32_t phase = pe ? (uint32_t)strtoul(pe, nullptr, 0) : 1u;
 #define MP_LAUNCH(SDV)                                                                            \
   if (c->mp_u8) {                                                                                 \
     MP_LAUNCH2(SDV, true);                                                                        \
@@ -601,7 +616,7 @@ spf_status launch_mssp(spf_ctx* c, const uint32_t* rows_src, uint32_t rows, uint
   hipLaunchKernelGGL((mssp_kernel<SDV, U8V>), g, b, mp_lds(N, SDV), s, c->d_sell_ptr.p, c->d_mp_ell.p, \
                      c->d_mp_smap.p, c->mp_slots, c->d_row_ptr.p, c->d_col.p, c->d_wt.p,        \
                      c->d_ovl.p, rows_src, rows, N, c->pitch, D, Dn, c->mp_ovf_at, rd, alt, dep, c->d_stamps.p, \
-                     maxd, c->d_mp_cls.p, phased ? c->mp_ncls : 0u)
+                     maxd, c->d_mp_cls.p, c->mp_ncls, phase)
   switch (sd) {
     case 8: MP_LAUNCH(8); break;
     case 4: MP_LAUNCH(4); break;

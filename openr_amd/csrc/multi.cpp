@@ -181,8 +181,11 @@ struct spf_mplan {
     // sets, its me list and outputs on this member's device
     DevBuf<unsigned long long> rowp, nhp, lh, rdig, rmin, rmetric;
     DevBuf<uint32_t> rsp, rsn, rme, rcnt, redge;
+    std::vector<uint32_t> h_rsp, h_rsn;  // host copies of the uploaded sets (re-upload only on change)
+    std::vector<uint64_t> h_lh;
     uint64_t r_epoch = ~0ull;  // execute count the address tables belong to
   };
+  std::vector<unsigned long long> h_rowp, h_nhp;  // the address tables (host; uploads read them)
   std::unique_ptr<Part[]> parts;  // [n_parts]
   uint32_t n_parts = 0;
   bool graphs = false;
@@ -581,13 +584,27 @@ spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t*
         (void)hipGetLastError();
       }
   }
-  std::vector<unsigned long long> rowp(N, 0), nhp(N, 0);
+  bool stale = false;
+  for (uint32_t r = 0; r < mp->n_parts; ++r) stale |= mp->parts[r].plan && mp->parts[r].r_epoch != mp->executes;
+  std::vector<unsigned long long>& rowp = mp->h_rowp;
+  std::vector<unsigned long long>& nhp = mp->h_nhp;
   std::vector<int> dev_of(N, -1);
+  if (stale) {  // no upload of the old tables may still be reading them
+    for (uint32_t r = 0; r < mp->n_parts; ++r)
+      if (mp->parts[r].plan) {
+        M_HIP(m, hipSetDevice(m->members[r]->device));
+        M_HIP(m, hipStreamSynchronize(m->exec[r]));
+      }
+    rowp.assign(N, 0);
+    nhp.assign(N, 0);
+  }
   for (uint32_t i = 0; i < mp->n_src; ++i) {
     const uint32_t v = mp->srcs[i], r = mp->owner[i], row = mp->row[i];
     const spf_mplan::Part& p = mp->parts[r];
-    rowp[v] = (unsigned long long)(uintptr_t)(p.dist.p + (size_t)row * c0->pitch);
-    nhp[v] = (unsigned long long)(uintptr_t)(p.nh.p + p.nh_off[row]);
+    if (stale) {
+      rowp[v] = (unsigned long long)(uintptr_t)(p.dist.p + (size_t)row * c0->pitch);
+      nhp[v] = (unsigned long long)(uintptr_t)(p.nh.p + p.nh_off[row]);
+    }
     dev_of[v] = m->members[r]->device;
   }
   if (lfa && !mp->peer) {
@@ -611,13 +628,28 @@ spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t*
       M_HIP(m, p.nhp.upload(nhp.data(), N, s));
       p.r_epoch = mp->executes;
     }
-    M_HIP(m, p.rsp.upload(set_ptr, n_sets + 1, s));
-    M_HIP(m, p.rsn.upload(set_nodes, std::max<uint32_t>(1, set_ptr[n_sets]), s));
-    if (link_hash) M_HIP(m, p.lh.upload(reinterpret_cast<const unsigned long long*>(link_hash),
-                                        std::max<uint32_t>(1, n_links), s));
-    // the tables' uploads are pageable copies: done before the caller's
-    // vectors go away (the set arrays are the caller's)
-    M_HIP(m, hipStreamSynchronize(s));
+    // the sets and link hashes of a call are usually the previous call's
+    // (every route build of a node list): uploaded only when they changed
+    const uint32_t n_mem = std::max<uint32_t>(1, set_ptr[n_sets]);
+    auto same = [](const auto& v, const auto* x, size_t n) {
+      return v.size() == n && std::equal(v.begin(), v.end(), x);
+    };
+    const bool up = !same(p.h_rsp, set_ptr, n_sets + 1) || !same(p.h_rsn, set_nodes, n_mem) ||
+                    (link_hash && !same(p.h_lh, link_hash, std::max<uint32_t>(1, n_links)));
+    if (up) M_HIP(m, hipStreamSynchronize(s));  // no upload still reads the host copies
+    if (!same(p.h_rsp, set_ptr, n_sets + 1)) {
+      p.h_rsp.assign(set_ptr, set_ptr + n_sets + 1);
+      M_HIP(m, p.rsp.upload(p.h_rsp.data(), n_sets + 1, s));
+    }
+    if (!same(p.h_rsn, set_nodes, n_mem)) {
+      p.h_rsn.assign(set_nodes, set_nodes + n_mem);
+      M_HIP(m, p.rsn.upload(p.h_rsn.data(), n_mem, s));
+    }
+    if (link_hash && !same(p.h_lh, link_hash, std::max<uint32_t>(1, n_links))) {
+      p.h_lh.assign(link_hash, link_hash + std::max<uint32_t>(1, n_links));
+      M_HIP(m, p.lh.upload(reinterpret_cast<const unsigned long long*>(p.h_lh.data()), p.h_lh.size(), s));
+    }
+    // (uploads read the host copies, which outlive the call)
   }
   return SPF_OK;
 }

@@ -449,7 +449,7 @@ class LinkState(N.NativeHandle):
         engine's route / KSP2 digests; cached until the topology changes."""
         import numpy as np
 
-        lid = self.flatten()[4]
+        lid = self._csr_link_ids()
         key = (len(lid), int(lid.max()) if len(lid) else -1, N.lib.ls_num_links(self._h))
         if getattr(self, "_lh_key", None) == key and self._lh is not None:
             return self._lh
@@ -478,7 +478,7 @@ class LinkState(N.NativeHandle):
         mp = N.lib.ls_all_sources_plan(self._h)
         if not mp:
             raise RuntimeError("allSourcesRouteDigests: no resident all-sources pass")
-        n = len(self.flatten()[0])
+        n = self._csr_sizes()[0]
         mes = np.arange(n, dtype=np.uint32) if mes is None else np.ascontiguousarray(mes, np.uint32)
         sp = np.ascontiguousarray(set_ptr, np.uint32)
         sn = np.ascontiguousarray(set_nodes if len(set_nodes) else [0], np.uint32)
@@ -534,6 +534,22 @@ class LinkState(N.NativeHandle):
         return bool(N.lib.ls_path_a_in_path_b(N.ptr(ea), len(a), N.ptr(eb), len(b)))
 
     # -- batch access to the flattened graph ---------------------------------------
+    def _csr_sizes(self):
+        """(nodes, directed edges) of the flattened graph, without copying it."""
+        n = C.c_uint32()
+        e = C.c_uint32()
+        self._err(N.lib.ls_flatten(self._h, C.byref(n), C.byref(e)))
+        return n.value, e.value
+
+    def _csr_link_ids(self):
+        """The flattened graph's link id per CSR edge (no node names)."""
+        import numpy as np
+
+        _, e = self._csr_sizes()
+        lid = np.zeros(max(1, e), np.uint32)
+        self._err(N.lib.ls_graph_csr(self._h, None, None, None, N.ptr(lid), None))
+        return lid[:e]
+
     def flatten(self):
         """(node names in id order, row_ptr, col, metric, link_id, overloaded)."""
         import numpy as np
