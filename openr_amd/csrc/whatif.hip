@@ -992,6 +992,14 @@ __device__ __forceinline__ void row_pairs(uint64_t pm, uint64_t sm, uint32_t ik,
   }
 }
 
+// Nodes per wave chunk of a team's node loops: the count spread over the
+// team's waves, 1..64 (team-uniform).
+template <int TEAM>
+__device__ __forceinline__ uint32_t team_chunk(uint32_t count) {
+  constexpr uint32_t kW = TEAM / 64;
+  return min(64u, max(1u, (count + kW - 1) / kW));
+}
+
 // CHK (the profiled wave instance, SPF_WHATIF_PROF): every scratch-derived
 // index is range-checked before use; an out-of-range one sets bit 4 of the
 // fault word with the site in bits 16-23 and is replaced by a safe value
@@ -1061,13 +1069,16 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       if (tt == 0) loop_bound_hit(g.fault, 1);
       break;
     }
-    // each wave takes 64 frontier nodes at a time, lanes over their
-    // flattened edges (wave_edges); new nodes are appended by one counter
-    // atomic per wave
-    for (uint32_t c0 = lo + wv * 64; c0 < n; c0 += TEAM) {
+    // each wave takes cs frontier nodes at a time (cs = the frontier over
+    // the team's waves, at most 64: a small frontier still spreads over every
+    // wave), lanes over their flattened edges (wave_edges); new nodes are
+    // appended by one counter atomic per wave
+    const uint32_t cs = team_chunk<TEAM>(n - lo);
+    for (uint32_t c0 = lo + wv * cs; c0 < n; c0 += (TEAM / 64) * cs) {
       const uint32_t i = c0 + lane;
-      const uint32_t v = i < n ? chk(dlist[i], g.N, false, 1, b) : 0u;
-      const bool x = i < n && !g.ovl[v];  // drained (v != src): no DAG children
+      const bool in = lane < cs && i < n;
+      const uint32_t v = in ? chk(dlist[i], g.N, false, 1, b) : 0u;
+      const bool x = in && !g.ovl[v];  // drained (v != src): no DAG children
       const uint32_t dv = x ? B.dist[v] : 0u;
       wave_edges(g.row_ptr, v, x, [&](uint32_t k, uint32_t e, bool act) {
         const uint32_t dk = lane_pull(dv, k);
@@ -1118,10 +1129,12 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   // the per-node minimum by atomics on dnew
   for (uint32_t i = tt; i < n; i += TEAM) stw<GROUP>(&dnew[i], kInf);
   team_sync<TEAM, GROUP>(ctl, g.fault);
-  for (uint32_t c0 = wv * 64; c0 < n; c0 += TEAM) {
+  const uint32_t cs_seed = team_chunk<TEAM>(n);
+  for (uint32_t c0 = wv * cs_seed; c0 < n; c0 += (TEAM / 64) * cs_seed) {
     const uint32_t i = c0 + lane;
-    const uint32_t v = i < n ? dlist[i] : 0u;
-    wave_edges(g.row_ptr, v, i < n, [&](uint32_t k, uint32_t e, bool act) {
+    const bool in = lane < cs_seed && i < n;
+    const uint32_t v = in ? dlist[i] : 0u;
+    wave_edges(g.row_ptr, v, in, [&](uint32_t k, uint32_t e, bool act) {
       uint32_t s = kInf;
       if (act && g.link[e] != l) {
         const uint32_t u = g.col[e];
@@ -1222,13 +1235,16 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
       }
     }
     team_sync<TEAM, GROUP>(ctl, g.fault);
-    // (b) level nodes, 64 per wave at a time, lanes over their flattened
-    // edges: tight predecessors give the next-hop rows (one pair at a time,
-    // coalesced row ORs), out-edges relax the pending nodes
+    // (b) level nodes, cs per wave at a time (a level of ~150 nodes in 64-
+    // node chunks kept 3 of a group team's 64 waves busy, each walking ~8
+    // flattened edge chunks in turn), lanes over their flattened edges:
+    // tight predecessors give the next-hop rows (row_pairs), out-edges relax
+    // the pending nodes
     const uint32_t K = ldw<GROUP>(cnt);
-    for (uint32_t q0 = wv * 64; q0 < K; q0 += TEAM) {
+    const uint32_t cs = team_chunk<TEAM>(K);
+    for (uint32_t q0 = wv * cs; q0 < K; q0 += (TEAM / 64) * cs) {
       const uint32_t q = q0 + lane;
-      const bool valid = q < K;
+      const bool valid = lane < cs && q < K;
       const uint32_t i = valid ? chk(ldw<GROUP>(&ord[q]), n, false, 9, 0) : 0u;
       const uint32_t v = valid ? chk(dlist[i], g.N, false, 10, b) : 0u;
       const uint32_t transit = valid && !g.ovl[v];  // drained: no transit
