@@ -75,6 +75,9 @@ class MplsAction(NamedTuple):
     pushLabels: Optional[Tuple[int, ...]] = None
 
 
+_PHP = MplsAction("PHP")
+
+
 class NextHopThrift(NamedTuple):
     """thrift::NextHopThrift (Network.thrift:65-86) as built by createNextHop
     (openr/common/Util.cpp:907-922): metric is an i32.  An immutable value
@@ -480,6 +483,12 @@ class SpfSolver:
         if info is None or info[0] is not ls or info[1] != me or info[2] is not self._lid:
             info = self._edge_info = (ls, me, self._lid, {})
         cache = info[3]
+        # one action object per call (the route's), the named tuples built
+        # with tuple.__new__ (the generated __new__ wrapper was a third of
+        # the host route assembly: ~10^5 next hops per fabric build)
+        swap = None if swapLabel is None else tuple.__new__(MplsAction, ("SWAP", swapLabel, None))
+        mk = tuple.__new__
+        add = out.add
         for e, metric in res.hops:
             li = cache.get(e)
             if li is None:
@@ -488,12 +497,10 @@ class SpfSolver:
                                  bytes(link.getNhV4FromNode(me)), bytes(link.getNhV6FromNode(me)),
                                  link.getArea())
             nb, iface, v4, v6, larea = li
-            action = None
-            if swapLabel is not None:
-                action = MplsAction("PHP") if nb in dsts else MplsAction("SWAP", swapLabel)
+            action = None if swap is None else (_PHP if nb in dsts else swap)
             m = metric & 0xFFFFFFFF
-            out.add(NextHopThrift(v4 if isV4 else v6, iface, m - (1 << 32) if m >= 1 << 31 else m,
-                                  action, larea, nb))
+            add(mk(NextHopThrift, (v4 if isV4 else v6, iface, m - (1 << 32) if m >= 1 << 31 else m,
+                                   action, larea, nb)))
         return out
 
     # -- SR_MPLS SP_ECMP: getNextHopsWithMetric / getNextHopsThrift with

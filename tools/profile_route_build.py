@@ -24,6 +24,7 @@ def main():
     wl.step()
     pr.disable()
     pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
     from openr_amd.engine import close_all
 
     close_all()
