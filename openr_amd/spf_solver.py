@@ -474,10 +474,11 @@ class SpfSolver:
         self._raw = (mins, cnt, edge, metric, deg)
         return _LazySetResults(mins, cnt, edge, metric, deg)
 
-    def _next_hops(self, ls: LinkState, me: str, area: str, res: _SetResult, isV4: bool,
+    def _next_hops(self, ls: LinkState, me: str, area: str, res, isV4: bool,
                    dsts: Set[str], swapLabel: Optional[int]) -> Set[NextHopThrift]:
         """getNextHopsThrift (Decision.cpp:1198-1305) from the kernel's
-        (link, metric) selection."""
+        (link, metric) selection (a _SetResult, or its hops: (edge, metric)
+        pairs)."""
         out: Set[NextHopThrift] = set()
         info = getattr(self, "_edge_info", None)
         if info is None or info[0] is not ls or info[1] != me or info[2] is not self._lid:
@@ -489,7 +490,7 @@ class SpfSolver:
         swap = None if swapLabel is None else tuple.__new__(MplsAction, ("SWAP", swapLabel, None))
         mk = tuple.__new__
         add = out.add
-        for e, metric in res.hops:
+        for e, metric in (res.hops if isinstance(res, _SetResult) else res):
             li = cache.get(e)
             if li is None:
                 link = ls._link(int(self._lid[e]))
@@ -866,21 +867,33 @@ class SpfSolver:
         uni: List[tuple] = []
         sr: List[tuple] = []
         for prefix, entries in prefixState.prefixes().items():
-            # entries of nodes unreachable in their own area are dropped
-            ents = {na: e for na, e in entries.items()
-                    if na[1] not in mine or na[0] in mine[na[1]]}
-            if not ents:
-                self._bump("decision.no_route_to_prefix")
-                continue
-            isV4 = next(iter(ents.values())).isV4
+            if len(entries) == 1:  # one advertiser (most prefixes): the same flags, directly
+                (na0, e0), = entries.items()
+                if na0[1] in mine and na0[0] not in mine[na0[1]]:
+                    self._bump("decision.no_route_to_prefix")
+                    continue
+                ents = entries
+                isV4 = e0.isV4
+                hasBGP = e0.type == "BGP"
+                hasNonBGP = not hasBGP
+                missingMv = hasBGP and e0.mv is None
+                hasSelfPrepend = na0[0] != me or e0.prependLabel is not None
+            else:
+                # entries of nodes unreachable in their own area are dropped
+                ents = {na: e for na, e in entries.items()
+                        if na[1] not in mine or na[0] in mine[na[1]]}
+                if not ents:
+                    self._bump("decision.no_route_to_prefix")
+                    continue
+                isV4 = next(iter(ents.values())).isV4
+                hasBGP = any(e.type == "BGP" for e in ents.values())
+                hasNonBGP = any(e.type != "BGP" for e in ents.values())
+                missingMv = any(e.type == "BGP" and e.mv is None for e in ents.values())
+                hasSelfPrepend = all(e.prependLabel is not None
+                                     for na, e in ents.items() if na[0] == me)
             if isV4 and not self.enableV4:
                 self._bump("decision.skipped_unicast_route")
                 continue
-            hasBGP = any(e.type == "BGP" for e in ents.values())
-            hasNonBGP = any(e.type != "BGP" for e in ents.values())
-            missingMv = any(e.type == "BGP" and e.mv is None for e in ents.values())
-            hasSelfPrepend = all(e.prependLabel is not None
-                                 for na, e in ents.items() if na[0] == me)
             if hasBGP and ((hasNonBGP and not self.enableBestRouteSelection) or missingMv):
                 self._bump("decision.skipped_unicast_route")
                 continue
@@ -1002,16 +1015,23 @@ class SpfSolver:
             if r is not None:
                 db.addUnicastRoute(r)
 
-        for (label, node), r_ in zip(label_to_node.items(), sel[len(uni):]):
+        # (the label sets' selections straight from the kernel's arrays: one
+        # tolist() each, not a _SetResult per label)
+        cnt_l = cnt[len(uni):].tolist()
+        first = len(uni) * deg
+        edge_l = edge[first:first + len(cnt_l) * deg].tolist()
+        metric_l = metric[first:first + len(cnt_l) * deg].tolist()
+        for k, (label, node) in enumerate(label_to_node.items()):
             if node == me:
                 db.addMplsRoute(RibMplsEntry(label, {NextHopThrift(
                     bytes(16), None, 0, MplsAction("POP_AND_LOOKUP"), area, None)}))
                 continue
-            if not r_.hops:
+            c, b = cnt_l[k], k * deg
+            if not c:
                 self._bump("decision.no_route_to_label")
                 continue
             db.addMplsRoute(RibMplsEntry(label, self._next_hops(
-                ls, me, area, r_, False, {node}, label)))
+                ls, me, area, zip(edge_l[b:b + c], metric_l[b:b + c]), False, {node}, label)))
 
     def getNextHops(self, ls: LinkState, me: str, dsts: Sequence[str], isV4: bool = False,
                     swapLabel: Optional[int] = None) -> Tuple[Optional[int], Set[NextHopThrift]]:
