@@ -24,6 +24,10 @@ Each fixture is ``tests/golden/fullsize_<name>.npz`` holding the oracle's
   3000 shortest-path-tree links with the largest subtrees (every failure
   whose affected region can exceed a GPU wave team; the affected nodes of a
   tree link's failure lie in its subtree).
+* ``ba20k_whatif_all`` -- config 5's repair machinery at a scale the oracle
+  covers whole: runSpf("0", true, {l}) digests for EVERY link of a 20k-node
+  Barabasi-Albert graph (m = 4, ~80k links; wave-team, group-team and
+  overflow repairs all occur).
 * ``ba250k_spf`` -- the large-graph regime (N2): 64 sampled sources of the
   config-5 graph, weighted SPF + next hops, integer restatement.
 
@@ -66,6 +70,7 @@ WORKLOADS = {
     "wan2k_ksp2_all": lambda: T.wan(2000, 1000, seed=1),
     "ba250k_whatif": lambda: T.barabasi_albert(250_000, 4, seed=1),
     "ba250k_spf": lambda: T.barabasi_albert(250_000, 4, seed=1),
+    "ba20k_whatif_all": lambda: T.barabasi_albert(20_000, 4, seed=7),
 }
 
 
@@ -165,6 +170,17 @@ def make(name: str, threads: int) -> None:
         out["srcs"] = srcs
         out["digest"] = ksp2_digests(orc, table, srcs, threads=threads)
         meta["oracle"] = "getKthPaths k=1,2 (trace + runSpf with ignore set), every source"
+    elif name == "ba20k_whatif_all":
+        links = np.unique(csr[3]).astype(np.uint32)
+        fails = [(ls._link(int(l))._n1, ls._link(int(l))._if1) for l in links]
+        base, dig = whatif_digests_int(orc, table, "0", fails, threads=threads)
+        out["links"] = links
+        out["n_dist_changed"] = dig["n_dist_changed"]
+        out["n_nh_changed"] = dig["n_nh_changed"]
+        out["hash"] = dig["hash"]
+        out["base"] = np.array(base, np.uint64)
+        meta["oracle"] = "integer-CSR restatement of runSpf(src, true, {link}), every link"
+        meta["src"] = "0"
     elif name == "ba250k_whatif":
         links, big = ba_failures(ls, names, csr, rng)
         fails = [(ls._link(int(l))._n1, ls._link(int(l))._if1) for l in links]

@@ -12,7 +12,8 @@ output layout) and compared source by source, failure by failure:
 * KSP2 (config 4): 256 sources x all 2000 destinations, per-pair digests
   for 8 of them;
 * what-if (config 5): ~16.5k single-link failures of the 250k-node graph,
-  including the 3000 shortest-path-tree links with the largest subtrees;
+  including the 3000 shortest-path-tree links with the largest subtrees,
+  and every one of the ~80k failures of a 20k-node graph of the same family;
 * large-graph SPF + next hops (N2): 64 sources of the 250k-node graph.
 """
 
@@ -111,6 +112,31 @@ def test_whatif_ba250k_16k_failures_match_oracle():
         _report(got[f], g[f], f"what-if {f}", [int(l) for l in links])
     # the sample reaches the large repairs (workgroup teams)
     assert int(g["n_nh_changed"].max()) > 50_000
+
+
+@pytest.mark.parametrize("wavecap", [None, "128"], ids=["default", "wavecap128"])
+def test_whatif_ba20k_every_failure_matches_oracle(wavecap, monkeypatch):
+    """Config 5's repair machinery where the oracle covers every failure: all
+    ~80k single-link failures of a 20k-node Barabasi-Albert graph from "0"
+    (cold, wave-team, group-team and overflow repairs), on the default path
+    and with the wave teams' |D| cap lowered so more repairs overflow to the
+    workgroup teams."""
+    if wavecap:
+        monkeypatch.setenv("SPF_WHATIF_WAVECAP", wavecap)
+    meta, g = golden("ba20k_whatif_all")
+    ls, names, csr, cd = _make("ba20k_whatif_all")
+    assert cd == meta["csr_digest"]
+    links = g["links"]
+    with _engine(csr) as eng:
+        got_links, got, base = eng.whatif(names.index(meta["src"]))
+    assert np.array_equal(np.sort(got_links), links)
+    order = np.argsort(got_links)
+    assert (int(base["n_dist_changed"]), int(base["n_nh_changed"]), int(base["hash"])) == \
+        tuple(int(x) for x in g["base"])
+    for f in ("n_dist_changed", "n_nh_changed", "hash"):
+        _report(got[f][order], g[f], f"what-if {f}", [int(l) for l in links])
+    # the graph reaches repairs past a wave team's cap (workgroup teams)
+    assert int(g["n_nh_changed"].max()) > 1024
 
 
 @pytest.mark.parametrize("big", ["1", "0"], ids=["big_kernel", "exact_kernel"])
