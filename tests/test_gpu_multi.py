@@ -8,7 +8,8 @@ N members there computes exactly what N GPUs would.
   members: per-source digests computed on the owning member against the
   oracle's (tests/golden/fullsize_*.npz);
 * a member's resident rows, bitmaps and pathLinks equal one plan's;
-* hipGraph replays of the members' executes (spf_mplan_set_graphs);
+* hipGraph replays of the members' executes (spf_mplan_set_graphs), also
+  interleaved with another context's grid-resident launches;
 * the facade: getSpfResult(node) answered from the resident pass equals the
   oracle (metrics, next hops, pathLinks order) and counts spf_runs like the
   reference's lazy getSpfResult (LinkState.cpp:815); a publication drops the
@@ -120,6 +121,43 @@ def test_multi_context_graph_replay_and_patch():
             b.free()
     assert (got != want).any()  # the drain changed results
     assert np.array_equal(got, ref)
+
+
+def test_graph_replays_beside_another_contexts_resident_launches():
+    """replays of captured team-BFS executes (grid-resident) and a
+    second context's grid-resident what-if launches, issued back to back on
+    the same device with no synchronisation between the two contexts, stay
+    ordered per device (resident_order around every replay): both results
+    are exact and no team barrier gives up."""
+    from openr_amd.engine import DIGEST_DTYPE
+
+    meta, g = golden("fabric_full")
+    ls, names, csr, cd = _make("fabric_full")
+    want = np.zeros(len(names), np.uint64)
+    want[g["srcs"].astype(np.int64)] = g["digest"]
+    topo = T.barabasi_albert(3000, 3, seed=5)
+    ls2 = LinkState(device=-1)
+    ls2.updateAdjacencyDatabases(topo.lsdb)
+    csr2 = ls2.flatten()[1:]
+    with SpfMultiEngine([0] * 8) as m, SpfEngine(0) as e2:
+        m.load(*csr)
+        p = m.plan(np.arange(len(names)))
+        assert p.member_kernels(0)[0] == "msbfs_team_kernel"
+        p.set_graphs(True)
+        e2.load(*csr2)
+        links, ref, base = e2.whatif(0)
+        wp = e2.whatif_plan(0)
+        out = hiprt.DeviceArray(2 * len(links), np.uint64, zero=True)
+        for _ in range(4):  # execute, capture, replays -- each beside a what-if launch
+            p.execute()
+            wp.execute(out.ptr)
+        p.synchronize()
+        e2.check()
+        assert np.array_equal(p.digest(), want)
+        got = out.numpy().view(DIGEST_DTYPE)[: len(links)]
+        out.free()
+    for f in ("n_dist_changed", "n_nh_changed", "hash"):
+        assert np.array_equal(got[f], ref[f])
 
 
 @pytest.mark.parametrize("ulm", [True, False], ids=["metric", "hops"])
