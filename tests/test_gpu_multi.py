@@ -123,6 +123,36 @@ def test_multi_context_graph_replay_and_patch():
     assert np.array_equal(got, ref)
 
 
+def test_patch_right_after_execute_is_ordered_after_it():
+    """a drain patched onto every replica right after an execute
+    (no synchronize between) waits for the members' executes still reading
+    the graph (repeated ids: members run on the first member's stream), and
+    the next execute follows the patched graph."""
+    ls, names, csr, cd = _make("fabric_full")
+    victim = names.index("3-2-5")
+    csr2 = list(csr)
+    csr2[4] = csr[4].copy()
+    csr2[4][victim] = 1
+    with SpfMultiEngine([0, 0, 0, 0]) as m, SpfMultiEngine([0]) as ref:
+        m.load(*csr)
+        p = m.plan(np.arange(len(names)))
+        for _ in range(2):
+            p.execute()
+            m.set_overload([victim], [1])  # no synchronize before the patch
+            p.execute()
+            m.set_overload([victim], [0])
+        m.set_overload([victim], [1])
+        p.execute()
+        p.synchronize()
+        got = p.digest()
+        ref.load(*csr2)
+        q = ref.plan(np.arange(len(names)))
+        q.execute()
+        q.synchronize()
+        want = q.digest()
+    assert np.array_equal(got, want)
+
+
 def test_graph_replays_beside_another_contexts_resident_launches():
     """replays of captured team-BFS executes (grid-resident) and a
     second context's grid-resident what-if launches, issued back to back on
