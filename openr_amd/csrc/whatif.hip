@@ -33,6 +33,7 @@
 //  graph (ascending id).
 // ============================================================================
 #include "engine_internal.h"
+#include "wave_ops.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -307,6 +308,7 @@ __global__ __launch_bounds__(kCoopThreads) void gsssp_coop_kernel(CoopSssp a) {
 // result hash.
 constexpr uint32_t kLevelCap = 1u << 16;  // distance values bucketed directly
 constexpr uint32_t kMaxLevels = 1024;     // non-empty levels worth a barrier each
+constexpr uint32_t kLdsHist = 4096;       // distance values a block histograms in LDS
 
 struct BaseArgs {
   CoopSssp sp;
@@ -319,6 +321,7 @@ struct BaseArgs {
   unsigned long long* prof;  // SPF_WHATIF_PROF: [16] phase clocks of block 0
   uint32_t* parent;     // [N] one tight expanded predecessor (levels path)
   uint32_t* sub;        // [N] subtree sizes of the parent tree, 0 without levels
+  unsigned long long* lprof = nullptr;  // SPF_WHATIF_PROF: [2 x 64] per-level clock, size
 };
 
 // word j of nh(v) from v's in-edges first, first + stride, ... (a wave
@@ -504,25 +507,49 @@ __device__ void seg_nh(const WiGraph& g, const uint32_t* dist, uint32_t* nhb, ui
 // lvl[d] = end of bucket d in `order`).  Starts and ends with a grid barrier.
 __device__ bool level_nh(const XGrid& grid, const WiGraph& g, const uint32_t* dist,
                          uint32_t* nhb, uint32_t* lvl, uint32_t* order, uint32_t* misc,
-                         uint32_t* parent) {
+                         uint32_t* parent, unsigned long long* lstamp = nullptr) {
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t gsz = gridDim.x * blockDim.x;  // a multiple of 64
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t N = g.N, W = g.W;
   const uint64_t NW = (uint64_t)N * W;
+  // per-block histogram of the distance values and the block's write
+  // cursors into `order` (LDS, when maxd < kLdsHist): one global atomic per
+  // (block, value) instead of one per node -- 250k node atomics on ~30
+  // counters (and on one for the maximum) were 1.6 ms of the what-if base
+  // pass's 2.4 ms next-hop phase (per-level clocks, r05_wb)
+  __shared__ uint32_t bh[kLdsHist], bc[kLdsHist];
   grid.sync();
-  // ---- distance range and per-value counts ----
-  for (uint32_t v = gtid; v < N; v += gsz) {
-    const uint32_t d = ld(&dist[v]);
-    if (d != kInf) atomicMax(&misc[0], d);
+  // ---- distance range (one atomic per wave) and per-value counts ----
+  {
+    uint32_t m = 0;
+    for (uint32_t v = gtid; v < N; v += gsz) {
+      const uint32_t d = ld(&dist[v]);
+      if (d != kInf) m = max(m, d);
+    }
+    m = wave_max32(m);
+    if (lane == 0 && m) atomicMax(&misc[0], m);
   }
   grid.sync();
   const uint32_t maxd = ld(&misc[0]);
   bool levels = maxd < kLevelCap;
+  const bool hist = maxd < kLdsHist;  // block-uniform
   if (levels) {
-    for (uint32_t v = gtid; v < N; v += gsz) {
-      const uint32_t d = ld(&dist[v]);
-      if (d != kInf && atomicAdd(&lvl[d], 1u) == 0) atomicAdd(&misc[1], 1u);
+    if (hist) {
+      for (uint32_t i = threadIdx.x; i <= maxd; i += blockDim.x) bh[i] = 0u;
+      __syncthreads();
+      for (uint32_t v = gtid; v < N; v += gsz) {
+        const uint32_t d = ld(&dist[v]);
+        if (d != kInf) atomicAdd(&bh[d], 1u);
+      }
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i <= maxd; i += blockDim.x)
+        if (bh[i] && atomicAdd(&lvl[i], bh[i]) == 0) atomicAdd(&misc[1], 1u);
+    } else {
+      for (uint32_t v = gtid; v < N; v += gsz) {
+        const uint32_t d = ld(&dist[v]);
+        if (d != kInf && atomicAdd(&lvl[d], 1u) == 0) atomicAdd(&misc[1], 1u);
+      }
     }
     grid.sync();
     levels = ld(&misc[1]) <= kMaxLevels;
@@ -555,10 +582,22 @@ __device__ bool level_nh(const XGrid& grid, const WiGraph& g, const uint32_t* di
       if (threadIdx.x == 0) st(&lvl[maxd + 1], carry);
     }
     grid.sync();
-    // scatter nodes into distance order (lvl[d] advances to the bucket end)
-    for (uint32_t v = gtid; v < N; v += gsz) {
-      const uint32_t d = ld(&dist[v]);
-      if (d != kInf) st(&order[atomicAdd(&lvl[d], 1u)], v);
+    // scatter nodes into distance order (lvl[d] advances to the bucket end):
+    // with the block histogram, one global atomic per (block, value)
+    // reserves the block's range, LDS cursors place its nodes
+    if (hist) {
+      for (uint32_t i = threadIdx.x; i <= maxd; i += blockDim.x)
+        if (bh[i]) bc[i] = atomicAdd(&lvl[i], bh[i]);
+      __syncthreads();
+      for (uint32_t v = gtid; v < N; v += gsz) {
+        const uint32_t d = ld(&dist[v]);
+        if (d != kInf) st(&order[atomicAdd(&bc[d], 1u)], v);
+      }
+    } else {
+      for (uint32_t v = gtid; v < N; v += gsz) {
+        const uint32_t d = ld(&dist[v]);
+        if (d != kInf) st(&order[atomicAdd(&lvl[d], 1u)], v);
+      }
     }
     grid.sync();
     // level by level: every predecessor of a level-d node sits at a lower level
@@ -586,6 +625,11 @@ __device__ bool level_nh(const XGrid& grid, const WiGraph& g, const uint32_t* di
       }
       begin = end;
       grid.sync();
+      // diagnostics (SPF_WHATIF_PROF): the clock after level d, its size
+      if (lstamp && gtid == 0 && d < 64) {
+        lstamp[2 * d] = wall_clock64();
+        lstamp[2 * d + 1] = n_lvl;
+      }
     }
   } else {
     // fixed-point sweeps (monotone union over the DAG), flags rotate by 3
@@ -629,7 +673,8 @@ __global__ __launch_bounds__(kCoopThreads) void whatif_base_kernel(BaseArgs a) {
   coop_sssp(grid, a.sp);  // starts and ends with a grid barrier
   if (stamp) a.prof[1] = wall_clock64();
   const uint32_t* dist = a.sp.dist;
-  const bool levels = level_nh(grid, g, dist, a.nhb, a.lvl, a.order, a.misc, a.parent);
+  const bool levels = level_nh(grid, g, dist, a.nhb, a.lvl, a.order, a.misc, a.parent, a.lprof);
+  if (stamp) a.prof[6] = wall_clock64();
   if (levels) {
     const uint32_t maxd = ld(&a.misc[0]);
     // subtree sizes of the parent tree, deepest level first: a lower bound
@@ -2106,7 +2151,7 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
   if (std::getenv("SPF_WHATIF_PROF")) {  // [bt teams][base][wave teams] x 16
-    const size_t slots = 16 * (bt + 1 + p->wave_teams);
+    const size_t slots = 16 * (bt + 1 + p->wave_teams) + 128;  // + the base's per-level clocks
     HIP_TRY(c, p->d_prof.alloc(slots));
     HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, slots * 8, c->stream));
   }
@@ -2161,6 +2206,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
                p->d_sub.p};
     a.sp.bar = p->d_bar.p;
     a.sp.fault = c->d_fault.p;
+    if (p->d_prof.p) a.lprof = p->d_prof.p + 16ull * (p->big_teams + 1 + p->wave_teams);
     HIP_TRY(c, hipMemsetAsync(p->d_bar.p, 0, 4 * kGridBarWords, s));
     void* args[] = {&a};
     if (const spf_status st = resident_order(c, s); st != SPF_OK) return st;
@@ -2233,7 +2279,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   }
   if (p->d_prof.p) {  // diagnostics: phase ticks (100 MHz) per team, accumulated over repairs
     const size_t bt = p->big_teams, wt = p->wave_teams;
-    std::vector<unsigned long long> h(16ull * (bt + 1 + wt));
+    std::vector<unsigned long long> h(16ull * (bt + 1 + wt) + 128);
     HIP_TRY(c, hipMemcpyAsync(h.data(), p->d_prof.p, h.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     auto line = [&](const char* who, const unsigned long long* r) {
@@ -2258,8 +2304,19 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
     line("wave-teams(sum)", sum.data());
     std::fprintf(stderr, "whatif wave teams %zu, busiest team %llu ticks (x10ns)\n", wt, busiest);
     const unsigned long long* r = &h[16 * bt];
-    std::fprintf(stderr, "whatif base sssp=%llu nh=%llu hash=%llu (x10ns) maxd=%llu levels=%llu W=%u\n",
-                 r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4], r[5], p->W);
+    std::fprintf(stderr, "whatif base sssp=%llu nh=%llu (of which subtree sizes %llu) hash=%llu (x10ns) maxd=%llu levels=%llu W=%u\n",
+                 r[1] - r[0], r[2] - r[1], r[6] ? r[2] - r[6] : 0ull, r[3] - r[2], r[4], r[5], p->W);
+    const unsigned long long* lv = &h[16 * (bt + 1 + wt)];
+    unsigned long long prev = 0;
+    std::string line2 = "whatif base levels (distance:nodes:ticks)";
+    for (int d = 1; d < 64; ++d) {
+      if (!lv[2 * d]) continue;
+      const unsigned long long t0 = prev ? prev : lv[2 * d];
+      line2 += " " + std::to_string(d) + ":" + std::to_string(lv[2 * d + 1]) + ":" +
+               std::to_string(prev ? lv[2 * d] - t0 : 0ull);
+      prev = lv[2 * d];
+    }
+    std::fprintf(stderr, "%s\n", line2.c_str());
   }
   if (d_base) {
     // the unfailed digest: nothing changed, hash = H
