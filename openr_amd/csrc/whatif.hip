@@ -201,6 +201,46 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
   return x;
 }
 
+// ---------------------------------------------------------------------------
+//  wave helpers of the repairs: lanes over flattened edges
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_pull(uint32_t x, uint32_t k) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)x);
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The edges of up to 64 nodes (lane k holds node v, `valid`), flattened:
+// chunks of 64 (node slot, edge) pairs.  f(k, e, act) runs on every lane of
+// the wave (so it may ballot / pull); `act` marks the lanes holding an edge,
+// k is the node slot (lane) that edge belongs to.  All 64 lanes must be
+// active.
+template <class F>
+__device__ __forceinline__ void wave_edges(const uint32_t* __restrict__ row_ptr, uint32_t v,
+                                           bool valid, F&& f) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t b0 = 0, deg = 0;
+  if (valid) {
+    b0 = row_ptr[v];
+    deg = row_ptr[v + 1] - b0;
+  }
+  const uint32_t incl = wave_incl_scan32(deg);
+  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+  const uint32_t excl = incl - deg;
+  for (uint32_t base = 0; base < total; base += 64) {
+    const uint32_t s = base + lane;
+    // owner: the last slot whose first edge is <= s (slots with no edges
+    // share their successor's offset and lose to it)
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+      if (lane_pull(excl, k + step) <= s) k += step;
+    const uint32_t e = lane_pull(b0, k) + s - lane_pull(excl, k);
+    f(k, e, s < total);
+  }
+}
+
 struct CoopSssp {
   const uint32_t* row_ptr;
   const uint32_t* col;
@@ -252,26 +292,23 @@ __device__ void coop_sssp(const XGrid& grid, const CoopSssp& a) {
       const uint32_t nd = du + (a.hop ? 1u : a.wt[e]);
       if (nd < atomicMin(&a.dist[v], nd)) atomicOr(&a.bm[v >> 5], 1u << (v & 31));
     };
+    // a wave takes 64 frontier nodes at a time, lanes over their flattened
+    // out-edges (wave_edges): a node's relaxations go out 64 at a time
+    // instead of one returning atomic after another per lane (a degree-30
+    // node was 30 dependent round trips of the iteration's critical path)
     for (uint32_t b = gtid - lane; b < len; b += gsz) {
       const uint32_t i = b + lane;
-      uint32_t e0 = 0, e1 = 0, du = 0;
+      uint32_t u = 0, du = 0;
+      bool x = false;
       if (i < len) {
-        const uint32_t u = ld(&cur[i]);
-        if (!a.ovl[u] || u == a.src) {  // drained: recorded, not expanded
-          du = ld(&a.dist[u]);
-          e0 = a.row_ptr[u];
-          e1 = a.row_ptr[u + 1];
-        }
+        u = ld(&cur[i]);
+        x = !a.ovl[u] || u == a.src;  // drained: recorded, not expanded
+        if (x) du = ld(&a.dist[u]);
       }
-      const bool hub = e1 - e0 > kCoopHubDeg;
-      if (!hub)
-        for (uint32_t e = e0; e < e1; ++e) relax(e, du);
-      for (uint64_t hubs = __ballot(hub); hubs; hubs &= hubs - 1) {
-        const int l = __builtin_ctzll(hubs);
-        const uint32_t hb = __builtin_amdgcn_readlane(e0, l), he = __builtin_amdgcn_readlane(e1, l),
-                       hd = __builtin_amdgcn_readlane(du, l);
-        for (uint32_t e = hb + lane; e < he; e += 64) relax(e, hd);
-      }
+      wave_edges(a.row_ptr, u, x, [&](uint32_t k, uint32_t e, bool act) {
+        const uint32_t dk = lane_pull(du, k);
+        if (act) relax(e, dk);
+      });
     }
     grid.sync();
     for (uint32_t wb = gtid - lane; wb < bm_words; wb += gsz) {  // wave-uniform
@@ -906,46 +943,6 @@ template <bool GROUP>
 __device__ __forceinline__ void stq(unsigned long long* p, unsigned long long v) {
   if constexpr (GROUP) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// ---------------------------------------------------------------------------
-//  wave helpers of the repairs: lanes over flattened edges
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_pull(uint32_t x, uint32_t k) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)x);
-}
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// The edges of up to 64 nodes (lane k holds node v, `valid`), flattened:
-// chunks of 64 (node slot, edge) pairs.  f(k, e, act) runs on every lane of
-// the wave (so it may ballot / pull); `act` marks the lanes holding an edge,
-// k is the node slot (lane) that edge belongs to.  All 64 lanes must be
-// active.
-template <class F>
-__device__ __forceinline__ void wave_edges(const uint32_t* __restrict__ row_ptr, uint32_t v,
-                                           bool valid, F&& f) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t b0 = 0, deg = 0;
-  if (valid) {
-    b0 = row_ptr[v];
-    deg = row_ptr[v + 1] - b0;
-  }
-  const uint32_t incl = wave_incl_scan32(deg);
-  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-  const uint32_t excl = incl - deg;
-  for (uint32_t base = 0; base < total; base += 64) {
-    const uint32_t s = base + lane;
-    // owner: the last slot whose first edge is <= s (slots with no edges
-    // share their successor's offset and lose to it)
-    uint32_t k = 0;
-#pragma unroll
-    for (uint32_t step = 32; step; step >>= 1)
-      if (lane_pull(excl, k + step) <= s) k += step;
-    const uint32_t e = lane_pull(b0, k) + s - lane_pull(excl, k);
-    f(k, e, s < total);
-  }
 }
 
 // FNV-1a of both next-hop rows of a D node and whether they differ: the
