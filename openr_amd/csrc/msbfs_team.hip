@@ -56,6 +56,16 @@ constexpr uint32_t kTmWindow = (1u << kTmPlanes) - 1;     // levels per window; 
 static_assert(kTmPlanes == (int)kTeamPlanes, "sdirect rows: the next-hop pass reads kTeamPlanes planes");
 constexpr int kTmCopy = 10;                               // uint4 per thread of the frontier copy
 constexpr uint32_t kTmRows = 16;                          // sources per flush tile (80 B each per node)
+static_assert(kTmRows == 16 && kTmPlanes == 4, "first-window flush: two 4 x 8 plane transposes per tile");
+// one flush-tile row of the first window: source r's code from the
+// transposed nibbles (see the flush), u32 (kInf if unreached) and u8 (0xF)
+__device__ __forceinline__ void flush_code(uint32_t* T32, uint8_t* T8, uint32_t lane, uint32_t r,
+                                           uint32_t X0, uint32_t X1) {
+  const uint32_t nbl = ((r >> 2) & 1u) | ((r & 1u) << 1) | (((r >> 1) & 1u) << 2);
+  const uint32_t q = (((r & 8u) ? X1 : X0) >> (4 * nbl)) & 0xFu;
+  T32[r * 64 + lane] = q == 0xFu ? kInf : q;  // first window: base == 0
+  T8[r * 64 + lane] = (uint8_t)q;              // q <= kTmWindow - 1 = 14, or 0xF
+}
 constexpr uint32_t kTmBarPad = 32;            // words per team: counter line + 3 flag lines
 constexpr uint32_t kSliceNodes = 64;          // nodes per sliced-ELL slice (= wave width)
 
@@ -354,23 +364,37 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
           if (sv[i] >= N) continue;  // wave-uniform
           const uint32_t v = sv[i] + lane;
           for (uint32_t g0 = 0; g0 < nb; g0 += kTmRows) {
-            const uint32_t gn = min(kTmRows, nb - g0);
-            // a group's 16 sources lie in one 32-bit half of the masks: 32-bit
-            // bit-field extracts, ~12 VALU per (source, node) (the 64-bit
-            // shifts made the flush VALU-bound)
-            const bool hi = g0 >= 32;
-            uint32_t pw[kTmPlanes];
+            const uint32_t gn = __builtin_amdgcn_readfirstlane(min(kTmRows, nb - g0));
+            // the group's codes as nibbles, by a 4 x 8 bit-matrix transpose per
+            // half: W = byte h of the four planes (bit 8b + r), two delta swaps
+            // (index bits 0 <-> 3, 1 <-> 4) put plane b of source 8h + r at bit
+            // 4 nbl(r) + b, nbl(r) = r2 + 2 r0 + 4 r1; a row then costs one
+            // constant bit-field extract (the per-row gather of four plane bits
+            // made the flush VALU-bound).  Unreached entries: all planes set
+            // (code 0xF; the planes hold no bit of an unreached node)
+            uint32_t X0, X1;
+            {
+              auto dswap = [](uint32_t x, uint32_t m, int d) {
+                const uint32_t t = ((x >> d) ^ x) & m;
+                return x ^ t ^ (t << d);
+              };
+              const uint32_t un = v < N ? ~(uint32_t)(vis[i] >> g0) : ~0u;
+              uint32_t pw[kTmPlanes];
 #pragma unroll
-            for (int b = 0; b < kTmPlanes; ++b) pw[b] = hi ? (uint32_t)(P[i][b] >> 32) : (uint32_t)P[i][b];
-            const uint32_t vw = v < N ? (hi ? (uint32_t)(vis[i] >> 32) : (uint32_t)vis[i]) : 0u;
-            for (uint32_t r = 0; r < gn; ++r) {
-              const uint32_t sh = (g0 + r) & 31u;
-              uint32_t q = 0;
+              for (int b = 0; b < kTmPlanes; ++b) pw[b] = (uint32_t)(P[i][b] >> g0) | un;
+              auto half = [&](int h) {
+                const uint32_t w = ((pw[0] >> (8 * h)) & 0xFFu) | (((pw[1] >> (8 * h)) & 0xFFu) << 8) |
+                                   (((pw[2] >> (8 * h)) & 0xFFu) << 16) | (((pw[3] >> (8 * h)) & 0xFFu) << 24);
+                return dswap(dswap(w, 0x00AA00AAu, 7), 0x0000CCCCu, 14);
+              };
+              X0 = half(0);
+              X1 = half(1);
+            }
+            if (gn == kTmRows) {
 #pragma unroll
-              for (int b = 0; b < kTmPlanes; ++b) q |= ((pw[b] >> sh) & 1u) << b;
-              const bool seen = (vw >> sh) & 1u;
-              T32[r * 64 + lane] = seen ? q : kInf;  // first window: base == 0
-              T8[r * 64 + lane] = seen ? q : 0xFFu;   // q <= kTmWindow - 1 < 254
+              for (uint32_t r = 0; r < kTmRows; ++r) flush_code(T32, T8, lane, r, X0, X1);
+            } else {
+              for (uint32_t r = 0; r < gn; ++r) flush_code(T32, T8, lane, r, X0, X1);
             }
             if (a.D && !(a.dbg & 1u))
               for (uint32_t r4 = 0; r4 < gn; r4 += 4) {
@@ -386,7 +410,7 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
             if (a.S && !(a.dbg & 2u)) {
               // the sliced rows (ecmp_sliced_kernel's layout with P =
               // kTmPlanes): word w of row r holds plane b at w * P + b, bit t
-              // = node 32w + t; code all-ones = unreachable (byte 0xFF; nodes
+              // = node 32w + t; code all-ones = unreachable (tile byte 0x0F; nodes
               // past N too).  From the byte tile: lane (row r = lane / 4,
               // quarter q = lane % 4) turns its 16 bytes into a 16-bit piece
               // of each plane (slice_rows_kernel's multiply gather), lanes
@@ -414,7 +438,12 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
             if (a.Dn) {
               const uint32_t r = lane >> 2;
               if (r < gn) {
-                const uint4 x = *reinterpret_cast<const uint4*>(T8 + r * 64 + (lane & 3) * 16);
+                uint4 x = *reinterpret_cast<const uint4*>(T8 + r * 64 + (lane & 3) * 16);
+                auto unreached = [](uint32_t w) {  // byte 0x0F (tile) -> 0xFF (u8 rows)
+                  const uint32_t m = w & (w >> 1) & (w >> 2) & (w >> 3) & 0x01010101u;
+                  return w | ((m << 8) - (m << 4));
+                };
+                x = make_uint4(unreached(x.x), unreached(x.y), unreached(x.z), unreached(x.w));
                 *reinterpret_cast<uint4*>(a.Dn + (size_t)(row0 + g0 + r) * a.npitch + sv[i] +
                                           (lane & 3) * 16) = x;
               }
