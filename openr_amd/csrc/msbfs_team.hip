@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kTmThreads) void msbfs_team_kernel(TeamArgs a,
   auto sweep = [&]() {
     uint64_t acc = 0;
     uint32_t cur = 0xFFFFFFFFu;
-    constexpr int H = 8;  // columns per step: two steps in flight (registers: OWN = 4 planes)
+    constexpr int H = OWN >= 2 ? 4 : 8;  // columns per step, two steps in flight (OWN >= 2: 4 -- x4 / x8 members 3-4 % faster than 8)
     uint32_t ca[H], cb[H];
     // a step's column loads: stream words by scalar loads, group offset in
     // an SGPR, lane offset in a VGPR
