@@ -407,6 +407,10 @@ class _SetResult:
 class SpfSolver:
     """``openr::SpfSolver`` (Decision.h) on the MI355X engine."""
 
+    # one-advertiser prefixes skip the selection walk (tests switch it off to
+    # compare against the generic walk)
+    _single_fast = True
+
     def __init__(self, myNodeName: str, enableV4: bool, computeLfaPaths: bool,
                  enableOrderedFib: bool = False, bgpDryRun: bool = False,
                  enableBestRouteSelection: bool = False) -> None:
@@ -896,6 +900,25 @@ class SpfSolver:
                 continue
             if hasBGP and ((hasNonBGP and not self.enableBestRouteSelection) or missingMv):
                 self._bump("decision.skipped_unicast_route")
+                continue
+            if ents is entries and self._single_fast and not self.enableBestRouteSelection:
+                # one advertiser, no best-route selection: the openr walk and the
+                # BGP walk (:791-832) both pick it, and the drained-node filter
+                # (:766-789) keeps the result whether it is drained or not
+                res = BestRouteSelectionResult(True, [na0], na0)
+                self._bestRoutesCache[prefix] = res
+                if na0[0] == me and not hasSelfPrepend:
+                    continue  # self-advertised
+                falgo = e0.forwardingAlgorithm
+                if not single:
+                    r = (self._selectBestPathsSpf if falgo == "SP_ECMP" else self._selectBestPathsKsp2)(
+                        me, prefix, res, ents, hasBGP, e0.forwardingType, areas)
+                    if r is not None:
+                        db.addUnicastRoute(r)
+                elif falgo == "SP_ECMP" and e0.forwardingType == "IP":
+                    uni.append((prefix, ents, [na0[0]], res, hasBGP))
+                else:
+                    sr.append((prefix, ents, res, falgo, hasBGP))
                 continue
             res = self._selectBestRoutes(me, ents, hasBGP, areaLinkStates)
             if not res.success:

@@ -100,3 +100,57 @@ def test_route_db_from_resident_pass_equals_plan_path(lfa):
         me = names[3]
         assert rows(SpfSolver(me, True, lfa).buildRouteDb(me, {"0": res}, ps)) == \
             rows(SpfSolver(me, True, lfa).buildRouteDb(me, {"0": one}, ps))
+
+
+@pytest.mark.parametrize("v4,bgp_dry", [(False, False), (True, True)], ids=["v6", "v4_bgpdry"])
+def test_single_advertiser_fast_path_equals_generic_walk(v4, bgp_dry):
+    """buildRouteDb's one-advertiser shortcut (no selection walk, no drained
+    filter) yields the same route DB, best-routes cache and counters as the
+    generic walk: loopbacks, v4 prefixes, a BGP prefix with a metric vector and
+    one without, SR_MPLS SP_ECMP / KSP2 prefixes, self-advertised prefixes with
+    and without a prepend label, a drained advertiser, anycast sets."""
+    from openr_amd.spf_solver import MetricEntity, MetricVector
+
+    topo = T.random_graph(40, 110, 5, max_metric=4, parallel_frac=0.2, overload_frac=0.1)
+    names = topo.nodes
+    ps = PrefixState()
+    mv = MetricVector(1, [MetricEntity(1, 10, metric=(5,))])
+    for i, node in enumerate(names):
+        ps.updatePrefix(node, "0", PrefixEntry(f"fd00:{i:x}::/64"))
+        ps.updatePrefix(node, "0", PrefixEntry(f"10.{i}.0.0/16"))
+        if i % 5 == 0:
+            ps.updatePrefix(node, "0", PrefixEntry(f"fd02:{i:x}::/64", type="BGP", mv=mv))
+        if i % 7 == 0:
+            ps.updatePrefix(node, "0", PrefixEntry(f"fd03:{i:x}::/64", type="BGP"))
+        if i % 4 == 0:
+            ps.updatePrefix(node, "0", PrefixEntry(f"fd04:{i:x}::/64", forwardingType="SR_MPLS"))
+        if i % 6 == 0:
+            ps.updatePrefix(node, "0", PrefixEntry(f"fd05:{i:x}::/64", forwardingType="SR_MPLS",
+                                                   forwardingAlgorithm="KSP2_ED_ECMP"))
+        if i % 3 == 0:
+            ps.updatePrefix(node, "0", PrefixEntry(f"fd06:{i:x}::/64", prependLabel=70000 + i,
+                                                   minNexthop=1))
+    for k in range(6):  # anycast (the generic walk on both sides)
+        for a in (k, k + 11, k + 23):
+            ps.updatePrefix(names[a], "0", PrefixEntry(f"fd01:{k:x}::/64"))
+
+    def dump(solver, db):
+        uni = {p: (sorted(db.unicastRoutes[p].nexthops, key=repr), db.unicastRoutes[p].bestArea,
+                   db.unicastRoutes[p].bestPrefixEntry, db.unicastRoutes[p].doNotInstall)
+               for p in db.unicastRoutes}
+        mpls = {l: sorted(r.nexthops, key=repr) for l, r in db.mplsRoutes.items()}
+        return uni, mpls, solver.getBestRoutesCache(), dict(solver.counters)
+
+    with LinkState() as ls:
+        ls.updateAdjacencyDatabases(topo.lsdb)
+        for me in (names[0], names[3], names[17]):
+            out = []
+            for fast in (True, False):
+                SpfSolver._single_fast = fast
+                try:
+                    sol = SpfSolver(me, v4, True, bgpDryRun=bgp_dry)
+                    out.append(dump(sol, sol.buildRouteDb(me, {"0": ls}, ps)))
+                finally:
+                    SpfSolver._single_fast = True
+            assert out[0] == out[1], me
+            assert out[0][0]  # routes exist
