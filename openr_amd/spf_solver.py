@@ -407,8 +407,9 @@ class _SetResult:
 class SpfSolver:
     """``openr::SpfSolver`` (Decision.h) on the MI355X engine."""
 
-    # one-advertiser prefixes skip the selection walk (tests switch it off to
-    # compare against the generic walk)
+    # one-advertiser prefixes skip the selection walk, and one-advertiser IP
+    # routes and label routes are assembled inline (tests switch it off to
+    # compare against the generic walk and getNextHopsThrift restatement)
     _single_fast = True
 
     def __init__(self, myNodeName: str, enableV4: bool, computeLfaPaths: bool,
@@ -484,10 +485,7 @@ class SpfSolver:
         (link, metric) selection (a _SetResult, or its hops: (edge, metric)
         pairs)."""
         out: Set[NextHopThrift] = set()
-        info = getattr(self, "_edge_info", None)
-        if info is None or info[0] is not ls or info[1] != me or info[2] is not self._lid:
-            info = self._edge_info = (ls, me, self._lid, {})
-        cache = info[3]
+        cache = self._link_fields(ls, me)
         # one action object per call (the route's), the named tuples built
         # with tuple.__new__ (the generated __new__ wrapper was a third of
         # the host route assembly: ~10^5 next hops per fabric build)
@@ -497,16 +495,28 @@ class SpfSolver:
         for e, metric in (res.hops if isinstance(res, _SetResult) else res):
             li = cache.get(e)
             if li is None:
-                link = ls._link(int(self._lid[e]))
-                li = cache[e] = (link.getOtherNodeName(me), link.getIfaceFromNode(me),
-                                 bytes(link.getNhV4FromNode(me)), bytes(link.getNhV6FromNode(me)),
-                                 link.getArea())
+                li = self._link_field(ls, me, cache, e)
             nb, iface, v4, v6, larea = li
             action = None if swap is None else (_PHP if nb in dsts else swap)
             m = metric & 0xFFFFFFFF
             add(mk(NextHopThrift, (v4 if isV4 else v6, iface, m - (1 << 32) if m >= 1 << 31 else m,
                                    action, larea, nb)))
         return out
+
+    def _link_fields(self, ls: LinkState, me: str) -> Dict[int, tuple]:
+        """directed edge -> (neighbour, iface, v4, v6, area) of me's link, kept
+        while the flattened graph (self._lid) is the same."""
+        info = getattr(self, "_edge_info", None)
+        if info is None or info[0] is not ls or info[1] != me or info[2] is not self._lid:
+            info = self._edge_info = (ls, me, self._lid, {})
+        return info[3]
+
+    def _link_field(self, ls: LinkState, me: str, cache: Dict[int, tuple], e: int) -> tuple:
+        link = ls._link(int(self._lid[e]))
+        li = cache[e] = (link.getOtherNodeName(me), link.getIfaceFromNode(me),
+                         bytes(link.getNhV4FromNode(me)), bytes(link.getNhV6FromNode(me)),
+                         link.getArea())
+        return li
 
     # -- SR_MPLS SP_ECMP: getNextHopsWithMetric / getNextHopsThrift with
     #    perDestination = true (Decision.cpp:829-893, 1107-1305) --------------------
@@ -916,7 +926,7 @@ class SpfSolver:
                     if r is not None:
                         db.addUnicastRoute(r)
                 elif falgo == "SP_ECMP" and e0.forwardingType == "IP":
-                    uni.append((prefix, ents, [na0[0]], res, hasBGP))
+                    uni.append((prefix, ents, [na0[0]], res, hasBGP, isV4))
                 else:
                     sr.append((prefix, ents, res, falgo, hasBGP))
                 continue
@@ -936,7 +946,7 @@ class SpfSolver:
                 if r is not None:
                     db.addUnicastRoute(r)
             elif falgo == "SP_ECMP" and ftype == "IP":
-                uni.append((prefix, ents, [na[0] for na in res.allNodeAreas], res, hasBGP))
+                uni.append((prefix, ents, [na[0] for na in res.allNodeAreas], res, hasBGP, isV4))
             else:
                 sr.append((prefix, ents, res, falgo, hasBGP))
 
@@ -996,25 +1006,40 @@ class SpfSolver:
                 continue
             label_to_node[label] = node
 
-        sets = [dsts for _, _, dsts, _, _ in uni] + [[n] for n in label_to_node.values()]
+        sets = [u[2] for u in uni] + [[n] for n in label_to_node.values()]
         sel = self._select(ls, me, sets)
 
         # IP routes with the same (link, metric) selection share one frozen
         # next-hop set (a fabric's destinations of one pod select alike)
         mins, cnt, edge, metric, deg = self._raw
         shared: Dict[tuple, FrozenSet[NextHopThrift]] = {}
-        for i, (prefix, ents, dsts, res, isBgp) in enumerate(uni):
-            c = int(cnt[i])
+        # the selections as bytes / lists once: per route only slices of them
+        # (numpy scalar reads and slices cost ~1 us each, 10^4 routes a build)
+        cnt_all = cnt.tolist()
+        eb, mb = edge.tobytes(), metric.tobytes()
+        dry = self.bgpDryRun
+        unicast = db.unicastRoutes
+        fast = self._single_fast
+        for i, (prefix, ents, dsts, res, isBgp, isV4) in enumerate(uni):
+            c = cnt_all[i]
             if not c:
                 self._bump("decision.no_route_to_prefix")
                 continue
-            isV4 = next(iter(ents.values())).isV4
-            key = (edge[i * deg:i * deg + c].tobytes(), metric[i * deg:i * deg + c].tobytes(), isV4)
+            b = i * deg
+            key = (eb[4 * b:4 * (b + c)], mb[8 * b:8 * (b + c)], isV4)
             nhs = shared.get(key)
             if nhs is None:
                 nhs = frozenset(self._next_hops(ls, me, area, sel[i], isV4, set(dsts), None))
                 shared[key] = nhs
-            r = self._addBestPaths(me, prefix, res.allNodeAreas, res.bestNodeArea, ents, nhs, isBgp)
+            best = res.allNodeAreas
+            if fast and len(best) == 1 and best[0][0] != me:  # _addBestPaths, one remote advertiser
+                need = ents[best[0]].minNexthop
+                if need is not None and need > len(nhs):
+                    continue  # min-nexthop requirement not met
+                bna = res.bestNodeArea  # (the drained filter keeps the unfiltered one)
+                unicast[prefix] = RibUnicastEntry(prefix, nhs, ents[bna], bna[1], isBgp and dry)
+                continue
+            r = self._addBestPaths(me, prefix, best, res.bestNodeArea, ents, nhs, isBgp)
             if r is not None:
                 db.addUnicastRoute(r)
 
@@ -1043,7 +1068,13 @@ class SpfSolver:
         cnt_l = cnt[len(uni):].tolist()
         first = len(uni) * deg
         edge_l = edge[first:first + len(cnt_l) * deg].tolist()
-        metric_l = metric[first:first + len(cnt_l) * deg].tolist()
+        metric_l = metric[first:first + len(cnt_l) * deg].astype(np.uint32).view(np.int32).tolist()
+        # next hops of a label route inline (getNextHopsThrift with a SWAP /
+        # PHP action, Decision.cpp:1198-1305): me's links' fields cached per
+        # directed edge, metrics as signed i32 (the thrift field) in one pass
+        info = self._link_fields(ls, me)
+        mk = tuple.__new__
+        mpls = db.mplsRoutes
         for k, (label, node) in enumerate(label_to_node.items()):
             if node == me:
                 db.addMplsRoute(RibMplsEntry(label, {NextHopThrift(
@@ -1053,8 +1084,21 @@ class SpfSolver:
             if not c:
                 self._bump("decision.no_route_to_label")
                 continue
-            db.addMplsRoute(RibMplsEntry(label, self._next_hops(
-                ls, me, area, zip(edge_l[b:b + c], metric_l[b:b + c]), False, {node}, label)))
+            if not fast:  # the generic getNextHopsThrift restatement (tests)
+                db.addMplsRoute(RibMplsEntry(label, self._next_hops(
+                    ls, me, area, zip(edge[first + b:first + b + c].tolist(),
+                                      metric[first + b:first + b + c].tolist()), False, {node}, label)))
+                continue
+            swap = mk(MplsAction, ("SWAP", label, None))
+            nhs = set()
+            add = nhs.add
+            for e, m in zip(edge_l[b:b + c], metric_l[b:b + c]):
+                li = info.get(e)
+                if li is None:
+                    li = self._link_field(ls, me, info, e)
+                nb = li[0]
+                add(mk(NextHopThrift, (li[3], li[1], m, _PHP if nb == node else swap, li[4], nb)))
+            mpls[label] = RibMplsEntry(label, nhs)
 
     def getNextHops(self, ls: LinkState, me: str, dsts: Sequence[str], isV4: bool = False,
                     swapLabel: Optional[int] = None) -> Tuple[Optional[int], Set[NextHopThrift]]:
