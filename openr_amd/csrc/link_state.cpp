@@ -226,6 +226,9 @@ struct ls_state {
   // getSpfResult cost by phase, ns (ls_debug_phase_ns): plan build, GPU
   // execute + copy back, pathLinks, host result assembly
   uint64_t phase_ns[4] = {0, 0, 0, 0};
+  // pathLinks scratch: one directed edge per predecessor at most, so a
+  // buffer of every edge takes them in one preds call (no sizing call)
+  std::vector<uint32_t> pred_scratch;
   std::map<std::tuple<uint32_t, uint32_t, uint64_t>, PathMemo> ksp_memo;
 
   uint32_t intern(const std::string& s) {
@@ -727,11 +730,11 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
       ls->phase_ns[1] += t1 - t0;
       m.pred_ptr.resize(N + 1);
       uint32_t npred = 0;
-      st = spf_mplan_preds(ls->all, s, m.pred_ptr.data(), nullptr, 0, &npred);
+      ls->pred_scratch.resize(std::max<size_t>(ls->edge_tail.size(), 1));
+      st = spf_mplan_preds(ls->all, s, m.pred_ptr.data(), ls->pred_scratch.data(),
+                           (uint32_t)ls->pred_scratch.size(), &npred);
       if (st != SPF_OK) return eng_fail(ls, st);
-      m.pred_edge.resize(npred);
-      st = spf_mplan_preds(ls->all, s, m.pred_ptr.data(), m.pred_edge.data(), npred, &npred);
-      if (st != SPF_OK) return eng_fail(ls, st);
+      m.pred_edge.assign(ls->pred_scratch.begin(), ls->pred_scratch.begin() + npred);
       t0 = now_ns();
       ls->phase_ns[2] += t0 - t1;
     } else if (needs_exact(ls, ulm)) {
@@ -753,11 +756,11 @@ spf_status spf_result(ls_state* ls, uint32_t node, bool ulm, const SpfMemo** out
       ls->phase_ns[1] += t0 - t1;
       m.pred_ptr.resize(N + 1);
       uint64_t npred = 0;
-      st = spf_plan_preds(plan.get(), m.pred_ptr.data(), nullptr, 0, &npred);
+      ls->pred_scratch.resize(std::max<size_t>(ls->edge_tail.size(), 1));
+      st = spf_plan_preds(plan.get(), m.pred_ptr.data(), ls->pred_scratch.data(),
+                          ls->pred_scratch.size(), &npred);
       if (st != SPF_OK) return eng_fail(ls, st);
-      m.pred_edge.resize(npred);
-      st = spf_plan_preds(plan.get(), m.pred_ptr.data(), m.pred_edge.data(), npred, &npred);
-      if (st != SPF_OK) return eng_fail(ls, st);
+      m.pred_edge.assign(ls->pred_scratch.begin(), ls->pred_scratch.begin() + npred);
       ls->phase_ns[2] += now_ns() - t0;
     }
     t0 = now_ns();
