@@ -1054,19 +1054,56 @@ class FacadeRouteBuild:
         self.survey_bytes = 0
         self.parallelism = "one LinkState per process (replicas)"
         self.pub, self.build, self.routes = [], [], 0
-
-    def step(self) -> None:
+        # Decision's one SpfSolver (C++, include/openr_decision.h): its route
+        # DB is built and left native, as a C++ Decision consumes it
         from openr_amd.spf_solver import SpfSolver
 
+        self.solver = SpfSolver(self.me, True, True)
+
+    def step(self) -> None:
         t0 = time.perf_counter()
         self.victim.isOverloaded = not self.victim.isOverloaded
         self.ls.updateAdjacencyDatabase(self.victim)
         t1 = time.perf_counter()
-        db = SpfSolver(self.me, True, True).buildRouteDb(self.me, {self.ls.getArea(): self.ls}, self.ps)
+        ndb = self.solver.buildRouteDbNative(self.me, {self.ls.getArea(): self.ls}, self.ps)
         t2 = time.perf_counter()
-        self.routes = len(db.unicastRoutes) + len(db.mplsRoutes)
+        self.routes = ndb.unicastCount() + ndb.mplsCount()
+        self.nexthops = len(ndb.nexthopRecords())
+        ndb.close()
         self.pub.append(t1 - t0)
         self.build.append(t2 - t1)
+
+    def verify(self):
+        """The native route DB of the current state against the Python
+        restatement of Decision.cpp's route computation (SpfSolver.native =
+        False), route by route: prefixes, next-hop sets, best entries."""
+        from openr_amd.spf_solver import SpfSolver
+
+        areas = {self.ls.getArea(): self.ls}
+        t0 = time.perf_counter()
+        ndb = self.solver.buildRouteDbNative(self.me, areas, self.ps)
+        nat = ndb.routeDb()
+        ndb.close()
+        t1 = time.perf_counter()
+        old = SpfSolver.native
+        SpfSolver.native = False
+        try:
+            py = SpfSolver(self.me, True, True).buildRouteDb(self.me, areas, self.ps)
+        finally:
+            SpfSolver.native = old
+        t2 = time.perf_counter()
+        bad = sum(1 for p, r in py.unicastRoutes.items()
+                  if p not in nat.unicastRoutes or set(nat.unicastRoutes[p].nexthops) != set(r.nexthops)
+                  or nat.unicastRoutes[p].bestPrefixEntry is not r.bestPrefixEntry)
+        bad += len(set(nat.unicastRoutes) ^ set(py.unicastRoutes))
+        bad += sum(1 for l, r in py.mplsRoutes.items()
+                   if l not in nat.mplsRoutes or set(nat.mplsRoutes[l].nexthops) != set(r.nexthops))
+        bad += len(set(nat.mplsRoutes) ^ set(py.mplsRoutes))
+        self.verify_ms = {"native build + materialise into Python objects": 1e3 * (t1 - t0),
+                          "python restatement build": 1e3 * (t2 - t1)}
+        return {"checked": "every route of the native DB vs the Python restatement "
+                           "(openr_amd/spf_solver.py, native=False)",
+                "routes": len(py.unicastRoutes) + len(py.mplsRoutes), "mismatches": bad}
 
     def enable_timing(self, k: int) -> None:
         self.pub, self.build = [], []
@@ -1075,9 +1112,11 @@ class FacadeRouteBuild:
     def kernel_ms(self):
         ph = [(b - a) / 1e6 / max(1, len(self.build)) for a, b in zip(self.ph0, self.ls.debugPhaseNs())]
         self.phase_ms = {"publication (updateAdjacencyDatabase + flatten patch)": 1e3 * float(np.mean(self.pub)),
-                         "buildRouteDb (selection kernel + host route assembly)": 1e3 * float(np.mean(self.build)),
+                         "buildRouteDb (C++ SpfSolver: selection kernel + route assembly)":
+                             1e3 * float(np.mean(self.build)),
                          "of which getSpfResult(me) facade phases (plan, execute+copy, pathLinks, "
-                         "host)": ph, "routes_per_build": self.routes}
+                         "host)": ph, "routes_per_build": self.routes,
+                         "nexthop_records_per_build": self.nexthops}
         return {"route_build": 1e3 * (float(np.mean(self.pub)) + float(np.mean(self.build)))}
 
     def edges_per_unit(self) -> int:
@@ -1381,6 +1420,8 @@ def main() -> None:
         out["config"]["next_hop_rows"] = wl.narrow  # u32 | u8 | sliced (bit planes)
     if isinstance(wl, (RoutesAllNodes, FacadeRouteBuild)):
         out["config"]["phase_ms_per_step"] = wl.phase_ms
+    if getattr(wl, "verify_ms", None):
+        out["config"]["verify_ms"] = wl.verify_ms
     if isinstance(wl, FacadeLfa):
         out["config"]["phase_ms_per_step"] = wl.phase_ms
         out["config"]["batched_prefetch"] = wl.prefetch

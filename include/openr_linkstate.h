@@ -178,6 +178,10 @@ uint64_t ls_spf_runs(const ls_state* ls);
  * node ids are ascending-name ranks; returns the engine context. */
 spf_ctx* ls_engine(ls_state* ls);
 spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges);
+/* Version of the flattened CSR structure (node ids, row_ptr, col, link ids):
+ * changes whenever ls_flatten rebuilds it, not when it patches metrics or
+ * overload bits in place.  Callers caching per-graph tables key them on it. */
+uint64_t ls_graph_epoch(const ls_state* ls);
 spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids /* [n_nodes] */);
 /* Copy of the flattened CSR (sizes from ls_flatten); any pointer may be NULL. */
 spf_status ls_graph_csr(ls_state* ls, uint32_t* row_ptr, uint32_t* col, int32_t* metric,
@@ -225,6 +229,18 @@ int ls_path_a_in_path_b(const uint32_t* a, uint32_t na, const uint32_t* b, uint3
  * node-label entry of a node present in two areas). */
 spf_status ls_string_map_order(const char* const* keys, uint32_t n, uint32_t* order,
                                uint32_t* n_out);
+
+/* Iteration order of a PrefixEntries map, std::unordered_map<NodeAndArea,
+ * PrefixEntry> (openr/common/Types.h:24, folly's std::hash<std::pair>), after
+ * the history PrefixState applied to it (PrefixState.cpp:47-60): op i emplaces
+ * (ops[i] = 1; an existing key is left where it is) or erases (ops[i] = 0)
+ * the key (nodes[i], areas[i]).  order[j] = the op index that inserted the
+ * j-th surviving key; *n_out = surviving keys.  runBestPathSelectionBgp
+ * (Decision.cpp:795-832) and addBestPaths' prepend-label walk (:1047-1053)
+ * visit the entries in this order. */
+spf_status ls_node_area_map_order(const char* const* nodes, const char* const* areas,
+                                  const uint8_t* ops, uint32_t n_ops, uint32_t* order,
+                                  uint32_t* n_out);
 
 /* HoldableValue<bool> / HoldableValue<LinkStateMetric> (LinkState.h:36-58,
  * LinkState.cpp:54-125). */

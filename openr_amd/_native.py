@@ -138,6 +138,38 @@ class LsPathsView(C.Structure):
     ]
 
 
+class DcMetricEntity(C.Structure):  # openr_decision.h dc_metric_entity
+    _fields_ = [("type", C.c_int64), ("priority", C.c_int64), ("op", C.c_uint32),
+                ("is_tie_breaker", C.c_uint32), ("n_metric", C.c_uint32),
+                ("metric", C.POINTER(C.c_int64))]
+
+
+class DcPrefixEntry(C.Structure):  # openr_decision.h dc_prefix_entry
+    _fields_ = [("prefix", C.c_char_p), ("is_v4", C.c_uint8), ("is_bgp", C.c_uint8),
+                ("forwarding_type", C.c_uint8), ("forwarding_algorithm", C.c_uint8),
+                ("has_prepend_label", C.c_uint8), ("has_min_nexthop", C.c_uint8),
+                ("has_mv", C.c_uint8), ("pad", C.c_uint8), ("prepend_label", C.c_int32),
+                ("min_nexthop", C.c_int64), ("path_preference", C.c_int32),
+                ("source_preference", C.c_int32), ("distance", C.c_int32),
+                ("mv_version", C.c_int32), ("n_mv", C.c_uint32),
+                ("mv", C.POINTER(DcMetricEntity))]
+
+
+class DcNexthop(C.Structure):  # openr_decision.h dc_nexthop
+    _fields_ = [("address", C.c_uint8 * 16), ("address_len", C.c_uint8),
+                ("mpls_action", C.c_uint8), ("n_push", C.c_uint8), ("pad", C.c_uint8),
+                ("metric", C.c_int32), ("swap_label", C.c_int32), ("push_off", C.c_uint32),
+                ("ifname", C.c_uint32), ("area", C.c_uint32), ("neighbor", C.c_uint32)]
+
+
+# numpy view of dc_nexthop records (the route db's table, read in one copy)
+DC_NEXTHOP_DTYPE = np.dtype([("address", "u1", (16,)), ("address_len", "u1"),
+                             ("mpls_action", "u1"), ("n_push", "u1"), ("pad", "u1"),
+                             ("metric", "<i4"), ("swap_label", "<i4"), ("push_off", "<u4"),
+                             ("ifname", "<u4"), ("area", "<u4"), ("neighbor", "<u4")])
+DC_NONE = 0xFFFFFFFF
+DC_MPLS_ACTIONS = (None, "PUSH", "SWAP", "PHP", "POP_AND_LOOKUP")
+
 _u32p = C.POINTER(C.c_uint32)
 _u64p = C.POINTER(C.c_uint64)
 _i32p = C.POINTER(C.c_int32)
@@ -305,6 +337,41 @@ PROTOTYPES = {
                                        C.POINTER(C.c_int)]),
     "ls_path_a_in_path_b": (C.c_int, [_u32p, C.c_uint32, _u32p, C.c_uint32]),
     "ls_string_map_order": (C.c_int, [C.POINTER(C.c_char_p), C.c_uint32, _u32p, _u32p]),
+    "ls_node_area_map_order": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                         C.POINTER(C.c_uint8), C.c_uint32, _u32p, _u32p]),
+    "ls_graph_epoch": (C.c_uint64, [_vp]),
+    # SpfSolver / PrefixState (include/openr_decision.h)
+    "dc_prefix_state_create": (_vp, []),
+    "dc_prefix_state_destroy": (None, [_vp]),
+    "dc_prefix_update": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.POINTER(DcPrefixEntry)]),
+    "dc_prefix_delete": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_char_p]),
+    "dc_prefix_entries": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                    C.c_uint32, _u32p]),
+    "dc_solver_create": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.POINTER(C.c_void_p)]),
+    "dc_solver_destroy": (None, [_vp]),
+    "dc_last_error": (C.c_char_p, [_vp]),
+    "dc_static_mpls_route_set": (C.c_int, [_vp, C.c_int32, C.POINTER(DcNexthop), C.c_uint32,
+                                           C.POINTER(C.c_char_p), C.POINTER(C.c_int32)]),
+    "dc_static_mpls_route_delete": (C.c_int, [_vp, C.c_int32]),
+    "dc_build_route_db": (C.c_int, [_vp, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), C.c_uint32,
+                                    _vp, C.POINTER(C.c_void_p)]),
+    "dc_counter": (C.c_uint64, [_vp, C.c_char_p]),
+    "dc_best_route": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_uint32, _u32p]),
+    "dc_route_db_destroy": (None, [_vp]),
+    "dc_route_db_strings": (C.c_uint32, [_vp]),
+    "dc_route_db_string": (C.c_char_p, [_vp, C.c_uint32]),
+    "dc_route_db_nexthops": (C.c_void_p, [_vp, _u32p]),
+    "dc_route_db_labels": (C.c_void_p, [_vp, _u32p]),
+    "dc_route_db_unicast_count": (C.c_uint32, [_vp]),
+    "dc_route_db_unicast": (C.c_int, [_vp, C.c_uint32, _u32p, _u32p, _u32p, C.POINTER(C.c_int),
+                                      _u32p, _u32p]),
+    "dc_route_db_mpls_count": (C.c_uint32, [_vp]),
+    "dc_route_db_mpls": (C.c_int, [_vp, C.c_uint32, _i32p, _u32p, _u32p]),
+    "dc_route_db_unicast_table": (C.c_void_p, [_vp, _u32p]),
+    "dc_route_db_mpls_table": (C.c_void_p, [_vp, _u32p]),
     "ls_holdable_create": (_vp, [C.c_int, C.c_uint64]),
     "ls_holdable_destroy": (None, [_vp]),
     "ls_holdable_value": (C.c_uint64, [_vp]),

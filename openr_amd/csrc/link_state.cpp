@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <array>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -213,6 +214,7 @@ struct ls_state {
 
   // flattened graph
   bool dirty = true;                 // links changed: re-flatten (patch or reload)
+  uint64_t flat_epoch = 0;           // bumped whenever the flattened CSR structure is rebuilt
   bool engine_loaded = false;        // the engine holds the flattened graph below
   std::vector<uint32_t> pending_ovl;  // name ids whose overload bit flipped since the last flatten
   std::vector<uint32_t> csr_name;   // csr id -> name id
@@ -557,6 +559,10 @@ spf_status flatten(ls_state* ls) {
     return SPF_OK;
   }
   ls->engine_loaded = false;
+  // names, row_ptr, col or link ids changed: a process-wide counter, so no
+  // two flattened graphs of any two states share an epoch
+  static std::atomic<uint64_t> next_epoch{0};
+  ls->flat_epoch = ++next_epoch;
   if (N > 0 && ls->eng) {
     spf_graph g;
     g.n_nodes = N;
@@ -1318,6 +1324,8 @@ uint64_t ls_spf_runs(const ls_state* ls) { return ls ? ls->spf_runs : 0; }
 
 spf_ctx* ls_engine(ls_state* ls) { return ls ? ls->eng : nullptr; }
 
+uint64_t ls_graph_epoch(const ls_state* ls) { return ls ? ls->flat_epoch : 0; }
+
 spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges) {
   if (!ls) return SPF_E_INVALID;
   const spf_status st = flatten(ls);
@@ -1461,6 +1469,35 @@ spf_status ls_string_map_order(const char* const* keys, uint32_t n, uint32_t* or
   for (uint32_t i = 0; i < n; ++i) {
     if (!keys[i]) return SPF_E_INVALID;
     m.emplace(keys[i], i);
+  }
+  uint32_t k = 0;
+  for (const auto& kv : m) order[k++] = kv.second;
+  *n_out = k;
+  return SPF_OK;
+}
+
+// PrefixEntries = std::unordered_map<NodeAndArea, PrefixEntry> (Types.h:24):
+// the same container, hashed by folly's std::hash<std::pair> (hash_128_to_64
+// of the two std::hash<std::string>), replayed through the emplace / erase
+// history PrefixState::updatePrefixDatabase applied (PrefixState.cpp:47-60).
+namespace {
+struct NodeAreaHash {
+  size_t operator()(const std::pair<std::string, std::string>& k) const {
+    return folly_mix(std::hash<std::string>()(k.first), std::hash<std::string>()(k.second));
+  }
+};
+}  // namespace
+
+spf_status ls_node_area_map_order(const char* const* nodes, const char* const* areas,
+                                  const uint8_t* ops, uint32_t n_ops, uint32_t* order,
+                                  uint32_t* n_out) {
+  if ((n_ops && (!nodes || !areas || !ops || !order)) || !n_out) return SPF_E_INVALID;
+  std::unordered_map<std::pair<std::string, std::string>, uint32_t, NodeAreaHash> m;
+  for (uint32_t i = 0; i < n_ops; ++i) {
+    if (!nodes[i] || !areas[i] || ops[i] > 1) return SPF_E_INVALID;
+    std::pair<std::string, std::string> key(nodes[i], areas[i]);
+    if (ops[i]) m.emplace(std::move(key), i);
+    else m.erase(key);
   }
   uint32_t k = 0;
   for (const auto& kv : m) order[k++] = kv.second;

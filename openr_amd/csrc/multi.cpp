@@ -556,8 +556,27 @@ namespace {
 // address, plus the sets, on that member's device.  Rows of another device
 // are read through peer access (xGMI): enabled here once, required for LFA
 // (neighbours' rows) when the members span devices.
+// Streams a route call has queued work on (copies into the caller's or the
+// call's own host memory, timing events): on any early return they are
+// drained and the events destroyed before that memory goes away.
+struct IssuedGuard {
+  spf_mctx* m;
+  std::vector<uint32_t> members;
+  std::vector<hipEvent_t>* ev = nullptr;
+  ~IssuedGuard() {
+    for (uint32_t r : members) {
+      (void)hipSetDevice(m->members[r]->device);
+      (void)hipStreamSynchronize(m->exec[r]);
+    }
+    if (ev)
+      for (hipEvent_t e : *ev)
+        if (e) (void)hipEventDestroy(e);
+  }
+};
+
 spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t* set_nodes,
-                         uint32_t n_sets, bool lfa, const uint64_t* link_hash, uint32_t n_links) {
+                         uint32_t n_sets, bool lfa, const uint64_t* link_hash, uint32_t n_links,
+                         const uint32_t* me_req, uint32_t n_me) {
   spf_mctx* m = mp->m;
   spf_ctx* c0 = m->members[0];
   const uint32_t N = c0->N;
@@ -606,6 +625,18 @@ spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t*
       nhp[v] = (unsigned long long)(uintptr_t)(p.nh.p + p.nh_off[row]);
     }
     dev_of[v] = m->members[r]->device;
+  }
+  if (lfa) {
+    // LFA reads every neighbour's row: a partial plan without one of them
+    // would silently drop that neighbour's LFA candidates
+    for (uint32_t t = 0; t < n_me; ++t) {
+      const uint32_t v = mp->srcs[me_req[t]];
+      for (uint32_t e = c0->nb_ptr[v]; e < c0->nb_ptr[v + 1]; ++e)
+        if (!rowp[c0->nb_id[e]])
+          return mfail(m, SPF_E_UNSUPPORTED,
+                       "LFA route selection for node %u needs its neighbour %u resident in the plan",
+                       v, c0->nb_id[e]);
+    }
   }
   if (lfa && !mp->peer) {
     // members on distinct devices without peer access: every neighbour of a
@@ -669,7 +700,8 @@ spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32
   for (uint32_t e = 0; e < c0->E; ++e)
     if (c0->link[e] >= n_links) return mfail(m, SPF_E_INVALID, "link_hash shorter than the link ids");
   const bool lfa = (flags & SPF_ROUTE_LFA) != 0;
-  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, link_hash, n_links);
+  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, link_hash, n_links,
+                                         me_req, n_me);
       st != SPF_OK)
     return st;
   std::vector<std::vector<uint32_t>> mine(mp->n_parts), slot(mp->n_parts);
@@ -680,11 +712,13 @@ spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32
   }
   std::vector<hipEvent_t> ev(2 * mp->n_parts, nullptr);
   std::vector<std::vector<uint64_t>> got(mp->n_parts);
+  IssuedGuard guard{m, {}, &ev};  // declared after got: drains before got is freed
   for (uint32_t r = 0; r < mp->n_parts; ++r) {
     spf_mplan::Part& p = mp->parts[r];
     if (mine[r].empty()) continue;
     spf_ctx* c = m->members[r];
     M_HIP(m, hipSetDevice(c->device));
+    guard.members.push_back(r);
     const hipStream_t s = m->exec[r];
     const uint32_t n = (uint32_t)mine[r].size();
     M_HIP(m, p.rme.upload(mine[r].data(), n, s));
@@ -711,8 +745,6 @@ spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32
       float t = 0;
       M_HIP(m, hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]));
       worst = std::max(worst, (double)t);
-      (void)hipEventDestroy(ev[2 * r]);
-      (void)hipEventDestroy(ev[2 * r + 1]);
     }
     for (size_t q = 0; q < got[r].size(); ++q) digests[slot[r][q]] = got[r][q];
   }
@@ -729,7 +761,8 @@ spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_
   spf_mctx* m = mp->m;
   if (me_req >= mp->n_src) return mfail(m, SPF_E_INVALID, "me %u is not a request index", me_req);
   const bool lfa = (flags & SPF_ROUTE_LFA) != 0;
-  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, nullptr, 0); st != SPF_OK)
+  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, nullptr, 0, &me_req, 1);
+      st != SPF_OK)
     return st;
   const uint32_t r = mp->owner[me_req];
   spf_mplan::Part& p = mp->parts[r];
@@ -739,6 +772,7 @@ spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_
   const size_t cap = (size_t)n_sets * std::max<uint32_t>(1, deg);
   M_HIP(m, hipSetDevice(c->device));
   const hipStream_t s = m->exec[r];
+  IssuedGuard guard{m, {r}};  // &me and the caller's outputs outlive every queued copy
   M_HIP(m, p.rme.upload(&me, 1, s));
   M_HIP(m, p.rmin.alloc(std::max<uint32_t>(1, n_sets)));
   M_HIP(m, p.rcnt.alloc(std::max<uint32_t>(1, n_sets)));

@@ -37,6 +37,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 
 using namespace spfi;
@@ -1042,26 +1043,48 @@ __device__ __forceinline__ uint32_t team_chunk(uint32_t count) {
   return min(64u, max(1u, (count + kW - 1) / kW));
 }
 
-// CHK (the profiled wave instance, SPF_WHATIF_PROF): every scratch-derived
+// Phase counters of a profiled repair (SPF_WHATIF_PROF).  Registers (GPH
+// false): ph is the caller's array, stored once when the team exits.  Global
+// (GPH true, SPF_WHATIF_PROF=global): ph is the team's 16-slot row of the
+// prof buffer, updated by the team's first thread with device atomics at
+// every event -- the round-5 variant that faulted; its row was
+// range-checked by the kernel before it got here.
+template <bool GPH>
+__device__ __forceinline__ void ph_add(uint64_t* ph, int k, uint64_t v, bool leader) {
+  if constexpr (GPH) {
+    if (leader) atomicAdd(reinterpret_cast<unsigned long long*>(ph + k), (unsigned long long)v);
+  } else {
+    ph[k] += v;
+  }
+}
+template <bool GPH>
+__device__ __forceinline__ void ph_max(uint64_t* ph, int k, uint64_t v, bool leader) {
+  if constexpr (GPH) {
+    if (leader) atomicMax(reinterpret_cast<unsigned long long*>(ph + k), (unsigned long long)v);
+  } else {
+    ph[k] = ph[k] > v ? ph[k] : v;
+  }
+}
+
+// CHK (the profiled instances, SPF_WHATIF_PROF): every scratch-derived
 // index is range-checked before use; an out-of-range one sets bit 4 of the
 // fault word with the site in bits 16-23 and is replaced by a safe value
 // (results then invalid, reported by spf_device_check).
-template <int TEAM, bool GROUP = false, bool CHK = false>
+template <int TEAM, bool GROUP = false, bool CHK = false, bool GPH = false>
 __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
                        uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, uint32_t cap,
                        TeamCtl* ctl, uint32_t tt, uint32_t e_fail, spf_whatif_digest* out,
                        uint64_t* ph = nullptr) {
-  // diagnostics (SPF_WHATIF_PROF): ph is the caller's register array of 12
-  // counters, accumulated over the team's failures and stored once when the
-  // team exits (no memory traffic inside a repair) -- [0] repairs, [1..5]
-  // 100 MHz ticks in D discovery, seeds, Dial, fallback sweeps, digest;
-  // [8] sum |D|, [9] sum Dial levels, [10] max |D|, [11] repairs given up
+  // diagnostics (SPF_WHATIF_PROF): 12 counters, accumulated over the team's
+  // failures (ph_add) -- [0] repairs, [1..5] 100 MHz ticks in D discovery,
+  // seeds, Dial, fallback sweeps, digest; [8] sum |D|, [9] sum Dial levels,
+  // [10] max |D|, [11] repairs given up
   uint64_t tprev = ph ? wall_clock64() : 0ull;
 #define WI_STAMP(k)                              \
   do {                                           \
     if (ph) {                                    \
       const uint64_t now_ = wall_clock64();      \
-      ph[k] += now_ - tprev;                     \
+      ph_add<GPH>(ph, k, now_ - tprev, tt == 0); \
       tprev = now_;                              \
     }                                            \
   } while (0)
@@ -1155,10 +1178,10 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   const bool ovf = ldw<GROUP>(&ctl->ovf) != 0 || bound_hit;
   WI_STAMP(1);
   if (ph) {
-    ph[0] += 1;
-    ph[8] += n;
-    ph[10] = ph[10] > n ? ph[10] : (uint64_t)n;
-    ph[11] += ovf;
+    ph_add<GPH>(ph, 0, 1, tt == 0);
+    ph_add<GPH>(ph, 8, n, tt == 0);
+    ph_max<GPH>(ph, 10, n, tt == 0);
+    ph_add<GPH>(ph, 11, ovf, tt == 0);
   }
   team_sync<TEAM, GROUP>(ctl, g.fault);
   if (ovf) {
@@ -1319,7 +1342,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     if (m != kInf) atomicMin(next, m);
     team_sync<TEAM, GROUP>(ctl, g.fault);
     t = ldw<GROUP>(next);
-    if (ph) ph[9] += 1;
+    if (ph) ph_add<GPH>(ph, 9, 1, tt == 0);
   }
   WI_STAMP(3);
   if (!settled) {
@@ -1467,19 +1490,19 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
 // (ballot + mbcnt compaction instead of counter atomics); the level list of
 // a D of <= 64 nodes never leaves the registers (ds_permute).  |D| <= cap <=
 // kDialLevels distinct values, so Dial always settles (no fallback sweeps).
-template <bool CHK>
+template <bool CHK, bool GPH = false>
 __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
                             uint32_t* dnew, uint32_t* nhn, uint32_t* ord, uint32_t cap,
                             TeamCtl* ctl, uint32_t lane, uint32_t e_fail, spf_whatif_digest* out,
                             uint64_t* ph) {
   uint64_t tprev = ph ? wall_clock64() : 0ull;
-#define WI_STAMP(k)                              \
-  do {                                           \
-    if (ph) {                                    \
-      const uint64_t now_ = wall_clock64();      \
-      ph[k] += now_ - tprev;                     \
-      tprev = now_;                              \
-    }                                            \
+#define WI_STAMP(k)                                \
+  do {                                             \
+    if (ph) {                                      \
+      const uint64_t now_ = wall_clock64();        \
+      ph_add<GPH>(ph, k, now_ - tprev, lane == 0); \
+      tprev = now_;                                \
+    }                                              \
   } while (0)
   auto chk = [&](uint32_t x, uint32_t lim, bool inf_ok, uint32_t site, uint32_t safe) -> uint32_t {
     if constexpr (CHK) {
@@ -1546,10 +1569,10 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
   n = min(n, cap);
   WI_STAMP(1);
   if (ph) {
-    ph[0] += 1;
-    ph[8] += n;
-    ph[10] = ph[10] > n ? ph[10] : (uint64_t)n;
-    ph[11] += ovf;
+    ph_add<GPH>(ph, 0, 1, lane == 0);
+    ph_add<GPH>(ph, 8, n, lane == 0);
+    ph_max<GPH>(ph, 10, n, lane == 0);
+    ph_add<GPH>(ph, 11, ovf, lane == 0);
   }
   if (ovf) {
     for (uint32_t i = lane; i < n; i += 64) stw<false>(&mark[ldw<false>(&dlist[i])], kInf);
@@ -1660,7 +1683,7 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
     }
     sync();
     t = wave_min32(m);
-    if (ph) ph[9] += 1;
+    if (ph) ph_add<GPH>(ph, 9, 1, lane == 0);
   }
   WI_STAMP(3);
   // ---- digest delta over D, scratch reset ----
@@ -1691,17 +1714,31 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
   return true;
 }
 
+// The profiled instances' phase-counter row of `team` (16 slots) in a
+// region of `rows` rows: a team past the region sets bit 5 of the fault word
+// (kernel in bits 24-31) and counts nothing -- the layout of the prof buffer
+// ([block / group teams][base][wave teams] x 16, spf_whatif_plan_create) is
+// checked, not assumed.
+__device__ __forceinline__ uint64_t* prof_row(unsigned long long* prof, size_t team, uint32_t rows,
+                                              uint32_t kernel, uint32_t* fault) {
+  if (team < rows) return reinterpret_cast<uint64_t*>(prof + 16 * team);
+  if (fault) __hip_atomic_fetch_or(fault, 32u | (kernel << 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return nullptr;
+}
+
 // wave teams over the hot list; failures whose D overflows kWaveCap are
-// queued for the workgroup teams.  PROF (SPF_WHATIF_PROF): a separate
-// instance with the per-team phase counters (prof + team * 16), so the
-// production instance's registers -- which set its co-residency with the
-// group teams, spf_whatif_plan_create -- do not change with diagnostics.
-template <bool PROF>
+// queued for the workgroup teams.  PROF (SPF_WHATIF_PROF): separate
+// instances with the per-team phase counters (prof row `team`, prof_rows
+// rows) -- 1: in registers, stored at team exit; 2: global read-modify-writes
+// per event -- so the production instance's registers, which set its
+// co-residency with the group teams (spf_whatif_plan_create), do not change
+// with diagnostics.
+template <int PROF>
 __global__ __launch_bounds__(256) void repair_wave_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ hot, const uint32_t* __restrict__ n_hot,
     uint32_t* cursor, uint2* big, uint32_t* n_big, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
     uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out, uint32_t cap,
-    unsigned long long* prof) {
+    unsigned long long* prof, uint32_t prof_rows) {
   __shared__ TeamCtl ctl[4];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t team = (size_t)blockIdx.x * 4 + w;
@@ -1713,26 +1750,28 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
   ord += team * 2 * cap;  // level list + its hubs
   const uint32_t total = *n_hot;
   uint64_t ph[12] = {};
+  uint64_t* gph = PROF == 2 ? prof_row(prof, team, prof_rows, 1, lane == 0 ? g.fault : nullptr) : nullptr;
   for (;;) {
     uint32_t k = 0;
     if (lane == 0) k = atomicAdd(cursor, 1u);
     k = __builtin_amdgcn_readlane(k, 0);
     if (k >= total) break;
     const uint2 h = hot[k];
-    if (!repair_wave<PROF>(g, B, mark, dlist, dnew, nhn, ord, cap, &ctl[w], lane, h.y, out + h.x,
-                           PROF ? ph : nullptr)) {
+    if (!repair_wave<PROF != 0, PROF == 2>(g, B, mark, dlist, dnew, nhn, ord, cap, &ctl[w], lane, h.y,
+                                          out + h.x, PROF == 1 ? ph : gph)) {
       if (lane == 0) big[atomicAdd(n_big, 1u)] = h;
     }
   }
-  if (PROF && lane == 0)
-    for (int q = 0; q < 12; ++q) prof[team * 16 + q] = ph[q];
+  if (PROF == 1 && lane == 0)
+    if (uint64_t* r = prof_row(prof, team, prof_rows, 1, g.fault))
+      for (int q = 0; q < 12; ++q) r[q] = ph[q];
 }
 
-template <bool PROF>
+template <int PROF>
 __global__ __launch_bounds__(1024) void repair_block_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
     uint32_t* mark, uint32_t* dlist, uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord,
-    spf_whatif_digest* out, unsigned long long* prof) {
+    spf_whatif_digest* out, unsigned long long* prof, uint32_t prof_rows) {
   __shared__ TeamCtl ctl;
   // the largest repairs are the critical path of a batch and share their CU
   // with wave teams running concurrently: win the issue arbitration
@@ -1746,13 +1785,16 @@ __global__ __launch_bounds__(1024) void repair_block_kernel(
   ord += team * 2 * (size_t)g.N;  // level list + its hubs
   const uint32_t total = *n_big;
   uint64_t ph[12] = {};
+  uint64_t* gph =
+      PROF == 2 ? prof_row(prof, team, prof_rows, 2, threadIdx.x == 0 ? g.fault : nullptr) : nullptr;
   for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
     const uint2 h = big[k];
-    repair<1024>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, &ctl, threadIdx.x, h.y, out + h.x,
-                 PROF ? ph : nullptr);
+    repair<1024, false, false, PROF == 2>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, &ctl,
+                                          threadIdx.x, h.y, out + h.x, PROF == 1 ? ph : gph);
   }
-  if (PROF && threadIdx.x == 0)
-    for (int q = 0; q < 12; ++q) prof[team * 16 + q] = ph[q];
+  if (PROF == 1 && threadIdx.x == 0)
+    if (uint64_t* r = prof_row(prof, team, prof_rows, 2, g.fault))
+      for (int q = 0; q < 12; ++q) r[q] = ph[q];
 }
 
 // The classified big failures, largest subtree first (the order the group
@@ -1786,12 +1828,12 @@ __global__ __launch_bounds__(1024) void sort_big_kernel(const uint2* __restrict_
 // both progress from the start.  Members of a team sit on one XCD (blocks x
 // and x + 8 share one); teams pull failures, largest first.
 constexpr int kGroupWg = 512;
-template <int G, bool PROF>
+template <int G, int PROF>
 __global__ __launch_bounds__(kGroupWg) void repair_group_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ big, const uint32_t* __restrict__ n_big,
     uint32_t* cursor, TeamCtl* ctls, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
     uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out,
-    unsigned long long* prof) {
+    unsigned long long* prof, uint32_t prof_rows) {
   constexpr int TEAM = kGroupWg * G;
   __builtin_amdgcn_s_setprio(3);
   const uint32_t idx = blockIdx.x >> 3;
@@ -1807,17 +1849,19 @@ __global__ __launch_bounds__(kGroupWg) void repair_group_kernel(
   ord += team * 2 * (size_t)g.N;
   const uint32_t total = *n_big;
   uint64_t ph[12] = {};
+  uint64_t* gph = PROF == 2 ? prof_row(prof, team, prof_rows, 3, tt == 0 ? g.fault : nullptr) : nullptr;
   for (;;) {
     if (tt == 0) stw<true>(&ctl->next, atomicAdd(cursor, 1u));
     team_sync<TEAM, true>(ctl, g.fault);
     const uint32_t k = ldw<true>(&ctl->next);
     if (k >= total) break;  // team-uniform
     const uint2 h = big[k];
-    repair<TEAM, true>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, ctl, tt, h.y, out + h.x,
-                       PROF ? ph : nullptr);
+    repair<TEAM, true, false, PROF == 2>(g, B, mark, dlist, dnew, nhn, lvl, ord, g.N, ctl, tt, h.y,
+                                         out + h.x, PROF == 1 ? ph : gph);
   }
-  if (PROF && tt == 0)
-    for (int q = 0; q < 12; ++q) prof[team * 16 + q] = ph[q];
+  if (PROF == 1 && tt == 0)
+    if (uint64_t* r = prof_row(prof, team, prof_rows, 3, g.fault))
+      for (int q = 0; q < 12; ++q) r[q] = ph[q];
 }
 
 struct GroupArgs {
@@ -1830,6 +1874,7 @@ struct GroupArgs {
   uint32_t *mark, *dlist, *dnew, *nhn, *lvl, *ord;
   spf_whatif_digest* out;
   unsigned long long* prof;
+  uint32_t prof_rows;  // rows of the prof region the group teams own
 };
 
 // A launch whose blocks meet at barriers (XGrid, the group teams'
@@ -1849,34 +1894,37 @@ hipError_t launch_resident(const void* kernel, uint32_t blocks, uint32_t threads
   return hipLaunchKernel(kernel, dim3(blocks), dim3(threads), args, 0, s);
 }
 
-template <int G>
-hipError_t launch_group_g(GroupArgs& a, uint32_t n_cu, hipStream_t s) {
-  void* args[] = {&a.g, &a.B, &a.big, &a.n_big, &a.cursor, &a.ctls, &a.mark, &a.dlist, &a.dnew,
-                  &a.nhn, &a.lvl, &a.ord, &a.out, &a.prof};
-  const void* k = a.prof ? (const void*)repair_group_kernel<G, true> : (const void*)repair_group_kernel<G, false>;
-  return launch_resident(k, n_cu, kGroupWg, args, n_cu, s);
+// SPF_WHATIF_PROF: unset 0 (production instances), "global" 2 (per-event
+// global read-modify-writes), anything else 1 (register counters)
+int whatif_prof_mode() {
+  const char* e = std::getenv("SPF_WHATIF_PROF");
+  return !e ? 0 : (std::strcmp(e, "global") == 0 ? 2 : 1);
 }
 
-const void* group_kernel(uint32_t G, bool prof) {
+template <int G>
+const void* group_kernel_g(int prof) {
+  return prof == 2 ? (const void*)repair_group_kernel<G, 2>
+                   : prof == 1 ? (const void*)repair_group_kernel<G, 1> : (const void*)repair_group_kernel<G, 0>;
+}
+
+const void* group_kernel(uint32_t G, int prof) {
   switch (G) {
-    case 2: return prof ? (const void*)repair_group_kernel<2, true> : (const void*)repair_group_kernel<2, false>;
-    case 4: return prof ? (const void*)repair_group_kernel<4, true> : (const void*)repair_group_kernel<4, false>;
-    case 8: return prof ? (const void*)repair_group_kernel<8, true> : (const void*)repair_group_kernel<8, false>;
-    case 16: return prof ? (const void*)repair_group_kernel<16, true> : (const void*)repair_group_kernel<16, false>;
+    case 2: return group_kernel_g<2>(prof);
+    case 4: return group_kernel_g<4>(prof);
+    case 8: return group_kernel_g<8>(prof);
+    case 16: return group_kernel_g<16>(prof);
     default: return nullptr;
   }
 }
 
 // one launch, a workgroup per CU (every member of every team resident at
 // once: the team barrier's precondition)
-hipError_t launch_group(uint32_t G, GroupArgs& a, uint32_t n_cu, hipStream_t s) {
-  switch (G) {
-    case 2: return launch_group_g<2>(a, n_cu, s);
-    case 4: return launch_group_g<4>(a, n_cu, s);
-    case 8: return launch_group_g<8>(a, n_cu, s);
-    case 16: return launch_group_g<16>(a, n_cu, s);
-    default: return hipErrorInvalidValue;
-  }
+hipError_t launch_group(uint32_t G, GroupArgs& a, uint32_t n_cu, int prof, hipStream_t s) {
+  const void* k = group_kernel(G, a.prof ? prof : 0);
+  if (!k) return hipErrorInvalidValue;
+  void* args[] = {&a.g, &a.B, &a.big, &a.n_big, &a.cursor, &a.ctls, &a.mark, &a.dlist, &a.dnew,
+                  &a.nhn, &a.lvl, &a.ord, &a.out, &a.prof, &a.prof_rows};
+  return launch_resident(k, n_cu, kGroupWg, args, n_cu, s);
 }
 
 __global__ void base_digest_kernel(spf_whatif_digest* o, const unsigned long long* H) {
@@ -1899,6 +1947,7 @@ struct spf_whatif_plan {
   DevBuf<uint32_t> d_cnt;
   DevBuf<unsigned char> d_ctl;  // group teams' TeamCtl
   uint32_t group = 0, group_teams = 0;  // workgroups per group team (0: one-workgroup teams)
+  int prof_mode = 0;                    // whatif_prof_mode() at plan creation
   DevBuf<uint32_t> d_parent, d_sub;
   uint32_t big_teams = 0;
   // |D| a wave team holds (its scratch) and the parent-subtree size past
@@ -2110,10 +2159,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
     // CU until both fit.  (Round 4's stamp pointer in the wave kernel --
     // 75 -> 80+ VGPRs at 4 waves per SIMD beside 2 x 88 -- broke this sum.)
     hipFuncAttributes fw{}, fg{};
-    const void* wk = std::getenv("SPF_WHATIF_PROF") ? (const void*)repair_wave_kernel<true>
-                                                    : (const void*)repair_wave_kernel<false>;
+    const int pm = whatif_prof_mode();
+    const void* wk = pm == 2 ? (const void*)repair_wave_kernel<2>
+                             : pm == 1 ? (const void*)repair_wave_kernel<1> : (const void*)repair_wave_kernel<0>;
     HIP_TRY(c, hipFuncGetAttributes(&fw, wk));
-    HIP_TRY(c, hipFuncGetAttributes(&fg, group_kernel(p->group, std::getenv("SPF_WHATIF_PROF") != nullptr)));
+    HIP_TRY(c, hipFuncGetAttributes(&fg, group_kernel(p->group, pm)));
     const auto gran = [](int r) { return (uint32_t)((std::max(r, 1) + 7) & ~7); };
     const uint32_t per_simd_group = kGroupWg / 64 / 4;
     const uint32_t vw = gran(fw.numRegs), vg = gran(fg.numRegs);
@@ -2147,7 +2197,8 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   // marks start (and are always left) at kInf
   HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
-  if (std::getenv("SPF_WHATIF_PROF")) {  // [bt teams][base][wave teams] x 16
+  p->prof_mode = whatif_prof_mode();
+  if (p->prof_mode) {  // [bt teams][base][wave teams] x 16 (row bounds checked in the kernels)
     const size_t slots = 16 * (bt + 1 + p->wave_teams) + 128;  // + the base's per-level clocks
     HIP_TRY(c, p->d_prof.alloc(slots));
     HIP_TRY(c, hipMemsetAsync(p->d_prof.p, 0, slots * 8, c->stream));
@@ -2238,39 +2289,52 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
       HIP_TRY(c, hipGetLastError());
       GroupArgs ga{g, B, p->d_big1.p, p->d_cnt.p + 3, p->d_cnt.p + 4,
                    reinterpret_cast<TeamCtl*>(p->d_ctl.p), p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
-                   p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p};
+                   p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p, p->big_teams};
       if (const spf_status st = resident_order(c, side); st != SPF_OK) return st;
-      grouped = launch_group(p->group, ga, c->n_cu, side) == hipSuccess;
+      grouped = launch_group(p->group, ga, c->n_cu, p->prof_mode, side) == hipSuccess;
       if (!grouped) (void)hipGetLastError();  // fall back to one-workgroup teams
       else if (const spf_status st = resident_done(c, side); st != SPF_OK) return st;
     }
     if (!grouped) {
-      if (p->d_prof.p)
-        hipLaunchKernelGGL(repair_block_kernel<true>, dim3(p->big_teams), dim3(1024), 0, side, g, B,
-                           p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
-                           p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p);
+      const uint32_t bt = p->big_teams;
+      if (p->prof_mode == 2)
+        hipLaunchKernelGGL(repair_block_kernel<2>, dim3(bt), dim3(1024), 0, side, g, B, p->d_big0.p,
+                           p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p, p->c_nhn.p,
+                           p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p, bt);
+      else if (p->prof_mode == 1)
+        hipLaunchKernelGGL(repair_block_kernel<1>, dim3(bt), dim3(1024), 0, side, g, B, p->d_big0.p,
+                           p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p, p->c_nhn.p,
+                           p->c_lvl.p, p->c_ord.p, d_out, p->d_prof.p, bt);
       else
-        hipLaunchKernelGGL(repair_block_kernel<false>, dim3(p->big_teams), dim3(1024), 0, side, g, B,
-                           p->d_big0.p, p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p,
-                           p->c_nhn.p, p->c_lvl.p, p->c_ord.p, d_out, nullptr);
+        hipLaunchKernelGGL(repair_block_kernel<0>, dim3(bt), dim3(1024), 0, side, g, B, p->d_big0.p,
+                           p->d_cnt.p + 3, p->c_mark.p, p->c_dlist.p, p->c_dnew.p, p->c_nhn.p,
+                           p->c_lvl.p, p->c_ord.p, d_out, nullptr, 0u);
     }
     HIP_TRY(c, hipGetLastError());
     if (c->side) HIP_TRY(c, hipEventRecord(c->side_join, c->side));
-    if (p->d_prof.p)
-      hipLaunchKernelGGL(repair_wave_kernel<true>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
-                         p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                         p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
-                         p->w_ord.p, d_out, p->wave_cap,
-                         p->d_prof.p + 16ull * (p->big_teams + 1));
-    else
-      hipLaunchKernelGGL(repair_wave_kernel<false>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
-                         p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                         p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
-                         p->w_ord.p, d_out, p->wave_cap, nullptr);
+    {
+      unsigned long long* wp = p->d_prof.p ? p->d_prof.p + 16ull * (p->big_teams + 1) : nullptr;
+      const uint32_t wr = p->wave_teams;
+      if (p->prof_mode == 2)
+        hipLaunchKernelGGL(repair_wave_kernel<2>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
+                           p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
+                           p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                           p->w_ord.p, d_out, p->wave_cap, wp, wr);
+      else if (p->prof_mode == 1)
+        hipLaunchKernelGGL(repair_wave_kernel<1>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
+                           p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
+                           p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                           p->w_ord.p, d_out, p->wave_cap, wp, wr);
+      else
+        hipLaunchKernelGGL(repair_wave_kernel<0>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
+                           p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
+                           p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                           p->w_ord.p, d_out, p->wave_cap, nullptr, 0u);
+    }
     HIP_TRY(c, hipGetLastError());
-    hipLaunchKernelGGL(repair_block_kernel<false>, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
+    hipLaunchKernelGGL(repair_block_kernel<0>, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
                        p->d_cnt.p + 2, p->b_mark.p, p->b_dlist.p, p->b_dnew.p, p->b_nhn.p,
-                       p->b_lvl.p, p->b_ord.p, d_out, nullptr);
+                       p->b_lvl.p, p->b_ord.p, d_out, nullptr, 0u);
     HIP_TRY(c, hipGetLastError());
     if (c->side) HIP_TRY(c, hipStreamWaitEvent(s, c->side_join, 0));
   }
@@ -2412,15 +2476,18 @@ spf_status spf_device_check(spf_ctx* c) {
   HIP_TRY(c, hipMemcpy(&flag, c->d_fault.p, sizeof flag, hipMemcpyDeviceToHost));
   if (!flag) return SPF_OK;
   HIP_TRY(c, hipMemset(c->d_fault.p, 0, sizeof flag));
-  if (flag & 24u) {
-    // what-if repair diagnostics: a loop bound (bit 3, phase in bits 8-15) or
-    // a range check of the profiled instance (bit 4, site in bits 16-23)
+  if (flag & 56u) {
+    // what-if repair diagnostics: a loop bound (bit 3, phase in bits 8-15), a
+    // range check of the profiled instances (bit 4, site in bits 16-23) or a
+    // team past its profile region (bit 5, kernel in bits 24-31)
     return fail(c, SPF_E_HIP,
-                "what-if repair on device %d: %s%s (fault word 0x%08x: loop phase %u, check site %u); "
-                "the results of this context's launches since the last check are invalid",
+                "what-if repair on device %d: %s%s%s (fault word 0x%08x: loop phase %u, check site %u, "
+                "profile kernel %u); the results of this context's launches since the last check are "
+                "invalid",
                 c->device, (flag & 8u) ? "a repair loop reached its iteration bound " : "",
-                (flag & 16u) ? "a scratch index failed its range check" : "", flag, (flag >> 8) & 0xFFu,
-                (flag >> 16) & 0xFFu);
+                (flag & 16u) ? "a scratch index failed its range check " : "",
+                (flag & 32u) ? "a team's profile row is outside the profile buffer" : "", flag,
+                (flag >> 8) & 0xFFu, (flag >> 16) & 0xFFu, flag >> 24);
   }
   if (flag & 2u) {
     // a team BFS gave up waiting for its members (another process's grid

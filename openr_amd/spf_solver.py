@@ -146,21 +146,114 @@ class PrefixEntry:
         return ":" not in self.prefix
 
 
+def nodeAreaMapOrder(ops: Sequence[Tuple[int, Tuple[str, str]]]) -> List[Tuple[str, str]]:
+    """The surviving keys of a PrefixEntries map (std::unordered_map<NodeAndArea,
+    PrefixEntry>, openr/common/Types.h:24) in its iteration order, after the
+    emplace (op 1) / erase (op 0) history ``ops`` (ls_node_area_map_order)."""
+    n = len(ops)
+    nodes = (C.c_char_p * n)(*[k[0].encode() for _, k in ops])
+    areas = (C.c_char_p * n)(*[k[1].encode() for _, k in ops])
+    code = (C.c_uint8 * n)(*[o for o, _ in ops])
+    order = (C.c_uint32 * n)()
+    got = C.c_uint32()
+    st = N.lib.ls_node_area_map_order(nodes, areas, code, n, order, C.byref(got))
+    if st != N.SPF_OK:
+        N.raise_for(st, "ls_node_area_map_order")
+    return [ops[order[i]][1] for i in range(got.value)]
+
+
+_OPS = {"WIN_IF_PRESENT": 0, "WIN_IF_NOT_PRESENT": 1, "IGNORE_IF_NOT_PRESENT": 2}
+
+
+class _NativePrefixState(N.NativeHandle):
+    """dc_prefix_state (include/openr_decision.h): the C++ SpfSolver's PrefixState."""
+
+    _LEVEL = 0
+    _destroy = "dc_prefix_state_destroy"
+
+    def __init__(self) -> None:
+        self._adopt(C.c_void_p(N.lib.dc_prefix_state_create()))
+
+    def update(self, node: str, area: str, e: "PrefixEntry") -> None:
+        r = N.DcPrefixEntry()
+        r.prefix = e.prefix.encode()
+        r.is_v4 = e.isV4
+        r.is_bgp = e.type == "BGP"
+        r.forwarding_type = _FWD_TYPE[e.forwardingType]
+        r.forwarding_algorithm = _FWD_ALGO[e.forwardingAlgorithm]
+        r.has_prepend_label = e.prependLabel is not None
+        r.prepend_label = e.prependLabel or 0
+        r.has_min_nexthop = e.minNexthop is not None
+        r.min_nexthop = e.minNexthop or 0
+        r.path_preference = e.metrics.path_preference
+        r.source_preference = e.metrics.source_preference
+        r.distance = e.metrics.distance
+        keep = []
+        if e.mv is not None:
+            ents = (N.DcMetricEntity * max(1, len(e.mv.metrics)))()
+            for i, m in enumerate(e.mv.metrics):
+                vals = (C.c_int64 * max(1, len(m.metric)))(*m.metric)
+                keep.append(vals)
+                ents[i].type, ents[i].priority = m.type, m.priority
+                ents[i].op, ents[i].is_tie_breaker = _OPS[m.op], m.isBestPathTieBreaker
+                ents[i].n_metric, ents[i].metric = len(m.metric), vals
+            r.has_mv, r.mv_version, r.n_mv, r.mv = 1, e.mv.version, len(e.mv.metrics), ents
+            keep.append(ents)
+        N.raise_for(N.lib.dc_prefix_update(self._h, node.encode(), area.encode(), C.byref(r)),
+                    "dc_prefix_update")
+
+
 class PrefixState:
-    """prefix -> {(node, area): PrefixEntry} (openr/decision/PrefixState.h)."""
+    """prefix -> {(node, area): PrefixEntry} (openr/decision/PrefixState.h).
+
+    Each prefix's dict iterates in the order of the reference's PrefixEntries
+    map (an std::unordered_map, Types.h:24): PrefixState.cpp:47-60 emplaces a
+    new advertiser and erases a withdrawn one, and the map's order follows
+    from that history, which is kept per prefix (dropped with the map when its
+    last advertiser goes, PrefixState.cpp:49-50) and replayed natively
+    whenever the key set of a prefix with several advertisers changes.
+    runBestPathSelectionBgp's TIE_WINNER / TIE outcome (Decision.cpp:795-832)
+    and addBestPaths' prepend-label walk (:1047-1053) depend on it."""
 
     def __init__(self) -> None:
         self._p: Dict[str, Dict[Tuple[str, str], PrefixEntry]] = {}
+        self._ops: Dict[str, List[Tuple[int, Tuple[str, str]]]] = {}
+        # the same state in the C++ SpfSolver's PrefixState (dc_prefix_state),
+        # kept in step with every update (entries are taken as values: an
+        # entry changed after updatePrefix must be updated again)
+        self._nat = _NativePrefixState()
+
+    def _reorder(self, prefix: str) -> None:
+        ent = self._p[prefix]
+        if len(ent) > 1:
+            self._p[prefix] = {k: ent[k] for k in nodeAreaMapOrder(self._ops[prefix])}
 
     def updatePrefix(self, node: str, area: str, entry: PrefixEntry) -> None:
-        self._p.setdefault(entry.prefix, {})[(node, area)] = entry
+        self._nat.update(node, area, entry)
+        key = (node, area)
+        ent = self._p.get(entry.prefix)
+        if ent is None:
+            self._p[entry.prefix] = {key: entry}
+            self._ops[entry.prefix] = [(1, key)]
+        elif key in ent:  # emplace finds it: assigned in place (:60-68)
+            ent[key] = entry
+        else:
+            ent[key] = entry
+            self._ops[entry.prefix].append((1, key))
+            self._reorder(entry.prefix)
 
     def deletePrefix(self, node: str, area: str, prefix: str) -> None:
+        N.raise_for(N.lib.dc_prefix_delete(self._nat._h, node.encode(), area.encode(),
+                                           prefix.encode()), "dc_prefix_delete")
         ent = self._p.get(prefix)
-        if ent is not None:
-            ent.pop((node, area), None)
+        if ent is not None and (node, area) in ent:
+            del ent[(node, area)]
             if not ent:
                 del self._p[prefix]
+                del self._ops[prefix]
+            else:
+                self._ops[prefix].append((0, (node, area)))
+                self._reorder(prefix)
 
     def prefixes(self) -> Dict[str, Dict[Tuple[str, str], PrefixEntry]]:
         return self._p
@@ -404,9 +497,130 @@ class _SetResult:
     hops: List[Tuple[int, int]]  # (directed edge me -> neighbour, metric)
 
 
-class SpfSolver:
-    """``openr::SpfSolver`` (Decision.h) on the MI355X engine."""
+class _NativeSolver(N.NativeHandle):
+    """dc_solver (include/openr_decision.h): the C++ SpfSolver."""
 
+    _LEVEL = 0
+    _destroy = "dc_solver_destroy"
+
+    def __init__(self, me: str, enableV4: bool, lfa: bool, dryRun: bool, brs: bool) -> None:
+        h = C.c_void_p()
+        N.raise_for(N.lib.dc_solver_create(me.encode(), int(enableV4), int(lfa), int(dryRun),
+                                           int(brs), C.byref(h)), "dc_solver_create")
+        self._adopt(h)
+
+    def set_static(self, label: int, nhs: Sequence["NextHopThrift"]) -> None:
+        recs = (N.DcNexthop * max(1, len(nhs)))()
+        strings: List[bytes] = []
+        labels: List[int] = []
+
+        def sid(x: Optional[str]) -> int:
+            if x is None:
+                return N.DC_NONE
+            strings.append(x.encode())
+            return len(strings) - 1
+
+        for r, nh in zip(recs, nhs):
+            r.address[:len(nh.address)] = list(nh.address)
+            r.address_len = len(nh.address)
+            r.metric = nh.metric
+            a = nh.mplsAction
+            if a is not None:
+                r.mpls_action = N.DC_MPLS_ACTIONS.index(a.action)
+                r.swap_label = a.swapLabel or 0
+                if a.pushLabels:
+                    r.push_off, r.n_push = len(labels), len(a.pushLabels)
+                    labels.extend(a.pushLabels)
+            r.ifname, r.area, r.neighbor = sid(nh.ifName), sid(nh.area), sid(nh.neighborNodeName)
+        sarr = (C.c_char_p * max(1, len(strings)))(*strings)
+        larr = (C.c_int32 * max(1, len(labels)))(*labels)
+        N.raise_for(N.lib.dc_static_mpls_route_set(self._h, label, recs, len(nhs), sarr, larr),
+                    (N.lib.dc_last_error(self._h) or b"").decode())
+
+
+class NativeRouteDb(N.NativeHandle):
+    """A DecisionRouteDb built by the C++ SpfSolver (dc_route_db): read as
+    tables, or materialised into the Python route types (``routeDb()``)."""
+
+    _LEVEL = 0
+    _destroy = "dc_route_db_destroy"
+
+    def __init__(self, h: C.c_void_p, prefixState: "PrefixState") -> None:
+        self._adopt(h)
+        self._ps = prefixState
+
+    def unicastCount(self) -> int:
+        return int(N.lib.dc_route_db_unicast_count(self._h))
+
+    def mplsCount(self) -> int:
+        return int(N.lib.dc_route_db_mpls_count(self._h))
+
+    def nexthopRecords(self) -> np.ndarray:
+        n = C.c_uint32()
+        p = N.lib.dc_route_db_nexthops(self._h, C.byref(n))
+        if not n.value:
+            return np.zeros(0, N.DC_NEXTHOP_DTYPE)
+        raw = (C.c_char * (n.value * N.DC_NEXTHOP_DTYPE.itemsize)).from_address(p)
+        return np.frombuffer(raw, N.DC_NEXTHOP_DTYPE).copy()
+
+    def _table(self, fn, cols: int) -> np.ndarray:
+        n = C.c_uint32()
+        p = getattr(N.lib, fn)(self._h, C.byref(n))
+        if not n.value:
+            return np.zeros((0, cols), np.uint32)
+        raw = (C.c_uint32 * (n.value * cols)).from_address(p)
+        return np.frombuffer(raw, np.uint32).reshape(n.value, cols).copy()
+
+    def routeDb(self) -> "DecisionRouteDb":
+        recs = self.nexthopRecords()
+        nl = C.c_uint32()
+        lp = N.lib.dc_route_db_labels(self._h, C.byref(nl))
+        pool = (np.frombuffer((C.c_int32 * nl.value).from_address(lp), np.int32).tolist()
+                if nl.value else [])
+        strs = [N.lib.dc_route_db_string(self._h, i).decode()
+                for i in range(N.lib.dc_route_db_strings(self._h))]
+        none = N.DC_NONE
+        actions: Dict[tuple, MplsAction] = {}
+        nhs: List[NextHopThrift] = []
+        for r in recs.tolist():
+            addr, alen, act, npush, _, metric, swap, poff, ifn, area, nb = r
+            a = None
+            if act:
+                key = (act, swap, tuple(pool[poff:poff + npush]) if act == 1 else ())
+                a = actions.get(key)
+                if a is None:
+                    name = N.DC_MPLS_ACTIONS[act]
+                    a = actions[key] = MplsAction(name, swap if name == "SWAP" else None,
+                                                  key[2] if name == "PUSH" else None)
+            nhs.append(NextHopThrift(bytes(addr[:alen]), None if ifn == none else strs[ifn], metric, a,
+                                     None if area == none else strs[area],
+                                     None if nb == none else strs[nb]))
+        db = DecisionRouteDb()
+        prefixes = self._ps.prefixes()
+        for p, node, area, dni, b, e in self._table("dc_route_db_unicast_table", 6).tolist():
+            prefix = strs[p]
+            na = (strs[node], strs[area])
+            db.addUnicastRoute(RibUnicastEntry(prefix, set(nhs[b:e]), prefixes[prefix][na], na[1],
+                                               bool(dni)))
+        for label, b, e in self._table("dc_route_db_mpls_table", 3).tolist():
+            label = label - (1 << 32) if label >= 1 << 31 else label
+            db.addMplsRoute(RibMplsEntry(label, set(nhs[b:e])))
+        return db
+
+
+_COUNTERS = ("decision.no_route_to_prefix", "decision.skipped_unicast_route",
+             "decision.no_route_to_label", "decision.incompatible_forwarding_type")
+
+
+class SpfSolver:
+    """``openr::SpfSolver`` (Decision.h) on the MI355X engine.
+
+    buildRouteDb runs the C++ SpfSolver (openr_amd/csrc/decision.cpp, the
+    C-ABI of include/openr_decision.h a C++ Decision calls) and materialises
+    its DecisionRouteDb here; ``native = False`` (or ``_generic``) takes the
+    Python restatement below instead, which the tests hold it equal to."""
+
+    native = True
     # one-advertiser prefixes skip the selection walk, and one-advertiser IP
     # routes and label routes are assembled inline (tests switch it off to
     # compare against the generic walk and getNextHopsThrift restatement)
@@ -423,10 +637,63 @@ class SpfSolver:
         self.enableBestRouteSelection = enableBestRouteSelection
         self._bestRoutesCache: Dict[str, BestRouteSelectionResult] = {}
         self.counters: Dict[str, int] = {}  # the fb303 stats SpfSolver bumps (subset)
+        self._nat: Dict[str, _NativeSolver] = {}  # C++ solvers by myNodeName
+        self._nat_counts: Dict[str, Dict[str, int]] = {}
+        self._nat_cache = None  # (solver, prefix state) of the last native build
 
     def getBestRoutesCache(self) -> Dict[str, BestRouteSelectionResult]:
         """SpfSolver::getBestRoutesCache: the last route build's selections."""
+        if self._nat_cache is not None:  # read from the C++ solver on demand
+            nat, ps = self._nat_cache
+            cache: Dict[str, BestRouteSelectionResult] = {}
+            for prefix in ps.prefixes():
+                found, ok = C.c_int(), C.c_int()
+                bn, ba = C.c_char_p(), C.c_char_p()
+                cnt = C.c_uint32()
+                pb = prefix.encode()
+                N.raise_for(N.lib.dc_best_route(nat._h, pb, C.byref(found), C.byref(ok), C.byref(bn),
+                                                C.byref(ba), None, None, 0, C.byref(cnt)), "dc_best_route")
+                if not found.value:
+                    continue
+                nodes = (C.c_char_p * max(1, cnt.value))()
+                areas = (C.c_char_p * max(1, cnt.value))()
+                N.lib.dc_best_route(nat._h, pb, C.byref(found), C.byref(ok), C.byref(bn), C.byref(ba),
+                                    nodes, areas, cnt.value, C.byref(cnt))
+                cache[prefix] = BestRouteSelectionResult(
+                    bool(ok.value), [(nodes[i].decode(), areas[i].decode()) for i in range(cnt.value)],
+                    None if bn.value is None else (bn.value.decode(), ba.value.decode()))
+            return cache
         return dict(self._bestRoutesCache)
+
+    def _native_solver(self, me: str) -> _NativeSolver:
+        nat = self._nat.get(me)
+        if nat is None:
+            nat = self._nat[me] = _NativeSolver(me, self.enableV4, self.computeLfaPaths,
+                                                self.bgpDryRun, self.enableBestRouteSelection)
+            self._nat_counts[me] = {}
+            for label, nhs in self.staticMplsRoutes.items():
+                nat.set_static(label, nhs)
+        return nat
+
+    def buildRouteDbNative(self, myNodeName: str, areaLinkStates: Dict[str, LinkState],
+                           prefixState: PrefixState) -> Optional[NativeRouteDb]:
+        """buildRouteDb on the C++ SpfSolver (dc_build_route_db), the route DB
+        left native (tables; NativeRouteDb.routeDb() materialises it)."""
+        nat = self._native_solver(myNodeName)
+        names = list(areaLinkStates)
+        arr = (C.c_char_p * max(1, len(names)))(*[a.encode() for a in names])
+        hs = (C.c_void_p * max(1, len(names)))(*[areaLinkStates[a]._h.value for a in names])
+        out = C.c_void_p()
+        st = N.lib.dc_build_route_db(nat._h, arr, hs, len(names), prefixState._nat._h, C.byref(out))
+        N.raise_for(st, (N.lib.dc_last_error(nat._h) or b"").decode())
+        seen = self._nat_counts[myNodeName]
+        for k in _COUNTERS:  # the fb303 counters bumped by this build
+            now = int(N.lib.dc_counter(nat._h, k.encode()))
+            if now != seen.get(k, 0):
+                self.counters[k] = self.counters.get(k, 0) + now - seen.get(k, 0)
+                seen[k] = now
+        self._nat_cache = (nat, prefixState)
+        return NativeRouteDb(out, prefixState) if out.value else None
 
     def _bump(self, key: str) -> None:
         self.counters[key] = self.counters.get(key, 0) + 1
@@ -436,14 +703,24 @@ class SpfSolver:
         """SpfSolver::updateStaticMplsRoutes (Decision.cpp): label -> next hops."""
         for label, nhs in routesToUpdate.items():
             self.staticMplsRoutes[label] = list(nhs)
+            for nat in self._nat.values():
+                nat.set_static(label, nhs)
         for label in routesToDelete:
             self.staticMplsRoutes.pop(label, None)
+            for nat in self._nat.values():
+                N.raise_for(N.lib.dc_static_mpls_route_delete(nat._h, label), "static delete")
 
     # -- batched next-hop selection (getMinCostNodes/..WithMetric/..Thrift) ----
     def _select(self, ls: LinkState, me: str, sets: Sequence[Sequence[str]]) -> List[_SetResult]:
         names, rp, col, met, lid, ovl = ls.flatten()
         id_of = {n: i for i, n in enumerate(names)}
         if me not in id_of or not sets:
+            # nothing selected: empty arrays of the same shapes, so
+            # _buildSingleArea reads this build's (empty) selection, never a
+            # previous build's
+            self._lid = lid
+            self._raw = (np.full(len(sets), (1 << 64) - 1, np.uint64), np.zeros(len(sets), np.uint32),
+                         np.zeros(len(sets), np.uint32), np.zeros(len(sets), np.uint64), 1)
             return [_SetResult(None, []) for _ in sets]
         ptr = np.zeros(len(sets) + 1, np.uint32)
         members: List[int] = []
@@ -642,7 +919,7 @@ class SpfSolver:
         if need is not None and need > len(nhs):
             return None  # min-nexthop requirement not met
         if any(na[0] == me for na in best):
-            prepend = next((e.prependLabel for na, e in sorted(ents.items())
+            prepend = next((e.prependLabel for na, e in ents.items()  # map order (:1047-1053)
                             if na[0] == me and e.prependLabel is not None), None)
             assert prepend is not None, "self route must carry a prepend label"
             nhs = set(nhs)
@@ -664,14 +941,16 @@ class SpfSolver:
 
     def _runBestPathSelectionBgp(self, ents: Dict[Tuple[str, str], PrefixEntry],
                                  areaLinkStates: Dict[str, LinkState]) -> BestRouteSelectionResult:
-        """:791-832.  The reference walks its std::unordered_map of entries;
-        here ascending (node, area) -- the outcome differs only where a tie
-        chain's result depends on the visit order."""
+        """:791-832, visiting the entries in the order of the reference's
+        PrefixEntries map (PrefixState keeps each prefix's dict in it; the
+        reachable-entry filter of createRouteForPrefix, :409-420, erases in
+        place and keeps the survivors' order): bestNodeArea (TIE_WINNER) and
+        whether a TIE / ERROR aborts before a later WINNER follow it."""
         ret = BestRouteSelectionResult()
         bestVector: Optional[MetricVector] = None
         chosen: List[Tuple[str, str]] = []
-        for na in sorted(ents):
-            mv = ents[na].mv
+        for na, e in ents.items():
+            mv = e.mv
             r = WINNER if bestVector is None else compareMetricVectors(mv, bestVector)
             if r == WINNER:
                 chosen = []
@@ -808,7 +1087,7 @@ class SpfSolver:
         perDest = ftype == "SR_MPLS"
         filtered = list(res.allNodeAreas)
         if res.hasNode(me) and perDest:
-            for na, e in sorted(ents.items()):
+            for na, e in ents.items():  # map order (:855-862)
                 if na[0] == me and e.prependLabel is not None:
                     if na in filtered:
                         filtered.remove(na)
@@ -867,7 +1146,15 @@ class SpfSolver:
     # -- buildRouteDb (Decision.cpp:557-722) ----------------------------------------
     def buildRouteDb(self, myNodeName: str, areaLinkStates: Dict[str, LinkState],
                      prefixState: PrefixState, _generic: bool = False) -> Optional[DecisionRouteDb]:
-        """``_generic`` (tests): take the several-area walk with one area too."""
+        """``_generic`` (tests): the Python restatement's several-area walk
+        with one area too."""
+        if self.native and not _generic:
+            ndb = self.buildRouteDbNative(myNodeName, areaLinkStates, prefixState)
+            if ndb is None:
+                return None
+            with ndb:
+                return ndb.routeDb()
+        self._nat_cache = None
         areas = areaOrder(areaLinkStates)
         if not any(ls.hasNode(myNodeName) for _, ls in areas):
             return None

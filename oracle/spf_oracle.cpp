@@ -1556,6 +1556,28 @@ uint32_t orc_keyvals_order(const char* const* keys, uint32_t n, uint32_t* perm_o
   return k;
 }
 
+// Iteration order of a PrefixEntries map (openr/common/Types.h:24:
+// std::unordered_map<NodeAndArea, PrefixEntry>, folly's std::hash<std::pair>)
+// after the emplace (op 1) / erase (op 0) history of PrefixState.cpp:47-60.
+// perm_out[j] = op index that inserted the j-th surviving key; returns their
+// number.  runBestPathSelectionBgp (Decision.cpp:795-832) walks this order.
+uint32_t orc_node_area_map_order(const char* const* nodes, const char* const* areas,
+                                 const uint8_t* ops, uint32_t n, uint32_t* perm_out) {
+  struct H {
+    size_t operator()(const std::pair<std::string, std::string>& k) const {
+      return orc::hashStrPair(k.first, k.second);
+    }
+  };
+  std::unordered_map<std::pair<std::string, std::string>, uint32_t, H> m;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (ops[i]) m.emplace(std::make_pair(std::string(nodes[i]), std::string(areas[i])), i);
+    else m.erase(std::make_pair(std::string(nodes[i]), std::string(areas[i])));
+  }
+  uint32_t k = 0;
+  for (const auto& kv : m) perm_out[k++] = kv.second;
+  return k;
+}
+
 uint64_t orc_link_keyhash(const char* n1, const char* if1, const char* n2, const char* if2) {
   return orc::keyHash(n1, if1, n2, if2);
 }

@@ -10,7 +10,7 @@ import ctypes as C
 import json
 import subprocess
 from pathlib import Path
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -372,6 +372,23 @@ def keyvals_order(keys: Sequence[str]) -> List[int]:
     out = np.zeros(max(1, len(keys)), np.uint32)
     k = lib.orc_keyvals_order(arr, len(keys), _p(out))
     return [int(x) for x in out[:k]]
+
+
+lib.orc_node_area_map_order.restype = C.c_uint32
+lib.orc_node_area_map_order.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                        C.POINTER(C.c_uint8), C.c_uint32, _u32p]
+
+
+def node_area_map_order(ops: Sequence[Tuple[int, Tuple[str, str]]]) -> List[Tuple[str, str]]:
+    """Surviving (node, area) keys of a PrefixEntries map in the reference's
+    iteration order after the emplace (1) / erase (0) history ``ops``."""
+    n = max(1, len(ops))
+    nodes = (C.c_char_p * n)(*[k[0].encode() for _, k in ops])
+    areas = (C.c_char_p * n)(*[k[1].encode() for _, k in ops])
+    code = (C.c_uint8 * n)(*[o for o, _ in ops])
+    out = np.zeros(n, np.uint32)
+    k = lib.orc_node_area_map_order(nodes, areas, code, len(ops), _p(out))
+    return [ops[int(i)][1] for i in out[:k]]
 
 
 def route_digests(orc: "OracleLinkState", table: NameTable, mes: Sequence[int],

@@ -131,19 +131,24 @@ def test_bgp_redistribution_basic(generic):
     bgp2 = PrefixEntry(addr3, type="BGP", mv=_mv(), data=b"data2")
     ps.updatePrefix("2", K, bgp2)
     assert len(build("1").unicastRoutes) == 1
-    # node 2's last metric one lower: back to node 1's
+    # node 2's last metric one lower: back to node 1's (thrift entries are
+    # values: the changed entry is published again, as the reference test does)
     bgp2.mv.metrics[-1].metric = (bgp2.mv.metrics[-1].metric[0] - 1,)
+    ps.updatePrefix("2", K, bgp2)
     db = build("2")
     assert len(db.unicastRoutes) == 2 and db.unicastRoutes[addr3].data == b"data1"
     assert rows(db.unicastRoutes[addr3].nexthops) == {nh(adj21, 10)}
     # node 2 better
     bgp2.mv.metrics[-1].metric = (bgp2.mv.metrics[-1].metric[0] + 2,)
+    ps.updatePrefix("2", K, bgp2)
     db = build("1")
     assert len(db.unicastRoutes) == 2 and db.unicastRoutes[addr3].data == b"data2"
     assert rows(db.unicastRoutes[addr3].nexthops) == {nh(adj12, 10)}
     # a tie-breaker metric: multipath; nodes 1 and 2 program no BGP route
     bgp1.mv.metrics[-1].isBestPathTieBreaker = True
     bgp2.mv.metrics[-1].isBestPathTieBreaker = True
+    ps.updatePrefix("1", K, bgp1)
+    ps.updatePrefix("2", K, bgp2)
     assert len(build("1").unicastRoutes) == 1
     db = build("3")
     assert len(db.unicastRoutes) == 3

@@ -90,6 +90,34 @@ def test_pop_and_adjacency_label_routes():
             assert nh.metric == link.getMetricFromNode(me)
 
 
+def test_no_prefixes_no_node_labels_fresh_solver():
+    """A single-area build with nothing to select (no prefixes, every node
+    label 0: non-SR mode) on a FRESH solver still returns the adjacency-label
+    routes (Decision.cpp:667-698) and static MPLS routes (:700-707); a reused
+    solver does not read the previous build's selection."""
+    from openr_amd.lsdb import PackedLsdb
+    from openr_amd.spf_solver import NextHopThrift, PrefixEntry, PrefixState
+
+    topo = T.grid(4)
+    dbs = topo.lsdb.dbs.copy()
+    dbs["node_label"] = 0  # non-SR mode: adjacency labels only
+    with LinkState() as ls:
+        ls.updateAdjacencyDatabases(PackedLsdb(topo.lsdb.blob, dbs, topo.lsdb.adjs))
+        assert not any(ls.getAdjacencyDatabaseLabels().values())
+        me = topo.nodes[5]
+        s = SpfSolver(me, True, False)
+        s.updateStaticMplsRoutes({77: [NextHopThrift(bytes(16), None, 0, None, None, None)]})
+        db = s.buildRouteDb(me, {ls.getArea(): ls}, PrefixState())
+        adj = {l.getAdjLabelFromNode(me) for l in ls.linksFromNode(me)}
+        assert not db.unicastRoutes and set(db.mplsRoutes) == adj | {77}
+        ps = PrefixState()
+        for node in topo.nodes:
+            ps.updatePrefix(node, ls.getArea(), PrefixEntry(f"fc00::{topo.nodes.index(node)}/128"))
+        assert len(s.buildRouteDb(me, {ls.getArea(): ls}, ps).unicastRoutes) == len(topo.nodes) - 1
+        db2 = s.buildRouteDb(me, {ls.getArea(): ls}, PrefixState())
+        assert not db2.unicastRoutes and set(db2.mplsRoutes) == adj | {77}
+
+
 @pytest.mark.parametrize("n", [2, 4, 6, 8])
 def test_grid_route_count_and_distances(n):
     """DecisionTest.cpp:4301-4356 (GridTopologyFixture.ShortestPathTest): every
