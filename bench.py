@@ -1105,9 +1105,20 @@ class FacadeRouteBuild:
                            "(openr_amd/spf_solver.py, native=False)",
                 "routes": len(py.unicastRoutes) + len(py.mplsRoutes), "mismatches": bad}
 
+    def _solver_ns(self):
+        import ctypes as C
+
+        from openr_amd import _native as N
+
+        out = (C.c_uint64 * 6)()
+        nat = self.solver._native_solver(self.me)
+        N.lib.dc_debug_phase_ns(nat._h, out)
+        return list(out)
+
     def enable_timing(self, k: int) -> None:
         self.pub, self.build = [], []
         self.ph0 = self.ls.debugPhaseNs()
+        self.sv0 = self._solver_ns()
 
     def kernel_ms(self):
         ph = [(b - a) / 1e6 / max(1, len(self.build)) for a, b in zip(self.ph0, self.ls.debugPhaseNs())]
@@ -1115,7 +1126,12 @@ class FacadeRouteBuild:
                          "buildRouteDb (C++ SpfSolver: selection kernel + route assembly)":
                              1e3 * float(np.mean(self.build)),
                          "of which getSpfResult(me) facade phases (plan, execute+copy, pathLinks, "
-                         "host)": ph, "routes_per_build": self.routes,
+                         "host)": ph,
+                         "of which C++ SpfSolver phases (setup + getSpfResult(me), prefix walk, "
+                         "label sets, batched selection, route assembly, adjacency/static)":
+                             [(b - a) / 1e6 / max(1, len(self.build))
+                              for a, b in zip(self.sv0, self._solver_ns())],
+                         "routes_per_build": self.routes,
                          "nexthop_records_per_build": self.nexthops}
         return {"route_build": 1e3 * (float(np.mean(self.pub)) + float(np.mean(self.build)))}
 

@@ -151,6 +151,14 @@ spf_status dc_best_route(const dc_solver* s, const char* prefix, int* found, int
                          const char** best_node, const char** best_area, const char** nodes,
                          const char** areas, uint32_t cap, uint32_t* count);
 
+/* Cumulative dc_build_route_db cost by phase in ns since creation (diagnostics;
+ * no reference counterpart): [0] area setup + getSpfResult(me), [1] the
+ * prefix walk (createRouteForPrefix; per-prefix SR / KSP2 / several-area
+ * routes included), [2] node-label collection + set layout, [3] the batched
+ * selection (spf_mplan_routes / spf_routes), [4] route assembly from it,
+ * [5] adjacency-label and static routes. */
+void dc_debug_phase_ns(const dc_solver* s, uint64_t* out);
+
 /* ---- DecisionRouteDb ---------------------------------------------------- */
 void dc_route_db_destroy(dc_route_db* db);
 /* the string table (interface names, areas, neighbours, prefixes) */

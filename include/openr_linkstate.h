@@ -114,6 +114,8 @@ uint64_t ls_num_links(const ls_state* ls);
 uint64_t ls_num_nodes(const ls_state* ls);
 int ls_has_node(const ls_state* ls, const char* node);
 int ls_is_node_overloaded(const ls_state* ls, const char* node);
+/* the same by interned name id (ls_name_id) */
+int ls_is_node_overloaded_id(const ls_state* ls, uint32_t node_id);
 
 uint32_t ls_name_id(ls_state* ls, const char* name);
 const char* ls_name(const ls_state* ls, uint32_t id);
@@ -129,6 +131,12 @@ spf_status ls_link_info(const ls_state* ls, uint32_t link_id, ls_link_desc* out)
 
 spf_status ls_get_spf_result(ls_state* ls, const char* node, int use_link_metric,
                              ls_spf_view* out);
+/* getSpfResult for callers that read metrics and next hops only (SpfSolver's
+ * route selection): the same memo entry and the same decision.spf_runs count,
+ * its pathLinks derived on the first later call that needs them (the view's
+ * pl_* are NULL until then). */
+spf_status ls_get_spf_metrics(ls_state* ls, const char* node, int use_link_metric,
+                              ls_spf_view* out);
 spf_status ls_get_kth_paths(ls_state* ls, const char* src, const char* dst,
                             uint64_t k, ls_paths_view* out);
 /* Batch fill of the getKthPaths memo: (src, d, 1) and (src, d, 2) for every
@@ -182,6 +190,9 @@ spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges);
  * changes whenever ls_flatten rebuilds it, not when it patches metrics or
  * overload bits in place.  Callers caching per-graph tables key them on it. */
 uint64_t ls_graph_epoch(const ls_state* ls);
+/* A process-unique id of the state (never reused, unlike its address): name
+ * ids (ls_name_id) are stable per state, so callers may cache them by it. */
+uint64_t ls_serial(const ls_state* ls);
 spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids /* [n_nodes] */);
 /* Copy of the flattened CSR (sizes from ls_flatten); any pointer may be NULL. */
 spf_status ls_graph_csr(ls_state* ls, uint32_t* row_ptr, uint32_t* col, int32_t* metric,

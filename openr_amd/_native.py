@@ -340,6 +340,9 @@ PROTOTYPES = {
     "ls_node_area_map_order": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
                                          C.POINTER(C.c_uint8), C.c_uint32, _u32p, _u32p]),
     "ls_graph_epoch": (C.c_uint64, [_vp]),
+    "ls_get_spf_metrics": (C.c_int, [_vp, C.c_char_p, C.c_int, C.POINTER(LsSpfView)]),
+    "ls_serial": (C.c_uint64, [_vp]),
+    "ls_is_node_overloaded_id": (C.c_int, [_vp, C.c_uint32]),
     # SpfSolver / PrefixState (include/openr_decision.h)
     "dc_prefix_state_create": (_vp, []),
     "dc_prefix_state_destroy": (None, [_vp]),
@@ -360,6 +363,7 @@ PROTOTYPES = {
     "dc_best_route": (C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                 C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
                                 C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_uint32, _u32p]),
+    "dc_debug_phase_ns": (None, [_vp, _u64p]),
     "dc_route_db_destroy": (None, [_vp]),
     "dc_route_db_strings": (C.c_uint32, [_vp]),
     "dc_route_db_string": (C.c_char_p, [_vp, C.c_uint32]),

@@ -21,6 +21,7 @@
 //  memoised SPF results / KSP2 paths of every area.
 // ============================================================================
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -39,6 +40,12 @@
 #include "openr_decision.h"
 
 namespace {
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 constexpr uint64_t kInf64 = ~0ull;
 
@@ -77,6 +84,10 @@ struct Entry {
   std::optional<int64_t> min_nexthop;
   int32_t pp = 0, sp = 0, distance = 0;
   std::optional<MetricVector> mv;
+  // the advertiser's name id in the LinkState with serial id_serial (a
+  // cache: ids are stable per state)
+  mutable uint64_t id_serial = 0;
+  mutable uint32_t id = 0;
 };
 // PrefixEntries (openr/common/Types.h:24): the reference's container
 using Entries = std::unordered_map<NodeArea, Entry, NodeAreaHash>;
@@ -149,11 +160,14 @@ CmpResult compare_metric_vectors(MetricVector& l, MetricVector& r) {
   return result;
 }
 
+using EntryRef = const std::pair<const NodeArea, Entry>*;
+
 // BestRouteSelectionResult (openr/decision/RibEntry.h); allNodeAreas is a std::set
 struct BestRoute {
   bool success = false;
   std::vector<NodeArea> all;  // ascending
   std::optional<NodeArea> best;
+  std::vector<EntryRef> refs;  // all[i]'s entry in the build's PrefixEntries (not cached)
   bool has_node(const std::string& n) const {
     for (const auto& na : all)
       if (na.first == n) return true;
@@ -214,6 +228,11 @@ struct dc_route_db {
     return id;
   }
   uint32_t opt(const std::optional<std::string>& s) { return s ? intern(*s) : DC_NONE; }
+  // a string no other record shares (a route's prefix): no lookup
+  uint32_t push_unique(const std::string& s) {
+    strs.push_back(s);
+    return (uint32_t)strs.size() - 1;
+  }
   // a next-hop set (sorted, unique) appended; returns [begin, end)
   std::pair<uint32_t, uint32_t> add_set(std::vector<NH>& set) {
     std::sort(set.begin(), set.end());
@@ -227,13 +246,23 @@ struct dc_route_db {
       r.metric = h.metric;
       r.swap_label = h.swap;
       r.n_push = (uint8_t)h.push.size();
-      r.push_off = (uint32_t)labels.size();
+      r.push_off = h.push.empty() ? 0u : (uint32_t)labels.size();
       labels.insert(labels.end(), h.push.begin(), h.push.end());
       r.ifname = opt(h.ifname);
       r.area = opt(h.area);
       r.neighbor = opt(h.neighbor);
       nhs.push_back(r);
     }
+    return {b, (uint32_t)nhs.size()};
+  }
+  // POD records (the kernel path's next hops: no PUSH labels) as a set
+  std::pair<uint32_t, uint32_t> add_records(std::vector<dc_nexthop>& v) {
+    auto lt = [](const dc_nexthop& a, const dc_nexthop& b) { return std::memcmp(&a, &b, sizeof a) < 0; };
+    auto eq = [](const dc_nexthop& a, const dc_nexthop& b) { return std::memcmp(&a, &b, sizeof a) == 0; };
+    std::sort(v.begin(), v.end(), lt);
+    v.erase(std::unique(v.begin(), v.end(), eq), v.end());
+    const uint32_t b = (uint32_t)nhs.size();
+    nhs.insert(nhs.end(), v.begin(), v.end());
     return {b, (uint32_t)nhs.size()};
   }
   void add_unicast(const std::string& prefix, const NodeArea& best, bool dni,
@@ -281,6 +310,8 @@ struct dc_solver {
   std::map<int32_t, std::vector<NH>> static_mpls;  // staticMplsRoutes_
   std::unordered_map<std::string, BestRoute> best_cache;  // bestRoutesCache_
   std::unordered_map<ls_state*, GraphCache> graphs;
+  // build cost by phase, ns since creation (dc_debug_phase_ns)
+  uint64_t phase_ns[6] = {0, 0, 0, 0, 0, 0};
 
   void bump(const char* k) { ++counters[k]; }
 };
@@ -301,7 +332,10 @@ spf_status sfail(dc_solver* s, spf_status st, const char* fmt, ...) {
 struct Area {
   std::string name;
   ls_state* ls = nullptr;
+  uint64_t serial = 0;  // ls_serial
   uint32_t me_id = 0;
+  std::vector<uint32_t> db_sid;  // name id -> route-db string id (+1; 0 = not yet)
+  uint32_t area_sid = DC_NONE;
   std::unordered_map<uint32_t, std::unique_ptr<SpfIdx>> spf;  // name id -> SPF result
   bool links_done = false;
   std::vector<MyLink> links;  // linksFromNode(me), in its order
@@ -309,6 +343,19 @@ struct Area {
   std::unordered_map<uint32_t, int32_t> labels;  // getAdjacencyDatabases(): node -> node label
 
   uint32_t id(const std::string& n) { return ls_name_id(ls, n.c_str()); }
+  uint32_t id(const std::pair<const NodeArea, Entry>& kv) {  // cached in the entry
+    const Entry& e = kv.second;
+    if (e.id_serial != serial) {
+      e.id = id(kv.first.first);
+      e.id_serial = serial;
+    }
+    return e.id;
+  }
+  uint32_t sid(dc_route_db* db, uint32_t name_id, const std::string& name) {
+    if (name_id >= db_sid.size()) db_sid.resize(std::max<size_t>(name_id + 1, 2 * db_sid.size()), 0);
+    if (!db_sid[name_id]) db_sid[name_id] = db->intern(name) + 1;
+    return db_sid[name_id] - 1;
+  }
   std::string name_of(uint32_t i) const { return ls_name(ls, i); }
 };
 
@@ -321,6 +368,11 @@ struct Build {
   spf_status st = SPF_OK;
 
   bool ok() const { return st == SPF_OK; }
+  Area* area_of(const std::string& name) {
+    if (areas.size() == 1) return areas[0]->name == name ? areas[0].get() : nullptr;
+    auto it = by_name.find(name);
+    return it == by_name.end() ? nullptr : it->second;
+  }
   spf_status ls_err(Area& a, spf_status code) {
     st = sfail(s, code, "LinkState of area %s: %s", a.name.c_str(), ls_last_error(a.ls));
     return st;
@@ -331,7 +383,7 @@ struct Build {
     auto it = a.spf.find(node);
     if (it != a.spf.end()) return it->second.get();
     auto x = std::make_unique<SpfIdx>();
-    const spf_status code = ls_get_spf_result(a.ls, a.name_of(node).c_str(), 1, &x->v);
+    const spf_status code = ls_get_spf_metrics(a.ls, a.name_of(node).c_str(), 1, &x->v);
     if (code != SPF_OK) {
       ls_err(a, code);
       return nullptr;
@@ -398,17 +450,31 @@ struct Build {
 
   // ---- best-route selection (Decision.cpp:724-832) ----
   std::optional<BestRoute> filter_drained(BestRoute r) {  // maybeFilterDrainedNodes :766-789
-    BestRoute f = r;
-    f.all.clear();
-    for (const auto& na : r.all) {
-      auto it = by_name.find(na.second);
-      if (it == by_name.end()) {  // areaLinkStates.at(area) throws
+    auto is_drained = [&](size_t i, bool& bad) {
+      const NodeArea& na = r.all[i];
+      Area* a = area_of(na.second);
+      if (!a) {  // areaLinkStates.at(area) throws
         st = sfail(s, SPF_E_INVALID, "advertiser %s in area %s, which has no LinkState",
                    na.first.c_str(), na.second.c_str());
-        return std::nullopt;
+        bad = true;
+        return false;
       }
-      if (!ls_is_node_overloaded(it->second->ls, na.first.c_str())) f.all.push_back(na);
-    }
+      return ls_is_node_overloaded_id(a->ls, a->id(*r.refs[i])) != 0;
+    };
+    bool any = false, bad = false;
+    for (size_t i = 0; i < r.all.size() && !any; ++i) any = is_drained(i, bad);
+    if (bad) return std::nullopt;
+    if (!any) return r;
+    std::vector<char> drained(r.all.size(), 0);
+    for (size_t i = 0; i < r.all.size(); ++i) drained[i] = is_drained(i, bad);
+    BestRoute f;
+    f.success = r.success;
+    f.best = r.best;
+    for (size_t i = 0; i < r.all.size(); ++i)
+      if (!drained[i]) {
+        f.all.push_back(r.all[i]);
+        f.refs.push_back(r.refs[i]);
+      }
     // (the filtered copy keeps the unfiltered bestNodeArea: the reference
     // compares the copy's bestNodeArea with its source's)
     return f.all.empty() ? r : f;
@@ -417,25 +483,29 @@ struct Build {
   std::optional<BestRoute> bgp_walk(const Entries& ents) {  // runBestPathSelectionBgp :791-832
     BestRoute ret;
     std::optional<MetricVector> best_v;
-    std::vector<NodeArea> chosen;
-    for (const auto& [na, e] : ents) {
-      MetricVector mv = *e.mv;  // the reference's entries are a copy (Decision.cpp:409)
+    std::vector<EntryRef> chosen;
+    auto by_key = [](EntryRef a, EntryRef b) { return a->first < b->first; };
+    auto set_all = [&]() {
+      std::sort(chosen.begin(), chosen.end(), by_key);
+      for (EntryRef x : chosen) ret.all.push_back(x->first);
+      ret.refs = chosen;
+    };
+    for (const auto& kv : ents) {
+      MetricVector mv = *kv.second.mv;  // the reference's entries are a copy (Decision.cpp:409)
       const CmpResult r = best_v ? compare_metric_vectors(mv, *best_v) : WINNER;
       if (r == WINNER) chosen.clear();
       if (r == WINNER || r == TIE_WINNER) {
         best_v = mv;
-        ret.best = na;
+        ret.best = kv.first;
       }
       if (r == WINNER || r == TIE_WINNER || r == TIE_LOOSER) {
-        chosen.push_back(na);
+        chosen.push_back(&kv);
       } else if (r == TIE || r == ERROR) {
-        std::sort(chosen.begin(), chosen.end());
-        ret.all = chosen;
+        set_all();
         return ret;  // success false: no route
       }
     }
-    std::sort(chosen.begin(), chosen.end());
-    ret.all = chosen;
+    set_all();
     ret.success = true;
     return filter_drained(std::move(ret));
   }
@@ -445,16 +515,18 @@ struct Build {
     if (s->best_route_selection) {
       // selectBestPrefixMetrics (Util.h:540-571): best (pp, sp, -distance) from (0, 0, 0)
       std::tuple<int64_t, int64_t, int64_t> bt{0, 0, 0};
-      for (const auto& [na, e] : ents) {
+      for (const auto& kv : ents) {
+        const Entry& e = kv.second;
         const std::tuple<int64_t, int64_t, int64_t> t{e.pp, e.sp, -(int64_t)e.distance};
         if (t < bt) continue;
         if (t > bt) {
           bt = t;
-          ret.all.clear();
+          ret.refs.clear();
         }
-        ret.all.push_back(na);
+        ret.refs.push_back(&kv);
       }
-      std::sort(ret.all.begin(), ret.all.end());
+      std::sort(ret.refs.begin(), ret.refs.end(), [](EntryRef a, EntryRef b) { return a->first < b->first; });
+      for (EntryRef x : ret.refs) ret.all.push_back(x->first);
       if (!ret.all.empty()) {  // selectBestNodeArea (Util.cpp:1028-1040)
         ret.best = ret.all[0];
         for (const auto& na : ret.all)
@@ -469,8 +541,10 @@ struct Build {
       if (!r) return std::nullopt;
       ret = std::move(*r);
     } else {  // openr routes: every advertiser is best
-      for (const auto& kv : ents) ret.all.push_back(kv.first);
-      std::sort(ret.all.begin(), ret.all.end());
+      for (const auto& kv : ents) ret.refs.push_back(&kv);
+      if (ret.refs.size() > 1)
+        std::sort(ret.refs.begin(), ret.refs.end(), [](EntryRef a, EntryRef b) { return a->first < b->first; });
+      for (EntryRef x : ret.refs) ret.all.push_back(x->first);
       ret.best = ret.all[0];
       ret.success = true;
     }
@@ -988,13 +1062,21 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     auto a = std::make_unique<Area>();
     a->name = name;
     a->ls = ls;
+    a->serial = ls_serial(ls);
     a->me_id = ls_name_id(ls, me.c_str());
     exists |= ls_has_node(ls, me.c_str()) != 0;
     b.by_name.emplace(name, a.get());
     b.areas.push_back(std::move(a));
   }
   if (!exists) return SPF_OK;  // std::nullopt
+  uint64_t t_ph = now_ns();
+  auto phase = [&](int k) {
+    const uint64_t t = now_ns();
+    s->phase_ns[k] += t - t_ph;
+    t_ph = t;
+  };
   s->best_cache.clear();
+  s->best_cache.reserve(ps->prefixes.size());
   const bool single = b.areas.size() == 1;
   std::vector<const SpfIdx*> mine;
   for (auto& a : b.areas) {
@@ -1002,25 +1084,43 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     if (!b.ok()) return b.st;
   }
 
+  phase(0);
   // ---- unicast: createRouteForPrefix (:389-555) ----
   struct Uni {
     const std::string* prefix;
-    Entries ents;
-    BestRoute res;
+    const Entries* ents;
+    std::unique_ptr<Entries> own;  // the filtered copy, when an entry was dropped
+    const BestRoute* res;           // in the solver's best-routes cache
     bool bgp, v4;
   };
   std::vector<Uni> uni;
+  uni.reserve(ps->prefixes.size());
   bool ksp_fetched = false;
+  std::unordered_map<const Area*, size_t> area_idx;
+  for (size_t i = 0; i < b.areas.size(); ++i) area_idx.emplace(b.areas[i].get(), i);
+  // an advertiser survives the reachability filter unless its area has a
+  // LinkState in which my SPF does not reach it
+  auto reached = [&](const std::pair<const NodeArea, Entry>& kv) {
+    Area* a = b.area_of(kv.first.second);
+    if (!a) return true;
+    return mine[area_idx.at(a)]->find(a->id(kv)) >= 0;
+  };
   for (const auto& [prefix, all] : ps->prefixes) {
-    // entries of nodes unreachable in their own area dropped (:409-420)
-    Entries ents = all;
-    for (size_t i = 0; i < b.areas.size(); ++i) {
-      Area& a = *b.areas[i];
-      for (auto it = ents.begin(); it != ents.end();) {
-        if (a.name != it->first.second || mine[i]->find(a.id(it->first.first)) >= 0) ++it;
-        else it = ents.erase(it);
+    // entries of nodes unreachable in their own area dropped (:409-420): the
+    // copy's erasures keep the survivors' order; no copy when none drops
+    std::unique_ptr<Entries> own;
+    const Entries* ep = &all;
+    for (const auto& kv : all)
+      if (!reached(kv)) {
+        own = std::make_unique<Entries>(all);
+        for (auto it = own->begin(); it != own->end();) {
+          if (reached(*it)) ++it;
+          else it = own->erase(it);
+        }
+        ep = own.get();
+        break;
       }
-    }
+    const Entries& ents = *ep;
     if (ents.empty()) {
       s->bump("decision.no_route_to_prefix");
       continue;
@@ -1043,27 +1143,24 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     }
     auto sel = b.select_best(ents, has_bgp);
     if (!b.ok()) return b.st;
-    BestRoute res = std::move(*sel);
-    if (!res.success) continue;
-    if (res.all.empty()) {
+    if (!sel->success) continue;
+    if (sel->all.empty()) {
       s->bump("decision.no_route_to_prefix");
       continue;
     }
-    s->best_cache[prefix] = res;
+    // bestRoutesCache_ (its refs point into this build's entries: cleared below)
+    const BestRoute& res = s->best_cache[prefix] = std::move(*sel);
     if (res.has_node(me) && !self_prepend) continue;  // self-advertised
     // getPrefixForwardingTypeAndAlgorithm (Util.cpp:617-643)
     uint8_t ftype = DC_FWD_SR_MPLS, falgo = DC_ALGO_KSP2_ED_ECMP;
-    {
-      std::set<NodeArea> best(res.all.begin(), res.all.end());
-      for (const auto& [na, e] : ents) {
-        if (!best.count(na)) continue;
-        ftype = std::min(ftype, e.ftype);
-        falgo = std::min(falgo, e.falgo);
-        if (ftype == DC_FWD_IP && falgo == DC_ALGO_SP_ECMP) break;
-      }
+    for (const auto& kv : ents) {  // (walked in map order, as the reference)
+      if (std::find(res.refs.begin(), res.refs.end(), &kv) == res.refs.end()) continue;
+      ftype = std::min(ftype, kv.second.ftype);
+      falgo = std::min(falgo, kv.second.falgo);
+      if (ftype == DC_FWD_IP && falgo == DC_ALGO_SP_ECMP) break;
     }
     if (single && falgo == DC_ALGO_SP_ECMP && ftype == DC_FWD_IP) {
-      uni.push_back({&prefix, std::move(ents), std::move(res), has_bgp, v4});
+      uni.push_back({&prefix, ep, std::move(own), &res, has_bgp, v4});
       continue;
     }
     if (single && falgo == DC_ALGO_KSP2_ED_ECMP && !ksp_fetched) {
@@ -1077,9 +1174,15 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     if (!b.ok()) return b.st;
   }
 
+  phase(1);
   // ---- node labels (:583-664) ----
   // label -> (node, area), the collision rule of :605-617 (the smaller name wins)
-  std::unordered_map<int32_t, std::pair<std::string, Area*>> label_to_node;
+  struct LabelOwner {
+    uint32_t node;  // name id in `area`
+    Area* area;
+    std::string name() const { return ls_name(area->ls, node); }
+  };
+  std::unordered_map<int32_t, LabelOwner> label_to_node;
   std::vector<int32_t> label_order;
   for (auto& ap : b.areas) {
     Area& a = *ap;
@@ -1088,17 +1191,15 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     std::vector<uint32_t> ids(n);
     std::vector<int32_t> lab(n);
     ls_adjacency_databases(a.ls, ids.data(), lab.data(), n, &n);
+    label_to_node.reserve(label_to_node.size() + n);
     for (uint32_t i = 0; i < n; ++i) {
       const int32_t top = lab[i];
       if (top == 0 || !mpls_label_valid(top)) continue;
-      const std::string node = a.name_of(ids[i]);
-      auto it = label_to_node.find(top);
-      if (it != label_to_node.end()) {
-        if (it->second.first < node) continue;
-        it->second = {node, &a};
-      } else {
-        label_to_node.emplace(top, std::make_pair(node, &a));
+      auto [it, fresh] = label_to_node.emplace(top, LabelOwner{ids[i], &a});
+      if (fresh) {
         label_order.push_back(top);
+      } else if (!(std::strcmp(ls_name(it->second.area->ls, it->second.node), ls_name(a.ls, ids[i])) < 0)) {
+        it->second = {ids[i], &a};  // the collision's smaller name wins (a tie: the later area)
       }
     }
   }
@@ -1109,23 +1210,25 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     GraphCache* g = nullptr;
     if (const spf_status c = graph_cache(s, a.ls, g); c != SPF_OK) return c;
     std::vector<uint32_t> set_ptr{0}, set_nodes;
-    auto add_node = [&](const std::string& n) {
-      const uint32_t id = a.id(n);
+    set_ptr.reserve(uni.size() + label_order.size() + 1);
+    set_nodes.reserve(uni.size() + label_order.size());
+    auto add_node = [&](uint32_t id) {
       if (id < g->csr_of.size() && g->csr_of[id] != ~0u) set_nodes.push_back(g->csr_of[id]);
     };
     for (const Uni& u : uni) {
-      for (const auto& na : u.res.all) add_node(na.first);
+      for (EntryRef r : u.res->refs) add_node(a.id(*r));
       set_ptr.push_back((uint32_t)set_nodes.size());
     }
     std::vector<int32_t> lab_routes;  // labels needing a selection, in set order
     for (int32_t top : label_order) {
-      const auto& [node, area] = label_to_node.at(top);
-      if (node == me) continue;
+      const LabelOwner& o = label_to_node.at(top);
+      if (o.node == a.me_id) continue;
       lab_routes.push_back(top);
-      add_node(node);
+      add_node(o.node);
       set_ptr.push_back((uint32_t)set_nodes.size());
     }
     const uint32_t n_sets = (uint32_t)set_ptr.size() - 1;
+    phase(2);
     Selection sel;
     const uint32_t m = a.me_id < g->csr_of.size() ? g->csr_of[a.me_id] : ~0u;
     if (m != ~0u && n_sets) {
@@ -1153,15 +1256,36 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     } else {
       sel.cnt.assign(n_sets, 0);
     }
-    // me's up links by CSR edge (the selection's edges), fields once
-    std::unordered_map<uint32_t, const MyLink*> by_link;
-    for (const MyLink& l : b.links(a)) by_link.emplace(l.id, &l);
-    auto edge_link = [&](uint32_t e) -> const MyLink* {
-      auto it = by_link.find(g->link_id[e]);
-      return it == by_link.end() ? nullptr : it->second;
+    phase(3);
+    // me's links by link id (the selection's edges), and each link's
+    // createNextHop record with its strings interned once
+    struct LinkRec {
+      const MyLink* l;
+      uint32_t nb_id;
+      dc_nexthop v4, v6;
     };
-    // IP routes: equal selections share one record range
-    std::map<std::tuple<std::vector<uint32_t>, std::vector<uint64_t>, bool>, std::vector<NH>> shared;
+    std::unordered_map<uint32_t, LinkRec> by_link;
+    for (const MyLink& l : b.links(a)) {
+      LinkRec r{&l, a.id(l.nb), {}, {}};
+      r.v6.address_len = 16;
+      std::memcpy(r.v6.address, l.v6.data(), 16);
+      r.v4.address_len = 4;
+      std::memcpy(r.v4.address, l.v4.data(), 4);
+      for (dc_nexthop* x : {&r.v4, &r.v6}) {
+        x->ifname = db->intern(l.ifname);
+        x->area = db->intern(a.name);
+        x->neighbor = db->intern(l.nb);
+      }
+      by_link.emplace(l.id, r);
+    }
+    auto edge_rec = [&](uint32_t e) -> const LinkRec* {
+      auto it = by_link.find(g->link_id[e]);
+      return it == by_link.end() ? nullptr : &it->second;
+    };
+    // IP routes: equal selections (edges, metrics, family) share one record range
+    std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> shared;
+    std::vector<dc_nexthop> recs;
+    std::string key;
     for (uint32_t i = 0; i < uni.size(); ++i) {
       const Uni& u = uni[i];
       const uint32_t c = sel.cnt[i];
@@ -1170,32 +1294,60 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
         continue;
       }
       const size_t o = (size_t)i * sel.deg;
-      auto key = std::make_tuple(std::vector<uint32_t>(sel.edge.begin() + o, sel.edge.begin() + o + c),
-                                 std::vector<uint64_t>(sel.metric.begin() + o, sel.metric.begin() + o + c),
-                                 u.v4);
-      auto it = shared.find(key);
-      if (it == shared.end()) {
+      if (u.res->has_node(me)) {  // self-advertised with a prepend label: addBestPaths' static hops
         std::vector<NH> v;
         for (uint32_t q = 0; q < c; ++q) {
-          const MyLink* l = edge_link(sel.edge[o + q]);
-          if (!l) return sfail(s, SPF_E_INVALID, "selected edge %u is not a link of %s", sel.edge[o + q], me.c_str());
-          v.push_back(b.link_nh(*l, a, u.v4, sel.metric[o + q]));
+          const LinkRec* r = edge_rec(sel.edge[o + q]);
+          if (!r) return sfail(s, SPF_E_INVALID, "selected edge %u is not a link of %s", sel.edge[o + q], me.c_str());
+          v.push_back(b.link_nh(*r->l, a, u.v4, sel.metric[o + q]));
         }
-        it = shared.emplace(std::move(key), std::move(v)).first;
+        b.add_best_paths(*u.prefix, *u.res, *u.ents, u.bgp, std::move(v));
+        if (!b.ok()) return b.st;
+        continue;
       }
-      b.add_best_paths(*u.prefix, u.res, u.ents, u.bgp, it->second);
-      if (!b.ok()) return b.st;
+      key.assign(reinterpret_cast<const char*>(sel.edge.data() + o), 4ull * c);
+      key.append(reinterpret_cast<const char*>(sel.metric.data() + o), 8ull * c);
+      key.push_back(u.v4 ? 1 : 0);
+      auto it = shared.find(key);
+      if (it == shared.end()) {
+        recs.clear();
+        for (uint32_t q = 0; q < c; ++q) {
+          const LinkRec* r = edge_rec(sel.edge[o + q]);
+          if (!r) return sfail(s, SPF_E_INVALID, "selected edge %u is not a link of %s", sel.edge[o + q], me.c_str());
+          dc_nexthop x = u.v4 ? r->v4 : r->v6;
+          x.metric = i32_metric(sel.metric[o + q]);
+          recs.push_back(x);
+        }
+        it = shared.emplace(key, db->add_records(recs)).first;
+      }
+      // addBestPaths (:1020-1080), one remote advertiser set: the min-nexthop check
+      std::optional<int64_t> need;
+      EntryRef best = nullptr;
+      for (EntryRef r : u.res->refs) {
+        const Entry& e = r->second;
+        if (e.min_nexthop && (!need || *e.min_nexthop > *need)) need = e.min_nexthop;
+        if (r->first == *u.res->best) best = r;
+      }
+      if (need && *need > (int64_t)(it->second.second - it->second.first)) continue;
+      if (best && best->first.second == a.name) {  // strings from the per-name cache
+        if (a.area_sid == DC_NONE) a.area_sid = db->intern(a.name);
+        db->uni.insert(db->uni.end(), {db->push_unique(*u.prefix), a.sid(db.get(), a.id(*best), best->first.first),
+                                       a.area_sid, (uint32_t)(u.bgp && s->bgp_dry_run), it->second.first,
+                                       it->second.second});
+      } else {  // (the drained filter kept an unfiltered bestNodeArea)
+        db->add_unicast(*u.prefix, *u.res->best, u.bgp && s->bgp_dry_run, it->second);
+      }
     }
     // node-label routes
     uint32_t k = (uint32_t)uni.size();
     std::unordered_map<int32_t, uint32_t> label_set;
     for (int32_t top : lab_routes) label_set.emplace(top, k++);
     for (int32_t top : label_order) {
-      const auto& [node, area] = label_to_node.at(top);
-      if (node == me) {
+      const LabelOwner& own = label_to_node.at(top);
+      if (own.node == a.me_id) {
         NH h;  // POP_AND_LOOKUP, address "::"
         h.action = DC_MPLS_POP_AND_LOOKUP;
-        h.area = area->name;
+        h.area = own.area->name;
         std::vector<NH> v{h};
         db->add_mpls(top, db->add_set(v));
         continue;
@@ -1207,33 +1359,35 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
         continue;
       }
       const size_t o = (size_t)i * sel.deg;
-      std::vector<NH> v;
+      recs.clear();
       for (uint32_t q = 0; q < c; ++q) {
-        const MyLink* l = edge_link(sel.edge[o + q]);
-        if (!l) return sfail(s, SPF_E_INVALID, "selected edge %u is not a link of %s", sel.edge[o + q], me.c_str());
-        NH h = b.link_nh(*l, a, false, sel.metric[o + q]);
-        if (l->nb == node) {
-          h.action = DC_MPLS_PHP;
+        const LinkRec* r = edge_rec(sel.edge[o + q]);
+        if (!r) return sfail(s, SPF_E_INVALID, "selected edge %u is not a link of %s", sel.edge[o + q], me.c_str());
+        dc_nexthop x = r->v6;
+        x.metric = i32_metric(sel.metric[o + q]);
+        if (r->nb_id == own.node) {
+          x.mpls_action = DC_MPLS_PHP;
         } else {
-          h.action = DC_MPLS_SWAP;
-          h.swap = top;
+          x.mpls_action = DC_MPLS_SWAP;
+          x.swap_label = top;
         }
-        v.push_back(std::move(h));
+        recs.push_back(x);
       }
-      db->add_mpls(top, db->add_set(v));
+      db->add_mpls(top, db->add_records(recs));
     }
   } else {
     for (int32_t top : label_order) {
-      const auto& [node, area] = label_to_node.at(top);
+      const LabelOwner& own = label_to_node.at(top);
+      const std::string node = own.name();
       if (node == me) {
         NH h;
         h.action = DC_MPLS_POP_AND_LOOKUP;
-        h.area = area->name;
+        h.area = own.area->name;
         std::vector<NH> v{h};
         db->add_mpls(top, db->add_set(v));
         continue;
       }
-      const std::vector<NodeArea> dst{{node, area->name}};
+      const std::vector<NodeArea> dst{{node, own.area->name}};
       auto [mn, nhn] = b.nexthops_with_metric(dst, false);
       if (!b.ok()) return b.st;
       if (nhn.empty()) {
@@ -1246,6 +1400,7 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     }
   }
 
+  phase(4);
   // ---- adjacency labels of every area (:667-698) ----
   for (auto& ap : b.areas) {
     Area& a = *ap;
@@ -1263,8 +1418,14 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     std::vector<NH> v = nhs;
     db->add_mpls(top, db->add_set(v));
   }
+  for (auto& kv : s->best_cache) kv.second.refs.clear();  // (they pointed into this build)
+  phase(5);
   *out = db.release();
   return SPF_OK;
+}
+
+void dc_debug_phase_ns(const dc_solver* s, uint64_t* out) {
+  for (int i = 0; i < 6; ++i) out[i] = s ? s->phase_ns[i] : 0;
 }
 
 void dc_route_db_destroy(dc_route_db* db) { delete db; }

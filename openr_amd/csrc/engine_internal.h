@@ -167,6 +167,16 @@ struct spf_ctx {
   // spf_plan_preds' pinned staging: lives with the context (the facade makes
   // a plan per query; pinning per plan cost more than it saved)
   spfi::PinBuf<uint32_t> pin_preds;
+  // spf_routes' (routes.hip) last plan, kept while its sources and the graph
+  // shape hold (executes re-derive it after in-place patches), and its
+  // buffers, which only grow: a route build per publication allocates nothing
+  struct RouteCache {
+    spf_plan* plan = nullptr;
+    std::vector<uint32_t> srcs;
+    uint64_t shape = ~0ull;
+    spfi::DevBuf<uint32_t> dist, nh, ecol, ew, ej, sp, sn, cnt, edge;
+    spfi::DevBuf<uint64_t> mn, metric;
+  } rt;
 };
 
 struct spf_plan {

@@ -288,10 +288,19 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
   const uint32_t nb0 = c->nb_ptr[me], k = c->nb_ptr[me + 1] - nb0;
   if (lfa)
     for (uint32_t j = 0; j < k; ++j) srcs.push_back(c->nb_id[nb0 + j]);
-  spf_plan* raw = nullptr;
-  spf_status st = spf_plan_create(c, srcs.data(), (uint32_t)srcs.size(), 0, &raw);
-  if (st != SPF_OK) return st;
-  std::unique_ptr<spf_plan, void (*)(spf_plan*)> p(raw, spf_plan_destroy);
+  // the previous call's plan when it solved the same sources on this graph
+  // shape (a route build per publication: me and its neighbours again)
+  spf_ctx::RouteCache& rc = c->rt;
+  spf_status st = SPF_OK;
+  if (!rc.plan || rc.shape != c->shape || rc.srcs != srcs) {
+    spf_plan_destroy(rc.plan);
+    rc.plan = nullptr;
+    st = spf_plan_create(c, srcs.data(), (uint32_t)srcs.size(), 0, &rc.plan);
+    if (st != SPF_OK) return st;
+    rc.srcs = srcs;
+    rc.shape = c->shape;
+  }
+  spf_plan* p = rc.plan;
   // me's up links in linksFromNode order, with the bitmap index of their far end
   const uint32_t e0 = c->row_ptr[me], deg = c->row_ptr[me + 1] - e0;
   std::vector<uint32_t> ecol(deg), ew(deg), ej(deg);
@@ -301,10 +310,19 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
     const uint32_t* f = std::lower_bound(c->nb_id.data() + nb0, c->nb_id.data() + nb0 + k, ecol[i]);
     ej[i] = (uint32_t)(f - (c->nb_id.data() + nb0));
   }
-  DevBuf<uint32_t> d_dist, d_nh, d_ecol, d_ew, d_ej, d_sp, d_sn, d_cnt, d_edge;
-  DevBuf<uint64_t> d_min, d_metric;
+  auto& d_dist = rc.dist;
+  auto& d_nh = rc.nh;
+  auto& d_ecol = rc.ecol;
+  auto& d_ew = rc.ew;
+  auto& d_ej = rc.ej;
+  auto& d_sp = rc.sp;
+  auto& d_sn = rc.sn;
+  auto& d_cnt = rc.cnt;
+  auto& d_edge = rc.edge;
+  auto& d_min = rc.mn;
+  auto& d_metric = rc.metric;
   HIP_TRY(c, d_dist.alloc((size_t)srcs.size() * c->pitch));
-  HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(1, spf_plan_nh_words(p.get()))));
+  HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(1, spf_plan_nh_words(p))));
   HIP_TRY(c, d_ecol.upload(ecol.data(), deg, c->stream));
   HIP_TRY(c, d_ew.upload(ew.data(), deg, c->stream));
   HIP_TRY(c, d_ej.upload(ej.data(), deg, c->stream));
@@ -315,7 +333,7 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
   HIP_TRY(c, d_cnt.alloc(std::max<uint32_t>(1, n_sets)));
   HIP_TRY(c, d_edge.alloc(cap));
   HIP_TRY(c, d_metric.alloc(cap));
-  st = spf_plan_execute(p.get(), d_dist.p, d_nh.p, c->stream);
+  st = spf_plan_execute(p, d_dist.p, d_nh.p, c->stream);
   if (st != SPF_OK) return st;
   // the plan's D rows: the caller buffer when the source set is closed,
   // otherwise the plan's own closure rows

@@ -1678,6 +1678,9 @@ void spf_ctx_destroy(spf_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   spfi::resident_forget(c);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  spf_plan_destroy(c->rt.plan);  // spf_routes' cached plan, before its context goes
+  c->rt.plan = nullptr;
   if (c->stream) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);

@@ -450,7 +450,9 @@ class LinkState(N.NativeHandle):
         import numpy as np
 
         lid = self._csr_link_ids()
-        key = (len(lid), int(lid.max()) if len(lid) else -1, N.lib.ls_num_links(self._h))
+        # keyed on the flattened graph's epoch: a link id freed and reused by
+        # another link changes the structure, hence the epoch
+        key = int(N.lib.ls_graph_epoch(self._h))
         if getattr(self, "_lh_key", None) == key and self._lh is not None:
             return self._lh
         lh = np.zeros(max(1, int(lid.max()) + 1 if len(lid) else 1), np.uint64)
