@@ -1164,6 +1164,61 @@ class FacadeRouteBuild:
                           f"(oracle/spf_oracle.cpp)"}
 
 
+class FacadeFlapRouteBuild(FacadeRouteBuild):
+    """CS-1 with a link flap (Overview.md:26, "local failures in under
+    100ms"): per step rack switch 3-1-0 publishes its adjacency database
+    with one uplink withdrawn, and on the next step with it advertised again
+    -- the link leaves linksFromNode and comes back (LinkState.cpp:564-719) --
+    then SpfSolver.buildRouteDb(me) with LFA.  The publication patches the
+    engine's CSR rows in place (dead slots, spf_graph_patch_rows): the line
+    reports the graph reloads (0) and row patches of the timed steps."""
+
+    def __init__(self, name: str, rank: int, world: int, dev, eng_cls, graph_from_lsdb):
+        super().__init__(name, rank, world, dev, eng_cls, graph_from_lsdb)
+        self.desc = ("fabric_full numOfSws=10000; me = rack switch 3-0-0, LFA on; a v6 loopback "
+                     "and a node label per node; per step one publication of rack switch 3-1-0 "
+                     "withdrawing (odd steps: re-advertising) its first uplink, then "
+                     "SpfSolver.buildRouteDb(me)")
+        self.held = None
+
+    def step(self) -> None:
+        import copy
+
+        t0 = time.perf_counter()
+        if self.held is None:
+            self.held = self.victim.adjacencies.pop(0)
+        else:
+            self.victim.adjacencies.insert(0, self.held)
+            self.held = None
+        self.ls.updateAdjacencyDatabase(copy.copy(self.victim))
+        t1 = time.perf_counter()
+        ndb = self.solver.buildRouteDbNative(self.me, {self.ls.getArea(): self.ls}, self.ps)
+        t2 = time.perf_counter()
+        self.routes = ndb.unicastCount() + ndb.mplsCount()
+        self.nexthops = len(ndb.nexthopRecords())
+        ndb.close()
+        self.pub.append(t1 - t0)
+        self.build.append(t2 - t1)
+
+    def enable_timing(self, k: int) -> None:
+        from openr_amd import _native as N
+        from openr_amd.engine import SpfEngine
+
+        super().enable_timing(k)
+        self.loads0 = SpfEngine(handle=self.ls.engine_handle()).loads
+        self.patches0 = int(N.lib.ls_debug_row_patches(self.ls._h))
+
+    def kernel_ms(self):
+        from openr_amd import _native as N
+        from openr_amd.engine import SpfEngine
+
+        out = super().kernel_ms()
+        self.phase_ms["graph_reloads_in_timed_steps"] = int(
+            SpfEngine(handle=self.ls.engine_handle()).loads - self.loads0)
+        self.phase_ms["row_patches_in_timed_steps"] = int(N.lib.ls_debug_row_patches(self.ls._h)) - self.patches0
+        return out
+
+
 def host_cores() -> int:
     sys.path.insert(0, str(ROOT / "tests"))
     from oracle import host_threads
@@ -1174,7 +1229,8 @@ def host_cores() -> int:
 WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
              "fabric_rtt": AllSources,
              "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks, "fabric_lfa": FacadeLfa,
-             "fabric_routes": RoutesAllNodes, "fabric_lfa_routes": FacadeRouteBuild}
+             "fabric_routes": RoutesAllNodes, "fabric_lfa_routes": FacadeRouteBuild,
+             "fabric_flap_routes": FacadeFlapRouteBuild}
 
 
 def _pmc_kernels(workload: str, kernels):
@@ -1401,6 +1457,8 @@ def main() -> None:
             if isinstance(wl, FacadeLfa) else
             "getDecisionRouteDb for every node (all-sources SPF + route selection) per sec, 10k fabric"
             if isinstance(wl, RoutesAllNodes) else
+            "link-flap publication + SpfSolver.buildRouteDb(me) with LFA per sec, 10k fabric"
+            if isinstance(wl, FacadeFlapRouteBuild) else
             "publication + SpfSolver.buildRouteDb(me) with LFA per sec, 10k fabric"
             if isinstance(wl, FacadeRouteBuild) else
             "what-if single-link-failure SPF reruns/sec, 1M-link scale-free graph"),

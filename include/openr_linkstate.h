@@ -187,12 +187,20 @@ uint64_t ls_spf_runs(const ls_state* ls);
 spf_ctx* ls_engine(ls_state* ls);
 spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges);
 /* Version of the flattened CSR structure (node ids, row_ptr, col, link ids):
- * changes whenever ls_flatten rebuilds it, not when it patches metrics or
- * overload bits in place.  Callers caching per-graph tables key them on it. */
+ * changes whenever ls_flatten rebuilds it or rewrites rows in place (a link
+ * down or up), not when it patches metrics or overload bits.  Callers caching per-graph tables key them on it. */
 uint64_t ls_graph_epoch(const ls_state* ls);
 /* A process-unique id of the state (never reused, unlike its address): name
  * ids (ls_name_id) are stable per state, so callers may cache them by it. */
 uint64_t ls_serial(const ls_state* ls);
+/* Flattens since creation that patched rows in place (a link down / up, an
+ * adjacency withdrawn / advertised again) instead of reloading the graph
+ * (diagnostics; spf_graph_loads counts the reloads). */
+uint64_t ls_debug_row_patches(const ls_state* ls);
+/* Flattens since creation that patched rows in place (a link down / up, an
+ * adjacency withdrawn / advertised again) instead of reloading the graph
+ * (diagnostics; spf_graph_loads counts the reloads). */
+uint64_t ls_debug_row_patches(const ls_state* ls);
 spf_status ls_graph_node_names(ls_state* ls, uint32_t* name_ids /* [n_nodes] */);
 /* Copy of the flattened CSR (sizes from ls_flatten); any pointer may be NULL. */
 spf_status ls_graph_csr(ls_state* ls, uint32_t* row_ptr, uint32_t* col, int32_t* metric,

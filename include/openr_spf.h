@@ -73,9 +73,15 @@ typedef enum spf_status {
 typedef struct spf_ctx spf_ctx;
 typedef struct spf_plan spf_plan;
 
+/* Dead slots: an edge u -> u (a self-loop) with metric 1 stands for no edge
+ * -- a link of u that is down, or withdrawn, kept in place so that a later
+ * change of that link patches the row instead of reloading the graph
+ * (spf_graph_patch_rows).  Both slots of such a link are self-loops sharing
+ * its link id.  No kernel relaxes, pushes or pulls over one; they are not
+ * distinct neighbours and never next hops or pathLinks. */
 typedef struct spf_graph {
   uint32_t n_nodes;
-  uint32_t n_edges;             /* directed up edges                            */
+  uint32_t n_edges;             /* directed up edges (and dead slots)           */
   const uint32_t* row_ptr;      /* [n_nodes+1]                                  */
   const uint32_t* col;          /* [n_edges] head node of edge                  */
   const int32_t* metric;        /* [n_edges] metric advertised by the tail      */
@@ -111,6 +117,17 @@ spf_status spf_graph_set_overload(spf_ctx* ctx, const uint32_t* nodes, const uin
                                   uint32_t n);
 spf_status spf_graph_set_metric(spf_ctx* ctx, const uint32_t* edges, const int32_t* metric,
                                 uint32_t n);
+/* Rows of nodes[0..n) rewritten in place, each with its current length:
+ * col / metric / link hold the new rows back to back (a dead slot: col = the
+ * node, metric 1).  What a link going down or up, or an adjacency withdrawn
+ * and advertised again, does to the CSR (LinkState::updateAdjacencyDatabase,
+ * LinkState.cpp:564-719; Link::isUp, :233-236) when every link id keeps its
+ * two slots.  Reverse edges, distinct-neighbour lists and the kernels' tables
+ * are patched; plans re-derive on their next execute, except a plan one of
+ * whose sources gained or lost a distinct neighbour (its next-hop layout):
+ * that one returns SPF_E_STATE and must be recreated. */
+spf_status spf_graph_patch_rows(spf_ctx* ctx, const uint32_t* nodes, uint32_t n, const uint32_t* col,
+                                const int32_t* metric, const uint32_t* link);
 uint64_t spf_graph_epoch(const spf_ctx* ctx);
 /* Number of spf_graph_load calls so far (patches do not count). */
 uint64_t spf_graph_loads(const spf_ctx* ctx);
@@ -451,6 +468,8 @@ int spf_mctx_device(const spf_mctx* m, uint32_t i);
 spf_status spf_mctx_graph_load(spf_mctx* m, const spf_graph* g);
 spf_status spf_mctx_graph_set_overload(spf_mctx* m, const uint32_t* nodes,
                                        const uint8_t* overloaded, uint32_t n);
+spf_status spf_mctx_graph_patch_rows(spf_mctx* m, const uint32_t* nodes, uint32_t n,
+                                     const uint32_t* col, const int32_t* metric, const uint32_t* link);
 spf_status spf_mctx_graph_set_metric(spf_mctx* m, const uint32_t* edges, const int32_t* metric,
                                      uint32_t n);
 

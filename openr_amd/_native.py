@@ -186,6 +186,8 @@ PROTOTYPES = {
     "spf_graph_load": (C.c_int, [_vp, C.POINTER(SpfGraph)]),
     "spf_graph_set_overload": (C.c_int, [_vp, _u32p, _u8p, C.c_uint32]),
     "spf_graph_set_metric": (C.c_int, [_vp, _u32p, _i32p, C.c_uint32]),
+    "spf_graph_patch_rows": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _i32p, _u32p]),
+    "spf_mctx_graph_patch_rows": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _i32p, _u32p]),
     "spf_graph_epoch": (C.c_uint64, [_vp]),
     "spf_graph_loads": (C.c_uint64, [_vp]),
     "spf_row_pitch": (C.c_uint32, [_vp]),
@@ -342,6 +344,7 @@ PROTOTYPES = {
     "ls_graph_epoch": (C.c_uint64, [_vp]),
     "ls_get_spf_metrics": (C.c_int, [_vp, C.c_char_p, C.c_int, C.POINTER(LsSpfView)]),
     "ls_serial": (C.c_uint64, [_vp]),
+    "ls_debug_row_patches": (C.c_uint64, [_vp]),
     "ls_is_node_overloaded_id": (C.c_int, [_vp, C.c_uint32]),
     # SpfSolver / PrefixState (include/openr_decision.h)
     "dc_prefix_state_create": (_vp, []),

@@ -49,6 +49,12 @@ struct DevBuf {
     if (e != hipSuccess || count == 0) return e;
     return hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s);
   }
+  // h[off, off + count) into the allocated buffer at the same offset
+  hipError_t upload_at(const T* h, size_t off, size_t count, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (!p || off + count > n) return hipErrorInvalidValue;
+    return hipMemcpyAsync(p + off, h + off, count * sizeof(T), hipMemcpyHostToDevice, s);
+  }
 };
 
 // Pinned host staging (hipHostMalloc): device-to-host copies at PCIe rate
@@ -120,6 +126,11 @@ struct spf_ctx {
   uint64_t solves = 0;
   uint64_t shape = 0;  // bumped by spf_graph_load (CSR structure)
   uint64_t epoch = 0;  // bumped by every graph change (load or in-place patch)
+  // bumped when a patch changes some node's distinct-neighbour count (a
+  // plan's next-hop layout); plans of the old layout fail with SPF_E_STATE
+  uint64_t layout = 0;
+  // the two CSR slots of every link id (kInf: none), kept by spf_graph_patch_rows
+  std::vector<uint32_t> link_slot;
   // graph
   bool loaded = false;
   uint32_t N = 0, E = 0, pitch = 0;
@@ -142,6 +153,7 @@ struct spf_ctx {
   std::vector<uint32_t> sell4_ptr, sell4;  // packed u16x4 columns (uint2 entries), planes BFS
   spfi::DevBuf<uint32_t> d_sell4_ptr, d_sell4;
   spfi::DevBuf<uint32_t> d_row_ptr, d_col, d_wt, d_rev, d_nb_ptr, d_nb_id, d_nb_w;
+  std::vector<uint32_t> edge_nb;     // host copy of d_edge_nb (patched in place)
   spfi::DevBuf<uint32_t> d_edge_nb;  // per CSR edge: its head's index among the tail's distinct neighbours
   spfi::DevBuf<uint8_t> d_ovl;
   // scratch for spf_preds
@@ -183,6 +195,7 @@ struct spf_plan {
   spf_ctx* ctx = nullptr;
   uint32_t n_src = 0, flags = 0;
   uint64_t shape = 0, epoch = 0;  // graph state the plan was derived from
+  uint64_t layout = 0;             // c->layout its next-hop layout was taken at
   std::vector<uint32_t> srcs, closure;
   std::vector<uint64_t> nh_off;
   std::vector<uint32_t> words;

@@ -222,6 +222,20 @@ struct ls_state {
   std::unordered_map<uint32_t, Holdable<bool>> node_ovl;
   std::vector<std::unique_ptr<LinkObj>> slab;
   std::vector<uint32_t> free_ids;
+  // link ids holding slots of the flattened CSR (in_csr) are not reused until
+  // the next full flatten: a withdrawn link leaves a dead slot under its id
+  // (ghost), and gets the same id -- the same slots -- when it comes back
+  std::vector<uint8_t> in_csr;
+  std::map<OrderedNames, uint32_t> ghost;
+  uint64_t row_patches = 0;  // flattens that patched rows in place (ls_debug_row_patches)
+  // nodes whose links changed since the last flatten (the rows a patch
+  // rewrites); touched_all: unknown, every row is compared
+  std::vector<uint32_t> touched;
+  bool touched_all = true;
+  void touch(const LinkObj* l) {
+    touched.push_back(l->s[0].node);
+    touched.push_back(l->s[1].node);
+  }
 
   // flattened graph
   bool dirty = true;                 // links changed: re-flatten (patch or reload)
@@ -294,6 +308,11 @@ spf_status eng_set_overload(ls_state* ls, const uint32_t* nodes, const uint8_t* 
   return ls->meng ? spf_mctx_graph_set_overload(ls->meng, nodes, v, n)
                   : spf_graph_set_overload(ls->eng, nodes, v, n);
 }
+spf_status eng_patch_rows(ls_state* ls, const uint32_t* nodes, uint32_t n, const uint32_t* col,
+                          const int32_t* m, const uint32_t* link) {
+  return ls->meng ? spf_mctx_graph_patch_rows(ls->meng, nodes, n, col, m, link)
+                  : spf_graph_patch_rows(ls->eng, nodes, n, col, m, link);
+}
 spf_status eng_set_metric(ls_state* ls, const uint32_t* edges, const int32_t* m, uint32_t n) {
   return ls->meng ? spf_mctx_graph_set_metric(ls->meng, edges, m, n)
                   : spf_graph_set_metric(ls->eng, edges, m, n);
@@ -357,7 +376,10 @@ std::unique_ptr<LinkObj> bidir(ls_state* ls, uint32_t node, const AdjIn& a) {
 
 LinkObj* adopt(ls_state* ls, std::unique_ptr<LinkObj> l) {
   uint32_t id;
-  if (!ls->free_ids.empty()) {
+  if (auto g = ls->ghost.find(l->names); g != ls->ghost.end()) {  // back in its old slots
+    id = g->second;
+    ls->ghost.erase(g);
+  } else if (!ls->free_ids.empty()) {
     id = ls->free_ids.back();
     ls->free_ids.pop_back();
   } else {
@@ -371,8 +393,9 @@ LinkObj* adopt(ls_state* ls, std::unique_ptr<LinkObj> l) {
 
 void release(ls_state* ls, LinkObj* l) {
   const uint32_t id = l->id;
+  if (id < ls->in_csr.size() && ls->in_csr[id]) ls->ghost[l->names] = id;  // keeps its slots
+  else ls->free_ids.push_back(id);
   ls->slab[id].reset();
-  ls->free_ids.push_back(id);
 }
 
 bool add_link(ls_state* ls, LinkObj* l) {
@@ -428,6 +451,7 @@ spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric do
     if (i < fresh.size() && (j == old_links.size() || fresh[i]->before(*old_links[j]))) {
       fresh[i]->hold_up = up;
       topo |= fresh[i]->up();
+      ls->touch(fresh[i].get());
       LinkObj* l = adopt(ls, std::move(fresh[i]));
       if (!add_link(ls, l))
         return lfail(ls, SPF_E_INVALID, "duplicate link while adding adjacency of %s",
@@ -438,6 +462,7 @@ spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric do
     if (j < old_links.size() && (i == fresh.size() || old_links[j]->before(*fresh[i]))) {
       LinkObj* l = old_links[j];
       topo |= l->up();
+      ls->touch(l);
       ls->link_map.at(first_node(ls, *l)).erase(l);
       ls->link_map.at(second_node(ls, *l)).erase(l);
       ls->all_links.erase(l);
@@ -450,8 +475,10 @@ spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric do
     const Side& n = fresh[i]->from(node);
     if (n.metric.get() != o.metric.get()) {
       topo |= o.metric.update(n.metric.get(), up, down);
+      ls->touch(old_links[j]);
     }
     if (n.overload.get() != o.overload.get()) {
+      ls->touch(old_links[j]);
       const bool was_up = old_links[j]->up();
       o.overload.update(n.overload.get(), up, down);
       topo |= was_up != old_links[j]->up();
@@ -507,68 +534,167 @@ spf_status flatten(ls_state* ls) {
     return SPF_OK;
   }
   ls->pending_ovl.clear();
-  // keep the flattened graph the engine holds, to patch it if only metrics
-  // and overload bits differ
-  const std::vector<uint32_t> old_name = ls->csr_name, old_rp = ls->row_ptr, old_col = ls->col,
-                              old_lid = ls->link_id;
-  const std::vector<int32_t> old_metric = ls->metric;
-  const std::vector<uint8_t> old_ovl = ls->ovl;
   std::vector<uint32_t> ids;
   ids.reserve(ls->dbs.size());
   for (const auto& kv : ls->dbs) ids.push_back(kv.first);
   std::sort(ids.begin(), ids.end(),
             [&](uint32_t a, uint32_t b) { return ls->names[a] < ls->names[b]; });
+  const uint32_t N = (uint32_t)ids.size();
+  // Every link of a node -- up or down -- has a slot in its row, in
+  // linksFromNode order; a down link's slot is dead (a self-loop of metric 1,
+  // openr_spf.h), so a link going down or up changes the row in place.  A
+  // withdrawn link keeps dead slots under its id (ghost) until the next full
+  // flatten.  When every node's links still fit the slots of its row (no new
+  // link identity), the changed rows are patched (spf_graph_patch_rows,
+  // spf_graph_set_metric, spf_graph_set_overload); otherwise the graph reloads.
+  auto slot_of = [&](const LinkObj* l, uint32_t u_name, uint32_t& col, int32_t& met) {
+    if (l->up()) {
+      col = ls->csr_of[l->other(u_name)];
+      met = (int32_t)(uint32_t)l->from(u_name).metric.get();
+    } else {
+      col = ls->csr_of[u_name];
+      met = 1;
+    }
+  };
+  if (N > 0 && ls->eng && ls->engine_loaded && ids == ls->csr_name) {
+    bool fits = true;
+    std::vector<uint32_t> new_col(ls->col), new_lid(ls->link_id);
+    std::vector<int32_t> new_met(ls->metric);
+    std::vector<uint8_t> new_ovl(N);
+    for (uint32_t u = 0; u < N; ++u) new_ovl[u] = node_overloaded(ls, ids[u]);
+    // the rows to rebuild: the touched nodes' (every row when unknown)
+    std::vector<uint32_t> cand;
+    if (ls->touched_all) {
+      cand.resize(N);
+      std::iota(cand.begin(), cand.end(), 0u);
+    } else {
+      for (uint32_t nm : ls->touched)
+        if (nm < ls->csr_of.size() && ls->csr_of[nm] != kNone) cand.push_back(ls->csr_of[nm]);
+      std::sort(cand.begin(), cand.end());
+      cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+    }
+    std::vector<uint8_t> used;
+    for (uint32_t u : cand) {
+      if (!fits) break;
+      const uint32_t nm = ids[u];
+      const uint32_t b = ls->row_ptr[u], e = ls->row_ptr[u + 1];
+      uint32_t k = b;
+      used.assign(e - b, 0);
+      auto it = ls->link_map.find(nm);
+      if (it != ls->link_map.end())
+        for (const LinkObj* l : it->second) {
+          uint32_t at = e;  // this link's slot in the old row
+          for (uint32_t q = b; q < e; ++q)
+            if (ls->link_id[q] == l->id && !used[q - b]) {
+              at = q;
+              break;
+            }
+          const uint32_t o = l->other(nm);
+          if (at == e || k == e || o >= ls->csr_of.size() || ls->csr_of[o] == kNone) {
+            fits = false;  // a new link, or more links than slots: reload
+            break;
+          }
+          used[at - b] = 1;
+          slot_of(l, nm, new_col[k], new_met[k]);
+          new_lid[k++] = l->id;
+        }
+      for (uint32_t q = b; q < e && fits; ++q)  // the withdrawn links' dead slots, in their old order
+        if (!used[q - b]) {
+          new_col[k] = u;
+          new_met[k] = 1;
+          new_lid[k++] = ls->link_id[q];
+        }
+    }
+    if (fits) {
+      std::vector<uint32_t> rows, rcol, rlid, medges, onodes;
+      std::vector<int32_t> rmet, mmet;
+      std::vector<uint8_t> ovals;
+      for (uint32_t u = 0; u < N; ++u)
+        if (new_ovl[u] != ls->ovl[u]) {
+          onodes.push_back(u);
+          ovals.push_back(new_ovl[u]);
+        }
+      for (uint32_t u : cand) {
+        const uint32_t b = ls->row_ptr[u], e = ls->row_ptr[u + 1];
+        bool structural = false;
+        for (uint32_t q = b; q < e; ++q) structural |= new_col[q] != ls->col[q] || new_lid[q] != ls->link_id[q];
+        if (structural) {
+          rows.push_back(u);
+          rcol.insert(rcol.end(), new_col.begin() + b, new_col.begin() + e);
+          rmet.insert(rmet.end(), new_met.begin() + b, new_met.begin() + e);
+          rlid.insert(rlid.end(), new_lid.begin() + b, new_lid.begin() + e);
+        } else {
+          for (uint32_t q = b; q < e; ++q)
+            if (new_met[q] != ls->metric[q]) {
+              medges.push_back(q);
+              mmet.push_back(new_met[q]);
+            }
+        }
+      }
+      spf_status st = SPF_OK;
+      if (!rows.empty())
+        st = eng_patch_rows(ls, rows.data(), (uint32_t)rows.size(), rcol.data(), rmet.data(), rlid.data());
+      if (st == SPF_OK && !medges.empty())
+        st = eng_set_metric(ls, medges.data(), mmet.data(), (uint32_t)medges.size());
+      if (st == SPF_OK && !onodes.empty())
+        st = eng_set_overload(ls, onodes.data(), ovals.data(), (uint32_t)onodes.size());
+      if (st != SPF_OK) {
+        ls->engine_loaded = false;
+        return eng_fail(ls, st);
+      }
+      ls->col.swap(new_col);
+      ls->metric.swap(new_met);
+      ls->link_id.swap(new_lid);
+      ls->ovl.swap(new_ovl);
+      if (!rows.empty()) {
+        ++ls->row_patches;
+        static std::atomic<uint64_t> next_patch_epoch{1ull << 62};
+        ls->flat_epoch = ++next_patch_epoch;  // link ids / cols of rows moved (ls_graph_epoch)
+        if (ls->all) {  // the resident pass's layout may have changed: rebuilt on demand
+          spf_mplan_destroy(ls->all);
+          ls->all = nullptr;
+        }
+      }
+      ls->dirty = false;
+      ls->touched.clear();
+      ls->touched_all = false;
+      return SPF_OK;
+    }
+  }
+  ls->touched.clear();
+  ls->touched_all = false;
+  // full flatten: every link in a slot, no ghosts (their ids are free again)
+  for (const auto& g : ls->ghost) ls->free_ids.push_back(g.second);
+  ls->ghost.clear();
   ls->csr_name = ids;
   ls->csr_of.assign(ls->names.size(), kNone);
   for (uint32_t i = 0; i < ids.size(); ++i) ls->csr_of[ids[i]] = i;
-  const uint32_t N = (uint32_t)ids.size();
   ls->row_ptr.assign(N + 1, 0);
   ls->col.clear();
   ls->metric.clear();
   ls->link_id.clear();
   ls->edge_tail.clear();
   ls->ovl.assign(N, 0);
+  ls->in_csr.assign(ls->slab.size(), 0);
   for (uint32_t u = 0; u < N; ++u) {
     const uint32_t nm = ids[u];
     ls->ovl[u] = node_overloaded(ls, nm);
     auto it = ls->link_map.find(nm);
     if (it != ls->link_map.end()) {
       for (const LinkObj* l : it->second) {
-        if (!l->up()) continue;
         const uint32_t v = ls->csr_of[l->other(nm)];
         if (v == kNone) return lfail(ls, SPF_E_INVALID, "link to node without a database");
-        ls->col.push_back(v);
-        ls->metric.push_back((int32_t)(uint32_t)l->from(nm).metric.get());
+        uint32_t c;
+        int32_t m;
+        slot_of(l, nm, c, m);
+        ls->col.push_back(c);
+        ls->metric.push_back(m);
         ls->link_id.push_back(l->id);
         ls->edge_tail.push_back(u);
+        ls->in_csr[l->id] = 1;
       }
     }
     ls->row_ptr[u + 1] = (uint32_t)ls->col.size();
-  }
-  if (N > 0 && ls->eng && ls->engine_loaded && ls->csr_name == old_name &&
-      ls->row_ptr == old_rp && ls->col == old_col && ls->link_id == old_lid) {
-    // same CSR structure: patch metrics and overload bits in place
-    std::vector<uint32_t> edges, nodes;
-    std::vector<int32_t> mets;
-    std::vector<uint8_t> vals;
-    for (uint32_t e = 0; e < (uint32_t)ls->metric.size(); ++e)
-      if (ls->metric[e] != old_metric[e]) {
-        edges.push_back(e);
-        mets.push_back(ls->metric[e]);
-      }
-    for (uint32_t u = 0; u < N; ++u)
-      if (ls->ovl[u] != old_ovl[u]) {
-        nodes.push_back(u);
-        vals.push_back(ls->ovl[u]);
-      }
-    spf_status st = eng_set_metric(ls, edges.data(), mets.data(), (uint32_t)edges.size());
-    if (st == SPF_OK) st = eng_set_overload(ls, nodes.data(), vals.data(), (uint32_t)nodes.size());
-    if (st != SPF_OK) {
-      ls->engine_loaded = false;
-      return eng_fail(ls, st);
-    }
-    ls->dirty = false;
-    return SPF_OK;
   }
   ls->engine_loaded = false;
   // names, row_ptr, col or link ids changed: a process-wide counter, so no
@@ -1104,6 +1230,7 @@ spf_status ls_delete_adjacency_database(ls_state* ls, const char* node, ls_chang
   }
   ls->dbs.erase(n);
   ls->db_order_valid = false;
+  ls->touched_all = true;
   clear_memo(ls);
   put_change(change, true, false, false);
   return SPF_OK;
@@ -1112,7 +1239,11 @@ spf_status ls_delete_adjacency_database(ls_state* ls, const char* node, ls_chang
 spf_status ls_decrement_holds(ls_state* ls, ls_change* change) {
   if (!ls) return SPF_E_INVALID;
   bool topo = false;
-  for (LinkObj* l : ls->all_links) topo |= l->tick();
+  for (LinkObj* l : ls->all_links)
+    if (l->tick()) {
+      topo = true;
+      ls->touch(l);
+    }
   for (auto& kv : ls->node_ovl) topo |= kv.second.tick();
   if (topo) clear_memo(ls);
   put_change(change, topo, false, false);
@@ -1416,6 +1547,7 @@ spf_ctx* ls_engine(ls_state* ls) { return ls ? ls->eng : nullptr; }
 
 uint64_t ls_graph_epoch(const ls_state* ls) { return ls ? ls->flat_epoch : 0; }
 uint64_t ls_serial(const ls_state* ls) { return ls ? ls->serial : 0; }
+uint64_t ls_debug_row_patches(const ls_state* ls) { return ls ? ls->row_patches : 0; }
 
 spf_status ls_flatten(ls_state* ls, uint32_t* n_nodes, uint32_t* n_edges) {
   if (!ls) return SPF_E_INVALID;

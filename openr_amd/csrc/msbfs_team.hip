@@ -781,7 +781,8 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
       tab[p->tm_push_at + k] = (uint32_t)lst.size();
       for (uint32_t b = 0; b < p->tm_bs && k * p->tm_bs + b < rows; ++b) {
         const uint32_t src = p->closure[k * p->tm_bs + b];
-        for (uint32_t e = c->row_ptr[src]; e < c->row_ptr[src + 1]; ++e) lst.push_back(c->col[e] | (b << 24));
+        for (uint32_t e = c->row_ptr[src]; e < c->row_ptr[src + 1]; ++e)
+          if (c->col[e] != src) lst.push_back(c->col[e] | (b << 24));  // (not a dead slot)
       }
     }
     tab[p->tm_push_at + nbat] = (uint32_t)lst.size();

@@ -390,6 +390,17 @@ spf_status spf_mctx_graph_set_metric(spf_mctx* m, const uint32_t* edges, const i
   return SPF_OK;
 }
 
+spf_status spf_mctx_graph_patch_rows(spf_mctx* m, const uint32_t* nodes, uint32_t n,
+                                     const uint32_t* col, const int32_t* metric, const uint32_t* link) {
+  if (!m) return mfail(m, SPF_E_INVALID, "spf_mctx_graph_patch_rows: NULL context");
+  if (const spf_status st = drain_exec(m); st != SPF_OK) return st;
+  for (uint32_t i = 0; i < m->members.size(); ++i) {
+    const spf_status st = spf_graph_patch_rows(m->members[i], nodes, n, col, metric, link);
+    if (st != SPF_OK) return member_fail(m, i, st);
+  }
+  return SPF_OK;
+}
+
 spf_status spf_mplan_create(spf_mctx* m, const uint32_t* srcs, uint32_t n_src, uint32_t flags,
                             uint32_t mode, spf_mplan** out) {
   if (!m || !out || !srcs || n_src == 0 || mode > SPF_PARTITION_LOCALITY)

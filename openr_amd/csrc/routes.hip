@@ -52,8 +52,9 @@ __global__ __launch_bounds__(64) void routes_kernel(
       if (k < me_deg) {
         const uint32_t x = me_edges_col[k], j = me_edges_j[k];
         // shortest-path next hop: x in nextHops() of a min-cost member
+        // (j == kInf: a dead slot, no link)
         uint64_t val = kInf64;
-        for (uint32_t i = b; i < e; ++i) {
+        for (uint32_t i = b; i < e && j != kInf; ++i) {
           const uint32_t d = set_nodes[i];
           if (Dme[d] != shortest) continue;
           if ((nh[(size_t)j * wpm + (d >> 5)] >> (d & 31)) & 1u) {
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(64) void routes_kernel(
             break;
           }
         }
-        if (lfa) {  // loop-free alternate: d(x, dst) < shortest + d(x, me)
+        if (lfa && j != kInf) {  // loop-free alternate: d(x, dst) < shortest + d(x, me)
           const uint32_t* Dx = D + (size_t)row_of[x] * pitch;
           const uint64_t back = Dx[me];
           for (uint32_t i = b; i < e; ++i) {
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
     __syncthreads();  // the previous chunk's reads are done
     for (uint32_t t = threadIdx.x; t < nl; t += kRsThreads) {
       const uint32_t q = c0 + t, x = col[q];
-      const unsigned long long rx = lfa ? rowp[x] : 0ull;
+      const unsigned long long rx = lfa && x != me ? rowp[x] : 0ull;
       s_j[t] = edge_nb[q];
       s_dmx[t] = Dme[x];
       s_w[t] = wt[q];
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
     __syncthreads();
     if (shortest == kInf64) continue;  // (every thread still meets the barriers)
     for (uint32_t t = 0; t < nl; ++t) {
+      if (s_j[t] == kInf) continue;  // a dead slot (no link)
       // getNextHopsWithMetric: x is a shortest-path next hop of a min-cost
       // member (via = shortest - d_me(x)), lowered with LFA to a member's
       // d_x(dst) < shortest + d_x(me)
@@ -308,7 +310,7 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
     ecol[i] = c->col[e0 + i];
     ew[i] = c->wt[e0 + i];
     const uint32_t* f = std::lower_bound(c->nb_id.data() + nb0, c->nb_id.data() + nb0 + k, ecol[i]);
-    ej[i] = (uint32_t)(f - (c->nb_id.data() + nb0));
+    ej[i] = ecol[i] == me ? kInf : (uint32_t)(f - (c->nb_id.data() + nb0));  // dead slot: none
   }
   auto& d_dist = rc.dist;
   auto& d_nh = rc.nh;
@@ -334,6 +336,15 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
   HIP_TRY(c, d_edge.alloc(cap));
   HIP_TRY(c, d_metric.alloc(cap));
   st = spf_plan_execute(p, d_dist.p, d_nh.p, c->stream);
+  if (st == SPF_E_STATE) {  // a row patch changed a source's next-hop layout: a new plan
+    spf_plan_destroy(rc.plan);
+    rc.plan = nullptr;
+    st = spf_plan_create(c, srcs.data(), (uint32_t)srcs.size(), 0, &rc.plan);
+    if (st != SPF_OK) return st;
+    p = rc.plan;
+    HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(1, spf_plan_nh_words(p))));
+    st = spf_plan_execute(p, d_dist.p, d_nh.p, c->stream);
+  }
   if (st != SPF_OK) return st;
   // the plan's D rows: the caller buffer when the source set is closed,
   // otherwise the plan's own closure rows

@@ -41,6 +41,7 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "engine_internal.h"
@@ -1727,14 +1728,19 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     if (c->row_ptr[u] > c->row_ptr[u + 1])
       return fail(c, SPF_E_INVALID, "row_ptr not monotone at %u", u);
   }
-  for (uint32_t e = 0; e < E; ++e) {
-    if (c->col[e] >= N) return fail(c, SPF_E_INVALID, "edge %u head %u out of range", e, c->col[e]);
-    const int32_t m = g->metric[e];
-    if (m <= 0) c->nonpos = true;
-    if (m < 0) c->needs64 = true;  // i32 -> u64 wraps (LinkState.h:22)
-    c->wt[e] = m > 0 ? (uint32_t)m : 0u;
-    c->max_metric = std::max(c->max_metric, c->wt[e]);
-  }
+  for (uint32_t u = 0; u < N; ++u)
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+      if (c->col[e] >= N) return fail(c, SPF_E_INVALID, "edge %u head %u out of range", e, c->col[e]);
+      const int32_t m = g->metric[e];
+      c->wt[e] = m > 0 ? (uint32_t)m : 0u;
+      if (c->col[e] == u) {  // a dead slot (see openr_spf.h): no edge
+        if (m != 1) return fail(c, SPF_E_INVALID, "dead slot %u (a self-loop) must carry metric 1", e);
+        continue;
+      }
+      if (m <= 0) c->nonpos = true;
+      if (m < 0) c->needs64 = true;  // i32 -> u64 wraps (LinkState.h:22)
+      c->max_metric = std::max(c->max_metric, c->wt[e]);
+    }
   c->unit = !c->nonpos && c->max_metric <= 1;
   // longest possible path beyond 32 bits: weighted solves take the exact
   // kernel's u64 labels (SPF_FLAG_DIST64)
@@ -1759,6 +1765,11 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     for (uint32_t e = 0; e < E; ++e)
       if (c->rev[e] == kInf)
         return fail(c, SPF_E_INVALID, "edge %u (link %u) has no reverse edge", e, c->link[e]);
+    c->link_slot.assign(2 * ((size_t)max_link + 1), kInf);
+    for (uint32_t e = 0; e < E; ++e) {
+      uint32_t* ls = &c->link_slot[2 * (size_t)c->link[e]];
+      ls[ls[0] == kInf ? 0 : 1] = e;
+    }
   }
   // distinct up neighbours per node, ascending id, min metric
   c->nb_ptr.assign(N + 1, 0);
@@ -1768,7 +1779,8 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   std::vector<std::pair<uint32_t, uint32_t>> tmp;
   for (uint32_t u = 0; u < N; ++u) {
     tmp.clear();
-    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) tmp.emplace_back(c->col[e], c->wt[e]);
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+      if (c->col[e] != u) tmp.emplace_back(c->col[e], c->wt[e]);
     if (c->row_ptr[u + 1] - c->row_ptr[u] > kBigDeg) ++c->big_nodes;
     std::sort(tmp.begin(), tmp.end());
     for (size_t i = 0; i < tmp.size(); ++i) {
@@ -1793,11 +1805,12 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
   {  // per edge: the head's index among the tail's distinct neighbours (the
      // route selection's next-hop bitmap of that neighbour)
-    std::vector<uint32_t> enb(std::max<uint32_t>(E, 1));
+    std::vector<uint32_t>& enb = c->edge_nb;
+    enb.assign(std::max<uint32_t>(E, 1), kInf);
     for (uint32_t u = 0; u < N; ++u) {
       const auto b = c->nb_id.begin() + c->nb_ptr[u], e = c->nb_id.begin() + c->nb_ptr[u + 1];
       for (uint32_t q = c->row_ptr[u]; q < c->row_ptr[u + 1]; ++q)
-        enb[q] = (uint32_t)(std::lower_bound(b, e, c->col[q]) - b);
+        enb[q] = c->col[q] == u ? kInf : (uint32_t)(std::lower_bound(b, e, c->col[q]) - b);
     }
     HIP_TRY(c, c->d_edge_nb.upload(enb.data(), enb.size(), c->stream));
   }
@@ -1820,8 +1833,10 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     c->sell_col.assign(c->sell_ptr[n_slices] + 32 * kSliceW, N);
     for (uint32_t v = 0; v < N; ++v) {
       const uint32_t sl = v / kSliceW, ln = v % kSliceW;
-      for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j)
-        c->sell_col[c->sell_ptr[sl] + j * kSliceW + ln] = c->col[c->row_ptr[v] + j];
+      for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j) {
+        const uint32_t x = c->col[c->row_ptr[v] + j];
+        c->sell_col[c->sell_ptr[sl] + j * kSliceW + ln] = x == v ? N : x;  // dead slot: padding
+      }
     }
     HIP_TRY(c, c->d_sell_ptr.upload(c->sell_ptr.data(), c->sell_ptr.size(), c->stream));
     HIP_TRY(c, c->d_sell_col.upload(c->sell_col.data(), c->sell_col.size(), c->stream));
@@ -1887,6 +1902,7 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   c->loaded = true;
   ++c->shape;
   ++c->epoch;
+  ++c->layout;
   return SPF_OK;
 }
 
@@ -1939,11 +1955,13 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
   if (!changed) return SPF_OK;
   bool nonpos = false, neg = false;
   uint32_t max_metric = 0;
-  for (uint32_t e = 0; e < c->E; ++e) {
-    nonpos |= met[e] <= 0;
-    neg |= met[e] < 0;
-    max_metric = std::max(max_metric, wt[e]);
-  }
+  for (uint32_t u = 0; u < c->N; ++u)
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+      if (c->col[e] == u) continue;  // dead slot
+      nonpos |= met[e] <= 0;
+      neg |= met[e] < 0;
+      max_metric = std::max(max_metric, wt[e]);
+    }
   c->wt.swap(wt);
   c->met.swap(met);
   c->needs64 = neg || (uint64_t)max_metric * (uint64_t)(c->N - 1) >= (uint64_t)kInf;
@@ -1961,6 +1979,7 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
     const uint32_t b = c->nb_ptr[u], e = c->nb_ptr[u + 1];
     for (uint32_t j = b; j < e; ++j) c->nb_w[j] = kInf;
     for (uint32_t k = c->row_ptr[u]; k < c->row_ptr[u + 1]; ++k) {
+      if (c->col[k] == u) continue;  // dead slot
       const uint32_t j = (uint32_t)(std::lower_bound(c->nb_id.begin() + b, c->nb_id.begin() + e,
                                                      c->col[k]) - c->nb_id.begin());
       c->nb_w[j] = std::min(c->nb_w[j], c->wt[k]);
@@ -1970,6 +1989,234 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
   HIP_TRY(c, c->d_wt.upload(c->wt.data(), c->E, c->stream));
   HIP_TRY(c, c->d_met.upload(c->met.data(), c->E, c->stream));
   HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  ++c->epoch;
+  return SPF_OK;
+}
+
+// Rows rewritten in place (a link going down or up,
+// or an adjacency withdrawn and advertised again, without a reload).  Each
+// listed node keeps its row length; a dead slot is a self-loop (col = the
+// node, metric 1): no kernel relaxes, pushes or pulls anything over one, the
+// distinct-neighbour lists and the route tables skip them.  The derived
+// tables of the touched rows are patched: reverse edges (by link id), the
+// distinct-neighbour lists (rebuilt when a count changes: plans whose
+// sources' next-hop layout changed fail with SPF_E_STATE), the route tables'
+// per-edge neighbour index and the sliced-ELL columns.  Plans re-derive at
+// their next execute, as after a metric patch.
+spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, const uint32_t* col,
+                                const int32_t* metric, const uint32_t* link) {
+  if (!c || (n && (!nodes || !col || !metric || !link)))
+    return fail(c, SPF_E_INVALID, "spf_graph_patch_rows: NULL argument");
+  if (!c->loaded) return fail(c, SPF_E_STATE, "no graph loaded");
+  const uint32_t N = c->N;
+  std::vector<uint8_t> touched(N, 0);
+
+  for (uint32_t i = 0; i < n; ++i) {
+    if (nodes[i] >= N) return fail(c, SPF_E_INVALID, "node %u out of range", nodes[i]);
+    if (touched[nodes[i]]++) return fail(c, SPF_E_INVALID, "node %u listed twice", nodes[i]);
+
+  }
+  if (!n) return SPF_OK;
+  // validate the new rows before changing anything
+  const uint32_t max_link = (uint32_t)(c->link_slot.size() / 2) - 1;
+  {
+    size_t o = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t u = nodes[i];
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e, ++o) {
+        if (col[o] >= N) return fail(c, SPF_E_INVALID, "row of %u: head %u out of range", u, col[o]);
+        if (link[o] > max_link)
+          return fail(c, SPF_E_INVALID, "row of %u: link %u is not a link of the loaded graph", u, link[o]);
+        if (col[o] == u && metric[o] != 1)
+          return fail(c, SPF_E_INVALID, "row of %u: a dead slot (self-loop) must carry metric 1", u);
+      }
+    }
+  }
+  std::vector<uint32_t> old_nb(n);
+  for (uint32_t i = 0; i < n; ++i) old_nb[i] = c->nb_ptr[nodes[i] + 1] - c->nb_ptr[nodes[i]];
+  // rows
+  {
+    size_t o = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t u = nodes[i];
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e, ++o) {
+        c->col[e] = col[o];
+        c->met[e] = metric[o];
+        c->wt[e] = metric[o] > 0 ? (uint32_t)metric[o] : 0u;
+        c->link[e] = link[o];
+      }
+    }
+  }
+  // link slots and reverse edges: a link's slot in an untouched row keeps its
+  // position; its slots in touched rows are where the new rows put them
+  auto tail = [&](uint32_t e) {
+    return (uint32_t)(std::upper_bound(c->row_ptr.begin(), c->row_ptr.end(), e) - c->row_ptr.begin()) - 1;
+  };
+  std::unordered_map<uint32_t, std::vector<uint32_t>> moved;  // link -> its slots in touched rows
+  for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t e = c->row_ptr[nodes[i]]; e < c->row_ptr[nodes[i] + 1]; ++e) moved[c->link[e]].push_back(e);
+  for (auto& [l, es] : moved) {
+    uint32_t* ls = &c->link_slot[2 * (size_t)l];
+    std::vector<uint32_t> slots = es;
+    for (int k = 0; k < 2; ++k)  // its slot in an untouched row, if any, stays
+      if (ls[k] != kInf && !touched[tail(ls[k])] && c->link[ls[k]] == l) slots.push_back(ls[k]);
+    if (slots.size() != 2)
+      return fail(c, SPF_E_INVALID, "link %u has %zu slots after the patch (2 needed)", l, slots.size());
+    ls[0] = slots[0];
+    ls[1] = slots[1];
+    c->rev[slots[0]] = slots[1];
+    c->rev[slots[1]] = slots[0];
+    const uint32_t a = tail(slots[0]), b = tail(slots[1]);
+    const bool dead0 = c->col[slots[0]] == a, dead1 = c->col[slots[1]] == b;
+    if (dead0 != dead1 || (!dead0 && (c->col[slots[0]] != b || c->col[slots[1]] != a)))
+      return fail(c, SPF_E_INVALID, "link %u: its two slots are not one link in both directions", l);
+  }
+  // graph-wide metric facts over live edges
+  bool nonpos = false, neg = false;
+  uint32_t max_metric = 0;
+  for (uint32_t u = 0; u < N; ++u)
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+      if (c->col[e] == u) continue;
+      nonpos |= c->met[e] <= 0;
+      neg |= c->met[e] < 0;
+      max_metric = std::max(max_metric, c->wt[e]);
+    }
+  c->nonpos = nonpos;
+  c->needs64 = neg || (uint64_t)max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf;
+  c->max_metric = max_metric;
+  c->unit = !nonpos && max_metric <= 1;
+  // distinct up neighbours of the touched nodes; the lists are rebuilt (every
+  // untouched node's range copied) when a count changes
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fresh(n);
+  bool counts = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t u = nodes[i];
+    auto& t = fresh[i];
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+      if (c->col[e] != u) t.emplace_back(c->col[e], c->wt[e]);
+    std::sort(t.begin(), t.end());
+    t.erase(std::unique(t.begin(), t.end(), [](const auto& a, const auto& b) { return a.first == b.first; }),
+            t.end());
+    counts |= t.size() != old_nb[i];
+  }
+  if (counts) {
+    std::vector<int32_t> slot(N, -1);
+    for (uint32_t i = 0; i < n; ++i) slot[nodes[i]] = (int32_t)i;
+    std::vector<uint32_t> ptr(N + 1, 0), id, w;
+    id.reserve(c->nb_id.size() + 16);
+    w.reserve(c->nb_id.size() + 16);
+    for (uint32_t u = 0; u < N; ++u) {
+      if (slot[u] >= 0) {
+        for (const auto& x : fresh[slot[u]]) {
+          id.push_back(x.first);
+          w.push_back(x.second);
+        }
+      } else {
+        id.insert(id.end(), c->nb_id.begin() + c->nb_ptr[u], c->nb_id.begin() + c->nb_ptr[u + 1]);
+        w.insert(w.end(), c->nb_w.begin() + c->nb_ptr[u], c->nb_w.begin() + c->nb_ptr[u + 1]);
+      }
+      ptr[u + 1] = (uint32_t)id.size();
+    }
+    c->nb_ptr.swap(ptr);
+    c->nb_id.swap(id);
+    c->nb_w.swap(w);
+    ++c->layout;
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t b = c->nb_ptr[nodes[i]];
+      for (size_t k = 0; k < fresh[i].size(); ++k) {
+        c->nb_id[b + k] = fresh[i][k].first;
+        c->nb_w[b + k] = fresh[i][k].second;
+      }
+    }
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  // the route tables' per-edge neighbour index (touched tails only)
+  std::vector<uint32_t>& enb = c->edge_nb;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t u = nodes[i];
+    const auto b = c->nb_id.begin() + c->nb_ptr[u], e = c->nb_id.begin() + c->nb_ptr[u + 1];
+    for (uint32_t q = c->row_ptr[u]; q < c->row_ptr[u + 1]; ++q)
+      enb[q] = c->col[q] == u ? kInf : (uint32_t)(std::lower_bound(b, e, c->col[q]) - b);
+  }
+  // sliced-ELL columns of the touched nodes (and their packed u16 copies)
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t v = nodes[i], sl = v / kSliceW, ln = v % kSliceW;
+    const uint32_t deg = c->row_ptr[v + 1] - c->row_ptr[v];
+    for (uint32_t j = 0; j < deg; ++j) {
+      const uint32_t x = c->col[c->row_ptr[v] + j];
+      c->sell_col[c->sell_ptr[sl] + j * kSliceW + ln] = x == v ? N : x;
+    }
+    if (!c->sell4.empty()) {
+      const uint32_t w = (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / kSliceW;
+      const uint32_t groups = (c->sell4_ptr[sl + 1] - c->sell4_ptr[sl]) / kSliceW;
+      for (uint32_t g = 0; g < groups; ++g) {
+        uint32_t id[4];
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t j = 4 * g + k;
+          id[k] = j < w ? c->sell_col[c->sell_ptr[sl] + j * kSliceW + ln] : N;
+        }
+        const size_t e = 2ull * (c->sell4_ptr[sl] + g * kSliceW + ln);
+        c->sell4[e] = 4 * id[0] | (4 * id[1] << 16);
+        c->sell4[e + 1] = 4 * id[2] | (4 * id[3] << 16);
+      }
+    }
+  }
+  // upload the changed ranges only: the touched rows (merged when adjacent),
+  // the partner slots their reverse edges point at, and the touched slices
+  std::vector<uint32_t> order(nodes, nodes + n);
+  std::sort(order.begin(), order.end());
+  std::vector<std::pair<uint32_t, uint32_t>> runs;  // [begin, end) edge ranges
+  for (uint32_t u : order) {
+    const uint32_t b = c->row_ptr[u], e = c->row_ptr[u + 1];
+    if (b == e) continue;
+    if (!runs.empty() && runs.back().second == b)
+      runs.back().second = e;
+    else
+      runs.emplace_back(b, e);
+  }
+  for (const auto& r : runs) {
+    const size_t b = r.first, k = r.second - r.first;
+    HIP_TRY(c, c->d_col.upload_at(c->col.data(), b, k, c->stream));
+    HIP_TRY(c, c->d_wt.upload_at(c->wt.data(), b, k, c->stream));
+    HIP_TRY(c, c->d_met.upload_at(c->met.data(), b, k, c->stream));
+    HIP_TRY(c, c->d_rev.upload_at(c->rev.data(), b, k, c->stream));
+    HIP_TRY(c, c->d_link.upload_at(c->link.data(), b, k, c->stream));
+    HIP_TRY(c, c->d_edge_nb.upload_at(enb.data(), b, k, c->stream));
+  }
+  {
+    std::vector<uint32_t> partners;
+    for (const auto& r : runs)
+      for (uint32_t q = r.first; q < r.second; ++q) partners.push_back(c->rev[q]);
+    std::sort(partners.begin(), partners.end());
+    partners.erase(std::unique(partners.begin(), partners.end()), partners.end());
+    for (uint32_t q : partners) HIP_TRY(c, c->d_rev.upload_at(c->rev.data(), q, 1, c->stream));
+  }
+  if (counts) {
+    HIP_TRY(c, c->d_nb_ptr.upload(c->nb_ptr.data(), N + 1, c->stream));
+    HIP_TRY(c, c->d_nb_id.upload(c->nb_id.data(), c->nb_id.size(), c->stream));
+    HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  } else {
+    for (uint32_t u : order) {
+      const size_t b = c->nb_ptr[u], k = c->nb_ptr[u + 1] - b;
+      HIP_TRY(c, c->d_nb_id.upload_at(c->nb_id.data(), b, k, c->stream));
+      HIP_TRY(c, c->d_nb_w.upload_at(c->nb_w.data(), b, k, c->stream));
+    }
+  }
+  {
+    std::vector<uint32_t> slices;
+    for (uint32_t u : order) slices.push_back(u / kSliceW);
+    slices.erase(std::unique(slices.begin(), slices.end()), slices.end());
+    for (uint32_t sl : slices) {
+      const size_t b = c->sell_ptr[sl], k = c->sell_ptr[sl + 1] - b;
+      HIP_TRY(c, c->d_sell_col.upload_at(c->sell_col.data(), b, k, c->stream));
+      if (!c->sell4.empty()) {
+        const size_t b4 = 2ull * c->sell4_ptr[sl], k4 = 2ull * (c->sell4_ptr[sl + 1] - c->sell4_ptr[sl]);
+        HIP_TRY(c, c->d_sell4.upload_at(c->sell4.data(), b4, k4, c->stream));
+      }
+    }
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   ++c->epoch;
   return SPF_OK;
@@ -2516,6 +2763,7 @@ spf_status spf_plan_create(spf_ctx* c, const uint32_t* srcs, uint32_t n_src,
   p->flags = flags;
   p->srcs.assign(srcs, srcs + n_src);
   p->shape = c->shape;
+  p->layout = c->layout;
   const spf_status st = build_plan(c, p.get());
   if (st != SPF_OK) return st;
   *out = p.release();
@@ -2992,6 +3240,15 @@ spf_status spf_plan_execute(spf_plan* p, uint32_t* d_dist, uint32_t* d_nh, void*
     return fail(c, SPF_E_INVALID, "spf_plan_execute: NULL output buffer");
   if (p->shape != c->shape)
     return fail(c, SPF_E_STATE, "graph reloaded since the plan was created: recreate it");
+  if (p->layout != c->layout) {
+    // a row patch changed some node's distinct neighbours: the plan's
+    // next-hop layout holds only if none of its sources was one of them
+    for (uint32_t i = 0; i < p->n_src; ++i)
+      if (c->nb_ptr[p->srcs[i] + 1] - c->nb_ptr[p->srcs[i]] != p->words[i])
+        return fail(c, SPF_E_STATE, "source %u's distinct neighbours changed since the plan was "
+                                    "created (its next-hop layout): recreate it", p->srcs[i]);
+    p->layout = c->layout;
+  }
   if (p->epoch != c->epoch || (p->tm_G && c->team_off)) {
     // patched in place, or teams turned off by a timeout: re-derive, same
     // output layout

@@ -2054,10 +2054,11 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   p->ctx = c;
   p->src = src;
   const uint32_t N = c->N, E = c->E;
-  // link -> one of its directed edges
+  // link -> one of its directed edges (up links only: a dead slot is a self-loop)
   std::vector<uint32_t> link_edge((size_t)c->max_link + 1, kInf);
-  for (uint32_t e = 0; e < E; ++e)
-    if (link_edge[c->link[e]] == kInf) link_edge[c->link[e]] = e;
+  for (uint32_t u = 0; u < N; ++u)
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+      if (c->col[e] != u && link_edge[c->link[e]] == kInf) link_edge[c->link[e]] = e;
   std::vector<uint32_t> fails;
   if (fail_links) {
     fails.assign(fail_links, fail_links + n_fail);

@@ -458,7 +458,10 @@ class LinkState(N.NativeHandle):
         lh = np.zeros(max(1, int(lid.max()) + 1 if len(lid) else 1), np.uint64)
         M, P = (1 << 64) - 1, 0x100000001b3
         for l in np.unique(lid):
-            (a, b), (c, d) = self._link(int(l)).orderedNames
+            try:
+                (a, b), (c, d) = self._link(int(l)).orderedNames
+            except N.SpfError:  # a withdrawn link's dead slots: never a result
+                continue
             f = 0xcbf29ce484222325
             for part in (a, b, c, d):
                 for ch in part.encode():

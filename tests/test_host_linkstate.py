@@ -113,7 +113,11 @@ def test_random_lsdb_sequences_match_oracle(seed):
             assert orc.is_overloaded(n) == ls.isNodeOverloaded(n)
 
 
-def test_flatten_is_the_up_subgraph_in_iteration_order():
+def test_flatten_is_every_link_in_iteration_order_down_links_dead():
+    """The flattened CSR holds a slot for every link of a node in linksFromNode
+    order: an up link towards its other end with the metric advertised by the
+    node, a down link as a dead slot (a self-loop of metric 1, openr_spf.h),
+    so that a link going down or up later patches its rows in place."""
     topo = T.random_graph(40, 90, 7, max_metric=9, parallel_frac=0.3, overload_frac=0.1,
                           link_overload_frac=0.1)
     orc = OracleLinkState()
@@ -122,16 +126,19 @@ def test_flatten_is_the_up_subgraph_in_iteration_order():
     ls.updateAdjacencyDatabases(topo.lsdb)
     names, rp, col, met, lid, ovl = ls.flatten()
     assert names == sorted(names)  # ids are ascending-name ranks (LinkState.h:488-498)
+    n_dead = 0
     for u, name in enumerate(names):
-        want = [(l[0], l[1]) for l in orc.links(name) if l[2]]  # up links, metric from u
-        got = []
-        for e in range(rp[u], rp[u + 1]):
-            got.append(int(met[e]))
-        assert got == [m for _, m in want]
-        other = [names[int(v)] for v in col[rp[u]: rp[u + 1]]]
-        exp_other = [k[2] if k[0] == name else k[0] for k, _ in want]
-        assert other == exp_other
+        want = orc.links(name)  # (key, metric from u, up) in iteration order
+        assert rp[u + 1] - rp[u] == len(want)
+        for e, (k, m, up) in zip(range(rp[u], rp[u + 1]), want):
+            if up:
+                assert int(met[e]) == m
+                assert names[int(col[e])] == (k[2] if k[0] == name else k[0])
+            else:
+                n_dead += 1
+                assert int(col[e]) == u and int(met[e]) == 1
         assert bool(ovl[u]) == orc.is_overloaded(name)
+    assert n_dead > 0
     # every link id appears exactly twice (both directions)
     _, counts = np.unique(lid, return_counts=True)
     assert (counts == 2).all()

@@ -90,7 +90,7 @@ def _planar(names, csr, dist, mats):
     pitch = (n + 63) // 64 * 64
     ks, offs, rows, off = [], [], [], 0
     for i in range(n):
-        k = len(set(int(c) for c in col[rp[i]:rp[i + 1]]))
+        k = len(set(int(c) for c in col[rp[i]:rp[i + 1]]) - {i})  # (dead slots: self-loops)
         ks.append(k)
         offs.append(off)
         for j in range(k):
