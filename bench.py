@@ -526,6 +526,37 @@ class AllSourcesMulti(AllSources):
         return {"execute": self.member_ms[slow]}
 
 
+def enqueue_stagger(wl, reps: int) -> dict:
+    """Host enqueue of an execute (after the timed steps, untimed): per member,
+    us from spf_mplan_execute's start until that member's launches were
+    enqueued -- the start stagger separate GPUs would see -- issued one member
+    after another from this thread, then from per-member threads
+    (spf_mplan_set_enqueue_threads)."""
+    out = {}
+    wl.plan.enable_timing(0)  # production executes: no timing events
+    for mode, graphs, key in ((0, False, "serial"), (1, False, "threads"), (0, True, "serial_graphs")):
+        wl.plan.set_enqueue_threads(mode)
+        wl.plan.set_graphs(graphs)
+        wl.plan.execute()  # (a graph capture happens on the first execute)
+        wl.plan.synchronize()
+        rows = []
+        for _ in range(reps):
+            wl.plan.execute()
+            ns, _thr = wl.plan.enqueue_ns()
+            rows.append(ns.astype(np.float64) / 1e3)
+            wl.plan.synchronize()
+        a = np.median(np.array(rows), axis=0)
+        out[key] = {"member_done_us": [round(float(x), 1) for x in a],
+                    "stagger_us": round(float(a.max() - a[a > 0].min()) if (a > 0).any() else 0.0, 1),
+                    "last_member_us": round(float(a.max()), 1)}
+    wl.plan.set_enqueue_threads(-1)
+    wl.plan.set_graphs(wl.graphs)
+    out["note"] = ("median over %d executes without timing events; members of one device share "
+                   "its stream, so the threads row here times only the host side; serial_graphs: "
+                   "each member's execute replayed from a captured hipGraph" % reps)
+    return out
+
+
 class Ksp2AllPairs:
     """configs[3]: KSP2 (k = 1 and k = 2 paths) for every pair of the WAN
     graph; sources dealt round-robin over ranks (strong scaling), the ranks'
@@ -955,12 +986,29 @@ class RoutesAllNodes:
         self.parallelism = "one LinkState per process (replicas); all sources resident on its GPU"
         self.t_pass, self.t_routes = [], []
         self.digests = None
+        self.n_records = 0
+        # algorithmic bytes of the route kernel: every resident u32 row and
+        # next-hop bitmap read once, the CSR, and the outputs (digests here;
+        # headers + records when materialised)
+        rp = self.ls.flatten()[1].astype(np.int64)
+        col = self.ls.flatten()[2].astype(np.int64)
+        k = np.array([len(np.unique(col[rp[v]:rp[v + 1]])) for v in range(self.n)], np.int64)
+        wpm = (self.n + 31) // 32
+        self.read_bytes = 4 * self.n * self.n + 4 * int(k.sum()) * wpm + 4 * (self.n + 1) + 12 * self.e
+        self.pmc_kernels = {"routes": ["route_sets_kernel"]}
+
+    def route_step(self):
+        self.digests, kms = self.ls.allSourcesRouteDigests(self.set_ptr, self.set_nodes, self.lfa)
+        return kms
+
+    def out_bytes(self) -> int:
+        return 8 * self.n
 
     def step(self) -> None:
         t0 = time.perf_counter()
         self.ls.prefetchAllSources()  # execute + synchronize
         t1 = time.perf_counter()
-        self.digests, kms = self.ls.allSourcesRouteDigests(self.set_ptr, self.set_nodes, self.lfa)
+        kms = self.route_step()
         self.t_pass.append(t1 - t0)
         self.t_routes.append(kms)
 
@@ -970,19 +1018,22 @@ class RoutesAllNodes:
     def kernel_ms(self):
         self.phase_ms = {"all-sources pass (execute + sync, host clock)": 1e3 * float(np.mean(self.t_pass)),
                          "route selection kernel (HIP events)": float(np.mean(self.t_routes))}
+        self.alg_bytes = {"allsources": 0, "routes": self.read_bytes + self.out_bytes()}
+        self.kernel_bytes = dict(self.alg_bytes)
         return {"allsources": 1e3 * float(np.mean(self.t_pass)), "routes": float(np.mean(self.t_routes))}
 
     def edges_per_unit(self) -> int:
         return self.e
 
-    def _oracle_digests(self, mes, orc=None):
+    def _oracle_digests(self, mes, orc=None, kept_min=False):
         sys.path.insert(0, str(ROOT / "tests"))
         from oracle import NameTable, route_digests  # checker / CPU baseline only
 
         if orc is None:
             orc = oracle()()
             orc.update_packed(self.topo.lsdb)
-        return route_digests(orc, NameTable(self.names), mes, self.set_ptr, self.set_nodes, self.lfa)
+        return route_digests(orc, NameTable(self.names), mes, self.set_ptr, self.set_nodes, self.lfa,
+                             kept_min=kept_min)
 
     def verify(self):
         """The last step's digests of 48 nodes (the 16 highest-degree ones
@@ -1011,6 +1062,51 @@ class RoutesAllNodes:
                 "sample": f"{done} nodes' route selections towards all {self.n} loopbacks"
                           f"{' with LFA' if self.lfa else ''}, their SPFs (+ neighbours') included, "
                           f"{dt:.1f} s on {host_cores()} cores of {cpu_model()} (oracle/spf_oracle.cpp)"}
+
+
+class RouteDbsAllNodes(RoutesAllNodes):
+    """CS-2 with every node's route database MATERIALISED:
+    per step one all-sources pass and every node's next-hop records towards
+    every loopback with LFA written into its GPU's HBM
+    (spf_mplan_route_records: per node and route a header, per next hop a
+    u64 record = CSR edge -- link, interface, neighbour -- | metric), what
+    Decision::getDecisionRouteDb(node) returns for every node
+    (Decision.cpp:1480-1500 -> buildRouteDb :556-722) minus the thrift
+    encoding.  value = route databases (nodes) materialised per second;
+    verify reads 48 nodes' databases back and checks them against the
+    oracle's restatement."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.desc = self.desc.replace("route selection", "route database (next-hop records, in HBM)")
+
+    def route_step(self):
+        self.n_records, kms = self.ls.allSourcesRouteRecords(self.set_ptr, self.set_nodes, self.lfa)
+        return kms
+
+    def out_bytes(self) -> int:
+        return 8 * self.n * (len(self.set_ptr) - 1) + 8 * self.n_records
+
+    def verify(self):
+        """48 nodes' databases (the 16 highest-degree and 32 random) read back,
+        reduced with the digest formula, against the oracle's restatement."""
+        sys.path.insert(0, str(ROOT / "tests"))
+        from helpers import route_db_digest  # checker only
+
+        deg = np.diff(self.ls.flatten()[1].astype(np.int64))
+        rng = np.random.default_rng(11)
+        mes = np.unique(np.concatenate([np.argsort(-deg)[:16], rng.choice(self.n, 32, replace=False)]))
+        lid = self.ls.flatten()[4]
+        lh = self.ls.linkValueHashes()
+        got = np.array([route_db_digest(*self.ls.allSourcesRouteDb(int(t)), lid, lh) for t in mes], np.uint64)
+        want = self._oracle_digests(mes, kept_min=True)
+        bad = np.nonzero(got != want)[0]
+        return {"checked_nodes": int(len(mes)), "sets_per_node": int(len(self.set_ptr) - 1),
+                "records": int(self.n_records), "mismatches": int(len(bad)),
+                "first_mismatch": self.names[int(mes[bad[0]])] if len(bad) else None,
+                "against": "oracle/spf_oracle.cpp orc_ls_route_digests (getMinCostNodes + "
+                           "getNextHopsWithMetric + getNextHopsThrift restated); each read-back "
+                           "database reduced with the same digest (tests/helpers.py route_db_digest)"}
 
 
 class FacadeRouteBuild:
@@ -1229,7 +1325,8 @@ def host_cores() -> int:
 WORKLOADS = {"fabric_full": AllSources, "fabric_ref": AllSources, "grid100": AllSources,
              "fabric_rtt": AllSources,
              "wan_ksp2": Ksp2AllPairs, "ba_whatif": WhatIfAllLinks, "fabric_lfa": FacadeLfa,
-             "fabric_routes": RoutesAllNodes, "fabric_lfa_routes": FacadeRouteBuild,
+             "fabric_routes": RoutesAllNodes, "fabric_route_dbs": RouteDbsAllNodes,
+             "fabric_lfa_routes": FacadeRouteBuild,
              "fabric_flap_routes": FacadeFlapRouteBuild}
 
 
@@ -1455,6 +1552,9 @@ def main() -> None:
             if isinstance(wl, Ksp2AllPairs) else
             "LinkState facade: publication + getSpfResult(me and every LFA neighbour) per sec"
             if isinstance(wl, FacadeLfa) else
+            "getDecisionRouteDb for every node, route databases materialised in HBM (all-sources SPF "
+            "+ next-hop records) per sec, 10k fabric"
+            if isinstance(wl, RouteDbsAllNodes) else
             "getDecisionRouteDb for every node (all-sources SPF + route selection) per sec, 10k fabric"
             if isinstance(wl, RoutesAllNodes) else
             "link-flap publication + SpfSolver.buildRouteDb(me) with LFA per sec, 10k fabric"
@@ -1541,6 +1641,7 @@ def main_multi(args) -> None:
     wl.finish()
     elapsed = time.perf_counter() - t0
     kms = wl.kernel_ms()
+    enq = enqueue_stagger(wl, max(5, args.steps))
     parity = wl.verify()
     distinct = sorted(set(devices))
     value = wl.units * args.steps / elapsed
@@ -1568,6 +1669,7 @@ def main_multi(args) -> None:
             "projected_step_ms_one_member_per_gpu": slow,
             "projected_value_one_member_per_gpu": wl.units / (slow * 1e-3),
             "hip_graphs": wl.graphs,
+            "host_enqueue": enq,
         },
         "roofline": roofline_block(wl, kms, sum(kms.values()), args.workload, 0),
         "cpu_baseline": None,

@@ -490,6 +490,16 @@ uint32_t spf_mplan_closure_rows(const spf_mplan* mp, uint32_t member);
  * first execute of a graph epoch and replayed after that (re-captured after
  * an in-place patch) */
 spf_status spf_mplan_set_graphs(spf_mplan* mp, int enable);
+/* Host enqueue threads: mode 1 issues each member's execute from its own host
+ * thread (spinning briefly between back-to-back executes, then sleeping), 0
+ * from the caller's thread one member after another, -1 (default) threads
+ * when the members with work sit on two or more distinct devices. */
+spf_status spf_mplan_set_enqueue_threads(spf_mplan* mp, int mode);
+/* The last execute's host enqueue: out[i] = ns from the execute's start until
+ * member i's launches were enqueued (0 for members without work); *threaded =
+ * 1 when it used the enqueue threads.  The spread of out[] is the start
+ * stagger the members' GPUs see. */
+spf_status spf_mplan_enqueue_ns(const spf_mplan* mp, uint64_t* out, uint32_t n, int* threaded);
 /* Enqueue every member's execute on its device's stream; no host wait. */
 spf_status spf_mplan_execute(spf_mplan* mp);
 /* Wait for every member and check its grid / team barriers (spf_device_check). */
@@ -528,6 +538,28 @@ spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_
                             const uint32_t* set_nodes, uint32_t n_sets, uint32_t flags,
                             uint64_t* min_metric, uint32_t* nh_count, uint32_t* nh_edge,
                             uint64_t* nh_metric);
+/* Every me's route database materialised on its owning device (the same
+ * selection as spf_mplan_route_digests, written out instead of hashed): what
+ * Decision::getDecisionRouteDb(node) returns for every node (Decision.cpp:
+ * 1480-1500 -> buildRouteDb :556-722, one area), in device memory.  Per me t
+ * and set p a header word = offset | count << 32: the route's `count` next
+ * hops are records offset .. offset + count - 1 of me's region, each a u64 =
+ * CSR edge (me -> neighbour: link id, interface, neighbour and the metric me
+ * advertises come with it) | metric << 32 (w(link) + dist(neighbour, dst)),
+ * in me's link order -- getNextHopsThrift's next hops.  Sets without a kept
+ * next hop have count 0.  Regions are sized from the previous call's counts
+ * (the first call, or one whose counts grew, runs the kernel a second time).
+ * SPF_E_UNSUPPORTED when a metric exceeds 2^32 - 1.  *n_records (optional) =
+ * records over every me; *kernel_ms (optional) = the slowest member's kernel.
+ * The databases stay resident until the next call. */
+spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32_t n_me,
+                                   const uint32_t* set_ptr, const uint32_t* set_nodes, uint32_t n_sets,
+                                   uint32_t flags, uint64_t* n_records, double* kernel_ms);
+/* me t's database from the last spf_mplan_route_records: hdr = [n_sets]
+ * headers (may be NULL), rec = its records (cap entries; SPF_E_NOMEM when
+ * fewer than *n), *n = its record count.  Waits. */
+spf_status spf_mplan_route_db(spf_mplan* mp, uint32_t t, uint64_t* hdr, uint64_t* rec, uint64_t cap,
+                              uint64_t* n);
 /* HIP-event time of each member's executes: ms[member] summed over the last
  * executes since enable / the last call, *n = executes. */
 spf_status spf_mplan_enable_timing(spf_mplan* mp, uint32_t max_executes);

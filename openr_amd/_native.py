@@ -259,6 +259,12 @@ PROTOTYPES = {
                                   C.POINTER(_vp)]),
     "spf_mplan_closure_rows": (C.c_uint32, [_vp, C.c_uint32]),
     "spf_mplan_set_graphs": (C.c_int, [_vp, C.c_int]),
+    "spf_mplan_set_enqueue_threads": (C.c_int, [_vp, C.c_int]),
+    "spf_mplan_route_records": (C.c_int, [_vp, _u32p, C.c_uint32, _u32p, _u32p, C.c_uint32, C.c_uint32,
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    "spf_mplan_route_db": (C.c_int, [_vp, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                     C.c_uint64, C.POINTER(C.c_uint64)]),
+    "spf_mplan_enqueue_ns": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_int)]),
     "spf_mplan_execute": (C.c_int, [_vp]),
     "spf_mplan_synchronize": (C.c_int, [_vp]),
     "spf_mplan_digest": (C.c_int, [_vp, _u64p]),

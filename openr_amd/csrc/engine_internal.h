@@ -335,14 +335,27 @@ spf_status set_lds_limits(spf_ctx* c);
 spf_status resident_order(spf_ctx* c, hipStream_t s);
 spf_status resident_done(spf_ctx* c, hipStream_t s);
 void resident_forget(const spf_ctx* c);
+// Materialised route databases of many `me` (routes.hip kRsDb): per me slot
+// its headers (n_sets words), its region of the record pool (base, cap), the
+// reservation cursor (zeroed before the launch) and the error flags.
+struct RouteDbOut {
+  unsigned long long* hdr = nullptr;
+  unsigned long long* pool = nullptr;
+  const unsigned long long* base = nullptr;
+  const uint32_t* cap = nullptr;
+  uint32_t* cursor = nullptr;
+  uint32_t* flags = nullptr;
+};
 // Route selection over resident rows for many `me` (routes.hip): digests per
-// me (d_digest, n_me slots, added to) or spf_routes' records of ONE me.
+// me (d_digest, n_me slots, added to), their route databases (db), or
+// spf_routes' records of ONE me.
 spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
                              const unsigned long long* d_nhp, const uint32_t* d_me, uint32_t n_me,
                              const uint32_t* d_set_ptr, const uint32_t* d_set_nodes, uint32_t n_sets,
                              bool lfa, const unsigned long long* d_link_hash,
                              unsigned long long* d_digest, uint64_t* d_min, uint32_t* d_cnt,
-                             uint32_t* d_edge, uint64_t* d_metric, hipStream_t s);
+                             uint32_t* d_edge, uint64_t* d_metric, hipStream_t s,
+                             const RouteDbOut* db = nullptr);
 // pathLinks of `src` from its u32 distance row on the device (spf_preds
 // without the upload; spf_mplan_preds reads a resident row).
 spf_status preds_from_row(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,

@@ -24,6 +24,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -31,7 +34,9 @@
 #include <map>
 #include <memory>
 #include <numeric>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine_internal.h"
@@ -184,7 +189,16 @@ struct spf_mplan {
     std::vector<uint32_t> h_rsp, h_rsn;  // host copies of the uploaded sets (re-upload only on change)
     std::vector<uint64_t> h_lh;
     uint64_t r_epoch = ~0ull;  // execute count the address tables belong to
+    // materialised route databases (spf_mplan_route_records): per me slot
+    // [n_sets] headers, its region of the record pool, reservation cursors
+    DevBuf<unsigned long long> dbhdr, dbpool, dbbase;
+    DevBuf<uint32_t> dbcap, dbcur, dbflags;
+    std::vector<uint32_t> db_me, h_dbcap, h_dbcnt;
+    std::vector<unsigned long long> h_dbbase;
   };
+  // the last spf_mplan_route_records: request t -> (member, slot), sets
+  std::vector<std::pair<uint32_t, uint32_t>> db_loc;
+  uint32_t db_sets = 0;
   std::vector<unsigned long long> h_rowp, h_nhp;  // the address tables (host; uploads read them)
   std::unique_ptr<Part[]> parts;  // [n_parts]
   uint32_t n_parts = 0;
@@ -192,7 +206,36 @@ struct spf_mplan {
   uint32_t timing_cap = 0, timing_n = 0;
   uint64_t executes = 0;   // bumps on every spf_mplan_execute (route tables follow it)
   int peer = -1;           // 1: every member can read every other member's HBM
+  // host enqueue: per member, ns from the execute's start until its launches
+  // were enqueued (the last execute; spf_mplan_enqueue_ns)
+  std::vector<uint64_t> enq_ns;
+  // per-member enqueue threads (spf_mplan_set_enqueue_threads): each member's
+  // launches issued from its own host thread, so the last GPU does not start
+  // n_members - 1 enqueues after the first
+  struct Pool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint64_t> gen{0};
+    std::atomic<uint32_t> pending{0};
+    std::atomic<bool> stop{false};
+    std::vector<spf_status> st;
+    std::chrono::steady_clock::time_point t0;
+  };
+  std::unique_ptr<Pool> pool;
+  int threads_mode = -1;  // -1: automatic (distinct devices), 0 off, 1 on
+  void stop_pool() {
+    if (!pool) return;
+    {
+      std::lock_guard<std::mutex> lk(pool->mu);
+      pool->stop = true;
+    }
+    pool->cv.notify_all();
+    for (auto& t : pool->th) t.join();
+    pool.reset();
+  }
   ~spf_mplan() {
+    stop_pool();
     for (size_t i = 0; i < n_parts; ++i) {
       Part& p = parts[i];
       if (!p.plan) continue;
@@ -211,7 +254,10 @@ struct spf_mplan {
 
 namespace {
 
+std::mutex g_err_mu;  // member errors may come from the enqueue threads
+
 spf_status mfail(spf_mctx* m, spf_status st, const char* fmt, ...) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -479,12 +525,92 @@ spf_status spf_mplan_set_graphs(spf_mplan* mp, int enable) {
   return SPF_OK;
 }
 
+namespace {
+
+// enqueue threads wanted: on when asked, or -- automatically -- when the
+// members with work sit on two or more distinct devices (members of one
+// device share its stream: nothing to overlap)
+bool want_threads(const spf_mplan* mp) {
+  if (mp->threads_mode >= 0) return mp->threads_mode == 1;
+  std::vector<int> devs;
+  for (uint32_t i = 0; i < mp->n_parts; ++i)
+    if (mp->parts[i].plan) devs.push_back(mp->m->members[i]->device);
+  std::sort(devs.begin(), devs.end());
+  return std::unique(devs.begin(), devs.end()) - devs.begin() > 1;
+}
+
+void enqueue_worker(spf_mplan* mp, uint32_t i) {
+  spf_mplan::Pool& P = *mp->pool;
+  uint64_t seen = 0;
+  for (;;) {
+    // spin briefly (back-to-back executes), then sleep until the next one
+    uint64_t g = P.gen.load(std::memory_order_acquire);
+    for (int k = 0; g == seen && k < 20000 && !P.stop.load(std::memory_order_relaxed); ++k) {
+      __builtin_ia32_pause();
+      g = P.gen.load(std::memory_order_acquire);
+    }
+    if (g == seen) {
+      std::unique_lock<std::mutex> lk(P.mu);
+      P.cv.wait(lk, [&] { return P.stop || P.gen.load(std::memory_order_acquire) != seen; });
+      if (P.stop) return;
+      g = P.gen.load(std::memory_order_acquire);
+    }
+    if (P.stop) return;
+    seen = g;
+    if (mp->parts[i].plan) {
+      P.st[i] = run_part(mp, i);
+      mp->enq_ns[i] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now() - P.t0).count();
+    }
+    P.pending.fetch_sub(1, std::memory_order_acq_rel);
+  }
+}
+
+}  // namespace
+
+spf_status spf_mplan_set_enqueue_threads(spf_mplan* mp, int mode) {
+  if (!mp || mode < -1 || mode > 1) return SPF_E_INVALID;
+  mp->threads_mode = mode;
+  if (!want_threads(mp)) mp->stop_pool();
+  return SPF_OK;
+}
+
+spf_status spf_mplan_enqueue_ns(const spf_mplan* mp, uint64_t* out, uint32_t n, int* threaded) {
+  if (!mp || (n && !out)) return SPF_E_INVALID;
+  for (uint32_t i = 0; i < n && i < mp->n_parts; ++i) out[i] = i < mp->enq_ns.size() ? mp->enq_ns[i] : 0;
+  if (threaded) *threaded = mp->pool ? 1 : 0;
+  return SPF_OK;
+}
+
 spf_status spf_mplan_execute(spf_mplan* mp) {
   if (!mp) return mfail(nullptr, SPF_E_INVALID, "spf_mplan_execute: NULL plan");
-  for (uint32_t i = 0; i < mp->n_parts; ++i) {
-    if (!mp->parts[i].plan) continue;
-    const spf_status st = run_part(mp, i);
-    if (st != SPF_OK) return st;
+  mp->enq_ns.assign(mp->n_parts, 0);
+  const auto t0 = std::chrono::steady_clock::now();
+  if (want_threads(mp)) {
+    if (!mp->pool) {
+      mp->pool = std::make_unique<spf_mplan::Pool>();
+      mp->pool->st.assign(mp->n_parts, SPF_OK);
+      for (uint32_t i = 0; i < mp->n_parts; ++i) mp->pool->th.emplace_back(enqueue_worker, mp, i);
+    }
+    spf_mplan::Pool& P = *mp->pool;
+    P.t0 = t0;
+    P.pending.store(mp->n_parts, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      P.gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    P.cv.notify_all();
+    while (P.pending.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    for (uint32_t i = 0; i < mp->n_parts; ++i)
+      if (P.st[i] != SPF_OK) return P.st[i];
+  } else {
+    for (uint32_t i = 0; i < mp->n_parts; ++i) {
+      if (!mp->parts[i].plan) continue;
+      const spf_status st = run_part(mp, i);
+      if (st != SPF_OK) return st;
+      mp->enq_ns[i] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now() - t0).count();
+    }
   }
   if (mp->timing_cap) ++mp->timing_n;
   ++mp->executes;
@@ -760,6 +886,161 @@ spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32
     for (size_t q = 0; q < got[r].size(); ++q) digests[slot[r][q]] = got[r][q];
   }
   if (kernel_ms) *kernel_ms = worst;
+  return SPF_OK;
+}
+
+namespace {
+
+// a member's record regions from per-slot capacities: bases, pool, uploads
+spf_status db_layout(spf_mplan* mp, uint32_t r, hipStream_t s) {
+  spf_mctx* m = mp->m;
+  spf_mplan::Part& p = mp->parts[r];
+  const size_t n = p.h_dbcap.size();
+  p.h_dbbase.assign(n, 0);
+  unsigned long long tot = 0;
+  for (size_t k = 0; k < n; ++k) {
+    p.h_dbbase[k] = tot;
+    tot += p.h_dbcap[k];
+  }
+  M_HIP(m, hipStreamSynchronize(s));  // no queued upload still reads the old host tables
+  M_HIP(m, p.dbpool.alloc(std::max<unsigned long long>(tot, 1)));
+  M_HIP(m, p.dbbase.upload(p.h_dbbase.data(), n, s));
+  M_HIP(m, p.dbcap.upload(p.h_dbcap.data(), n, s));
+  return SPF_OK;
+}
+
+}  // namespace
+
+spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32_t n_me,
+                                   const uint32_t* set_ptr, const uint32_t* set_nodes, uint32_t n_sets,
+                                   uint32_t flags, uint64_t* n_records, double* kernel_ms) {
+  if (!mp || (n_me && !me_req) || !set_ptr)
+    return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_route_records: NULL argument");
+  spf_mctx* m = mp->m;
+  spf_ctx* c0 = m->members[0];
+  for (uint32_t t = 0; t < n_me; ++t)
+    if (me_req[t] >= mp->n_src) return mfail(m, SPF_E_INVALID, "me %u is not a request index", me_req[t]);
+  const bool lfa = (flags & SPF_ROUTE_LFA) != 0;
+  if (const spf_status st = route_prepare(mp, set_ptr, set_nodes, n_sets, lfa, nullptr, 0, me_req, n_me);
+      st != SPF_OK)
+    return st;
+  mp->db_loc.assign(n_me, {0u, 0u});
+  mp->db_sets = n_sets;
+  std::vector<std::vector<uint32_t>> mine(mp->n_parts);
+  for (uint32_t t = 0; t < n_me; ++t) {
+    const uint32_t r = mp->owner[me_req[t]];
+    mp->db_loc[t] = {r, (uint32_t)mine[r].size()};
+    mine[r].push_back(mp->srcs[me_req[t]]);
+  }
+  std::vector<hipEvent_t> ev(2 * mp->n_parts, nullptr);
+  std::vector<std::vector<uint32_t>> fl(mp->n_parts);
+  IssuedGuard guard{m, {}, &ev};  // declared after fl: drains before it is freed
+  auto launch = [&](uint32_t r) -> spf_status {
+    spf_mplan::Part& p = mp->parts[r];
+    spf_ctx* c = m->members[r];
+    const hipStream_t s = m->exec[r];
+    const uint32_t n = (uint32_t)mine[r].size();
+    M_HIP(m, hipMemsetAsync(p.dbcur.p, 0, 4ull * n, s));
+    M_HIP(m, hipMemsetAsync(p.dbflags.p, 0, 4, s));
+    if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r], s));
+    RouteDbOut db;
+    db.hdr = p.dbhdr.p;
+    db.pool = p.dbpool.p;
+    db.base = p.dbbase.p;
+    db.cap = p.dbcap.p;
+    db.cursor = p.dbcur.p;
+    db.flags = p.dbflags.p;
+    const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, n, p.rsp.p, p.rsn.p, n_sets, lfa,
+                                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s, &db);
+    if (st != SPF_OK) return member_fail(m, r, st);
+    if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r + 1], s));
+    fl[r].resize(n + 1);
+    M_HIP(m, hipMemcpyAsync(fl[r].data(), p.dbcur.p, 4ull * n, hipMemcpyDeviceToHost, s));
+    M_HIP(m, hipMemcpyAsync(fl[r].data() + n, p.dbflags.p, 4, hipMemcpyDeviceToHost, s));
+    return SPF_OK;
+  };
+  for (uint32_t r = 0; r < mp->n_parts; ++r) {
+    spf_mplan::Part& p = mp->parts[r];
+    if (mine[r].empty()) continue;
+    spf_ctx* c = m->members[r];
+    M_HIP(m, hipSetDevice(c->device));
+    guard.members.push_back(r);
+    const hipStream_t s = m->exec[r];
+    const uint32_t n = (uint32_t)mine[r].size();
+    if (kernel_ms) {
+      M_HIP(m, hipEventCreate(&ev[2 * r]));
+      M_HIP(m, hipEventCreate(&ev[2 * r + 1]));
+    }
+    if (p.db_me != mine[r] || p.h_dbcap.size() != n) {  // a first guess of the regions: 4 hops a route
+      M_HIP(m, hipStreamSynchronize(s));
+      p.db_me = mine[r];
+      p.h_dbcap.assign(n, 0);
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t v = mine[r][k];
+        p.h_dbcap[k] = (uint32_t)std::min<uint64_t>(
+            0xFFFFFFFFull, (uint64_t)n_sets * std::min<uint32_t>(4, c0->row_ptr[v + 1] - c0->row_ptr[v]));
+      }
+      M_HIP(m, p.rme.upload(p.db_me.data(), n, s));
+      if (const spf_status st = db_layout(mp, r, s); st != SPF_OK) return st;
+    } else {
+      M_HIP(m, p.rme.upload(p.db_me.data(), n, s));
+    }
+    M_HIP(m, p.dbhdr.alloc(std::max<size_t>(1, (size_t)n * n_sets)));
+    M_HIP(m, p.dbcur.alloc(n));
+    M_HIP(m, p.dbflags.alloc(1));
+    if (const spf_status st = launch(r); st != SPF_OK) return st;
+  }
+  double worst = 0;
+  uint64_t total = 0;
+  for (uint32_t r = 0; r < mp->n_parts; ++r) {
+    spf_mplan::Part& p = mp->parts[r];
+    if (mine[r].empty()) continue;
+    M_HIP(m, hipSetDevice(m->members[r]->device));
+    const hipStream_t s = m->exec[r];
+    M_HIP(m, hipStreamSynchronize(s));
+    const uint32_t n = (uint32_t)mine[r].size();
+    if (fl[r][n] & 2u) return mfail(m, SPF_E_UNSUPPORTED, "a next-hop metric exceeds 2^32 - 1");
+    if (fl[r][n] & 1u) {  // a region was too small: size them from the cursors and run again
+      p.h_dbcap.assign(fl[r].begin(), fl[r].begin() + n);
+      if (const spf_status st = db_layout(mp, r, s); st != SPF_OK) return st;
+      if (const spf_status st = launch(r); st != SPF_OK) return st;
+      M_HIP(m, hipStreamSynchronize(s));
+      if (fl[r][n]) return mfail(m, SPF_E_STATE, "route records still overflow after sizing (flags %u)", fl[r][n]);
+    }
+    p.h_dbcnt.assign(fl[r].begin(), fl[r].begin() + n);
+    for (uint32_t k = 0; k < n; ++k) total += p.h_dbcnt[k];
+    if (kernel_ms) {
+      float t = 0;
+      M_HIP(m, hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]));
+      worst = std::max(worst, (double)t);
+    }
+  }
+  if (n_records) *n_records = total;
+  if (kernel_ms) *kernel_ms = worst;
+  return SPF_OK;
+}
+
+spf_status spf_mplan_route_db(spf_mplan* mp, uint32_t t, uint64_t* hdr, uint64_t* rec, uint64_t cap,
+                              uint64_t* n) {
+  if (!mp || t >= mp->db_loc.size())
+    return mfail(mp ? mp->m : nullptr, SPF_E_INVALID, "spf_mplan_route_db: no such me (call spf_mplan_route_records)");
+  spf_mctx* m = mp->m;
+  const auto [r, k] = mp->db_loc[t];
+  spf_mplan::Part& p = mp->parts[r];
+  const uint32_t cnt = p.h_dbcnt[k];
+  if (n) *n = cnt;
+  M_HIP(m, hipSetDevice(m->members[r]->device));
+  const hipStream_t s = m->exec[r];
+  if (hdr && mp->db_sets)
+    M_HIP(m, hipMemcpyAsync(hdr, p.dbhdr.p + (size_t)k * mp->db_sets, 8ull * mp->db_sets, hipMemcpyDeviceToHost, s));
+  if (rec && cnt) {
+    if (cap < cnt) {
+      M_HIP(m, hipStreamSynchronize(s));
+      return mfail(m, SPF_E_NOMEM, "route db of %u records, room for %llu", cnt, (unsigned long long)cap);
+    }
+    M_HIP(m, hipMemcpyAsync(rec, p.dbpool.p + p.h_dbbase[k], 8ull * cnt, hipMemcpyDeviceToHost, s));
+  }
+  M_HIP(m, hipStreamSynchronize(s));
   return SPF_OK;
 }
 

@@ -555,6 +555,20 @@ class SpfMultiPlan(NativeHandle):
     def set_graphs(self, enable: bool) -> None:
         self._eng._err(N.lib.spf_mplan_set_graphs(self._h, int(bool(enable))))
 
+    def set_enqueue_threads(self, mode: int) -> None:
+        """1: each member's execute enqueued from its own host thread, 0: one
+        after another from the caller's, -1: threads for distinct devices."""
+        self._eng._err(N.lib.spf_mplan_set_enqueue_threads(self._h, int(mode)))
+
+    def enqueue_ns(self) -> Tuple[np.ndarray, bool]:
+        """The last execute's host enqueue: per member, ns from the execute's
+        start until its launches were enqueued; and whether threads issued them."""
+        n = len(self.shard_sizes())
+        out = np.zeros(max(1, n), np.uint64)
+        thr = C.c_int()
+        self._eng._err(N.lib.spf_mplan_enqueue_ns(self._h, N.ptr(out, C.c_uint64), n, C.byref(thr)))
+        return out[:n], bool(thr.value)
+
     def execute(self) -> None:
         self._eng._err(N.lib.spf_mplan_execute(self._h))
 

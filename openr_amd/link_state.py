@@ -497,6 +497,46 @@ class LinkState(N.NativeHandle):
         N.raise_for(st, N.global_error())
         return out[: len(mes)], ms.value
 
+    def allSourcesRouteRecords(self, set_ptr, set_nodes, lfa: bool, mes=None):
+        """Every node's (or the csr ids in `mes`) route database materialised
+        on its owning GPU from the resident all-sources pass
+        (spf_mplan_route_records): returns (records over every node, the
+        slowest member's kernel ms); read one node's with allSourcesRouteDb."""
+        import numpy as np
+
+        mp = N.lib.ls_all_sources_plan(self._h)
+        if not mp:
+            raise RuntimeError("allSourcesRouteRecords: no resident all-sources pass")
+        n = self._csr_sizes()[0]
+        mes = np.arange(n, dtype=np.uint32) if mes is None else np.ascontiguousarray(mes, np.uint32)
+        sp = np.ascontiguousarray(set_ptr, np.uint32)
+        sn = np.ascontiguousarray(set_nodes if len(set_nodes) else [0], np.uint32)
+        tot, ms = C.c_uint64(), C.c_double()
+        st = N.lib.spf_mplan_route_records(C.c_void_p(mp), N.ptr(mes), len(mes), N.ptr(sp), N.ptr(sn),
+                                           len(sp) - 1, N.SPF_ROUTE_LFA if lfa else 0, C.byref(tot),
+                                           C.byref(ms))
+        N.raise_for(st, N.global_error())
+        self._db_sets = len(sp) - 1
+        return int(tot.value), ms.value
+
+    def allSourcesRouteDb(self, t: int):
+        """Node t's (index into the last allSourcesRouteRecords' node list)
+        database: (headers [n_sets] u64 = offset | count << 32, records u64 =
+        CSR edge | metric << 32)."""
+        import numpy as np
+
+        mp = N.lib.ls_all_sources_plan(self._h)
+        if not mp:
+            raise RuntimeError("allSourcesRouteDb: no resident all-sources pass")
+        n = C.c_uint64()
+        hdr = np.zeros(max(1, self._db_sets), np.uint64)
+        N.raise_for(N.lib.spf_mplan_route_db(C.c_void_p(mp), int(t), N.ptr(hdr, C.c_uint64), None, 0,
+                                             C.byref(n)), N.global_error())
+        rec = np.zeros(max(1, n.value), np.uint64)
+        N.raise_for(N.lib.spf_mplan_route_db(C.c_void_p(mp), int(t), None, N.ptr(rec, C.c_uint64),
+                                             n.value, C.byref(n)), N.global_error())
+        return hdr[: self._db_sets], rec[: n.value]
+
     def debugPhaseNs(self) -> Tuple[int, int, int, int]:
         """Cumulative getSpfResult cost (ns): plan build, GPU execute + copy
         back, pathLinks, host assembly (ls_debug_phase_ns)."""

@@ -1704,10 +1704,16 @@ int orc_ls_ksp2_digests(orc_ls* p, const char* blob, const uint32_t* off, const 
 // perDestination = false, one area), exactly as orc_ls_nexthops_json, reduced
 // to sum over sets with a kept link of mix(mix(0x9e3779b97f4a7c15 (p+1) +
 // shortest) + sum over kept links of mix(keyHash(link) + (u32) metric) + p).
+// lfa bit 1 (value 2): key each route by its smallest kept next-hop metric
+// instead of `shortest` -- what a materialised route database
+// (spf_mplan_route_records) holds; they differ where an LFA neighbour that
+// does not carry transit (overloaded) offers a smaller metric.
 int orc_ls_route_digests(orc_ls* p, const char* blob, const uint32_t* off, const uint32_t* len,
                          uint32_t n, const uint32_t* mes, uint32_t n_me, const uint32_t* set_ptr,
                          const uint32_t* set_nodes, uint32_t n_sets, int lfa, int threads,
                          uint64_t* out) {
+  const bool kept_min = (lfa & 2) != 0;
+  lfa &= 1;
   const orc::NameIds t(blob, off, len, n);
   const orc::LinkState& ls = p->ls;
   // the SPF results every me needs (its own, with LFA its neighbours'):
@@ -1775,16 +1781,18 @@ int orc_ls_route_digests(orc_ls* p, const char* blob, const uint32_t* off, const
       }
       uint64_t rec = 0;
       uint32_t kept = 0;
+      orc::Metric least = std::numeric_limits<orc::Metric>::max();
       for (const auto& l : ls.linksFrom(me)) {
         auto f = nextHopNodes.find(l->other(me));
         if (f == nextHopNodes.end() || !l->isUp()) continue;
         const orc::Metric over = l->metricFrom(me) + f->second;
         if (!lfa && over != shortest) continue;
         rec += mix64(orc::linkKeyHash(*l) + (uint32_t)over);
+        least = std::min(least, over);
         ++kept;
       }
       if (kept)
-        acc += mix64(mix64(0x9e3779b97f4a7c15ULL * (q + 1) + shortest) + rec + q);
+        acc += mix64(mix64(0x9e3779b97f4a7c15ULL * (q + 1) + (kept_min ? least : shortest)) + rec + q);
     }
     out[i] = acc;
   });

@@ -89,3 +89,52 @@ def planar_rows(ks, dist, mats, pitch):
             rows.append(np.packbits(row, bitorder="little").view(np.uint32))
     nh = np.concatenate(rows) if rows else np.zeros(0, np.uint32)
     return d32, nh
+
+
+def _mix64(z):
+    """splitmix64's finaliser over a uint64 array (wrapping arithmetic)."""
+    import numpy as np
+
+    z = np.asarray(z, np.uint64)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return z ^ (z >> np.uint64(31))
+
+
+def route_db_digest(hdr, rec, link_id, link_hash) -> int:
+    """One node's materialised route database (spf_mplan_route_records:
+    headers offset | count << 32, records CSR edge | metric << 32) reduced
+    with spf_mplan_route_digests' formula keyed by the smallest next-hop
+    metric (oracle route_digests(kept_min=True)): per set p with next hops,
+    mix(mix(K (p + 1) + least) + sum mix(link_hash[link] + metric) + p),
+    summed over p.  (Without LFA, least == the shortest distance and this is
+    the digest kernel's value.)  Also checks each route's next hops are in
+    link order."""
+    import numpy as np
+
+    hdr = np.asarray(hdr, np.uint64)
+    rec = np.asarray(rec, np.uint64)
+    off = (hdr & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    cnt = (hdr >> np.uint64(32)).astype(np.int64)
+    edge = (rec & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    met = rec >> np.uint64(32)
+    lh = np.asarray(link_hash, np.uint64)
+    per = _mix64(lh[np.asarray(link_id, np.int64)[edge]] + met) if len(rec) else np.zeros(0, np.uint64)
+    nz = np.nonzero(cnt)[0]
+    if len(nz) == 0:
+        return 0
+    c = cnt[nz]
+    seg = np.concatenate([[0], np.cumsum(c)[:-1]])
+    idx = np.repeat(off[nz], c) + (np.arange(int(c.sum())) - np.repeat(seg, c))
+    assert idx.max() < len(rec), "a route's records run past the node's region"
+    e = edge[idx]
+    inner = np.ones(len(idx), bool)
+    inner[seg] = False
+    assert np.all(np.diff(e)[inner[1:]] > 0), "next hops not in link order"
+    with np.errstate(over="ignore"):
+        sums = np.add.reduceat(per[idx], seg, dtype=np.uint64)
+        shortest = np.minimum.reduceat(met[idx], seg)
+        p = nz.astype(np.uint64)
+        h = _mix64(_mix64(np.uint64(0x9e3779b97f4a7c15) * (p + np.uint64(1)) + shortest) + sums + p)
+        total = h.sum(dtype=np.uint64)
+    return int(total)

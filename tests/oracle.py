@@ -393,15 +393,17 @@ def node_area_map_order(ops: Sequence[Tuple[int, Tuple[str, str]]]) -> List[Tupl
 
 def route_digests(orc: "OracleLinkState", table: NameTable, mes: Sequence[int],
                   set_ptr: np.ndarray, set_nodes: np.ndarray, lfa: bool,
-                  threads: int = 0) -> np.ndarray:
+                  threads: int = 0, kept_min: bool = False) -> np.ndarray:
     """spf_mplan_route_digests' reduction of the reference's route selection
-    (orc_ls_route_digests): one u64 per me (ids into `table`)."""
+    (orc_ls_route_digests): one u64 per me (ids into `table`).  kept_min:
+    each route keyed by its smallest next-hop metric instead of the shortest
+    distance (the form a materialised database is checked in)."""
     mes = np.ascontiguousarray(mes, np.uint32)
     sp = np.ascontiguousarray(set_ptr, np.uint32)
     sn = np.ascontiguousarray(set_nodes if len(set_nodes) else [0], np.uint32)
     out = np.zeros(max(1, len(mes)), np.uint64)
     rc = lib.orc_ls_route_digests(orc._h, table.blob, _p(table.offs), _p(table.lens), table.n,
-                                  _p(mes), len(mes), _p(sp), _p(sn), len(sp) - 1, int(lfa),
+                                  _p(mes), len(mes), _p(sp), _p(sn), len(sp) - 1, int(lfa) | (2 if kept_min else 0),
                                   threads or host_threads(), _p(out, C.c_uint64))
     assert rc == 0
     return out[: len(mes)]

@@ -57,6 +57,34 @@ def test_multi_context_every_source_matches_oracle(name, world):
     assert len(bad) == 0, f"{name} x{world}: {len(bad)} sources differ, first {bad[:5]}"
 
 
+def test_multi_context_enqueue_threads_every_source_matches_oracle():
+    """Each member's execute issued from its own host thread
+    (spf_mplan_set_enqueue_threads(1)): the same digests, repeated executes,
+    and the enqueue times are reported for every member."""
+    meta, g = golden("fabric_full")
+    ls, names, csr, cd = _make("fabric_full")
+    want = np.zeros(len(names), np.uint64)
+    want[g["srcs"].astype(np.int64)] = g["digest"]
+    with SpfMultiEngine([0] * 4) as m:
+        m.load(*csr)
+        p = m.plan(np.arange(len(names)))
+        p.set_enqueue_threads(1)
+        for _ in range(3):
+            p.execute()
+            ns, threaded = p.enqueue_ns()
+            assert threaded and len(ns) == 4 and (ns > 0).all()
+        p.synchronize()
+        got = p.digest()
+        p.set_enqueue_threads(0)
+        p.execute()
+        ns, threaded = p.enqueue_ns()
+        assert not threaded and (np.diff(ns.astype(np.int64)) > 0).all()  # one after another
+        p.synchronize()
+        assert np.array_equal(p.digest(), got)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} sources differ, first {bad[:5]}"
+
+
 def test_multi_context_rows_bitmaps_preds_equal_one_plan():
     topo = T.fabric(1000, full=True)
     ls = LinkState(device=-1)

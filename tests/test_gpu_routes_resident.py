@@ -9,6 +9,8 @@ CS-2) computes, with no SPF per node.
   (oracle/spf_oracle.cpp orc_ls_route_digests), on random multigraphs with
   drained nodes and links, a WAN and a fabric, members of 1, 2 and 3 on one
   GPU;
+* every node's materialised route database (spf_mplan_route_records) read
+  back and reduced with the same digest, against the oracle's;
 * SpfSolver.buildRouteDb answered from the resident pass (spf_mplan_routes)
   equals the one-node plan path (spf_routes), before and after a
   publication drops the pass.
@@ -17,6 +19,7 @@ CS-2) computes, with no SPF per node.
 import numpy as np
 import pytest
 
+from helpers import route_db_digest
 from oracle import NameTable, OracleLinkState, route_digests
 from openr_amd import topology as T
 from openr_amd.link_state import LinkState
@@ -62,6 +65,48 @@ def test_every_node_route_digests_match_oracle(name, make, members, lfa):
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, f"{len(bad)} nodes differ, first {[names[i] for i in bad[:5]]}"
     assert np.count_nonzero(want) > len(names) // 2  # routes exist
+
+
+@pytest.mark.parametrize("name,make", GRAPHS, ids=[g[0] for g in GRAPHS])
+@pytest.mark.parametrize("members", [1, 3])
+@pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
+def test_every_node_materialised_route_db_matches_oracle(name, make, members, lfa):
+    """spf_mplan_route_records: every node's database, read back and reduced
+    with the digest formula, equals the oracle's digest; the record count
+    is the sum of the headers' counts; a second call (regions sized from the
+    first) gives the same databases."""
+    topo = make()
+    with LinkState(devices=[0] * members) as ls:
+        ls.updateAdjacencyDatabases(topo.lsdb)
+        ls.prefetchAllSources()
+        names, _rp, _col, _met, lid = ls.flatten()[:5]
+        names = list(names)
+        lh = ls.linkValueHashes()
+        ptr, nodes = sets_for(len(names), np.random.default_rng(len(names)))
+        dig_kernel, _ = ls.allSourcesRouteDigests(ptr, nodes, lfa)
+        for call in range(2):
+            total, ms = ls.allSourcesRouteRecords(ptr, nodes, lfa)
+            assert ms >= 0
+            got = np.zeros(len(names), np.uint64)
+            seen = 0
+            for t in range(len(names)):
+                hdr, rec = ls.allSourcesRouteDb(t)
+                assert len(hdr) == len(ptr) - 1
+                assert int((hdr >> np.uint64(32)).sum()) == len(rec)
+                seen += len(rec)
+                got[t] = route_db_digest(hdr, rec, lid, lh)
+            assert seen == total
+            if not lfa:  # (keyed alike only without LFA)
+                assert np.array_equal(got, dig_kernel), f"call {call}: records differ from the digest kernel"
+            if call == 0:
+                first = got.copy()
+            else:
+                assert np.array_equal(got, first)
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    want = route_digests(orc, NameTable(names), np.arange(len(names)), ptr, nodes, lfa, kept_min=True)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, f"{len(bad)} nodes differ, first {[names[i] for i in bad[:5]]}"
 
 
 @pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
