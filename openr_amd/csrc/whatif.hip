@@ -87,6 +87,10 @@ struct WiGraph {
   uint32_t N, src, W;
   uint32_t hop = 0;  // hop counts: every up link weighs 1 (useLinkMetric = false)
   uint32_t* fault = nullptr;  // the context's barrier-timeout word (spf_device_check)
+  // per CSR edge, interleaved: {col, wt, link, wt of the reverse edge} -- one
+  // 16-byte load where the wave teams' repairs read four arrays (and the
+  // rev -> wt chain) at random nodes (what-if plans)
+  const uint4* ed = nullptr;
 };
 
 // directed weight of the edge reverse to e (tail -> head of the in-edge)
@@ -1150,8 +1154,9 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         uint32_t c = 0;
         bool won = false;
         if (act) {
-          c = g.col[e];
-          if (dk + g.wt[e] == B.dist[c]) won = atomicCAS(&mark[c], kInf, kBusy) == kInf;
+          const uint4 q = g.ed[e];
+          c = q.x;
+          if (dk + q.y == B.dist[c]) won = atomicCAS(&mark[c], kInf, kBusy) == kInf;
         }
         const uint64_t wm = __ballot(won);
         if (wm) {
@@ -1201,11 +1206,12 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
     const uint32_t v = in ? dlist[i] : 0u;
     wave_edges(g.row_ptr, v, in, [&](uint32_t k, uint32_t e, bool act) {
       uint32_t s = kInf;
-      if (act && g.link[e] != l) {
-        const uint32_t u = g.col[e];
+      const uint4 q = act ? g.ed[e] : make_uint4(0u, 0u, l, 0u);
+      if (act && q.z != l) {
+        const uint32_t u = q.x;
         if (ldw<GROUP>(&mark[u]) == kInf && !(g.ovl[u] && u != g.src)) {
           const uint32_t du = B.dist[u];
-          if (du != kInf) s = du + g.wt[g.rev[e]];
+          if (du != kInf) s = du + q.w;
         }
       }
       if (s != kInf) {
@@ -1319,15 +1325,16 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
         const uint32_t ik = lane_pull(i, k), tk = lane_pull(transit, k), jk = lane_pull(jb, k);
         uint32_t u = 0, mu = kInf;
         bool tight = false, from_src = false;
-        if (act && g.link[e] != l) {
-          u = g.col[e];
+        const uint4 q = act ? g.ed[e] : make_uint4(0u, 0u, l, 0u);
+        if (act && q.z != l) {
+          u = q.x;
           mu = chk(ldw<GROUP>(&mark[u]), n, true, 13, kInf);
           if (!(g.ovl[u] && u != g.src)) {
             const uint32_t du = mu != kInf ? ldw<GROUP>(&dnew[mu]) : B.dist[u];
-            tight = du != kInf && du + in_w(g, e) == t;
+            tight = du != kInf && du + (g.hop ? 1u : q.w) == t;
           }
           if (tk && mu != kInf) {  // relax v -> u (u pending: its value only drops)
-            const uint32_t nd = t + g.wt[e];
+            const uint32_t nd = t + q.y;
             if (nd < atomicMin(&dnew[mu], nd)) m = min(m, nd);
           }
           if (tight && u == g.src) {
@@ -1480,6 +1487,58 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
   return true;
 }
 
+// A wave team's node -> D-index map: an open-addressed table of T = 4 * cap
+// (a power of two) u64 slots, key (node) in the low word, value (D index, or
+// kBusy while being claimed) in the high word, linear probing from a
+// multiplicative hash.  It replaces an N-word `mark` array per wave team:
+// 4,096 teams x 250k nodes x 4 B = 4 GB of scratch whose random lookups
+// missed every cache -- the tables take 32 KB a team.
+// Slots start (and are always left) empty (~0): a repair clears the slots it
+// used, an aborted one the whole table.
+struct WaveSet {
+  unsigned long long* tab;
+  uint32_t mask, shift;  // T - 1, 32 - log2(T)
+};
+constexpr unsigned long long kSlotEmpty = ~0ull;
+__device__ __forceinline__ unsigned long long ws_ld(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ws_st(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// insert v (value kBusy): its slot, or ~0u when v is present already; `full`
+// when no slot is left (the caller aborts the repair)
+__device__ __forceinline__ uint32_t ws_claim(const WaveSet& s, uint32_t v, bool& full) {
+  uint32_t h = (v * 0x9E3779B1u) >> s.shift;
+  for (uint32_t k = 0; k <= s.mask; ++k, h = (h + 1) & s.mask) {
+    const unsigned long long old = atomicCAS(&s.tab[h], kSlotEmpty, ((unsigned long long)kBusy << 32) | v);
+    if (old == kSlotEmpty) return h;
+    if ((uint32_t)old == v) return ~0u;
+  }
+  full = true;
+  return ~0u;
+}
+// v's slot, or ~0u when absent
+__device__ __forceinline__ uint32_t ws_slot(const WaveSet& s, uint32_t v) {
+  uint32_t h = (v * 0x9E3779B1u) >> s.shift;
+  for (uint32_t k = 0; k <= s.mask; ++k, h = (h + 1) & s.mask) {
+    const unsigned long long x = ws_ld(&s.tab[h]);
+    if ((uint32_t)x == v) return h;
+    if (x == kSlotEmpty) return ~0u;
+  }
+  return ~0u;
+}
+// v's value (its D index), kInf when absent
+__device__ __forceinline__ uint32_t ws_find(const WaveSet& s, uint32_t v) {
+  uint32_t h = (v * 0x9E3779B1u) >> s.shift;
+  for (uint32_t k = 0; k <= s.mask; ++k, h = (h + 1) & s.mask) {
+    const unsigned long long x = ws_ld(&s.tab[h]);
+    if ((uint32_t)x == v) return (uint32_t)(x >> 32);
+    if (x == kSlotEmpty) return kInf;
+  }
+  return kInf;
+}
+
 // A wave team's repair (|D| <= cap): repair()'s three phases -- D discovery,
 // seeds, Dial with next hops inline -- and its digest delta, bit for bit, but
 // with the wave's lanes over the flattened edges of up to 64 nodes at a time
@@ -1491,7 +1550,7 @@ __device__ bool repair(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32
 // a D of <= 64 nodes never leaves the registers (ds_permute).  |D| <= cap <=
 // kDialLevels distinct values, so Dial always settles (no fallback sweeps).
 template <bool CHK, bool GPH = false>
-__device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, uint32_t* dlist,
+__device__ bool repair_wave(const WiGraph& g, const WiBase& B, const WaveSet& hs, uint32_t* dlist,
                             uint32_t* dnew, uint32_t* nhn, uint32_t* ord, uint32_t cap,
                             TeamCtl* ctl, uint32_t lane, uint32_t e_fail, spf_whatif_digest* out,
                             uint64_t* ph) {
@@ -1520,7 +1579,9 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
   const uint32_t b = g.col[e_fail];
   if (lane == 0) {
     dlist[0] = b;
-    stw<false>(&mark[b], 0u);
+    bool full = false;
+    const uint32_t s0 = ws_claim(hs, b, full);  // (the table is empty)
+    ws_st(&hs.tab[s0], b);                      // value 0: D index 0
     stq<false>(&ctl->ndist, 0ull);
     stq<false>(&ctl->nnh, 0ull);
     stq<false>(&ctl->dh, 0ull);
@@ -1541,29 +1602,32 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
       const uint32_t v = i < hi ? chk(ldw<false>(&dlist[i]), g.N, false, 1, b) : 0u;
       const bool x = i < hi && !g.ovl[v];  // drained (v != src): no DAG children
       const uint32_t dv = x ? B.dist[v] : 0u;
+      bool full = false;
       wave_edges(g.row_ptr, v, x, [&](uint32_t k, uint32_t e, bool act) {
         const uint32_t dk = lane_pull(dv, k);
-        uint32_t c = 0;
-        bool won = false;
+        uint32_t c = 0, slot = ~0u;
         if (act) {
-          c = g.col[e];
-          if (dk + g.wt[e] == B.dist[c]) won = atomicCAS(&mark[c], kInf, kBusy) == kInf;
+          const uint4 q = g.ed[e];
+          c = q.x;
+          if (dk + q.y == B.dist[c]) slot = ws_claim(hs, c, full);
         }
+        const bool won = slot != ~0u;
         const uint64_t wm = __ballot(won);
         if (won) {
           const uint32_t idx = n + lanes_below(wm);
-          if (idx < cap) {
-            dlist[idx] = c;
-            stw<false>(&mark[c], idx);
-          } else {
-            stw<false>(&mark[c], kInf);
-          }
+          ws_st(&hs.tab[slot], ((unsigned long long)(idx < cap ? idx : kInf) << 32) | c);
+          if (idx < cap) dlist[idx] = c;
         }
         n += (uint32_t)__popcll(wm);
       });
+      if (__ballot(full)) {  // no slot left: abort as an overflow
+        bad = true;
+        break;
+      }
     }
     lo = hi;
     sync();
+    if (bad) break;
   }
   const bool ovf = n > cap || bad;
   n = min(n, cap);
@@ -1574,8 +1638,8 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
     ph_max<GPH>(ph, 10, n, lane == 0);
     ph_add<GPH>(ph, 11, ovf, lane == 0);
   }
-  if (ovf) {
-    for (uint32_t i = lane; i < n; i += 64) stw<false>(&mark[ldw<false>(&dlist[i])], kInf);
+  if (ovf) {  // slots past the cap hold kInf values: clear the whole table
+    for (uint32_t q = lane; q <= hs.mask; q += 64) ws_st(&hs.tab[q], kSlotEmpty);
     sync();
     return false;
   }
@@ -1588,11 +1652,12 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
     const uint32_t v = i < n ? ldw<false>(&dlist[i]) : 0u;
     wave_edges(g.row_ptr, v, i < n, [&](uint32_t k, uint32_t e, bool act) {
       uint32_t s = kInf;
-      if (act && g.link[e] != l) {
-        const uint32_t u = g.col[e];
-        if (ldw<false>(&mark[u]) == kInf && !(g.ovl[u] && u != g.src)) {
+      const uint4 q = act ? g.ed[e] : make_uint4(0u, 0u, l, 0u);
+      if (act && q.z != l) {
+        const uint32_t u = q.x;
+        if (ws_find(hs, u) == kInf && !(g.ovl[u] && u != g.src)) {
           const uint32_t du = B.dist[u];
-          if (du != kInf) s = du + g.wt[g.rev[e]];
+          if (du != kInf) s = du + q.w;
         }
       }
       if (s != kInf)
@@ -1660,15 +1725,16 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
         const uint32_t ik = lane_pull(i, k), tk = lane_pull(transit, k), jk = lane_pull(jb, k);
         uint32_t u = 0, mu = kInf;
         bool tight = false, from_src = false;
-        if (act && g.link[e] != l) {
-          u = g.col[e];
-          mu = chk(ldw<false>(&mark[u]), n, true, 13, kInf);
+        const uint4 q = act ? g.ed[e] : make_uint4(0u, 0u, l, 0u);
+        if (act && q.z != l) {
+          u = q.x;
+          mu = chk(ws_find(hs, u), n, true, 13, kInf);
           if (!(g.ovl[u] && u != g.src)) {
             const uint32_t du = mu != kInf ? ldw<false>(&dnew[mu]) : B.dist[u];
-            tight = du != kInf && du + in_w(g, e) == t;
+            tight = du != kInf && du + (g.hop ? 1u : q.w) == t;
           }
           if (tk && mu != kInf) {  // relax v -> u (u pending: its value only drops)
-            const uint32_t nd = t + g.wt[e];
+            const uint32_t nd = t + q.y;
             if (nd < atomicMin(&dnew[mu], nd)) m = min(m, nd);
           }
           if (tight && u == g.src) {
@@ -1699,7 +1765,12 @@ __device__ bool repair_wave(const WiGraph& g, const WiBase& B, uint32_t* mark, u
     nd_ += d1 != d0;
     nn_ += diff;
     dh += (d1 == kInf ? 0ull : mix64(base + d1) ^ f1) - (mix64(base + d0) ^ f0);
-    stw<false>(&mark[v], kInf);
+    stw<false>(&dnew[i], ws_slot(hs, v));  // (every lookup is done: find the slots, then clear)
+  }
+  sync();
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t q = ldw<false>(&dnew[i]);
+    if (q <= hs.mask) ws_st(&hs.tab[q], kSlotEmpty);
   }
   if (nd_) atomicAdd(&ctl->ndist, (unsigned long long)nd_);
   if (nn_) atomicAdd(&ctl->nnh, (unsigned long long)nn_);
@@ -1736,13 +1807,13 @@ __device__ __forceinline__ uint64_t* prof_row(unsigned long long* prof, size_t t
 template <int PROF>
 __global__ __launch_bounds__(256) void repair_wave_kernel(
     WiGraph g, WiBase B, const uint2* __restrict__ hot, const uint32_t* __restrict__ n_hot,
-    uint32_t* cursor, uint2* big, uint32_t* n_big, uint32_t* mark, uint32_t* dlist, uint32_t* dnew,
-    uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out, uint32_t cap,
-    unsigned long long* prof, uint32_t prof_rows) {
+    uint32_t* cursor, uint2* big, uint32_t* n_big, unsigned long long* tab, uint32_t* dlist,
+    uint32_t* dnew, uint32_t* nhn, uint32_t* lvl, uint32_t* ord, spf_whatif_digest* out, uint32_t cap,
+    uint32_t tab_log2, unsigned long long* prof, uint32_t prof_rows) {
   __shared__ TeamCtl ctl[4];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t team = (size_t)blockIdx.x * 4 + w;
-  mark += team * g.N;
+  const WaveSet hs{tab + (team << tab_log2), (1u << tab_log2) - 1u, 32u - tab_log2};
   dlist += team * cap;
   dnew += team * cap;
   nhn += team * cap * g.W;
@@ -1757,7 +1828,7 @@ __global__ __launch_bounds__(256) void repair_wave_kernel(
     k = __builtin_amdgcn_readlane(k, 0);
     if (k >= total) break;
     const uint2 h = hot[k];
-    if (!repair_wave<PROF != 0, PROF == 2>(g, B, mark, dlist, dnew, nhn, ord, cap, &ctl[w], lane, h.y,
+    if (!repair_wave<PROF != 0, PROF == 2>(g, B, hs, dlist, dnew, nhn, ord, cap, &ctl[w], lane, h.y,
                                           out + h.x, PROF == 1 ? ph : gph)) {
       if (lane == 0) big[atomicAdd(n_big, 1u)] = h;
     }
@@ -1955,7 +2026,10 @@ struct spf_whatif_plan {
   // SPF_WHATIF_WAVECAP, SPF_WHATIF_CLASSIFY)
   uint32_t wave_cap = kWaveCap, classify_cap = kWaveCap;
   DevBuf<unsigned long long> d_prof;  // SPF_WHATIF_PROF diagnostics
-  DevBuf<uint32_t> w_mark, w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
+  DevBuf<uint32_t> w_dlist, w_dnew, w_nhn, w_lvl, w_ord;  // wave-team scratch
+  DevBuf<unsigned long long> w_tab;  // wave-team node sets (WaveSet), 1 << tab_log2 slots each
+  DevBuf<uint4> d_ed;                 // interleaved edges (WiGraph::ed)
+  uint32_t tab_log2 = 0;
   DevBuf<uint32_t> b_mark, b_dlist, b_dnew, b_nhn, b_lvl, b_ord;  // workgroup-team scratch
   DevBuf<uint32_t> c_mark, c_dlist, c_dnew, c_nhn, c_lvl, c_ord;  // same, concurrent set
   std::vector<hipEvent_t> ev;
@@ -2176,7 +2250,14 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
                    fw.numRegs, p->group, fg.numRegs, p->wave_teams, per_simd_wave);
   }
   const size_t wt = p->wave_teams;
-  HIP_TRY(c, p->w_mark.alloc(wt * N));
+  while ((1u << p->tab_log2) < 4 * p->wave_cap) ++p->tab_log2;
+  {  // WiGraph::ed from the context's host CSR (the plan lives within one graph epoch)
+    std::vector<uint4> ed(std::max<uint32_t>(c->E, 1));
+    for (uint32_t e = 0; e < c->E; ++e) ed[e] = make_uint4(c->col[e], c->wt[e], c->link[e], c->wt[c->rev[e]]);
+    HIP_TRY(c, p->d_ed.upload(ed.data(), ed.size(), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // (ed is freed on return)
+  }
+  HIP_TRY(c, p->w_tab.alloc(wt << p->tab_log2));
   HIP_TRY(c, p->w_dlist.alloc(wt * p->wave_cap));
   HIP_TRY(c, p->w_dnew.alloc(wt * p->wave_cap));
   HIP_TRY(c, p->w_nhn.alloc(wt * p->wave_cap * p->W));
@@ -2196,7 +2277,7 @@ spf_status spf_whatif_plan_create(spf_ctx* c, uint32_t src, const uint32_t* fail
   HIP_TRY(c, p->c_ord.alloc(bt * 2 * N));
   HIP_TRY(c, hipMemsetAsync(p->c_mark.p, 0xFF, bt * N * 4, c->stream));
   // marks start (and are always left) at kInf
-  HIP_TRY(c, hipMemsetAsync(p->w_mark.p, 0xFF, wt * N * 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(p->w_tab.p, 0xFF, (wt << p->tab_log2) * 8, c->stream));
   HIP_TRY(c, hipMemsetAsync(p->b_mark.p, 0xFF, bt * N * 4, c->stream));
   p->prof_mode = whatif_prof_mode();
   if (p->prof_mode) {  // [bt teams][base][wave teams] x 16 (row bounds checked in the kernels)
@@ -2246,6 +2327,7 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
   WiGraph g{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_rev.p, c->d_link.p, c->d_ovl.p,
             p->d_nbr_bit.p, N, p->src, p->W};
   g.fault = c->d_fault.p;
+  g.ed = p->d_ed.p;
   // 1. unfailed SPF, next hops, hash: one grid-resident launch
   {
     BaseArgs a{CoopSssp{c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_ovl.p, c->d_link.p, nullptr,
@@ -2319,18 +2401,18 @@ spf_status spf_whatif_execute(spf_whatif_plan* p, spf_whatif_digest* d_out,
       if (p->prof_mode == 2)
         hipLaunchKernelGGL(repair_wave_kernel<2>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                            p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                           p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
-                           p->w_ord.p, d_out, p->wave_cap, wp, wr);
+                           p->w_tab.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                           p->w_ord.p, d_out, p->wave_cap, p->tab_log2, wp, wr);
       else if (p->prof_mode == 1)
         hipLaunchKernelGGL(repair_wave_kernel<1>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                            p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                           p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
-                           p->w_ord.p, d_out, p->wave_cap, wp, wr);
+                           p->w_tab.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                           p->w_ord.p, d_out, p->wave_cap, p->tab_log2, wp, wr);
       else
         hipLaunchKernelGGL(repair_wave_kernel<0>, dim3(p->wave_teams / 4), dim3(256), 0, s, g, B,
                            p->d_hot.p, p->d_cnt.p, p->d_cnt.p + 1, p->d_big.p, p->d_cnt.p + 2,
-                           p->w_mark.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
-                           p->w_ord.p, d_out, p->wave_cap, nullptr, 0u);
+                           p->w_tab.p, p->w_dlist.p, p->w_dnew.p, p->w_nhn.p, p->w_lvl.p,
+                           p->w_ord.p, d_out, p->wave_cap, p->tab_log2, nullptr, 0u);
     }
     HIP_TRY(c, hipGetLastError());
     hipLaunchKernelGGL(repair_block_kernel<0>, dim3(p->big_teams), dim3(1024), 0, s, g, B, p->d_big.p,
