@@ -542,22 +542,26 @@ spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_
  * selection as spf_mplan_route_digests, written out instead of hashed): what
  * Decision::getDecisionRouteDb(node) returns for every node (Decision.cpp:
  * 1480-1500 -> buildRouteDb :556-722, one area), in device memory.  Per me t
- * and set p a header word = offset | count << 32: the route's `count` next
- * hops are records offset .. offset + count - 1 of me's region, each a u64 =
- * CSR edge (me -> neighbour: link id, interface, neighbour and the metric me
- * advertises come with it) | metric << 32 (w(link) + dist(neighbour, dst)),
- * in me's link order -- getNextHopsThrift's next hops.  Sets without a kept
- * next hop have count 0.  Regions are sized from the previous call's counts
- * (the first call, or one whose counts grew, runs the kernel a second time).
- * SPF_E_UNSUPPORTED when a metric exceeds 2^32 - 1.  *n_records (optional) =
- * records over every me; *kernel_ms (optional) = the slowest member's kernel.
- * The databases stay resident until the next call. */
+ * and set p a header word = offset | count << 32 | stride << 48: the route's
+ * k-th next hop (k < count) is record offset + k * stride of me's region, a
+ * u64 = CSR edge (me -> neighbour: link id, interface, neighbour and the
+ * metric me advertises come with it) | metric << 32 (w(link) +
+ * dist(neighbour, dst)), in me's link order -- getNextHopsThrift's next
+ * hops.  Device layout: me's region is one [deg(me)][256] tile per 256 sets
+ * (stride 256), so consecutive routes' k-th next hops are adjacent; a region
+ * holds ceil(n_sets / 256) * 256 * deg(me) record slots (unused ones are
+ * never written).  Sets without a kept next hop have count 0.
+ * SPF_E_UNSUPPORTED when a metric exceeds 2^32 - 1 or a region 2^32 slots.
+ * *n_records (optional) = records over every me; *kernel_ms (optional) = the
+ * slowest member's kernel.  The databases stay resident until the next call. */
 spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32_t n_me,
                                    const uint32_t* set_ptr, const uint32_t* set_nodes, uint32_t n_sets,
                                    uint32_t flags, uint64_t* n_records, double* kernel_ms);
-/* me t's database from the last spf_mplan_route_records: hdr = [n_sets]
- * headers (may be NULL), rec = its records (cap entries; SPF_E_NOMEM when
- * fewer than *n), *n = its record count.  Waits. */
+/* me t's database from the last spf_mplan_route_records, compacted on the
+ * host: hdr = [n_sets] headers offset | count << 32 (stride 1: route p's next
+ * hops contiguous, routes in set order; may be NULL), rec = its records (cap
+ * entries; SPF_E_NOMEM when fewer than *n; may be NULL), *n = its record
+ * count.  Waits. */
 spf_status spf_mplan_route_db(spf_mplan* mp, uint32_t t, uint64_t* hdr, uint64_t* rec, uint64_t cap,
                               uint64_t* n);
 /* HIP-event time of each member's executes: ms[member] summed over the last

@@ -336,14 +336,14 @@ spf_status resident_order(spf_ctx* c, hipStream_t s);
 spf_status resident_done(spf_ctx* c, hipStream_t s);
 void resident_forget(const spf_ctx* c);
 // Materialised route databases of many `me` (routes.hip kRsDb): per me slot
-// its headers (n_sets words), its region of the record pool (base, cap), the
-// reservation cursor (zeroed before the launch) and the error flags.
+// its headers (n_sets words), where its region of the record pool starts
+// (n_chunks x 256 x deg(me) records), its record count (zeroed before the
+// launch, added to) and the error flags.
 struct RouteDbOut {
   unsigned long long* hdr = nullptr;
   unsigned long long* pool = nullptr;
   const unsigned long long* base = nullptr;
-  const uint32_t* cap = nullptr;
-  uint32_t* cursor = nullptr;
+  uint32_t* count = nullptr;
   uint32_t* flags = nullptr;
 };
 // Route selection over resident rows for many `me` (routes.hip): digests per

@@ -192,9 +192,10 @@ struct spf_mplan {
     // materialised route databases (spf_mplan_route_records): per me slot
     // [n_sets] headers, its region of the record pool, reservation cursors
     DevBuf<unsigned long long> dbhdr, dbpool, dbbase;
-    DevBuf<uint32_t> dbcap, dbcur, dbflags;
-    std::vector<uint32_t> db_me, h_dbcap, h_dbcnt;
+    DevBuf<uint32_t> dbcnt, dbflags;
+    std::vector<uint32_t> db_me, h_dbcnt;
     std::vector<unsigned long long> h_dbbase;
+    uint64_t db_tiles = 0;  // sets rounded up to whole 256-set tiles
   };
   // the last spf_mplan_route_records: request t -> (member, slot), sets
   std::vector<std::pair<uint32_t, uint32_t>> db_loc;
@@ -889,28 +890,6 @@ spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32
   return SPF_OK;
 }
 
-namespace {
-
-// a member's record regions from per-slot capacities: bases, pool, uploads
-spf_status db_layout(spf_mplan* mp, uint32_t r, hipStream_t s) {
-  spf_mctx* m = mp->m;
-  spf_mplan::Part& p = mp->parts[r];
-  const size_t n = p.h_dbcap.size();
-  p.h_dbbase.assign(n, 0);
-  unsigned long long tot = 0;
-  for (size_t k = 0; k < n; ++k) {
-    p.h_dbbase[k] = tot;
-    tot += p.h_dbcap[k];
-  }
-  M_HIP(m, hipStreamSynchronize(s));  // no queued upload still reads the old host tables
-  M_HIP(m, p.dbpool.alloc(std::max<unsigned long long>(tot, 1)));
-  M_HIP(m, p.dbbase.upload(p.h_dbbase.data(), n, s));
-  M_HIP(m, p.dbcap.upload(p.h_dbcap.data(), n, s));
-  return SPF_OK;
-}
-
-}  // namespace
-
 spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32_t n_me,
                                    const uint32_t* set_ptr, const uint32_t* set_nodes, uint32_t n_sets,
                                    uint32_t flags, uint64_t* n_records, double* kernel_ms) {
@@ -932,33 +911,11 @@ spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32
     mp->db_loc[t] = {r, (uint32_t)mine[r].size()};
     mine[r].push_back(mp->srcs[me_req[t]]);
   }
+  // me's region: one [deg(me)][256] tile per chunk of 256 sets (route_sets_kernel<kRsDb>)
+  const uint64_t tiles = ((uint64_t)n_sets + 255) / 256 * 256;
   std::vector<hipEvent_t> ev(2 * mp->n_parts, nullptr);
   std::vector<std::vector<uint32_t>> fl(mp->n_parts);
   IssuedGuard guard{m, {}, &ev};  // declared after fl: drains before it is freed
-  auto launch = [&](uint32_t r) -> spf_status {
-    spf_mplan::Part& p = mp->parts[r];
-    spf_ctx* c = m->members[r];
-    const hipStream_t s = m->exec[r];
-    const uint32_t n = (uint32_t)mine[r].size();
-    M_HIP(m, hipMemsetAsync(p.dbcur.p, 0, 4ull * n, s));
-    M_HIP(m, hipMemsetAsync(p.dbflags.p, 0, 4, s));
-    if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r], s));
-    RouteDbOut db;
-    db.hdr = p.dbhdr.p;
-    db.pool = p.dbpool.p;
-    db.base = p.dbbase.p;
-    db.cap = p.dbcap.p;
-    db.cursor = p.dbcur.p;
-    db.flags = p.dbflags.p;
-    const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, n, p.rsp.p, p.rsn.p, n_sets, lfa,
-                                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s, &db);
-    if (st != SPF_OK) return member_fail(m, r, st);
-    if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r + 1], s));
-    fl[r].resize(n + 1);
-    M_HIP(m, hipMemcpyAsync(fl[r].data(), p.dbcur.p, 4ull * n, hipMemcpyDeviceToHost, s));
-    M_HIP(m, hipMemcpyAsync(fl[r].data() + n, p.dbflags.p, 4, hipMemcpyDeviceToHost, s));
-    return SPF_OK;
-  };
   for (uint32_t r = 0; r < mp->n_parts; ++r) {
     spf_mplan::Part& p = mp->parts[r];
     if (mine[r].empty()) continue;
@@ -967,28 +924,48 @@ spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32
     guard.members.push_back(r);
     const hipStream_t s = m->exec[r];
     const uint32_t n = (uint32_t)mine[r].size();
+    if (p.db_me != mine[r] || p.db_tiles != tiles) {
+      M_HIP(m, hipStreamSynchronize(s));  // no queued upload still reads the host tables
+      p.db_me = mine[r];
+      p.db_tiles = tiles;
+      p.h_dbbase.assign(n, 0);
+      unsigned long long tot = 0;
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t v = mine[r][k];
+        const uint64_t region = tiles * (c0->row_ptr[v + 1] - c0->row_ptr[v]);
+        if (region >= (1ull << 32))
+          return mfail(m, SPF_E_UNSUPPORTED, "route database of node %u: %llu record slots (2^32 max)", v,
+                       (unsigned long long)region);
+        p.h_dbbase[k] = tot;
+        tot += region;
+      }
+      M_HIP(m, p.dbpool.alloc(std::max<unsigned long long>(tot, 1)));
+      M_HIP(m, p.dbbase.upload(p.h_dbbase.data(), n, s));
+    }
+    M_HIP(m, p.rme.upload(p.db_me.data(), n, s));
+    M_HIP(m, p.dbhdr.alloc(std::max<size_t>(1, (size_t)n * n_sets)));
+    M_HIP(m, p.dbcnt.alloc(n));
+    M_HIP(m, p.dbflags.alloc(1));
+    M_HIP(m, hipMemsetAsync(p.dbcnt.p, 0, 4ull * n, s));
+    M_HIP(m, hipMemsetAsync(p.dbflags.p, 0, 4, s));
     if (kernel_ms) {
       M_HIP(m, hipEventCreate(&ev[2 * r]));
       M_HIP(m, hipEventCreate(&ev[2 * r + 1]));
+      M_HIP(m, hipEventRecord(ev[2 * r], s));
     }
-    if (p.db_me != mine[r] || p.h_dbcap.size() != n) {  // a first guess of the regions: 4 hops a route
-      M_HIP(m, hipStreamSynchronize(s));
-      p.db_me = mine[r];
-      p.h_dbcap.assign(n, 0);
-      for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t v = mine[r][k];
-        p.h_dbcap[k] = (uint32_t)std::min<uint64_t>(
-            0xFFFFFFFFull, (uint64_t)n_sets * std::min<uint32_t>(4, c0->row_ptr[v + 1] - c0->row_ptr[v]));
-      }
-      M_HIP(m, p.rme.upload(p.db_me.data(), n, s));
-      if (const spf_status st = db_layout(mp, r, s); st != SPF_OK) return st;
-    } else {
-      M_HIP(m, p.rme.upload(p.db_me.data(), n, s));
-    }
-    M_HIP(m, p.dbhdr.alloc(std::max<size_t>(1, (size_t)n * n_sets)));
-    M_HIP(m, p.dbcur.alloc(n));
-    M_HIP(m, p.dbflags.alloc(1));
-    if (const spf_status st = launch(r); st != SPF_OK) return st;
+    RouteDbOut db;
+    db.hdr = p.dbhdr.p;
+    db.pool = p.dbpool.p;
+    db.base = p.dbbase.p;
+    db.count = p.dbcnt.p;
+    db.flags = p.dbflags.p;
+    const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, n, p.rsp.p, p.rsn.p, n_sets, lfa,
+                                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s, &db);
+    if (st != SPF_OK) return member_fail(m, r, st);
+    if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r + 1], s));
+    fl[r].resize(n + 1);
+    M_HIP(m, hipMemcpyAsync(fl[r].data(), p.dbcnt.p, 4ull * n, hipMemcpyDeviceToHost, s));
+    M_HIP(m, hipMemcpyAsync(fl[r].data() + n, p.dbflags.p, 4, hipMemcpyDeviceToHost, s));
   }
   double worst = 0;
   uint64_t total = 0;
@@ -996,17 +973,9 @@ spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32
     spf_mplan::Part& p = mp->parts[r];
     if (mine[r].empty()) continue;
     M_HIP(m, hipSetDevice(m->members[r]->device));
-    const hipStream_t s = m->exec[r];
-    M_HIP(m, hipStreamSynchronize(s));
+    M_HIP(m, hipStreamSynchronize(m->exec[r]));
     const uint32_t n = (uint32_t)mine[r].size();
     if (fl[r][n] & 2u) return mfail(m, SPF_E_UNSUPPORTED, "a next-hop metric exceeds 2^32 - 1");
-    if (fl[r][n] & 1u) {  // a region was too small: size them from the cursors and run again
-      p.h_dbcap.assign(fl[r].begin(), fl[r].begin() + n);
-      if (const spf_status st = db_layout(mp, r, s); st != SPF_OK) return st;
-      if (const spf_status st = launch(r); st != SPF_OK) return st;
-      M_HIP(m, hipStreamSynchronize(s));
-      if (fl[r][n]) return mfail(m, SPF_E_STATE, "route records still overflow after sizing (flags %u)", fl[r][n]);
-    }
     p.h_dbcnt.assign(fl[r].begin(), fl[r].begin() + n);
     for (uint32_t k = 0; k < n; ++k) total += p.h_dbcnt[k];
     if (kernel_ms) {
@@ -1029,18 +998,30 @@ spf_status spf_mplan_route_db(spf_mplan* mp, uint32_t t, uint64_t* hdr, uint64_t
   spf_mplan::Part& p = mp->parts[r];
   const uint32_t cnt = p.h_dbcnt[k];
   if (n) *n = cnt;
+  if (!hdr && !rec) return SPF_OK;
+  if (rec && cap < cnt)
+    return mfail(m, SPF_E_NOMEM, "route db of %u records, room for %llu", cnt, (unsigned long long)cap);
+  // the device headers and me's tiled region, compacted here: route p's
+  // records contiguous from its header's offset, in set order
+  const uint32_t S = mp->db_sets;
+  std::vector<uint64_t> h(S);
+  const uint32_t me = p.db_me[k];
+  const uint64_t region = p.db_tiles * (mp->m->members[r]->row_ptr[me + 1] - mp->m->members[r]->row_ptr[me]);
+  std::vector<uint64_t> tile(std::max<uint64_t>(region, 1));
   M_HIP(m, hipSetDevice(m->members[r]->device));
   const hipStream_t s = m->exec[r];
-  if (hdr && mp->db_sets)
-    M_HIP(m, hipMemcpyAsync(hdr, p.dbhdr.p + (size_t)k * mp->db_sets, 8ull * mp->db_sets, hipMemcpyDeviceToHost, s));
-  if (rec && cnt) {
-    if (cap < cnt) {
-      M_HIP(m, hipStreamSynchronize(s));
-      return mfail(m, SPF_E_NOMEM, "route db of %u records, room for %llu", cnt, (unsigned long long)cap);
-    }
-    M_HIP(m, hipMemcpyAsync(rec, p.dbpool.p + p.h_dbbase[k], 8ull * cnt, hipMemcpyDeviceToHost, s));
-  }
+  if (S) M_HIP(m, hipMemcpyAsync(h.data(), p.dbhdr.p + (size_t)k * S, 8ull * S, hipMemcpyDeviceToHost, s));
+  if (rec && region)
+    M_HIP(m, hipMemcpyAsync(tile.data(), p.dbpool.p + p.h_dbbase[k], 8ull * region, hipMemcpyDeviceToHost, s));
   M_HIP(m, hipStreamSynchronize(s));
+  uint64_t at = 0;
+  for (uint32_t q = 0; q < S; ++q) {
+    const uint64_t off = h[q] & 0xFFFFFFFFull, c = (h[q] >> 32) & 0xFFFFull, stride = h[q] >> 48;
+    if (rec)
+      for (uint64_t j = 0; j < c; ++j) rec[at + j] = tile[off + j * stride];
+    if (hdr) hdr[q] = at | (c << 32);
+    at += c;
+  }
   return SPF_OK;
 }
 

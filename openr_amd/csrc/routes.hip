@@ -117,23 +117,20 @@ __device__ __forceinline__ uint64_t rmix64(uint64_t z) {
 //              mix(K (p + 1) + shortest) + sum over kept links of
 //              mix(link_hash[l] + (u32) over);
 //   kRsDb      every me's route database materialised (spf_mplan_route_records):
-//              hdr[slot * n_sets + p] = offset | count << 32, the route's next
-//              hops at pool[base[slot] + offset ...], one u64 each = CSR edge |
-//              metric << 32, in link order.  A block's routes of up to kRsKeep
-//              next hops wait in LDS, take one contiguous range in set order
-//              (one atomic on the me's cursor after a block scan) and leave
-//              with coalesced stores; a longer route (LFA on wide nodes)
-//              reserves its own range and the block walks the links again to
-//              write it.
-//              cursor[slot] ends at the me's record count even past cap[slot]
-//              (then nothing is written past it and flags bit 0 is set: the
-//              host sizes the pool from the cursors and runs again); a metric
-//              past 2^32 - 1 sets bit 1.
+//              hdr[slot * n_sets + p] = offset | count << 32 | 256 << 48, the
+//              route's k-th next hop at pool[base[slot] + offset + 256 k], one
+//              u64 each = CSR edge | metric << 32, in link order.  A block's
+//              256 routes share a [deg(me)][256] tile of me's region: the k-th
+//              next hops of consecutive sets sit side by side, so lanes that
+//              keep their k-th next hop at the same link -- consecutive
+//              destinations of one pod do -- store to one line, and the
+//              layout needs no count before the walk (no scan, no atomics, no
+//              second walk); a tile's unused slots are never written.  A metric
+//              past 2^32 - 1 sets flags bit 1.
 constexpr int kRsOne = 0, kRsDigest = 1, kRsDb = 2;
 constexpr uint32_t kRsThreads = 256;
 constexpr uint32_t kRsGroup = 4;  // consecutive me slots per XCD turn
 constexpr uint32_t kRsLinks = 256;  // me's links staged in LDS per pass
-constexpr uint32_t kRsKeep = 16;    // next hops per route staged in LDS (kRsDb)
 template <int MODE>
 __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
     const unsigned long long* __restrict__ rowp, const unsigned long long* __restrict__ nhp,
@@ -156,7 +153,8 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
   const uint32_t slot = ((L / kRsGroup) * 8 + g) * kRsGroup + L % kRsGroup;
   if (slot >= n_me) return;  // whole block
   const uint32_t me = me_ids[slot];
-  const uint32_t p = (i % n_chunks) * kRsThreads + threadIdx.x;
+  const uint32_t chunk = i % n_chunks;
+  const uint32_t p = chunk * kRsThreads + threadIdx.x;
   const uint32_t* Dme = reinterpret_cast<const uint32_t*>(rowp[me]);
   const uint32_t* NHme = reinterpret_cast<const uint32_t*>(nhp[me]);
   const uint32_t e0 = row_ptr[me], e1 = row_ptr[me + 1];
@@ -170,6 +168,9 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
   // a one-member set (a loopback, a node label): its node
   const bool one = e == b + 1;
   const uint32_t d0 = one ? set_nodes[b] : 0u;
+  // (kRsDb) this block's tile of me's region: [deg][kRsThreads] records
+  const uint64_t tile = MODE == kRsDb ? (uint64_t)chunk * kRsThreads * (e1 - e0) : 0ull;
+  unsigned long long* const out = MODE == kRsDb ? db.pool + db.base[slot] + tile + threadIdx.x : nullptr;
   // me's up links, kRsLinks at a time, staged in LDS by the whole block: the
   // neighbour's bitmap index, its row's address, d_me(x), d_x(me), the link's
   // metric and hash -- formerly a dependent scalar chain per link and thread
@@ -177,141 +178,71 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
   // spine's 173 links made its blocks the pass's tail
   __shared__ uint32_t s_j[kRsLinks], s_dmx[kRsLinks], s_back[kRsLinks], s_w[kRsLinks];
   __shared__ unsigned long long s_row[kRsLinks], s_lh[kRsLinks];
-  // (kRsDb) staged next hops, packed: position in me's row | metric << 16
-  __shared__ uint32_t s_keep[MODE == kRsDb ? kRsKeep * kRsThreads : 1];
-  __shared__ uint32_t s_wsum[kRsThreads / 64], s_base, s_long;
   uint64_t rec = 0;
-  uint32_t cnt = 0, first = 0, mine = 0;  // (kRsDb) this route's offset and record count
-  bool big = false, packs = true;
-  for (uint32_t pass = 0;; ++pass) {  // block-uniform; a second pass only in kRsDb
-    rec = 0;
-    cnt = 0;
-    for (uint32_t c0 = e0; c0 < e1; c0 += kRsLinks) {  // block-uniform
-      const uint32_t nl = min(kRsLinks, e1 - c0);
-      __syncthreads();  // the previous chunk's reads are done
-      for (uint32_t t = threadIdx.x; t < nl; t += kRsThreads) {
-        const uint32_t q = c0 + t, x = col[q];
-        const unsigned long long rx = lfa && x != me ? rowp[x] : 0ull;
-        s_j[t] = edge_nb[q];
-        s_dmx[t] = Dme[x];
-        s_w[t] = wt[q];
-        s_row[t] = rx;
-        s_back[t] = rx ? reinterpret_cast<const uint32_t*>(rx)[me] : kInf;
-        if constexpr (MODE == kRsDigest) s_lh[t] = link_hash[link[q]];
-      }
-      __syncthreads();
-      if (shortest == kInf64) continue;  // (every thread still meets the barriers)
-      if (pass && !big) continue;        // second pass: the long routes only
-      for (uint32_t t = 0; t < nl; ++t) {
-        if (s_j[t] == kInf) continue;  // a dead slot (no link)
-        // getNextHopsWithMetric: x is a shortest-path next hop of a min-cost
-        // member (via = shortest - d_me(x)), lowered with LFA to a member's
-        // d_x(dst) < shortest + d_x(me)
-        uint64_t via = kInf64;
-        const uint32_t* bm = NHme + (size_t)s_j[t] * wpm;
-        const uint32_t* Dx = reinterpret_cast<const uint32_t*>(s_row[t]);
-        const uint64_t back = s_back[t];
-        if (one) {  // Dme[d0] == shortest
-          const uint32_t bw = bm[d0 >> 5];
-          const uint32_t dxd = Dx ? Dx[d0] : kInf;  // (Dx is null without LFA)
-          if ((bw >> (d0 & 31)) & 1u) via = shortest - s_dmx[t];
-          if (lfa && dxd != kInf && back != kInf && (uint64_t)dxd < shortest + back &&
-              (via == kInf64 || via > dxd))
-            via = dxd;
-        } else {
-          for (uint32_t k = b; k < e; ++k) {
-            const uint32_t d = set_nodes[k];
-            if (Dme[d] != shortest) continue;
-            if ((bm[d >> 5] >> (d & 31)) & 1u) {
-              via = shortest - s_dmx[t];
-              break;
-            }
-          }
-          if (Dx)
-            for (uint32_t k = b; k < e; ++k) {
-              const uint32_t dxd = Dx[set_nodes[k]];
-              if (dxd == kInf || back == kInf) continue;
-              if ((uint64_t)dxd < shortest + back && (via == kInf64 || via > dxd)) via = dxd;
-            }
-        }
-        if (via == kInf64) continue;
-        const uint64_t over = (uint64_t)s_w[t] + via;
-        if (!lfa && over != shortest) continue;
-        if constexpr (MODE == kRsDigest) {
-          rec += rmix64(s_lh[t] + (uint32_t)over);
-        } else if constexpr (MODE == kRsDb) {
-          if (over >> 32) atomicOr(db.flags, 2u);
-          const unsigned long long r = (unsigned long long)(c0 + t) | (over << 32);
-          if (pass == 0) {
-            const uint32_t at = c0 + t - e0;
-            if (over >= 65536u || at >= 65536u) packs = false;  // written by the second pass
-            else if (cnt < kRsKeep) s_keep[cnt * kRsThreads + threadIdx.x] = at | ((uint32_t)over << 16);
-          } else if (first + mine <= db.cap[slot]) {
-            db.pool[db.base[slot] + first + cnt] = r;
-          }
-        } else {
-          const uint32_t deg = e1 - e0;
-          out_edge[(size_t)p * deg + cnt] = c0 + t;
-          out_metric[(size_t)p * deg + cnt] = over;
-        }
-        ++cnt;
-      }
+  uint32_t cnt = 0;
+  bool wide = false;
+  for (uint32_t c0 = e0; c0 < e1; c0 += kRsLinks) {  // block-uniform
+    const uint32_t nl = min(kRsLinks, e1 - c0);
+    __syncthreads();  // the previous chunk's reads are done
+    for (uint32_t t = threadIdx.x; t < nl; t += kRsThreads) {
+      const uint32_t q = c0 + t, x = col[q];
+      const unsigned long long rx = lfa && x != me ? rowp[x] : 0ull;
+      s_j[t] = edge_nb[q];
+      s_dmx[t] = Dme[x];
+      s_w[t] = wt[q];
+      s_row[t] = rx;
+      s_back[t] = rx ? reinterpret_cast<const uint32_t*>(rx)[me] : kInf;
+      if constexpr (MODE == kRsDigest) s_lh[t] = link_hash[link[q]];
     }
-    if constexpr (MODE != kRsDb) {
-      break;
-    } else {
-      if (pass) break;
-      // The block's short routes (<= kRsKeep next hops, staged in LDS) take
-      // one contiguous range, reserved with one atomic after a block scan and
-      // written by the whole block with coalesced stores; a longer route
-      // reserves its own range and is written by the second pass.
-      mine = live ? cnt : 0u;
-      big = mine > kRsKeep || !packs;
-      const uint32_t small = big ? 0u : mine;
-      const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-      uint32_t x = small;
-      for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-      }
-      if (lane == 63) s_wsum[w] = x;
-      if (threadIdx.x == 0) s_long = 0;
-      // this thread's staged records into registers (the LDS is compacted next)
-      uint32_t keep[kRsKeep];
-#pragma unroll
-      for (uint32_t k = 0; k < kRsKeep; ++k)
-        keep[k] = k < small ? s_keep[k * kRsThreads + threadIdx.x] : 0u;
-      __syncthreads();
-      if (big) s_long = 1;  // (benign same-value race)
-      if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (uint32_t k = 0; k < kRsThreads / 64; ++k) tot += s_wsum[k];
-        s_wsum[kRsThreads / 64 - 1] = tot;  // (read back below as the block total)
-        s_base = tot ? atomicAdd(&db.cursor[slot], tot) : 0u;
-      }
-      uint32_t within = x - small;  // exclusive, in the block
-      for (uint32_t k = 0; k < w; ++k) within += s_wsum[k];
-      // (a wave reads the sums of the waves before it, never the last slot,
-      // which thread 0 reuses for the block total)
-#pragma unroll
-      for (uint32_t k = 0; k < kRsKeep; ++k)
-        if (k < small) s_keep[within + k] = keep[k];
-      first = big ? atomicAdd(&db.cursor[slot], mine) : 0u;
-      __syncthreads();
-      const uint32_t tot = s_wsum[kRsThreads / 64 - 1], base = s_base;
-      if (!big) first = base + within;
-      if (live) db.hdr[(size_t)slot * n_sets + p] = (unsigned long long)first | ((unsigned long long)mine << 32);
-      if (big && first + mine > db.cap[slot]) atomicOr(db.flags, 1u);
-      if (base + tot > db.cap[slot]) {
-        if (threadIdx.x == 0 && tot) atomicOr(db.flags, 1u);
+    __syncthreads();
+    if (shortest == kInf64) continue;  // (every thread still meets the barriers)
+    for (uint32_t t = 0; t < nl; ++t) {
+      if (s_j[t] == kInf) continue;  // a dead slot (no link)
+      // getNextHopsWithMetric: x is a shortest-path next hop of a min-cost
+      // member (via = shortest - d_me(x)), lowered with LFA to a member's
+      // d_x(dst) < shortest + d_x(me)
+      uint64_t via = kInf64;
+      const uint32_t* bm = NHme + (size_t)s_j[t] * wpm;
+      const uint32_t* Dx = reinterpret_cast<const uint32_t*>(s_row[t]);
+      const uint64_t back = s_back[t];
+      if (one) {  // Dme[d0] == shortest
+        const uint32_t bw = bm[d0 >> 5];
+        const uint32_t dxd = Dx ? Dx[d0] : kInf;  // (Dx is null without LFA)
+        if ((bw >> (d0 & 31)) & 1u) via = shortest - s_dmx[t];
+        if (lfa && dxd != kInf && back != kInf && (uint64_t)dxd < shortest + back &&
+            (via == kInf64 || via > dxd))
+          via = dxd;
       } else {
-        unsigned long long* dst = db.pool + db.base[slot] + base;
-        for (uint32_t k = threadIdx.x; k < tot; k += kRsThreads) {
-          const uint32_t v = s_keep[k];
-          dst[k] = (unsigned long long)(e0 + (v & 0xFFFFu)) | ((unsigned long long)(v >> 16) << 32);
+        for (uint32_t k = b; k < e; ++k) {
+          const uint32_t d = set_nodes[k];
+          if (Dme[d] != shortest) continue;
+          if ((bm[d >> 5] >> (d & 31)) & 1u) {
+            via = shortest - s_dmx[t];
+            break;
+          }
         }
+        if (Dx)
+          for (uint32_t k = b; k < e; ++k) {
+            const uint32_t dxd = Dx[set_nodes[k]];
+            if (dxd == kInf || back == kInf) continue;
+            if ((uint64_t)dxd < shortest + back && (via == kInf64 || via > dxd)) via = dxd;
+          }
       }
-      if (!s_long) break;  // block-uniform (read after the barrier above)
+      if (via == kInf64) continue;
+      const uint64_t over = (uint64_t)s_w[t] + via;
+      if (!lfa && over != shortest) continue;
+      if constexpr (MODE == kRsDigest) {
+        rec += rmix64(s_lh[t] + (uint32_t)over);
+      } else if constexpr (MODE == kRsDb) {
+        wide |= (over >> 32) != 0;
+        __builtin_nontemporal_store((unsigned long long)(c0 + t) | (over << 32),
+                                    out + (size_t)cnt * kRsThreads);
+      } else {
+        const uint32_t deg = e1 - e0;
+        out_edge[(size_t)p * deg + cnt] = c0 + t;
+        out_metric[(size_t)p * deg + cnt] = over;
+      }
+      ++cnt;
     }
   }
   if constexpr (MODE == kRsDigest) {
@@ -322,7 +253,15 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
       h += ((uint64_t)hi2 << 32) | lo2;
     }
     if ((threadIdx.x & 63) == 0 && h) atomicAdd(&digest[slot], (unsigned long long)h);
-  } else if constexpr (MODE == kRsOne) {
+  } else if constexpr (MODE == kRsDb) {
+    if (wide) atomicOr(db.flags, 2u);
+    uint32_t wsum = live ? cnt : 0u;  // the me's record count: one atomic per wave
+    for (int d = 32; d >= 1; d >>= 1) wsum += __shfl_down(wsum, d, 64);
+    if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&db.count[slot], wsum);
+    if (live)
+      db.hdr[(size_t)slot * n_sets + p] = (tile + threadIdx.x) | ((unsigned long long)cnt << 32) |
+                                          ((unsigned long long)kRsThreads << 48);
+  } else {
     if (live) {
       out_min[p] = shortest;
       out_cnt[p] = cnt;
