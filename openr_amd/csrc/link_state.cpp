@@ -502,8 +502,9 @@ spf_status apply_db(ls_state* ls, uint32_t node, DbIn&& db, Metric up, Metric do
     clear_memo(ls);
   } else if (node_flip) {
     clear_results(ls);
-    ls->pending_ovl.push_back(node);
   }
+  // (the flatten patches these nodes' overload bits, with or without rows)
+  if (node_flip) ls->pending_ovl.push_back(node);
   // a new node joins the CSR on the next flatten; like the reference, its
   // first database signals no topology change and keeps the memo
   if (!known) ls->dirty = true;
@@ -533,12 +534,26 @@ spf_status flatten(ls_state* ls) {
     }
     return SPF_OK;
   }
+  const std::vector<uint32_t> povl = std::move(ls->pending_ovl);
   ls->pending_ovl.clear();
+  // the node order: the last flatten's when the node set is the same (no
+  // string sort per publication), else every name sorted again
+  bool same_nodes = ls->dbs.size() == ls->csr_name.size();
+  if (same_nodes)
+    for (const auto& kv : ls->dbs)
+      if (kv.first >= ls->csr_of.size() || ls->csr_of[kv.first] == kNone) {
+        same_nodes = false;
+        break;
+      }
   std::vector<uint32_t> ids;
-  ids.reserve(ls->dbs.size());
-  for (const auto& kv : ls->dbs) ids.push_back(kv.first);
-  std::sort(ids.begin(), ids.end(),
-            [&](uint32_t a, uint32_t b) { return ls->names[a] < ls->names[b]; });
+  if (same_nodes) {
+    ids = ls->csr_name;
+  } else {
+    ids.reserve(ls->dbs.size());
+    for (const auto& kv : ls->dbs) ids.push_back(kv.first);
+    std::sort(ids.begin(), ids.end(),
+              [&](uint32_t a, uint32_t b) { return ls->names[a] < ls->names[b]; });
+  }
   const uint32_t N = (uint32_t)ids.size();
   // Every link of a node -- up or down -- has a slot in its row, in
   // linksFromNode order; a down link's slot is dead (a self-loop of metric 1,
@@ -558,10 +573,10 @@ spf_status flatten(ls_state* ls) {
   };
   if (N > 0 && ls->eng && ls->engine_loaded && ids == ls->csr_name) {
     bool fits = true;
-    std::vector<uint32_t> new_col(ls->col), new_lid(ls->link_id);
-    std::vector<int32_t> new_met(ls->metric);
-    std::vector<uint8_t> new_ovl(N);
-    for (uint32_t u = 0; u < N; ++u) new_ovl[u] = node_overloaded(ls, ids[u]);
+    // overload bits: only nodes whose database flipped one can differ
+    std::vector<uint8_t> new_ovl(ls->ovl);
+    for (uint32_t nm : povl)
+      if (nm < ls->csr_of.size() && ls->csr_of[nm] != kNone) new_ovl[ls->csr_of[nm]] = node_overloaded(ls, nm);
     // the rows to rebuild: the touched nodes' (every row when unknown)
     std::vector<uint32_t> cand;
     if (ls->touched_all) {
@@ -573,12 +588,20 @@ spf_status flatten(ls_state* ls) {
       std::sort(cand.begin(), cand.end());
       cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
     }
+    // the candidate rows' new slots, back to back in candidate order (the
+    // CSR arrays themselves change only once the engine took the patch)
+    std::vector<uint32_t> nc, nl;
+    std::vector<int32_t> nmt;
     std::vector<uint8_t> used;
     for (uint32_t u : cand) {
       if (!fits) break;
       const uint32_t nm = ids[u];
       const uint32_t b = ls->row_ptr[u], e = ls->row_ptr[u + 1];
-      uint32_t k = b;
+      const size_t k0 = nc.size();
+      nc.resize(k0 + (e - b));
+      nl.resize(k0 + (e - b));
+      nmt.resize(k0 + (e - b));
+      size_t k = k0;
       used.assign(e - b, 0);
       auto it = ls->link_map.find(nm);
       if (it != ls->link_map.end())
@@ -590,46 +613,51 @@ spf_status flatten(ls_state* ls) {
               break;
             }
           const uint32_t o = l->other(nm);
-          if (at == e || k == e || o >= ls->csr_of.size() || ls->csr_of[o] == kNone) {
+          if (at == e || k == k0 + (e - b) || o >= ls->csr_of.size() || ls->csr_of[o] == kNone) {
             fits = false;  // a new link, or more links than slots: reload
             break;
           }
           used[at - b] = 1;
-          slot_of(l, nm, new_col[k], new_met[k]);
-          new_lid[k++] = l->id;
+          slot_of(l, nm, nc[k], nmt[k]);
+          nl[k++] = l->id;
         }
       for (uint32_t q = b; q < e && fits; ++q)  // the withdrawn links' dead slots, in their old order
         if (!used[q - b]) {
-          new_col[k] = u;
-          new_met[k] = 1;
-          new_lid[k++] = ls->link_id[q];
+          nc[k] = u;
+          nmt[k] = 1;
+          nl[k++] = ls->link_id[q];
         }
     }
     if (fits) {
       std::vector<uint32_t> rows, rcol, rlid, medges, onodes;
       std::vector<int32_t> rmet, mmet;
       std::vector<uint8_t> ovals;
-      for (uint32_t u = 0; u < N; ++u)
-        if (new_ovl[u] != ls->ovl[u]) {
-          onodes.push_back(u);
-          ovals.push_back(new_ovl[u]);
-        }
+      for (uint32_t nm : povl) {
+        const uint32_t u = nm < ls->csr_of.size() ? ls->csr_of[nm] : kNone;
+        if (u == kNone || new_ovl[u] == ls->ovl[u]) continue;
+        if (std::find(onodes.begin(), onodes.end(), u) != onodes.end()) continue;
+        onodes.push_back(u);
+        ovals.push_back(new_ovl[u]);
+      }
+      size_t k0 = 0;
       for (uint32_t u : cand) {
         const uint32_t b = ls->row_ptr[u], e = ls->row_ptr[u + 1];
         bool structural = false;
-        for (uint32_t q = b; q < e; ++q) structural |= new_col[q] != ls->col[q] || new_lid[q] != ls->link_id[q];
+        for (uint32_t q = b; q < e; ++q)
+          structural |= nc[k0 + q - b] != ls->col[q] || nl[k0 + q - b] != ls->link_id[q];
         if (structural) {
           rows.push_back(u);
-          rcol.insert(rcol.end(), new_col.begin() + b, new_col.begin() + e);
-          rmet.insert(rmet.end(), new_met.begin() + b, new_met.begin() + e);
-          rlid.insert(rlid.end(), new_lid.begin() + b, new_lid.begin() + e);
+          rcol.insert(rcol.end(), nc.begin() + k0, nc.begin() + k0 + (e - b));
+          rmet.insert(rmet.end(), nmt.begin() + k0, nmt.begin() + k0 + (e - b));
+          rlid.insert(rlid.end(), nl.begin() + k0, nl.begin() + k0 + (e - b));
         } else {
           for (uint32_t q = b; q < e; ++q)
-            if (new_met[q] != ls->metric[q]) {
+            if (nmt[k0 + q - b] != ls->metric[q]) {
               medges.push_back(q);
-              mmet.push_back(new_met[q]);
+              mmet.push_back(nmt[k0 + q - b]);
             }
         }
+        k0 += e - b;
       }
       spf_status st = SPF_OK;
       if (!rows.empty())
@@ -642,9 +670,14 @@ spf_status flatten(ls_state* ls) {
         ls->engine_loaded = false;
         return eng_fail(ls, st);
       }
-      ls->col.swap(new_col);
-      ls->metric.swap(new_met);
-      ls->link_id.swap(new_lid);
+      k0 = 0;  // the engine has the patch: the host CSR follows
+      for (uint32_t u : cand) {
+        const uint32_t b = ls->row_ptr[u], e = ls->row_ptr[u + 1];
+        std::copy(nc.begin() + k0, nc.begin() + k0 + (e - b), ls->col.begin() + b);
+        std::copy(nmt.begin() + k0, nmt.begin() + k0 + (e - b), ls->metric.begin() + b);
+        std::copy(nl.begin() + k0, nl.begin() + k0 + (e - b), ls->link_id.begin() + b);
+        k0 += e - b;
+      }
       ls->ovl.swap(new_ovl);
       if (!rows.empty()) {
         ++ls->row_patches;

@@ -2101,23 +2101,32 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
     counts |= t.size() != old_nb[i];
   }
   if (counts) {
-    std::vector<int32_t> slot(N, -1);
-    for (uint32_t i = 0; i < n; ++i) slot[nodes[i]] = (int32_t)i;
+    // the untouched nodes' lists move as whole blocks between touched nodes
+    std::vector<uint32_t> order(n);
+    std::iota(order.begin(), order.end(), 0u);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nodes[a] < nodes[b]; });
     std::vector<uint32_t> ptr(N + 1, 0), id, w;
     id.reserve(c->nb_id.size() + 16);
     w.reserve(c->nb_id.size() + 16);
-    for (uint32_t u = 0; u < N; ++u) {
-      if (slot[u] >= 0) {
-        for (const auto& x : fresh[slot[u]]) {
-          id.push_back(x.first);
-          w.push_back(x.second);
-        }
-      } else {
-        id.insert(id.end(), c->nb_id.begin() + c->nb_ptr[u], c->nb_id.begin() + c->nb_ptr[u + 1]);
-        w.insert(w.end(), c->nb_w.begin() + c->nb_ptr[u], c->nb_w.begin() + c->nb_ptr[u + 1]);
+    uint32_t next = 0;  // first node not yet placed
+    auto block = [&](uint32_t to) {  // untouched nodes next .. to - 1
+      const uint32_t b = c->nb_ptr[next], e = c->nb_ptr[to];
+      const int64_t shift = (int64_t)id.size() - (int64_t)b;
+      id.insert(id.end(), c->nb_id.begin() + b, c->nb_id.begin() + e);
+      w.insert(w.end(), c->nb_w.begin() + b, c->nb_w.begin() + e);
+      for (uint32_t u = next; u < to; ++u) ptr[u + 1] = (uint32_t)((int64_t)c->nb_ptr[u + 1] + shift);
+    };
+    for (uint32_t oi : order) {
+      const uint32_t u = nodes[oi];
+      block(u);
+      for (const auto& x : fresh[oi]) {
+        id.push_back(x.first);
+        w.push_back(x.second);
       }
       ptr[u + 1] = (uint32_t)id.size();
+      next = u + 1;
     }
+    block(N);
     c->nb_ptr.swap(ptr);
     c->nb_id.swap(id);
     c->nb_w.swap(w);

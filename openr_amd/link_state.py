@@ -129,7 +129,9 @@ class NodeSpfResult:
 
     __slots__ = ("_metric", "_nh", "_pl")
 
-    def __init__(self, metric: int, nh: Set[str], pl: List[PathLink]) -> None:
+    def __init__(self, metric: int, nh: Set[str], pl) -> None:
+        # pl: the list, or a callable building it on first use (pathLinks are
+        # derived only for the callers that read them)
         self._metric, self._nh, self._pl = metric, nh, pl
 
     def metric(self) -> int:
@@ -139,6 +141,8 @@ class NodeSpfResult:
         return self._nh
 
     def pathLinks(self) -> List[PathLink]:
+        if callable(self._pl):
+            self._pl = self._pl()
         return self._pl
 
     def __repr__(self) -> str:
@@ -162,7 +166,7 @@ class _LazySpfResult(Mapping):
     LinkState's link table, so reading an unmaterialised entry after the
     topology changed raises instead of naming the wrong links."""
 
-    def __init__(self, ls: "LinkState", v: "N.LsSpfView") -> None:
+    def __init__(self, ls: "LinkState", v: "N.LsSpfView", key=None) -> None:
         import numpy as np
 
         def arr(ptr, n, dt):
@@ -171,16 +175,35 @@ class _LazySpfResult(Mapping):
         n = int(v.n)
         self._ls = ls
         self._gen = ls._gen
+        self._key = key
         self._node = arr(v.node, n, np.uint32)
         self._metric = arr(v.metric, n, np.uint64)
         self._nh_ptr = arr(v.nh_ptr, n + 1, np.uint32)
         self._nh_node = arr(v.nh_node, int(self._nh_ptr[-1]) if n else 0, np.uint32)
-        self._pl_ptr = arr(v.pl_ptr, n + 1, np.uint32)
-        m = int(self._pl_ptr[-1]) if n else 0
-        self._pl_link = arr(v.pl_link, m, np.uint32)
-        self._pl_prev = arr(v.pl_prev, m, np.uint32)
+        self._pl_ptr = None
+        if v.pl_ptr:
+            self._take_pl(v)
         self._index: Optional[Dict[str, int]] = None
         self._made: Dict[str, NodeSpfResult] = {}
+
+    def _take_pl(self, v) -> None:
+        import numpy as np
+
+        n = len(self._node)
+        self._pl_ptr = np.ctypeslib.as_array(v.pl_ptr, (n + 1,)).astype(np.uint32) if n else np.zeros(1, np.uint32)
+        m = int(self._pl_ptr[-1]) if n else 0
+        self._pl_link = np.ctypeslib.as_array(v.pl_link, (m,)).astype(np.uint32) if m else np.zeros(0, np.uint32)
+        self._pl_prev = np.ctypeslib.as_array(v.pl_prev, (m,)).astype(np.uint32) if m else np.zeros(0, np.uint32)
+
+    def _path_links(self, i: int) -> List[PathLink]:
+        ls = self._ls
+        if ls._gen != self._gen:
+            raise RuntimeError("SpfResult read after a topology change: call getSpfResult again")
+        if self._pl_ptr is None:  # the same memo entry, its pathLinks now (spf_runs unchanged)
+            self._take_pl(ls._spf_view(*self._key))
+        a, b = int(self._pl_ptr[i]), int(self._pl_ptr[i + 1])
+        return [PathLink(ls._link(int(l)), ls._name(int(p)))
+                for l, p in zip(self._pl_link[a:b], self._pl_prev[a:b])]
 
     def _idx(self) -> Dict[str, int]:
         if self._index is None:
@@ -197,10 +220,7 @@ class _LazySpfResult(Mapping):
             i = self._idx()[key]
             a, b = int(self._nh_ptr[i]), int(self._nh_ptr[i + 1])
             nh = {ls._name(int(x)) for x in self._nh_node[a:b]}
-            a, b = int(self._pl_ptr[i]), int(self._pl_ptr[i + 1])
-            pl = [PathLink(ls._link(int(l)), ls._name(int(p)))
-                  for l, p in zip(self._pl_link[a:b], self._pl_prev[a:b])]
-            r = self._made[key] = NodeSpfResult(int(self._metric[i]), nh, pl)
+            r = self._made[key] = NodeSpfResult(int(self._metric[i]), nh, lambda i=i: self._path_links(i))
         return r
 
     def __iter__(self):
@@ -375,13 +395,17 @@ class LinkState(N.NativeHandle):
     def getSpfResult(self, nodeName: str, useLinkMetric: bool = True) -> SpfResult:
         """``getSpfResult`` (LinkState.cpp:793-803): a read-only mapping node
         name -> NodeSpfResult over the C-ABI's result arrays (copied once);
-        entries are materialised on access."""
+        entries are materialised on access, pathLinks on the first
+        ``pathLinks()`` of the result (ls_get_spf_metrics now, the same memo
+        entry's pathLinks from ls_get_spf_result then: one spf_runs count)."""
         key = (nodeName, bool(useLinkMetric))
         hit = self._spf_cache.get(key)
         if hit is not None:
             return hit
-        v = self._spf_view(nodeName, useLinkMetric)
-        res = _LazySpfResult(self, v)
+        v = N.LsSpfView()  # metrics and next hops now, pathLinks when first read
+        self._err(N.lib.ls_get_spf_metrics(self._h, nodeName.encode(), int(bool(useLinkMetric)),
+                                           C.byref(v)))
+        res = _LazySpfResult(self, v, key)
         self._spf_cache[key] = res
         return res
 
