@@ -547,10 +547,10 @@ spf_status spf_mplan_routes(spf_mplan* mp, uint32_t me_req, const uint32_t* set_
  * u64 = CSR edge (me -> neighbour: link id, interface, neighbour and the
  * metric me advertises come with it) | metric << 32 (w(link) +
  * dist(neighbour, dst)), in me's link order -- getNextHopsThrift's next
- * hops.  Device layout: me's region is one [deg(me)][256] tile per 256 sets
- * (stride 256), so consecutive routes' k-th next hops are adjacent; a region
- * holds ceil(n_sets / 256) * 256 * deg(me) record slots (unused ones are
- * never written).  Sets without a kept next hop have count 0.
+ * hops.  Device layout: me's region is one [deg(me)][1024] tile per 1024
+ * sets (stride 1024), so consecutive routes' k-th next hops are adjacent; a
+ * region holds ceil(n_sets / 1024) * 1024 * deg(me) record slots (unused ones
+ * are never written).  Sets without a kept next hop have count 0.
  * SPF_E_UNSUPPORTED when a metric exceeds 2^32 - 1 or a region 2^32 slots.
  * *n_records (optional) = records over every me; *kernel_ms (optional) = the
  * slowest member's kernel.  The databases stay resident until the next call. */

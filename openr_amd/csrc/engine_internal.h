@@ -346,6 +346,8 @@ struct RouteDbOut {
   uint32_t* count = nullptr;
   uint32_t* flags = nullptr;
 };
+// sets per kRsDb tile (the [deg][sets] tiles of a route database region)
+uint32_t route_db_tile_sets();
 // Route selection over resident rows for many `me` (routes.hip): digests per
 // me (d_digest, n_me slots, added to), their route databases (db), or
 // spf_routes' records of ONE me.

@@ -911,8 +911,9 @@ spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32
     mp->db_loc[t] = {r, (uint32_t)mine[r].size()};
     mine[r].push_back(mp->srcs[me_req[t]]);
   }
-  // me's region: one [deg(me)][256] tile per chunk of 256 sets (route_sets_kernel<kRsDb>)
-  const uint64_t tiles = ((uint64_t)n_sets + 255) / 256 * 256;
+  // me's region: one [deg(me)][ts] tile per chunk of ts sets (route_quads_kernel<kRsDb>)
+  const uint64_t ts = route_db_tile_sets();
+  const uint64_t tiles = ((uint64_t)n_sets + ts - 1) / ts * ts;
   std::vector<hipEvent_t> ev(2 * mp->n_parts, nullptr);
   std::vector<std::vector<uint32_t>> fl(mp->n_parts);
   IssuedGuard guard{m, {}, &ev};  // declared after fl: drains before it is freed

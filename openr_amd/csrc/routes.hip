@@ -16,6 +16,7 @@
 // ============================================================================
 #include "engine_internal.h"
 
+#include <cstdlib>
 #include <memory>
 
 using namespace spfi;
@@ -269,9 +270,217 @@ __global__ __launch_bounds__(kRsThreads) void route_sets_kernel(
   }
 }
 
+// The many-me modes (kRsDigest, kRsDb) with four sets per thread: 1,024 sets
+// per block.  When a thread's four sets are single nodes d, d+1, d+2, d+3 (d
+// a multiple of 4: every node's loopback, CS-2), one link costs one bitmap
+// word and one 16-byte load of d_x(d .. d+3) for all four -- a quarter of the
+// load instructions of a thread per set (the selection is bound by them, not
+// by bytes: reading u8 rows instead made it slower).  Other sets take the
+// per-set path.  kRsDb tiles are [deg(me)][1024].
+constexpr uint32_t kRqSets = 4;
+constexpr uint32_t kRqPerBlock = kRqSets * kRsThreads;
+constexpr bool kRqNt = true;  // streaming 32-byte stores (full lines when a wave's routes agree)
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+template <int MODE>
+__global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
+    const unsigned long long* __restrict__ rowp, const unsigned long long* __restrict__ nhp,
+    uint32_t wpm, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+    const uint32_t* __restrict__ wt, const uint32_t* __restrict__ link,
+    const uint32_t* __restrict__ edge_nb,
+    const uint32_t* __restrict__ me_ids, const uint32_t* __restrict__ set_ptr,
+    const uint32_t* __restrict__ set_nodes, uint32_t n_sets, uint32_t lfa,
+    const unsigned long long* __restrict__ link_hash, unsigned long long* __restrict__ digest,
+    uint32_t n_me, uint32_t n_chunks, RouteDbOut db) {
+  const uint32_t g = blockIdx.x & 7u, i = blockIdx.x >> 3;  // XCD-aware order, as route_sets_kernel
+  const uint32_t L = i / n_chunks;
+  const uint32_t slot = ((L / kRsGroup) * 8 + g) * kRsGroup + L % kRsGroup;
+  if (slot >= n_me) return;  // whole block
+  const uint32_t me = me_ids[slot];
+  const uint32_t chunk = i % n_chunks;
+  const uint32_t p0 = chunk * kRqPerBlock + kRqSets * threadIdx.x;
+  const uint32_t* Dme = reinterpret_cast<const uint32_t*>(rowp[me]);
+  const uint32_t* NHme = reinterpret_cast<const uint32_t*>(nhp[me]);
+  const uint32_t e0 = row_ptr[me], e1 = row_ptr[me + 1];
+  uint64_t sh[kRqSets], rec[kRqSets];
+  uint32_t cnt[kRqSets], b[kRqSets], e[kRqSets];
+  bool vec = true;
+#pragma unroll
+  for (uint32_t j = 0; j < kRqSets; ++j) {
+    const bool live = p0 + j < n_sets;
+    b[j] = live ? set_ptr[p0 + j] : 0u;
+    e[j] = live ? set_ptr[p0 + j + 1] : 0u;
+    vec &= e[j] == b[j] + 1;
+    sh[j] = kInf64;
+    rec[j] = 0;
+    cnt[j] = 0;
+  }
+  const uint32_t d0 = vec ? set_nodes[b[0]] : 0u;
+  if (vec) {
+#pragma unroll
+    for (uint32_t j = 1; j < kRqSets; ++j) vec &= set_nodes[b[j]] == d0 + j;
+    vec &= (d0 & 3u) == 0u;
+  }
+  if (vec) {
+    const uint4 d4 = *reinterpret_cast<const uint4*>(Dme + d0);
+    const uint32_t dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (uint32_t j = 0; j < kRqSets; ++j) sh[j] = dd[j] == kInf ? kInf64 : dd[j];
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kRqSets; ++j)
+      for (uint32_t k = b[j]; k < e[j]; ++k) {
+        const uint32_t d = Dme[set_nodes[k]];
+        if (d != kInf && d < sh[j]) sh[j] = d;
+      }
+  }
+  bool any_route = false;
+#pragma unroll
+  for (uint32_t j = 0; j < kRqSets; ++j) any_route |= sh[j] != kInf64;
+  const uint64_t tile = MODE == kRsDb ? (uint64_t)chunk * kRqPerBlock * (e1 - e0) : 0ull;
+  unsigned long long* const out =
+      MODE == kRsDb ? db.pool + db.base[slot] + tile + kRqSets * threadIdx.x : nullptr;
+  __shared__ uint32_t s_j[kRsLinks], s_dmx[kRsLinks], s_back[kRsLinks], s_w[kRsLinks];
+  __shared__ unsigned long long s_row[kRsLinks], s_lh[kRsLinks];
+  bool wide = false;
+  for (uint32_t c0 = e0; c0 < e1; c0 += kRsLinks) {  // block-uniform
+    const uint32_t nl = min(kRsLinks, e1 - c0);
+    __syncthreads();  // the previous chunk's reads are done
+    for (uint32_t t = threadIdx.x; t < nl; t += kRsThreads) {
+      const uint32_t q = c0 + t, x = col[q];
+      const unsigned long long rx = lfa && x != me ? rowp[x] : 0ull;
+      s_j[t] = edge_nb[q];
+      s_dmx[t] = Dme[x];
+      s_w[t] = wt[q];
+      s_row[t] = rx;
+      s_back[t] = rx ? reinterpret_cast<const uint32_t*>(rx)[me] : kInf;
+      if constexpr (MODE == kRsDigest) s_lh[t] = link_hash[link[q]];
+    }
+    __syncthreads();
+    if (!any_route) continue;  // (every thread still meets the barriers)
+    for (uint32_t t = 0; t < nl; ++t) {
+      if (s_j[t] == kInf) continue;  // a dead slot (no link)
+      const uint32_t* bm = NHme + (size_t)s_j[t] * wpm;
+      const uint32_t* Dx = reinterpret_cast<const uint32_t*>(s_row[t]);
+      const uint64_t back = s_back[t];
+      const uint32_t dmx = s_dmx[t];
+      uint64_t via[kRqSets];
+      if (vec) {  // four consecutive single destinations: one word, one 16-byte load
+        const uint32_t bw = bm[d0 >> 5];
+        uint32_t dx[4] = {kInf, kInf, kInf, kInf};
+        if (Dx) {
+          const uint4 x4 = *reinterpret_cast<const uint4*>(Dx + d0);
+          dx[0] = x4.x, dx[1] = x4.y, dx[2] = x4.z, dx[3] = x4.w;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kRqSets; ++j) {
+          via[j] = kInf64;
+          if (sh[j] == kInf64) continue;
+          if ((bw >> ((d0 + j) & 31)) & 1u) via[j] = sh[j] - dmx;
+          if (lfa && dx[j] != kInf && back != kInf && (uint64_t)dx[j] < sh[j] + back &&
+              (via[j] == kInf64 || via[j] > dx[j]))
+            via[j] = dx[j];
+        }
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kRqSets; ++j) {
+          via[j] = kInf64;
+          if (sh[j] == kInf64) continue;
+          for (uint32_t k = b[j]; k < e[j]; ++k) {
+            const uint32_t d = set_nodes[k];
+            if (Dme[d] != sh[j]) continue;
+            if ((bm[d >> 5] >> (d & 31)) & 1u) {
+              via[j] = sh[j] - dmx;
+              break;
+            }
+          }
+          if (Dx)
+            for (uint32_t k = b[j]; k < e[j]; ++k) {
+              const uint32_t dxd = Dx[set_nodes[k]];
+              if (dxd == kInf || back == kInf) continue;
+              if ((uint64_t)dxd < sh[j] + back && (via[j] == kInf64 || via[j] > dxd)) via[j] = dxd;
+            }
+        }
+      }
+      uint64_t over[kRqSets];
+      bool keep[kRqSets];
+#pragma unroll
+      for (uint32_t j = 0; j < kRqSets; ++j) {
+        over[j] = (uint64_t)s_w[t] + via[j];
+        keep[j] = via[j] != kInf64 && (lfa || over[j] == sh[j]);
+      }
+      if constexpr (MODE == kRsDigest) {
+#pragma unroll
+        for (uint32_t j = 0; j < kRqSets; ++j)
+          if (keep[j]) {
+            rec[j] += rmix64(s_lh[t] + (uint32_t)over[j]);
+            ++cnt[j];
+          }
+      } else {
+        const unsigned long long eb = c0 + t;
+        if (keep[0] && keep[1] && keep[2] && keep[3] && cnt[0] == cnt[1] && cnt[1] == cnt[2] &&
+            cnt[2] == cnt[3]) {
+          // the four routes' next hop at the same position (consecutive
+          // destinations of one pod): one 32-byte store
+          u64x2* o = reinterpret_cast<u64x2*>(out + (size_t)cnt[0] * kRqPerBlock);
+          const u64x2 a = {eb | (over[0] << 32), eb | (over[1] << 32)};
+          const u64x2 z = {eb | (over[2] << 32), eb | (over[3] << 32)};
+          if constexpr (kRqNt) {
+            __builtin_nontemporal_store(a, o);
+            __builtin_nontemporal_store(z, o + 1);
+          } else {
+            o[0] = a;
+            o[1] = z;
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < kRqSets; ++j) {
+            wide |= (over[j] >> 32) != 0;
+            ++cnt[j];
+          }
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < kRqSets; ++j)
+            if (keep[j]) {
+              wide |= (over[j] >> 32) != 0;
+              out[(size_t)cnt[j] * kRqPerBlock + j] = eb | (over[j] << 32);
+              ++cnt[j];
+            }
+        }
+      }
+    }
+  }
+  if constexpr (MODE == kRsDigest) {
+    uint64_t h = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kRqSets; ++j) {
+      const uint32_t p = p0 + j;
+      if (p < n_sets && cnt[j]) h += rmix64(rmix64(0x9e3779b97f4a7c15ull * (p + 1) + sh[j]) + rec[j] + p);
+    }
+    for (int d = 32; d >= 1; d >>= 1) {  // wave sum, one atomic per wave
+      const uint32_t lo2 = __shfl_down((uint32_t)h, d, 64), hi2 = __shfl_down((uint32_t)(h >> 32), d, 64);
+      h += ((uint64_t)hi2 << 32) | lo2;
+    }
+    if ((threadIdx.x & 63) == 0 && h) atomicAdd(&digest[slot], (unsigned long long)h);
+  } else {
+    if (wide) atomicOr(db.flags, 2u);
+    uint32_t wsum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kRqSets; ++j) {
+      const uint32_t p = p0 + j;
+      if (p >= n_sets) continue;
+      wsum += cnt[j];
+      db.hdr[(size_t)slot * n_sets + p] = (tile + kRqSets * threadIdx.x + j) | ((unsigned long long)cnt[j] << 32) |
+                                          ((unsigned long long)kRqPerBlock << 48);
+    }
+    for (int d = 32; d >= 1; d >>= 1) wsum += __shfl_down(wsum, d, 64);
+    if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&db.count[slot], wsum);
+  }
+}
+
 }  // namespace
 
 namespace spfi {
+
+uint32_t route_db_tile_sets() { return std::getenv("SPF_ROUTE_SETS1") ? kRsThreads : kRqPerBlock; }
 
 spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
                              const unsigned long long* d_nhp, const uint32_t* d_me, uint32_t n_me,
@@ -280,6 +489,24 @@ spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
                              unsigned long long* d_digest, uint64_t* d_min, uint32_t* d_cnt,
                              uint32_t* d_edge, uint64_t* d_metric, hipStream_t s, const RouteDbOut* db) {
   if (!n_me || !n_sets) return SPF_OK;
+  if ((db || d_digest) && !std::getenv("SPF_ROUTE_SETS1")) {  // four sets per thread (SPF_ROUTE_SETS1: one, A/B)
+    const uint32_t n_chunks = (n_sets + kRqPerBlock - 1) / kRqPerBlock;
+    const uint32_t groups = (n_me + kRsGroup - 1) / kRsGroup;
+    const uint64_t blocks = 8ull * ((groups + 7) / 8 * kRsGroup) * n_chunks;
+    if (blocks >= (1ull << 31)) return fail(c, SPF_E_INVALID, "route sets: grid too large");
+    if (db)
+      hipLaunchKernelGGL(route_quads_kernel<kRsDb>, dim3((uint32_t)blocks), dim3(kRsThreads), 0, s, d_rowp, d_nhp,
+                         c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p,
+                         d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, nullptr, nullptr, n_me,
+                         n_chunks, *db);
+    else
+      hipLaunchKernelGGL(route_quads_kernel<kRsDigest>, dim3((uint32_t)blocks), dim3(kRsThreads), 0, s, d_rowp,
+                         d_nhp, c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p,
+                         c->d_edge_nb.p, d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, d_link_hash,
+                         d_digest, n_me, n_chunks, RouteDbOut{});
+    HIP_TRY(c, hipGetLastError());
+    return SPF_OK;
+  }
   const uint32_t n_chunks = (n_sets + kRsThreads - 1) / kRsThreads;
   const uint32_t groups = (n_me + kRsGroup - 1) / kRsGroup;
   const uint32_t per_xcd = (groups + 7) / 8 * kRsGroup;  // the most me slots any XCD takes
