@@ -995,7 +995,7 @@ class RoutesAllNodes:
         k = np.array([len(np.unique(col[rp[v]:rp[v + 1]])) for v in range(self.n)], np.int64)
         wpm = (self.n + 31) // 32
         self.read_bytes = 4 * self.n * self.n + 4 * int(k.sum()) * wpm + 4 * (self.n + 1) + 12 * self.e
-        self.pmc_kernels = {"routes": ["route_sets_kernel"]}
+        self.pmc_kernels = {"routes": ["route_quads_kernel"]}
 
     def route_step(self):
         self.digests, kms = self.ls.allSourcesRouteDigests(self.set_ptr, self.set_nodes, self.lfa)
