@@ -1165,7 +1165,7 @@ class FacadeRouteBuild:
         ndb = self.solver.buildRouteDbNative(self.me, {self.ls.getArea(): self.ls}, self.ps)
         t2 = time.perf_counter()
         self.routes = ndb.unicastCount() + ndb.mplsCount()
-        self.nexthops = len(ndb.nexthopRecords())
+        self.nexthops = ndb.nexthopCount()
         ndb.close()
         self.pub.append(t1 - t0)
         self.build.append(t2 - t1)
@@ -1304,7 +1304,7 @@ class FacadeFlapRouteBuild(FacadeRouteBuild):
         ndb = self.solver.buildRouteDbNative(self.me, {self.ls.getArea(): self.ls}, self.ps)
         t2 = time.perf_counter()
         self.routes = ndb.unicastCount() + ndb.mplsCount()
-        self.nexthops = len(ndb.nexthopRecords())
+        self.nexthops = ndb.nexthopCount()
         ndb.close()
         self.pub.append(t1 - t0)
         self.build.append(t2 - t1)

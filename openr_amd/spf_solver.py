@@ -555,6 +555,11 @@ class NativeRouteDb(N.NativeHandle):
     def mplsCount(self) -> int:
         return int(N.lib.dc_route_db_mpls_count(self._h))
 
+    def nexthopCount(self) -> int:
+        n = C.c_uint32()
+        N.lib.dc_route_db_nexthops(self._h, C.byref(n))
+        return int(n.value)
+
     def nexthopRecords(self) -> np.ndarray:
         n = C.c_uint32()
         p = N.lib.dc_route_db_nexthops(self._h, C.byref(n))

@@ -189,3 +189,24 @@ def test_native_no_route_for_absent_node():
         ls.updateAdjacencyDatabases(topo.lsdb)
         assert SpfSolver("nope", True, False).buildRouteDb("nope", {ls.getArea(): ls},
                                                            PrefixState()) is None
+
+
+def test_native_route_db_counts_match_tables():
+    """NativeRouteDb's count accessors (unicastCount / mplsCount /
+    nexthopCount: no copy, what the CS-1 bench reads) agree with the
+    materialised tables."""
+    topo = T.fabric(1000, full=True)
+    with LinkState() as ls:
+        ls.updateAdjacencyDatabases(labelled(topo, 70000))
+        ps = PrefixState()
+        random_prefixes(ps, topo.nodes, ls.getArea(), np.random.default_rng(5), 30, 2)
+        me = topo.nodes[7]
+        with impl(True):
+            ndb = SpfSolver(me, True, True).buildRouteDbNative(me, {ls.getArea(): ls}, ps)
+        try:
+            db = ndb.routeDb()
+            assert ndb.nexthopCount() == len(ndb.nexthopRecords()) > 0
+            assert ndb.unicastCount() == len(db.unicastRoutes)
+            assert ndb.mplsCount() == len(db.mplsRoutes)
+        finally:
+            ndb.close()
