@@ -168,6 +168,7 @@ struct BestRoute {
   std::vector<NodeArea> all;  // ascending
   std::optional<NodeArea> best;
   std::vector<EntryRef> refs;  // all[i]'s entry in the build's PrefixEntries (not cached)
+  uint64_t gen = 0;            // the build that stored it (dc_solver::build_gen)
   bool has_node(const std::string& n) const {
     for (const auto& na : all)
       if (na.first == n) return true;
@@ -309,6 +310,7 @@ struct dc_solver {
   std::map<std::string, uint64_t> counters;
   std::map<int32_t, std::vector<NH>> static_mpls;  // staticMplsRoutes_
   std::unordered_map<std::string, BestRoute> best_cache;  // bestRoutesCache_
+  uint64_t build_gen = 0;  // bumped per build: entries it did not store are swept
   std::unordered_map<ls_state*, GraphCache> graphs;
   // build cost by phase, ns since creation (dc_debug_phase_ns)
   uint64_t phase_ns[6] = {0, 0, 0, 0, 0, 0};
@@ -1075,7 +1077,24 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     s->phase_ns[k] += t - t_ph;
     t_ph = t;
   };
-  s->best_cache.clear();
+  // bestRoutesCache_.clear() (Decision.cpp:575): entries this build does not store again
+  // are swept when it ends; stored ones reuse their node and key (no string
+  // allocation per prefix and build)
+  const uint64_t gen = ++s->build_gen;
+  struct Sweep {
+    dc_solver* s;
+    uint64_t gen;
+    ~Sweep() {
+      for (auto it = s->best_cache.begin(); it != s->best_cache.end();) {
+        if (it->second.gen != gen) {
+          it = s->best_cache.erase(it);
+        } else {
+          it->second.refs.clear();  // (they pointed into this build)
+          ++it;
+        }
+      }
+    }
+  } sweep{s, gen};
   s->best_cache.reserve(ps->prefixes.size());
   const bool single = b.areas.size() == 1;
   std::vector<const SpfIdx*> mine;
@@ -1149,7 +1168,10 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
       continue;
     }
     // bestRoutesCache_ (its refs point into this build's entries: cleared below)
-    const BestRoute& res = s->best_cache[prefix] = std::move(*sel);
+    BestRoute& slot = s->best_cache[prefix];
+    slot = std::move(*sel);
+    slot.gen = gen;
+    const BestRoute& res = slot;
     if (res.has_node(me) && !self_prepend) continue;  // self-advertised
     // getPrefixForwardingTypeAndAlgorithm (Util.cpp:617-643)
     uint8_t ftype = DC_FWD_SR_MPLS, falgo = DC_ALGO_KSP2_ED_ECMP;
@@ -1219,11 +1241,12 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
       for (EntryRef r : u.res->refs) add_node(a.id(*r));
       set_ptr.push_back((uint32_t)set_nodes.size());
     }
-    std::vector<int32_t> lab_routes;  // labels needing a selection, in set order
-    for (int32_t top : label_order) {
-      const LabelOwner& o = label_to_node.at(top);
+    // each label's final owner (after the collision rule), in label order
+    std::vector<LabelOwner> owner;
+    owner.reserve(label_order.size());
+    for (int32_t top : label_order) owner.push_back(label_to_node.at(top));
+    for (const LabelOwner& o : owner) {  // labels needing a selection, in set order
       if (o.node == a.me_id) continue;
-      lab_routes.push_back(top);
       add_node(o.node);
       set_ptr.push_back((uint32_t)set_nodes.size());
     }
@@ -1284,6 +1307,8 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     };
     // IP routes: equal selections (edges, metrics, family) share one record range
     std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> shared;
+    db->strs.reserve(db->strs.size() + uni.size());
+    db->uni.reserve(db->uni.size() + 6 * uni.size());
     std::vector<dc_nexthop> recs;
     std::string key;
     for (uint32_t i = 0; i < uni.size(); ++i) {
@@ -1338,12 +1363,13 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
         db->add_unicast(*u.prefix, *u.res->best, u.bgp && s->bgp_dry_run, it->second);
       }
     }
-    // node-label routes
+    // node-label routes (selection sets after the IP ones, in label order)
     uint32_t k = (uint32_t)uni.size();
-    std::unordered_map<int32_t, uint32_t> label_set;
-    for (int32_t top : lab_routes) label_set.emplace(top, k++);
-    for (int32_t top : label_order) {
-      const LabelOwner& own = label_to_node.at(top);
+    db->mpls_row.reserve(db->mpls_row.size() + label_order.size());
+    db->mpls.reserve(db->mpls.size() + 3 * label_order.size());
+    for (size_t li = 0; li < label_order.size(); ++li) {
+      const int32_t top = label_order[li];
+      const LabelOwner& own = owner[li];
       if (own.node == a.me_id) {
         NH h;  // POP_AND_LOOKUP, address "::"
         h.action = DC_MPLS_POP_AND_LOOKUP;
@@ -1352,7 +1378,7 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
         db->add_mpls(top, db->add_set(v));
         continue;
       }
-      const uint32_t i = label_set.at(top);
+      const uint32_t i = k++;
       const uint32_t c = sel.cnt[i];
       if (!c) {
         s->bump("decision.no_route_to_label");
@@ -1418,7 +1444,6 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     std::vector<NH> v = nhs;
     db->add_mpls(top, db->add_set(v));
   }
-  for (auto& kv : s->best_cache) kv.second.refs.clear();  // (they pointed into this build)
   phase(5);
   *out = db.release();
   return SPF_OK;

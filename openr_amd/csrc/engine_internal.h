@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -148,6 +149,16 @@ struct spf_ctx {
   bool unit = false;                         // every up edge has metric 1
   uint32_t npitch = 0;                       // narrow (u8) row pitch
   std::vector<uint32_t> sell_ptr, sell_col;  // sliced-ELL columns (64-node slices)
+  uint64_t sell_ver = 0;  // bumped whenever sell_ptr / sell_col change (load, row patch)
+  // msbfs_team_prepare's graph-derived tables for one team size (slices to
+  // members, finalize slots, column streams, frontier slices each member
+  // reads): valid while sell_ver holds, shared by every plan of the context
+  struct TeamTables {
+    uint64_t ver = ~0ull;
+    uint32_t G = 0, own = 0, n_acc = 0, need_words = 0;
+    bool full_copy = false;
+    std::vector<uint32_t> fin, mptr, meta, need;
+  } tm_tab;
   spfi::DevBuf<uint32_t> d_sell_ptr, d_sell_col;
   spfi::DevBuf<uint32_t> d_ms_smap;  // msbfs_kernel: slice of (wave, slot), balanced by width
   std::vector<uint32_t> sell4_ptr, sell4;  // packed u16x4 columns (uint2 entries), planes BFS
@@ -179,6 +190,10 @@ struct spf_ctx {
   // spf_plan_preds' pinned staging: lives with the context (the facade makes
   // a plan per query; pinning per plan cost more than it saved)
   spfi::PinBuf<uint32_t> pin_preds;
+  // plan builds' host-to-device uploads (spfi::stage_upload): one pinned
+  // buffer, copies queued on `stream`, reused once `stream` has synchronised
+  spfi::PinBuf<uint8_t> stage;
+  size_t stage_used = 0;
   // spf_routes' (routes.hip) last plan, kept while its sources and the graph
   // shape hold (executes re-derive it after in-place patches), and its
   // buffers, which only grow: a route build per publication allocates nothing
@@ -190,6 +205,40 @@ struct spf_ctx {
     spfi::DevBuf<uint64_t> mn, metric;
   } rt;
 };
+
+namespace spfi {
+// A plan build's uploads (build_plan, msbfs_team_prepare) through the
+// context's pinned stage: a pageable hipMemcpyAsync is a blocking staged copy
+// (~35 us each on MI355X boxes, a dozen per build_plan), a pinned one is only
+// queued.  Copies go on c->stream; the stage is reused after that stream has
+// synchronised (here when it runs full, and stage_done after a build's final
+// synchronize).  Payloads above kStageMax take the plain path.
+constexpr size_t kStageMax = 8u << 20;
+template <typename T>
+hipError_t stage_upload(spf_ctx* c, DevBuf<T>& d, const T* h, size_t count) {
+  hipError_t e = d.alloc(count);
+  if (e != hipSuccess || count == 0) return e;
+  const size_t bytes = count * sizeof(T);
+  if (bytes > kStageMax) return hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, c->stream);
+  size_t at = (c->stage_used + 255) & ~(size_t)255;
+  if (!c->stage.p || at + bytes > c->stage.n) {
+    if (c->stage_used) {
+      e = hipStreamSynchronize(c->stream);  // every copy out of the stage has landed
+      if (e != hipSuccess) return e;
+    }
+    c->stage_used = at = 0;
+    if (bytes > c->stage.n || !c->stage.p) {
+      e = c->stage.alloc(std::max<size_t>(std::max<size_t>(bytes, 2 * c->stage.n), 1u << 20));
+      if (e != hipSuccess) return e;
+    }
+  }
+  std::memcpy(c->stage.p + at, h, bytes);
+  c->stage_used = at + bytes;
+  return hipMemcpyAsync(d.p, c->stage.p + at, bytes, hipMemcpyHostToDevice, c->stream);
+}
+// after a synchronize of c->stream: the stage's copies are done
+inline void stage_done(spf_ctx* c) { c->stage_used = 0; }
+}  // namespace spfi
 
 struct spf_plan {
   spf_ctx* ctx = nullptr;

@@ -656,53 +656,89 @@ uint32_t msbfs_team_size(const spf_ctx* c, uint32_t rows) {
 spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
   const uint32_t n_slices = (c->N + 63) / 64;
   auto width = [&](uint32_t sl) { return (c->sell_ptr[sl + 1] - c->sell_ptr[sl]) / 64; };
-  // slices to members, widest first to the least-loaded member (column
-  // groups + a slice's finalize cost)
-  std::vector<uint32_t> order(n_slices);
-  for (uint32_t i = 0; i < n_slices; ++i) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return width(x) > width(y); });
-  std::vector<std::vector<uint32_t>> mem(G);
-  std::vector<uint64_t> load(G, 0);
-  for (uint32_t sl : order) {
-    uint32_t best = 0;
-    for (uint32_t m = 1; m < G; ++m)
-      if (load[m] < load[best] || (load[m] == load[best] && mem[m].size() < mem[best].size())) best = m;
-    mem[best].push_back(sl);
-    load[best] += width(sl) + 2;
-  }
-  uint32_t n_acc = 1;
-  for (auto& v : mem) n_acc = std::max<uint32_t>(n_acc, (uint32_t)v.size());
-  const uint32_t need = (n_acc + kTmWaves - 1) / kTmWaves;
-  const uint32_t own = need <= 1 ? 1 : need <= 2 ? 2 : 4;
-  if (need > 4 || team_lds(team_fwords(c->N), n_acc) > kTmMaxLds)
-    return fail(c, SPF_E_INVALID, "msbfs_team: %u slices per member do not fit", n_acc);
-  // per member: finalize slots dealt round robin to the waves; the member's
-  // column groups (its slices' in order) cut into kTmWaves equal ranges, each
-  // range a stream of {group | slot << 20}, padded to whole chunks of 16 with
-  // the all-padding group after the last slice (sell_col's tail)
-  const uint32_t units = G * kTmWaves;
-  const uint32_t dummy = c->sell_ptr.back() / 64;
-  if (dummy >= (1u << 20) || n_acc >= (1u << 12))
-    return fail(c, SPF_E_INVALID, "msbfs_team: column groups exceed the stream encoding");
-  std::vector<uint32_t> fin((size_t)units * own, 0xFFFFu), mptr(units + 1, 0);
-  std::vector<uint32_t> meta;
-  for (uint32_t m = 0; m < G; ++m) {
-    const auto& S = mem[m];
-    for (uint32_t k = 0; k < S.size(); ++k)
-      fin[((size_t)m * kTmWaves + k % kTmWaves) * own + k / kTmWaves] = S[k] | (k << 16);
-    std::vector<uint32_t> all;  // the member's stream
-    for (uint32_t k = 0; k < S.size(); ++k)
-      for (uint32_t g = 0; g < width(S[k]); ++g) all.push_back((c->sell_ptr[S[k]] / 64 + g) | (k << 20));
-    const uint64_t T = all.size();
-    for (uint32_t w = 0; w < kTmWaves; ++w) {
-      mptr[m * kTmWaves + w] = (uint32_t)meta.size();
-      const uint64_t b = T * w / kTmWaves, e = T * (w + 1) / kTmWaves;
-      for (uint64_t t = b; t < e; ++t) meta.push_back(all[t]);
-      if (e > b)
-        while (meta.size() % 16) meta.push_back(dummy | (all[e - 1] & 0xFFF00000u));
+  const char* ne = std::getenv("SPF_TEAM_FULLCOPY");  // A/B: copy the whole frontier
+  const bool full_copy = ne && ne[0] == '1';
+  spf_ctx::TeamTables& T = c->tm_tab;
+  // the graph-derived tables: computed once per sliced-ELL state and team
+  // size (a plan re-derived after an overload or metric patch, or a new
+  // single-source plan per query, reuses them -- the need pass alone walks
+  // every column of the graph)
+  if (T.ver != c->sell_ver || T.G != G || T.full_copy != full_copy) {
+    T.ver = ~0ull;
+    // slices to members, widest first to the least-loaded member (column
+    // groups + a slice's finalize cost)
+    std::vector<uint32_t> order(n_slices);
+    for (uint32_t i = 0; i < n_slices; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return width(x) > width(y); });
+    std::vector<std::vector<uint32_t>> mem(G);
+    std::vector<uint64_t> load(G, 0);
+    for (uint32_t sl : order) {
+      uint32_t best = 0;
+      for (uint32_t m = 1; m < G; ++m)
+        if (load[m] < load[best] || (load[m] == load[best] && mem[m].size() < mem[best].size())) best = m;
+      mem[best].push_back(sl);
+      load[best] += width(sl) + 2;
     }
+    uint32_t n_acc = 1;
+    for (auto& v : mem) n_acc = std::max<uint32_t>(n_acc, (uint32_t)v.size());
+    const uint32_t need = (n_acc + kTmWaves - 1) / kTmWaves;
+    const uint32_t own = need <= 1 ? 1 : need <= 2 ? 2 : 4;
+    if (need > 4 || team_lds(team_fwords(c->N), n_acc) > kTmMaxLds)
+      return fail(c, SPF_E_INVALID, "msbfs_team: %u slices per member do not fit", n_acc);
+    // per member: finalize slots dealt round robin to the waves; the member's
+    // column groups (its slices' in order) cut into kTmWaves equal ranges, each
+    // range a stream of {group | slot << 20}, padded to whole chunks of 16 with
+    // the all-padding group after the last slice (sell_col's tail)
+    const uint32_t units = G * kTmWaves;
+    const uint32_t dummy = c->sell_ptr.back() / 64;
+    if (dummy >= (1u << 20) || n_acc >= (1u << 12))
+      return fail(c, SPF_E_INVALID, "msbfs_team: column groups exceed the stream encoding");
+    std::vector<uint32_t>& fin = T.fin;
+    std::vector<uint32_t>& mptr = T.mptr;
+    std::vector<uint32_t>& meta = T.meta;
+    fin.assign((size_t)units * own, 0xFFFFu);
+    mptr.assign(units + 1, 0);
+    meta.clear();
+    for (uint32_t m = 0; m < G; ++m) {
+      const auto& S = mem[m];
+      for (uint32_t k = 0; k < S.size(); ++k)
+        fin[((size_t)m * kTmWaves + k % kTmWaves) * own + k / kTmWaves] = S[k] | (k << 16);
+      std::vector<uint32_t> all;  // the member's stream
+      for (uint32_t k = 0; k < S.size(); ++k)
+        for (uint32_t g = 0; g < width(S[k]); ++g) all.push_back((c->sell_ptr[S[k]] / 64 + g) | (k << 20));
+      const uint64_t Tn = all.size();
+      for (uint32_t w = 0; w < kTmWaves; ++w) {
+        mptr[m * kTmWaves + w] = (uint32_t)meta.size();
+        const uint64_t b = Tn * w / kTmWaves, e = Tn * (w + 1) / kTmWaves;
+        for (uint64_t t = b; t < e; ++t) meta.push_back(all[t]);
+        if (e > b)
+          while (meta.size() % 16) meta.push_back(dummy | (all[e - 1] & 0xFFF00000u));
+      }
+    }
+    mptr[units] = (uint32_t)meta.size();
+    // per member: the 64-node slices its stream's columns read (frontier copy)
+    const uint32_t fslices = (team_fwords(c->N) + 63) / 64;
+    const uint32_t nw = (fslices + 31) / 32;
+    T.need.assign((size_t)G * nw, full_copy ? ~0u : 0u);
+    if (!full_copy)
+      for (uint32_t m = 0; m < G; ++m)
+        for (uint32_t sl : mem[m])
+          for (uint32_t e = c->sell_ptr[sl]; e < c->sell_ptr[sl + 1]; ++e) {
+            const uint32_t x = c->sell_col[e] / 64;
+            T.need[(size_t)m * nw + x / 32] |= 1u << (x % 32);
+          }
+    T.need_words = nw;
+    T.n_acc = n_acc;
+    T.own = own;
+    T.G = G;
+    T.full_copy = full_copy;
+    T.ver = c->sell_ver;
   }
-  mptr[units] = (uint32_t)meta.size();
+  const uint32_t n_acc = T.n_acc, own = T.own;
+  const std::vector<uint32_t>& fin = T.fin;
+  const std::vector<uint32_t>& mptr = T.mptr;
+  const std::vector<uint32_t>& meta = T.meta;
+  const uint32_t dummy = c->sell_ptr.back() / 64;
   const uint32_t per_xcd = c->n_cu / 8;
   const uint32_t teams = 8 * (per_xcd / G);
   const uint32_t rows = (uint32_t)p->closure.size();
@@ -748,21 +784,10 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
   p->tm_runs_at = (uint32_t)tab.size();
   tab.insert(tab.end(), meta.begin(), meta.end());
   tab.insert(tab.end(), 32, dummy);  // the sweep's loads run up to two chunks past a range
-  {  // per member: the 64-node slices its stream's columns read (frontier copy)
-    const uint32_t fslices = (team_fwords(c->N) + 63) / 64;
-    const uint32_t nw = (fslices + 31) / 32;
+  {  // per member: the frontier slices its stream reads (cached above)
     p->tm_need_at = (uint32_t)tab.size();
-    p->tm_need_words = nw;
-    tab.resize(tab.size() + (size_t)G * nw, 0u);
-    uint32_t* need = tab.data() + p->tm_need_at;
-    const char* ne = std::getenv("SPF_TEAM_FULLCOPY");  // A/B: copy the whole frontier
-    for (uint32_t m = 0; m < G; ++m)
-      for (uint32_t sl : mem[m])
-        for (uint32_t e = c->sell_ptr[sl]; e < c->sell_ptr[sl + 1]; ++e) {
-          const uint32_t x = c->sell_col[e] / 64;
-          need[(size_t)m * nw + x / 32] |= 1u << (x % 32);
-        }
-    if (ne && ne[0] == '1') std::fill(need, need + (size_t)G * nw, ~0u);
+    p->tm_need_words = T.need_words;
+    tab.insert(tab.end(), T.need.begin(), T.need.end());
   }
   // the drained nodes (level 1 is pushed into every node's entry; these
   // keep none of it as frontier)
@@ -790,7 +815,7 @@ spf_status msbfs_team_prepare(spf_ctx* c, spf_plan* p, uint32_t G) {
       return fail(c, SPF_E_INVALID, "msbfs_team: push list exceeds its encoding");
     tab.insert(tab.end(), lst.begin(), lst.end());
   }
-  HIP_TRY(c, p->d_tm_map.upload(tab.data(), tab.size(), c->stream));
+  HIP_TRY(c, stage_upload(c, p->d_tm_map, tab.data(), tab.size()));
   HIP_TRY(c, p->d_tm_F.alloc((size_t)teams * 2 * fw * 2));  // u64 as 2 words
   HIP_TRY(c, p->d_tm_bar.alloc((size_t)teams * kTmBarPad * 4));
   // zeroed once: every launch leaves them zero (the kernel's exit protocol)

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1831,6 +1832,7 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
     // kernel's stream pads with, and the BFS kernels' unconditional loads up
     // to three groups of 8 columns past a slice's last column
     c->sell_col.assign(c->sell_ptr[n_slices] + 32 * kSliceW, N);
+    ++c->sell_ver;
     for (uint32_t v = 0; v < N; ++v) {
       const uint32_t sl = v / kSliceW, ln = v % kSliceW;
       for (uint32_t j = 0; j < c->row_ptr[v + 1] - c->row_ptr[v]; ++j) {
@@ -2172,6 +2174,7 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
       }
     }
   }
+  ++c->sell_ver;  // (msbfs_team_prepare's cached tables read sell_col)
   // upload the changed ranges only: the touched rows (merged when adjacent),
   // the partner slots their reverse edges point at, and the touched slices
   std::vector<uint32_t> order(nodes, nodes + n);
@@ -2348,6 +2351,16 @@ bool use_narrow(const spf_ctx* c, const spf_plan* p) {
 // (spf_graph_set_overload / spf_graph_set_metric); the output layout
 // (nh_off, words) depends only on the CSR structure, which patches keep.
 spf_status build_plan(spf_ctx* c, spf_plan* p) {
+  // SPF_PLAN_DEBUG: per-phase host time of the build on stderr (diagnostics)
+  static const bool pd_on = std::getenv("SPF_PLAN_DEBUG") != nullptr;
+  auto pd_t0 = std::chrono::steady_clock::now();
+  auto PD = [&](const char* what) {
+    if (!pd_on) return;
+    (void)hipStreamSynchronize(c->stream);
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "build_plan %s %.1f us\n", what, std::chrono::duration<double, std::micro>(t - pd_t0).count());
+    pd_t0 = t;
+  };
   const uint32_t n_src = p->n_src;
   const uint32_t* srcs = p->srcs.data();
   const bool hop = (p->flags & SPF_FLAG_HOP_COUNT) != 0;
@@ -2393,13 +2406,15 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       const spf_status st = exact_reserve(c, &p->xs, n_src, p->wmax);
       if (st != SPF_OK) return st;
     }
-    HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
-    HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
-    HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
+    HIP_TRY(c, stage_upload(c, p->d_srcs, p->srcs.data(), n_src));
+    HIP_TRY(c, stage_upload(c, p->d_nh_off, p->nh_off.data(), n_src));
+    HIP_TRY(c, stage_upload(c, p->d_words, p->words.data(), n_src));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    stage_done(c);
     p->epoch = c->epoch;
     return SPF_OK;
   }
+  PD("start");
   p->closure.clear();
   std::vector<uint32_t> row_of(N, kInf);
   bool distinct = true;
@@ -2463,12 +2478,12 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
   p->q16 = N <= 65535;
   p->lds_bytes = sssp_lds_bytes(N, c->pitch, c->big_nodes, p->q16);
   HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, p->d_srcs.upload(p->srcs.data(), n_src, c->stream));
-  HIP_TRY(c, p->d_closure.upload(p->closure.data(), p->closure.size(), c->stream));
-  HIP_TRY(c, p->d_row_of.upload(row_of.data(), N, c->stream));
-  HIP_TRY(c, p->d_req_rows.upload(req_rows.data(), n_src, c->stream));
-  HIP_TRY(c, p->d_nh_off.upload(p->nh_off.data(), n_src, c->stream));
-  HIP_TRY(c, p->d_words.upload(p->words.data(), n_src, c->stream));
+  HIP_TRY(c, stage_upload(c, p->d_srcs, p->srcs.data(), n_src));
+  HIP_TRY(c, stage_upload(c, p->d_closure, p->closure.data(), p->closure.size()));
+  HIP_TRY(c, stage_upload(c, p->d_row_of, row_of.data(), N));
+  HIP_TRY(c, stage_upload(c, p->d_req_rows, req_rows.data(), n_src));
+  HIP_TRY(c, stage_upload(c, p->d_nh_off, p->nh_off.data(), n_src));
+  HIP_TRY(c, stage_upload(c, p->d_words, p->words.data(), n_src));
   p->ms = (hop || c->unit) && N <= kMsMaxNodes;
   // register-plane BFS: batches of similar depth, deepest first (more than
   // one round of batches only; SPF_PL_ORDER=0 keeps the plan order, A/B)
@@ -2482,12 +2497,13 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
         return ecc[p->closure[a]] > ecc[p->closure[b]];
       });
-      HIP_TRY(c, p->d_pl_order.upload(order.data(), order.size(), c->stream));
+      HIP_TRY(c, stage_upload(c, p->d_pl_order, order.data(), order.size()));
       p->pl_order = true;
     }
   }
   // few batches (a rank's share of a multi-GPU pass): teams of workgroups
   // per batch (msbfs_team.hip) instead of one workgroup sweeping everything
+  PD("uploads1");
   p->tm_G = 0;
   if (p->ms && !use_planes(c) && !p->expand && !c->team_off) {
     const uint32_t G = msbfs_team_size(c, (uint32_t)p->closure.size());
@@ -2497,6 +2513,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     }
   }
   // weighted: S sources per workgroup on mssp_kernel where it applies
+  PD("team");
   p->mp = !p->ms && !hop && mssp_words(c) > 0;
   if (p->mp) {
     const spf_status st = mssp_prepare(c);
@@ -2554,9 +2571,9 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       const size_t k = nb_row.size() - nb_row_off[i];
       nb_row.resize(nb_row_off[i] + (k + 7) / 8 * 8 + 8, dead);
     }
-    HIP_TRY(c, p->d_nb_row.upload(nb_row.data(), nb_row.size(), c->stream));
-    HIP_TRY(c, p->d_nb_row_off.upload(nb_row_off.data(), n_src, c->stream));
-    HIP_TRY(c, p->d_nb_drained.upload(nb_drained.data(), n_src, c->stream));
+    HIP_TRY(c, stage_upload(c, p->d_nb_row, nb_row.data(), nb_row.size()));
+    HIP_TRY(c, stage_upload(c, p->d_nb_row_off, nb_row_off.data(), n_src));
+    HIP_TRY(c, stage_upload(c, p->d_nb_drained, nb_drained.data(), n_src));
     // next-hop blocks per XCD: runs of consecutive sources of about
     // 1/(8 * runs) of the work each, every run to the XCD with the least
     // work so far (runs come in request order: the heavy spine and fabric
@@ -2582,6 +2599,7 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
         i = e;
       }
     }
+    PD("nb_rows");
     if (p->sliced) {
       // sliced-pass work units per XCD, in the XCD's source order: a source
       // whose neighbour-chunk matches fit kSlUnit is one unit, a heavier one
@@ -2715,10 +2733,10 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       }
       unit_off[8] = (uint32_t)(units.size() / 4);
       if (units.empty()) units.assign(4, 0);
-      HIP_TRY(c, p->d_units.upload(units.data(), units.size(), c->stream));
-      HIP_TRY(c, p->d_unit_off.upload(unit_off.data(), 9, c->stream));
+      HIP_TRY(c, stage_upload(c, p->d_units, units.data(), units.size()));
+      HIP_TRY(c, stage_upload(c, p->d_unit_off, unit_off.data(), 9));
       if (gtab.empty()) gtab.push_back(0);
-      HIP_TRY(c, p->d_gtab.upload(gtab.data(), gtab.size(), c->stream));
+      HIP_TRY(c, stage_upload(c, p->d_gtab, gtab.data(), gtab.size()));
     }
     size_t most = 0;
     for (auto& l : lists) most = std::max(most, l.size());
@@ -2727,9 +2745,11 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
       for (size_t t = 0; t < lists[g].size(); ++t) slot[t * 8 + g] = lists[g][t];
     p->slots = slot.size();
     if (slot.empty()) slot.push_back(kInf);
-    HIP_TRY(c, p->d_slot_src.upload(slot.data(), slot.size(), c->stream));
+    HIP_TRY(c, stage_upload(c, p->d_slot_src, slot.data(), slot.size()));
     HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors end here
+    stage_done(c);
   }
+  PD("units+slots");
   if (!p->direct) HIP_TRY(c, p->d_D.alloc((size_t)p->closure.size() * c->pitch));
   if (p->narrow && !p->sdirect) {  // narrow rows + the dead row (all 0xFF) of the next-hop pass
     HIP_TRY(c, p->d_Dn.alloc((p->closure.size() + 1) * c->npitch));
@@ -2749,7 +2769,9 @@ spf_status build_plan(spf_ctx* c, spf_plan* p) {
     const spf_status st = set_lds_limits(c);  // kernels need > 64 KiB of dynamic LDS
     if (st != SPF_OK) return st;
   }
+  PD("allocs");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  stage_done(c);
   p->epoch = c->epoch;
   return SPF_OK;
 }
