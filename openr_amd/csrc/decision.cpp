@@ -218,7 +218,26 @@ struct dc_route_db {
   std::vector<int32_t> labels;
   std::vector<uint32_t> uni;   // rows of 6
   std::vector<uint32_t> mpls;  // rows of 3
-  std::unordered_map<int32_t, size_t> mpls_row;
+  // label -> its row in mpls: open addressing, (label, row + 1) per slot, row
+  // + 1 == 0 empty (a build adds one per node label: no node allocation each)
+  std::vector<std::pair<uint32_t, uint32_t>> lrow;
+  size_t lrow_used = 0;
+
+  void reserve_labels(size_t n) {
+    size_t want = 64;
+    while (want < 2 * (lrow_used + n)) want *= 2;
+    if (want <= lrow.size()) return;
+    std::vector<std::pair<uint32_t, uint32_t>> old(want, {0u, 0u});
+    old.swap(lrow);
+    for (const auto& kv : old)
+      if (kv.second) lrow[lrow_slot(kv.first)] = kv;
+  }
+  size_t lrow_slot(uint32_t label) const {  // the label's slot, or the empty one ending its probe
+    const size_t mask = lrow.size() - 1;
+    size_t h = (size_t)(label * 0x9E3779B1u) & mask;
+    while (lrow[h].second && lrow[h].first != label) h = (h + 1) & mask;
+    return h;
+  }
 
   uint32_t intern(const std::string& s) {
     auto it = sid.find(s);
@@ -274,13 +293,15 @@ struct dc_route_db {
   // dict assignment, as the restatement's DecisionRouteDb (the reference
   // CHECKs that a label is added once, Decision.h:116-120)
   void add_mpls(int32_t label, std::pair<uint32_t, uint32_t> r) {
-    auto it = mpls_row.find(label);
-    if (it != mpls_row.end()) {
-      mpls[it->second + 1] = r.first;
-      mpls[it->second + 2] = r.second;
+    reserve_labels(1);
+    auto& slot = lrow[lrow_slot((uint32_t)label)];
+    if (slot.second) {  // a later route for the label replaces the earlier one
+      mpls[slot.second - 1 + 1] = r.first;
+      mpls[slot.second - 1 + 2] = r.second;
       return;
     }
-    mpls_row.emplace(label, mpls.size());
+    slot = {(uint32_t)label, (uint32_t)mpls.size() + 1};
+    ++lrow_used;
     mpls.insert(mpls.end(), {(uint32_t)label, r.first, r.second});
   }
 };
@@ -1301,7 +1322,15 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
       }
       by_link.emplace(l.id, r);
     }
+    // me's CSR edges -> their link's record (the selection returns edges of me's row)
+    const uint32_t e0 = m != ~0u ? g->row_ptr[m] : 0u, e1 = m != ~0u ? g->row_ptr[m + 1] : 0u;
+    std::vector<const LinkRec*> rec_at(e1 - e0, nullptr);
+    for (uint32_t e = e0; e < e1; ++e) {
+      auto it = by_link.find(g->link_id[e]);
+      rec_at[e - e0] = it == by_link.end() ? nullptr : &it->second;
+    }
     auto edge_rec = [&](uint32_t e) -> const LinkRec* {
+      if (e - e0 < rec_at.size()) return rec_at[e - e0];
       auto it = by_link.find(g->link_id[e]);
       return it == by_link.end() ? nullptr : &it->second;
     };
@@ -1365,7 +1394,7 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     }
     // node-label routes (selection sets after the IP ones, in label order)
     uint32_t k = (uint32_t)uni.size();
-    db->mpls_row.reserve(db->mpls_row.size() + label_order.size());
+    db->reserve_labels(label_order.size());
     db->mpls.reserve(db->mpls.size() + 3 * label_order.size());
     for (size_t li = 0; li < label_order.size(); ++li) {
       const int32_t top = label_order[li];
