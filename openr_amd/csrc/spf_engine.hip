@@ -2309,23 +2309,35 @@ const std::vector<uint32_t>& ecc_estimate(spf_ctx* c) {
 // copy (bound < 254) never need u32 rows of non-source closure rows.
 uint32_t depth_bound(spf_ctx* c) {
   if (c->dbound_epoch == c->epoch) return c->dbound;
+  // one level-synchronous BFS per component over the distinct up neighbours;
+  // drained nodes are neither roots nor transit, so they start out seen (one
+  // byte test per edge -- recomputed after every patch, on the path of the
+  // first plan build of a publication)
   const uint32_t N = c->N;
-  std::vector<uint32_t> d(N, kInf), q;
+  std::vector<uint8_t> seen(N);
+  for (uint32_t v = 0; v < N; ++v) seen[v] = c->ovl[v] != 0;
+  std::vector<uint32_t> q(std::max<uint32_t>(N, 1));
+  const uint32_t* nbp = c->nb_ptr.data();
+  const uint32_t* nbi = c->nb_id.data();
   uint32_t worst = 0;
   for (uint32_t r = 0; r < N; ++r) {
-    if (c->ovl[r] || d[r] != kInf) continue;
-    d[r] = 0;
-    q.assign(1, r);
+    if (seen[r]) continue;
+    seen[r] = 1;
+    size_t head = 0, tail = 0, level_end = 1;
+    q[tail++] = r;
     uint32_t ecc = 0;
-    for (size_t h = 0; h < q.size(); ++h) {
-      const uint32_t u = q[h];
-      ecc = std::max(ecc, d[u]);
-      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
-        const uint32_t x = c->col[e];
-        if (!c->ovl[x] && d[x] == kInf) {
-          d[x] = d[u] + 1;
-          q.push_back(x);
+    while (head < tail) {
+      const uint32_t u = q[head++];
+      for (uint32_t e = nbp[u]; e < nbp[u + 1]; ++e) {
+        const uint32_t x = nbi[e];
+        if (!seen[x]) {
+          seen[x] = 1;
+          q[tail++] = x;
         }
+      }
+      if (head == level_end && head < tail) {  // the next level starts
+        ++ecc;
+        level_end = tail;
       }
     }
     worst = std::max(worst, ecc);
