@@ -376,7 +376,8 @@ struct Area {
   }
   uint32_t sid(dc_route_db* db, uint32_t name_id, const std::string& name) {
     if (name_id >= db_sid.size()) db_sid.resize(std::max<size_t>(name_id + 1, 2 * db_sid.size()), 0);
-    if (!db_sid[name_id]) db_sid[name_id] = db->intern(name) + 1;
+    // (one table entry per name and build: no lookup among the other strings)
+    if (!db_sid[name_id]) db_sid[name_id] = db->push_unique(name) + 1;
     return db_sid[name_id] - 1;
   }
   std::string name_of(uint32_t i) const { return ls_name(ls, i); }
@@ -533,8 +534,8 @@ struct Build {
     return filter_drained(std::move(ret));
   }
 
-  std::optional<BestRoute> select_best(const Entries& ents, bool bgp) {  // selectBestRoutes :728-748
-    BestRoute ret;
+  // `ret`: an empty result whose vectors may hold capacity (the cache slot's)
+  std::optional<BestRoute> select_best(const Entries& ents, bool bgp, BestRoute ret = {}) {  // selectBestRoutes :728-748
     if (s->best_route_selection) {
       // selectBestPrefixMetrics (Util.h:540-571): best (pp, sp, -distance) from (0, 0, 0)
       std::tuple<int64_t, int64_t, int64_t> bt{0, 0, 0};
@@ -1143,7 +1144,7 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
   auto reached = [&](const std::pair<const NodeArea, Entry>& kv) {
     Area* a = b.area_of(kv.first.second);
     if (!a) return true;
-    return mine[area_idx.at(a)]->find(a->id(kv)) >= 0;
+    return mine[single ? 0 : area_idx.at(a)]->find(a->id(kv)) >= 0;
   };
   for (const auto& [prefix, all] : ps->prefixes) {
     // entries of nodes unreachable in their own area dropped (:409-420): the
@@ -1181,15 +1182,23 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
       s->bump("decision.skipped_unicast_route");
       continue;
     }
-    auto sel = b.select_best(ents, has_bgp);
+    // bestRoutesCache_ (its refs point into this build's entries: cleared
+    // when the build ends); the selection starts from the slot's vectors, so
+    // a prefix re-selected every build allocates nothing (a slot this build
+    // does not fill keeps an old generation and is swept)
+    BestRoute& slot = s->best_cache[prefix];
+    BestRoute scratch;
+    scratch.all.swap(slot.all);
+    scratch.refs.swap(slot.refs);
+    scratch.all.clear();
+    scratch.refs.clear();
+    auto sel = b.select_best(ents, has_bgp, std::move(scratch));
     if (!b.ok()) return b.st;
     if (!sel->success) continue;
     if (sel->all.empty()) {
       s->bump("decision.no_route_to_prefix");
       continue;
     }
-    // bestRoutesCache_ (its refs point into this build's entries: cleared below)
-    BestRoute& slot = s->best_cache[prefix];
     slot = std::move(*sel);
     slot.gen = gen;
     const BestRoute& res = slot;
