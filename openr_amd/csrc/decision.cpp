@@ -1234,8 +1234,17 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     Area* area;
     std::string name() const { return ls_name(area->ls, node); }
   };
-  std::unordered_map<int32_t, LabelOwner> label_to_node;
+  // labels in first-seen order with their owners; label -> position by open
+  // addressing (one slot per label, no node allocation per label)
   std::vector<int32_t> label_order;
+  std::vector<LabelOwner> owner;
+  std::vector<uint32_t> lpos;  // position + 1, 0 = empty
+  auto lslot = [&](int32_t top) {
+    const size_t mask = lpos.size() - 1;
+    size_t h = (size_t)((uint32_t)top * 0x9E3779B1u) & mask;
+    while (lpos[h] && label_order[lpos[h] - 1] != top) h = (h + 1) & mask;
+    return h;
+  };
   for (auto& ap : b.areas) {
     Area& a = *ap;
     uint32_t n = 0;
@@ -1243,15 +1252,26 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     std::vector<uint32_t> ids(n);
     std::vector<int32_t> lab(n);
     ls_adjacency_databases(a.ls, ids.data(), lab.data(), n, &n);
-    label_to_node.reserve(label_to_node.size() + n);
+    {  // room for every label of this area at <= 1/2 load
+      size_t want = 64;
+      while (want < 2 * (label_order.size() + n)) want *= 2;
+      if (want > lpos.size()) {
+        lpos.assign(want, 0u);
+        for (uint32_t k = 0; k < label_order.size(); ++k) lpos[lslot(label_order[k])] = k + 1;
+      }
+    }
     for (uint32_t i = 0; i < n; ++i) {
       const int32_t top = lab[i];
       if (top == 0 || !mpls_label_valid(top)) continue;
-      auto [it, fresh] = label_to_node.emplace(top, LabelOwner{ids[i], &a});
-      if (fresh) {
+      uint32_t& pos = lpos[lslot(top)];
+      if (!pos) {
         label_order.push_back(top);
-      } else if (!(std::strcmp(ls_name(it->second.area->ls, it->second.node), ls_name(a.ls, ids[i])) < 0)) {
-        it->second = {ids[i], &a};  // the collision's smaller name wins (a tie: the later area)
+        owner.push_back({ids[i], &a});
+        pos = (uint32_t)label_order.size();
+      } else {
+        LabelOwner& o = owner[pos - 1];
+        if (!(std::strcmp(ls_name(o.area->ls, o.node), ls_name(a.ls, ids[i])) < 0))
+          o = {ids[i], &a};  // the collision's smaller name wins (a tie: the later area)
       }
     }
   }
@@ -1271,10 +1291,6 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
       for (EntryRef r : u.res->refs) add_node(a.id(*r));
       set_ptr.push_back((uint32_t)set_nodes.size());
     }
-    // each label's final owner (after the collision rule), in label order
-    std::vector<LabelOwner> owner;
-    owner.reserve(label_order.size());
-    for (int32_t top : label_order) owner.push_back(label_to_node.at(top));
     for (const LabelOwner& o : owner) {  // labels needing a selection, in set order
       if (o.node == a.me_id) continue;
       add_node(o.node);
@@ -1440,8 +1456,9 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
       db->add_mpls(top, db->add_records(recs));
     }
   } else {
-    for (int32_t top : label_order) {
-      const LabelOwner& own = label_to_node.at(top);
+    for (size_t li = 0; li < label_order.size(); ++li) {
+      const int32_t top = label_order[li];
+      const LabelOwner& own = owner[li];
       const std::string node = own.name();
       if (node == me) {
         NH h;
