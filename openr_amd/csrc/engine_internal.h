@@ -138,6 +138,9 @@ struct spf_ctx {
   bool nonpos = false;
   bool needs64 = false;  // a negative metric or max metric x (N-1) >= 2^32 - 1: u64 labels
   uint32_t max_metric = 0;
+  // live directed edges with metric <= 0, < 0, and weight == max_metric: a
+  // row patch updates the metric facts from these without a graph scan
+  uint64_t n_nonpos = 0, n_neg = 0, n_at_max = 0;
   std::vector<uint32_t> row_ptr, col, wt, rev, link;
   std::vector<int32_t> met;  // metrics as advertised (exact kernel)
   spfi::DevBuf<int32_t> d_met;
@@ -214,27 +217,38 @@ namespace spfi {
 // synchronised (here when it runs full, and stage_done after a build's final
 // synchronize).  Payloads above kStageMax take the plain path.
 constexpr size_t kStageMax = 8u << 20;
-template <typename T>
-hipError_t stage_upload(spf_ctx* c, DevBuf<T>& d, const T* h, size_t count) {
-  hipError_t e = d.alloc(count);
-  if (e != hipSuccess || count == 0) return e;
-  const size_t bytes = count * sizeof(T);
-  if (bytes > kStageMax) return hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, c->stream);
+// bytes from host memory to device memory through the stage (queued on c->stream)
+inline hipError_t stage_copy(spf_ctx* c, void* dst, const void* h, size_t bytes) {
+  if (bytes == 0) return hipSuccess;
+  if (bytes > kStageMax) return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, c->stream);
   size_t at = (c->stage_used + 255) & ~(size_t)255;
   if (!c->stage.p || at + bytes > c->stage.n) {
     if (c->stage_used) {
-      e = hipStreamSynchronize(c->stream);  // every copy out of the stage has landed
+      const hipError_t e = hipStreamSynchronize(c->stream);  // every copy out of the stage has landed
       if (e != hipSuccess) return e;
     }
     c->stage_used = at = 0;
     if (bytes > c->stage.n || !c->stage.p) {
-      e = c->stage.alloc(std::max<size_t>(std::max<size_t>(bytes, 2 * c->stage.n), 1u << 20));
+      const hipError_t e = c->stage.alloc(std::max<size_t>(std::max<size_t>(bytes, 2 * c->stage.n), 1u << 20));
       if (e != hipSuccess) return e;
     }
   }
   std::memcpy(c->stage.p + at, h, bytes);
   c->stage_used = at + bytes;
-  return hipMemcpyAsync(d.p, c->stage.p + at, bytes, hipMemcpyHostToDevice, c->stream);
+  return hipMemcpyAsync(dst, c->stage.p + at, bytes, hipMemcpyHostToDevice, c->stream);
+}
+template <typename T>
+hipError_t stage_upload(spf_ctx* c, DevBuf<T>& d, const T* h, size_t count) {
+  const hipError_t e = d.alloc(count);
+  if (e != hipSuccess || count == 0) return e;
+  return stage_copy(c, d.p, h, count * sizeof(T));
+}
+// h[off, off + count) into the allocated buffer at the same offset
+template <typename T>
+hipError_t stage_upload_at(spf_ctx* c, DevBuf<T>& d, const T* h, size_t off, size_t count) {
+  if (count == 0) return hipSuccess;
+  if (!d.p || off + count > d.n) return hipErrorInvalidValue;
+  return stage_copy(c, d.p + off, h + off, count * sizeof(T));
 }
 // after a synchronize of c->stream: the stage's copies are done
 inline void stage_done(spf_ctx* c) { c->stage_used = 0; }

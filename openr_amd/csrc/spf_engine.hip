@@ -1696,6 +1696,33 @@ void spf_ctx_destroy(spf_ctx* c) {
   delete c;
 }
 
+// Live-edge metric facts (nonpos, needs64, max_metric, unit) from a scan of
+// the graph, with the counts a row patch keeps them current by
+static void metric_flags(spf_ctx* c) {
+  c->nonpos = c->n_nonpos > 0;
+  // i32 -> u64 wraps (LinkState.h:22); the longest possible path beyond 32
+  // bits takes the exact kernel's u64 labels (SPF_FLAG_DIST64)
+  c->needs64 = c->n_neg > 0 || (uint64_t)c->max_metric * (uint64_t)(c->N - 1) >= (uint64_t)kInf;
+  c->unit = !c->nonpos && c->max_metric <= 1;
+}
+static void metric_facts(spf_ctx* c) {
+  c->n_nonpos = c->n_neg = c->n_at_max = 0;
+  c->max_metric = 0;
+  for (uint32_t u = 0; u < c->N; ++u)
+    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
+      if (c->col[e] == u) continue;  // dead slot
+      c->n_nonpos += c->met[e] <= 0;
+      c->n_neg += c->met[e] < 0;
+      if (c->wt[e] > c->max_metric) {
+        c->max_metric = c->wt[e];
+        c->n_at_max = 1;
+      } else if (c->wt[e] == c->max_metric) {
+        ++c->n_at_max;
+      }
+    }
+  metric_flags(c);
+}
+
 spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
   if (!c || !g) return fail(c, SPF_E_INVALID, "spf_graph_load: NULL argument");
   const uint32_t N = g->n_nodes, E = g->n_edges;
@@ -1742,10 +1769,7 @@ spf_status spf_graph_load(spf_ctx* c, const spf_graph* g) {
       if (m < 0) c->needs64 = true;  // i32 -> u64 wraps (LinkState.h:22)
       c->max_metric = std::max(c->max_metric, c->wt[e]);
     }
-  c->unit = !c->nonpos && c->max_metric <= 1;
-  // longest possible path beyond 32 bits: weighted solves take the exact
-  // kernel's u64 labels (SPF_FLAG_DIST64)
-  if ((uint64_t)c->max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf) c->needs64 = true;
+  metric_facts(c);  // (the same facts, with the counts row patches update)
   // reverse edge of every directed edge (same link id, swapped ends)
   c->rev.assign(E, kInf);
   {
@@ -1955,21 +1979,9 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
     met[edges[i]] = metric[i];
   }
   if (!changed) return SPF_OK;
-  bool nonpos = false, neg = false;
-  uint32_t max_metric = 0;
-  for (uint32_t u = 0; u < c->N; ++u)
-    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
-      if (c->col[e] == u) continue;  // dead slot
-      nonpos |= met[e] <= 0;
-      neg |= met[e] < 0;
-      max_metric = std::max(max_metric, wt[e]);
-    }
   c->wt.swap(wt);
   c->met.swap(met);
-  c->needs64 = neg || (uint64_t)max_metric * (uint64_t)(c->N - 1) >= (uint64_t)kInf;
-  c->nonpos = nonpos;
-  c->max_metric = max_metric;
-  c->unit = !nonpos && max_metric <= 1;
+  metric_facts(c);
   // min metric per distinct neighbour of every tail touched
   std::vector<uint32_t> tails;
   for (uint32_t i = 0; i < n; ++i)
@@ -2037,9 +2049,19 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
   }
   std::vector<uint32_t> old_nb(n);
   for (uint32_t i = 0; i < n; ++i) old_nb[i] = c->nb_ptr[nodes[i] + 1] - c->nb_ptr[nodes[i]];
-  // rows
+  // rows (the metric-fact counts lose the old rows' live edges and gain the
+  // new ones')
   {
     size_t o = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t u = nodes[i];
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+        if (c->col[e] != u) {
+          c->n_nonpos -= c->met[e] <= 0;
+          c->n_neg -= c->met[e] < 0;
+          c->n_at_max -= c->wt[e] == c->max_metric;
+        }
+    }
     for (uint32_t i = 0; i < n; ++i) {
       const uint32_t u = nodes[i];
       for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e, ++o) {
@@ -2049,6 +2071,20 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
         c->link[e] = link[o];
       }
     }
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t u = nodes[i];
+      for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e)
+        if (c->col[e] != u) {
+          c->n_nonpos += c->met[e] <= 0;
+          c->n_neg += c->met[e] < 0;
+          if (c->wt[e] > c->max_metric) {
+            c->max_metric = c->wt[e];
+            c->n_at_max = 1;
+          } else if (c->wt[e] == c->max_metric) {
+            ++c->n_at_max;
+          }
+        }
+    }
   }
   // link slots and reverse edges: a link's slot in an untouched row keeps its
   // position; its slots in touched rows are where the new rows put them
@@ -2056,6 +2092,13 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
     return (uint32_t)(std::upper_bound(c->row_ptr.begin(), c->row_ptr.end(), e) - c->row_ptr.begin()) - 1;
   };
   std::unordered_map<uint32_t, std::vector<uint32_t>> moved;  // link -> its slots in touched rows
+  std::vector<uint32_t> rev_dirty;  // reverse-edge entries whose value changed
+  auto set_rev = [&](uint32_t e, uint32_t r) {
+    if (c->rev[e] != r) {
+      c->rev[e] = r;
+      rev_dirty.push_back(e);
+    }
+  };
   for (uint32_t i = 0; i < n; ++i)
     for (uint32_t e = c->row_ptr[nodes[i]]; e < c->row_ptr[nodes[i] + 1]; ++e) moved[c->link[e]].push_back(e);
   for (auto& [l, es] : moved) {
@@ -2067,27 +2110,17 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
       return fail(c, SPF_E_INVALID, "link %u has %zu slots after the patch (2 needed)", l, slots.size());
     ls[0] = slots[0];
     ls[1] = slots[1];
-    c->rev[slots[0]] = slots[1];
-    c->rev[slots[1]] = slots[0];
+    set_rev(slots[0], slots[1]);
+    set_rev(slots[1], slots[0]);
     const uint32_t a = tail(slots[0]), b = tail(slots[1]);
     const bool dead0 = c->col[slots[0]] == a, dead1 = c->col[slots[1]] == b;
     if (dead0 != dead1 || (!dead0 && (c->col[slots[0]] != b || c->col[slots[1]] != a)))
       return fail(c, SPF_E_INVALID, "link %u: its two slots are not one link in both directions", l);
   }
-  // graph-wide metric facts over live edges
-  bool nonpos = false, neg = false;
-  uint32_t max_metric = 0;
-  for (uint32_t u = 0; u < N; ++u)
-    for (uint32_t e = c->row_ptr[u]; e < c->row_ptr[u + 1]; ++e) {
-      if (c->col[e] == u) continue;
-      nonpos |= c->met[e] <= 0;
-      neg |= c->met[e] < 0;
-      max_metric = std::max(max_metric, c->wt[e]);
-    }
-  c->nonpos = nonpos;
-  c->needs64 = neg || (uint64_t)max_metric * (uint64_t)(N - 1) >= (uint64_t)kInf;
-  c->max_metric = max_metric;
-  c->unit = !nonpos && max_metric <= 1;
+  // graph-wide metric facts over live edges: from the counts, unless every
+  // edge at the old maximum left (then the maximum fell: one scan)
+  if (c->n_at_max == 0) metric_facts(c);
+  else metric_flags(c);
   // distinct up neighbours of the touched nodes; the lists are rebuilt (every
   // untouched node's range copied) when a count changes
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fresh(n);
@@ -2188,32 +2221,50 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
     else
       runs.emplace_back(b, e);
   }
+  // (uploads through the pinned stage: queued, not a blocking pageable copy each)
   for (const auto& r : runs) {
     const size_t b = r.first, k = r.second - r.first;
-    HIP_TRY(c, c->d_col.upload_at(c->col.data(), b, k, c->stream));
-    HIP_TRY(c, c->d_wt.upload_at(c->wt.data(), b, k, c->stream));
-    HIP_TRY(c, c->d_met.upload_at(c->met.data(), b, k, c->stream));
-    HIP_TRY(c, c->d_rev.upload_at(c->rev.data(), b, k, c->stream));
-    HIP_TRY(c, c->d_link.upload_at(c->link.data(), b, k, c->stream));
-    HIP_TRY(c, c->d_edge_nb.upload_at(enb.data(), b, k, c->stream));
+    HIP_TRY(c, stage_upload_at(c, c->d_col, c->col.data(), b, k));
+    HIP_TRY(c, stage_upload_at(c, c->d_wt, c->wt.data(), b, k));
+    HIP_TRY(c, stage_upload_at(c, c->d_met, c->met.data(), b, k));
+    HIP_TRY(c, stage_upload_at(c, c->d_rev, c->rev.data(), b, k));
+    HIP_TRY(c, stage_upload_at(c, c->d_link, c->link.data(), b, k));
+    HIP_TRY(c, stage_upload_at(c, c->d_edge_nb, enb.data(), b, k));
   }
-  {
-    std::vector<uint32_t> partners;
-    for (const auto& r : runs)
-      for (uint32_t q = r.first; q < r.second; ++q) partners.push_back(c->rev[q]);
-    std::sort(partners.begin(), partners.end());
-    partners.erase(std::unique(partners.begin(), partners.end()), partners.end());
-    for (uint32_t q : partners) HIP_TRY(c, c->d_rev.upload_at(c->rev.data(), q, 1, c->stream));
+  {  // reverse-edge entries outside the touched rows whose value changed
+    std::sort(rev_dirty.begin(), rev_dirty.end());
+    rev_dirty.erase(std::unique(rev_dirty.begin(), rev_dirty.end()), rev_dirty.end());
+    auto in_runs = [&](uint32_t q) {
+      auto it = std::upper_bound(runs.begin(), runs.end(), std::make_pair(q, ~0u));
+      return it != runs.begin() && q < std::prev(it)->second;
+    };
+    for (size_t a = 0; a < rev_dirty.size();) {
+      if (in_runs(rev_dirty[a])) {
+        ++a;
+        continue;
+      }
+      size_t b = a + 1;
+      while (b < rev_dirty.size() && rev_dirty[b] == rev_dirty[b - 1] + 1 && !in_runs(rev_dirty[b])) ++b;
+      HIP_TRY(c, stage_upload_at(c, c->d_rev, c->rev.data(), rev_dirty[a], b - a));
+      a = b;
+    }
   }
-  if (counts) {
-    HIP_TRY(c, c->d_nb_ptr.upload(c->nb_ptr.data(), N + 1, c->stream));
-    HIP_TRY(c, c->d_nb_id.upload(c->nb_id.data(), c->nb_id.size(), c->stream));
-    HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  if (counts) {  // the lists moved from the first touched node on
+    const uint32_t u0 = order.front();
+    const size_t b = c->nb_ptr[u0];
+    HIP_TRY(c, stage_upload_at(c, c->d_nb_ptr, c->nb_ptr.data(), u0, N + 1 - u0));
+    if (c->d_nb_id.n < c->nb_id.size()) {  // (the lists outgrew the buffers)
+      HIP_TRY(c, stage_upload(c, c->d_nb_id, c->nb_id.data(), c->nb_id.size()));
+      HIP_TRY(c, stage_upload(c, c->d_nb_w, c->nb_w.data(), c->nb_w.size()));
+    } else {
+      HIP_TRY(c, stage_upload_at(c, c->d_nb_id, c->nb_id.data(), b, c->nb_id.size() - b));
+      HIP_TRY(c, stage_upload_at(c, c->d_nb_w, c->nb_w.data(), b, c->nb_w.size() - b));
+    }
   } else {
     for (uint32_t u : order) {
       const size_t b = c->nb_ptr[u], k = c->nb_ptr[u + 1] - b;
-      HIP_TRY(c, c->d_nb_id.upload_at(c->nb_id.data(), b, k, c->stream));
-      HIP_TRY(c, c->d_nb_w.upload_at(c->nb_w.data(), b, k, c->stream));
+      HIP_TRY(c, stage_upload_at(c, c->d_nb_id, c->nb_id.data(), b, k));
+      HIP_TRY(c, stage_upload_at(c, c->d_nb_w, c->nb_w.data(), b, k));
     }
   }
   {
@@ -2222,14 +2273,15 @@ spf_status spf_graph_patch_rows(spf_ctx* c, const uint32_t* nodes, uint32_t n, c
     slices.erase(std::unique(slices.begin(), slices.end()), slices.end());
     for (uint32_t sl : slices) {
       const size_t b = c->sell_ptr[sl], k = c->sell_ptr[sl + 1] - b;
-      HIP_TRY(c, c->d_sell_col.upload_at(c->sell_col.data(), b, k, c->stream));
+      HIP_TRY(c, stage_upload_at(c, c->d_sell_col, c->sell_col.data(), b, k));
       if (!c->sell4.empty()) {
         const size_t b4 = 2ull * c->sell4_ptr[sl], k4 = 2ull * (c->sell4_ptr[sl + 1] - c->sell4_ptr[sl]);
-        HIP_TRY(c, c->d_sell4.upload_at(c->sell4.data(), b4, k4, c->stream));
+        HIP_TRY(c, stage_upload_at(c, c->d_sell4, c->sell4.data(), b4, k4));
       }
     }
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  stage_done(c);
   ++c->epoch;
   return SPF_OK;
 }

@@ -287,3 +287,69 @@ def test_link_flap_route_build_and_resident_pass():
             ls.prefetchAllSources()
             for n in names[::37]:
                 assert spf_canonical(ls.getSpfResult(n)) == o.spf(n), (step, n)
+
+
+def test_row_patch_keeps_metric_facts():
+    """spf_graph_patch_rows keeps the graph's metric facts (unit, max metric)
+    from per-edge counts: taking down the only heavy link of a unit grid
+    makes the graph unit again (plans go back to the BFS kernels), bringing
+    it up makes it weighted; results equal a fresh load of the same CSR."""
+    import ctypes as C
+
+    from openr_amd import _native as N
+
+    topo = T.grid(6)
+    names, rp, col, met, lid, ovl = graph_from_lsdb(topo.lsdb)
+    met = met.copy()
+    u = 7
+    e = int(rp[u])  # u's first slot and its reverse slot carry metric 5
+    v = int(col[e])
+    r = [q for q in range(int(rp[v]), int(rp[v + 1])) if lid[q] == lid[e]][0]
+    met[e] = met[r] = 5
+    eng = SpfEngine(0)
+    eng.load(rp, col, met, lid, ovl)
+    srcs = list(range(len(names)))
+    assert eng.plan(srcs, hop=False).kernels()[0] not in ("msbfs_kernel", "msbfs_planes_kernel",
+                                                          "msbfs_team_kernel")
+
+    def patch(up):
+        nodes = np.array([u, v], np.uint32)
+        rows_c, rows_m, rows_l = [], [], []
+        for x in (u, v):
+            for q in range(int(rp[x]), int(rp[x + 1])):
+                dead = (q in (e, r)) and not up
+                rows_c.append(x if dead else int(col[q]))
+                rows_m.append(1 if dead else int(met[q]))
+                rows_l.append(int(lid[q]))
+        cc = np.array(rows_c, np.uint32)
+        mm = np.array(rows_m, np.int32)
+        ll = np.array(rows_l, np.uint32)
+        eng._err(N.lib.spf_graph_patch_rows(eng._h, N.ptr(nodes), 2, N.ptr(cc), N.ptr(mm, C.c_int32),
+                                            N.ptr(ll)))
+        return cc, mm
+
+    def same_as_fresh(cc, mm):
+        col2, met2 = col.copy(), met.copy()
+        o = 0
+        for x in (u, v):
+            for q in range(int(rp[x]), int(rp[x + 1])):
+                col2[q], met2[q] = cc[o], mm[o]
+                o += 1
+        ref = SpfEngine(0)
+        ref.load(rp, col2, met2, lid, ovl)
+        got = eng.plan(srcs, hop=False).execute_host()
+        exp = ref.plan(srcs, hop=False).execute_host()
+        assert np.array_equal(got.dist, exp.dist)
+        for i in range(len(srcs)):
+            assert np.array_equal(got.nh_matrix(i), exp.nh_matrix(i))
+        ref.close()
+
+    cc, mm = patch(up=False)  # the heavy link down: every live edge has metric 1
+    assert eng.plan(srcs, hop=False).kernels()[0] in ("msbfs_kernel", "msbfs_planes_kernel",
+                                                      "msbfs_team_kernel")
+    same_as_fresh(cc, mm)
+    cc, mm = patch(up=True)  # and up again: weighted
+    assert eng.plan(srcs, hop=False).kernels()[0] not in ("msbfs_kernel", "msbfs_planes_kernel",
+                                                          "msbfs_team_kernel")
+    same_as_fresh(cc, mm)
+    eng.close()
