@@ -1956,8 +1956,9 @@ spf_status spf_graph_set_overload(spf_ctx* c, const uint32_t* nodes, const uint8
   }
   if (!changed) return SPF_OK;
   HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, c->d_ovl.upload(c->ovl.data(), c->N, c->stream));
+  HIP_TRY(c, stage_upload(c, c->d_ovl, c->ovl.data(), c->N));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  stage_done(c);
   ++c->epoch;
   return SPF_OK;
 }
@@ -2000,10 +2001,11 @@ spf_status spf_graph_set_metric(spf_ctx* c, const uint32_t* edges, const int32_t
     }
   }
   HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, c->d_wt.upload(c->wt.data(), c->E, c->stream));
-  HIP_TRY(c, c->d_met.upload(c->met.data(), c->E, c->stream));
-  HIP_TRY(c, c->d_nb_w.upload(c->nb_w.data(), c->nb_w.size(), c->stream));
+  HIP_TRY(c, stage_upload(c, c->d_wt, c->wt.data(), c->E));
+  HIP_TRY(c, stage_upload(c, c->d_met, c->met.data(), c->E));
+  HIP_TRY(c, stage_upload(c, c->d_nb_w, c->nb_w.data(), c->nb_w.size()));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  stage_done(c);
   ++c->epoch;
   return SPF_OK;
 }
