@@ -281,7 +281,7 @@ constexpr uint32_t kRqSets = 4;
 constexpr uint32_t kRqPerBlock = kRqSets * kRsThreads;
 constexpr bool kRqNt = true;  // streaming 32-byte stores (full lines when a wave's routes agree)
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-template <int MODE>
+template <int MODE, typename Dist>
 __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
     const unsigned long long* __restrict__ rowp, const unsigned long long* __restrict__ nhp,
     uint32_t wpm, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
@@ -301,7 +301,12 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
   const uint32_t* Dme = reinterpret_cast<const uint32_t*>(rowp[me]);
   const uint32_t* NHme = reinterpret_cast<const uint32_t*>(nhp[me]);
   const uint32_t e0 = row_ptr[me], e1 = row_ptr[me + 1];
-  uint64_t sh[kRqSets], rec[kRqSets];
+  // Dist: the selection's sums (d + metric, shortest + d_x(me)) in u64, or
+  // in u32 when the host proved every finite sum stays below kInf (fewer
+  // VALU instructions: the selection is VALU-bound)
+  constexpr Dist kInfD = (Dist)~(Dist)0;
+  Dist sh[kRqSets];
+  uint64_t rec[kRqSets];
   uint32_t cnt[kRqSets], b[kRqSets], e[kRqSets];
   bool vec = true;
 #pragma unroll
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
     b[j] = live ? set_ptr[p0 + j] : 0u;
     e[j] = live ? set_ptr[p0 + j + 1] : 0u;
     vec &= e[j] == b[j] + 1;
-    sh[j] = kInf64;
+    sh[j] = kInfD;
     rec[j] = 0;
     cnt[j] = 0;
   }
@@ -324,7 +329,7 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
     const uint4 d4 = *reinterpret_cast<const uint4*>(Dme + d0);
     const uint32_t dd[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-    for (uint32_t j = 0; j < kRqSets; ++j) sh[j] = dd[j] == kInf ? kInf64 : dd[j];
+    for (uint32_t j = 0; j < kRqSets; ++j) sh[j] = dd[j] == kInf ? kInfD : (Dist)dd[j];
   } else {
 #pragma unroll
     for (uint32_t j = 0; j < kRqSets; ++j)
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
   }
   bool any_route = false;
 #pragma unroll
-  for (uint32_t j = 0; j < kRqSets; ++j) any_route |= sh[j] != kInf64;
+  for (uint32_t j = 0; j < kRqSets; ++j) any_route |= sh[j] != kInfD;
   const uint64_t tile = MODE == kRsDb ? (uint64_t)chunk * kRqPerBlock * (e1 - e0) : 0ull;
   unsigned long long* const out =
       MODE == kRsDb ? db.pool + db.base[slot] + tile + kRqSets * threadIdx.x : nullptr;
@@ -361,9 +366,9 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
       if (s_j[t] == kInf) continue;  // a dead slot (no link)
       const uint32_t* bm = NHme + (size_t)s_j[t] * wpm;
       const uint32_t* Dx = reinterpret_cast<const uint32_t*>(s_row[t]);
-      const uint64_t back = s_back[t];
+      const Dist back = s_back[t] == kInf ? kInfD : (Dist)s_back[t];
       const uint32_t dmx = s_dmx[t];
-      uint64_t via[kRqSets];
+      Dist via[kRqSets];
       if (vec) {  // four consecutive single destinations: one word, one 16-byte load
         const uint32_t bw = bm[d0 >> 5];
         uint32_t dx[4] = {kInf, kInf, kInf, kInf};
@@ -373,18 +378,18 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
         }
 #pragma unroll
         for (uint32_t j = 0; j < kRqSets; ++j) {
-          via[j] = kInf64;
-          if (sh[j] == kInf64) continue;
+          via[j] = kInfD;
+          if (sh[j] == kInfD) continue;
           if ((bw >> ((d0 + j) & 31)) & 1u) via[j] = sh[j] - dmx;
-          if (lfa && dx[j] != kInf && back != kInf && (uint64_t)dx[j] < sh[j] + back &&
-              (via[j] == kInf64 || via[j] > dx[j]))
+          if (lfa && dx[j] != kInf && back != kInfD && (Dist)dx[j] < sh[j] + back &&
+              (via[j] == kInfD || via[j] > (Dist)dx[j]))
             via[j] = dx[j];
         }
       } else {
 #pragma unroll
         for (uint32_t j = 0; j < kRqSets; ++j) {
-          via[j] = kInf64;
-          if (sh[j] == kInf64) continue;
+          via[j] = kInfD;
+          if (sh[j] == kInfD) continue;
           for (uint32_t k = b[j]; k < e[j]; ++k) {
             const uint32_t d = set_nodes[k];
             if (Dme[d] != sh[j]) continue;
@@ -396,17 +401,17 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
           if (Dx)
             for (uint32_t k = b[j]; k < e[j]; ++k) {
               const uint32_t dxd = Dx[set_nodes[k]];
-              if (dxd == kInf || back == kInf) continue;
-              if ((uint64_t)dxd < sh[j] + back && (via[j] == kInf64 || via[j] > dxd)) via[j] = dxd;
+              if (dxd == kInf || back == kInfD) continue;
+              if ((Dist)dxd < sh[j] + back && (via[j] == kInfD || via[j] > (Dist)dxd)) via[j] = dxd;
             }
         }
       }
-      uint64_t over[kRqSets];
+      Dist over[kRqSets];
       bool keep[kRqSets];
 #pragma unroll
       for (uint32_t j = 0; j < kRqSets; ++j) {
-        over[j] = (uint64_t)s_w[t] + via[j];
-        keep[j] = via[j] != kInf64 && (lfa || over[j] == sh[j]);
+        over[j] = (Dist)s_w[t] + via[j];
+        keep[j] = via[j] != kInfD && (lfa || over[j] == sh[j]);
       }
       if constexpr (MODE == kRsDigest) {
 #pragma unroll
@@ -422,8 +427,8 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
           // the four routes' next hop at the same position (consecutive
           // destinations of one pod): one 32-byte store
           u64x2* o = reinterpret_cast<u64x2*>(out + (size_t)cnt[0] * kRqPerBlock);
-          const u64x2 a = {eb | (over[0] << 32), eb | (over[1] << 32)};
-          const u64x2 z = {eb | (over[2] << 32), eb | (over[3] << 32)};
+          const u64x2 a = {eb | ((uint64_t)over[0] << 32), eb | ((uint64_t)over[1] << 32)};
+          const u64x2 z = {eb | ((uint64_t)over[2] << 32), eb | ((uint64_t)over[3] << 32)};
           if constexpr (kRqNt) {
             __builtin_nontemporal_store(a, o);
             __builtin_nontemporal_store(z, o + 1);
@@ -433,15 +438,15 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
           }
 #pragma unroll
           for (uint32_t j = 0; j < kRqSets; ++j) {
-            wide |= (over[j] >> 32) != 0;
+            wide |= ((uint64_t)over[j] >> 32) != 0;
             ++cnt[j];
           }
         } else {
 #pragma unroll
           for (uint32_t j = 0; j < kRqSets; ++j)
             if (keep[j]) {
-              wide |= (over[j] >> 32) != 0;
-              out[(size_t)cnt[j] * kRqPerBlock + j] = eb | (over[j] << 32);
+              wide |= ((uint64_t)over[j] >> 32) != 0;
+              out[(size_t)cnt[j] * kRqPerBlock + j] = eb | ((uint64_t)over[j] << 32);
               ++cnt[j];
             }
         }
@@ -494,16 +499,31 @@ spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
     const uint32_t groups = (n_me + kRsGroup - 1) / kRsGroup;
     const uint64_t blocks = 8ull * ((groups + 7) / 8 * kRsGroup) * n_chunks;
     if (blocks >= (1ull << 31)) return fail(c, SPF_E_INVALID, "route sets: grid too large");
-    if (db)
-      hipLaunchKernelGGL(route_quads_kernel<kRsDb>, dim3((uint32_t)blocks), dim3(kRsThreads), 0, s, d_rowp, d_nhp,
-                         c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p,
-                         d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, nullptr, nullptr, n_me,
-                         n_chunks, *db);
+    // u32 sums when no finite one can reach kInf: distances are at most
+    // B = max metric x (N - 1), a sum at most 2B + max metric (SPF_ROUTE_U64=1: A/B)
+    const uint64_t mm = std::max<uint32_t>(c->max_metric, 1u);
+    const uint64_t B = mm * (uint64_t)(c->N ? c->N - 1 : 0);
+    const bool n32 = !c->needs64 && 2 * B + mm < (uint64_t)kInf && !std::getenv("SPF_ROUTE_U64");
+    const dim3 grid((uint32_t)blocks), block(kRsThreads);
+    const uint32_t wpm = c->pitch / 32, lf = lfa ? 1u : 0u;
+    if (db && n32)
+      hipLaunchKernelGGL((route_quads_kernel<kRsDb, uint32_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
+                         c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
+                         d_set_ptr, d_set_nodes, n_sets, lf, nullptr, nullptr, n_me, n_chunks, *db);
+    else if (db)
+      hipLaunchKernelGGL((route_quads_kernel<kRsDb, uint64_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
+                         c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
+                         d_set_ptr, d_set_nodes, n_sets, lf, nullptr, nullptr, n_me, n_chunks, *db);
+    else if (n32)
+      hipLaunchKernelGGL((route_quads_kernel<kRsDigest, uint32_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
+                         c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
+                         d_set_ptr, d_set_nodes, n_sets, lf, d_link_hash, d_digest, n_me, n_chunks,
+                         RouteDbOut{});
     else
-      hipLaunchKernelGGL(route_quads_kernel<kRsDigest>, dim3((uint32_t)blocks), dim3(kRsThreads), 0, s, d_rowp,
-                         d_nhp, c->pitch / 32, c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p,
-                         c->d_edge_nb.p, d_me, d_set_ptr, d_set_nodes, n_sets, lfa ? 1u : 0u, d_link_hash,
-                         d_digest, n_me, n_chunks, RouteDbOut{});
+      hipLaunchKernelGGL((route_quads_kernel<kRsDigest, uint64_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
+                         c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
+                         d_set_ptr, d_set_nodes, n_sets, lf, d_link_hash, d_digest, n_me, n_chunks,
+                         RouteDbOut{});
     HIP_TRY(c, hipGetLastError());
     return SPF_OK;
   }
