@@ -324,7 +324,16 @@ struct GraphCache {
 
 }  // namespace
 
+// the single-area batched selection: one spf_mplan_routes / spf_routes call
+// (kept by the solver: a build of the same shape resizes nothing)
+struct Selection {
+  uint32_t deg = 1;
+  std::vector<uint64_t> mins, metric;
+  std::vector<uint32_t> cnt, edge;
+};
+
 struct dc_solver {
+  Selection sel;  // the last build's batched selection buffers
   std::string me;
   bool enable_v4 = false, lfa = false, bgp_dry_run = false, best_route_selection = false;
   std::string err;
@@ -891,12 +900,6 @@ struct Build {
   }
 };
 
-// the single-area batched selection: one spf_mplan_routes / spf_routes call
-struct Selection {
-  uint32_t deg = 1;
-  std::vector<uint64_t> mins, metric;
-  std::vector<uint32_t> cnt, edge;
-};
 
 spf_status graph_cache(dc_solver* s, ls_state* ls, GraphCache*& out) {
   uint32_t N = 0, E = 0;
@@ -1298,14 +1301,16 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     }
     const uint32_t n_sets = (uint32_t)set_ptr.size() - 1;
     phase(2);
-    Selection sel;
+    Selection& sel = s->sel;
     const uint32_t m = a.me_id < g->csr_of.size() ? g->csr_of[a.me_id] : ~0u;
     if (m != ~0u && n_sets) {
+      // every min and count is written by the selection, and a set's first
+      // count edges and metrics: no fill (the same sizes resize nothing)
       sel.deg = std::max<uint32_t>(1, g->row_ptr[m + 1] - g->row_ptr[m]);
-      sel.mins.assign(n_sets, kInf64);
-      sel.cnt.assign(n_sets, 0);
-      sel.edge.assign((size_t)n_sets * sel.deg, 0);
-      sel.metric.assign((size_t)n_sets * sel.deg, 0);
+      sel.mins.resize(n_sets);
+      sel.cnt.resize(n_sets);
+      sel.edge.resize((size_t)n_sets * sel.deg);
+      sel.metric.resize((size_t)n_sets * sel.deg);
       if (set_nodes.empty()) set_nodes.push_back(0);
       const uint32_t flags = s->lfa ? SPF_ROUTE_LFA : 0u;
       spf_status c = SPF_E_UNSUPPORTED;

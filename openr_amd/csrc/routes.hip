@@ -610,11 +610,11 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
   auto& d_metric = rc.metric;
   HIP_TRY(c, d_dist.alloc((size_t)srcs.size() * c->pitch));
   HIP_TRY(c, d_nh.alloc(std::max<uint64_t>(1, spf_plan_nh_words(p))));
-  HIP_TRY(c, d_ecol.upload(ecol.data(), deg, c->stream));
-  HIP_TRY(c, d_ew.upload(ew.data(), deg, c->stream));
-  HIP_TRY(c, d_ej.upload(ej.data(), deg, c->stream));
-  HIP_TRY(c, d_sp.upload(set_ptr, n_sets + 1, c->stream));
-  HIP_TRY(c, d_sn.upload(set_nodes, std::max<uint32_t>(1, n_members), c->stream));
+  HIP_TRY(c, stage_upload(c, d_ecol, ecol.data(), deg));
+  HIP_TRY(c, stage_upload(c, d_ew, ew.data(), deg));
+  HIP_TRY(c, stage_upload(c, d_ej, ej.data(), deg));
+  HIP_TRY(c, stage_upload(c, d_sp, set_ptr, n_sets + 1));
+  HIP_TRY(c, stage_upload(c, d_sn, set_nodes, std::max<uint32_t>(1, n_members)));
   const size_t cap = (size_t)n_sets * std::max<uint32_t>(1, deg);
   HIP_TRY(c, d_min.alloc(std::max<uint32_t>(1, n_sets)));
   HIP_TRY(c, d_cnt.alloc(std::max<uint32_t>(1, n_sets)));
@@ -647,6 +647,7 @@ spf_status spf_routes(spf_ctx* c, uint32_t me, const uint32_t* set_ptr,
     }
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  stage_done(c);
   // out edges are positions in me's CSR row: make them global edge ids
   for (size_t i = 0; i < (size_t)n_sets; ++i)
     for (uint32_t t = 0; t < nh_count[i]; ++t) nh_edge[i * deg + t] += e0;
