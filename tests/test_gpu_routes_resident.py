@@ -199,3 +199,42 @@ def test_single_advertiser_fast_path_equals_generic_walk(v4, bgp_dry):
                     SpfSolver._single_fast = True
             assert out[0] == out[1], me
             assert out[0][0]  # routes exist
+
+
+@pytest.mark.parametrize("lfa", [False, True], ids=["sp", "lfa"])
+def test_route_sums_u32_and_u64_paths_agree(lfa, monkeypatch):
+    """The many-me route kernel runs its sums in u32 when the host proves no
+    finite sum reaches kInf (routes.hip, route_quads_kernel<MODE, Dist>):
+    digests and materialised records equal the u64 kernel's (SPF_ROUTE_U64=1)
+    on a small-metric graph, and a graph whose metrics rule u32 out (up to
+    2^26 per link: 2 x max metric x (N - 1) passes 2^32 while the distances
+    themselves still fit u32) takes the u64 kernel and matches the oracle."""
+    topo = T.random_graph(60, 170, 12, max_metric=6, parallel_frac=0.25, overload_frac=0.1,
+                          link_overload_frac=0.05)
+    with LinkState(devices=[0]) as ls:
+        ls.updateAdjacencyDatabases(topo.lsdb)
+        ls.prefetchAllSources()
+        names = list(ls.flatten()[0])
+        ptr, nodes = sets_for(len(names), np.random.default_rng(3))
+        d32, _ = ls.allSourcesRouteDigests(ptr, nodes, lfa)
+        ls.allSourcesRouteRecords(ptr, nodes, lfa)
+        r32 = [ls.allSourcesRouteDb(t) for t in range(len(names))]
+        monkeypatch.setenv("SPF_ROUTE_U64", "1")
+        d64, _ = ls.allSourcesRouteDigests(ptr, nodes, lfa)
+        ls.allSourcesRouteRecords(ptr, nodes, lfa)
+        r64 = [ls.allSourcesRouteDb(t) for t in range(len(names))]
+        monkeypatch.delenv("SPF_ROUTE_U64")
+    assert np.array_equal(d32, d64)
+    for (h32, c32), (h64, c64) in zip(r32, r64):
+        assert np.array_equal(h32, h64) and np.array_equal(c32, c64)
+    wide = T.random_graph(50, 140, 9, max_metric=1 << 26, parallel_frac=0.2, overload_frac=0.1)
+    with LinkState(devices=[0]) as ls:
+        ls.updateAdjacencyDatabases(wide.lsdb)
+        ls.prefetchAllSources()
+        names = list(ls.flatten()[0])
+        ptr, nodes = sets_for(len(names), np.random.default_rng(4))
+        got, _ = ls.allSourcesRouteDigests(ptr, nodes, lfa)
+    orc = OracleLinkState()
+    orc.update_packed(wide.lsdb)
+    want = route_digests(orc, NameTable(names), np.arange(len(names)), ptr, nodes, lfa)
+    assert np.array_equal(got, want)
