@@ -179,6 +179,15 @@ struct spf_ctx {
   std::vector<uint32_t> ecc;
   uint64_t ecc_epoch = ~0ull;
   uint32_t dbound = 0;  // hop-distance upper bound (depth_bound), for dbound_epoch
+  // recent bounds by (sliced-ELL structure version, drain bits): a drain bit
+  // toggled back and forth (the BM_DecisionFabric publication) or a metric
+  // patch (the bound counts hops) finds its bound again without a BFS
+  struct DboundMemo {
+    uint64_t sell_ver;
+    std::vector<uint8_t> ovl;
+    uint32_t dbound;
+  };
+  std::vector<DboundMemo> dbound_memo;
   uint64_t dbound_epoch = ~0ull;
   // mssp_kernel tables (mssp.hip), valid for graph epoch mp_epoch
   spfi::DevBuf<uint32_t> d_mp_ell, d_mp_smap;

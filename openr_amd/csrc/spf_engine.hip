@@ -2363,6 +2363,12 @@ const std::vector<uint32_t>& ecc_estimate(spf_ctx* c) {
 // copy (bound < 254) never need u32 rows of non-source closure rows.
 uint32_t depth_bound(spf_ctx* c) {
   if (c->dbound_epoch == c->epoch) return c->dbound;
+  for (const auto& m : c->dbound_memo)  // the same structure and drain bits as a recent epoch
+    if (m.sell_ver == c->sell_ver && m.ovl == c->ovl) {
+      c->dbound = m.dbound;
+      c->dbound_epoch = c->epoch;
+      return c->dbound;
+    }
   // one level-synchronous BFS per component over the distinct up neighbours;
   // drained nodes are neither roots nor transit, so they start out seen (one
   // byte test per edge -- recomputed after every patch, on the path of the
@@ -2398,6 +2404,8 @@ uint32_t depth_bound(spf_ctx* c) {
   }
   c->dbound = 2 + 2 * worst;
   c->dbound_epoch = c->epoch;
+  if (c->dbound_memo.size() >= 4) c->dbound_memo.erase(c->dbound_memo.begin());
+  c->dbound_memo.push_back({c->sell_ver, c->ovl, c->dbound});
   return c->dbound;
 }
 
