@@ -429,7 +429,8 @@ spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
                              bool lfa, const unsigned long long* d_link_hash,
                              unsigned long long* d_digest, uint64_t* d_min, uint32_t* d_cnt,
                              uint32_t* d_edge, uint64_t* d_metric, hipStream_t s,
-                             const RouteDbOut* db = nullptr);
+                             const RouteDbOut* db = nullptr,
+                             const unsigned long long* d_nrowp = nullptr);
 // pathLinks of `src` from its u32 distance row on the device (spf_preds
 // without the upload; spf_mplan_preds reads a resident row).
 spf_status preds_from_row(spf_ctx* c, uint32_t src, bool hop, const uint32_t* ign,

@@ -185,6 +185,7 @@ struct spf_mplan {
     // spf_mplan_routes): every resident row's device address, the request's
     // sets, its me list and outputs on this member's device
     DevBuf<unsigned long long> rowp, nhp, lh, rdig, rmin, rmetric;
+    DevBuf<unsigned long long> nrowp;  // every resident node's exact u8 row (u8 LFA loads), or none
     DevBuf<uint32_t> rsp, rsn, rme, rcnt, redge;
     std::vector<uint32_t> h_rsp, h_rsn;  // host copies of the uploaded sets (re-upload only on change)
     std::vector<uint64_t> h_lh;
@@ -201,6 +202,7 @@ struct spf_mplan {
   std::vector<std::pair<uint32_t, uint32_t>> db_loc;
   uint32_t db_sets = 0;
   std::vector<unsigned long long> h_rowp, h_nhp;  // the address tables (host; uploads read them)
+  std::vector<unsigned long long> h_nrowp;  // u8 rows, when every member's are exact (else empty)
   std::unique_ptr<Part[]> parts;  // [n_parts]
   uint32_t n_parts = 0;
   bool graphs = false;
@@ -754,6 +756,34 @@ spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t*
       }
     rowp.assign(N, 0);
     nhp.assign(N, 0);
+    // the members' u8 row copies (the BFS's narrow rows, closure order) are
+    // exact distances when every metric is 1 and no row reached 254: the
+    // records kernel's LFA then loads 4 bytes for 4 destinations instead of
+    // 16 (it is bound by HBM bytes: 3.94 -> 3.77 ms on fabric_full,
+    // profiles/r06_routes/u8lfa).  SPF_ROUTE_U8=0: u32 loads (A/B)
+    mp->h_nrowp.clear();
+    const char* ue = std::getenv("SPF_ROUTE_U8");
+    bool u8 = c0->unit && !(ue && ue[0] == '0');
+    for (uint32_t r = 0; r < mp->n_parts && u8; ++r) {
+      const spf_plan* pl = mp->parts[r].plan;
+      if (!pl) continue;
+      u8 = pl->narrow && pl->sliced && !pl->sdirect && !pl->expand && pl->d_Dn.p && pl->d_maxd.p;
+      if (!u8) break;
+      uint32_t md = ~0u;
+      M_HIP(m, hipSetDevice(m->members[r]->device));
+      M_HIP(m, hipMemcpy(&md, pl->d_maxd.p, 4, hipMemcpyDeviceToHost));
+      u8 = md < 254;
+    }
+    if (u8) {
+      mp->h_nrowp.assign(N, 0);
+      for (uint32_t r = 0; r < mp->n_parts; ++r) {
+        const spf_plan* pl = mp->parts[r].plan;
+        if (!pl) continue;
+        const uint32_t np = m->members[r]->npitch;
+        for (size_t ci = 0; ci < pl->closure.size(); ++ci)
+          mp->h_nrowp[pl->closure[ci]] = (unsigned long long)(uintptr_t)(pl->d_Dn.p + ci * np);
+      }
+    }
   }
   for (uint32_t i = 0; i < mp->n_src; ++i) {
     const uint32_t v = mp->srcs[i], r = mp->owner[i], row = mp->row[i];
@@ -795,6 +825,7 @@ spf_status route_prepare(spf_mplan* mp, const uint32_t* set_ptr, const uint32_t*
     if (p.r_epoch != mp->executes) {
       M_HIP(m, p.rowp.upload(rowp.data(), N, s));
       M_HIP(m, p.nhp.upload(nhp.data(), N, s));
+      if (!mp->h_nrowp.empty()) M_HIP(m, p.nrowp.upload(mp->h_nrowp.data(), N, s));
       p.r_epoch = mp->executes;
     }
     // the sets and link hashes of a call are usually the previous call's
@@ -869,6 +900,8 @@ spf_status spf_mplan_route_digests(spf_mplan* mp, const uint32_t* me_req, uint32
     }
     const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, n, p.rsp.p, p.rsn.p, n_sets,
                                             lfa, p.lh.p, p.rdig.p, nullptr, nullptr, nullptr, nullptr, s);
+    // (u8 LFA loads only for the records kernel: the digest kernel is
+    // VALU-bound and the byte unpacking made it slower, 2.33 -> 2.42 ms)
     if (st != SPF_OK) return member_fail(m, r, st);
     if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r + 1], s));
     got[r].resize(n);
@@ -961,7 +994,8 @@ spf_status spf_mplan_route_records(spf_mplan* mp, const uint32_t* me_req, uint32
     db.count = p.dbcnt.p;
     db.flags = p.dbflags.p;
     const spf_status st = launch_route_sets(c, p.rowp.p, p.nhp.p, p.rme.p, n, p.rsp.p, p.rsn.p, n_sets, lfa,
-                                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s, &db);
+                                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s, &db,
+                                            mp->h_nrowp.empty() ? nullptr : p.nrowp.p);
     if (st != SPF_OK) return member_fail(m, r, st);
     if (kernel_ms) M_HIP(m, hipEventRecord(ev[2 * r + 1], s));
     fl[r].resize(n + 1);

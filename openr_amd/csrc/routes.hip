@@ -290,7 +290,8 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
     const uint32_t* __restrict__ me_ids, const uint32_t* __restrict__ set_ptr,
     const uint32_t* __restrict__ set_nodes, uint32_t n_sets, uint32_t lfa,
     const unsigned long long* __restrict__ link_hash, unsigned long long* __restrict__ digest,
-    uint32_t n_me, uint32_t n_chunks, RouteDbOut db) {
+    uint32_t n_me, uint32_t n_chunks, RouteDbOut db,
+    const unsigned long long* __restrict__ nrowp /* exact u8 rows (LFA loads), or null */) {
   const uint32_t g = blockIdx.x & 7u, i = blockIdx.x >> 3;  // XCD-aware order, as route_sets_kernel
   const uint32_t L = i / n_chunks;
   const uint32_t slot = ((L / kRsGroup) * 8 + g) * kRsGroup + L % kRsGroup;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
   unsigned long long* const out =
       MODE == kRsDb ? db.pool + db.base[slot] + tile + kRqSets * threadIdx.x : nullptr;
   __shared__ uint32_t s_j[kRsLinks], s_dmx[kRsLinks], s_back[kRsLinks], s_w[kRsLinks];
-  __shared__ unsigned long long s_row[kRsLinks], s_lh[kRsLinks];
+  __shared__ unsigned long long s_row[kRsLinks], s_lh[kRsLinks], s_row8[kRsLinks];
   bool wide = false;
   for (uint32_t c0 = e0; c0 < e1; c0 += kRsLinks) {  // block-uniform
     const uint32_t nl = min(kRsLinks, e1 - c0);
@@ -357,6 +358,7 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
       s_dmx[t] = Dme[x];
       s_w[t] = wt[q];
       s_row[t] = rx;
+      s_row8[t] = rx && nrowp ? nrowp[x] : 0ull;
       s_back[t] = rx ? reinterpret_cast<const uint32_t*>(rx)[me] : kInf;
       if constexpr (MODE == kRsDigest) s_lh[t] = link_hash[link[q]];
     }
@@ -372,7 +374,15 @@ __global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
       if (vec) {  // four consecutive single destinations: one word, one 16-byte load
         const uint32_t bw = bm[d0 >> 5];
         uint32_t dx[4] = {kInf, kInf, kInf, kInf};
-        if (Dx) {
+        if (const uint8_t* Dx8 = reinterpret_cast<const uint8_t*>(s_row8[t])) {
+          // the same four distances as bytes (exact: unit metrics, depth < 254)
+          const uint32_t b4 = *reinterpret_cast<const uint32_t*>(Dx8 + d0);
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t v = (b4 >> (8 * j)) & 0xFFu;
+            dx[j] = v == 0xFFu ? kInf : v;
+          }
+        } else if (Dx) {
           const uint4 x4 = *reinterpret_cast<const uint4*>(Dx + d0);
           dx[0] = x4.x, dx[1] = x4.y, dx[2] = x4.z, dx[3] = x4.w;
         }
@@ -492,7 +502,8 @@ spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
                              const uint32_t* d_set_ptr, const uint32_t* d_set_nodes, uint32_t n_sets,
                              bool lfa, const unsigned long long* d_link_hash,
                              unsigned long long* d_digest, uint64_t* d_min, uint32_t* d_cnt,
-                             uint32_t* d_edge, uint64_t* d_metric, hipStream_t s, const RouteDbOut* db) {
+                             uint32_t* d_edge, uint64_t* d_metric, hipStream_t s, const RouteDbOut* db,
+                             const unsigned long long* d_nrowp) {
   if (!n_me || !n_sets) return SPF_OK;
   if ((db || d_digest) && !std::getenv("SPF_ROUTE_SETS1")) {  // four sets per thread (SPF_ROUTE_SETS1: one, A/B)
     const uint32_t n_chunks = (n_sets + kRqPerBlock - 1) / kRqPerBlock;
@@ -509,21 +520,21 @@ spf_status launch_route_sets(spf_ctx* c, const unsigned long long* d_rowp,
     if (db && n32)
       hipLaunchKernelGGL((route_quads_kernel<kRsDb, uint32_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
                          c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
-                         d_set_ptr, d_set_nodes, n_sets, lf, nullptr, nullptr, n_me, n_chunks, *db);
+                         d_set_ptr, d_set_nodes, n_sets, lf, nullptr, nullptr, n_me, n_chunks, *db, d_nrowp);
     else if (db)
       hipLaunchKernelGGL((route_quads_kernel<kRsDb, uint64_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
                          c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
-                         d_set_ptr, d_set_nodes, n_sets, lf, nullptr, nullptr, n_me, n_chunks, *db);
+                         d_set_ptr, d_set_nodes, n_sets, lf, nullptr, nullptr, n_me, n_chunks, *db, d_nrowp);
     else if (n32)
       hipLaunchKernelGGL((route_quads_kernel<kRsDigest, uint32_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
                          c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
                          d_set_ptr, d_set_nodes, n_sets, lf, d_link_hash, d_digest, n_me, n_chunks,
-                         RouteDbOut{});
+                         RouteDbOut{}, d_nrowp);
     else
       hipLaunchKernelGGL((route_quads_kernel<kRsDigest, uint64_t>), grid, block, 0, s, d_rowp, d_nhp, wpm,
                          c->d_row_ptr.p, c->d_col.p, c->d_wt.p, c->d_link.p, c->d_edge_nb.p, d_me,
                          d_set_ptr, d_set_nodes, n_sets, lf, d_link_hash, d_digest, n_me, n_chunks,
-                         RouteDbOut{});
+                         RouteDbOut{}, d_nrowp);
     HIP_TRY(c, hipGetLastError());
     return SPF_OK;
   }

@@ -238,3 +238,38 @@ def test_route_sums_u32_and_u64_paths_agree(lfa, monkeypatch):
     orc.update_packed(wide.lsdb)
     want = route_digests(orc, NameTable(names), np.arange(len(names)), ptr, nodes, lfa)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("members", [1, 2])
+def test_route_lfa_u8_row_loads_match_oracle(members, monkeypatch):
+    """With unit metrics and every member's BFS rows below depth 254, the
+    many-me route kernel's LFA reads the members' u8 row copies (4 bytes per
+    4 destinations, multi.cpp route_prepare): every node's digests and
+    materialised databases equal the u32 loads' (SPF_ROUTE_U8=0) and the
+    oracle's.  (Team plans keep no u8 rows: SPF_MSBFS_TEAM=0 gives every
+    member the one-workgroup-per-batch BFS that writes them.)"""
+    monkeypatch.setenv("SPF_MSBFS_TEAM", "0")
+    topo = T.fabric(1000, full=True)
+    out = {}
+    for u8 in ("1", "0"):
+        monkeypatch.setenv("SPF_ROUTE_U8", u8)
+        with LinkState(devices=[0] * members) as ls:
+            ls.updateAdjacencyDatabases(topo.lsdb)
+            ls.prefetchAllSources()
+            names, _rp, _col, _met, lid = ls.flatten()[:5]
+            names = list(names)
+            lh = ls.linkValueHashes()
+            ptr, nodes = sets_for(len(names), np.random.default_rng(9))
+            dig, _ = ls.allSourcesRouteDigests(ptr, nodes, True)
+            ls.allSourcesRouteRecords(ptr, nodes, True)
+            recs = np.array([route_db_digest(*ls.allSourcesRouteDb(t), lid, lh) for t in range(len(names))],
+                            np.uint64)
+        out[u8] = (dig, recs)
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
+    orc = OracleLinkState()
+    orc.update_packed(topo.lsdb)
+    want = route_digests(orc, NameTable(names), np.arange(len(names)), ptr, nodes, True)
+    assert np.array_equal(out["1"][0], want)
+    want_min = route_digests(orc, NameTable(names), np.arange(len(names)), ptr, nodes, True, kept_min=True)
+    assert np.array_equal(out["1"][1], want_min)
