@@ -212,7 +212,12 @@ struct dc_prefix_state {
 
 // ---- DecisionRouteDb -------------------------------------------------------------
 struct dc_route_db {
-  std::vector<std::string> strs;
+  // the string table: NUL-terminated strings back to back in one arena, by
+  // offset (a route's prefix is one append, not one allocation; the arena
+  // stops growing when the build returns, so dc_route_db_string's pointers
+  // stay valid)
+  std::string arena;
+  std::vector<uint32_t> str_off;
   std::unordered_map<std::string, uint32_t> sid;
   std::vector<dc_nexthop> nhs;
   std::vector<int32_t> labels;
@@ -242,17 +247,19 @@ struct dc_route_db {
   uint32_t intern(const std::string& s) {
     auto it = sid.find(s);
     if (it != sid.end()) return it->second;
-    const uint32_t id = (uint32_t)strs.size();
-    strs.push_back(s);
+    const uint32_t id = push_unique(s);
     sid.emplace(s, id);
     return id;
   }
   uint32_t opt(const std::optional<std::string>& s) { return s ? intern(*s) : DC_NONE; }
   // a string no other record shares (a route's prefix): no lookup
   uint32_t push_unique(const std::string& s) {
-    strs.push_back(s);
-    return (uint32_t)strs.size() - 1;
+    str_off.push_back((uint32_t)arena.size());
+    arena.append(s.data(), s.size());
+    arena.push_back('\0');
+    return (uint32_t)str_off.size() - 1;
   }
+  const char* str(uint32_t id) const { return arena.data() + str_off[id]; }
   // a next-hop set (sorted, unique) appended; returns [begin, end)
   std::pair<uint32_t, uint32_t> add_set(std::vector<NH>& set) {
     std::sort(set.begin(), set.end());
@@ -1391,7 +1398,8 @@ spf_status dc_build_route_db(dc_solver* s, const char* const* area_names, ls_sta
     };
     // IP routes: equal selections (edges, metrics, family) share one record range
     std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> shared;
-    db->strs.reserve(db->strs.size() + uni.size());
+    db->str_off.reserve(db->str_off.size() + 2 * uni.size());
+    db->arena.reserve(db->arena.size() + 24 * uni.size());
     db->uni.reserve(db->uni.size() + 6 * uni.size());
     std::vector<dc_nexthop> recs;
     std::string key;
@@ -1539,9 +1547,9 @@ void dc_debug_phase_ns(const dc_solver* s, uint64_t* out) {
 }
 
 void dc_route_db_destroy(dc_route_db* db) { delete db; }
-uint32_t dc_route_db_strings(const dc_route_db* db) { return db ? (uint32_t)db->strs.size() : 0; }
+uint32_t dc_route_db_strings(const dc_route_db* db) { return db ? (uint32_t)db->str_off.size() : 0; }
 const char* dc_route_db_string(const dc_route_db* db, uint32_t id) {
-  return db && id < db->strs.size() ? db->strs[id].c_str() : nullptr;
+  return db && id < db->str_off.size() ? db->str(id) : nullptr;
 }
 const dc_nexthop* dc_route_db_nexthops(const dc_route_db* db, uint32_t* n) {
   if (n) *n = db ? (uint32_t)db->nhs.size() : 0;
