@@ -282,7 +282,8 @@ constexpr uint32_t kRqPerBlock = kRqSets * kRsThreads;
 constexpr bool kRqNt = true;  // streaming 32-byte stores (full lines when a wave's routes agree)
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 template <int MODE, typename Dist>
-__global__ __launch_bounds__(kRsThreads) void route_quads_kernel(
+__global__ __launch_bounds__(kRsThreads) __attribute__((amdgpu_waves_per_eu(MODE == kRsDb && sizeof(Dist) == 4 ? 8 : 1)))
+void route_quads_kernel(
     const unsigned long long* __restrict__ rowp, const unsigned long long* __restrict__ nhp,
     uint32_t wpm, const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
     const uint32_t* __restrict__ wt, const uint32_t* __restrict__ link,
